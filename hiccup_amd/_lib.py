@@ -1,0 +1,111 @@
+"""ctypes binding of libhiccup_hip.so (include/hiccup_hip.h).
+
+This is the drop-in boundary: hiccup's Python surface (transform / quantization /
+codec / compression) calls these C-ABI entry points, which launch the gfx950
+HIP kernels.  There is no CPU fallback anywhere in the package: if the shared
+library or a GPU is missing, every call raises ``HipUnavailable``.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("HICCUP_HIP_LIB", os.path.join(_HERE, "lib", "libhiccup_hip.so"))
+
+HIC_OK = 0
+HIC_ERR_ARG = -1
+HIC_ERR_HIP = -2
+HIC_ERR_CAPACITY = -3
+
+TABLE_LUMINANCE = 0
+TABLE_CHROMINANCE = 1
+
+LAYOUT_RASTER_I32 = 0
+LAYOUT_RASTER_I16 = 1
+LAYOUT_ZIGZAG_I16 = 2
+
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_int = ctypes.c_int
+_sz = ctypes.c_size_t
+
+# name -> (restype, argtypes); mirrors include/hiccup_hip.h exactly
+SIGNATURES = {
+    "hic_abi_version": (_int, []),
+    "hic_last_error": (_int, [ctypes.c_char_p, _sz]),
+    "hic_device_count": (_int, [ctypes.POINTER(_int)]),
+    "hic_stream_sync": (_int, [_vp]),
+    "hic_dct_quant_u8": (_int, [_vp, _i64, _i64, _i64, _int, _int, _vp, _vp]),
+    "hic_dequant_idct_u8": (_int, [_vp, _int, _i64, _i64, _int, _vp, _i64, _vp]),
+    "hic_dct2_f64": (_int, [_vp, _i64, _vp, _vp]),
+    "hic_idct2_f64": (_int, [_vp, _i64, _vp, _vp]),
+    "hic_quantize_f64": (_int, [_vp, _i64, _int, _vp, _vp]),
+    "hic_dequantize_i32": (_int, [_vp, _i64, _int, _vp, _vp]),
+    "hic_rgb_to_ycrcb420": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp]),
+    "hic_rgb_to_ycrcb": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp]),
+    "hic_pyr_down_u8": (_int, [_vp, _i64, _i64, _vp, _i64, _i64, _vp]),
+    "hic_pyr_up_u8": (_int, [_vp, _i64, _i64, _vp, _i64, _i64, _vp]),
+    "hic_ycrcb420_to_rgb": (_int, [_vp, _i64, _vp, _vp, _i64, _i64, _vp, _vp]),
+    "hic_zigzag_blocks_i32": (_int, [_vp, _i64, _i64, _int, _vp, _vp]),
+    "hic_izigzag_blocks_i32": (_int, [_vp, _i64, _i64, _int, _vp, _vp]),
+    "hic_rle_workspace_bytes": (_sz, [_i64, _int]),
+    "hic_rle_shard_summary_i16": (_int, [_vp, _i64, _int, _vp, _vp, _vp]),
+    "hic_rle_shard_summary_i32": (_int, [_vp, _i64, _int, _vp, _vp, _vp]),
+    "hic_rle_encode_i16": (_int, [_vp, _i64, _int, _int, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
+    "hic_rle_encode_i32": (_int, [_vp, _i64, _int, _int, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
+    "hic_rle_stitch": (_int, [_vp, _int, _int, _vp, _vp]),
+    "hic_rle_stream_encode_i32": (_int, [_vp, _i64, _int, _vp, _vp, _i64, _vp, _vp, _vp]),
+    "hic_rle_stream_decode_i32": (_int, [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _vp]),
+    "hic_rld_workspace_bytes": (_sz, [_i64, _i64]),
+    "hic_rle_decode_i16": (_int, [_vp, _vp, _i64, _vp, _i64, _int, _vp, _vp, _vp, _vp]),
+    "hic_rle_decode_i32": (_int, [_vp, _vp, _i64, _vp, _i64, _int, _vp, _vp, _vp, _vp]),
+}
+
+
+class HipUnavailable(RuntimeError):
+    """The HIP extension (libhiccup_hip.so) or an MI355X device is missing."""
+
+
+class HipError(RuntimeError):
+    """A C-ABI call returned a HIP runtime error."""
+
+
+_lib = None
+
+
+def load():
+    """Load the shared library (no GPU needed: symbol resolution only)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise HipUnavailable(
+                "libhiccup_hip.so not found at %s: build it with `python -c "
+                "'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)" % LIB_PATH)
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def last_error():
+    buf = ctypes.create_string_buffer(512)
+    load().hic_last_error(buf, 512)
+    return buf.value.decode(errors="replace")
+
+
+def check(status, what=""):
+    """Map a C-ABI status to the reference's error behaviour."""
+    if status == HIC_OK:
+        return
+    msg = "%s: %s" % (what, last_error()) if what else last_error()
+    if status == HIC_ERR_ARG:
+        raise ValueError(msg)
+    if status == HIC_ERR_CAPACITY:
+        raise MemoryError(msg)
+    raise HipError(msg)
+
+
+def call(name, *args):
+    check(getattr(load(), name)(*args), name)

@@ -1,0 +1,250 @@
+// color.hip -- RGB <-> YCrCb (OpenCV 8U fixed point) and the 4:2:0 chroma
+// pyramid (cv2.pyrDown / cv2.pyrUp), as called by compression.jpeg_compression /
+// jpeg_decompression (compression.py:16-56) and transform.down_sample / up_sample
+// (transform.py:151-166).
+//
+// PARITY UNPINNED: OpenCV is absent from this image, so these kernels restate
+// OpenCV's published 8U algorithms (yuv_shift = 14 fixed point; pyrDown 5x5
+// [1 4 6 4 1]^2 / 256 with BORDER_REFLECT_101; pyrUp [1 6 1]/[4 4] taps with
+// OpenCV's reflect-101-left / replicate-right edge rule) and are checked against
+// the oracle's restatement (oracle/oracle.py), not against cv2 itself.
+#include "hic_common.h"
+
+namespace hic {
+namespace {
+
+constexpr int kR2Y = 4899, kG2Y = 9617, kB2Y = 1868, kYCRI = 11682, kYCBI = 9241;
+constexpr int kCR2R = 22987, kCR2G = -11698, kCB2G = -5636, kCB2B = 29049;
+
+__device__ __forceinline__ int descale14(int x) { return (x + (1 << 13)) >> 14; }
+__device__ __forceinline__ uint32_t sat8(int v) { return (uint32_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+
+struct YCC {
+  uint32_t y, cr, cb;
+};
+__device__ __forceinline__ YCC rgb2ycc(int r, int g, int b) {
+  const int y = descale14(r * kR2Y + g * kG2Y + b * kB2Y);
+  return {(uint32_t)y, sat8(descale14((r - y) * kYCRI + (128 << 14))),
+          sat8(descale14((b - y) * kYCBI + (128 << 14)))};
+}
+
+__device__ __forceinline__ int refl101(int i, int n) {
+  if (n == 1) return 0;
+  while (i < 0 || i >= n) i = i < 0 ? -i : 2 * n - 2 - i;
+  return i;
+}
+
+// ---------------------------------------------------------------------------
+// Fused cvtColor(RGB2YCrCb) + pyrDown(Cr), pyrDown(Cb): one workgroup per
+// TX x TY tile of chroma output; the full-resolution Cr/Cb region it needs
+// (with a 2-pixel halo, reflect-101 at image borders) lives only in LDS.
+constexpr int TX = 32, TY = 16;
+constexpr int RW = 2 * TX + 8;  // region columns [2*ox0 - 4, 2*ox0 + 2*TX + 4): 4-pixel aligned
+constexpr int RH = 2 * TY + 4;  // region rows    [2*oy0 - 2, 2*oy0 + 2*TY + 2)
+
+__global__ __launch_bounds__(256) void k_rgb_ycrcb420(const uint8_t *__restrict__ rgb, int H, int W,
+                                                      uint8_t *__restrict__ Y, uint8_t *__restrict__ Cr,
+                                                      uint8_t *__restrict__ Cb, int dh, int dw) {
+  __shared__ uint8_t s_c[2][RH][RW];
+  __shared__ int s_h[2][RH][TX];
+  const int ox0 = blockIdx.x * TX, oy0 = blockIdx.y * TY;
+  const int gxs = 2 * ox0 - 4, gys = 2 * oy0 - 2;
+  // pixels whose Y this tile writes (the last tile row/column also owns odd leftovers)
+  const int cx0 = 2 * ox0, cx1 = (ox0 + TX >= dw) ? W : 2 * (ox0 + TX);
+  const int cy0 = 2 * oy0, cy1 = (oy0 + TY >= dh) ? H : 2 * (oy0 + TY);
+  const bool interior = gxs >= 0 && gys >= 0 && gxs + RW <= W && gys + RH <= H && (W % 4) == 0;
+
+  if (interior) {
+    // 4 pixels (3 dwords) per lane per step: 18 quads x 36 rows
+    constexpr int QW = RW / 4;
+    for (int i = threadIdx.x; i < RH * QW; i += 256) {
+      const int ry = i / QW, qx = i - ry * QW;
+      const int gy = gys + ry, gx = gxs + 4 * qx;
+      const uint32_t *p = reinterpret_cast<const uint32_t *>(rgb + ((int64_t)gy * W + gx) * 3);
+      const uint32_t w0 = p[0], w1 = p[1], w2 = p[2];
+      const int px[12] = {(int)(w0 & 255), (int)((w0 >> 8) & 255), (int)((w0 >> 16) & 255), (int)(w0 >> 24),
+                          (int)(w1 & 255), (int)((w1 >> 8) & 255), (int)((w1 >> 16) & 255), (int)(w1 >> 24),
+                          (int)(w2 & 255), (int)((w2 >> 8) & 255), (int)((w2 >> 16) & 255), (int)(w2 >> 24)};
+      uint32_t yq = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const YCC c = rgb2ycc(px[3 * k], px[3 * k + 1], px[3 * k + 2]);
+        yq |= c.y << (8 * k);
+        s_c[0][ry][4 * qx + k] = (uint8_t)c.cr;
+        s_c[1][ry][4 * qx + k] = (uint8_t)c.cb;
+      }
+      if (gy >= cy0 && gy < cy1 && gx >= cx0 && gx + 4 <= cx1)
+        *reinterpret_cast<uint32_t *>(Y + (int64_t)gy * W + gx) = yq;
+    }
+  } else {
+    for (int i = threadIdx.x; i < RH * RW; i += 256) {
+      const int ry = i / RW, rx = i - ry * RW;
+      const int gy = gys + ry, gx = gxs + rx;
+      const int sy = refl101(gy, H), sx = refl101(gx, W);
+      const uint8_t *p = rgb + ((int64_t)sy * W + sx) * 3;
+      const YCC c = rgb2ycc(p[0], p[1], p[2]);
+      s_c[0][ry][rx] = (uint8_t)c.cr;
+      s_c[1][ry][rx] = (uint8_t)c.cb;
+      if (gy >= cy0 && gy < cy1 && gx >= cx0 && gx < cx1) Y[(int64_t)gy * W + gx] = (uint8_t)c.y;
+    }
+  }
+  __syncthreads();
+  // horizontal [1 4 6 4 1] at even columns: center column 2*lox + 4 of the region
+  for (int i = threadIdx.x; i < 2 * RH * TX; i += 256) {
+    const int pl = i / (RH * TX), rem = i - pl * RH * TX;
+    const int ry = rem / TX, lx = rem - ry * TX;
+    const uint8_t *row = &s_c[pl][ry][2 * lx + 2];
+    s_h[pl][ry][lx] = row[0] + 4 * (row[1] + row[3]) + 6 * row[2] + row[4];
+  }
+  __syncthreads();
+  // vertical: center row 2*loy + 2 of the region
+  for (int i = threadIdx.x; i < 2 * TY * TX; i += 256) {
+    const int pl = i / (TY * TX), rem = i - pl * TY * TX;
+    const int ly = rem / TX, lx = rem - ly * TX;
+    const int oy = oy0 + ly, ox = ox0 + lx;
+    if (oy < dh && ox < dw) {
+      const int v = s_h[pl][2 * ly][lx] + 4 * (s_h[pl][2 * ly + 1][lx] + s_h[pl][2 * ly + 3][lx]) +
+                    6 * s_h[pl][2 * ly + 2][lx] + s_h[pl][2 * ly + 4][lx];
+      (pl ? Cb : Cr)[(int64_t)oy * dw + ox] = (uint8_t)sat8((v + 128) >> 8);
+    }
+  }
+}
+
+__global__ void k_rgb_ycrcb(const uint8_t *__restrict__ rgb, int64_t npix, uint8_t *__restrict__ Y,
+                            uint8_t *__restrict__ Cr, uint8_t *__restrict__ Cb) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npix) return;
+  const uint8_t *p = rgb + 3 * i;
+  const YCC c = rgb2ycc(p[0], p[1], p[2]);
+  Y[i] = (uint8_t)c.y;
+  Cr[i] = (uint8_t)c.cr;
+  Cb[i] = (uint8_t)c.cb;
+}
+
+__global__ void k_pyr_down(const uint8_t *__restrict__ src, int H, int W, uint8_t *__restrict__ dst, int DH,
+                           int DW) {
+  const int ox = blockIdx.x * blockDim.x + threadIdx.x, oy = blockIdx.y;
+  if (ox >= DW || oy >= DH) return;
+  constexpr int K[5] = {1, 4, 6, 4, 1};
+  int acc = 0;
+#pragma unroll
+  for (int a = 0; a < 5; ++a) {
+    const int sy = refl101(2 * oy + a - 2, H);
+    int row = 0;
+#pragma unroll
+    for (int b = 0; b < 5; ++b) row += K[b] * src[(int64_t)sy * W + refl101(2 * ox + b - 2, W)];
+    acc += K[a] * row;
+  }
+  dst[(int64_t)oy * DW + ox] = (uint8_t)sat8((acc + 128) >> 8);
+}
+
+// pyrUp taps for output index o of a length-n source: even o -> [1 6 1] around o/2,
+// odd o -> [4 4] on (o/2, o/2+1); left border reflect-101, right border replicate.
+__device__ __forceinline__ void up_taps(int o, int n, int (&idx)[3], int (&w)[3]) {
+  const int s = o >> 1;
+  idx[0] = s > 0 ? s - 1 : (n > 1 ? 1 : 0);
+  idx[1] = s;
+  idx[2] = s + 1 < n ? s + 1 : n - 1;
+  if (o & 1) {
+    w[0] = 0; w[1] = 4; w[2] = 4;
+  } else {
+    w[0] = 1; w[1] = 6; w[2] = 1;
+  }
+}
+
+__device__ __forceinline__ int pyr_up_at(const uint8_t *__restrict__ src, int H, int W, int oy, int ox) {
+  int iy[3], wy[3], ix[3], wx[3];
+  up_taps(oy, H, iy, wy);
+  up_taps(ox, W, ix, wx);
+  int acc = 0;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    int row = 0;
+#pragma unroll
+    for (int b = 0; b < 3; ++b) row += wx[b] * src[(int64_t)iy[a] * W + ix[b]];
+    acc += wy[a] * row;
+  }
+  return (int)sat8((acc + 32) >> 6);
+}
+
+__global__ void k_pyr_up(const uint8_t *__restrict__ src, int H, int W, uint8_t *__restrict__ dst, int DH,
+                         int DW) {
+  const int ox = blockIdx.x * blockDim.x + threadIdx.x, oy = blockIdx.y;
+  if (ox >= DW || oy >= DH) return;
+  dst[(int64_t)oy * DW + ox] = (uint8_t)pyr_up_at(src, H, W, oy, ox);
+}
+
+// pyrUp(cr), pyrUp(cb) to 2h x 2w, crop y, cvtColor(YCrCb2RGB)
+__global__ void k_ycrcb420_rgb(const uint8_t *__restrict__ Y, int64_t ystride, const uint8_t *__restrict__ Cr,
+                               const uint8_t *__restrict__ Cb, int h, int w, uint8_t *__restrict__ rgb) {
+  const int ox = blockIdx.x * blockDim.x + threadIdx.x, oy = blockIdx.y;
+  if (ox >= 2 * w || oy >= 2 * h) return;
+  const int y = Y[(int64_t)oy * ystride + ox];
+  const int cr = pyr_up_at(Cr, h, w, oy, ox) - 128;
+  const int cb = pyr_up_at(Cb, h, w, oy, ox) - 128;
+  uint8_t *o = rgb + ((int64_t)oy * 2 * w + ox) * 3;
+  o[0] = (uint8_t)sat8(y + descale14(cr * kCR2R));
+  o[1] = (uint8_t)sat8(y + descale14(cb * kCB2G + cr * kCR2G));
+  o[2] = (uint8_t)sat8(y + descale14(cb * kCB2B));
+}
+
+bool dims_ok(int64_t H, int64_t W) { return H > 0 && W > 0 && H < (1 << 20) && W < (1 << 20); }
+
+}  // namespace
+}  // namespace hic
+
+using namespace hic;
+
+extern "C" int hic_rgb_to_ycrcb420(const uint8_t *rgb, int64_t H, int64_t W, uint8_t *y, uint8_t *cr,
+                                   uint8_t *cb, void *stream) {
+  if (!rgb || !y || !cr || !cb) return arg_error("null pointer");
+  if (!dims_ok(H, W) || H < 2 || W < 2) return arg_error("image shape (needs >= 2x2)");
+  if (reinterpret_cast<uintptr_t>(rgb) % 4 || reinterpret_cast<uintptr_t>(y) % 4)
+    return arg_error("rgb / y must be 4-byte aligned");
+  const int dh = (int)(H / 2), dw = (int)(W / 2);
+  const dim3 grid((dw + TX - 1) / TX, (dh + TY - 1) / TY);
+  hipLaunchKernelGGL(k_rgb_ycrcb420, grid, dim3(256), 0, as_stream(stream), rgb, (int)H, (int)W, y, cr, cb, dh, dw);
+  return check_launch("k_rgb_ycrcb420");
+}
+
+extern "C" int hic_rgb_to_ycrcb(const uint8_t *rgb, int64_t H, int64_t W, uint8_t *y, uint8_t *cr, uint8_t *cb,
+                                void *stream) {
+  if (!rgb || !y || !cr || !cb) return arg_error("null pointer");
+  if (!dims_ok(H, W)) return arg_error("image shape");
+  const int64_t n = H * W;
+  hipLaunchKernelGGL(k_rgb_ycrcb, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), rgb, n, y,
+                     cr, cb);
+  return check_launch("k_rgb_ycrcb");
+}
+
+extern "C" int hic_pyr_down_u8(const uint8_t *src, int64_t H, int64_t W, uint8_t *dst, int64_t DH, int64_t DW,
+                               void *stream) {
+  if (!src || !dst) return arg_error("null pointer");
+  if (!dims_ok(H, W) || DH <= 0 || DW <= 0) return arg_error("shape");
+  // OpenCV: |2*dsize - ssize| <= 2 in each dimension
+  if (2 * DW - W > 2 || W - 2 * DW > 2 || 2 * DH - H > 2 || H - 2 * DH > 2) return arg_error("pyrDown dstsize");
+  hipLaunchKernelGGL(k_pyr_down, dim3((unsigned)((DW + 255) / 256), (unsigned)DH), dim3(256), 0,
+                     as_stream(stream), src, (int)H, (int)W, dst, (int)DH, (int)DW);
+  return check_launch("k_pyr_down");
+}
+
+extern "C" int hic_pyr_up_u8(const uint8_t *src, int64_t H, int64_t W, uint8_t *dst, int64_t DH, int64_t DW,
+                             void *stream) {
+  if (!src || !dst) return arg_error("null pointer");
+  if (!dims_ok(H, W) || DH <= 0 || DW <= 0) return arg_error("shape");
+  // OpenCV: |dsize - 2*ssize| <= dsize % 2
+  if (DW - 2 * W > DW % 2 || 2 * W - DW > DW % 2 || DH - 2 * H > DH % 2 || 2 * H - DH > DH % 2)
+    return arg_error("pyrUp dstsize");
+  hipLaunchKernelGGL(k_pyr_up, dim3((unsigned)((DW + 255) / 256), (unsigned)DH), dim3(256), 0, as_stream(stream),
+                     src, (int)H, (int)W, dst, (int)DH, (int)DW);
+  return check_launch("k_pyr_up");
+}
+
+extern "C" int hic_ycrcb420_to_rgb(const uint8_t *y, int64_t y_stride, const uint8_t *cr, const uint8_t *cb,
+                                   int64_t h, int64_t w, uint8_t *rgb, void *stream) {
+  if (!y || !cr || !cb || !rgb) return arg_error("null pointer");
+  if (!dims_ok(2 * h, 2 * w) || y_stride < 2 * w) return arg_error("shape");
+  hipLaunchKernelGGL(k_ycrcb420_rgb, dim3((unsigned)((2 * w + 255) / 256), (unsigned)(2 * h)), dim3(256), 0,
+                     as_stream(stream), y, y_stride, cr, cb, (int)h, (int)w, rgb);
+  return check_launch("k_ycrcb420_rgb");
+}

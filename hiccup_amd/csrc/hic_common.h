@@ -1,0 +1,46 @@
+// hic_common.h -- shared plumbing for the libhiccup_hip.so C-ABI: error state,
+// launch checks, wave-level helpers.  gfx950 only (wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../../include/hiccup_hip.h"
+
+namespace hic {
+
+// Per-thread last-error text (hic_last_error).
+void set_error(const char *fmt, ...);
+
+inline int arg_error(const char *what) {
+  set_error("invalid argument: %s", what);
+  return HIC_ERR_ARG;
+}
+
+inline int check_launch(const char *kernel) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s launch failed: %s", kernel, hipGetErrorString(e));
+    return HIC_ERR_HIP;
+  }
+  return HIC_OK;
+}
+
+inline int hip_status(hipError_t e, const char *what) {
+  if (e != hipSuccess) {
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return HIC_ERR_HIP;
+  }
+  return HIC_OK;
+}
+
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+constexpr int kWave = 64;
+
+// Round n up to a multiple of a.
+__host__ __device__ inline int64_t round_up(int64_t n, int64_t a) { return (n + a - 1) / a * a; }
+__host__ __device__ inline int64_t ceil_div(int64_t n, int64_t a) { return (n + a - 1) / a; }
+
+}  // namespace hic

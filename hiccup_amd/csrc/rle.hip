@@ -1,0 +1,664 @@
+// rle.hip -- zig-zag / DC-DPCM / AC run-length front end of hiccup's JPEG codec
+// and its inverse, on MI355X.
+//
+// Reference: codec.run_length_coding (codec.py:55-99), codec.decode_run_length
+// (codec.py:102-113), codec.differential_coding (codec.py:47-52),
+// utils.differences / invert_differences (utils.py:51-73), the AC-stream
+// assembly of codec.jpeg_encode (codec.py:292-301: for every block in raster
+// order, zigzag(block)[1:], concatenated over the whole channel) and its
+// inverse in codec.jpeg_decode (codec.py:397-425).
+//
+// The reference RLE is ONE sequential scan over a channel's entire AC stream:
+// runs cross block boundaries, a trailing zero run becomes the single EOB (0,0),
+// and a run l >= max_len becomes l/max_len fillers (max_len-1, 0) + (l%max_len, v).
+// Here it is a three-pass decoupled scan:
+//   K1 (per tile of 256 blocks, one block per lane): first/last nonzero and the
+//       symbol count of every nonzero whose predecessor is inside the tile;
+//   K2 (one workgroup): exclusive max-scan of "last nonzero" and exclusive
+//       sum-scan of per-tile symbol counts -> tile offsets; EOB; total count;
+//   K3 (per tile): recompute, scan inside the tile, write symbols (SoA) and the
+//       DC differences.  Long filler runs (a nonzero after many all-zero blocks)
+//       are written cooperatively by the whole workgroup.
+// Sharding: the same kernels take a carry (zeros preceding the shard since the
+// last nonzero of earlier shards), the previous shard's last DC, and whether this
+// shard closes the stream (EOB) -- see hic_rle_stitch.
+#include "hic_common.h"
+
+namespace hic {
+namespace {
+
+constexpr int kTB = 256;  // blocks (= lanes) per tile
+
+// ---- workgroup scan helpers (256 threads = 4 waves) -------------------------
+template <typename T>
+__device__ __forceinline__ T wave_incl_sum(T v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const T o = __shfl_up(v, d, 64);
+    if (lane >= d) v += o;
+  }
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_incl_max(T v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const T o = __shfl_up(v, d, 64);
+    if (lane >= d) v = v > o ? v : o;
+  }
+  return v;
+}
+
+// Exclusive sum over the workgroup; returns the exclusive prefix, sets total.
+template <typename T, int NT>
+__device__ __forceinline__ T block_excl_sum(T v, T *s_buf, T &total) {
+  constexpr int NW = NT / 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const T incl = wave_incl_sum(v);
+  if (lane == 63) s_buf[wave] = incl;
+  __syncthreads();
+  T pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    if (w < wave) pre += s_buf[w];
+    tot += s_buf[w];
+  }
+  __syncthreads();
+  total = tot;
+  return pre + incl - v;
+}
+// Exclusive max over the workgroup (identity `ident`); sets the overall max.
+template <typename T, int NT>
+__device__ __forceinline__ T block_excl_max(T v, T ident, T *s_buf, T &all) {
+  constexpr int NW = NT / 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const T incl = wave_incl_max(v);
+  T excl = __shfl_up(incl, 1, 64);
+  if (lane == 0) excl = ident;
+  if (lane == 63) s_buf[wave] = incl;
+  __syncthreads();
+  T pre = ident, a = ident;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    if (w < wave) pre = pre > s_buf[w] ? pre : s_buf[w];
+    a = a > s_buf[w] ? a : s_buf[w];
+  }
+  __syncthreads();
+  all = a;
+  return excl > pre ? excl : pre;
+}
+
+// Block scan: first/last nonzero AC index (-1 if none) and the symbols of every
+// nonzero after the first (runs inside the block).
+__device__ __forceinline__ int syms_for_run(int64_t run, int M) { return 1 + (M > 0 ? (int)(run / M) : 0); }
+
+// Element j (0 <= j < A) of block b lives at blocks[b*L + off + j]; its global
+// stream position is b*A + j and only positions < n_ac exist.
+struct StreamGeo {
+  int L, off, A;
+  int64_t n_ac;
+};
+
+template <typename T>
+__device__ __forceinline__ void summarize(const T *__restrict__ blocks, int64_t b, const StreamGeo &g, int M,
+                                          int &first, int &last, int &nsym_in) {
+  first = -1;
+  last = -1;
+  nsym_in = 0;
+  const T *blk = blocks + b * g.L + g.off;
+  if (sizeof(T) == 2 && g.L == 64 && g.off == 1 && (b + 1) * g.A <= g.n_ac) {
+    // hot path: one 128-byte zig-zag block held in registers
+    const uint4 *q = reinterpret_cast<const uint4 *>(blocks + b * 64);
+    uint32_t w[32];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint4 t = q[k];
+      w[4 * k] = t.x; w[4 * k + 1] = t.y; w[4 * k + 2] = t.z; w[4 * k + 3] = t.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 63; ++j) {
+      const int s = j + 1;
+      const bool nz = ((w[s >> 1] >> (16 * (s & 1))) & 0xFFFFu) != 0;
+      if (nz) {
+        if (first < 0)
+          first = j;
+        else
+          nsym_in += syms_for_run(j - last - 1, M);
+        last = j;
+      }
+    }
+  } else {
+    const int64_t lim = g.n_ac - b * g.A;
+    const int A = lim < g.A ? (int)(lim > 0 ? lim : 0) : g.A;
+    for (int j = 0; j < A; ++j) {
+      if (blk[j] != 0) {
+        if (first < 0)
+          first = j;
+        else
+          nsym_in += syms_for_run(j - last - 1, M);
+        last = j;
+      }
+    }
+  }
+}
+
+// K1: per-tile aggregates.  ws layout per tile: [0] first (global), [1] last
+// (global), [2] symbols except the tile's first nonzero's.
+template <typename T>
+__global__ __launch_bounds__(kTB) void k_rle_tile(const T *__restrict__ blocks, int64_t nblk, StreamGeo g, int M,
+                                                  int64_t *__restrict__ tiles) {
+  __shared__ int64_t s_buf[8];
+  const int64_t b = (int64_t)blockIdx.x * kTB + threadIdx.x;
+  int first = -1, last = -1, nsym = 0;
+  if (b < nblk) summarize(blocks, b, g, M, first, last, nsym);
+  const int64_t base = b * g.A;
+  const int64_t lastg = last >= 0 ? base + last : -1;
+  int64_t all_last;
+  const int64_t prev = block_excl_max<int64_t, kTB>(lastg, (int64_t)-1, s_buf, all_last);
+  int64_t cnt = nsym;
+  if (first >= 0 && prev >= 0) cnt += syms_for_run(base + first - prev - 1, M);
+  int64_t total;
+  block_excl_sum<int64_t, kTB>(cnt, s_buf, total);
+  // the tile's first nonzero: the only lane with a nonzero and no predecessor
+  if (first >= 0 && prev < 0) tiles[blockIdx.x * 3 + 0] = base + first;
+  if (threadIdx.x == 0) {
+    tiles[blockIdx.x * 3 + 1] = all_last;
+    tiles[blockIdx.x * 3 + 2] = total;
+    if (all_last < 0) tiles[blockIdx.x * 3 + 0] = -1;
+  }
+}
+
+// K2: single workgroup of 1024 threads.  Produces per tile: [3] symbol offset,
+// [4] global position of the last nonzero before the tile (virtual -1-carry if
+// none).  Writes the EOB symbol and the count.
+constexpr int kScanT = 1024;
+template <typename L_T, typename V_T>
+__global__ __launch_bounds__(kScanT) void k_rle_scan(int64_t *__restrict__ tiles, int64_t *__restrict__ offs,
+                                                     int64_t ntiles, int64_t n_ac, int M,
+                                                     const int64_t *__restrict__ stitch, L_T *__restrict__ sym_len,
+                                                     V_T *__restrict__ sym_val, int64_t cap,
+                                                     int64_t *__restrict__ d_count) {
+  __shared__ int64_t s_buf[32];
+  const int64_t carry = stitch ? stitch[0] : 0;
+  const bool emit_eob = stitch ? stitch[1] != 0 : true;
+  int64_t run_prev = -1 - carry;  // running "last nonzero" before the chunk
+  int64_t run_off = 0;
+  for (int64_t c0 = 0; c0 < ntiles; c0 += kScanT) {
+    const int64_t t = c0 + threadIdx.x;
+    int64_t first = -1, last = -1, nsym = 0;
+    if (t < ntiles) {
+      first = tiles[t * 3 + 0];
+      last = tiles[t * 3 + 1];
+      nsym = tiles[t * 3 + 2];
+    }
+    int64_t chunk_last;
+    int64_t prev = block_excl_max<int64_t, kScanT>(last, (int64_t)-1, s_buf, chunk_last);
+    if (prev < 0) prev = run_prev;
+    int64_t cnt = nsym + (first >= 0 ? syms_for_run(first - prev - 1, M) : 0);
+    int64_t chunk_total;
+    const int64_t off = run_off + block_excl_sum<int64_t, kScanT>(cnt, s_buf, chunk_total);
+    if (t < ntiles) {
+      offs[t * 2 + 0] = off;
+      offs[t * 2 + 1] = prev;
+    }
+    if (chunk_last >= 0) run_prev = chunk_last;
+    run_off += chunk_total;
+  }
+  if (threadIdx.x == 0) {
+    const bool ends_nonzero = n_ac > 0 && run_prev == n_ac - 1;
+    int64_t total = run_off;
+    if (emit_eob && !ends_nonzero) {
+      if (total < cap) {
+        sym_len[total] = 0;
+        sym_val[total] = 0;
+      }
+      ++total;
+    }
+    *d_count = total <= cap ? total : -total;
+  }
+}
+
+// K3: emit symbols (+ DC differences when dc_diff != nullptr).
+template <typename T, typename L_T, typename V_T>
+__global__ __launch_bounds__(kTB) void k_rle_emit(const T *__restrict__ blocks, int64_t nblk, StreamGeo g, int M,
+                                                  const int64_t *__restrict__ offs, const int64_t *__restrict__ stitch,
+                                                  int32_t *__restrict__ dc_diff, L_T *__restrict__ sym_len,
+                                                  V_T *__restrict__ sym_val, int64_t cap) {
+  __shared__ int64_t s_buf[8];
+  __shared__ int64_t s_fill_start[kTB];
+  __shared__ int64_t s_fill_count[kTB];
+  __shared__ int s_nfill;
+  if (threadIdx.x == 0) s_nfill = 0;
+  const int64_t b = (int64_t)blockIdx.x * kTB + threadIdx.x;
+  int first = -1, last = -1, nsym = 0;
+  if (b < nblk) summarize(blocks, b, g, M, first, last, nsym);
+  const int64_t base = b * g.A;
+  const int64_t lastg = last >= 0 ? base + last : -1;
+  int64_t all_last;
+  int64_t prev = block_excl_max<int64_t, kTB>(lastg, (int64_t)-1, s_buf, all_last);
+  if (prev < 0) prev = offs[blockIdx.x * 2 + 1];
+  const int64_t cnt = nsym + (first >= 0 ? syms_for_run(base + first - prev - 1, M) : 0);
+  int64_t total;
+  int64_t o = offs[blockIdx.x * 2 + 0] + block_excl_sum<int64_t, kTB>(cnt, s_buf, total);
+
+  if (b < nblk) {
+    if (dc_diff) {  // codec.differential_coding over raster-ordered blocks
+      const int dc = (int)blocks[b * g.L];
+      if (b > 0)
+        dc_diff[b] = dc - (int)blocks[(b - 1) * g.L];
+      else
+        dc_diff[b] = (stitch && stitch[2]) ? dc - (int)stitch[3] : dc;
+    }
+    if (first >= 0) {
+      const T *blk = blocks + b * g.L + g.off;
+      int64_t p = prev;
+      for (int j = first; j <= last; ++j) {
+        const int v = (int)blk[j];
+        if (v == 0) continue;
+        int64_t run = base + j - p - 1;
+        if (M > 0) {
+          const int64_t nf = run / M;
+          if (nf > 32) {
+            // long carried-in run: the whole workgroup writes the fillers
+            const int slot = atomicAdd(&s_nfill, 1);
+            s_fill_start[slot] = o;
+            s_fill_count[slot] = nf;
+            o += nf;
+          } else {
+            for (int64_t k = 0; k < nf; ++k, ++o)
+              if (o < cap) {
+                sym_len[o] = (L_T)(M - 1);
+                sym_val[o] = 0;
+              }
+          }
+          run -= nf * M;
+        }
+        if (o < cap) {
+          sym_len[o] = (L_T)run;
+          sym_val[o] = (V_T)v;
+        }
+        ++o;
+        p = base + j;
+      }
+    }
+  }
+  __syncthreads();
+  const int nfill = s_nfill;
+  for (int f = 0; f < nfill; ++f) {
+    const int64_t s0 = s_fill_start[f], nf = s_fill_count[f];
+    for (int64_t k = threadIdx.x; k < nf; k += kTB)
+      if (s0 + k < cap) {
+        sym_len[s0 + k] = (L_T)(M - 1);
+        sym_val[s0 + k] = 0;
+      }
+  }
+}
+
+// Shard summary: {trailing_zeros, has_nonzero, first_dc, last_dc}
+template <typename T>
+__global__ void k_rle_summary(const T *__restrict__ blocks, int64_t nblk, StreamGeo g,
+                              const int64_t *__restrict__ tiles, int64_t ntiles, int64_t *__restrict__ out) {
+  __shared__ int64_t s_buf[8];
+  int64_t m = -1;
+  for (int64_t t = threadIdx.x; t < ntiles; t += kTB) {
+    const int64_t v = tiles[t * 3 + 1];
+    m = v > m ? v : m;
+  }
+  int64_t all;
+  block_excl_max<int64_t, kTB>(m, (int64_t)-1, s_buf, all);
+  if (threadIdx.x == 0) {
+    out[0] = g.n_ac - 1 - all;  // == n_ac when there is no nonzero
+    out[1] = all >= 0 ? 1 : 0;
+    out[2] = nblk > 0 ? (int64_t)blocks[0] : 0;
+    out[3] = nblk > 0 ? (int64_t)blocks[(nblk - 1) * g.L] : 0;
+  }
+}
+
+__global__ void k_rle_stitch(const int64_t *__restrict__ all, int world, int rank, int64_t *__restrict__ st) {
+  if (threadIdx.x != 0) return;
+  int64_t carry = 0;
+  for (int r = rank - 1; r >= 0; --r) {
+    carry += all[r * 4 + 0];
+    if (all[r * 4 + 1]) break;
+  }
+  st[0] = carry;
+  st[1] = rank == world - 1 ? 1 : 0;
+  st[2] = rank > 0 ? 1 : 0;
+  st[3] = rank > 0 ? all[(rank - 1) * 4 + 3] : 0;
+}
+
+// ---------------------------------------------------------------------------
+// Decode: symbols -> zig-zag blocks
+constexpr int kSPT = 8;                // symbols per thread
+constexpr int kTS = kTB * kSPT;        // symbols per tile
+
+template <typename L_T>
+__global__ __launch_bounds__(kTB) void k_rld_tile(const L_T *__restrict__ sym_len, int64_t nsym,
+                                                  int64_t *__restrict__ tile_sum) {
+  __shared__ int64_t s_buf[8];
+  const int64_t s0 = (int64_t)blockIdx.x * kTS + (int64_t)threadIdx.x * kSPT;
+  int64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < kSPT; ++k)
+    if (s0 + k < nsym) acc += (int64_t)sym_len[s0 + k] + 1;
+  int64_t total;
+  block_excl_sum<int64_t, kTB>(acc, s_buf, total);
+  if (threadIdx.x == 0) tile_sum[blockIdx.x] = total;
+}
+
+// In-place exclusive scan of n int64 values by one workgroup; returns total in *out_total.
+__global__ __launch_bounds__(kScanT) void k_scan_inplace(int64_t *__restrict__ v, int64_t n,
+                                                         int64_t *__restrict__ out_total) {
+  __shared__ int64_t s_buf[32];
+  int64_t run = 0;
+  for (int64_t c0 = 0; c0 < n; c0 += kScanT) {
+    const int64_t i = c0 + threadIdx.x;
+    const int64_t x = i < n ? v[i] : 0;
+    int64_t tot;
+    const int64_t e = block_excl_sum<int64_t, kScanT>(x, s_buf, tot);
+    if (i < n) v[i] = run + e;
+    run += tot;
+  }
+  if (threadIdx.x == 0) *out_total = run;
+}
+
+template <typename L_T, typename V_T, typename T>
+__global__ __launch_bounds__(kTB) void k_rld_scatter(const L_T *__restrict__ sym_len, const V_T *__restrict__ sym_val,
+                                                     int64_t nsym, const int64_t *__restrict__ tile_off, StreamGeo g,
+                                                     T *__restrict__ blocks) {
+  __shared__ int64_t s_buf[8];
+  const int64_t s0 = (int64_t)blockIdx.x * kTS + (int64_t)threadIdx.x * kSPT;
+  int64_t acc = 0;
+  int lens[kSPT];
+#pragma unroll
+  for (int k = 0; k < kSPT; ++k) {
+    lens[k] = s0 + k < nsym ? (int)sym_len[s0 + k] : 0;
+    if (s0 + k < nsym) acc += (int64_t)lens[k] + 1;
+  }
+  int64_t total;
+  int64_t pos = tile_off[blockIdx.x] + block_excl_sum<int64_t, kTB>(acc, s_buf, total);
+#pragma unroll
+  for (int k = 0; k < kSPT; ++k) {
+    if (s0 + k < nsym) {
+      pos += lens[k];
+      if (pos < g.n_ac) {
+        const int64_t bb = pos / g.A, j = pos - bb * g.A;
+        blocks[bb * g.L + g.off + j] = (T)sym_val[s0 + k];
+      }
+      ++pos;
+    }
+  }
+}
+
+// DC: per-tile sums, scan, then write prefix sums into slot 0 of every block.
+__global__ __launch_bounds__(kTB) void k_dc_tile(const int32_t *__restrict__ diff, int64_t nblk,
+                                                 int64_t *__restrict__ tile_sum) {
+  __shared__ int64_t s_buf[8];
+  const int64_t s0 = (int64_t)blockIdx.x * kTS + (int64_t)threadIdx.x * kSPT;
+  int64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < kSPT; ++k)
+    if (s0 + k < nblk) acc += diff[s0 + k];
+  int64_t total;
+  block_excl_sum<int64_t, kTB>(acc, s_buf, total);
+  if (threadIdx.x == 0) tile_sum[blockIdx.x] = total;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kTB) void k_dc_apply(const int32_t *__restrict__ diff, int64_t nblk,
+                                                  const int64_t *__restrict__ tile_off, int L, T *__restrict__ blocks) {
+  __shared__ int64_t s_buf[8];
+  const int64_t s0 = (int64_t)blockIdx.x * kTS + (int64_t)threadIdx.x * kSPT;
+  int64_t acc = 0;
+  int d[kSPT];
+#pragma unroll
+  for (int k = 0; k < kSPT; ++k) {
+    d[k] = s0 + k < nblk ? diff[s0 + k] : 0;
+    acc += d[k];
+  }
+  int64_t total;
+  int64_t run = tile_off[blockIdx.x] + block_excl_sum<int64_t, kTB>(acc, s_buf, total);
+#pragma unroll
+  for (int k = 0; k < kSPT; ++k)
+    if (s0 + k < nblk) {
+      run += d[k];
+      blocks[(s0 + k) * L] = (T)run;
+    }
+}
+
+__global__ void k_rld_status(const int64_t *__restrict__ total, const int64_t *__restrict__ last_sym, int64_t n_ac,
+                             int64_t *__restrict__ status) {
+  // codec.decode_run_length: EOB (last symbol (0,0)) zero-fills up to `length`
+  const int64_t t = *total;
+  const bool eob = last_sym[0] == 0 && last_sym[1] == 0;
+  *status = (eob && t < n_ac) ? n_ac : t;
+}
+
+template <typename L_T, typename V_T>
+__global__ void k_last_sym(const L_T *__restrict__ sym_len, const V_T *__restrict__ sym_val, int64_t nsym,
+                           int64_t *__restrict__ out) {
+  out[0] = nsym > 0 ? (int64_t)sym_len[nsym - 1] : 1;
+  out[1] = nsym > 0 ? (int64_t)sym_val[nsym - 1] : 1;
+}
+
+// ---------------------------------------------------------------------------
+// Generic split_matrix + zigzag for block size N (any N), int32.
+__device__ __forceinline__ void zz_pos(int z, int N, int &y, int &x) {
+  int s = 0;
+  for (;; ++s) {
+    const int len = s < N ? s + 1 : 2 * N - 1 - s;
+    if (z < len) break;
+    z -= len;
+  }
+  const int ylo = s - (N - 1) > 0 ? s - (N - 1) : 0;
+  const int yhi = s < N - 1 ? s : N - 1;
+  y = (s % 2 == 0) ? ylo + z : yhi - z;
+  x = s - y;
+}
+
+__global__ void k_zigzag_i32(const int32_t *__restrict__ raster, int H, int W, int N, int nbx, int64_t total,
+                             int32_t *__restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int NN = N * N;
+  const int64_t b = i / NN;
+  const int z = (int)(i - b * NN);
+  const int bi = (int)(b / nbx), bj = (int)(b - (int64_t)bi * nbx);
+  int u, v;
+  zz_pos(z, N, u, v);
+  const int yy = bi * N + u, xx = bj * N + v;
+  out[i] = (yy < H && xx < W) ? raster[(int64_t)yy * W + xx] : 0;
+}
+
+__global__ void k_izigzag_i32(const int32_t *__restrict__ blocks, int H, int W, int N, int nbx, int64_t total,
+                              int32_t *__restrict__ raster) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int NN = N * N;
+  const int64_t b = i / NN;
+  const int z = (int)(i - b * NN);
+  const int bi = (int)(b / nbx), bj = (int)(b - (int64_t)bi * nbx);
+  int u, v;
+  zz_pos(z, N, u, v);
+  const int yy = bi * N + u, xx = bj * N + v;
+  if (yy < H && xx < W) raster[(int64_t)yy * W + xx] = blocks[i];
+}
+
+// ---------------------------------------------------------------------------
+inline int64_t ntiles_of(int64_t nblk) { return (nblk + kTB - 1) / kTB; }
+
+template <typename T, typename L_T, typename V_T>
+int rle_encode(const T *blocks, int64_t nblk, StreamGeo g, int M, const int64_t *stitch, int32_t *dc_diff,
+               L_T *sym_len, V_T *sym_val, int64_t cap, int64_t *d_count, void *ws, hipStream_t s) {
+  if (!blocks || !sym_len || !sym_val || !d_count || !ws) return arg_error("null pointer");
+  if (nblk <= 0 || g.A < 1 || g.n_ac < 0) return arg_error("nblk / block_len");
+  if (M < 0) return arg_error("max_len");
+  const int64_t nt = ntiles_of(nblk);
+  int64_t *tiles = static_cast<int64_t *>(ws);
+  int64_t *offs = tiles + 3 * nt;
+  hipLaunchKernelGGL((k_rle_tile<T>), dim3((unsigned)nt), dim3(kTB), 0, s, blocks, nblk, g, M, tiles);
+  if (int e = check_launch("k_rle_tile")) return e;
+  hipLaunchKernelGGL((k_rle_scan<L_T, V_T>), dim3(1), dim3(kScanT), 0, s, tiles, offs, nt, g.n_ac, M, stitch,
+                     sym_len, sym_val, cap, d_count);
+  if (int e = check_launch("k_rle_scan")) return e;
+  hipLaunchKernelGGL((k_rle_emit<T, L_T, V_T>), dim3((unsigned)nt), dim3(kTB), 0, s, blocks, nblk, g, M, offs,
+                     stitch, dc_diff, sym_len, sym_val, cap);
+  return check_launch("k_rle_emit");
+}
+
+inline StreamGeo block_geo(int64_t nblk, int L) { return StreamGeo{L, 1, L - 1, nblk * (L - 1)}; }
+inline StreamGeo raw_geo(int64_t n) { return StreamGeo{64, 0, 64, n}; }
+
+template <typename T>
+int rle_summary(const T *blocks, int64_t nblk, int L, void *ws, int64_t *d_summary, hipStream_t s) {
+  if (!blocks || !ws || !d_summary) return arg_error("null pointer");
+  if (nblk <= 0 || L < 2) return arg_error("nblk / block_len");
+  const int64_t nt = ntiles_of(nblk);
+  const StreamGeo g = block_geo(nblk, L);
+  int64_t *tiles = static_cast<int64_t *>(ws);
+  hipLaunchKernelGGL((k_rle_tile<T>), dim3((unsigned)nt), dim3(kTB), 0, s, blocks, nblk, g, 15, tiles);
+  if (int e = check_launch("k_rle_tile")) return e;
+  hipLaunchKernelGGL((k_rle_summary<T>), dim3(1), dim3(kTB), 0, s, blocks, nblk, g, tiles, nt, d_summary);
+  return check_launch("k_rle_summary");
+}
+
+template <typename L_T, typename V_T, typename T>
+int rle_decode(const L_T *sym_len, const V_T *sym_val, int64_t nsym, const int32_t *dc_diff, int64_t nblk,
+               StreamGeo g, int64_t length, T *blocks, int64_t *d_status, void *ws, hipStream_t s) {
+  if (!sym_len || !sym_val || !blocks || !d_status || !ws) return arg_error("null pointer");
+  if (nblk <= 0 || g.A < 1 || nsym < 0) return arg_error("sizes");
+  const int64_t nts = (nsym + kTS - 1) / kTS, ntb = (nblk + kTS - 1) / kTS;
+  int64_t *w = static_cast<int64_t *>(ws);
+  int64_t *tsum = w, *dsum = w + nts + 1, *tot = dsum + ntb + 1, *last = tot + 2;
+  if (int e = hip_status(hipMemsetAsync(blocks, 0, (size_t)nblk * g.L * sizeof(T), s), "hipMemsetAsync")) return e;
+  if (nsym > 0) {
+    hipLaunchKernelGGL((k_rld_tile<L_T>), dim3((unsigned)nts), dim3(kTB), 0, s, sym_len, nsym, tsum);
+    if (int e = check_launch("k_rld_tile")) return e;
+  }
+  hipLaunchKernelGGL(k_scan_inplace, dim3(1), dim3(kScanT), 0, s, tsum, nts, tot);
+  if (nsym > 0) {
+    hipLaunchKernelGGL((k_rld_scatter<L_T, V_T, T>), dim3((unsigned)nts), dim3(kTB), 0, s, sym_len, sym_val, nsym,
+                       tsum, g, blocks);
+    if (int e = check_launch("k_rld_scatter")) return e;
+  }
+  if (dc_diff) {
+    hipLaunchKernelGGL(k_dc_tile, dim3((unsigned)ntb), dim3(kTB), 0, s, dc_diff, nblk, dsum);
+    hipLaunchKernelGGL(k_scan_inplace, dim3(1), dim3(kScanT), 0, s, dsum, ntb, tot + 1);
+    hipLaunchKernelGGL((k_dc_apply<T>), dim3((unsigned)ntb), dim3(kTB), 0, s, dc_diff, nblk, dsum, g.L, blocks);
+  }
+  hipLaunchKernelGGL((k_last_sym<L_T, V_T>), dim3(1), dim3(1), 0, s, sym_len, sym_val, nsym, last);
+  hipLaunchKernelGGL(k_rld_status, dim3(1), dim3(1), 0, s, tot, last, length, d_status);
+  return check_launch("k_rld_status");
+}
+
+}  // namespace
+}  // namespace hic
+
+using namespace hic;
+
+extern "C" size_t hic_rle_workspace_bytes(int64_t nblk, int block_len) {
+  (void)block_len;
+  return (size_t)(5 * ntiles_of(nblk > 0 ? nblk : 1) + 8) * sizeof(int64_t);
+}
+
+extern "C" int hic_rle_shard_summary_i16(const int16_t *blocks, int64_t nblk, int block_len, void *workspace,
+                                         int64_t *d_summary, void *stream) {
+  return rle_summary(blocks, nblk, block_len, workspace, d_summary, as_stream(stream));
+}
+extern "C" int hic_rle_shard_summary_i32(const int32_t *blocks, int64_t nblk, int block_len, void *workspace,
+                                         int64_t *d_summary, void *stream) {
+  return rle_summary(blocks, nblk, block_len, workspace, d_summary, as_stream(stream));
+}
+
+extern "C" int hic_rle_encode_i16(const int16_t *blocks, int64_t nblk, int block_len, int max_len,
+                                  const int64_t *d_stitch, int32_t *dc_diff, uint8_t *sym_len, int16_t *sym_val,
+                                  int64_t sym_cap, int64_t *d_count, void *workspace, void *stream) {
+  // uint8 lengths: fillers are max_len-1 <= 255 and residual runs < max_len
+  if (max_len < 1 || max_len > 256) return arg_error("max_len must be in [1, 256] for uint8 symbol lengths");
+  if (block_len < 2) return arg_error("block_len");
+  if (!dc_diff) return arg_error("null dc_diff");
+  return rle_encode(blocks, nblk, block_geo(nblk, block_len), max_len, d_stitch, dc_diff, sym_len, sym_val, sym_cap,
+                    d_count, workspace, as_stream(stream));
+}
+
+extern "C" int hic_rle_encode_i32(const int32_t *blocks, int64_t nblk, int block_len, int max_len,
+                                  const int64_t *d_stitch, int32_t *dc_diff, int32_t *sym_len, int32_t *sym_val,
+                                  int64_t sym_cap, int64_t *d_count, void *workspace, void *stream) {
+  if (block_len < 2) return arg_error("block_len");
+  if (!dc_diff) return arg_error("null dc_diff");
+  return rle_encode(blocks, nblk, block_geo(nblk, block_len), max_len, d_stitch, dc_diff, sym_len, sym_val, sym_cap,
+                    d_count, workspace, as_stream(stream));
+}
+
+extern "C" int hic_rle_stream_encode_i32(const int32_t *arr, int64_t n, int max_len, int32_t *sym_len,
+                                         int32_t *sym_val, int64_t sym_cap, int64_t *d_count, void *workspace,
+                                         void *stream) {
+  // codec.run_length_coding on an arbitrary 1-D array (n may be 0: -> [EOB])
+  static const int32_t kZero = 0;
+  const int64_t nblk = n > 0 ? (n + 63) / 64 : 1;
+  return rle_encode(n > 0 ? arr : &kZero, nblk, raw_geo(n), max_len, nullptr, nullptr, sym_len, sym_val, sym_cap,
+                    d_count, workspace, as_stream(stream));
+}
+
+extern "C" int hic_rle_stitch(const int64_t *d_all_summaries, int world, int rank, int64_t *d_stitch, void *stream) {
+  if (!d_all_summaries || !d_stitch) return arg_error("null pointer");
+  if (world < 1 || rank < 0 || rank >= world) return arg_error("world / rank");
+  hipLaunchKernelGGL(k_rle_stitch, dim3(1), dim3(64), 0, as_stream(stream), d_all_summaries, world, rank, d_stitch);
+  return check_launch("k_rle_stitch");
+}
+
+extern "C" size_t hic_rld_workspace_bytes(int64_t nsym, int64_t nblk) {
+  return (size_t)((nsym + kTS - 1) / kTS + (nblk + kTS - 1) / kTS + 8) * sizeof(int64_t);
+}
+
+extern "C" int hic_rle_decode_i16(const uint8_t *sym_len, const int16_t *sym_val, int64_t nsym,
+                                  const int32_t *dc_diff, int64_t nblk, int block_len, int16_t *blocks,
+                                  int64_t *d_status, void *workspace, void *stream) {
+  if (block_len < 2 || !dc_diff) return arg_error("block_len / dc_diff");
+  return rle_decode(sym_len, sym_val, nsym, dc_diff, nblk, block_geo(nblk, block_len), nblk * (block_len - 1), blocks,
+                    d_status, workspace,
+                    as_stream(stream));
+}
+
+extern "C" int hic_rle_decode_i32(const int32_t *sym_len, const int32_t *sym_val, int64_t nsym,
+                                  const int32_t *dc_diff, int64_t nblk, int block_len, int32_t *blocks,
+                                  int64_t *d_status, void *workspace, void *stream) {
+  if (block_len < 2 || !dc_diff) return arg_error("block_len / dc_diff");
+  return rle_decode(sym_len, sym_val, nsym, dc_diff, nblk, block_geo(nblk, block_len), nblk * (block_len - 1), blocks,
+                    d_status, workspace,
+                    as_stream(stream));
+}
+
+extern "C" int hic_rle_stream_decode_i32(const int32_t *sym_len, const int32_t *sym_val, int64_t nsym, int64_t length,
+                                         int32_t *out, int64_t out_cap, int64_t *d_status, void *workspace,
+                                         void *stream) {
+  // codec.decode_run_length: out[0:*d_status] is the decoded list; out has room for
+  // out_cap >= max(length, sum(len+1)) elements, out_cap a multiple of 64.
+  if (out_cap < 64 || out_cap % 64) return arg_error("out_cap must be a positive multiple of 64");
+  if (length < 0) return arg_error("length");
+  return rle_decode(sym_len, sym_val, nsym, nullptr, out_cap / 64, raw_geo(out_cap), length, out, d_status, workspace,
+                    as_stream(stream));
+}
+
+extern "C" int hic_zigzag_blocks_i32(const int32_t *raster, int64_t H, int64_t W, int N, int32_t *out, void *stream) {
+  if (!raster || !out) return arg_error("null pointer");
+  if (H <= 0 || W <= 0 || N <= 0 || N > 256) return arg_error("shape / N");
+  const int nbx = (int)((W + N - 1) / N), nby = (int)((H + N - 1) / N);
+  const int64_t total = (int64_t)nbx * nby * N * N;
+  hipLaunchKernelGGL(k_zigzag_i32, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream), raster,
+                     (int)H, (int)W, N, nbx, total, out);
+  return check_launch("k_zigzag_i32");
+}
+
+extern "C" int hic_izigzag_blocks_i32(const int32_t *blocks, int64_t H, int64_t W, int N, int32_t *raster,
+                                      void *stream) {
+  if (!raster || !blocks) return arg_error("null pointer");
+  if (H <= 0 || W <= 0 || N <= 0 || N > 256) return arg_error("shape / N");
+  const int nbx = (int)((W + N - 1) / N), nby = (int)((H + N - 1) / N);
+  const int64_t total = (int64_t)nbx * nby * N * N;
+  hipLaunchKernelGGL(k_izigzag_i32, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream), blocks,
+                     (int)H, (int)W, N, nbx, total, raster);
+  return check_launch("k_izigzag_i32");
+}

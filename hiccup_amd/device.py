@@ -1,0 +1,59 @@
+"""Device plumbing: PyTorch-ROCm provides HBM allocations and the HIP stream;
+the compute is entirely in libhiccup_hip.so.  No CPU fallback: without a HIP
+device every entry point raises ``HipUnavailable``."""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import HipUnavailable
+
+_checked = False
+
+
+def require_gpu():
+    global _checked
+    if not _checked:
+        _lib.load()
+        if not torch.cuda.is_available():
+            raise HipUnavailable("no HIP device visible: hiccup_amd runs only on MI355X (gfx950); "
+                                 "there is no CPU fallback")
+        _checked = True
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def to_device(a):
+    require_gpu()
+    return torch.from_numpy(np.ascontiguousarray(a)).to("cuda")
+
+
+def empty(shape, dtype):
+    require_gpu()
+    return torch.empty(shape, dtype=dtype, device="cuda")
+
+
+def zeros(shape, dtype):
+    require_gpu()
+    return torch.zeros(shape, dtype=dtype, device="cuda")
+
+
+def workspace(nbytes):
+    return empty((max(int(nbytes), 8) + 7) // 8, torch.int64)
+
+
+def sync(stream=None):
+    _lib.call("hic_stream_sync", stream_ptr(stream))
+
+
+def to_host(t):
+    sync()
+    return t.cpu().numpy()

@@ -1,0 +1,182 @@
+/*
+ * hiccup_hip.h -- C-ABI of libhiccup_hip.so, the MI355X (gfx950) implementation
+ * of hiccup's 8x8 block DCT -> quantize -> zig-zag -> DC-DPCM / AC-RLE encode
+ * path and its inverse.
+ *
+ * The reference (nhomble/hiccup) is pure Python and has no FFI: its drop-in
+ * boundary is the Python function surface listed below.  Each entry point here
+ * is what that surface binds (through ctypes, see hiccup_amd/_lib.py and
+ * INTEGRATION.md); the comment on each cites the reference function it
+ * replaces (/root/reference/<file>:<line>).
+ *
+ * Conventions (all entry points):
+ *   - plain pointers and sizes; no Python / torch types cross the ABI;
+ *   - every array pointer is a DEVICE pointer (hipMalloc / torch CUDA tensor)
+ *     unless the parameter name starts with h_;
+ *   - caller-allocated outputs; the library never allocates on the hot path;
+ *   - `stream` is a hipStream_t passed as void* (NULL = legacy default stream);
+ *     calls are asynchronous on that stream and may be captured in a hipGraph;
+ *   - return value: HIC_OK (0) or a negative HIC_ERR_*; hic_last_error() gives
+ *     the message of the last failure on the calling thread.  Nothing throws.
+ */
+#ifndef HICCUP_HIP_H
+#define HICCUP_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HIC_ABI_VERSION 1
+
+#define HIC_OK 0
+#define HIC_ERR_ARG (-1)      /* bad shape / pointer / enum: the reference asserts or raises */
+#define HIC_ERR_HIP (-2)      /* HIP runtime failure (launch, memcpy) */
+#define HIC_ERR_CAPACITY (-3) /* caller's output buffer too small */
+
+/* model.QTables (model.py:25-27) -> quantization.table (quantization.py:14-37) */
+#define HIC_TABLE_LUMINANCE 0
+#define HIC_TABLE_CHROMINANCE 1
+
+/* Coefficient layouts in HBM.
+ * RASTER_I32: the reference's "coefficient image" (transform.dct_channel output,
+ *             transform.py:182-193): int32 H x W, block (i,j) coef (u,v) at [8i+u][8j+v].
+ * RASTER_I16: same, int16 (lossless: |q| <= 3277).
+ * ZIGZAG_I16: block-major stream: for every 8x8 block in raster block order
+ *             (padded blocks included), 64 int16 in transposed zig-zag order
+ *             (transform.zigzag, transform.py:106-135); coefficients whose
+ *             position falls outside H x W are 0 (jpeg_encode re-splits the
+ *             cropped coefficient image with zero padding, codec.py:287-294). */
+#define HIC_LAYOUT_RASTER_I32 0
+#define HIC_LAYOUT_RASTER_I16 1
+#define HIC_LAYOUT_ZIGZAG_I16 2
+
+int hic_abi_version(void);
+/* Copies the last error message of this thread into buf (NUL-terminated). */
+int hic_last_error(char *h_buf, size_t n);
+/* Number of visible HIP devices. */
+int hic_device_count(int *h_n);
+/* Synchronises `stream`; returns HIC_ERR_HIP if an earlier async launch failed. */
+int hic_stream_sync(void *stream);
+
+/* ---- forward transform: replaces transform.dct_channel (transform.py:182-193) =
+ *      offset -128 (:186), split_matrix/pad (:33-42), dct2 (:67-84, scipy pocketfft
+ *      DCT-II bit-exact), jpeg_quantize (quantization.py:47-52,80-81:
+ *      round-half-even(b / T)), merge_blocks/crop (:45-64).
+ *  plane: uint8 H x W with row pitch `stride` bytes.  out: per `layout`. */
+int hic_dct_quant_u8(const uint8_t *plane, int64_t H, int64_t W, int64_t stride, int table_id,
+                     int layout, void *out, void *stream);
+
+/* ---- inverse transform: replaces transform.inv_dct_channel (transform.py:169-179) =
+ *      split (:174), invert_jpeg_quantize q*T (quantization.py:55-57), idct2
+ *      (:87-103, pocketfft DCT-III bit-exact, /256), merge/crop, +128,
+ *      astype(uint8) (truncate toward zero, wrap mod 256).
+ *  coef: per `layout` (H x W coefficient image, or the zig-zag block stream of it).
+ *  out : uint8 H x W with row pitch out_stride. */
+int hic_dequant_idct_u8(const void *coef, int layout, int64_t H, int64_t W, int table_id,
+                        uint8_t *out, int64_t out_stride, void *stream);
+
+/* ---- block-level helpers on batches of 8x8 blocks (float64 bit-exact):
+ *  hic_dct2_f64  = transform.dct2  (transform.py:67-84)  in[nblk][8][8] -> out
+ *  hic_idct2_f64 = transform.idct2 (transform.py:87-103, includes /256)
+ *  hic_quantize_f64   = quantization.jpeg_quantize (quantization.py:47-52,80-81) -> int32
+ *  hic_dequantize_i32 = quantization.invert_jpeg_quantize (quantization.py:55-57) -> int64 */
+int hic_dct2_f64(const double *in, int64_t nblk, double *out, void *stream);
+int hic_idct2_f64(const double *in, int64_t nblk, double *out, void *stream);
+int hic_quantize_f64(const double *in, int64_t nblk, int table_id, int32_t *out, void *stream);
+int hic_dequantize_i32(const int32_t *in, int64_t nblk, int table_id, int64_t *out, void *stream);
+
+/* ---- colour + chroma resampling (compression.py:21,56; transform.py:151-166).
+ *      OpenCV 8U semantics restated (parity UNPINNED: cv2 absent).
+ *  hic_rgb_to_ycrcb420: rgb H x W x 3 (pitch W*3) -> y H x W, cr/cb (H/2) x (W/2)
+ *      = cvtColor(RGB2YCrCb) then pyrDown(dstsize=(W/2,H/2)) on Cr and Cb. */
+int hic_rgb_to_ycrcb420(const uint8_t *rgb, int64_t H, int64_t W, uint8_t *y, uint8_t *cr,
+                        uint8_t *cb, void *stream);
+/* cv2.cvtColor(RGB2YCrCb), full resolution, no resampling. */
+int hic_rgb_to_ycrcb(const uint8_t *rgb, int64_t H, int64_t W, uint8_t *y, uint8_t *cr,
+                     uint8_t *cb, void *stream);
+/* transform.down_sample = cv2.pyrDown(src, dstsize=(DW, DH)) */
+int hic_pyr_down_u8(const uint8_t *src, int64_t H, int64_t W, uint8_t *dst, int64_t DH,
+                    int64_t DW, void *stream);
+/* transform.up_sample = cv2.pyrUp(src, dstsize=(DW, DH)) */
+int hic_pyr_up_u8(const uint8_t *src, int64_t H, int64_t W, uint8_t *dst, int64_t DH,
+                  int64_t DW, void *stream);
+/* compression.jpeg_decompression tail (compression.py:47-56): pyrUp cr/cb (h x w) to
+ * 2h x 2w, crop y (row pitch y_stride) to that (transform.force_merge,
+ * transform.py:269-277), cvtColor(YCrCb2RGB) -> rgb (2h) x (2w) x 3. */
+int hic_ycrcb420_to_rgb(const uint8_t *y, int64_t y_stride, const uint8_t *cr, const uint8_t *cb,
+                        int64_t h, int64_t w, uint8_t *rgb, void *stream);
+
+/* ---- generic block split + zig-zag for any block size N (codec.jpeg_encode with
+ *      settings.JPEG_BLOCK_SIZE != 8, codec.py:287-294; transform.zigzag):
+ *      raster int32 H x W -> out[nblk][N*N] int32, zero padding.  And its inverse
+ *      (izigzag + merge_blocks + crop, codec.py:415-425). */
+int hic_zigzag_blocks_i32(const int32_t *raster, int64_t H, int64_t W, int N, int32_t *out,
+                          void *stream);
+int hic_izigzag_blocks_i32(const int32_t *blocks, int64_t H, int64_t W, int N, int32_t *raster,
+                           void *stream);
+
+/* ---- entropy front end: DC DPCM (codec.differential_coding, codec.py:47-52) and
+ *      global AC run-length coding (codec.run_length_coding, codec.py:55-99) over
+ *      the AC stream of `nblk` blocks of `block_len` coefficients (AC = slots
+ *      1..block_len-1 of every block, blocks in order).
+ *  Symbols are written SoA: sym_len[i] zeros followed by sym_val[i]; a trailing
+ *  zero run becomes the single EOB (0,0); runs >= max_len are split into
+ *  (max_len-1, 0) fillers (max_len 0 = no split, reference max_len=None).
+ *  *d_count (device int64) receives the symbol count, or -(needed) if sym_cap was
+ *  too small (nothing past sym_cap is written).
+ *  Sharded use (tile-sharded image, one stream across ranks): d_stitch (device,
+ *  int64[4] = {carry_zeros, emit_eob, has_prev_dc, prev_dc}) or NULL for a whole
+ *  stream {0, 1, 0, 0}.  hic_rle_shard_summary fills d_summary (device int64[4]
+ *  = {trailing_zeros, has_nonzero, first_dc, last_dc}) for the exchange step. */
+size_t hic_rle_workspace_bytes(int64_t nblk, int block_len);
+int hic_rle_shard_summary_i16(const int16_t *blocks, int64_t nblk, int block_len,
+                              void *workspace, int64_t *d_summary, void *stream);
+int hic_rle_encode_i16(const int16_t *blocks, int64_t nblk, int block_len, int max_len,
+                       const int64_t *d_stitch, int32_t *dc_diff, uint8_t *sym_len,
+                       int16_t *sym_val, int64_t sym_cap, int64_t *d_count, void *workspace,
+                       void *stream);
+int hic_rle_shard_summary_i32(const int32_t *blocks, int64_t nblk, int block_len,
+                              void *workspace, int64_t *d_summary, void *stream);
+int hic_rle_encode_i32(const int32_t *blocks, int64_t nblk, int block_len, int max_len,
+                       const int64_t *d_stitch, int32_t *dc_diff, int32_t *sym_len,
+                       int32_t *sym_val, int64_t sym_cap, int64_t *d_count, void *workspace,
+                       void *stream);
+/* codec.run_length_coding (codec.py:55-99) on an arbitrary 1-D int32 array of n
+ * elements (n = 0 gives the single EOB).  Same symbol / count conventions. */
+int hic_rle_stream_encode_i32(const int32_t *arr, int64_t n, int max_len, int32_t *sym_len,
+                              int32_t *sym_val, int64_t sym_cap, int64_t *d_count, void *workspace,
+                              void *stream);
+/* Computes this rank's d_stitch from all ranks' summaries (device int64[world][4],
+ * e.g. after an all-gather): carry = trailing zeros of the preceding ranks back to
+ * the last one holding a nonzero; EOB only on the last rank; prev_dc = last DC of
+ * rank-1. */
+int hic_rle_stitch(const int64_t *d_all_summaries, int world, int rank, int64_t *d_stitch,
+                   void *stream);
+
+/* ---- entropy front end, inverse: codec.decode_run_length (codec.py:102-113) +
+ *      utils.group_tuples (:412) + utils.invert_differences (utils.py:66-73) +
+ *      [dc, *ac] reassembly (codec.py:415-421) -> zig-zag blocks (nblk x block_len).
+ *  *d_status (device int64) receives the decoded AC length (EOB zero-fill
+ *  included); the reference asserts unless it equals nblk*(block_len-1). */
+size_t hic_rld_workspace_bytes(int64_t nsym, int64_t nblk);
+int hic_rle_decode_i16(const uint8_t *sym_len, const int16_t *sym_val, int64_t nsym,
+                       const int32_t *dc_diff, int64_t nblk, int block_len, int16_t *blocks,
+                       int64_t *d_status, void *workspace, void *stream);
+int hic_rle_decode_i32(const int32_t *sym_len, const int32_t *sym_val, int64_t nsym,
+                       const int32_t *dc_diff, int64_t nblk, int block_len, int32_t *blocks,
+                       int64_t *d_status, void *workspace, void *stream);
+/* codec.decode_run_length on a bare symbol list: out (room for out_cap int32,
+ * out_cap a multiple of 64 and >= max(length, sum(len+1))) receives the decoded
+ * list; *d_status its length (EOB zero-fill to `length` included).
+ * workspace >= hic_rld_workspace_bytes(nsym, out_cap / 64). */
+int hic_rle_stream_decode_i32(const int32_t *sym_len, const int32_t *sym_val, int64_t nsym,
+                              int64_t length, int32_t *out, int64_t out_cap, int64_t *d_status,
+                              void *workspace, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HICCUP_HIP_H */

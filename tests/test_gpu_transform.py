@@ -1,0 +1,134 @@
+"""GPU parity: forward / inverse 8x8 DCT kernels vs the reference's outputs.
+
+Small cases are compared with the golden fixtures the reference itself produced
+(tests/golden/make_golden.py); full 4K / 8K planes are compared bit-exactly with
+the C oracle (oracle/hiccup_oracle.c, pinned against the same fixtures).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+import oracle.oracle as orc  # noqa: E402
+import oracle.oracle_c as orcc  # noqa: E402
+from hiccup_amd import _lib, device, model, quantization, transform  # noqa: E402
+
+QT = {0: model.QTables.JPEG_LUMINANCE, 1: model.QTables.JPEG_CHROMINANCE}
+
+
+def _names(d, prefix):
+    return sorted(k[len(prefix):] for k in d if k.startswith(prefix))
+
+
+def test_dct_channel_golden(golden_transform):
+    g = golden_transform
+    for name in _names(g, "in_"):
+        tab = int(g["tab_" + name])
+        q = transform.dct_channel(g["in_" + name], QT[tab])
+        assert q.dtype == np.int32
+        np.testing.assert_array_equal(q, g["q_" + name], err_msg=name)
+
+
+def test_inv_dct_channel_golden(golden_transform):
+    g = golden_transform
+    for name in _names(g, "in_"):
+        tab = int(g["tab_" + name])
+        rec = transform.inv_dct_channel(g["q_" + name], QT[tab])
+        assert rec.dtype == np.uint8
+        np.testing.assert_array_equal(rec, g["rec_" + name], err_msg=name)
+    for name in _names(g, "icin_"):
+        tab = int(g["ictab_" + name])
+        np.testing.assert_array_equal(transform.inv_dct_channel(g["icin_" + name], QT[tab]),
+                                      g["icout_" + name], err_msg=name)
+
+
+def test_inv_dct_float_planes(golden_transform):
+    """jpeg_decode hands float64 (integer-valued) planes to inv_dct_channel."""
+    g = golden_transform
+    q = g["q_r256_lum"].astype(np.float64)
+    np.testing.assert_array_equal(transform.inv_dct_channel(q, QT[0]), g["rec_r256_lum"])
+
+
+def test_dct2_idct2_bits(golden_transform):
+    g = golden_transform
+    out = transform.dct2(g["dct2_in"])
+    assert np.array_equal(out.view(np.int64), g["dct2_out"].view(np.int64))
+    back = transform.idct2(g["dct2_out"])
+    assert np.array_equal(back.view(np.int64), g["idct2_out"].view(np.int64))
+
+
+def test_quantize_helpers(golden_transform):
+    # quantizationtest.py:12-25
+    mat = np.ones((8, 8))
+    mat[0, 0] = 16
+    q = quantization.jpeg_quantize(mat, model.QTables.JPEG_LUMINANCE)
+    assert q[0][0] == 1 and np.sum(q) == 1
+    g = golden_transform
+    b = g["dct2_out"]
+    for tab in (0, 1):
+        exp = np.round(b / orc.TABLES[tab]).astype(np.int32)
+        np.testing.assert_array_equal(quantization.jpeg_quantize(b, QT[tab]), exp)
+        np.testing.assert_array_equal(quantization.invert_jpeg_quantize(exp, QT[tab]), exp * orc.TABLES[tab])
+
+
+def test_constant_images():
+    # transformtest.py:148-161
+    assert np.sum(transform.dct_channel(np.full((120, 80), 128, np.uint8), model.QTables.JPEG_CHROMINANCE)) == 0
+    assert np.abs(np.sum(transform.dct_channel(np.ones((120, 80), np.uint8), model.QTables.JPEG_LUMINANCE))) > 0
+    assert np.sum(transform.dct_channel(np.zeros((120, 80), np.uint8), model.QTables.JPEG_LUMINANCE)) < 1e-10
+
+
+@pytest.mark.parametrize("layout", [_lib.LAYOUT_RASTER_I32, _lib.LAYOUT_RASTER_I16, _lib.LAYOUT_ZIGZAG_I16])
+@pytest.mark.parametrize("shape", [(64, 64), (37, 53), (8, 200), (130, 7)])
+def test_layouts_roundtrip(layout, shape):
+    rng = np.random.default_rng(sum(shape) + layout)
+    plane = rng.integers(0, 256, shape, dtype=np.uint8)
+    for tab in (0, 1):
+        exp = orcc.dct_channel(plane, tab)
+        coef = transform.dct_channel_device(device.to_device(plane), tab, layout)
+        got = device.to_host(coef)
+        if layout == _lib.LAYOUT_ZIGZAG_I16:
+            np.testing.assert_array_equal(got.astype(np.int32), orcc.zigzag_blocks(exp, 8))
+        else:
+            np.testing.assert_array_equal(got.astype(np.int32), exp)
+        rec = transform.inv_dct_channel_device(coef, shape[0], shape[1], tab, layout)
+        np.testing.assert_array_equal(device.to_host(rec), orcc.inv_dct_channel(exp, tab))
+
+
+@pytest.mark.parametrize("H,W", [(4096, 4096), (4320, 7680)])
+def test_full_size_bit_exact(H, W):
+    """BASELINE configs 2/3 plane sizes, bit-exact against the C oracle (multi-threaded)."""
+    rng = np.random.default_rng(2)
+    plane = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    exp = orcc.dct_channel(plane, 0, threads=16)
+    coef = transform.dct_channel_device(device.to_device(plane), 0, _lib.LAYOUT_ZIGZAG_I16)
+    zz = device.to_host(coef)
+    raster = orc.merge_blocks(zz[:, np.argsort(orc.ZZ8)].reshape(-1, 8, 8), (H, W))
+    np.testing.assert_array_equal(raster.astype(np.int32), exp)
+    # inverse: a size-independent property -- dequant+IDCT of the GPU coefficients
+    rec = device.to_host(transform.inv_dct_channel_device(coef, H, W, 0, _lib.LAYOUT_ZIGZAG_I16))
+    np.testing.assert_array_equal(rec[:1024], orcc.inv_dct_channel(exp[:1024], 0))
+    # reconstruction quality is what a JPEG-style lum table gives on noise
+    assert np.mean(np.abs(rec.astype(np.int32) - plane.astype(np.int32))) < 40
+
+
+def test_tie_blocks_many():
+    """Exact .5 quotients at DC / (4,4) on 100k random blocks (25% / ~3% of blocks)."""
+    rng = np.random.default_rng(11)
+    plane = rng.integers(0, 256, (8 * 250, 8 * 400), dtype=np.uint8)
+    for tab in (0, 1):
+        np.testing.assert_array_equal(transform.dct_channel(plane, QT[tab]), orcc.dct_channel(plane, tab, threads=8))
+
+
+def test_bad_args():
+    with pytest.raises(ValueError):
+        transform.dct_channel(np.zeros((8, 8), np.uint8), model.QTables.JPEG_LUMINANCE, block_size=4)
+    with pytest.raises(ValueError):
+        transform.dct_channel(np.zeros((8, 8, 3), np.uint8), model.QTables.JPEG_LUMINANCE)
+    dev = device.to_device(np.zeros((8, 8), np.uint8))
+    out = device.empty((8, 8), torch.int32)
+    with pytest.raises(ValueError):
+        _lib.call("hic_dct_quant_u8", device.ptr(dev), 8, 8, 8, 7, 0, device.ptr(out), device.stream_ptr())
+    with pytest.raises(ValueError):
+        _lib.call("hic_dct_quant_u8", device.ptr(dev), 8, 8, 8, 0, 9, device.ptr(out), device.stream_ptr())

@@ -41,6 +41,7 @@ SIGNATURES = {
     "hic_quantize_f64": (_int, [_vp, _i64, _int, _vp, _vp]),
     "hic_dequantize_i32": (_int, [_vp, _i64, _int, _vp, _vp]),
     "hic_rgb_to_ycrcb420": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp]),
+    "hic_rgb_to_ycrcb420_rows": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),
     "hic_rgb_to_ycrcb": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp]),
     "hic_pyr_down_u8": (_int, [_vp, _i64, _i64, _vp, _i64, _i64, _vp]),
     "hic_pyr_up_u8": (_int, [_vp, _i64, _i64, _vp, _i64, _i64, _vp]),
@@ -52,7 +53,7 @@ SIGNATURES = {
     "hic_rle_shard_summary_i32": (_int, [_vp, _i64, _int, _vp, _vp, _vp]),
     "hic_rle_encode_i16": (_int, [_vp, _i64, _int, _int, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
     "hic_rle_encode_i32": (_int, [_vp, _i64, _int, _int, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
-    "hic_rle_stitch": (_int, [_vp, _int, _int, _vp, _vp]),
+    "hic_rle_stitch": (_int, [_vp, _int, _int, _int, _vp, _vp]),
     "hic_rle_stream_encode_i32": (_int, [_vp, _i64, _int, _vp, _vp, _i64, _vp, _vp, _vp]),
     "hic_rle_stream_decode_i32": (_int, [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _vp]),
     "hic_rld_workspace_bytes": (_sz, [_i64, _i64]),

@@ -1,0 +1,267 @@
+"""Entropy coding front end (mirrors hiccup/codec.py:23-426), JPEG flavour.
+
+GPU (libhiccup_hip.so):
+* ``run_length_coding``  -> hic_rle_stream_encode_i32 (codec.py:55-99)
+* ``decode_run_length``  -> hic_rle_stream_decode_i32 (codec.py:102-113)
+* ``jpeg_encode``: per channel, split + zig-zag (hic_zigzag_blocks_i32), DC DPCM
+  and the channel-wide AC RLE (hic_rle_encode_i32) -- codec.py:286-301
+* ``jpeg_decode``: AC RLE decode + group into blocks + DC integration
+  (hic_rle_decode_i32) and izigzag + merge + crop (hic_izigzag_blocks_i32) --
+  codec.py:397-425
+Host ("next" row): the Huffman stage and payload assembly
+(codec.py:242-272,304-334,354-394), byte-compatible with the reference.
+
+Deliberate deviation: jpeg_decode does not print the luminance AC list to
+stdout (the reference's debugging print at codec.py:406-408).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib, device, hicimage as hic, huffman, model, settings, utils
+
+MAX_LEN = 0xF
+_OUT_OF_SCOPE = "the wavelet (HIC) scheme is out of scope (DESIGN.md)"
+
+
+class RunLength:
+    """(zeros-before, value) symbol (codec.py:23-44)."""
+
+    @classmethod
+    def from_dict(cls, d):
+        return cls(d["value"], d["zeros"])
+
+    def __init__(self, value=0, length=0):
+        self.value = value
+        self.length = length
+
+    def __eq__(self, other):
+        return type(self) == type(other) and self.value == other.value and self.length == other.length
+
+    def __str__(self):
+        return "(%d, %d)" % (self.length, self.value)
+
+    __repr__ = __str__
+
+    @property
+    def segment(self):
+        return [0] * self.length + [self.value]
+
+    @property
+    def is_trailing(self):
+        return self.value == 0 and self.length == 0
+
+
+def _i32(a, what):
+    a = np.asarray(a)
+    if a.size and not np.issubdtype(a.dtype, np.integer):
+        if not np.all(np.mod(a, 1) == 0):
+            raise ValueError("%s must be integer-valued" % what)
+    a = a.astype(np.int64)
+    if a.size and (a.min() < -(1 << 31) or a.max() >= (1 << 31)):
+        raise ValueError("%s out of int32 range" % what)
+    return a.astype(np.int32)
+
+
+def differential_coding(blocks):
+    """codec.py:47-52: [dc0, dc1 - dc0, ...] over the blocks' [0][0] entries."""
+    return utils.differences([b[0][0] for b in blocks])
+
+
+# ------------------------------------------------------------------ RLE on GPU
+def rle_encode_device(arr_dev, n, max_len=MAX_LEN, stream=None):
+    """run_length_coding of a device int32 array -> (lengths, values, count) device tensors."""
+    cap = n + 1  # each element yields at most one symbol, plus the EOB
+    L = device.empty((cap,), torch.int32)
+    V = device.empty((cap,), torch.int32)
+    cnt = device.empty((1,), torch.int64)
+    lib = _lib.load()
+    ws = device.workspace(lib.hic_rle_workspace_bytes(max(1, -(-n // 64)), 64))
+    src = device.ptr(arr_dev) if n > 0 else ctypes.c_void_p(0)
+    _lib.call("hic_rle_stream_encode_i32", src, n, max_len, device.ptr(L), device.ptr(V), cap, device.ptr(cnt),
+              device.ptr(ws), device.stream_ptr(stream))
+    return L, V, cnt
+
+
+def run_length_coding(arr, max_len=MAX_LEN):
+    """codec.py:55-99 -> list of RunLength."""
+    if max_len is not None:
+        if max_len == 0:
+            raise ZeroDivisionError("integer division or modulo by zero")
+        if max_len < 0:
+            raise ValueError("max_len must be positive")
+    a = _i32(np.asarray(arr).reshape(-1), "run_length_coding input")
+    utils.debug_msg("Going to determine RLE for %d size array" % len(a))
+    n = len(a)
+    dev = device.to_device(a) if n else device.empty((1,), torch.int32)
+    L, V, cnt = rle_encode_device(dev, n, max_len or 0)
+    count = int(device.to_host(cnt)[0])
+    assert count > 0
+    Lh = L[:count].cpu().numpy()
+    Vh = V[:count].cpu().numpy()
+    return [RunLength(int(v), int(l)) for l, v in zip(Lh, Vh)]
+
+
+def decode_run_length(rles, length):
+    """codec.py:102-113 -> list of ints (EOB zero-fills up to `length`)."""
+    if len(rles) == 0:
+        # the reference flattens an empty list with functools.reduce
+        raise TypeError("reduce() of empty iterable with no initial value")
+    Lh = _i32([r.length for r in rles], "run lengths")
+    Vh = _i32([r.value for r in rles], "run values")
+    total = int(np.sum(Lh.astype(np.int64) + 1))
+    cap = -(-max(total, int(length), 1) // 64) * 64
+    out = device.empty((cap,), torch.int32)
+    status = device.empty((1,), torch.int64)
+    lib = _lib.load()
+    ws = device.workspace(lib.hic_rld_workspace_bytes(len(Lh), cap // 64))
+    Ld, Vd = device.to_device(Lh), device.to_device(Vh)
+    _lib.call("hic_rle_stream_decode_i32", device.ptr(Ld), device.ptr(Vd), len(Lh), int(length), device.ptr(out),
+              cap, device.ptr(status), device.ptr(ws), device.stream_ptr())
+    n = int(device.to_host(status)[0])
+    return out[:n].cpu().numpy().tolist()
+
+
+# ------------------------------------------------------------------ jpeg_encode
+def encode_channel_device(raster_dev, H, W, bs, stream=None):
+    """Front half of jpeg_encode for one int32 coefficient plane on the device:
+    split + zig-zag (block size bs), DC DPCM, AC RLE.  Returns device tensors
+    (dc_diff int32[nblk], lengths int32, values int32, count int64[1])."""
+    nbx, nby = -(-W // bs), -(-H // bs)
+    nblk, L = nbx * nby, bs * bs
+    blocks = device.empty((nblk, L), torch.int32)
+    _lib.call("hic_zigzag_blocks_i32", device.ptr(raster_dev), H, W, bs, device.ptr(blocks),
+              device.stream_ptr(stream))
+    if L == 1:
+        # no AC coefficients: the AC stream is empty -> [EOB]
+        dc = blocks.view(-1).clone()
+        dc[1:] = blocks.view(-1)[1:] - blocks.view(-1)[:-1]
+        Ls, Vs, cnt = rle_encode_device(dc, 0, MAX_LEN, stream)
+        return dc, Ls, Vs, cnt
+    cap = nblk * (L - 1) + 1
+    dc = device.empty((nblk,), torch.int32)
+    Ls = device.empty((cap,), torch.int32)
+    Vs = device.empty((cap,), torch.int32)
+    cnt = device.empty((1,), torch.int64)
+    ws = device.workspace(_lib.load().hic_rle_workspace_bytes(nblk, L))
+    _lib.call("hic_rle_encode_i32", device.ptr(blocks), nblk, L, MAX_LEN, ctypes.c_void_p(0), device.ptr(dc),
+              device.ptr(Ls), device.ptr(Vs), cap, device.ptr(cnt), device.ptr(ws), device.stream_ptr(stream))
+    return dc, Ls, Vs, cnt
+
+
+def encode_channel(plane, bs=None):
+    """(dc_diffs, ac_lengths, ac_values) numpy arrays for one coefficient plane."""
+    bs = settings.JPEG_BLOCK_SIZE if bs is None else bs
+    p = _i32(plane, "coefficient plane")
+    if p.ndim != 2:
+        raise ValueError("expected a 2-D coefficient plane")
+    H, W = p.shape
+    dc, Ls, Vs, cnt = encode_channel_device(device.to_device(p), H, W, bs)
+    count = int(device.to_host(cnt)[0])
+    return dc.cpu().numpy(), Ls[:count].cpu().numpy(), Vs[:count].cpu().numpy()
+
+
+def _huff_from_keys(keys):
+    uniq, counts = huffman.first_appearance_counts(keys)
+    return huffman.HuffmanTree.construct_from_counts(uniq, counts)
+
+
+def huffman_encode(huff):
+    return hic.PayloadStringP(hic.TupP, [hic.TupP(v, c) for v, c in huff.encode_table()])
+
+
+def huffman_decode(data):
+    return huffman.HuffmanTree.construct_from_coding([p.numbers for p in data.payloads])
+
+
+def huffman_data_encode(huff):
+    return hic.BitStringP(huff.encode_data())
+
+
+def huffman_data_decode(data, tree):
+    return tree.decode_data(data.payload)
+
+
+def jpeg_encode(compressed):
+    """codec.py:275-334: CompressedImage -> HicImage (9 tables, 9 bit strings, 2 shapes)."""
+    utils.debug_msg("Starting JPEG encoding")
+    bs = settings.JPEG_BLOCK_SIZE
+    streams = utils.dict_map(compressed.as_dict, lambda k, v: encode_channel(v, bs))
+    trees = {}
+    for k, (dc, L, V) in streams.items():
+        trees[k] = (_huff_from_keys(dc), _huff_from_keys(V), _huff_from_keys(L))
+    chans = ("lum", "cr", "cb")
+    tables = [huffman_encode(trees[k][j]) for j in range(3) for k in chans]
+    keysets = {0: 0, 1: 2, 2: 1}  # tree j encodes stream keysets[j] (dc, values, lengths)
+    data = [hic.BitStringP(trees[k][j].encode_keys(streams[k][keysets[j]])) for j in range(3) for k in chans]
+    shape = compressed.shape
+    payloads = tables + data + [hic.TupP(shape[0][0], shape[0][1]), hic.TupP(shape[1][0], shape[1][1])]
+    return hic.HicImage.jpeg_image(payloads)
+
+
+def jpeg_decode(hic_image):
+    """codec.py:337-426: HicImage -> CompressedImage (float64 planes)."""
+    utils.debug_msg("JPEG decode")
+    assert hic_image.hic_type == model.Compression.JPEG
+    p = hic_image.payloads
+    chans = ("lum", "cr", "cb")
+    shapes = {"lum": p[18].numbers, "cr": p[19].numbers, "cb": p[19].numbers}
+    bs = settings.JPEG_BLOCK_SIZE
+    sub_length = bs * bs - 1
+    out = {}
+    for c, k in enumerate(chans):
+        dc = huffman_data_decode(p[9 + c], huffman_decode(p[c]))
+        vals = huffman_data_decode(p[12 + c], huffman_decode(p[3 + c]))
+        lens = huffman_data_decode(p[15 + c], huffman_decode(p[6 + c]))
+        n = min(len(vals), len(lens))  # zip() in codec.py:399-400
+        vals, lens = vals[:n], lens[:n]
+        # the reference's assertions (utils.group_tuples, codec.py:418), evaluated up front
+        total = int(np.sum(np.asarray(lens, dtype=np.int64) + 1))
+        eob = n > 0 and lens[-1] == 0 and vals[-1] == 0
+        ac_length = utils.size(shapes[k]) - len(dc)
+        decoded = max(total, ac_length) if eob else total
+        if n == 0:
+            raise TypeError("reduce() of empty iterable with no initial value")
+        if sub_length == 0:
+            raise ZeroDivisionError("integer division or modulo by zero")
+        assert decoded % sub_length == 0
+        assert decoded // sub_length == len(dc)
+        out[k] = _decode_channel(dc, lens, vals, shapes[k], bs)
+    return model.CompressedImage.from_dict(out)
+
+
+def _decode_channel(dc, lens, vals, shape, bs):
+    nblk, L = len(dc), bs * bs
+    H, W = int(shape[0]), int(shape[1])
+    blocks = device.empty((nblk, L), torch.int32)
+    status = device.empty((1,), torch.int64)
+    Ld, Vd, Dd = device.to_device(_i32(lens, "lengths")), device.to_device(_i32(vals, "values")), \
+        device.to_device(_i32(dc, "dc"))
+    ws = device.workspace(_lib.load().hic_rld_workspace_bytes(len(lens), nblk))
+    _lib.call("hic_rle_decode_i32", device.ptr(Ld), device.ptr(Vd), len(lens), device.ptr(Dd), nblk, L,
+              device.ptr(blocks), device.ptr(status), device.ptr(ws), device.stream_ptr())
+    raster = device.zeros((H, W), torch.int32)
+    _lib.call("hic_izigzag_blocks_i32", device.ptr(blocks), H, W, bs, device.ptr(raster), device.stream_ptr())
+    return device.to_host(raster).astype(np.float64)
+
+
+# ------------------------------------------------------------------ out of scope
+def wavelet_encode(compressed):
+    raise NotImplementedError(_OUT_OF_SCOPE)
+
+
+def wavelet_decode(hic_image):
+    raise NotImplementedError(_OUT_OF_SCOPE)
+
+
+def wavelet_decode_pull_subbands(data, shapes):
+    raise NotImplementedError(_OUT_OF_SCOPE)
+
+
+def wavelet_decoded_subbands_shapes(min_shape, max_shape):
+    raise NotImplementedError(_OUT_OF_SCOPE)
+
+
+def wavelet_decoded_length(min_shape, max_shape):
+    raise NotImplementedError(_OUT_OF_SCOPE)

@@ -42,17 +42,27 @@ constexpr int TX = 32, TY = 16;
 constexpr int RW = 2 * TX + 8;  // region columns [2*ox0 - 4, 2*ox0 + 2*TX + 4): 4-pixel aligned
 constexpr int RH = 2 * TY + 4;  // region rows    [2*oy0 - 2, 2*oy0 + 2*TY + 2)
 
-__global__ __launch_bounds__(256) void k_rgb_ycrcb420(const uint8_t *__restrict__ rgb, int H, int W,
-                                                      uint8_t *__restrict__ Y, uint8_t *__restrict__ Cr,
-                                                      uint8_t *__restrict__ Cb, int dh, int dw) {
+// Row-shard form: the input holds image rows [in_row0, in_row0 + in_rows) of an
+// H x W image (a shard plus its 2-row pyrDown halo); the kernel writes Y rows
+// [out_row0, out_row0 + out_rows) (to y, relative to out_row0) and chroma rows
+// [out_row0/2, out_row0/2 + dh_out) (relative).  Reflect-101 happens only at the
+// true image border, so a shard's output equals the same rows of the whole image.
+__global__ __launch_bounds__(256) void k_rgb_ycrcb420(const uint8_t *__restrict__ rgb, int in_row0, int in_rows, int H, int W,
+                                                      int out_row0, int out_rows, uint8_t *__restrict__ Y,
+                                                      uint8_t *__restrict__ Cr, uint8_t *__restrict__ Cb, int dh_out,
+                                                      int dw) {
   __shared__ uint8_t s_c[2][RH][RW];
   __shared__ int s_h[2][RH][TX];
-  const int ox0 = blockIdx.x * TX, oy0 = blockIdx.y * TY;
+  const int ox0 = blockIdx.x * TX, oyl0 = blockIdx.y * TY;  // chroma tile origin (shard-relative row)
+  const int oy0 = out_row0 / 2 + oyl0;                       // global chroma row
   const int gxs = 2 * ox0 - 4, gys = 2 * oy0 - 2;
-  // pixels whose Y this tile writes (the last tile row/column also owns odd leftovers)
+  // Y pixels this tile writes: its 2x chroma footprint; the last tile row / column
+  // of the shard also owns the odd leftover row / column of the image
   const int cx0 = 2 * ox0, cx1 = (ox0 + TX >= dw) ? W : 2 * (ox0 + TX);
-  const int cy0 = 2 * oy0, cy1 = (oy0 + TY >= dh) ? H : 2 * (oy0 + TY);
-  const bool interior = gxs >= 0 && gys >= 0 && gxs + RW <= W && gys + RH <= H && (W % 4) == 0;
+  const int cy0 = 2 * oy0;
+  const int cy1 = (oyl0 + TY >= dh_out) ? out_row0 + out_rows : 2 * (oy0 + TY);
+  const int in_row1 = in_row0 + in_rows;
+  const bool interior = gxs >= 0 && gys >= in_row0 && gxs + RW <= W && gys + RH <= in_row1 && (W % 4) == 0;
 
   if (interior) {
     // 4 pixels (3 dwords) per lane per step: 18 quads x 36 rows
@@ -60,7 +70,7 @@ __global__ __launch_bounds__(256) void k_rgb_ycrcb420(const uint8_t *__restrict_
     for (int i = threadIdx.x; i < RH * QW; i += 256) {
       const int ry = i / QW, qx = i - ry * QW;
       const int gy = gys + ry, gx = gxs + 4 * qx;
-      const uint32_t *p = reinterpret_cast<const uint32_t *>(rgb + ((int64_t)gy * W + gx) * 3);
+      const uint32_t *p = reinterpret_cast<const uint32_t *>(rgb + ((int64_t)(gy - in_row0) * W + gx) * 3);
       const uint32_t w0 = p[0], w1 = p[1], w2 = p[2];
       const int px[12] = {(int)(w0 & 255), (int)((w0 >> 8) & 255), (int)((w0 >> 16) & 255), (int)(w0 >> 24),
                           (int)(w1 & 255), (int)((w1 >> 8) & 255), (int)((w1 >> 16) & 255), (int)(w1 >> 24),
@@ -74,18 +84,21 @@ __global__ __launch_bounds__(256) void k_rgb_ycrcb420(const uint8_t *__restrict_
         s_c[1][ry][4 * qx + k] = (uint8_t)c.cb;
       }
       if (gy >= cy0 && gy < cy1 && gx >= cx0 && gx + 4 <= cx1)
-        *reinterpret_cast<uint32_t *>(Y + (int64_t)gy * W + gx) = yq;
+        *reinterpret_cast<uint32_t *>(Y + (int64_t)(gy - out_row0) * W + gx) = yq;
     }
   } else {
     for (int i = threadIdx.x; i < RH * RW; i += 256) {
       const int ry = i / RW, rx = i - ry * RW;
       const int gy = gys + ry, gx = gxs + rx;
-      const int sy = refl101(gy, H), sx = refl101(gx, W);
-      const uint8_t *p = rgb + ((int64_t)sy * W + sx) * 3;
+      int sy = refl101(gy, H);
+      // rows outside the provided span only feed chroma rows past the shard (discarded)
+      sy = sy < in_row0 ? in_row0 : (sy >= in_row1 ? in_row1 - 1 : sy);
+      const int sx = refl101(gx, W);
+      const uint8_t *p = rgb + ((int64_t)(sy - in_row0) * W + sx) * 3;
       const YCC c = rgb2ycc(p[0], p[1], p[2]);
       s_c[0][ry][rx] = (uint8_t)c.cr;
       s_c[1][ry][rx] = (uint8_t)c.cb;
-      if (gy >= cy0 && gy < cy1 && gx >= cx0 && gx < cx1) Y[(int64_t)gy * W + gx] = (uint8_t)c.y;
+      if (gy >= cy0 && gy < cy1 && gx >= cx0 && gx < cx1) Y[(int64_t)(gy - out_row0) * W + gx] = (uint8_t)c.y;
     }
   }
   __syncthreads();
@@ -101,11 +114,11 @@ __global__ __launch_bounds__(256) void k_rgb_ycrcb420(const uint8_t *__restrict_
   for (int i = threadIdx.x; i < 2 * TY * TX; i += 256) {
     const int pl = i / (TY * TX), rem = i - pl * TY * TX;
     const int ly = rem / TX, lx = rem - ly * TX;
-    const int oy = oy0 + ly, ox = ox0 + lx;
-    if (oy < dh && ox < dw) {
+    const int oyl = oyl0 + ly, ox = ox0 + lx;
+    if (oyl < dh_out && ox < dw) {
       const int v = s_h[pl][2 * ly][lx] + 4 * (s_h[pl][2 * ly + 1][lx] + s_h[pl][2 * ly + 3][lx]) +
                     6 * s_h[pl][2 * ly + 2][lx] + s_h[pl][2 * ly + 4][lx];
-      (pl ? Cb : Cr)[(int64_t)oy * dw + ox] = (uint8_t)sat8((v + 128) >> 8);
+      (pl ? Cb : Cr)[(int64_t)oyl * dw + ox] = (uint8_t)sat8((v + 128) >> 8);
     }
   }
 }
@@ -195,16 +208,33 @@ bool dims_ok(int64_t H, int64_t W) { return H > 0 && W > 0 && H < (1 << 20) && W
 
 using namespace hic;
 
-extern "C" int hic_rgb_to_ycrcb420(const uint8_t *rgb, int64_t H, int64_t W, uint8_t *y, uint8_t *cr,
-                                   uint8_t *cb, void *stream) {
-  if (!rgb || !y || !cr || !cb) return arg_error("null pointer");
+extern "C" int hic_rgb_to_ycrcb420_rows(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, int64_t H,
+                                        int64_t W, int64_t out_row0, int64_t out_rows, uint8_t *y, uint8_t *cr,
+                                        uint8_t *cb, void *stream) {
+  if (!rgb_rows || !y || !cr || !cb) return arg_error("null pointer");
   if (!dims_ok(H, W) || H < 2 || W < 2) return arg_error("image shape (needs >= 2x2)");
-  if (reinterpret_cast<uintptr_t>(rgb) % 4 || reinterpret_cast<uintptr_t>(y) % 4)
+  if (reinterpret_cast<uintptr_t>(rgb_rows) % 4 || reinterpret_cast<uintptr_t>(y) % 4)
     return arg_error("rgb / y must be 4-byte aligned");
-  const int dh = (int)(H / 2), dw = (int)(W / 2);
-  const dim3 grid((dw + TX - 1) / TX, (dh + TY - 1) / TY);
-  hipLaunchKernelGGL(k_rgb_ycrcb420, grid, dim3(256), 0, as_stream(stream), rgb, (int)H, (int)W, y, cr, cb, dh, dw);
+  if (out_row0 < 0 || out_rows < 1 || out_row0 % 2 || out_row0 + out_rows > H) return arg_error("output row range");
+  if (out_rows % 2 && out_row0 + out_rows != H) return arg_error("odd output row count before the last row");
+  const int64_t dh = H / 2, dw = W / 2;
+  const int64_t c0 = out_row0 / 2, c1 = (out_row0 + out_rows) / 2 < dh ? (out_row0 + out_rows) / 2 : dh;
+  // rows the kernel reads: chroma rows [c0, c1) need image rows [2*c0 - 2, 2*c1 + 2) (reflected);
+  // the Y rows are inside that span
+  const int64_t need0 = 2 * c0 - 2 < 0 ? 0 : 2 * c0 - 2;
+  const int64_t need1 = (2 * c1 + 2 > H ? H : 2 * c1 + 2) > out_row0 + out_rows ? (2 * c1 + 2 > H ? H : 2 * c1 + 2)
+                                                                                : out_row0 + out_rows;
+  if (in_row0 > need0 || in_row0 + in_rows < need1) return arg_error("input rows do not cover the pyrDown halo");
+  if (c1 <= c0) return arg_error("no chroma rows in the output range");
+  const dim3 grid((unsigned)((dw + TX - 1) / TX), (unsigned)((c1 - c0 + TY - 1) / TY));
+  hipLaunchKernelGGL(k_rgb_ycrcb420, grid, dim3(256), 0, as_stream(stream), rgb_rows, (int)in_row0, (int)in_rows, (int)H, (int)W,
+                     (int)out_row0, (int)out_rows, y, cr, cb, (int)(c1 - c0), (int)dw);
   return check_launch("k_rgb_ycrcb420");
+}
+
+extern "C" int hic_rgb_to_ycrcb420(const uint8_t *rgb, int64_t H, int64_t W, uint8_t *y, uint8_t *cr, uint8_t *cb,
+                                   void *stream) {
+  return hic_rgb_to_ycrcb420_rows(rgb, 0, H, H, W, 0, H, y, cr, cb, stream);
 }
 
 extern "C" int hic_rgb_to_ycrcb(const uint8_t *rgb, int64_t H, int64_t W, uint8_t *y, uint8_t *cr, uint8_t *cb,

@@ -316,17 +316,18 @@ __global__ void k_rle_summary(const T *__restrict__ blocks, int64_t nblk, Stream
   }
 }
 
-__global__ void k_rle_stitch(const int64_t *__restrict__ all, int world, int rank, int64_t *__restrict__ st) {
+__global__ void k_rle_stitch(const int64_t *__restrict__ all, int world, int rank, int stride,
+                             int64_t *__restrict__ st) {
   if (threadIdx.x != 0) return;
   int64_t carry = 0;
   for (int r = rank - 1; r >= 0; --r) {
-    carry += all[r * 4 + 0];
-    if (all[r * 4 + 1]) break;
+    carry += all[(int64_t)r * stride + 0];
+    if (all[(int64_t)r * stride + 1]) break;
   }
   st[0] = carry;
   st[1] = rank == world - 1 ? 1 : 0;
   st[2] = rank > 0 ? 1 : 0;
-  st[3] = rank > 0 ? all[(rank - 1) * 4 + 3] : 0;
+  st[3] = rank > 0 ? all[(int64_t)(rank - 1) * stride + 3] : 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -602,10 +603,12 @@ extern "C" int hic_rle_stream_encode_i32(const int32_t *arr, int64_t n, int max_
                     d_count, workspace, as_stream(stream));
 }
 
-extern "C" int hic_rle_stitch(const int64_t *d_all_summaries, int world, int rank, int64_t *d_stitch, void *stream) {
+extern "C" int hic_rle_stitch(const int64_t *d_all_summaries, int world, int rank, int rank_stride, int64_t *d_stitch,
+                              void *stream) {
   if (!d_all_summaries || !d_stitch) return arg_error("null pointer");
-  if (world < 1 || rank < 0 || rank >= world) return arg_error("world / rank");
-  hipLaunchKernelGGL(k_rle_stitch, dim3(1), dim3(64), 0, as_stream(stream), d_all_summaries, world, rank, d_stitch);
+  if (world < 1 || rank < 0 || rank >= world || rank_stride < 4) return arg_error("world / rank / stride");
+  hipLaunchKernelGGL(k_rle_stitch, dim3(1), dim3(64), 0, as_stream(stream), d_all_summaries, world, rank, rank_stride,
+                     d_stitch);
   return check_launch("k_rle_stitch");
 }
 

@@ -1,0 +1,224 @@
+"""Huffman entropy back end (mirrors hiccup/huffman.py:11-259).
+
+Host-side: SURVEY.md section 8(f) ranks the Huffman stage as the first "next"
+row after the GPU front end.  The tree is built exactly as the reference does
+(a ``heapq`` of nodes ordered by frequency only, leaves in first-appearance
+order of the keys, the first popped node becomes the LEFT child, codes read
+root -> leaf with left = "1", right = "0"; a one-symbol alphabet gets the code
+"1"), so tables and bit strings are identical to the reference's
+(tests/test_codec_host.py pins them against golden payloads).
+
+Encoding is vectorised (a code lookup per distinct key, then one join) instead
+of the reference's per-symbol parent walk (huffman.py:131-142).
+"""
+import heapq
+
+import numpy as np
+
+from . import utils
+
+
+class HuffmanTree:
+    class Node:
+        GROUND = None
+        ROOT = None
+
+        def __init__(self, left, right, value, frequency):
+            self.id = id(self)
+            self.parent = self.ROOT
+            self.left = left
+            self.right = right
+            self.value = value
+            self.frequency = frequency
+
+        @classmethod
+        def leaf(cls, value, frequency):
+            return cls(cls.GROUND, cls.GROUND, value, frequency)
+
+        @classmethod
+        def combine(cls, l, r):
+            node = cls(l, r, None, l.frequency + r.frequency)
+            l.parent = node
+            r.parent = node
+            return node
+
+        @classmethod
+        def singleton(cls, n):
+            node = cls(n, cls.GROUND, None, n.frequency)
+            n.parent = node
+            return node
+
+        def path(self, nodes=None):
+            nodes = [] if nodes is None else nodes
+            node = self
+            while True:
+                nodes.append(node)
+                if node.is_root:
+                    return nodes
+                node = node.parent
+
+        def inherit(self, child):
+            child.parent = self
+            return self
+
+        def mass_adopt(self):
+            self.inherit(self.left).inherit(self.right)
+
+        @property
+        def encoding(self):
+            return self.value, self.path()
+
+        @property
+        def is_leaf(self):
+            return self.left is self.GROUND and self.right is self.GROUND
+
+        @property
+        def is_root(self):
+            return self.parent is self.ROOT
+
+        @property
+        def depth(self):
+            if self.is_leaf:
+                return 1
+            return 1 + max(self.left.depth, self.right.depth)
+
+        def __eq__(self, other):
+            return type(self) == type(other) and self.id == other.id
+
+        __hash__ = object.__hash__
+
+        def __lt__(self, other):
+            return self.frequency < other.frequency
+
+        def __gt__(self, other):
+            return self.frequency > other.frequency
+
+        def __le__(self, other):
+            return self < other or self == other
+
+        def __ge__(self, other):
+            return self > other or self == other
+
+    # ------------------------------------------------------------ construction
+    @classmethod
+    def construct_from_data(cls, data, key_func=utils.identity):
+        groups = utils.group_by(data, key_func=key_func)
+        leaves = [cls.Node.leaf(k, len(v)) for k, v in groups.items()]
+        return cls(cls._construct(leaves), leaves, data, key_func)
+
+    @classmethod
+    def construct_from_counts(cls, keys, counts, data=None, key_func=utils.identity):
+        """Fast path: keys already in first-appearance order with their counts."""
+        leaves = [cls.Node.leaf(k, int(c)) for k, c in zip(keys, counts)]
+        return cls(cls._construct(leaves), leaves, data, key_func)
+
+    @classmethod
+    def construct_from_leaves(cls, segments, key_func=utils.identity):
+        leaves = [cls.Node.leaf(*s) for s in segments]
+        return cls(cls._construct(leaves), leaves, None, key_func)
+
+    @classmethod
+    def construct_from_coding(cls, segments, key_func=utils.identity):
+        """Rebuild a decoding tree from (value, code) pairs (huffman.py:30-58)."""
+        by_code = dict((code, value) for value, code in segments)
+        levels = max(len(code) for _, code in segments)
+        root = cls.Node(None, None, None, None)
+        leaves = []
+        stack = [(root, 0, "")]
+        while stack:
+            node, depth, code = stack.pop()
+            if code in by_code:
+                node.value = by_code[code]
+                leaves.append(node)
+                continue
+            if depth != levels:
+                node.left = cls.Node.leaf(None, None)
+                node.right = cls.Node.leaf(None, None)
+                node.mass_adopt()
+                # visit left ("1") before right ("0"), as the reference's recursion does
+                stack.append((node.right, depth + 1, code + "0"))
+                stack.append((node.left, depth + 1, code + "1"))
+        return cls(root, leaves, None, key_func)
+
+    @classmethod
+    def _construct(cls, leaves):
+        if len(leaves) == 1:
+            return cls.Node.singleton(leaves[0])
+        heap = list(leaves)
+        heapq.heapify(heap)
+        while len(heap) > 1:
+            a = heapq.heappop(heap)
+            b = heapq.heappop(heap)
+            heapq.heappush(heap, cls.Node.combine(a, b))
+        return heapq.heappop(heap)
+
+    def __init__(self, root, leaves, data, key_func):
+        self.root = root
+        self.leaves = leaves
+        self.data = data
+        self.key_func = key_func
+        self._codes = None
+
+    # ------------------------------------------------------------ codes
+    @staticmethod
+    def _code_of(leaf):
+        bits = []
+        node = leaf
+        while not node.is_root:
+            parent = node.parent
+            bits.append("1" if parent.left is node else "0")
+            node = parent
+        return "".join(reversed(bits))
+
+    def codes(self):
+        """{key: code string} for every leaf."""
+        if self._codes is None:
+            self._codes = dict((leaf.value, self._code_of(leaf)) for leaf in self.leaves)
+        return self._codes
+
+    def get_leaf(self, value):
+        return utils.first(self.leaves, lambda l: l.value == value)
+
+    def translate_path(self, path, s=""):
+        return s + self._code_of(path[0]) if path else s
+
+    def encode_table(self):
+        return [(leaf.value, self._code_of(leaf)) for leaf in self.leaves]
+
+    def encode_data(self, data=None):
+        data = self.data if data is None else data
+        codes = self.codes()
+        return "".join(codes[self.key_func(d)] for d in data)
+
+    def encode_keys(self, keys):
+        """Vectorised encode of an integer key array (the jpeg_encode fast path)."""
+        keys = np.asarray(keys)
+        if keys.size == 0:
+            return ""
+        uniq, inv = np.unique(keys, return_inverse=True)
+        codes = self.codes()
+        table = np.array([codes[int(k)] for k in uniq], dtype=object)
+        return "".join(table[inv].tolist())
+
+    def decode_data(self, bits):
+        out = []
+        node = self.root
+        for ch in bits:
+            if ch == "1":
+                node = node.left
+            elif ch == "0":
+                node = node.right
+            else:
+                raise RuntimeError("Illegal state")
+            if node.is_leaf:
+                out.append(node.value)
+                node = self.root
+        return out
+
+
+def first_appearance_counts(keys):
+    """(unique keys in first-appearance order, counts) -- utils.group_by order."""
+    keys = np.asarray(keys)
+    uniq, first, counts = np.unique(keys, return_index=True, return_counts=True)
+    order = np.argsort(first, kind="stable")
+    return [int(k) for k in uniq[order]], counts[order]

@@ -1,0 +1,165 @@
+"""Device-resident JPEG-style encode / decode pipeline (the hot path, no host hops).
+
+``Encoder.encode(rgb)`` = compression.jpeg_compression + the zig-zag / DC / RLE
+half of codec.jpeg_encode (compression.py:16-39, codec.py:286-301) for one
+H x W x 3 uint8 image that already lives in HBM:
+
+  1. hic_rgb_to_ycrcb420      RGB -> Y (H x W) + pyrDown'd Cr, Cb (H/2 x W/2)
+  2. hic_dct_quant_u8 x 3     8x8 DCT + quantize + zig-zag -> int16 blocks (ZIGZAG_I16)
+  3. hic_rle_encode_i16 x 3   DC DPCM + channel-wide AC RLE -> (uint8 len, int16 val)
+
+All launches are asynchronous on one stream; buffers are allocated once.
+``Decoder.decode`` runs the inverse chain (codec.jpeg_decode's RLE/DC/izigzag
+half + compression.jpeg_decompression).  The optional ``stitch`` tensors make
+an encoder one tile-shard of a larger image (see sharding.py).
+"""
+import ctypes
+
+import torch
+
+from . import _lib, device
+
+CHANNELS = ("lum", "cr", "cb")
+TABLES = {"lum": _lib.TABLE_LUMINANCE, "cr": _lib.TABLE_CHROMINANCE, "cb": _lib.TABLE_CHROMINANCE}
+
+
+def _nblk(h, w):
+    return -(-h // 8) * -(-w // 8)
+
+
+def input_span(H, r0, r1):
+    """Rows of an H-row image that hic_rgb_to_ycrcb420_rows needs for output rows [r0, r1)."""
+    c0, c1 = r0 // 2, min(H // 2, r1 // 2)
+    return max(0, 2 * c0 - 2), max(r1, min(H, 2 * c1 + 2))
+
+
+class Encoder:
+    """rows=(r0, r1) makes this encoder one row-shard of an H x W image (r0 even;
+    shards of one image split at multiples of 16 rows so chroma blocks align)."""
+
+    def __init__(self, H, W, max_len=15, rows=None):
+        if H < 2 or W < 2:
+            raise ValueError("image must be at least 2 x 2")
+        device.require_gpu()
+        self.H, self.W, self.max_len = H, W, max_len
+        r0, r1 = rows if rows is not None else (0, H)
+        if r0 % 2 or not (0 <= r0 < r1 <= H):
+            raise ValueError("bad row range %r" % ((r0, r1),))
+        self.rows = (r0, r1)
+        c0, c1 = r0 // 2, min(H // 2, r1 // 2)
+        self.shapes = {"lum": (r1 - r0, W), "cr": (c1 - c0, W // 2), "cb": (c1 - c0, W // 2)}
+        ys, cs = self.shapes["lum"], self.shapes["cr"]
+        lib = _lib.load()
+        self.y = device.empty(ys, torch.uint8)
+        self.cr = device.empty(cs, torch.uint8)
+        self.cb = device.empty(cs, torch.uint8)
+        self.planes = {"lum": self.y, "cr": self.cr, "cb": self.cb}
+        self.coef, self.dc, self.sym_len, self.sym_val, self.ws = {}, {}, {}, {}, {}
+        self.cap = {}
+        self.counts = device.zeros((3,), torch.int64)
+        self.summaries = device.zeros((3, 4), torch.int64)
+        for k in CHANNELS:
+            n = _nblk(*self.shapes[k])
+            self.coef[k] = device.empty((n, 64), torch.int16)
+            self.dc[k] = device.empty((n,), torch.int32)
+            self.cap[k] = n * 63 + 1
+            self.sym_len[k] = device.empty((self.cap[k],), torch.uint8)
+            self.sym_val[k] = device.empty((self.cap[k],), torch.int16)
+            self.ws[k] = device.workspace(lib.hic_rle_workspace_bytes(n, 64))
+
+    @property
+    def pixels(self):
+        return (self.rows[1] - self.rows[0]) * self.W
+
+    def input_span(self):
+        """Image rows [in0, in1) this encoder reads: its rows plus the pyrDown halo."""
+        return input_span(self.H, *self.rows)
+
+    def transform(self, rgb, stream=None, in_row0=None):
+        """Steps 1-2: colour + 4:2:0 + DCT/quantize/zig-zag of the three planes.
+        rgb holds image rows [in_row0, in_row0 + rgb.shape[0]) (default: the
+        whole image for an unsharded encoder, input_span() for a shard)."""
+        s = device.stream_ptr(stream)
+        if in_row0 is None:
+            in_row0 = 0 if self.rows == (0, self.H) else self.input_span()[0]
+        r0, r1 = self.rows
+        _lib.call("hic_rgb_to_ycrcb420_rows", device.ptr(rgb), in_row0, rgb.shape[0], self.H, self.W, r0, r1 - r0,
+                  device.ptr(self.y), device.ptr(self.cr), device.ptr(self.cb), s)
+        for k in CHANNELS:
+            h, w = self.shapes[k]
+            p = self.planes[k]
+            _lib.call("hic_dct_quant_u8", device.ptr(p), h, w, p.stride(0), TABLES[k], _lib.LAYOUT_ZIGZAG_I16,
+                      device.ptr(self.coef[k]), s)
+
+    def shard_summaries(self, stream=None):
+        """Per-channel {trailing zeros, has nonzero, first DC, last DC} (sharded encode)."""
+        s = device.stream_ptr(stream)
+        for i, k in enumerate(CHANNELS):
+            n = self.coef[k].shape[0]
+            _lib.call("hic_rle_shard_summary_i16", device.ptr(self.coef[k]), n, 64, device.ptr(self.ws[k]),
+                      device.ptr(self.summaries[i]), s)
+        return self.summaries
+
+    def entropy(self, stream=None, stitch=None):
+        """Step 3: DC DPCM + AC RLE per channel.  stitch: None or a (3, 4) int64
+        device tensor of per-channel {carry_zeros, emit_eob, has_prev_dc, prev_dc}."""
+        s = device.stream_ptr(stream)
+        for i, k in enumerate(CHANNELS):
+            n = self.coef[k].shape[0]
+            st = device.ptr(stitch[i]) if stitch is not None else ctypes.c_void_p(0)
+            _lib.call("hic_rle_encode_i16", device.ptr(self.coef[k]), n, 64, self.max_len, st, device.ptr(self.dc[k]),
+                      device.ptr(self.sym_len[k]), device.ptr(self.sym_val[k]), self.cap[k],
+                      device.ptr(self.counts[i:i + 1]), device.ptr(self.ws[k]), s)
+
+    def encode(self, rgb, stream=None):
+        self.transform(rgb, stream)
+        self.entropy(stream)
+
+    def result(self):
+        """Host copies: {channel: (zigzag blocks, dc_diff, sym_len, sym_val)} (syncs)."""
+        device.sync()
+        counts = self.counts.cpu().numpy()
+        out = {}
+        for i, k in enumerate(CHANNELS):
+            c = int(counts[i])
+            if c < 0:
+                raise MemoryError("symbol buffer too small for channel %s" % k)
+            out[k] = (self.coef[k].cpu().numpy(), self.dc[k].cpu().numpy(), self.sym_len[k][:c].cpu().numpy(),
+                      self.sym_val[k][:c].cpu().numpy())
+        return out
+
+
+class Decoder:
+    """Inverse chain: symbols -> zig-zag blocks -> pixels -> RGB (2h x 2w x 3)."""
+
+    def __init__(self, H, W):
+        device.require_gpu()
+        self.H, self.W = H, W
+        self.shapes = {"lum": (H, W), "cr": (H // 2, W // 2), "cb": (H // 2, W // 2)}
+        self.blocks, self.pix, self.status = {}, {}, device.zeros((3,), torch.int64)
+        for k in CHANNELS:
+            h, w = self.shapes[k]
+            self.blocks[k] = device.empty((_nblk(h, w), 64), torch.int16)
+            self.pix[k] = device.empty((h, w), torch.uint8)
+        self.rgb = device.empty((2 * (H // 2), 2 * (W // 2), 3), torch.uint8)
+        self._ws = {}
+
+    def decode(self, sym_len, sym_val, counts, dc, stream=None):
+        """sym_len/sym_val/dc: {channel: device tensor}; counts: host ints per channel."""
+        s = device.stream_ptr(stream)
+        lib = _lib.load()
+        for i, k in enumerate(CHANNELS):
+            h, w = self.shapes[k]
+            n = self.blocks[k].shape[0]
+            nsym = int(counts[i])
+            need = lib.hic_rld_workspace_bytes(nsym, n)
+            if k not in self._ws or self._ws[k].numel() * 8 < need:
+                self._ws[k] = device.workspace(need)
+            _lib.call("hic_rle_decode_i16", device.ptr(sym_len[k]), device.ptr(sym_val[k]), nsym, device.ptr(dc[k]), n,
+                      64, device.ptr(self.blocks[k]), device.ptr(self.status[i:i + 1]), device.ptr(self._ws[k]), s)
+            _lib.call("hic_dequant_idct_u8", device.ptr(self.blocks[k]), _lib.LAYOUT_ZIGZAG_I16, h, w, TABLES[k],
+                      device.ptr(self.pix[k]), self.pix[k].stride(0), s)
+        h, w = self.shapes["cr"]
+        _lib.call("hic_ycrcb420_to_rgb", device.ptr(self.pix["lum"]), self.pix["lum"].stride(0),
+                  device.ptr(self.pix["cr"]), device.ptr(self.pix["cb"]), h, w, device.ptr(self.rgb), s)
+        return self.rgb

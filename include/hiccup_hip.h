@@ -94,6 +94,15 @@ int hic_dequantize_i32(const int32_t *in, int64_t nblk, int table_id, int64_t *o
  *      = cvtColor(RGB2YCrCb) then pyrDown(dstsize=(W/2,H/2)) on Cr and Cb. */
 int hic_rgb_to_ycrcb420(const uint8_t *rgb, int64_t H, int64_t W, uint8_t *y, uint8_t *cr,
                         uint8_t *cb, void *stream);
+/* Row-shard form for tile-sharded encode: rgb_rows holds image rows
+ * [in_row0, in_row0 + in_rows) of an H x W image (the shard plus the 2-row pyrDown
+ * halo on each side, clipped at the image border); writes Y rows
+ * [out_row0, out_row0 + out_rows) and chroma rows [out_row0/2, out_row0/2 + ceil..)
+ * to y / cr / cb (relative to the shard).  out_row0 must be even; reflect-101 is
+ * applied only at the true image border, so shard outputs equal the whole-image rows. */
+int hic_rgb_to_ycrcb420_rows(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, int64_t H,
+                             int64_t W, int64_t out_row0, int64_t out_rows, uint8_t *y, uint8_t *cr,
+                             uint8_t *cb, void *stream);
 /* cv2.cvtColor(RGB2YCrCb), full resolution, no resampling. */
 int hic_rgb_to_ycrcb(const uint8_t *rgb, int64_t H, int64_t W, uint8_t *y, uint8_t *cr,
                      uint8_t *cb, void *stream);
@@ -149,12 +158,12 @@ int hic_rle_encode_i32(const int32_t *blocks, int64_t nblk, int block_len, int m
 int hic_rle_stream_encode_i32(const int32_t *arr, int64_t n, int max_len, int32_t *sym_len,
                               int32_t *sym_val, int64_t sym_cap, int64_t *d_count, void *workspace,
                               void *stream);
-/* Computes this rank's d_stitch from all ranks' summaries (device int64[world][4],
- * e.g. after an all-gather): carry = trailing zeros of the preceding ranks back to
+/* Computes this rank's d_stitch from all ranks' summaries (device int64, rank r's
+ * 4 values at d_all_summaries[r * rank_stride], e.g. after an all-gather): carry = trailing zeros of the preceding ranks back to
  * the last one holding a nonzero; EOB only on the last rank; prev_dc = last DC of
  * rank-1. */
-int hic_rle_stitch(const int64_t *d_all_summaries, int world, int rank, int64_t *d_stitch,
-                   void *stream);
+int hic_rle_stitch(const int64_t *d_all_summaries, int world, int rank, int rank_stride,
+                   int64_t *d_stitch, void *stream);
 
 /* ---- entropy front end, inverse: codec.decode_run_length (codec.py:102-113) +
  *      utils.group_tuples (:412) + utils.invert_differences (utils.py:66-73) +

@@ -1,0 +1,222 @@
+"""GPU parity: RLE / DPCM / zig-zag kernels, jpeg_encode / jpeg_decode, the
+device pipeline and the shard stitching, against the reference's golden outputs
+(tests/golden/) and the C oracle at full size."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+import oracle.oracle as orc  # noqa: E402
+import oracle.oracle_c as orcc  # noqa: E402
+from hiccup_amd import (_lib, codec, compression, device, hicimage, model, pipeline, settings,  # noqa: E402
+                        sharding, transform)
+
+
+def _names(d, prefix):
+    return sorted(k[len(prefix):] for k in d if k.startswith(prefix))
+
+
+@pytest.fixture(autouse=True)
+def _block_size():
+    settings.DEBUG = False
+    yield
+    settings.JPEG_BLOCK_SIZE = 8
+
+
+def test_run_length_golden(golden_rle):
+    g = golden_rle
+    for name in _names(g, "in_"):
+        arr, ml = g["in_" + name], int(g["ml_" + name])
+        rl = codec.run_length_coding(arr, max_len=(ml if ml else None))
+        assert [r.length for r in rl] == g["len_" + name].tolist(), name
+        assert [r.value for r in rl] == g["val_" + name].tolist(), name
+        dec = codec.decode_run_length(rl, len(arr))
+        assert dec == g["dec_" + name].tolist(), name
+
+
+def test_codectest_cases():
+    # codectest.py:20-67,125-191
+    rl = codec.run_length_coding(transform.zigzag(np.array([[1, 2], [3, 4]]))[1:])
+    assert rl == [codec.RunLength(3, 0), codec.RunLength(2, 0), codec.RunLength(4, 0)]
+    assert [s.length for s in codec.run_length_coding(np.array([0] * 17 + [1]), max_len=0xF)] == [14, 2]
+    assert codec.run_length_coding(np.array([0, 0, 5]))[-1].is_trailing is False
+    assert codec.run_length_coding(np.array([0, 0, 5, 0, 0]))[-1].is_trailing is True
+    rle = [codec.RunLength(value=0, length=14), codec.RunLength(value=31, length=0)]
+    assert codec.run_length_coding(codec.decode_run_length(rle, 15), max_len=0xF) == rle
+    arr = [int(x) for x in np.random.default_rng(3).integers(-5, 5, 10000)]
+    assert codec.decode_run_length(codec.run_length_coding(np.array(arr)), 10000) == arr
+    with pytest.raises(ZeroDivisionError):
+        codec.run_length_coding([1, 0, 2], max_len=0)
+    with pytest.raises(TypeError):
+        codec.decode_run_length([], 5)
+
+
+def test_rle_long_carried_runs():
+    """A nonzero after thousands of all-zero blocks: the cooperative filler path."""
+    n = 63 * 5000
+    arr = np.zeros(n, np.int64)
+    arr[[3, 40000, n - 70000, n - 2]] = [5, -7, 9, 1]
+    rl = codec.run_length_coding(arr)
+    L, V = orc.rle_encode(arr, 15)
+    assert [r.length for r in rl] == L.tolist() and [r.value for r in rl] == V.tolist()
+    rl1 = codec.run_length_coding(arr, max_len=1)
+    L1, V1 = orc.rle_encode(arr, 1)
+    assert [r.length for r in rl1] == L1.tolist() and [r.value for r in rl1] == V1.tolist()
+
+
+def test_jpeg_encode_golden(golden_codec):
+    g = golden_codec
+    for name in _names(g, "bs_"):
+        settings.JPEG_BLOCK_SIZE = int(g["bs_" + name])
+        ci = model.CompressedImage(*(g["in_%s_%s" % (ch, name)] for ch in ("lum", "cr", "cb")))
+        hic = codec.jpeg_encode(ci)
+        p = hic.payloads
+        assert len(p) == 20 and hic.hic_type == model.Compression.JPEG
+        for k, ch in enumerate(("lum", "cr", "cb")):
+            for j, kind in enumerate(("dch", "avh", "alh")):
+                table = p[3 * j + k].payloads
+                assert [t.numbers[0] for t in table] == g["%sv_%s_%s" % (kind, ch, name)].tolist(), (name, kind)
+                assert [t.numbers[1] for t in table] == g["%sc_%s_%s" % (kind, ch, name)].tolist(), (name, kind)
+            for j, kind in enumerate(("dcb", "avb", "alb")):
+                assert p[9 + 3 * j + k].payload == str(g["%s_%s_%s" % (kind, ch, name)]), (name, kind)
+        assert p[18].numbers == tuple(g["shape0_" + name]) and p[19].numbers == tuple(g["shape1_" + name])
+        # codectest.py:69-80: first DC table entry of the lum channel
+        if name == "t_encode":
+            assert p[0].payloads[0].numbers == (1, "1")
+        # bytes round trip of the container (hicimagetest.py)
+        back = hicimage.HicImage.from_bytes(hic.byte_stream())
+        assert all(a == b for a, b in zip(hic.payloads, back.payloads))
+        if int(g["decfail_" + name]):
+            with pytest.raises(AssertionError):
+                codec.jpeg_decode(hic)
+        else:
+            dec = codec.jpeg_decode(hic)
+            for ch in ("lum", "cr", "cb"):
+                np.testing.assert_array_equal(dec.as_dict[ch], g["dec_%s_%s" % (ch, name)])
+            assert dec == ci
+
+
+def test_encode_channel_lenna(golden_lenna):
+    g = golden_lenna
+    for ch in ("cr", "cb"):
+        dc, L, V = codec.encode_channel(g["q_" + ch])
+        np.testing.assert_array_equal(dc, g["dc_" + ch])
+        np.testing.assert_array_equal(L, g["acl_" + ch])
+        np.testing.assert_array_equal(V, g["acv_" + ch])
+    dc, L, V = codec.encode_channel(g["q_y"][:256])
+    np.testing.assert_array_equal(L, g["acl_y256"])
+    np.testing.assert_array_equal(V, g["acv_y256"])
+
+
+def test_colour_kernels_vs_restatement():
+    rng = np.random.default_rng(8)
+    for H, W in ((64, 64), (37, 50), (130, 258), (2, 2), (3, 7), (1080, 1920)):
+        rgb = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+        y, cr, cb = compression.ycrcb420_device(device.to_device(rgb))
+        ry, rcr, rcb = orcc.rgb_to_ycrcb(rgb)
+        np.testing.assert_array_equal(device.to_host(y), ry, err_msg=str((H, W)))
+        np.testing.assert_array_equal(device.to_host(cr), orcc.pyr_down(rcr), err_msg=str((H, W)))
+        np.testing.assert_array_equal(device.to_host(cb), orcc.pyr_down(rcb), err_msg=str((H, W)))
+        if H >= 2 and W >= 2:
+            np.testing.assert_array_equal(transform.down_sample(ry), orcc.pyr_down(ry))
+        np.testing.assert_array_equal(transform.up_sample(rcr), orcc.pyr_up(rcr))
+    # transformtest.py:122-146
+    np.testing.assert_array_equal(transform.up_sample(np.full((2, 2), 2, np.uint8)), np.full((4, 4), 2, np.uint8))
+    np.testing.assert_array_equal(transform.down_sample(np.full((4, 4), 2, np.uint8)), np.full((2, 2), 2, np.uint8))
+
+
+def test_jpeg_compression_roundtrip(golden_lenna):
+    g = golden_lenna
+    ci = compression.jpeg_compression(g["rgb"])
+    np.testing.assert_array_equal(ci.luminance_component, g["q_y"])
+    np.testing.assert_array_equal(ci.red_chrominance_component, g["q_cr"])
+    np.testing.assert_array_equal(ci.blue_chrominance_component, g["q_cb"])
+    rgb = compression.jpeg_decompression(ci)
+    up = lambda p: orcc.pyr_up(p)  # noqa: E731
+    exp = orcc.ycrcb_to_rgb(g["rec_y"], up(g["rec_cr"]), up(g["rec_cb"]))
+    np.testing.assert_array_equal(rgb, exp)
+    err = np.abs(rgb.astype(np.int32) - g["rgb"].astype(np.int32)).mean()
+    assert err < 6.0
+
+
+def _oracle_encode(rgb):
+    y, cr, cb = orcc.rgb_to_ycrcb(rgb)
+    planes = {"lum": (y, 0), "cr": (orcc.pyr_down(cr), 1), "cb": (orcc.pyr_down(cb), 1)}
+    out = {}
+    for k, (p, t) in planes.items():
+        q = orcc.dct_channel(p, t, threads=16)
+        zz = orcc.zigzag_blocks(q, 8)
+        L, V = orcc.rle_encode(zz[:, 1:].reshape(-1), 15)
+        out[k] = (zz, orcc.dpcm(zz[:, 0].copy()), L, V)
+    return out
+
+
+@pytest.mark.parametrize("H,W", [(64, 96), (4320, 7680), (250, 330)])
+def test_pipeline_encoder(H, W):
+    rng = np.random.default_rng(H)
+    rgb = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    if H == 250:
+        rgb[:, :100] = 128  # flat region: all-zero AC blocks, long runs
+    enc = pipeline.Encoder(H, W)
+    enc.encode(device.to_device(rgb))
+    got = enc.result()
+    exp = _oracle_encode(rgb)
+    for k in pipeline.CHANNELS:
+        zz, dc, L, V = got[k]
+        ezz, edc, eL, eV = exp[k]
+        np.testing.assert_array_equal(zz.astype(np.int32), ezz, err_msg=k)
+        np.testing.assert_array_equal(dc, edc, err_msg=k)
+        np.testing.assert_array_equal(L.astype(np.int32), eL, err_msg=k)
+        np.testing.assert_array_equal(V.astype(np.int32), eV, err_msg=k)
+    # decode back through the device chain: equals the oracle's inverse
+    dec = pipeline.Decoder(H, W)
+    dev = {k: (device.to_device(got[k][2]), device.to_device(got[k][3]), device.to_device(got[k][1]))
+           for k in pipeline.CHANNELS}
+    counts = [len(got[k][2]) for k in pipeline.CHANNELS]
+    rgb2 = device.to_host(dec.decode({k: v[0] for k, v in dev.items()}, {k: v[1] for k, v in dev.items()}, counts,
+                                     {k: v[2] for k, v in dev.items()}))
+    assert np.all(dec.status.cpu().numpy() == [len(got[k][0]) * 63 for k in pipeline.CHANNELS])
+    rec = {}
+    for k, (p, t) in {"lum": (H, 0), "cr": (0, 1), "cb": (0, 1)}.items():
+        zz = exp[k][0]
+        h, w = (H, W) if k == "lum" else (H // 2, W // 2)
+        raster = orc.merge_blocks(zz[:, np.argsort(orc.ZZ8)].reshape(-1, 8, 8), (h, w))
+        rec[k] = orcc.inv_dct_channel(raster, t)
+    h, w = H // 2, W // 2
+    exp_rgb = orcc.ycrcb_to_rgb(rec["lum"][:2 * h, :2 * w], orcc.pyr_up(rec["cr"]), orcc.pyr_up(rec["cb"]))
+    np.testing.assert_array_equal(rgb2, exp_rgb)
+
+
+@pytest.mark.parametrize("H,W,world", [(4320, 7680, 8), (250, 330, 3), (96, 64, 2)])
+def test_shards_stitch_to_single_stream(H, W, world):
+    """Row shards (with pyrDown halos) + the stitch record reproduce the
+    single-GPU stream exactly (the multi-GPU path, simulated on one device)."""
+    rng = np.random.default_rng(W)
+    rgb = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    rgb[H // 3: H // 3 + 40] = 128  # zero runs that cross shard boundaries
+    whole = pipeline.Encoder(H, W)
+    whole.encode(device.to_device(rgb))
+    ref = whole.result()
+    encs = []
+    for rows in sharding.plan(H, world):
+        e = pipeline.Encoder(H, W, rows=rows)
+        a, b = e.input_span()
+        e.transform(device.to_device(rgb[a:b]))
+        encs.append(e)
+    summ = np.stack([e.shard_summaries().cpu().numpy() for e in encs])  # (world, 3, 4)
+    allsum = device.to_device(summ)
+    for r, e in enumerate(encs):
+        st = device.zeros((3, 4), torch.int64)
+        for c in range(3):
+            import ctypes
+            _lib.call("hic_rle_stitch", ctypes.c_void_p(allsum.data_ptr() + 32 * c), world, r, 12,
+                      device.ptr(st[c]), device.stream_ptr())
+            np.testing.assert_array_equal(st[c].cpu().numpy(), sharding.stitch_host(summ[:, c], r))
+        e.entropy(stitch=st)
+    parts = [e.result() for e in encs]
+    for k in pipeline.CHANNELS:
+        zz = np.concatenate([p[k][0] for p in parts])
+        np.testing.assert_array_equal(zz, ref[k][0], err_msg=k)
+        for j in (1, 2, 3):
+            np.testing.assert_array_equal(np.concatenate([p[k][j] for p in parts]), ref[k][j], err_msg=(k, j))

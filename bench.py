@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""bench.py -- hiccup encode throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2], the 8K encode the metric is quoted on): a
+7680 x 4320 RGB uint8 image, already resident in HBM, through the full encode
+front end = compression.jpeg_compression + the zig-zag / DC / RLE half of
+codec.jpeg_encode:
+  RGB -> YCrCb + 4:2:0 pyrDown  (1 fused kernel)
+  8x8 DCT + quantize + zig-zag   (3 planes, bit-exact float64)
+  DC DPCM + channel-wide AC RLE  (3 planes, 3 kernels each)
+One "step" encodes one such image per GPU.
+
+--gpus N > 1 (launched by torch.distributed.run, one process per GPU, RCCL):
+  --mode weak   (default): an (N*4320) x 7680 image, one 4320-row tile-shard per
+                rank; ranks all-gather their per-channel RLE/DC boundary
+                summaries (the only exchange the path needs), stitch, and emit
+                their slice of the single global symbol stream.
+  --mode strong: one 8K image split N ways.
+  --gather      also reassembles the whole stream on rank 0 (RCCL send/recv)
+                inside the timed region.
+value = pixels encoded by all ranks / max-over-ranks wall time of the K steps.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+H8K, W8K = 4320, 7680
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+ROT_BYTES = 1.2e9      # rotate >= 1.2 GB of inputs: defeats the 256 MiB Infinity Cache
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--mode", choices=("weak", "strong"), default="weak")
+    ap.add_argument("--gather", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget-s", type=float, default=25.0)
+    return ap.parse_args()
+
+
+def cpu_baseline(budget_s):
+    """The C oracle (scalar restatement of hiccup's CPU path, 1 thread) on a
+    bounded sample of the same workload: leading 8K rows until ~budget."""
+    import oracle.oracle_c as orcc
+    rng = np.random.default_rng(3)
+    rows = 1088  # 1/4 of the 8K frame (multiple of 16); grown below if fast
+    done_px, elapsed = 0, 0.0
+    sample = None
+    while elapsed < budget_s * 0.5:
+        rgb = rng.integers(0, 256, (rows, W8K, 3), dtype=np.uint8)
+        t0 = time.perf_counter()
+        y, cr, cb = orcc.rgb_to_ycrcb(rgb)
+        for p, t in ((y, 0), (orcc.pyr_down(cr), 1), (orcc.pyr_down(cb), 1)):
+            q = orcc.dct_channel(p, t)
+            zz = orcc.zigzag_blocks(q, 8)
+            orcc.dpcm(zz[:, 0].copy())
+            orcc.rle_encode(zz[:, 1:].reshape(-1), 15)
+        dt = time.perf_counter() - t0
+        done_px += rows * W8K
+        elapsed += dt
+        sample = "%d x %d RGB rows of the 8K workload, %d pass(es), full encode chain" % (rows, W8K, 1)
+        if dt > budget_s * 0.5:
+            break
+    return {"value": round(done_px / elapsed / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "port",
+            "sample": "%s; %.1f s; oracle/hiccup_oracle.c (scalar restatement, bit-identical to the GPU path)"
+                      % (sample, elapsed),
+            "reference_measured_in_build_container": "hiccup's own numpy path ~0.7 Mpix/s (8K 4:2:0 DCT+quantize, "
+                                                     "BASELINE.md); its RLE is quadratic (infeasible at 8K)"}
+
+
+def load_pmc_traffic():
+    """HBM bytes per luminance-DCT launch from the committed rocprofv3 PMC summary
+    (profiles/pmc_dct_lum.json, FETCH_SIZE doubled per MI355X_MICROARCH.md)."""
+    p = os.path.join(HERE, "profiles", "pmc_dct_lum.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        return json.load(f)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        if world == 1:
+            raise SystemExit("--gpus %d needs torch.distributed.run --nproc-per-node %d" % (args.gpus, args.gpus))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from hiccup_amd import device, pipeline, sharding
+    device.require_gpu()
+
+    if world > 1:
+        H = H8K * world if args.mode == "weak" else H8K
+        make = lambda: sharding.ShardEncoder(H, W8K, rank=rank, world=world)  # noqa: E731
+    else:
+        H = H8K
+        make = lambda: pipeline.Encoder(H8K, W8K)  # noqa: E731
+    encs = [make() for _ in range(4)]  # rotate outputs too (~1.2 GB)
+    span = encs[0].span if world > 1 else (0, H)
+    in_rows = span[1] - span[0]
+    nin = max(2, int(np.ceil(ROT_BYTES / (in_rows * W8K * 3))))
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3 + rank)
+    inputs = [torch.randint(0, 256, (in_rows, W8K, 3), dtype=torch.uint8, device="cuda", generator=g)
+              for _ in range(nin)]
+    enc0 = encs[0].enc if world > 1 else encs[0]
+    lum_px = enc0.shapes["lum"][0] * enc0.shapes["lum"][1]
+    px_per_step_rank = enc0.pixels
+
+    timed_events = []
+
+    def step(i, record=False):
+        e = encs[i % len(encs)]
+        x = inputs[i % nin]
+        ev = None
+        if record:  # HIP events around the luminance DCT launch, on its stream
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            timed_events.append(ev)
+        e.encode(x, lum_events=ev)
+        if world > 1 and args.gather:
+            sharding.gather_streams(e)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i, record=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---- dominant kernel: luminance DCT+quantize+zig-zag, HIP events recorded
+    # around its launch inside the timed steps (same stream)
+    dct_us = float(np.mean([s.elapsed_time(t) for s, t in timed_events])) * 1e3
+    achieved = lum_px * 3 / (dct_us * 1e-6) / 1e9  # u8 in + int16 out per pixel
+
+    if rank == 0:
+        total_px = px_per_step_rank * world * args.steps
+        value = total_px / elapsed / 1e6
+        pmc = load_pmc_traffic()
+        out = {
+            "metric": "Mpixels/s encode (DCT+quantize+zig-zag) at 8K; % HBM roofline, 1/2/4/8 GPU",
+            "value": round(value, 2),
+            "unit": "Mpixels/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak" if (world == 1 or args.mode == "weak") else "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (uniform random uint8 RGB, resident in HBM)",
+            "config": {
+                "workload": "7680x4320 RGB -> YCrCb 4:2:0 full encode: colour+pyrDown, 8x8 DCT+quantize+zig-zag "
+                            "(3 planes), DC DPCM + AC RLE (3 planes)",
+                "image_hw": [H, W8K],
+                "per_rank_rows": in_rows if world == 1 else encs[0].rows[1] - encs[0].rows[0],
+                "mode": "single" if world == 1 else args.mode,
+                "gather_to_rank0": bool(args.gather and world > 1),
+                "parallelism": "dp%d tile-shard" % world,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_dct_quant_2ph (luminance, 4320x7680)",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                "algorithmic_bytes": lum_px * 3,
+                "avg_launch_us": round(dct_us, 2),
+            },
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_budget_s)
+        elif not args.no_cpu_baseline:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

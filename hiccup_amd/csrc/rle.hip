@@ -221,6 +221,47 @@ __global__ __launch_bounds__(kScanT) void k_rle_scan(int64_t *__restrict__ tiles
 }
 
 // K3: emit symbols (+ DC differences when dc_diff != nullptr).
+// Each lane writes its block's symbols into an LDS stage at the tile-relative
+// offset, then the workgroup copies the tile's contiguous symbol range out with
+// aligned 4-byte stores (partial edge words by element stores).  A tile whose
+// symbols exceed the stage (a nonzero after >~1300 carried-in zeros) takes the
+// direct path, with long filler runs written cooperatively.
+constexpr int kStageSyms = kTB * 68;
+
+template <typename L_T, typename V_T>
+__device__ __forceinline__ void put_sym(bool staged, int64_t o, int64_t o_tile, int lo, int vo, uint8_t *s_len,
+                                        V_T *s_val, L_T *__restrict__ sym_len, V_T *__restrict__ sym_val, int64_t cap,
+                                        int len, int val) {
+  if (staged) {
+    const int r = (int)(o - o_tile);
+    s_len[lo + r] = (uint8_t)len;
+    s_val[vo + r] = (V_T)val;
+  } else if (o < cap) {
+    sym_len[o] = (L_T)len;
+    sym_val[o] = (V_T)val;
+  }
+}
+
+// Copy n elements from LDS (element e at s[a + e]) to global g[o0 + e], where
+// a == o0 mod (4 / sizeof(T)): aligned 4-byte stores, element stores at the edges.
+template <typename T>
+__device__ __forceinline__ void copy_out(const T *s, int a, T *__restrict__ g, int64_t o0, int n, int64_t cap) {
+  constexpr int E = 4 / (int)sizeof(T);  // elements per word
+  const int64_t w0 = o0 / E, w1 = (o0 + n + E - 1) / E;
+  for (int64_t w = w0 + threadIdx.x; w < w1; w += kTB) {
+    const int64_t e0 = w * E;
+    if (e0 >= o0 && e0 + E <= o0 + n && e0 + E <= cap) {
+      const int li = (int)(e0 - o0) + a;  // multiple of E
+      *reinterpret_cast<uint32_t *>(g + e0) = *reinterpret_cast<const uint32_t *>(s + li);
+    } else {
+      for (int k = 0; k < E; ++k) {
+        const int64_t e = e0 + k;
+        if (e >= o0 && e < o0 + n && e < cap) g[e] = s[(int)(e - o0) + a];
+      }
+    }
+  }
+}
+
 template <typename T, typename L_T, typename V_T>
 __global__ __launch_bounds__(kTB) void k_rle_emit(const T *__restrict__ blocks, int64_t nblk, StreamGeo g, int M,
                                                   const int64_t *__restrict__ offs, const int64_t *__restrict__ stitch,
@@ -230,6 +271,8 @@ __global__ __launch_bounds__(kTB) void k_rle_emit(const T *__restrict__ blocks, 
   __shared__ int64_t s_fill_start[kTB];
   __shared__ int64_t s_fill_count[kTB];
   __shared__ int s_nfill;
+  __shared__ uint8_t s_len[kStageSyms + 4];
+  __shared__ V_T s_val[kStageSyms + 4];
   if (threadIdx.x == 0) s_nfill = 0;
   const int64_t b = (int64_t)blockIdx.x * kTB + threadIdx.x;
   int first = -1, last = -1, nsym = 0;
@@ -241,7 +284,10 @@ __global__ __launch_bounds__(kTB) void k_rle_emit(const T *__restrict__ blocks, 
   if (prev < 0) prev = offs[blockIdx.x * 2 + 1];
   const int64_t cnt = nsym + (first >= 0 ? syms_for_run(base + first - prev - 1, M) : 0);
   int64_t total;
-  int64_t o = offs[blockIdx.x * 2 + 0] + block_excl_sum<int64_t, kTB>(cnt, s_buf, total);
+  const int64_t o_tile = offs[blockIdx.x * 2 + 0];
+  int64_t o = o_tile + block_excl_sum<int64_t, kTB>(cnt, s_buf, total);
+  const bool staged = total <= kStageSyms;  // uniform across the workgroup
+  const int lo = (int)(o_tile & 3), vo = (int)(o_tile & ((4 / (int)sizeof(V_T)) - 1));
 
   if (b < nblk) {
     if (dc_diff) {  // codec.differential_coding over raster-ordered blocks
@@ -260,7 +306,7 @@ __global__ __launch_bounds__(kTB) void k_rle_emit(const T *__restrict__ blocks, 
         int64_t run = base + j - p - 1;
         if (M > 0) {
           const int64_t nf = run / M;
-          if (nf > 32) {
+          if (!staged && nf > 32) {
             // long carried-in run: the whole workgroup writes the fillers
             const int slot = atomicAdd(&s_nfill, 1);
             s_fill_start[slot] = o;
@@ -268,31 +314,225 @@ __global__ __launch_bounds__(kTB) void k_rle_emit(const T *__restrict__ blocks, 
             o += nf;
           } else {
             for (int64_t k = 0; k < nf; ++k, ++o)
-              if (o < cap) {
-                sym_len[o] = (L_T)(M - 1);
-                sym_val[o] = 0;
-              }
+              put_sym<L_T, V_T>(staged, o, o_tile, lo, vo, s_len, s_val, sym_len, sym_val, cap, M - 1, 0);
           }
           run -= nf * M;
         }
-        if (o < cap) {
-          sym_len[o] = (L_T)run;
-          sym_val[o] = (V_T)v;
-        }
+        put_sym<L_T, V_T>(staged, o, o_tile, lo, vo, s_len, s_val, sym_len, sym_val, cap, (int)run, v);
         ++o;
         p = base + j;
       }
     }
   }
   __syncthreads();
-  const int nfill = s_nfill;
-  for (int f = 0; f < nfill; ++f) {
-    const int64_t s0 = s_fill_start[f], nf = s_fill_count[f];
-    for (int64_t k = threadIdx.x; k < nf; k += kTB)
-      if (s0 + k < cap) {
-        sym_len[s0 + k] = (L_T)(M - 1);
-        sym_val[s0 + k] = 0;
+  if (staged) {
+    if (sizeof(L_T) == 1) {
+      copy_out<uint8_t>(s_len, lo, reinterpret_cast<uint8_t *>(sym_len), o_tile, (int)total, cap);
+    } else {
+      for (int k = threadIdx.x; k < (int)total; k += kTB)
+        if (o_tile + k < cap) sym_len[o_tile + k] = (L_T)s_len[lo + k];
+    }
+    copy_out<V_T>(s_val, vo, sym_val, o_tile, (int)total, cap);
+  } else {
+    const int nfill = s_nfill;
+    for (int f = 0; f < nfill; ++f) {
+      const int64_t s0 = s_fill_start[f], nf = s_fill_count[f];
+      for (int64_t k = threadIdx.x; k < nf; k += kTB)
+        if (s0 + k < cap) {
+          sym_len[s0 + k] = (L_T)(M - 1);
+          sym_val[s0 + k] = 0;
+        }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Hot path: int16 zig-zag blocks of 64 (the DCT kernel's output), AC = slots 1..63.
+// The block stays in registers (8 x 16-byte loads); runs inside a block are int32;
+// MF = 15 specialises the run / max_len division (the jpeg_encode default).
+__device__ __forceinline__ int zz_ac(const uint32_t (&w)[32], int j) {
+  const int s = j + 1;
+  return (int)(int16_t)((w[s >> 1] >> (16 * (s & 1))) & 0xFFFFu);
+}
+
+__device__ __forceinline__ void load_block16(const int16_t *__restrict__ blocks, int64_t b, uint32_t (&w)[32]) {
+  const uint4 *q = reinterpret_cast<const uint4 *>(blocks + b * 64);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint4 t = q[k];
+    w[4 * k] = t.x; w[4 * k + 1] = t.y; w[4 * k + 2] = t.z; w[4 * k + 3] = t.w;
+  }
+}
+
+template <int MF>
+__device__ __forceinline__ int div_m(int run, int M) {
+  return MF == 15 ? (int)(((uint32_t)run * 0x8889u) >> 19) : run / M;  // exact for run < 2^16
+}
+
+template <int MF>
+__device__ __forceinline__ void summarize16(const uint32_t (&w)[32], int M, int &first, int &last, int &nsym) {
+  first = -1;
+  last = -1;
+  nsym = 0;
+#pragma unroll
+  for (int j = 0; j < 63; ++j) {
+    if (zz_ac(w, j) != 0) {
+      if (first >= 0) nsym += 1 + div_m<MF>(j - last - 1, M);
+      first = first < 0 ? j : first;
+      last = j;
+    }
+  }
+}
+
+template <int MF>
+__global__ __launch_bounds__(kTB) void k_rle_tile16(const int16_t *__restrict__ blocks, int64_t nblk, int M,
+                                                    int64_t *__restrict__ tiles) {
+  __shared__ int64_t s_buf[8];
+  const int64_t b = (int64_t)blockIdx.x * kTB + threadIdx.x;
+  int first = -1, last = -1, nsym = 0;
+  if (b < nblk) {
+    uint32_t w[32];
+    load_block16(blocks, b, w);
+    summarize16<MF>(w, M, first, last, nsym);
+  }
+  const int64_t base = b * 63;
+  const int64_t lastg = last >= 0 ? base + last : -1;
+  int64_t all_last;
+  const int64_t prev = block_excl_max<int64_t, kTB>(lastg, (int64_t)-1, s_buf, all_last);
+  int64_t cnt = nsym;
+  if (first >= 0 && prev >= 0) cnt += syms_for_run(base + first - prev - 1, M);
+  int64_t total;
+  block_excl_sum<int64_t, kTB>(cnt, s_buf, total);
+  if (first >= 0 && prev < 0) tiles[blockIdx.x * 3 + 0] = base + first;
+  if (threadIdx.x == 0) {
+    tiles[blockIdx.x * 3 + 1] = all_last;
+    tiles[blockIdx.x * 3 + 2] = total;
+    if (all_last < 0) tiles[blockIdx.x * 3 + 0] = -1;
+  }
+}
+
+template <int MF>
+__global__ __launch_bounds__(kTB) void k_rle_emit16(const int16_t *__restrict__ blocks, int64_t nblk, int M,
+                                                    const int64_t *__restrict__ offs,
+                                                    const int64_t *__restrict__ stitch, int32_t *__restrict__ dc_diff,
+                                                    uint8_t *__restrict__ sym_len, int16_t *__restrict__ sym_val,
+                                                    int64_t cap) {
+  __shared__ int64_t s_buf[8];
+  __shared__ int64_t s_fill_start[kTB];
+  __shared__ int64_t s_fill_count[kTB];
+  __shared__ int s_nfill;
+  __shared__ uint8_t s_len[kStageSyms + 4];
+  __shared__ int16_t s_val[kStageSyms + 4];
+  if (threadIdx.x == 0) s_nfill = 0;
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * kTB + threadIdx.x;
+  uint32_t w[32];
+  int first = -1, last = -1, nsym = 0;
+  if (b < nblk) {
+    load_block16(blocks, b, w);
+    summarize16<MF>(w, M, first, last, nsym);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 32; ++k) w[k] = 0;
+  }
+  const int64_t base = b * 63;
+  const int64_t lastg = last >= 0 ? base + last : -1;
+  int64_t all_last;
+  int64_t prev = block_excl_max<int64_t, kTB>(lastg, (int64_t)-1, s_buf, all_last);
+  if (prev < 0) prev = offs[blockIdx.x * 2 + 1];
+  const int64_t run0 = base + first - prev - 1;  // carried run before the first nonzero
+  const int64_t cnt = nsym + (first >= 0 ? syms_for_run(run0, M) : 0);
+  int64_t total;
+  const int64_t o_tile = offs[blockIdx.x * 2 + 0];
+  const int64_t o_thr = o_tile + block_excl_sum<int64_t, kTB>(cnt, s_buf, total);
+  const bool staged = total <= kStageSyms;
+  const int lo = (int)(o_tile & 3), vo = (int)(o_tile & 1);
+
+  // DC differences: the previous block's DC comes from the neighbouring lane
+  const int dc = (int)(int16_t)(w[0] & 0xFFFFu);
+  int pdc = __shfl_up(dc, 1, 64);
+  if (b < nblk) {
+    if (lane == 0 && b > 0) pdc = (int)blocks[(b - 1) * 64];
+    if (b > 0)
+      dc_diff[b] = dc - pdc;
+    else
+      dc_diff[b] = (stitch && stitch[2]) ? dc - (int)stitch[3] : dc;
+  }
+
+  if (first >= 0) {
+    int64_t o = o_thr;
+    // first nonzero: possibly long carried-in run
+    {
+      const int64_t nf = run0 / M;
+      if (!staged && nf > 32) {
+        const int slot = atomicAdd(&s_nfill, 1);
+        s_fill_start[slot] = o;
+        s_fill_count[slot] = nf;
+        o += nf;
+      } else {
+        for (int64_t k = 0; k < nf; ++k, ++o)
+          put_sym<uint8_t, int16_t>(staged, o, o_tile, lo, vo, s_len, s_val, sym_len, sym_val, cap, M - 1, 0);
       }
+      put_sym<uint8_t, int16_t>(staged, o, o_tile, lo, vo, s_len, s_val, sym_len, sym_val, cap, (int)(run0 - nf * M),
+                                zz_ac(w, first));
+      ++o;
+    }
+    if (staged) {
+      int r = (int)(o - o_tile);  // tile-relative output position
+      int pl = first;
+#pragma unroll
+      for (int j = 1; j < 63; ++j) {
+        const int v = zz_ac(w, j);
+        if (j > first && v != 0) {
+          int run = j - pl - 1;
+          const int nf = div_m<MF>(run, M);
+          for (int k = 0; k < nf; ++k, ++r) {
+            s_len[lo + r] = (uint8_t)(M - 1);
+            s_val[vo + r] = 0;
+          }
+          run -= nf * M;
+          s_len[lo + r] = (uint8_t)run;
+          s_val[vo + r] = (int16_t)v;
+          ++r;
+          pl = j;
+        }
+      }
+    } else {
+      int pl = first;
+      for (int j = first + 1; j <= last; ++j) {
+        const int v = zz_ac(w, j);
+        if (v == 0) continue;
+        int run = j - pl - 1;
+        const int nf = run / M;
+        for (int k = 0; k < nf; ++k, ++o)
+          if (o < cap) {
+            sym_len[o] = (uint8_t)(M - 1);
+            sym_val[o] = 0;
+          }
+        run -= nf * M;
+        if (o < cap) {
+          sym_len[o] = (uint8_t)run;
+          sym_val[o] = (int16_t)v;
+        }
+        ++o;
+        pl = j;
+      }
+    }
+  }
+  __syncthreads();
+  if (staged) {
+    copy_out<uint8_t>(s_len, lo, sym_len, o_tile, (int)total, cap);
+    copy_out<int16_t>(s_val, vo, sym_val, o_tile, (int)total, cap);
+  } else {
+    const int nfill = s_nfill;
+    for (int f = 0; f < nfill; ++f) {
+      const int64_t s0 = s_fill_start[f], nf = s_fill_count[f];
+      for (int64_t k = threadIdx.x; k < nf; k += kTB)
+        if (s0 + k < cap) {
+          sym_len[s0 + k] = (uint8_t)(M - 1);
+          sym_val[s0 + k] = 0;
+        }
+    }
   }
 }
 
@@ -578,6 +818,29 @@ extern "C" int hic_rle_encode_i16(const int16_t *blocks, int64_t nblk, int block
                                   int64_t sym_cap, int64_t *d_count, void *workspace, void *stream) {
   // uint8 lengths: fillers are max_len-1 <= 255 and residual runs < max_len
   if (max_len < 1 || max_len > 256) return arg_error("max_len must be in [1, 256] for uint8 symbol lengths");
+  if (block_len == 64 && (reinterpret_cast<uintptr_t>(blocks) & 15) == 0) {
+    if (!blocks || !dc_diff || !sym_len || !sym_val || !d_count || !workspace) return arg_error("null pointer");
+    if (nblk <= 0) return arg_error("nblk");
+    hipStream_t s = as_stream(stream);
+    const int64_t nt = ntiles_of(nblk);
+    int64_t *tiles = static_cast<int64_t *>(workspace);
+    int64_t *offs = tiles + 3 * nt;
+    if (max_len == 15)
+      hipLaunchKernelGGL((k_rle_tile16<15>), dim3((unsigned)nt), dim3(kTB), 0, s, blocks, nblk, max_len, tiles);
+    else
+      hipLaunchKernelGGL((k_rle_tile16<0>), dim3((unsigned)nt), dim3(kTB), 0, s, blocks, nblk, max_len, tiles);
+    if (int e = check_launch("k_rle_tile16")) return e;
+    hipLaunchKernelGGL((k_rle_scan<uint8_t, int16_t>), dim3(1), dim3(kScanT), 0, s, tiles, offs, nt, nblk * 63,
+                       max_len, d_stitch, sym_len, sym_val, sym_cap, d_count);
+    if (int e = check_launch("k_rle_scan")) return e;
+    if (max_len == 15)
+      hipLaunchKernelGGL((k_rle_emit16<15>), dim3((unsigned)nt), dim3(kTB), 0, s, blocks, nblk, max_len, offs,
+                         d_stitch, dc_diff, sym_len, sym_val, sym_cap);
+    else
+      hipLaunchKernelGGL((k_rle_emit16<0>), dim3((unsigned)nt), dim3(kTB), 0, s, blocks, nblk, max_len, offs,
+                         d_stitch, dc_diff, sym_len, sym_val, sym_cap);
+    return check_launch("k_rle_emit16");
+  }
   if (block_len < 2) return arg_error("block_len");
   if (!dc_diff) return arg_error("null dc_diff");
   return rle_encode(blocks, nblk, block_geo(nblk, block_len), max_len, d_stitch, dc_diff, sym_len, sym_val, sym_cap,

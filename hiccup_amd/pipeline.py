@@ -75,7 +75,7 @@ class Encoder:
         """Image rows [in0, in1) this encoder reads: its rows plus the pyrDown halo."""
         return input_span(self.H, *self.rows)
 
-    def transform(self, rgb, stream=None, in_row0=None):
+    def transform(self, rgb, stream=None, in_row0=None, lum_events=None):
         """Steps 1-2: colour + 4:2:0 + DCT/quantize/zig-zag of the three planes.
         rgb holds image rows [in_row0, in_row0 + rgb.shape[0]) (default: the
         whole image for an unsharded encoder, input_span() for a shard)."""
@@ -88,8 +88,12 @@ class Encoder:
         for k in CHANNELS:
             h, w = self.shapes[k]
             p = self.planes[k]
+            if lum_events is not None and k == "lum":
+                lum_events[0].record(stream)
             _lib.call("hic_dct_quant_u8", device.ptr(p), h, w, p.stride(0), TABLES[k], _lib.LAYOUT_ZIGZAG_I16,
                       device.ptr(self.coef[k]), s)
+            if lum_events is not None and k == "lum":
+                lum_events[1].record(stream)
 
     def shard_summaries(self, stream=None):
         """Per-channel {trailing zeros, has nonzero, first DC, last DC} (sharded encode)."""
@@ -111,8 +115,8 @@ class Encoder:
                       device.ptr(self.sym_len[k]), device.ptr(self.sym_val[k]), self.cap[k],
                       device.ptr(self.counts[i:i + 1]), device.ptr(self.ws[k]), s)
 
-    def encode(self, rgb, stream=None):
-        self.transform(rgb, stream)
+    def encode(self, rgb, stream=None, lum_events=None):
+        self.transform(rgb, stream, lum_events=lum_events)
         self.entropy(stream)
 
     def result(self):

@@ -71,10 +71,10 @@ class ShardEncoder:
     def pixels(self):
         return self.enc.pixels
 
-    def encode(self, rgb_rows, stream=None):
+    def encode(self, rgb_rows, stream=None, lum_events=None):
         """rgb_rows: device uint8 tensor of image rows self.span (shard + halo)."""
         enc = self.enc
-        enc.transform(rgb_rows, stream, in_row0=self.span[0])
+        enc.transform(rgb_rows, stream, in_row0=self.span[0], lum_events=lum_events)
         summ = enc.shard_summaries(stream)
         # the exchange step: 96 bytes per rank over RCCL
         dist.all_gather_into_tensor(self.all_summ, summ, group=self.group)

@@ -52,6 +52,15 @@ def stitch_host(summaries, rank):
                     dtype=np.int64)
 
 
+def exchange(summ_local, world, group=None):
+    """All-gather every rank's (3, 4) channel summaries -> (world, 3, 4): the one
+    collective of the sharded encode (RCCL on GPU tensors, gloo on CPU ones)."""
+    shape = tuple(summ_local.shape)
+    out = torch.empty((world * shape[0],) + shape[1:], dtype=summ_local.dtype, device=summ_local.device)
+    dist.all_gather_into_tensor(out, summ_local.contiguous(), group=group)
+    return out.view((world,) + shape)
+
+
 class ShardEncoder:
     """One rank's part of a tile-sharded encode of an H x W RGB image."""
 
@@ -77,13 +86,13 @@ class ShardEncoder:
         enc.transform(rgb_rows, stream, in_row0=self.span[0], lum_events=lum_events)
         summ = enc.shard_summaries(stream)
         # the exchange step: 96 bytes per rank over RCCL
-        dist.all_gather_into_tensor(self.all_summ, summ, group=self.group)
+        dist.all_gather_into_tensor(self.all_summ.view(self.world * 3, 4), summ, group=self.group)
         s = device.stream_ptr(stream)
         for c in range(3):
             _lib.call("hic_rle_stitch", ctypes.c_void_p(self.all_summ.data_ptr() + 8 * 4 * c), self.world, self.rank,
                       12, device.ptr(self.stitch[c]), s)
         enc.entropy(stream, stitch=self.stitch)
-        dist.all_gather_into_tensor(self.all_counts, enc.counts, group=self.group)
+        dist.all_gather_into_tensor(self.all_counts.view(-1), enc.counts, group=self.group)
 
     def offsets(self):
         """(this rank's symbol offset per channel, global totals) -- host ints (syncs)."""
@@ -97,7 +106,7 @@ def gather_streams(se, dst=0):
     counts = se.all_counts.cpu().numpy()
     nblk = torch.tensor([se.enc.dc[k].numel() for k in CHANNELS], dtype=torch.int64, device=se.all_counts.device)
     all_nblk = torch.zeros((se.world, 3), dtype=torch.int64, device=nblk.device)
-    dist.all_gather_into_tensor(all_nblk, nblk, group=se.group)
+    dist.all_gather_into_tensor(all_nblk.view(-1), nblk, group=se.group)
     all_nblk = all_nblk.cpu().numpy()
     out = {} if se.rank == dst else None
     for ci, k in enumerate(CHANNELS):

@@ -1,0 +1,170 @@
+"""CPU tests: the C-ABI library and its declarations, and the host-side parts of
+the package (Huffman back end, container, helpers) against the reference's
+golden payloads.  No GPU, no kernel calls."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from hiccup_amd import _lib, hicimage, huffman, iohelper, sharding, transform, utils
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "hiccup_hip.h")
+
+
+def _declared():
+    txt = open(HEADER).read()
+    return dict((m.group(2), m.group(3)) for m in
+                re.finditer(r"^(int|size_t)\s+(hic_\w+)\(([^;]*?)\);", txt, re.M | re.S))
+
+
+def test_header_and_library_symbols():
+    decl = _declared()
+    assert len(decl) >= 25
+    lib = ctypes.CDLL(_lib.LIB_PATH)  # loads without a GPU
+    for name in decl:
+        assert hasattr(lib, name), name
+
+
+def test_ctypes_signatures_match_header():
+    decl = _declared()
+    assert set(decl) == set(_lib.SIGNATURES)
+    for name, args in decl.items():
+        nargs = 0 if args.strip() == "void" else len([a for a in args.split(",") if a.strip()])
+        assert nargs == len(_lib.SIGNATURES[name][1]), name
+    assert _lib.load().hic_abi_version() == 1
+
+
+def test_last_error_roundtrip():
+    lib = _lib.load()
+    rc = lib.hic_dct_quant_u8(None, 8, 8, 8, 0, 0, None, None)
+    assert rc == _lib.HIC_ERR_ARG
+    assert "null pointer" in _lib.last_error()
+    with pytest.raises(ValueError):
+        _lib.check(rc, "x")
+
+
+def _names(d, prefix):
+    return sorted(k[len(prefix):] for k in d if k.startswith(prefix))
+
+
+def test_huffman_tables_and_bits_golden(golden_codec):
+    """Host Huffman (byte-compatible with huffman.py) on the reference's own DC / RLE
+    streams reproduces its tables and bit strings."""
+    g = golden_codec
+    for name in _names(g, "bs_"):
+        for ch in ("lum", "cr", "cb"):
+            streams = {"dc": g["dc_%s_%s" % (ch, name)], "av": g["acv_%s_%s" % (ch, name)],
+                       "al": g["acl_%s_%s" % (ch, name)]}
+            for kind, key in (("dc", "dc"), ("av", "av"), ("al", "al")):
+                keys = streams[key]
+                tree = huffman.HuffmanTree.construct_from_counts(*huffman.first_appearance_counts(keys))
+                table = tree.encode_table()
+                assert [v for v, _ in table] == g["%shv_%s_%s" % (kind, ch, name)].tolist(), (name, ch, kind)
+                assert [c for _, c in table] == g["%shc_%s_%s" % (kind, ch, name)].tolist(), (name, ch, kind)
+                bits = tree.encode_keys(keys)
+                assert bits == str(g["%sb_%s_%s" % (kind, ch, name)]), (name, ch, kind)
+                # decode side: rebuild from the table, decode the bits
+                dec = huffman.HuffmanTree.construct_from_coding(table)
+                assert dec.decode_data(bits) == keys.tolist()
+                # the slow generic path agrees with the vectorised one
+                slow = huffman.HuffmanTree.construct_from_data(keys.tolist())
+                assert slow.encode_table() == table and slow.encode_data() == bits
+
+
+def test_huffman_reference_unit_cases():
+    # huffmantest.py
+    t = huffman.HuffmanTree.construct_from_data([0, 0, 0, 0, 0])
+    assert len(t.leaves) == 1 and t.encode_data() == "11111"
+    t = huffman.HuffmanTree.construct_from_data([0, 0, 0, 1])
+    assert t.root.frequency == 4 and t.root.left.value == 1 and t.root.right.value == 0
+    data = [1, 2, 2, 3, 3, 3, 4, 4, 4, 4]
+    t = huffman.HuffmanTree.construct_from_data(data)
+    out = t.encode_data()
+    assert out == "001" + ("000" * 2) + ("01" * 3) + ("1" * 4)
+    assert t.decode_data(out) == data
+    t = huffman.HuffmanTree.construct_from_data([("A", 0), ("B", 1), ("B", 0)], key_func=lambda x: x[0])
+    assert t.root.left.value == "A" and t.root.right.value == "B"
+
+
+def test_iohelper_reference_cases():
+    # iohelpertest.py
+    assert iohelper.bin_string(3) == "11"
+    assert iohelper.padded_bs_2_bytes("101") == b"\x05\xa0"
+    assert iohelper.padded_bytes_2_bs(bytearray(b"\x05\xa0")) == "101"
+    for s in ["01", "0000", "1010000", "00000", "000111", "00000001", "000001", "0000001", "10010110",
+              "0" * 777 + "1"] + [bin(i)[2:] for i in range(1, 5000, 37)]:
+        assert iohelper.padded_bytes_2_bs(iohelper.padded_bs_2_bytes(s)) == s
+    with pytest.raises(AssertionError):
+        iohelper.bin_string_as_bytes("0")
+
+
+def test_utils_reference_cases():
+    # utilstest.py
+    assert utils.group_tuples([1, 2, 3, 4], 2) == [(1, 2), (3, 4)]
+    with pytest.raises(AssertionError):
+        utils.group_tuples([1, 2, 3], 2)
+    for n, b in [[0, 0], [1, 1], [2, 2], [3, 2], [4, 3], [100, 7], [-60, 6], [-1, 1]]:
+        assert utils.num_bits_for_int(n) == b
+    assert utils.differences([1, 5, 12, 0]) == [1, 4, 7, -12]
+    assert utils.invert_differences([1, 1, 1, 1]) == [1, 2, 3, 4]
+    assert utils.group_by([1, 2, 2, 3, 3, 3])[3] == [3, 3, 3]
+    assert utils.flatten([[1, 2], [3, 4]]) == [1, 2, 3, 4]
+    assert utils.img_as_list(np.array([[1, 2], [3, 4]])) == [1, 2, 3, 4]
+    assert utils.dict_map({"a": 1, "b": 2}, lambda k, v: k + str(v)) == {"a": "a1", "b": "b2"}
+    assert utils.is_gray(np.array([[1, 2], [2, 3]])) and not utils.is_gray(np.array([[1, 2]]))
+    with pytest.raises(RuntimeError):
+        utils.first([1, 2], lambda x: x < 0)
+
+
+def test_transform_host_helpers(golden_tables):
+    # transformtest.py:21-53,70-120,195-211
+    sq = np.array([[1, 2], [3, 4]])
+    sp = transform.split_matrix(sq, 1)
+    assert len(sp) == 4 and [b[0][0] for b in sp] == [1, 2, 3, 4]
+    sp = transform.split_matrix(np.arange(1, 10).reshape(3, 3), 2)
+    assert len(sp) == 4 and np.sum(sp[0]) == 12 and np.sum(sp[3]) == 9
+    blocks = np.array([[[1, 2], [7, 8]], [[3, 4], [9, 10]], [[5, 6], [11, 12]],
+                       [[13, 14], [0, 0]], [[15, 16], [0, 0]], [[17, 18], [0, 0]]])
+    assert np.array_equiv(transform.merge_blocks(blocks, (4, 6)),
+                          [[1, 2, 3, 4, 5, 6], [7, 8, 9, 10, 11, 12], [13, 14, 15, 16, 17, 18], [0] * 6])
+    m = np.random.default_rng(0).integers(0, 256, (8, 12))
+    assert np.array_equiv(transform.merge_blocks(transform.split_matrix(m, 4), m.shape), m)
+    assert transform.zigzag(np.arange(1, 10).reshape(3, 3)) == [1, 4, 2, 3, 5, 7, 8, 6, 9]
+    assert np.array_equiv(transform.izigzag(np.array([1, 4, 2, 3, 5, 7, 8, 6, 9]), (3, 3)),
+                          np.arange(1, 10).reshape(3, 3))
+    m = np.random.default_rng(1).integers(0, 256, (17, 19))
+    assert np.array_equiv(transform.izigzag(transform.zigzag(m), m.shape), m)
+    for n in (2, 3, 4, 8):
+        order = [y * n + x for y, x in transform._zigzag_indices(np.zeros((n, n)))]
+        assert order == golden_tables["zz%d" % n].tolist()
+    assert transform.dc_component(np.array([[1, 2], [3, 4]])) == 1
+    assert transform.ac_components(np.array([[[1, 2], [3, 4]], [[5, 6], [7, 8]]])) == [3, 2, 4, 7, 6, 8]
+
+
+def test_container_roundtrip(tmp_path):
+    payloads = ([hicimage.PayloadStringP(hicimage.TupP, [hicimage.TupP(5, "10"), hicimage.TupP(-3, "0")])] * 9
+                + [hicimage.BitStringP("1011")] * 9 + [hicimage.TupP(16, 24), hicimage.TupP(8, 12)])
+    img = hicimage.HicImage.jpeg_image(payloads)
+    back = hicimage.HicImage.from_bytes(img.byte_stream())
+    assert all(a == b for a, b in zip(img.payloads, back.payloads))
+    path = str(tmp_path / "x.hic")
+    img.write_file(path)
+    again = hicimage.HicImage.from_file(path)
+    assert all(a == b for a, b in zip(img.payloads, again.payloads))
+
+
+def test_shard_plan_and_stitch():
+    for H, world in ((4320, 8), (4320 * 8, 8), (33, 2), (250, 3), (97, 5)):
+        p = sharding.plan(H, world)
+        assert p[0][0] == 0 and p[-1][1] == H
+        assert all(a[1] == b[0] for a, b in zip(p, p[1:]))
+        assert all(r0 % 16 == 0 for r0, _ in p)
+    with pytest.raises(ValueError):
+        sharding.plan(16, 2)
+    s = np.array([[3, 1, 5, 6], [63, 0, 1, 1], [10, 1, 2, 3]])
+    assert sharding.stitch_host(s, 0).tolist() == [0, 0, 0, 0]
+    assert sharding.stitch_host(s, 1).tolist() == [3, 0, 1, 6]
+    assert sharding.stitch_host(s, 2).tolist() == [66, 1, 1, 1]

@@ -1,0 +1,120 @@
+"""Multi-process (world_size 2 and 3, gloo on CPU) test of the tile-sharded
+encode's exchange step: each rank holds a block-row shard of the coefficient
+streams, all-gathers its channel summaries with sharding.exchange, derives its
+stitch record with sharding.stitch_host, run-length codes its slice, and rank 0
+reassembles the streams with point-to-point sends.  The result must equal the
+single-stream encode.  (Per-shard compute here is the CPU oracle -- test
+infrastructure; the GPU kernels for the same steps are covered by
+tests/test_gpu_codec.py::test_shards_stitch_to_single_stream.)"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle.oracle as orc
+from hiccup_amd import pipeline, sharding
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _image(H, W):
+    rng = np.random.default_rng(42)
+    rgb = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    rgb[H // 3: H // 3 + 40] = 128  # zero runs crossing shard boundaries
+    rgb[:, : W // 4] = 200
+    return rgb
+
+
+def _zz_planes(rgb):
+    y, cr, cb = orc.rgb_to_ycrcb(rgb)
+    out = {}
+    for k, p, t in (("lum", y, 0), ("cr", orc.pyr_down(cr), 1), ("cb", orc.pyr_down(cb), 1)):
+        out[k] = orc.zigzag_blocks(orc.split_blocks(orc.dct_channel(p, t)).astype(np.int64))
+    return out
+
+
+def _summary(zz):
+    ac = zz[:, 1:].reshape(-1)
+    nz = np.flatnonzero(ac)
+    return [len(ac) - 1 - (nz[-1] if len(nz) else -1), int(len(nz) > 0), int(zz[0, 0]), int(zz[-1, 0])]
+
+
+def _rle_stitched(zz, st):
+    carry, emit_eob, has_prev, prev_dc = (int(x) for x in st)
+    dc = zz[:, 0].astype(np.int64)
+    diff = orc.dpcm(dc)
+    if has_prev:
+        diff[0] = dc[0] - prev_dc
+    ac = zz[:, 1:].reshape(-1)
+    L, V = orc.rle_encode(np.concatenate([np.zeros(carry, np.int64), ac]), 15)
+    if not emit_eob and (len(ac) == 0 or ac[-1] == 0):
+        L, V = L[:-1], V[:-1]
+    return diff, L, V
+
+
+def _worker(rank, world, port, H, W, results):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        zz = _zz_planes(_image(H, W))
+        r0, r1 = sharding.plan(H, world)[rank]
+        mine = {}
+        for k in pipeline.CHANNELS:
+            nbx = -(-(W if k == "lum" else W // 2) // 8)
+            if k == "lum":
+                b0, b1 = (r0 // 8) * nbx, (-(-r1 // 8)) * nbx
+            else:
+                c1 = min(H // 2, r1 // 2)
+                b0, b1 = (r0 // 16) * nbx, (-(-c1 // 8)) * nbx
+            mine[k] = zz[k][b0:b1]
+        summ = torch.tensor([_summary(mine[k]) for k in pipeline.CHANNELS], dtype=torch.int64)
+        allsum = sharding.exchange(summ, world).numpy()
+        enc = {k: _rle_stitched(mine[k], sharding.stitch_host(allsum[:, c], rank))
+               for c, k in enumerate(pipeline.CHANNELS)}
+        # reassemble on rank 0: sizes first, then point-to-point payloads
+        sizes = torch.tensor([[len(enc[k][0]), len(enc[k][1])] for k in pipeline.CHANNELS], dtype=torch.int64)
+        all_sizes = sharding.exchange(sizes, world).numpy()
+        if rank == 0:
+            got = {}
+            for c, k in enumerate(pipeline.CHANNELS):
+                parts = [enc[k]]
+                for r in range(1, world):
+                    nb, ns = all_sizes[r, c]
+                    bufs = [torch.empty(nb, dtype=torch.int64), torch.empty(ns, dtype=torch.int64),
+                            torch.empty(ns, dtype=torch.int64)]
+                    for b in bufs:
+                        dist.recv(b, src=r)
+                    parts.append(tuple(b.numpy() for b in bufs))
+                got[k] = tuple(np.concatenate([p[j] for p in parts]) for j in range(3))
+            for k in pipeline.CHANNELS:
+                diff = orc.dpcm(zz[k][:, 0].astype(np.int64))
+                L, V = orc.rle_encode(zz[k][:, 1:].reshape(-1), 15)
+                ok = (np.array_equal(got[k][0], diff) and np.array_equal(got[k][1], L)
+                      and np.array_equal(got[k][2], V))
+                results[k] = bool(ok)
+        else:
+            for k in pipeline.CHANNELS:
+                for a in enc[k]:
+                    dist.send(torch.from_numpy(np.ascontiguousarray(a, dtype=np.int64)), dst=0)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,H,W", [(2, 96, 80), (3, 130, 72)])
+def test_sharded_exchange_gloo(world, H, W):
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), H, W, results), nprocs=world, join=True)
+    assert dict(results) == {k: True for k in pipeline.CHANNELS}

@@ -29,12 +29,26 @@ _int = ctypes.c_int
 _sz = ctypes.c_size_t
 
 # name -> (restype, argtypes); mirrors include/hiccup_hip.h exactly
+class RleJob16(ctypes.Structure):
+    """hic_rle_job16 (include/hiccup_hip.h)."""
+    _fields_ = [("blocks", _vp), ("nblk", _i64), ("d_stitch", _vp), ("dc_diff", _vp), ("sym_len", _vp),
+                ("sym_val", _vp), ("sym_cap", _i64), ("d_count", _vp), ("workspace", _vp)]
+
+
 SIGNATURES = {
     "hic_abi_version": (_int, []),
     "hic_last_error": (_int, [ctypes.c_char_p, _sz]),
     "hic_device_count": (_int, [ctypes.POINTER(_int)]),
     "hic_stream_sync": (_int, [_vp]),
     "hic_dct_quant_u8": (_int, [_vp, _i64, _i64, _i64, _int, _int, _vp, _vp]),
+    "hic_dct_quant_u8_timed": (_int, [_vp, _i64, _i64, _i64, _int, _int, _vp, _vp, _vp, _vp]),
+    "hic_dct_quant_rle_u8": (_int, [_vp, _i64, _i64, _i64, _int, _int, _vp, _vp, _vp, _vp, _vp]),
+    "hic_rle_encode_i16_tiles": (_int, [_vp, _i64, _int, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
+    "hic_rle_shard_summary_tiles": (_int, [_vp, _i64, _vp, _vp, _vp]),
+    "hic_rle_encode_i16_tiles_batch": (_int, [_int, _vp, _int, _vp]),
+    "hic_event_create": (_int, [_vp]),
+    "hic_event_destroy": (_int, [_vp]),
+    "hic_event_elapsed_ms": (_int, [_vp, _vp, _vp]),
     "hic_dequant_idct_u8": (_int, [_vp, _int, _i64, _i64, _int, _vp, _i64, _vp]),
     "hic_dct2_f64": (_int, [_vp, _i64, _vp, _vp]),
     "hic_idct2_f64": (_int, [_vp, _i64, _vp, _vp]),

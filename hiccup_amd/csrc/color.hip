@@ -8,6 +8,8 @@
 // [1 4 6 4 1]^2 / 256 with BORDER_REFLECT_101; pyrUp [1 6 1]/[4 4] taps with
 // OpenCV's reflect-101-left / replicate-right edge rule) and are checked against
 // the oracle's restatement (oracle/oracle.py), not against cv2 itself.
+#include <stdlib.h>
+
 #include "hic_common.h"
 
 namespace hic {
@@ -123,6 +125,145 @@ __global__ __launch_bounds__(256) void k_rgb_ycrcb420(const uint8_t *__restrict_
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fast form of the same fused op for W % 4 == 0: no LDS, no barriers.
+// A wave owns a strip of 64 RGB quads (4 pixels = 12 B per lane) and walks down
+// kSegC chroma rows:
+//  - each input row is loaded as one dwordx3 per lane (768 contiguous bytes per
+//    wave);
+//  - it is converted to Y (stored as one dword per lane: 256 B per wave, whole
+//    cache lines when W % 256 == 0), Cr, Cb;
+//  - the horizontal [1 4 6 4 1] at the two even columns of each quad takes its
+//    neighbour pixels through DPP wave shifts (wave_shr / wave_shl);
+//  - the strip's own halo pixels (x0-2, x0-1 and x0+256) for every row of the
+//    segment are converted once per segment, one row per lane, and enter the
+//    shifts at lanes 0 / 63 (v_readlane);
+//  - the vertical pass keeps a 5-row register window and writes each chroma row
+//    (2 B per lane per plane) as soon as its last input row is in.
+// All rows of a segment are loaded up front (2*kSegC + 3 rows).  Reflect-101 at
+// the left / right image border only ever needs pixels of the border quad
+// itself (x = -2, -1 -> 2, 1; x = W -> W - 2).
+constexpr int kStripQ = 64;
+
+// DPP wave shifts.  The edge lane's value is selected explicitly afterwards: relying
+// on update_dpp's `old` operand for the disabled lane miscompiles once the move is
+// folded into a consumer (bits 16-31 of lane 0 came out wrong).
+__device__ __forceinline__ uint32_t shr1(uint32_t v) {  // lane i <- lane i-1
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t shl1(uint32_t v) {  // lane i <- lane i+1
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);
+}
+
+// Packs four bytes.  The asm barrier keeps the backend from fusing the preceding
+// descale + saturate of two of them into v_ashr_pk_u8_i32: gfx950 codegen
+// assumes that instruction zeroes bits 16-31 of its destination, but they
+// came back holding the source's stale high half, OR-ed into the upper two bytes.
+__device__ __forceinline__ uint32_t pack4(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) {
+  asm volatile("" : "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3));
+  return b0 | b1 << 8 | b2 << 16 | b3 << 24;
+}
+
+template <int kSegC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kSegC == 8 ? 4 : 3))) void k_rgb_ycrcb420_walk(const uint8_t *__restrict__ rgb, int in_row0, int in_rows,
+                                                           int H, int W, int out_row0, int out_rows,
+                                                           uint8_t *__restrict__ Y, uint8_t *__restrict__ Cr,
+                                                           uint8_t *__restrict__ Cb, int dh_out, int nstrips,
+                                                           int nwaves) {
+  constexpr int kSegR = 2 * kSegC + 3;
+  static_assert(kSegR <= 64, "one halo row per lane");
+  const int lane = threadIdx.x & 63;
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wid >= nwaves) return;
+  const int seg = wid / nstrips, strip = wid - seg * nstrips;
+  const int nq = W >> 2, dw = W >> 1;
+  const int q0 = strip * kStripQ, q = q0 + lane;
+  const bool owner = q < nq;
+  const int qc = owner ? q : nq - 1;
+  const int oyl0 = seg * kSegC;                                  // shard-relative chroma row
+  const int ncr = dh_out - oyl0 < kSegC ? dh_out - oyl0 : kSegC;  // chroma rows of this segment
+  const int nr = 2 * ncr + 3;                                    // input rows of this segment
+  const int oy0 = out_row0 / 2 + oyl0;
+  const int gy0 = 2 * oy0 - 2;
+  const int in_row1 = in_row0 + in_rows;
+  // Y rows this wave writes: the 2x footprint of its chroma rows; the last segment
+  // of the shard also owns the odd leftover row of the image
+  const int yw0 = 2 * oy0;
+  const int yw1 = (oyl0 + kSegC >= dh_out) ? out_row0 + out_rows : 2 * (oy0 + ncr);
+  auto src_row = [&](int r) {
+    int sy = refl101(gy0 + r, H);
+    sy = sy < in_row0 ? in_row0 : (sy >= in_row1 ? in_row1 - 1 : sy);
+    return rgb + (int64_t)(sy - in_row0) * W * 3;
+  };
+
+  uint32_t raw[kSegR][3];
+#pragma unroll
+  for (int r = 0; r < kSegR; ++r) {
+    if (r < nr) {
+      const uint32_t *p = reinterpret_cast<const uint32_t *>(src_row(r) + 12 * qc);
+      raw[r][0] = p[0];
+      raw[r][1] = p[1];
+      raw[r][2] = p[2];
+    }
+  }
+  // halo of row `lane`: left = (cr, cr, cb, cb) of x0-2, x0-1; right = (cr, cb) of x0+256
+  uint32_t hal_l = 0, hal_r = 0;
+  if (lane < nr) {
+    const uint8_t *row = src_row(lane);
+    const int x0 = 4 * q0;
+    if (x0 >= 2) {
+      const uint8_t *p = row + 3 * (x0 - 2);
+      const YCC a = rgb2ycc(p[0], p[1], p[2]), b = rgb2ycc(p[3], p[4], p[5]);
+      hal_l = pack4(a.cr, b.cr, a.cb, b.cb);
+    }
+    if (x0 + 256 < W) {
+      const uint8_t *p = row + 3 * (x0 + 256);
+      const YCC c = rgb2ycc(p[0], p[1], p[2]);
+      hal_r = c.cr | c.cb << 8;
+    }
+  }
+  int hcr0[kSegR], hcr2[kSegR], hcb0[kSegR], hcb2[kSegR];
+#pragma unroll
+  for (int r = 0; r < kSegR; ++r) {
+    if (r < nr) {
+      const uint32_t w0 = raw[r][0], w1 = raw[r][1], w2 = raw[r][2];
+      const int px[12] = {(int)(w0 & 255), (int)((w0 >> 8) & 255), (int)((w0 >> 16) & 255), (int)(w0 >> 24),
+                          (int)(w1 & 255), (int)((w1 >> 8) & 255), (int)((w1 >> 16) & 255), (int)(w1 >> 24),
+                          (int)(w2 & 255), (int)((w2 >> 8) & 255), (int)((w2 >> 16) & 255), (int)(w2 >> 24)};
+      int cr[4], cb[4];
+      uint32_t yq = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const YCC c = rgb2ycc(px[3 * k], px[3 * k + 1], px[3 * k + 2]);
+        yq |= c.y << (8 * k);
+        cr[k] = (int)c.cr;
+        cb[k] = (int)c.cb;
+      }
+      const int gy = gy0 + r;
+      if (owner && gy >= yw0 && gy < yw1) *reinterpret_cast<uint32_t *>(Y + (int64_t)(gy - out_row0) * W + 4 * q) = yq;
+      // neighbours: pixels x-2, x-1 from the left quad, x+4 from the right quad
+      uint32_t lft = shr1(pack4(cr[2], cr[3], cb[2], cb[3]));
+      uint32_t rgt = shl1((uint32_t)cr[0] | (uint32_t)cb[0] << 8);
+      if (lane == 0) lft = (uint32_t)__builtin_amdgcn_readlane((int)hal_l, r);
+      if (lane == 63) rgt = (uint32_t)__builtin_amdgcn_readlane((int)hal_r, r);
+      if (q == 0) lft = pack4(cr[2], cr[1], cb[2], cb[1]);
+      if (q == nq - 1) rgt = (uint32_t)cr[2] | (uint32_t)cb[2] << 8;
+      hcr0[r] = (int)(lft & 255) + 4 * ((int)((lft >> 8) & 255) + cr[1]) + 6 * cr[0] + cr[2];
+      hcb0[r] = (int)((lft >> 16) & 255) + 4 * ((int)(lft >> 24) + cb[1]) + 6 * cb[0] + cb[2];
+      hcr2[r] = cr[0] + 4 * (cr[1] + cr[3]) + 6 * cr[2] + (int)(rgt & 255);
+      hcb2[r] = cb[0] + 4 * (cb[1] + cb[3]) + 6 * cb[2] + (int)((rgt >> 8) & 255);
+      if (r >= 4 && r % 2 == 0 && owner) {  // chroma row k = r/2 - 2 is complete
+        const int a = r - 4, k = r / 2 - 2;
+#define HIC_V(h) ((((h)[a] + 4 * ((h)[a + 1] + (h)[a + 3]) + 6 * (h)[a + 2] + (h)[a + 4]) + 128) >> 8)
+        const int64_t o = (int64_t)(oyl0 + k) * dw + 2 * q;
+        *reinterpret_cast<uint16_t *>(Cr + o) = (uint16_t)(sat8(HIC_V(hcr0)) | sat8(HIC_V(hcr2)) << 8);
+        *reinterpret_cast<uint16_t *>(Cb + o) = (uint16_t)(sat8(HIC_V(hcb0)) | sat8(HIC_V(hcb2)) << 8);
+#undef HIC_V
+      }
+    }
+  }
+}
+
 __global__ void k_rgb_ycrcb(const uint8_t *__restrict__ rgb, int64_t npix, uint8_t *__restrict__ Y,
                             uint8_t *__restrict__ Cr, uint8_t *__restrict__ Cb) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -226,6 +367,24 @@ extern "C" int hic_rgb_to_ycrcb420_rows(const uint8_t *rgb_rows, int64_t in_row0
                                                                                 : out_row0 + out_rows;
   if (in_row0 > need0 || in_row0 + in_rows < need1) return arg_error("input rows do not cover the pyrDown halo");
   if (c1 <= c0) return arg_error("no chroma rows in the output range");
+  if (W % 4 == 0 && reinterpret_cast<uintptr_t>(cr) % 2 == 0 && reinterpret_cast<uintptr_t>(cb) % 2 == 0 &&
+      getenv("HIC_COLOR_TILED") == nullptr) {
+    const int nstrips = (int)((W / 4 + kStripQ - 1) / kStripQ);
+    const char *sv = getenv("HIC_COLOR_SEG");
+    const int segc = sv && atoi(sv) == 16 ? 16 : 8;
+    const int nseg = (int)((c1 - c0 + segc - 1) / segc);
+    const int nwaves = nstrips * nseg;
+    const dim3 grid((unsigned)((nwaves + 3) / 4));
+    if (segc == 16)
+      hipLaunchKernelGGL(k_rgb_ycrcb420_walk<16>, grid, dim3(256), 0, as_stream(stream), rgb_rows, (int)in_row0,
+                         (int)in_rows, (int)H, (int)W, (int)out_row0, (int)out_rows, y, cr, cb, (int)(c1 - c0),
+                         nstrips, nwaves);
+    else
+      hipLaunchKernelGGL(k_rgb_ycrcb420_walk<8>, grid, dim3(256), 0, as_stream(stream), rgb_rows, (int)in_row0,
+                         (int)in_rows, (int)H, (int)W, (int)out_row0, (int)out_rows, y, cr, cb, (int)(c1 - c0),
+                         nstrips, nwaves);
+    return check_launch("k_rgb_ycrcb420_walk");
+  }
   const dim3 grid((unsigned)((dw + TX - 1) / TX), (unsigned)((c1 - c0 + TY - 1) / TY));
   hipLaunchKernelGGL(k_rgb_ycrcb420, grid, dim3(256), 0, as_stream(stream), rgb_rows, (int)in_row0, (int)in_rows, (int)H, (int)W,
                      (int)out_row0, (int)out_rows, y, cr, cb, (int)(c1 - c0), (int)dw);

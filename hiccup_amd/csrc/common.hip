@@ -35,3 +35,23 @@ extern "C" int hic_device_count(int *h_n) {
 extern "C" int hic_stream_sync(void *stream) {
   return hic::hip_status(hipStreamSynchronize(hic::as_stream(stream)), "hipStreamSynchronize");
 }
+
+extern "C" int hic_event_create(void **h_event) {
+  if (!h_event) return hic::arg_error("null pointer");
+  hipEvent_t e = nullptr;
+  const int rc = hic::hip_status(hipEventCreate(&e), "hipEventCreate");
+  *h_event = rc == HIC_OK ? (void *)e : nullptr;
+  return rc;
+}
+
+extern "C" int hic_event_destroy(void *event) {
+  if (!event) return hic::arg_error("null event");
+  return hic::hip_status(hipEventDestroy((hipEvent_t)event), "hipEventDestroy");
+}
+
+extern "C" int hic_event_elapsed_ms(void *start, void *stop, float *h_ms) {
+  if (!start || !stop || !h_ms) return hic::arg_error("null pointer");
+  int rc = hic::hip_status(hipEventSynchronize((hipEvent_t)stop), "hipEventSynchronize");
+  if (rc != HIC_OK) return rc;
+  return hic::hip_status(hipEventElapsedTime(h_ms, (hipEvent_t)start, (hipEvent_t)stop), "hipEventElapsedTime");
+}

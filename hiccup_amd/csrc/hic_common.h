@@ -1,6 +1,7 @@
 // hic_common.h -- shared plumbing for the libhiccup_hip.so C-ABI: error state,
 // launch checks, wave-level helpers.  gfx950 only (wave64).
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdint.h>
@@ -15,6 +16,13 @@ void set_error(const char *fmt, ...);
 
 inline int arg_error(const char *what) {
   set_error("invalid argument: %s", what);
+  return HIC_ERR_ARG;
+}
+template <typename... A>
+inline int arg_error(const char *fmt, A... args) {
+  char buf[200];
+  snprintf(buf, sizeof buf, fmt, args...);
+  set_error("invalid argument: %s", buf);
   return HIC_ERR_ARG;
 }
 
@@ -42,5 +50,22 @@ constexpr int kWave = 64;
 // Round n up to a multiple of a.
 __host__ __device__ inline int64_t round_up(int64_t n, int64_t a) { return (n + a - 1) / a * a; }
 __host__ __device__ inline int64_t ceil_div(int64_t n, int64_t a) { return (n + a - 1) / a; }
+
+// Compute units of the current device (cached).
+inline int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+      n = prop.multiProcessorCount;
+    if (n <= 0) n = 256;
+  }
+  return n;
+}
+
+// Cross-file launchers (rle.hip): the hot-path RLE tile pass on int16 zig-zag
+// blocks of 64, for callers whose transform did not fuse it.
+int rle_tile16_launch(const int16_t *blocks, int64_t nblk, int max_len, int64_t *tiles, hipStream_t s);
 
 }  // namespace hic

@@ -22,34 +22,12 @@
 // Sharding: the same kernels take a carry (zeros preceding the shard since the
 // last nonzero of earlier shards), the previous shard's last DC, and whether this
 // shard closes the stream (EOB) -- see hic_rle_stitch.
-#include "hic_common.h"
+#include "rle_core.h"
 
 namespace hic {
 namespace {
 
 constexpr int kTB = 256;  // blocks (= lanes) per tile
-
-// ---- workgroup scan helpers (256 threads = 4 waves) -------------------------
-template <typename T>
-__device__ __forceinline__ T wave_incl_sum(T v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const T o = __shfl_up(v, d, 64);
-    if (lane >= d) v += o;
-  }
-  return v;
-}
-template <typename T>
-__device__ __forceinline__ T wave_incl_max(T v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const T o = __shfl_up(v, d, 64);
-    if (lane >= d) v = v > o ? v : o;
-  }
-  return v;
-}
 
 // Exclusive sum over the workgroup; returns the exclusive prefix, sets total.
 template <typename T, int NT>
@@ -89,10 +67,6 @@ __device__ __forceinline__ T block_excl_max(T v, T ident, T *s_buf, T &all) {
   all = a;
   return excl > pre ? excl : pre;
 }
-
-// Block scan: first/last nonzero AC index (-1 if none) and the symbols of every
-// nonzero after the first (runs inside the block).
-__device__ __forceinline__ int syms_for_run(int64_t run, int M) { return 1 + (M > 0 ? (int)(run / M) : 0); }
 
 // Element j (0 <= j < A) of block b lives at blocks[b*L + off + j]; its global
 // stream position is b*A + j and only positions < n_ac exist.
@@ -170,45 +144,91 @@ __global__ __launch_bounds__(kTB) void k_rle_tile(const T *__restrict__ blocks, 
   }
 }
 
-// K2: single workgroup of 1024 threads.  Produces per tile: [3] symbol offset,
-// [4] global position of the last nonzero before the tile (virtual -1-carry if
+// K2: single workgroup of 1024 threads.  Produces per tile: [0] symbol offset,
+// [1] global position of the last nonzero before the tile (virtual -1-carry if
 // none).  Writes the EOB symbol and the count.
+// Each thread folds kScanK consecutive tile records in registers, one
+// workgroup-wide exclusive scan combines the per-thread aggregates, and each
+// thread walks its tiles again to write their offsets.  The aggregate of a run
+// of tiles is itself a tile record {first, last, count except the first
+// nonzero's symbols}; combining A then B adds B's first-nonzero symbols, whose
+// run starts after A's last nonzero.
 constexpr int kScanT = 1024;
+constexpr int kScanK = 8;  // tiles per thread per pass
+
+struct Agg {
+  int64_t first, last, cnt;
+};
+__device__ __forceinline__ Agg agg_combine(const Agg &A, const Agg &B, int M) {
+  if (B.last < 0) return A;
+  if (A.last < 0) return B;
+  return Agg{A.first, B.last, A.cnt + B.cnt + syms_for_run(B.first - A.last - 1, M)};
+}
+__device__ __forceinline__ Agg agg_shfl_up(const Agg &a, int d) {
+  return Agg{__shfl_up(a.first, d, 64), __shfl_up(a.last, d, 64), __shfl_up(a.cnt, d, 64)};
+}
+
 template <typename L_T, typename V_T>
-__global__ __launch_bounds__(kScanT) void k_rle_scan(int64_t *__restrict__ tiles, int64_t *__restrict__ offs,
+__device__ __forceinline__ void scan_tiles(const int64_t *__restrict__ tiles, int64_t *__restrict__ offs,
                                                      int64_t ntiles, int64_t n_ac, int M,
                                                      const int64_t *__restrict__ stitch, L_T *__restrict__ sym_len,
                                                      V_T *__restrict__ sym_val, int64_t cap,
-                                                     int64_t *__restrict__ d_count) {
-  __shared__ int64_t s_buf[32];
+                                                     int64_t *__restrict__ d_count, Agg *s_wave_buf) {
+  Agg *s_wave = s_wave_buf;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t carry = stitch ? stitch[0] : 0;
   const bool emit_eob = stitch ? stitch[1] != 0 : true;
-  int64_t run_prev = -1 - carry;  // running "last nonzero" before the chunk
-  int64_t run_off = 0;
-  for (int64_t c0 = 0; c0 < ntiles; c0 += kScanT) {
-    const int64_t t = c0 + threadIdx.x;
-    int64_t first = -1, last = -1, nsym = 0;
-    if (t < ntiles) {
-      first = tiles[t * 3 + 0];
-      last = tiles[t * 3 + 1];
-      nsym = tiles[t * 3 + 2];
+  const int64_t p0 = -1 - carry;  // virtual last nonzero before the stream
+  Agg run{-1, -1, 0};             // aggregate of all tiles of earlier passes
+  for (int64_t c0 = 0; c0 < ntiles; c0 += (int64_t)kScanT * kScanK) {
+    const int64_t t0 = c0 + (int64_t)threadIdx.x * kScanK;
+    Agg rec[kScanK];
+#pragma unroll
+    for (int k = 0; k < kScanK; ++k) {
+      const int64_t t = t0 + k;
+      rec[k] = t < ntiles ? Agg{tiles[t * 3 + 0], tiles[t * 3 + 1], tiles[t * 3 + 2]} : Agg{-1, -1, 0};
     }
-    int64_t chunk_last;
-    int64_t prev = block_excl_max<int64_t, kScanT>(last, (int64_t)-1, s_buf, chunk_last);
-    if (prev < 0) prev = run_prev;
-    int64_t cnt = nsym + (first >= 0 ? syms_for_run(first - prev - 1, M) : 0);
-    int64_t chunk_total;
-    const int64_t off = run_off + block_excl_sum<int64_t, kScanT>(cnt, s_buf, chunk_total);
-    if (t < ntiles) {
-      offs[t * 2 + 0] = off;
-      offs[t * 2 + 1] = prev;
+    Agg mine = rec[0];
+#pragma unroll
+    for (int k = 1; k < kScanK; ++k) mine = agg_combine(mine, rec[k], M);
+    // workgroup-wide inclusive scan of the per-thread aggregates
+    Agg incl = mine;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const Agg o = agg_shfl_up(incl, d);
+      if (lane >= d) incl = agg_combine(o, incl, M);
     }
-    if (chunk_last >= 0) run_prev = chunk_last;
-    run_off += chunk_total;
+    if (lane == 63) s_wave[wave] = incl;
+    __syncthreads();
+    Agg excl = agg_shfl_up(incl, 1);
+    if (lane == 0) excl = Agg{-1, -1, 0};
+    Agg pre = run;
+    for (int w = 0; w < wave; ++w) pre = agg_combine(pre, s_wave[w], M);
+    excl = agg_combine(pre, excl, M);
+    Agg all = run;
+    for (int w = 0; w < kScanT / 64; ++w) all = agg_combine(all, s_wave[w], M);
+    __syncthreads();
+    // state entering this thread's first tile
+    int64_t prev = excl.last >= 0 ? excl.last : p0;
+    int64_t off = excl.last >= 0 ? excl.cnt + syms_for_run(excl.first - p0 - 1, M) : 0;
+#pragma unroll
+    for (int k = 0; k < kScanK; ++k) {
+      const int64_t t = t0 + k;
+      if (t < ntiles) {
+        offs[t * 2 + 0] = off;
+        offs[t * 2 + 1] = prev;
+        if (rec[k].last >= 0) {
+          off += rec[k].cnt + syms_for_run(rec[k].first - prev - 1, M);
+          prev = rec[k].last;
+        }
+      }
+    }
+    run = all;
   }
   if (threadIdx.x == 0) {
-    const bool ends_nonzero = n_ac > 0 && run_prev == n_ac - 1;
-    int64_t total = run_off;
+    const int64_t last = run.last >= 0 ? run.last : p0;
+    const bool ends_nonzero = n_ac > 0 && last == n_ac - 1;
+    int64_t total = run.last >= 0 ? run.cnt + syms_for_run(run.first - p0 - 1, M) : 0;
     if (emit_eob && !ends_nonzero) {
       if (total < cap) {
         sym_len[total] = 0;
@@ -218,6 +238,16 @@ __global__ __launch_bounds__(kScanT) void k_rle_scan(int64_t *__restrict__ tiles
     }
     *d_count = total <= cap ? total : -total;
   }
+}
+
+template <typename L_T, typename V_T>
+__global__ __launch_bounds__(kScanT) void k_rle_scan(const int64_t *__restrict__ tiles, int64_t *__restrict__ offs,
+                                                     int64_t ntiles, int64_t n_ac, int M,
+                                                     const int64_t *__restrict__ stitch, L_T *__restrict__ sym_len,
+                                                     V_T *__restrict__ sym_val, int64_t cap,
+                                                     int64_t *__restrict__ d_count) {
+  __shared__ Agg s_wave[kScanT / 64];
+  scan_tiles<L_T, V_T>(tiles, offs, ntiles, n_ac, M, stitch, sym_len, sym_val, cap, d_count, s_wave);
 }
 
 // K3: emit symbols (+ DC differences when dc_diff != nullptr).
@@ -305,7 +335,7 @@ __global__ __launch_bounds__(kTB) void k_rle_emit(const T *__restrict__ blocks, 
         if (v == 0) continue;
         int64_t run = base + j - p - 1;
         if (M > 0) {
-          const int64_t nf = run / M;
+          const int64_t nf = div_run(run, M);
           if (!staged && nf > 32) {
             // long carried-in run: the whole workgroup writes the fillers
             const int slot = atomicAdd(&s_nfill, 1);
@@ -347,154 +377,96 @@ __global__ __launch_bounds__(kTB) void k_rle_emit(const T *__restrict__ blocks, 
 }
 
 // ---------------------------------------------------------------------------
-// Hot path: int16 zig-zag blocks of 64 (the DCT kernel's output), AC = slots 1..63.
-// The block stays in registers (8 x 16-byte loads); runs inside a block are int32;
-// MF = 15 specialises the run / max_len division (the jpeg_encode default).
-__device__ __forceinline__ int zz_ac(const uint32_t (&w)[32], int j) {
-  const int s = j + 1;
-  return (int)(int16_t)((w[s >> 1] >> (16 * (s & 1))) & 0xFFFFu);
-}
-
-__device__ __forceinline__ void load_block16(const int16_t *__restrict__ blocks, int64_t b, uint32_t (&w)[32]) {
-  const uint4 *q = reinterpret_cast<const uint4 *>(blocks + b * 64);
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const uint4 t = q[k];
-    w[4 * k] = t.x; w[4 * k + 1] = t.y; w[4 * k + 2] = t.z; w[4 * k + 3] = t.w;
-  }
-}
-
+// Hot path (rle_core.h geometry): one tile per wave, no workgroup barriers.
 template <int MF>
-__device__ __forceinline__ int div_m(int run, int M) {
-  return MF == 15 ? (int)(((uint32_t)run * 0x8889u) >> 19) : run / M;  // exact for run < 2^16
-}
-
-template <int MF>
-__device__ __forceinline__ void summarize16(const uint32_t (&w)[32], int M, int &first, int &last, int &nsym) {
-  first = -1;
-  last = -1;
-  nsym = 0;
-#pragma unroll
-  for (int j = 0; j < 63; ++j) {
-    if (zz_ac(w, j) != 0) {
-      if (first >= 0) nsym += 1 + div_m<MF>(j - last - 1, M);
-      first = first < 0 ? j : first;
-      last = j;
-    }
-  }
-}
-
-template <int MF>
-__global__ __launch_bounds__(kTB) void k_rle_tile16(const int16_t *__restrict__ blocks, int64_t nblk, int M,
+__global__ __launch_bounds__(256) void k_rle_tile16(const int16_t *__restrict__ blocks, int64_t nblk, int M,
                                                     int64_t *__restrict__ tiles) {
-  __shared__ int64_t s_buf[8];
-  const int64_t b = (int64_t)blockIdx.x * kTB + threadIdx.x;
-  int first = -1, last = -1, nsym = 0;
-  if (b < nblk) {
-    uint32_t w[32];
-    load_block16(blocks, b, w);
-    summarize16<MF>(w, M, first, last, nsym);
-  }
-  const int64_t base = b * 63;
-  const int64_t lastg = last >= 0 ? base + last : -1;
-  int64_t all_last;
-  const int64_t prev = block_excl_max<int64_t, kTB>(lastg, (int64_t)-1, s_buf, all_last);
-  int64_t cnt = nsym;
-  if (first >= 0 && prev >= 0) cnt += syms_for_run(base + first - prev - 1, M);
-  int64_t total;
-  block_excl_sum<int64_t, kTB>(cnt, s_buf, total);
-  if (first >= 0 && prev < 0) tiles[blockIdx.x * 3 + 0] = base + first;
-  if (threadIdx.x == 0) {
-    tiles[blockIdx.x * 3 + 1] = all_last;
-    tiles[blockIdx.x * 3 + 2] = total;
-    if (all_last < 0) tiles[blockIdx.x * 3 + 0] = -1;
-  }
+  const int64_t tw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t b = tw * kWT + (threadIdx.x & 63);
+  uint32_t w[32];
+  if (b < nblk) load_block16(blocks, b, w);
+  tile_record16<MF>(w, b < nblk, b, M, tiles + tw * 3);
 }
 
+// Symbols of one tile.  Each lane writes its block's symbols into the wave's LDS
+// stage at their tile-relative positions, then the wave copies the contiguous
+// range out with aligned 4-byte stores.  A tile with more symbols than the stage
+// (a nonzero after >~960 carried-in zeros) writes directly, its long filler runs
+// by the whole wave.
+constexpr int kWSyms = 4096;  // staged symbols per wave (a dense tile has <= 64 * 63)
+
 template <int MF>
-__global__ __launch_bounds__(kTB) void k_rle_emit16(const int16_t *__restrict__ blocks, int64_t nblk, int M,
-                                                    const int64_t *__restrict__ offs,
-                                                    const int64_t *__restrict__ stitch, int32_t *__restrict__ dc_diff,
-                                                    uint8_t *__restrict__ sym_len, int16_t *__restrict__ sym_val,
-                                                    int64_t cap) {
-  __shared__ int64_t s_buf[8];
-  __shared__ int64_t s_fill_start[kTB];
-  __shared__ int64_t s_fill_count[kTB];
-  __shared__ int s_nfill;
-  __shared__ uint8_t s_len[kStageSyms + 4];
-  __shared__ int16_t s_val[kStageSyms + 4];
-  if (threadIdx.x == 0) s_nfill = 0;
+__device__ __forceinline__ void emit_tile16(const uint32_t (&w)[32], bool valid, int64_t b, int64_t nblk, int M,
+                                            int64_t o_tile, int64_t prev_tile, uint8_t *s_len, int16_t *s_val,
+                                            uint8_t *__restrict__ sym_len, int16_t *__restrict__ sym_val,
+                                            int64_t cap) {
   const int lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * kTB + threadIdx.x;
-  uint32_t w[32];
   int first = -1, last = -1, nsym = 0;
-  if (b < nblk) {
-    load_block16(blocks, b, w);
-    summarize16<MF>(w, M, first, last, nsym);
-  } else {
-#pragma unroll
-    for (int k = 0; k < 32; ++k) w[k] = 0;
-  }
+  if (valid) summarize16<MF>(w, M, first, last, nsym);
   const int64_t base = b * 63;
   const int64_t lastg = last >= 0 ? base + last : -1;
-  int64_t all_last;
-  int64_t prev = block_excl_max<int64_t, kTB>(lastg, (int64_t)-1, s_buf, all_last);
-  if (prev < 0) prev = offs[blockIdx.x * 2 + 1];
+  const int64_t incl = wave_incl_max(lastg);
+  int64_t prev = __shfl_up(incl, 1, 64);
+  if (lane == 0 || prev < 0) prev = prev_tile;  // no nonzero before it inside the tile
   const int64_t run0 = base + first - prev - 1;  // carried run before the first nonzero
   const int64_t cnt = nsym + (first >= 0 ? syms_for_run(run0, M) : 0);
-  int64_t total;
-  const int64_t o_tile = offs[blockIdx.x * 2 + 0];
-  const int64_t o_thr = o_tile + block_excl_sum<int64_t, kTB>(cnt, s_buf, total);
-  const bool staged = total <= kStageSyms;
+  const int64_t incl_cnt = wave_incl_sum(cnt);
+  const int64_t total = __shfl(incl_cnt, 63, 64);
+  const int64_t o_thr = o_tile + incl_cnt - cnt;
+  const bool staged = total <= kWSyms;  // uniform across the wave
   const int lo = (int)(o_tile & 3), vo = (int)(o_tile & 1);
-
-  // DC differences: the previous block's DC comes from the neighbouring lane
-  const int dc = (int)(int16_t)(w[0] & 0xFFFFu);
-  int pdc = __shfl_up(dc, 1, 64);
-  if (b < nblk) {
-    if (lane == 0 && b > 0) pdc = (int)blocks[(b - 1) * 64];
-    if (b > 0)
-      dc_diff[b] = dc - pdc;
-    else
-      dc_diff[b] = (stitch && stitch[2]) ? dc - (int)stitch[3] : dc;
-  }
-
+  int64_t nf0 = 0;  // fillers of a long carried run written by the whole wave (unstaged)
   if (first >= 0) {
     int64_t o = o_thr;
-    // first nonzero: possibly long carried-in run
     {
-      const int64_t nf = run0 / M;
-      if (!staged && nf > 32) {
-        const int slot = atomicAdd(&s_nfill, 1);
-        s_fill_start[slot] = o;
-        s_fill_count[slot] = nf;
-        o += nf;
+      const int64_t nf = div_run(run0, M);
+      const int64_t rem = run0 - nf * M;
+      if (staged) {
+        int r = (int)(o - o_tile);
+        for (int64_t k = 0; k < nf; ++k, ++r) {
+          s_len[lo + r] = (uint8_t)(M - 1);
+          s_val[vo + r] = 0;
+        }
+        s_len[lo + r] = (uint8_t)rem;
+        s_val[vo + r] = (int16_t)zz_ac(w, first);
       } else {
-        for (int64_t k = 0; k < nf; ++k, ++o)
-          put_sym<uint8_t, int16_t>(staged, o, o_tile, lo, vo, s_len, s_val, sym_len, sym_val, cap, M - 1, 0);
+        nf0 = nf;
+        if (o + nf < cap) {
+          sym_len[o + nf] = (uint8_t)rem;
+          sym_val[o + nf] = (int16_t)zz_ac(w, first);
+        }
       }
-      put_sym<uint8_t, int16_t>(staged, o, o_tile, lo, vo, s_len, s_val, sym_len, sym_val, cap, (int)(run0 - nf * M),
-                                zz_ac(w, first));
-      ++o;
+      o += nf + 1;
     }
     if (staged) {
       int r = (int)(o - o_tile);  // tile-relative output position
       int pl = first;
+      // rolled over the block's 32 dwords (uniform index: v_movrels, not memory)
+      // so the kernel's code stays small
+      typedef uint32_t v32u __attribute__((ext_vector_type(32)));
+      v32u wv;
 #pragma unroll
-      for (int j = 1; j < 63; ++j) {
-        const int v = zz_ac(w, j);
-        if (j > first && v != 0) {
-          int run = j - pl - 1;
-          const int nf = div_m<MF>(run, M);
-          for (int k = 0; k < nf; ++k, ++r) {
-            s_len[lo + r] = (uint8_t)(M - 1);
-            s_val[vo + r] = 0;
+      for (int k = 0; k < 32; ++k) wv[k] = w[k];
+#pragma unroll 1
+      for (int k = 1; k < 32; ++k) {
+        const uint32_t d = wv[k];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int j = 2 * k - 1 + h;  // AC index of slot 2k + h
+          const int v = (int)(int16_t)(h ? (d >> 16) : (d & 0xFFFFu));
+          if (j > first && v != 0) {
+            int run = j - pl - 1;
+            const int nf = div_m<MF>(run, M);
+            for (int f = 0; f < nf; ++f, ++r) {
+              s_len[lo + r] = (uint8_t)(M - 1);
+              s_val[vo + r] = 0;
+            }
+            run -= nf * M;
+            s_len[lo + r] = (uint8_t)run;
+            s_val[vo + r] = (int16_t)v;
+            ++r;
+            pl = j;
           }
-          run -= nf * M;
-          s_len[lo + r] = (uint8_t)run;
-          s_val[vo + r] = (int16_t)v;
-          ++r;
-          pl = j;
         }
       }
     } else {
@@ -519,20 +491,118 @@ __global__ __launch_bounds__(kTB) void k_rle_emit16(const int16_t *__restrict__ 
       }
     }
   }
-  __syncthreads();
+  __builtin_amdgcn_wave_barrier();
+  // the persistent caller's prefetch of its next tile must not hold the copy-out:
+  // wait for every outstanding vector-memory op here, once per tile
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (staged) {
-    copy_out<uint8_t>(s_len, lo, sym_len, o_tile, (int)total, cap);
-    copy_out<int16_t>(s_val, vo, sym_val, o_tile, (int)total, cap);
+    copy_out_wave<uint8_t>(s_len, lo, sym_len, o_tile, (int)total, cap);
+    copy_out_wave<int16_t>(s_val, vo, sym_val, o_tile, (int)total, cap);
   } else {
-    const int nfill = s_nfill;
-    for (int f = 0; f < nfill; ++f) {
-      const int64_t s0 = s_fill_start[f], nf = s_fill_count[f];
-      for (int64_t k = threadIdx.x; k < nf; k += kTB)
+    // long carried runs: the whole wave writes each lane's fillers
+    uint64_t m = __ballot(nf0 > 0);
+    while (m) {
+      const int l = __builtin_ctzll(m);
+      m &= m - 1;
+      const int64_t s0 = __shfl(o_thr, l, 64), nf = __shfl(nf0, l, 64);
+      for (int64_t k = lane; k < nf; k += 64)
         if (s0 + k < cap) {
           sym_len[s0 + k] = (uint8_t)(M - 1);
           sym_val[s0 + k] = 0;
         }
     }
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Batched hot path: the scan and the emit of up to kMaxJobs channels (e.g. Y, Cr,
+// Cb of one image) in one launch each.  The scan runs one workgroup per channel;
+// the emit's persistent waves walk the concatenated tile space of all channels.
+constexpr int kMaxJobs = 4;
+struct RleJob16 {
+  const int16_t *blocks;
+  int64_t nblk;
+  const int64_t *stitch;
+  int32_t *dc_diff;
+  uint8_t *sym_len;
+  int16_t *sym_val;
+  int64_t cap;
+  int64_t *d_count;
+  int64_t *ws;     // tile records [3 * ntiles] then offsets [2 * ntiles]
+  int64_t ntiles;
+  int64_t tile0;   // first global tile index of this job
+};
+struct RleJobs16 {
+  RleJob16 j[kMaxJobs];
+  int n;
+  int M;
+  int64_t total_tiles;
+};
+
+__global__ __launch_bounds__(kScanT) void k_rle_scan16b(RleJobs16 jobs) {
+  __shared__ Agg s_wave[kScanT / 64];
+  const RleJob16 &J = jobs.j[blockIdx.x];
+  scan_tiles<uint8_t, int16_t>(J.ws, J.ws + 3 * J.ntiles, J.ntiles, J.nblk * 63, jobs.M, J.stitch, J.sym_len,
+                               J.sym_val, J.cap, J.d_count, s_wave);
+}
+
+template <int MF>
+__global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
+  __shared__ uint8_t s_len_all[4][kWSyms + 4];
+  __shared__ int16_t s_val_all[4][kWSyms + 4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  const int M = jobs.M;
+  int64_t g = (int64_t)blockIdx.x * 4 + wv;
+  if (g >= jobs.total_tiles) return;  // wave-uniform
+  struct Next {
+    uint32_t w[32];
+    int64_t off, prev;
+    int pdc;
+  };
+  auto job_of = [&](int64_t gt) {
+    int k = 0;
+    while (k + 1 < jobs.n && gt >= jobs.j[k + 1].tile0) ++k;
+    return k;
+  };
+  auto fetch = [&](int64_t gt, Next &n) {
+    const RleJob16 &J = jobs.j[job_of(gt)];
+    const int64_t t = gt - J.tile0;
+    const int64_t b = t * kWT + lane;
+    if (b < J.nblk) {
+      load_block16(J.blocks, b, n.w);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 32; ++k) n.w[k] = 0;
+    }
+    const int64_t *offs = J.ws + 3 * J.ntiles;
+    n.off = offs[t * 2 + 0];
+    n.prev = offs[t * 2 + 1];
+    n.pdc = (lane == 0 && b > 0 && b <= J.nblk) ? (int)J.blocks[(b - 1) * 64] : 0;
+  };
+  Next cur;
+  fetch(g, cur);
+  for (;;) {
+    const int64_t gn = g + nwaves;
+    Next nxt;
+    if (gn < jobs.total_tiles) fetch(gn, nxt);
+    const RleJob16 &J = jobs.j[job_of(g)];
+    const int64_t b = (g - J.tile0) * kWT + lane;
+    // DC differences: the previous block's DC comes from the neighbouring lane
+    const int dc = (int)(int16_t)(cur.w[0] & 0xFFFFu);
+    int pdc = __shfl_up(dc, 1, 64);
+    if (lane == 0) pdc = cur.pdc;
+    if (b < J.nblk) {
+      if (b > 0)
+        J.dc_diff[b] = dc - pdc;
+      else
+        J.dc_diff[b] = (J.stitch && J.stitch[2]) ? dc - (int)J.stitch[3] : dc;
+    }
+    emit_tile16<MF>(cur.w, b < J.nblk, b, J.nblk, M, cur.off, cur.prev, s_len_all[wv], s_val_all[wv], J.sym_len,
+                    J.sym_val, J.cap);
+    if (gn >= jobs.total_tiles) break;
+    g = gn;
+    cur = nxt;
   }
 }
 
@@ -749,6 +819,49 @@ int rle_encode(const T *blocks, int64_t nblk, StreamGeo g, int M, const int64_t 
   return check_launch("k_rle_emit");
 }
 
+inline int64_t ntiles16(int64_t nblk) { return (nblk + kWT - 1) / kWT; }
+
+int launch_tile16(const int16_t *blocks, int64_t nblk, int M, int64_t *tiles, hipStream_t s) {
+  const dim3 grid((unsigned)((ntiles16(nblk) + 3) / 4));
+  if (M == 15)
+    hipLaunchKernelGGL((k_rle_tile16<15>), grid, dim3(256), 0, s, blocks, nblk, M, tiles);
+  else
+    hipLaunchKernelGGL((k_rle_tile16<0>), grid, dim3(256), 0, s, blocks, nblk, M, tiles);
+  return check_launch("k_rle_tile16");
+}
+
+// K2 + K3 of the hot path on tile records already in the workspaces (from
+// k_rle_tile16 or the fused DCT epilogue), for up to kMaxJobs channels at once.
+int encode_batch16(RleJobs16 &jobs, hipStream_t s) {
+  int64_t t0 = 0;
+  for (int k = 0; k < jobs.n; ++k) {
+    jobs.j[k].ntiles = ntiles16(jobs.j[k].nblk);
+    jobs.j[k].tile0 = t0;
+    t0 += jobs.j[k].ntiles;
+  }
+  jobs.total_tiles = t0;
+  hipLaunchKernelGGL(k_rle_scan16b, dim3((unsigned)jobs.n), dim3(kScanT), 0, s, jobs);
+  if (int e = check_launch("k_rle_scan16b")) return e;
+  // persistent: 3 workgroups (12 waves) per CU fit the 51 KB LDS stage and the registers
+  const int64_t cap = 12 * (int64_t)cu_count();
+  const int64_t waves = t0 < cap ? t0 : cap;
+  const dim3 grid((unsigned)((waves + 3) / 4));
+  if (jobs.M == 15)
+    hipLaunchKernelGGL((k_rle_emit16b<15>), grid, dim3(256), 0, s, jobs);
+  else
+    hipLaunchKernelGGL((k_rle_emit16b<0>), grid, dim3(256), 0, s, jobs);
+  return check_launch("k_rle_emit16b");
+}
+
+int encode_from_tiles16(const int16_t *blocks, int64_t nblk, int M, const int64_t *stitch, int32_t *dc_diff,
+                        uint8_t *sym_len, int16_t *sym_val, int64_t cap, int64_t *d_count, void *ws, hipStream_t s) {
+  RleJobs16 jobs{};
+  jobs.n = 1;
+  jobs.M = M;
+  jobs.j[0] = RleJob16{blocks, nblk, stitch, dc_diff, sym_len, sym_val, cap, d_count, static_cast<int64_t *>(ws), 0, 0};
+  return encode_batch16(jobs, s);
+}
+
 inline StreamGeo block_geo(int64_t nblk, int L) { return StreamGeo{L, 1, L - 1, nblk * (L - 1)}; }
 inline StreamGeo raw_geo(int64_t n) { return StreamGeo{64, 0, 64, n}; }
 
@@ -797,11 +910,19 @@ int rle_decode(const L_T *sym_len, const V_T *sym_val, int64_t nsym, const int32
 }  // namespace
 }  // namespace hic
 
+namespace hic {
+int rle_tile16_launch(const int16_t *blocks, int64_t nblk, int max_len, int64_t *tiles, hipStream_t s) {
+  if (nblk <= 0) return arg_error("nblk");
+  return launch_tile16(blocks, nblk, max_len, tiles, s);
+}
+}  // namespace hic
+
 using namespace hic;
 
 extern "C" size_t hic_rle_workspace_bytes(int64_t nblk, int block_len) {
-  (void)block_len;
-  return (size_t)(5 * ntiles_of(nblk > 0 ? nblk : 1) + 8) * sizeof(int64_t);
+  (void)block_len;  // sized for the hot path's 64-block tiles (>= the generic 256-block tiles)
+  const int64_t n = nblk > 0 ? nblk : 1;
+  return (size_t)(5 * ((n + kWT - 1) / kWT) + 8) * sizeof(int64_t);
 }
 
 extern "C" int hic_rle_shard_summary_i16(const int16_t *blocks, int64_t nblk, int block_len, void *workspace,
@@ -822,29 +943,52 @@ extern "C" int hic_rle_encode_i16(const int16_t *blocks, int64_t nblk, int block
     if (!blocks || !dc_diff || !sym_len || !sym_val || !d_count || !workspace) return arg_error("null pointer");
     if (nblk <= 0) return arg_error("nblk");
     hipStream_t s = as_stream(stream);
-    const int64_t nt = ntiles_of(nblk);
-    int64_t *tiles = static_cast<int64_t *>(workspace);
-    int64_t *offs = tiles + 3 * nt;
-    if (max_len == 15)
-      hipLaunchKernelGGL((k_rle_tile16<15>), dim3((unsigned)nt), dim3(kTB), 0, s, blocks, nblk, max_len, tiles);
-    else
-      hipLaunchKernelGGL((k_rle_tile16<0>), dim3((unsigned)nt), dim3(kTB), 0, s, blocks, nblk, max_len, tiles);
-    if (int e = check_launch("k_rle_tile16")) return e;
-    hipLaunchKernelGGL((k_rle_scan<uint8_t, int16_t>), dim3(1), dim3(kScanT), 0, s, tiles, offs, nt, nblk * 63,
-                       max_len, d_stitch, sym_len, sym_val, sym_cap, d_count);
-    if (int e = check_launch("k_rle_scan")) return e;
-    if (max_len == 15)
-      hipLaunchKernelGGL((k_rle_emit16<15>), dim3((unsigned)nt), dim3(kTB), 0, s, blocks, nblk, max_len, offs,
-                         d_stitch, dc_diff, sym_len, sym_val, sym_cap);
-    else
-      hipLaunchKernelGGL((k_rle_emit16<0>), dim3((unsigned)nt), dim3(kTB), 0, s, blocks, nblk, max_len, offs,
-                         d_stitch, dc_diff, sym_len, sym_val, sym_cap);
-    return check_launch("k_rle_emit16");
+    if (int e = launch_tile16(blocks, nblk, max_len, static_cast<int64_t *>(workspace), s)) return e;
+    return encode_from_tiles16(blocks, nblk, max_len, d_stitch, dc_diff, sym_len, sym_val, sym_cap, d_count,
+                               workspace, s);
   }
   if (block_len < 2) return arg_error("block_len");
   if (!dc_diff) return arg_error("null dc_diff");
   return rle_encode(blocks, nblk, block_geo(nblk, block_len), max_len, d_stitch, dc_diff, sym_len, sym_val, sym_cap,
                     d_count, workspace, as_stream(stream));
+}
+
+extern "C" int hic_rle_encode_i16_tiles(const int16_t *blocks, int64_t nblk, int max_len, const int64_t *d_stitch,
+                                        int32_t *dc_diff, uint8_t *sym_len, int16_t *sym_val, int64_t sym_cap,
+                                        int64_t *d_count, void *workspace, void *stream) {
+  if (!blocks || !dc_diff || !sym_len || !sym_val || !d_count || !workspace) return arg_error("null pointer");
+  if (nblk <= 0) return arg_error("nblk");
+  if (max_len < 1 || max_len > 256) return arg_error("max_len must be in [1, 256] for uint8 symbol lengths");
+  if (reinterpret_cast<uintptr_t>(blocks) & 15) return arg_error("blocks must be 16-byte aligned");
+  return encode_from_tiles16(blocks, nblk, max_len, d_stitch, dc_diff, sym_len, sym_val, sym_cap, d_count, workspace,
+                             as_stream(stream));
+}
+
+extern "C" int hic_rle_encode_i16_tiles_batch(int n, const hic_rle_job16 *jobs, int max_len, void *stream) {
+  if (n < 1 || n > kMaxJobs || !jobs) return arg_error("1 <= n <= %d jobs", kMaxJobs);
+  if (max_len < 1 || max_len > 256) return arg_error("max_len must be in [1, 256] for uint8 symbol lengths");
+  RleJobs16 J{};
+  J.n = n;
+  J.M = max_len;
+  for (int k = 0; k < n; ++k) {
+    const hic_rle_job16 &a = jobs[k];
+    if (!a.blocks || !a.dc_diff || !a.sym_len || !a.sym_val || !a.d_count || !a.workspace)
+      return arg_error("job %d: null pointer", k);
+    if (a.nblk <= 0) return arg_error("job %d: nblk", k);
+    if (reinterpret_cast<uintptr_t>(a.blocks) & 15) return arg_error("job %d: blocks must be 16-byte aligned", k);
+    J.j[k] = RleJob16{a.blocks, a.nblk, a.d_stitch, a.dc_diff, a.sym_len, a.sym_val, a.sym_cap, a.d_count,
+                      static_cast<int64_t *>(a.workspace), 0, 0};
+  }
+  return encode_batch16(J, as_stream(stream));
+}
+
+extern "C" int hic_rle_shard_summary_tiles(const int16_t *blocks, int64_t nblk, void *workspace, int64_t *d_summary,
+                                           void *stream) {
+  if (!blocks || !workspace || !d_summary) return arg_error("null pointer");
+  if (nblk <= 0) return arg_error("nblk");
+  hipLaunchKernelGGL((k_rle_summary<int16_t>), dim3(1), dim3(kTB), 0, as_stream(stream), blocks, nblk,
+                     block_geo(nblk, 64), static_cast<const int64_t *>(workspace), ntiles16(nblk), d_summary);
+  return check_launch("k_rle_summary");
 }
 
 extern "C" int hic_rle_encode_i32(const int32_t *blocks, int64_t nblk, int block_len, int max_len,

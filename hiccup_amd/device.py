@@ -57,3 +57,26 @@ def sync(stream=None):
 def to_host(t):
     sync()
     return t.cpu().numpy()
+
+
+class KernelEvents:
+    """A pair of HIP events that a *_timed entry point fills with one kernel's
+    own begin / end timestamps (hipExtLaunchKernelGGL)."""
+
+    def __init__(self):
+        require_gpu()
+        self._lib = _lib.load()
+        a, b = ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.call("hic_event_create", ctypes.byref(a))
+        _lib.call("hic_event_create", ctypes.byref(b))
+        self.start, self.stop = a, b
+
+    def elapsed_ms(self):
+        ms = ctypes.c_float()
+        _lib.call("hic_event_elapsed_ms", self.start, self.stop, ctypes.byref(ms))
+        return float(ms.value)
+
+    def __del__(self):
+        for e in (getattr(self, "start", None), getattr(self, "stop", None)):
+            if e is not None and e.value:
+                self._lib.hic_event_destroy(e)

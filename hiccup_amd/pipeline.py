@@ -5,8 +5,10 @@ half of codec.jpeg_encode (compression.py:16-39, codec.py:286-301) for one
 H x W x 3 uint8 image that already lives in HBM:
 
   1. hic_rgb_to_ycrcb420      RGB -> Y (H x W) + pyrDown'd Cr, Cb (H/2 x W/2)
-  2. hic_dct_quant_u8 x 3     8x8 DCT + quantize + zig-zag -> int16 blocks (ZIGZAG_I16)
-  3. hic_rle_encode_i16 x 3   DC DPCM + channel-wide AC RLE -> (uint8 len, int16 val)
+  2. hic_dct_quant_rle_u8 x 3 8x8 DCT + quantize + zig-zag -> int16 blocks (ZIGZAG_I16),
+                              with the RLE tile pass fused into the epilogue
+  3. hic_rle_encode_i16_tiles_batch  DC DPCM + channel-wide AC RLE of all three
+                              channels (one scan + one emit launch) -> (uint8 len, int16 val)
 
 All launches are asynchronous on one stream; buffers are allocated once.
 ``Decoder.decode`` runs the inverse chain (codec.jpeg_decode's RLE/DC/izigzag
@@ -88,32 +90,33 @@ class Encoder:
         for k in CHANNELS:
             h, w = self.shapes[k]
             p = self.planes[k]
-            if lum_events is not None and k == "lum":
-                lum_events[0].record(stream)
-            _lib.call("hic_dct_quant_u8", device.ptr(p), h, w, p.stride(0), TABLES[k], _lib.LAYOUT_ZIGZAG_I16,
-                      device.ptr(self.coef[k]), s)
-            if lum_events is not None and k == "lum":
-                lum_events[1].record(stream)
+            # DCT + quantize + zig-zag with the RLE tile pass fused into its epilogue;
+            # lum_events (device.KernelEvents) receive the kernel's own timestamps
+            ev = (lum_events.start, lum_events.stop) if (lum_events is not None and k == "lum") else (None, None)
+            _lib.call("hic_dct_quant_rle_u8", device.ptr(p), h, w, p.stride(0), TABLES[k], self.max_len,
+                      device.ptr(self.coef[k]), device.ptr(self.ws[k]), s, *ev)
 
     def shard_summaries(self, stream=None):
         """Per-channel {trailing zeros, has nonzero, first DC, last DC} (sharded encode)."""
         s = device.stream_ptr(stream)
         for i, k in enumerate(CHANNELS):
             n = self.coef[k].shape[0]
-            _lib.call("hic_rle_shard_summary_i16", device.ptr(self.coef[k]), n, 64, device.ptr(self.ws[k]),
+            _lib.call("hic_rle_shard_summary_tiles", device.ptr(self.coef[k]), n, device.ptr(self.ws[k]),
                       device.ptr(self.summaries[i]), s)
         return self.summaries
 
     def entropy(self, stream=None, stitch=None):
-        """Step 3: DC DPCM + AC RLE per channel.  stitch: None or a (3, 4) int64
-        device tensor of per-channel {carry_zeros, emit_eob, has_prev_dc, prev_dc}."""
+        """Step 3: DC DPCM + AC RLE of the three channels (one scan launch and one
+        emit launch for all three).  stitch: None or a (3, 4) int64 device tensor of
+        per-channel {carry_zeros, emit_eob, has_prev_dc, prev_dc}."""
         s = device.stream_ptr(stream)
+        jobs = (_lib.RleJob16 * 3)()
         for i, k in enumerate(CHANNELS):
-            n = self.coef[k].shape[0]
-            st = device.ptr(stitch[i]) if stitch is not None else ctypes.c_void_p(0)
-            _lib.call("hic_rle_encode_i16", device.ptr(self.coef[k]), n, 64, self.max_len, st, device.ptr(self.dc[k]),
-                      device.ptr(self.sym_len[k]), device.ptr(self.sym_val[k]), self.cap[k],
-                      device.ptr(self.counts[i:i + 1]), device.ptr(self.ws[k]), s)
+            jobs[i] = _lib.RleJob16(self.coef[k].data_ptr(), self.coef[k].shape[0],
+                                    stitch[i].data_ptr() if stitch is not None else None, self.dc[k].data_ptr(),
+                                    self.sym_len[k].data_ptr(), self.sym_val[k].data_ptr(), self.cap[k],
+                                    self.counts[i:i + 1].data_ptr(), self.ws[k].data_ptr())
+        _lib.call("hic_rle_encode_i16_tiles_batch", 3, jobs, self.max_len, s)
 
     def encode(self, rgb, stream=None, lum_events=None):
         self.transform(rgb, stream, lum_events=lum_events)

@@ -68,6 +68,23 @@ int hic_stream_sync(void *stream);
  *  plane: uint8 H x W with row pitch `stride` bytes.  out: per `layout`. */
 int hic_dct_quant_u8(const uint8_t *plane, int64_t H, int64_t W, int64_t stride, int table_id,
                      int layout, void *out, void *stream);
+/* Same, and the kernel's own begin / end timestamps are recorded into two
+ * events from hic_event_create (hipExtLaunchKernelGGL): the measurement
+ * bench.py reports as the kernel's launch duration.  Null events = untimed. */
+int hic_dct_quant_u8_timed(const uint8_t *plane, int64_t H, int64_t W, int64_t stride, int table_id,
+                           int layout, void *out, void *stream, void *ev_start, void *ev_stop);
+/* Forward transform to HIC_LAYOUT_ZIGZAG_I16 with the RLE tile pass of
+ * hic_rle_encode_i16 (its first kernel) fused into the epilogue: the per-tile
+ * records land in `rle_workspace` (hic_rle_workspace_bytes(nblk, 64) bytes).
+ * Follow with hic_rle_encode_i16_tiles (and, for a row shard, first
+ * hic_rle_shard_summary_tiles).  Events as in hic_dct_quant_u8_timed (nullable). */
+int hic_dct_quant_rle_u8(const uint8_t *plane, int64_t H, int64_t W, int64_t stride, int table_id, int max_len,
+                         int16_t *out, void *rle_workspace, void *stream, void *ev_start, void *ev_stop);
+/* Timing events (hipEvent_t handles) for the *_timed entry points. */
+int hic_event_create(void **h_event);
+int hic_event_destroy(void *event);
+/* Milliseconds between two completed events (synchronises on `stop`). */
+int hic_event_elapsed_ms(void *start, void *stop, float *h_ms);
 
 /* ---- inverse transform: replaces transform.inv_dct_channel (transform.py:169-179) =
  *      split (:174), invert_jpeg_quantize q*T (quantization.py:55-57), idct2
@@ -147,6 +164,28 @@ int hic_rle_encode_i16(const int16_t *blocks, int64_t nblk, int block_len, int m
                        const int64_t *d_stitch, int32_t *dc_diff, uint8_t *sym_len,
                        int16_t *sym_val, int64_t sym_cap, int64_t *d_count, void *workspace,
                        void *stream);
+/* hic_rle_encode_i16 for int16 zig-zag blocks of 64 whose tile records are already
+ * in `workspace` (hic_dct_quant_rle_u8): runs only the scan and emit kernels. */
+int hic_rle_encode_i16_tiles(const int16_t *blocks, int64_t nblk, int max_len, const int64_t *d_stitch,
+                             int32_t *dc_diff, uint8_t *sym_len, int16_t *sym_val, int64_t sym_cap,
+                             int64_t *d_count, void *workspace, void *stream);
+/* hic_rle_encode_i16_tiles for up to 4 streams (e.g. the Y, Cr, Cb planes of one
+ * image) in two launches in total; all with the same max_len. */
+typedef struct {
+  const int16_t *blocks;
+  int64_t nblk;
+  const int64_t *d_stitch;
+  int32_t *dc_diff;
+  uint8_t *sym_len;
+  int16_t *sym_val;
+  int64_t sym_cap;
+  int64_t *d_count;
+  void *workspace;
+} hic_rle_job16;
+int hic_rle_encode_i16_tiles_batch(int n, const hic_rle_job16 *jobs, int max_len, void *stream);
+/* hic_rle_shard_summary_i16 from the tile records of hic_dct_quant_rle_u8. */
+int hic_rle_shard_summary_tiles(const int16_t *blocks, int64_t nblk, void *workspace, int64_t *d_summary,
+                                void *stream);
 int hic_rle_shard_summary_i32(const int32_t *blocks, int64_t nblk, int block_len,
                               void *workspace, int64_t *d_summary, void *stream);
 int hic_rle_encode_i32(const int32_t *blocks, int64_t nblk, int block_len, int max_len,

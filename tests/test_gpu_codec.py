@@ -65,6 +65,37 @@ def test_rle_long_carried_runs():
     assert [r.length for r in rl1] == L1.tolist() and [r.value for r in rl1] == V1.tolist()
 
 
+@pytest.mark.parametrize("max_len", [15, 4, 1])
+def test_rle_encode_i16_hot_path(max_len):
+    """hic_rle_encode_i16 on int16 zig-zag blocks of 64 (the wave-tile hot path):
+    dense tiles, sparse tiles, all-zero stretches and a dense tile after a long
+    carried run (the unstaged path with wave-cooperative fillers)."""
+    rng = np.random.default_rng(max_len)
+    nblk = 64 * 40 + 17
+    blocks = rng.integers(-40, 41, (nblk, 64)).astype(np.int16)
+    blocks[64:200] *= (rng.random((136, 64)) < 0.05)            # sparse
+    blocks[300:700, 1:] = 0                                      # long zero stretch (AC only)
+    blocks[900:1000] = 0
+    blocks[1000:1064] = rng.integers(1, 9, (64, 64))             # dense tile after 100 zero blocks
+    blocks[2000:2100, 5:] = 0
+    nb = blocks.shape[0]
+    ws = device.workspace(_lib.load().hic_rle_workspace_bytes(nb, 64))
+    d_blocks = device.to_device(blocks)
+    cap = nb * 63 + 1
+    L = device.empty((cap,), torch.uint8)
+    V = device.empty((cap,), torch.int16)
+    dc = device.empty((nb,), torch.int32)
+    cnt = device.zeros((1,), torch.int64)
+    import ctypes
+    _lib.call("hic_rle_encode_i16", device.ptr(d_blocks), nb, 64, max_len, ctypes.c_void_p(0), device.ptr(dc),
+              device.ptr(L), device.ptr(V), cap, device.ptr(cnt), device.ptr(ws), device.stream_ptr())
+    n = int(device.to_host(cnt)[0])
+    eL, eV = orc.rle_encode(blocks[:, 1:].reshape(-1).astype(np.int64), max_len)
+    np.testing.assert_array_equal(device.to_host(L)[:n].astype(np.int64), eL)
+    np.testing.assert_array_equal(device.to_host(V)[:n].astype(np.int64), eV)
+    np.testing.assert_array_equal(device.to_host(dc), orc.dpcm(blocks[:, 0].astype(np.int64)))
+
+
 def test_jpeg_encode_golden(golden_codec):
     g = golden_codec
     for name in _names(g, "bs_"):
@@ -109,9 +140,16 @@ def test_encode_channel_lenna(golden_lenna):
     np.testing.assert_array_equal(V, g["acv_y256"])
 
 
-def test_colour_kernels_vs_restatement():
+COLOUR_SHAPES = ((64, 64), (37, 50), (130, 258), (2, 2), (3, 7), (1080, 1920), (4, 4), (5, 4), (9, 8), (2, 8),
+                 (33, 252), (35, 500), (71, 996), (64, 7680))
+
+
+@pytest.mark.parametrize("variant", [{}, {"HIC_COLOR_SEG": "16"}, {"HIC_COLOR_TILED": "1"}])
+def test_colour_kernels_vs_restatement(variant, monkeypatch):
+    for k, v in variant.items():
+        monkeypatch.setenv(k, v)
     rng = np.random.default_rng(8)
-    for H, W in ((64, 64), (37, 50), (130, 258), (2, 2), (3, 7), (1080, 1920)):
+    for H, W in COLOUR_SHAPES:
         rgb = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
         y, cr, cb = compression.ycrcb420_device(device.to_device(rgb))
         ry, rcr, rcb = orcc.rgb_to_ycrcb(rgb)

@@ -22,6 +22,9 @@
 // Sharding: the same kernels take a carry (zeros preceding the shard since the
 // last nonzero of earlier shards), the previous shard's last DC, and whether this
 // shard closes the stream (EOB) -- see hic_rle_stitch.
+#include <atomic>
+#include <climits>
+
 #include "rle_core.h"
 
 namespace hic {
@@ -156,6 +159,27 @@ __global__ __launch_bounds__(kTB) void k_rle_tile(const T *__restrict__ blocks, 
 constexpr int kScanT = 1024;
 constexpr int kScanK = 8;  // tiles per thread per pass
 
+// Phase timestamps for the dev harness (tools/micro/scan_stamps.hip); compiled out
+// of the library.
+#ifdef HIC_STAMPS
+__device__ unsigned long long g_stamps[64];
+#define HIC_STAMP(i) \
+  if (threadIdx.x == 0 && blockIdx.x == 0) g_stamps[i] = __builtin_amdgcn_s_memtime()
+__device__ unsigned long long g_phase[16];
+__device__ unsigned long long g_tphase[1 << 16][8];  // per tile, per phase (no contention)
+#define HIC_PHASE_BEGIN unsigned long long hic_t0 = __builtin_amdgcn_s_memtime()
+#define HIC_PHASE(i)                                                          \
+  do {                                                                        \
+    const unsigned long long hic_t1 = __builtin_amdgcn_s_memtime();          \
+    if ((threadIdx.x & 63) == 0) g_tphase[(b / 64) & 0xFFFF][i] = hic_t1 - hic_t0; \
+    hic_t0 = hic_t1;                                                          \
+  } while (0)
+#else
+#define HIC_STAMP(i)
+#define HIC_PHASE_BEGIN
+#define HIC_PHASE(i)
+#endif
+
 struct Agg {
   int64_t first, last, cnt;
 };
@@ -180,6 +204,7 @@ __device__ __forceinline__ void scan_tiles(const int64_t *__restrict__ tiles, in
   const bool emit_eob = stitch ? stitch[1] != 0 : true;
   const int64_t p0 = -1 - carry;  // virtual last nonzero before the stream
   Agg run{-1, -1, 0};             // aggregate of all tiles of earlier passes
+  HIC_STAMP(0);
   for (int64_t c0 = 0; c0 < ntiles; c0 += (int64_t)kScanT * kScanK) {
     const int64_t t0 = c0 + (int64_t)threadIdx.x * kScanK;
     Agg rec[kScanK];
@@ -191,6 +216,7 @@ __device__ __forceinline__ void scan_tiles(const int64_t *__restrict__ tiles, in
     Agg mine = rec[0];
 #pragma unroll
     for (int k = 1; k < kScanK; ++k) mine = agg_combine(mine, rec[k], M);
+    HIC_STAMP(1);
     // workgroup-wide inclusive scan of the per-thread aggregates
     Agg incl = mine;
 #pragma unroll
@@ -198,16 +224,33 @@ __device__ __forceinline__ void scan_tiles(const int64_t *__restrict__ tiles, in
       const Agg o = agg_shfl_up(incl, d);
       if (lane >= d) incl = agg_combine(o, incl, M);
     }
+    HIC_STAMP(2);
     if (lane == 63) s_wave[wave] = incl;
+    __syncthreads();
+    HIC_STAMP(3);
+    // wave 0 scans the 16 wave totals (exclusive) in place; lane 15 also forms the
+    // aggregate of everything so far
+    if (wave == 0) {
+      constexpr int NW = kScanT / 64;
+      Agg t = lane < NW ? s_wave[lane] : Agg{-1, -1, 0};
+      Agg it = t;
+#pragma unroll
+      for (int d = 1; d < NW; d <<= 1) {
+        const Agg o = agg_shfl_up(it, d);
+        if (lane >= d) it = agg_combine(o, it, M);
+      }
+      Agg ex = agg_shfl_up(it, 1);
+      if (lane == 0) ex = Agg{-1, -1, 0};
+      if (lane < NW) s_wave[lane] = agg_combine(run, ex, M);
+      if (lane == NW - 1) s_wave[NW] = agg_combine(run, it, M);
+    }
     __syncthreads();
     Agg excl = agg_shfl_up(incl, 1);
     if (lane == 0) excl = Agg{-1, -1, 0};
-    Agg pre = run;
-    for (int w = 0; w < wave; ++w) pre = agg_combine(pre, s_wave[w], M);
-    excl = agg_combine(pre, excl, M);
-    Agg all = run;
-    for (int w = 0; w < kScanT / 64; ++w) all = agg_combine(all, s_wave[w], M);
+    excl = agg_combine(s_wave[wave], excl, M);
+    const Agg all = s_wave[kScanT / 64];
     __syncthreads();
+    HIC_STAMP(4);
     // state entering this thread's first tile
     int64_t prev = excl.last >= 0 ? excl.last : p0;
     int64_t off = excl.last >= 0 ? excl.cnt + syms_for_run(excl.first - p0 - 1, M) : 0;
@@ -224,6 +267,7 @@ __device__ __forceinline__ void scan_tiles(const int64_t *__restrict__ tiles, in
       }
     }
     run = all;
+    HIC_STAMP(5);
   }
   if (threadIdx.x == 0) {
     const int64_t last = run.last >= 0 ? run.last : p0;
@@ -246,7 +290,7 @@ __global__ __launch_bounds__(kScanT) void k_rle_scan(const int64_t *__restrict__
                                                      const int64_t *__restrict__ stitch, L_T *__restrict__ sym_len,
                                                      V_T *__restrict__ sym_val, int64_t cap,
                                                      int64_t *__restrict__ d_count) {
-  __shared__ Agg s_wave[kScanT / 64];
+  __shared__ Agg s_wave[kScanT / 64 + 1];
   scan_tiles<L_T, V_T>(tiles, offs, ntiles, n_ac, M, stitch, sym_len, sym_val, cap, d_count, s_wave);
 }
 
@@ -396,25 +440,33 @@ __global__ __launch_bounds__(256) void k_rle_tile16(const int16_t *__restrict__ 
 constexpr int kWSyms = 4096;  // staged symbols per wave (a dense tile has <= 64 * 63)
 
 template <int MF>
-__device__ __forceinline__ void emit_tile16(const uint32_t (&w)[32], bool valid, int64_t b, int64_t nblk, int M,
-                                            int64_t o_tile, int64_t prev_tile, uint8_t *s_len, int16_t *s_val,
-                                            uint8_t *__restrict__ sym_len, int16_t *__restrict__ sym_val,
-                                            int64_t cap) {
+// w: this lane's block in registers; blk: the same block in global memory, read
+// for lane-varying coefficient indices (keeps w out of scratch).
+__device__ __forceinline__ void emit_tile16(const uint32_t (&w)[32], const int16_t *__restrict__ blk, bool valid,
+                                            int64_t b, int64_t nblk, int M, int64_t o_tile, int64_t prev_tile,
+                                            uint8_t *s_len, int16_t *s_val, uint8_t *__restrict__ sym_len,
+                                            int16_t *__restrict__ sym_val, int64_t cap) {
   const int lane = threadIdx.x & 63;
+  HIC_PHASE_BEGIN;
   int first = -1, last = -1, nsym = 0;
-  if (valid) summarize16<MF>(w, M, first, last, nsym);
+  uint64_t ac = 0;
+  if (valid) summarize16<MF>(w, M, first, last, nsym, &ac);
+  HIC_PHASE(1);
   const int64_t base = b * 63;
-  const int64_t lastg = last >= 0 ? base + last : -1;
-  const int64_t incl = wave_incl_max(lastg);
-  int64_t prev = __shfl_up(incl, 1, 64);
-  if (lane == 0 || prev < 0) prev = prev_tile;  // no nonzero before it inside the tile
+  // in-tile positions (lane * 63 + j) and counts fit int32: DPP scans
+  const int incl = wave_incl_max_i32(last >= 0 ? lane * 63 + last : -1);
+  const int prevr = wave_shr1_i32(-1, incl);
+  // no nonzero before it inside the tile: the tile's carried-in predecessor
+  const int64_t prev = prevr >= 0 ? (b - lane) * 63 + prevr : prev_tile;
   const int64_t run0 = base + first - prev - 1;  // carried run before the first nonzero
-  const int64_t cnt = nsym + (first >= 0 ? syms_for_run(run0, M) : 0);
-  const int64_t incl_cnt = wave_incl_sum(cnt);
-  const int64_t total = __shfl(incl_cnt, 63, 64);
+  const int cnt = nsym + (first >= 0 ? syms_for_run(run0, M) : 0);
+  const int incl_cnt = wave_incl_sum_i32(cnt);
+  const int total = wave_last_i32(incl_cnt);
   const int64_t o_thr = o_tile + incl_cnt - cnt;
+  HIC_PHASE(2);
   const bool staged = total <= kWSyms;  // uniform across the wave
-  const int lo = (int)(o_tile & 3), vo = (int)(o_tile & 1);
+  // stage offsets congruent to the output position mod 16 bytes (16-byte copy-out)
+  const int lo = (int)(o_tile & 15), vo = (int)(o_tile & 7);
   int64_t nf0 = 0;  // fillers of a long carried run written by the whole wave (unstaged)
   if (first >= 0) {
     int64_t o = o_thr;
@@ -428,52 +480,55 @@ __device__ __forceinline__ void emit_tile16(const uint32_t (&w)[32], bool valid,
           s_val[vo + r] = 0;
         }
         s_len[lo + r] = (uint8_t)rem;
-        s_val[vo + r] = (int16_t)zz_ac(w, first);
+        s_val[vo + r] = blk[1 + first];
       } else {
         nf0 = nf;
         if (o + nf < cap) {
           sym_len[o + nf] = (uint8_t)rem;
-          sym_val[o + nf] = (int16_t)zz_ac(w, first);
+          sym_val[o + nf] = blk[1 + first];
         }
       }
       o += nf + 1;
     }
-    if (staged) {
+    if (staged && nsym == __builtin_popcountll(ac) - 1) {
+      // no run inside the block reaches max_len (the dense case): one symbol per
+      // nonzero after the first, branch-free -- a zero coefficient writes to the
+      // stage's dummy slot and does not advance r
+      int r = (int)(o - o_tile) + lo;  // stage index of the next symbol (len array)
+      const int dv = vo - lo;          // val index = len index + dv
+      int pl = first;
+#pragma unroll
+      for (int j = 1; j < 63; ++j) {
+        const int v = zz_ac(w, j);
+        const bool nz = (v != 0) & (j > first);
+        s_len[nz ? r : kWSyms + 16] = (uint8_t)(j - pl - 1);  // dummy slots lie past every
+        s_val[nz ? r + dv : kWSyms + 24] = (int16_t)v;         // real one (lo, vo < 16)
+        r += nz ? 1 : 0;
+        pl = nz ? j : pl;
+      }
+    } else if (staged) {
       int r = (int)(o - o_tile);  // tile-relative output position
       int pl = first;
-      // rolled over the block's 32 dwords (uniform index: v_movrels, not memory)
-      // so the kernel's code stays small
-      typedef uint32_t v32u __attribute__((ext_vector_type(32)));
-      v32u wv;
-#pragma unroll
-      for (int k = 0; k < 32; ++k) wv[k] = w[k];
-#pragma unroll 1
-      for (int k = 1; k < 32; ++k) {
-        const uint32_t d = wv[k];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int j = 2 * k - 1 + h;  // AC index of slot 2k + h
-          const int v = (int)(int16_t)(h ? (d >> 16) : (d & 0xFFFFu));
-          if (j > first && v != 0) {
-            int run = j - pl - 1;
-            const int nf = div_m<MF>(run, M);
-            for (int f = 0; f < nf; ++f, ++r) {
-              s_len[lo + r] = (uint8_t)(M - 1);
-              s_val[vo + r] = 0;
-            }
-            run -= nf * M;
-            s_len[lo + r] = (uint8_t)run;
-            s_val[vo + r] = (int16_t)v;
-            ++r;
-            pl = j;
-          }
+      for (uint64_t m = ac & (ac - 1); m; m &= m - 1) {  // nonzeros after the first
+        const int j = __builtin_ctzll(m);
+        const int v = blk[1 + j];
+        int run = j - pl - 1;
+        const int nf = div_m<MF>(run, M);
+        for (int f = 0; f < nf; ++f, ++r) {
+          s_len[lo + r] = (uint8_t)(M - 1);
+          s_val[vo + r] = 0;
         }
+        run -= nf * M;
+        s_len[lo + r] = (uint8_t)run;
+        s_val[vo + r] = (int16_t)v;
+        ++r;
+        pl = j;
       }
     } else {
       int pl = first;
-      for (int j = first + 1; j <= last; ++j) {
-        const int v = zz_ac(w, j);
-        if (v == 0) continue;
+      for (uint64_t m = ac & (ac - 1); m; m &= m - 1) {
+        const int j = __builtin_ctzll(m);
+        const int v = blk[1 + j];
         int run = j - pl - 1;
         const int nf = run / M;
         for (int k = 0; k < nf; ++k, ++o)
@@ -492,12 +547,15 @@ __device__ __forceinline__ void emit_tile16(const uint32_t (&w)[32], bool valid,
     }
   }
   __builtin_amdgcn_wave_barrier();
+  HIC_PHASE(3);
   // the persistent caller's prefetch of its next tile must not hold the copy-out:
   // wait for every outstanding vector-memory op here, once per tile
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  HIC_PHASE(4);
   if (staged) {
-    copy_out_wave<uint8_t>(s_len, lo, sym_len, o_tile, (int)total, cap);
-    copy_out_wave<int16_t>(s_val, vo, sym_val, o_tile, (int)total, cap);
+    copy_out_wave16<uint8_t>(s_len, lo, sym_len, o_tile, (int)total, cap);
+    copy_out_wave16<int16_t>(s_val, vo, sym_val, o_tile, (int)total, cap);
+    HIC_PHASE(5);
   } else {
     // long carried runs: the whole wave writes each lane's fillers
     uint64_t m = __ballot(nf0 > 0);
@@ -539,17 +597,130 @@ struct RleJobs16 {
   int64_t total_tiles;
 };
 
-__global__ __launch_bounds__(kScanT) void k_rle_scan16b(RleJobs16 jobs) {
-  __shared__ Agg s_wave[kScanT / 64];
-  const RleJob16 &J = jobs.j[blockIdx.x];
-  scan_tiles<uint8_t, int16_t>(J.ws, J.ws + 3 * J.ntiles, J.ntiles, J.nblk * 63, jobs.M, J.stitch, J.sym_len,
-                               J.sym_val, J.cap, J.d_count, s_wave);
+// Multi-workgroup scan for the batched hot path: each channel's tiles are cut
+// into partitions of kScanT tiles, one workgroup per partition (all resident at
+// once: a few dozen workgroups).  A partition reduces its tiles, publishes the
+// aggregate as three tagged 8-byte granules {value, epoch tag} (sc1 stores:
+// MI355X_MICROARCH.md, granule hand-off; no fences), polls the granules of every
+// earlier partition of its channel (sc1 loads) and folds them, then scans its
+// own tiles (one tile per thread, coalesced record loads and offset stores).
+// The epoch is unique per launch, so stale granules never match; a bounded spin
+// reports failure through d_count instead of hanging.
+__device__ __forceinline__ void put_granule(uint64_t *g, int64_t v, uint32_t tag) {
+  __hip_atomic_store(g, (uint64_t)(uint32_t)(int32_t)v | ((uint64_t)tag << 32), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool get_granule(const uint64_t *g, uint32_t tag, int64_t &v) {
+  const uint64_t x = __hip_atomic_load(const_cast<uint64_t *>(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  v = (int64_t)(int32_t)(uint32_t)x;
+  return (uint32_t)(x >> 32) == tag;
+}
+
+__global__ __launch_bounds__(kScanT) void k_rle_scan16b(RleJobs16 jobs, uint32_t epoch) {
+  __shared__ Agg s_wave[kScanT / 64 + 1];
+  __shared__ Agg s_pre;
+  __shared__ int s_fail;
+  // workgroup -> (job, partition)
+  int jb = 0;
+  int64_t p = blockIdx.x;
+  while (jb + 1 < jobs.n && p >= (jobs.j[jb].ntiles + kScanT - 1) / kScanT) {
+    p -= (jobs.j[jb].ntiles + kScanT - 1) / kScanT;
+    ++jb;
+  }
+  const RleJob16 &J = jobs.j[jb];
+  const int M = jobs.M;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t nt = J.ntiles, np = (nt + kScanT - 1) / kScanT;
+  const int64_t *tiles = J.ws;
+  int64_t *offs = J.ws + 3 * nt;
+  uint64_t *gran = reinterpret_cast<uint64_t *>(J.ws + 5 * nt);  // 3 per partition
+  const uint32_t tag = (epoch << 2) | 1u;
+  const int64_t t = p * kScanT + threadIdx.x;
+  const Agg rec = t < nt ? Agg{tiles[t * 3 + 0], tiles[t * 3 + 1], tiles[t * 3 + 2]} : Agg{-1, -1, 0};
+  // workgroup inclusive scan of the partition's tile records
+  Agg incl = rec;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const Agg o = agg_shfl_up(incl, d);
+    if (lane >= d) incl = agg_combine(o, incl, M);
+  }
+  if (lane == 63) s_wave[wave] = incl;
+  if (threadIdx.x == 0) s_fail = 0;
+  __syncthreads();
+  if (wave == 0) {
+    constexpr int NW = kScanT / 64;
+    Agg it = lane < NW ? s_wave[lane] : Agg{-1, -1, 0};
+#pragma unroll
+    for (int d = 1; d < NW; d <<= 1) {
+      const Agg o = agg_shfl_up(it, d);
+      if (lane >= d) it = agg_combine(o, it, M);
+    }
+    Agg ex = agg_shfl_up(it, 1);
+    if (lane == 0) ex = Agg{-1, -1, 0};
+    if (lane < NW) s_wave[lane] = ex;
+    if (lane == NW - 1) {
+      s_wave[NW] = it;  // the partition's aggregate: publish it
+      put_granule(gran + 3 * p + 0, it.first, tag);
+      put_granule(gran + 3 * p + 1, it.last, tag);
+      put_granule(gran + 3 * p + 2, it.cnt, tag);
+    }
+    // fold the aggregates of the earlier partitions (lane q < p polls partition q)
+    Agg pre{-1, -1, 0};
+    for (int64_t q0 = 0; q0 < p; q0 += 64) {
+      const int64_t q = q0 + lane;
+      Agg a{-1, -1, 0};
+      if (q < p) {
+        bool ok = false;
+        for (int spin = 0; spin < (1 << 22) && !ok; ++spin) {
+          int64_t f, l, c;
+          ok = get_granule(gran + 3 * q + 0, tag, f) & get_granule(gran + 3 * q + 1, tag, l) &
+               get_granule(gran + 3 * q + 2, tag, c);
+          if (ok) a = Agg{f, l, c};
+          else __builtin_amdgcn_s_sleep(2);
+        }
+        if (!ok) s_fail = 1;
+      }
+      // ordered fold of this window (64 partitions at most per window; usually one)
+      for (int k = 0; k < 64 && q0 + k < p; ++k) {
+        const Agg ak{__shfl(a.first, k, 64), __shfl(a.last, k, 64), __shfl(a.cnt, k, 64)};
+        pre = agg_combine(pre, ak, M);
+      }
+    }
+    if (lane == 0) s_pre = pre;
+  }
+  __syncthreads();
+  const int64_t carry = J.stitch ? J.stitch[0] : 0;
+  const int64_t p0 = -1 - carry;  // virtual last nonzero before the stream
+  Agg excl = agg_shfl_up(incl, 1);
+  if (lane == 0) excl = Agg{-1, -1, 0};
+  excl = agg_combine(agg_combine(s_pre, s_wave[wave], M), excl, M);
+  if (t < nt) {
+    offs[t * 2 + 0] = excl.last >= 0 ? excl.cnt + syms_for_run(excl.first - p0 - 1, M) : 0;
+    offs[t * 2 + 1] = excl.last >= 0 ? excl.last : p0;
+  }
+  if (p == np - 1 && threadIdx.x == 0) {  // the channel's last partition closes the stream
+    const Agg all = agg_combine(s_pre, s_wave[kScanT / 64], M);
+    const int64_t last = all.last >= 0 ? all.last : p0;
+    const int64_t n_ac = J.nblk * 63;
+    const bool emit_eob = J.stitch ? J.stitch[1] != 0 : true;
+    int64_t total = all.last >= 0 ? all.cnt + syms_for_run(all.first - p0 - 1, M) : 0;
+    if (emit_eob && !(n_ac > 0 && last == n_ac - 1)) {
+      if (total < J.cap) {
+        J.sym_len[total] = 0;
+        J.sym_val[total] = 0;
+      }
+      ++total;
+    }
+    *J.d_count = total <= J.cap ? total : -total;
+  }
+  if (s_fail && threadIdx.x == 0) *J.d_count = INT64_MIN;  // hand-off timed out: report, do not hang
 }
 
 template <int MF>
 __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
-  __shared__ uint8_t s_len_all[4][kWSyms + 4];
-  __shared__ int16_t s_val_all[4][kWSyms + 4];
+  // per wave: kWSyms symbols + 16-byte alignment slack + the dummy slot
+  __shared__ __attribute__((aligned(16))) uint8_t s_len_all[4][kWSyms + 32];
+  __shared__ __attribute__((aligned(16))) int16_t s_val_all[4][kWSyms + 32];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   const int M = jobs.M;
@@ -598,8 +769,8 @@ __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
       else
         J.dc_diff[b] = (J.stitch && J.stitch[2]) ? dc - (int)J.stitch[3] : dc;
     }
-    emit_tile16<MF>(cur.w, b < J.nblk, b, J.nblk, M, cur.off, cur.prev, s_len_all[wv], s_val_all[wv], J.sym_len,
-                    J.sym_val, J.cap);
+    emit_tile16<MF>(cur.w, J.blocks + (b < J.nblk ? b : 0) * 64, b < J.nblk, b, J.nblk, M, cur.off, cur.prev,
+                    s_len_all[wv], s_val_all[wv], J.sym_len, J.sym_val, J.cap);
     if (gn >= jobs.total_tiles) break;
     g = gn;
     cur = nxt;
@@ -835,12 +1006,18 @@ int launch_tile16(const int16_t *blocks, int64_t nblk, int M, int64_t *tiles, hi
 int encode_batch16(RleJobs16 &jobs, hipStream_t s) {
   int64_t t0 = 0;
   for (int k = 0; k < jobs.n; ++k) {
+    // stream positions and counts travel as int32 through the scan's hand-off
+    if (jobs.j[k].nblk > (int64_t)INT32_MAX / 63) return arg_error("nblk too large (AC stream >= 2^31)");
     jobs.j[k].ntiles = ntiles16(jobs.j[k].nblk);
     jobs.j[k].tile0 = t0;
     t0 += jobs.j[k].ntiles;
   }
   jobs.total_tiles = t0;
-  hipLaunchKernelGGL(k_rle_scan16b, dim3((unsigned)jobs.n), dim3(kScanT), 0, s, jobs);
+  static std::atomic<uint32_t> epoch{0};
+  const uint32_t ep = (epoch.fetch_add(1) % ((1u << 30) - 1)) + 1;  // never 0 (zeroed workspace)
+  int64_t nparts = 0;
+  for (int k = 0; k < jobs.n; ++k) nparts += (jobs.j[k].ntiles + kScanT - 1) / kScanT;
+  hipLaunchKernelGGL(k_rle_scan16b, dim3((unsigned)nparts), dim3(kScanT), 0, s, jobs, ep);
   if (int e = check_launch("k_rle_scan16b")) return e;
   // persistent: 3 workgroups (12 waves) per CU fit the 51 KB LDS stage and the registers
   const int64_t cap = 12 * (int64_t)cu_count();
@@ -921,8 +1098,9 @@ using namespace hic;
 
 extern "C" size_t hic_rle_workspace_bytes(int64_t nblk, int block_len) {
   (void)block_len;  // sized for the hot path's 64-block tiles (>= the generic 256-block tiles)
-  const int64_t n = nblk > 0 ? nblk : 1;
-  return (size_t)(5 * ((n + kWT - 1) / kWT) + 8) * sizeof(int64_t);
+  const int64_t n = nblk > 0 ? nblk : 1, nt = (n + kWT - 1) / kWT;
+  // tile records (3), offsets (2) per tile; 3 hand-off granules per scan partition
+  return (size_t)(5 * nt + 3 * ((nt + kScanT - 1) / kScanT) + 8) * sizeof(int64_t);
 }
 
 extern "C" int hic_rle_shard_summary_i16(const int16_t *blocks, int64_t nblk, int block_len, void *workspace,

@@ -29,8 +29,36 @@ __device__ __forceinline__ T wave_incl_max(T v) {
   return v;
 }
 
-// Symbols produced by a nonzero preceded by `run` zeros: run / M fillers
-// (M-1, 0) then (run % M, value).
+// int32 wave64 inclusive scans on DPP (no LDS round trips): row_shr 1/2/4/8
+// inside each 16-lane row, then row_bcast:15 / row_bcast:31 across rows (GFX9
+// DPP).  Lanes whose DPP source is out of range read `ident`.
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ int dpp_i32(int ident, int v) {
+  return __builtin_amdgcn_update_dpp(ident, v, CTRL, ROWS, 0xF, false);
+}
+__device__ __forceinline__ int wave_incl_sum_i32(int v) {
+  v += dpp_i32<0x111>(0, v);
+  v += dpp_i32<0x112>(0, v);
+  v += dpp_i32<0x114>(0, v);
+  v += dpp_i32<0x118>(0, v);
+  v += dpp_i32<0x142, 0xA>(0, v);
+  v += dpp_i32<0x143, 0xC>(0, v);
+  return v;
+}
+__device__ __forceinline__ int wave_incl_max_i32(int v) {
+  constexpr int I = -2147483647 - 1;
+  v = max(v, dpp_i32<0x111>(I, v));
+  v = max(v, dpp_i32<0x112>(I, v));
+  v = max(v, dpp_i32<0x114>(I, v));
+  v = max(v, dpp_i32<0x118>(I, v));
+  v = max(v, dpp_i32<0x142, 0xA>(I, v));
+  v = max(v, dpp_i32<0x143, 0xC>(I, v));
+  return v;
+}
+// lane i <- lane i-1 (lane 0 <- ident)
+__device__ __forceinline__ int wave_shr1_i32(int ident, int v) { return dpp_i32<0x138>(ident, v); }
+__device__ __forceinline__ int wave_last_i32(int v) { return __builtin_amdgcn_readlane(v, 63); }
+
 // run / M without a 64-bit division (a long software sequence on the GPU): runs
 // are < 2^32 in practice; M = 15 (jpeg_encode's default) by multiply-shift.
 __device__ __attribute__((noinline)) int64_t div_run_wide(int64_t run, int M) { return run / M; }
@@ -91,8 +119,10 @@ __device__ __forceinline__ uint64_t nz_mask16(const uint32_t (&w)[32]) {
 // first / last nonzero AC index (-1 if none) and the symbols of every nonzero
 // after the first (runs inside the block), from the block's nonzero mask.
 template <int MF>
-__device__ __forceinline__ void summarize16(const uint32_t (&w)[32], int M, int &first, int &last, int &nsym) {
+__device__ __forceinline__ void summarize16(const uint32_t (&w)[32], int M, int &first, int &last, int &nsym,
+                                            uint64_t *ac_out = nullptr) {
   const uint64_t ac = nz_mask16(w) >> 1;  // bit j = AC j (slot j + 1), j = 0..62
+  if (ac_out) *ac_out = ac;
   if (ac == 0) {
     first = last = -1;
     nsym = 0;
@@ -152,18 +182,18 @@ __device__ __forceinline__ void tile_record16(const uint32_t (&w)[32], bool vali
   const int lane = threadIdx.x & 63;
   int first = -1, last = -1, nsym = 0;
   if (valid) summarize16<MF>(w, M, first, last, nsym);
-  const int64_t base = b * 63;
-  const int64_t lastg = last >= 0 ? base + last : -1;
-  const int64_t incl = wave_incl_max(lastg);
-  int64_t prev = __shfl_up(incl, 1, 64);
-  if (lane == 0) prev = -1;
-  int64_t cnt = nsym;
-  if (first >= 0 && prev >= 0) cnt += syms_for_run(base + first - prev - 1, M);
-  const int64_t total = __shfl(wave_incl_sum(cnt), 63, 64);
-  const int64_t all_last = __shfl(incl, 63, 64);
-  if (first >= 0 && prev < 0) rec[0] = base + first;
+  // positions relative to the tile's first AC element (lane * 63 + j) fit int32
+  const int lastr = last >= 0 ? lane * 63 + last : -1;
+  const int incl = wave_incl_max_i32(lastr);
+  const int prev = wave_shr1_i32(-1, incl);  // last nonzero of earlier lanes, -1: none
+  int cnt = nsym;
+  if (first >= 0 && prev >= 0) cnt += syms_for_run(lane * 63 + first - prev - 1, M);
+  const int total = wave_last_i32(wave_incl_sum_i32(cnt));
+  const int all_last = wave_last_i32(incl);
+  const int64_t base = (b - lane) * 63;  // the tile's first AC element
+  if (first >= 0 && prev < 0) rec[0] = base + lane * 63 + first;
   if (lane == 0) {
-    rec[1] = all_last;
+    rec[1] = all_last >= 0 ? base + all_last : -1;
     rec[2] = total;
     if (all_last < 0) rec[0] = -1;
   }
@@ -177,18 +207,55 @@ __device__ __forceinline__ void copy_out_wave(const T *s, int a, T *__restrict__
   constexpr int E = 4 / (int)sizeof(T);  // elements per word
   const int lane = threadIdx.x & 63;
   const int64_t w0 = o0 / E, w1 = (o0 + n + E - 1) / E;
-  for (int64_t w = w0 + lane; w < w1; w += 64) {
-    const int64_t e0 = w * E;
-    if (e0 >= o0 && e0 + E <= o0 + n && e0 + E <= cap) {
-      const int li = (int)(e0 - o0) + a;  // multiple of E
-      *reinterpret_cast<uint32_t *>(g + e0) = *reinterpret_cast<const uint32_t *>(s + li);
-    } else {
-      for (int k = 0; k < E; ++k) {
-        const int64_t e = e0 + k;
-        if (e >= o0 && e < o0 + n && e < cap) g[e] = s[(int)(e - o0) + a];
-      }
-    }
+  // whole words inside [o0, o0 + n) and below the cap: aligned 4-byte copies,
+  // four LDS reads in flight per lane
+  const int64_t i0 = (o0 + E - 1) / E;
+  int64_t i1 = (o0 + n) / E;
+  if (i1 > cap / E) i1 = cap / E;
+  if (i1 < i0) i1 = i0;
+  auto src = [&](int64_t w) { return *reinterpret_cast<const uint32_t *>(s + (int)(w * E - o0) + a); };
+  int64_t w = i0 + lane;
+  for (; w + 192 < i1; w += 256) {
+    const uint32_t v0 = src(w), v1 = src(w + 64), v2 = src(w + 128), v3 = src(w + 192);
+    *reinterpret_cast<uint32_t *>(g + w * E) = v0;
+    *reinterpret_cast<uint32_t *>(g + (w + 64) * E) = v1;
+    *reinterpret_cast<uint32_t *>(g + (w + 128) * E) = v2;
+    *reinterpret_cast<uint32_t *>(g + (w + 192) * E) = v3;
   }
+  for (; w < i1; w += 64) *reinterpret_cast<uint32_t *>(g + w * E) = src(w);
+  // partial words at either end (and any words cut by the cap): element stores
+  auto edge = [&](int64_t ew) {
+    for (int k = 0; k < E; ++k) {
+      const int64_t e = ew * E + k;
+      if (e >= o0 && e < o0 + n && e < cap) g[e] = s[(int)(e - o0) + a];
+    }
+  };
+  if (lane == 0 && w0 < i0) edge(w0);
+  for (int64_t ew = (i1 > w0 ? i1 : w0 + (w0 < i0 ? 1 : 0)) + lane; ew < w1; ew += 64) edge(ew);
+}
+
+// Copy n elements from LDS (element e at s[a + e], s 16-byte aligned) to global
+// g[o0 + e] (g 16-byte aligned), where a == o0 mod (16 / sizeof(T)): one
+// ds_read_b128 + global_store_dwordx4 per 16-byte chunk, element stores for the
+// partial chunks at either end and anything cut by the cap.
+template <typename T>
+__device__ __forceinline__ void copy_out_wave16(const T *s, int a, T *__restrict__ g, int64_t o0, int n, int64_t cap) {
+  constexpr int C = 16 / (int)sizeof(T);  // elements per chunk
+  const int lane = threadIdx.x & 63;
+  const int64_t c0 = (o0 + C - 1) / C;
+  int64_t c1 = (o0 + n) / C;
+  if (c1 > cap / C) c1 = cap / C;
+  if (c1 < c0) c1 = c0;
+  const int64_t sb = o0 - a;  // global element at s[0]
+  for (int64_t c = c0 + lane; c < c1; c += 64)
+    *reinterpret_cast<uint4 *>(g + c * C) = *reinterpret_cast<const uint4 *>(s + (int)(c * C - sb));
+  // head: [o0, c0*C); tail: [c1*C, o0+n) -- each at most C - 1 elements unless the cap cut
+  const int64_t hend = c0 * C < o0 + n ? c0 * C : o0 + n;
+  for (int64_t e = o0 + lane; e < hend; e += 64)
+    if (e < cap) g[e] = s[(int)(e - sb)];
+  const int64_t tbeg = c1 * C > hend ? c1 * C : hend;
+  for (int64_t e = tbeg + lane; e < o0 + n; e += 64)
+    if (e < cap) g[e] = s[(int)(e - sb)];
 }
 
 }  // namespace

@@ -47,7 +47,9 @@ def zeros(shape, dtype):
 
 
 def workspace(nbytes):
-    return empty((max(int(nbytes), 8) + 7) // 8, torch.int64)
+    """Zero-filled int64 scratch (the RLE scan's hand-off granules expect zeros
+    before their first use; see hic_rle_workspace_bytes)."""
+    return zeros((max(int(nbytes), 8) + 7) // 8, torch.int64)
 
 
 def sync(stream=None):

@@ -157,6 +157,8 @@ int hic_izigzag_blocks_i32(const int32_t *blocks, int64_t H, int64_t W, int N, i
  *  int64[4] = {carry_zeros, emit_eob, has_prev_dc, prev_dc}) or NULL for a whole
  *  stream {0, 1, 0, 0}.  hic_rle_shard_summary fills d_summary (device int64[4]
  *  = {trailing_zeros, has_nonzero, first_dc, last_dc}) for the exchange step. */
+/* The workspace must be zero-filled before its first use (it carries tagged
+ * hand-off records between the scan's workgroups); it may be reused after. */
 size_t hic_rle_workspace_bytes(int64_t nblk, int block_len);
 int hic_rle_shard_summary_i16(const int16_t *blocks, int64_t nblk, int block_len,
                               void *workspace, int64_t *d_summary, void *stream);

@@ -254,25 +254,29 @@ __global__ __launch_bounds__(256) void k_dequant_idct(const void *__restrict__ c
 // set (a set is exactly one 64-block RLE tile, rle_core.h) -- the K1 pass of
 // hic_rle_encode_i16 fused into the epilogue; TMF = 15 specialises max_len 15.
 template <int TABLE, int LAYOUT, int TMF = -1>
-__global__ __launch_bounds__(256) void k_dct_quant_2ph(const uint8_t *__restrict__ plane, int64_t stride, int W,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_dct_quant_2ph(const uint8_t *__restrict__ plane, int64_t stride, int W,
                                                        int nbx, int nblk, int nsets, void *__restrict__ out,
-                                                       int M = 0, int64_t *__restrict__ tiles = nullptr) {
+                                                       int M = 0, int64_t *__restrict__ tiles = nullptr,
+                                                       int path = 1) {
   __shared__ uint4 s_stage[4 * 64 * kStagePad];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nwaves = gridDim.x * 4;
+  const int set0 = blockIdx.x * 4 + wv;
   uint4 *st4 = s_stage + wv * 64 * kStagePad;
   int16_t *st = reinterpret_cast<int16_t *>(st4 + lane * kStagePad);
 
-  for (int set = blockIdx.x * 4 + wv; set < nsets; set += nwaves) {
-    int blk = set * 64 + lane;
+  auto load = [&](int set, uint2 (&w)[8]) {
+    const int blk = set * 64 + lane;
     const int cblk = blk < nblk ? blk : nblk - 1;
     const int bi = cblk / nbx, bj = cblk - bi * nbx;
     const uint8_t *p = plane + (int64_t)bi * 8 * stride + bj * 8;
-    uint2 w[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) w[r] = *reinterpret_cast<const uint2 *>(p + r * stride);
-    dct_block_2ph<TABLE, LAYOUT>(w, st);
+  };
+  // stage -> output layout (+ the RLE tile record)
+  auto store = [&](int set) {
     __builtin_amdgcn_wave_barrier();
+    const int blk = set * 64 + lane;
     if (LAYOUT == HIC_LAYOUT_ZIGZAG_I16) {
       uint4 *o = reinterpret_cast<uint4 *>(static_cast<int16_t *>(out) + (int64_t)set * 64 * 64);
 #pragma unroll
@@ -291,6 +295,7 @@ __global__ __launch_bounds__(256) void k_dct_quant_2ph(const uint8_t *__restrict
         tile_record16<TMF>(zw, blk < nblk, blk, M, tiles + (int64_t)set * 3);
       }
     } else if (blk < nblk) {
+      const int bi = blk / nbx, bj = blk - bi * nbx;
       if (LAYOUT == HIC_LAYOUT_RASTER_I16) {
         int16_t *o = static_cast<int16_t *>(out) + (int64_t)bi * 8 * W + bj * 8;
 #pragma unroll
@@ -311,9 +316,84 @@ __global__ __launch_bounds__(256) void k_dct_quant_2ph(const uint8_t *__restrict
       }
     }
     __builtin_amdgcn_wave_barrier();
+  };
+
+  // Main loop: the fast AAN path.  A set (64 blocks) with any coefficient inside
+  // the quantiser's tie window is remembered (bit i of `redo` = this wave's i-th
+  // set; the launcher keeps every wave at <= 64 sets) and redone after the loop
+  // on the exact pocketfft replica -- a separate code region, so the two paths
+  // do not share one register allocation.  path 0 (A/B tests): exact only;
+  // path 2: fast only (timing, not bit-exact).
+  uint64_t redo = 0, fix = 0;
+  int i = 0;
+  if (path != 0) {
+    for (int set = set0; set < nsets; set += nwaves, ++i) {
+      uint2 w[8];
+      load(set, w);
+      bool t26;
+      const bool f = dct_block_aan<TABLE, LAYOUT>(w, st, &t26);
+      if (__builtin_amdgcn_ballot_w64(f) != 0 && path == 1) redo |= 1ull << i;
+      if (__builtin_amdgcn_ballot_w64(t26) != 0 && path == 1) fix |= 1ull << i;
+      store(set);
+    }
+  } else {
+    for (int set = set0; set < nsets; set += nwaves, ++i) redo |= 1ull << i;
+  }
+  fix &= ~redo;
+  // (2,2)-class exact ties: rewrite just those four coefficients of the set's
+  // blocks in the output (and the set's RLE tile record)
+  while (fix) {
+    const int k = __builtin_ctzll(fix);
+    fix &= fix - 1;
+    const int set = set0 + k * nwaves;
+    const int blk = set * 64 + lane;
+    uint2 w[8];
+    load(set, w);
+    int q[4];
+    dct_fix26<TABLE>(w, q);
+    if (blk < nblk) {
+      constexpr SlotOf<LAYOUT> kSlot{};
+      constexpr int idx[4] = {18, 22, 50, 54};
+      if (LAYOUT == HIC_LAYOUT_ZIGZAG_I16) {
+        int16_t *o = static_cast<int16_t *>(out) + (int64_t)blk * 64;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[kSlot.s[idx[j]]] = (int16_t)q[j];
+      } else {
+        const int bi = blk / nbx, bj = blk - bi * nbx;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int64_t at = (int64_t)(bi * 8 + idx[j] / 8) * W + bj * 8 + idx[j] % 8;
+          if (LAYOUT == HIC_LAYOUT_RASTER_I16)
+            static_cast<int16_t *>(out)[at] = (int16_t)q[j];
+          else
+            static_cast<int32_t *>(out)[at] = q[j];
+        }
+      }
+    }
+    if (LAYOUT == HIC_LAYOUT_ZIGZAG_I16 && TMF >= 0) {
+      uint32_t zw[32];
+      if (blk < nblk) {
+        const uint4 *b4 = reinterpret_cast<const uint4 *>(static_cast<const int16_t *>(out) + (int64_t)blk * 64);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint4 t = b4[j];
+          zw[4 * j] = t.x; zw[4 * j + 1] = t.y; zw[4 * j + 2] = t.z; zw[4 * j + 3] = t.w;
+        }
+      }
+      tile_record16<TMF>(zw, blk < nblk, blk, M, tiles + (int64_t)set * 3);
+    }
+  }
+  // any other tie (rare): the whole set again on the exact pocketfft replica
+  while (redo) {
+    const int k = __builtin_ctzll(redo);
+    redo &= redo - 1;
+    const int set = set0 + k * nwaves;
+    uint2 w[8];
+    load(set, w);
+    dct_block_2ph<TABLE, LAYOUT>(w, st);
+    store(set);
   }
 }
-
 
 // ---------------------------------------------------------------------------
 // Block-level helpers (transform.dct2 / idct2, quantization.jpeg_quantize /
@@ -395,6 +475,16 @@ inline int dct_waves_per_cu() {
 }
 
 // HIC_DCT_VARIANT=single selects the one-pass single-lane kernel (A/B tests).
+// HIC_DCT_PATH=exact forces the pocketfft replica for every block (A/B tests).
+inline int dct_path() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("HIC_DCT_PATH");
+    v = !e ? 1 : (e[0] == 'e') ? 0 : (e[0] == 'n') ? 2 : 1;
+  }
+  return v;
+}
+
 inline int dct_variant() {
   static int v = -1;
   if (v < 0) {
@@ -416,14 +506,15 @@ int launch_fwd(const uint8_t *plane, int H, int W, int64_t stride, void *out, hi
   const dim3 grid((nblk + 255) / 256), block(256);
   if (fast && dct_variant() == 3) {
     const int nsets = (nblk + 63) / 64;
-    const int cap = dct_waves_per_cu() * cu_count();
+    int cap = dct_waves_per_cu() * cu_count();
+    if (cap > 0 && (nsets + cap - 1) / cap > 64) cap = (nsets + 63) / 64;  // <= 64 sets per wave (redo mask)
     const int waves = (cap == 0 || nsets < cap) ? nsets : cap;
     if (e0 || e1)
       hipExtLaunchKernelGGL((k_dct_quant_2ph<TABLE, LAYOUT, TMF>), dim3((waves + 3) / 4), block, 0, s, e0, e1, 0,
-                            plane, stride, W, nbx, nblk, nsets, out, M, tiles);
+                            plane, stride, W, nbx, nblk, nsets, out, M, tiles, dct_path());
     else
       hipLaunchKernelGGL((k_dct_quant_2ph<TABLE, LAYOUT, TMF>), dim3((waves + 3) / 4), block, 0, s, plane, stride, W,
-                         nbx, nblk, nsets, out, M, tiles);
+                         nbx, nblk, nsets, out, M, tiles, dct_path());
     return check_launch("k_dct_quant_2ph");
   } else if (fast) {
     hipLaunchKernelGGL((k_dct_quant<TABLE, LAYOUT, true>), grid, block, 0, s, plane, H, W, stride, nbx, nblk, out);

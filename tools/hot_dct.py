@@ -16,7 +16,7 @@ def run(H, W, rot, n=40):
     for i in range(n): f(i)
     e.record(); torch.cuda.synchronize()
     us = s.elapsed_time(e) / n * 1e3
-    print("%s %dx%d rot=%d: %.1f us  %.1f ps/block" % (os.environ.get('HIC_DCT_VARIANT', '2ph'), H, W, rot, us, us * 1e6 / nblk))
+    print("%s %dx%d rot=%d: %.1f us  %.1f ps/block" % (os.environ.get('HIC_DCT_PATH', 'aan'), H, W, rot, us, us * 1e6 / nblk))
 run(4320, 7680, 12)
 run(4320, 7680, 1)
 run(2048, 4096, 1)

@@ -121,6 +121,42 @@ def test_tie_blocks_many():
         np.testing.assert_array_equal(transform.dct_channel(plane, QT[tab]), orcc.dct_channel(plane, tab, threads=8))
 
 
+@pytest.mark.parametrize("kind", ["levels4", "nearflat", "stripes", "checker"])
+def test_fast_path_structured_ties(kind):
+    """Planes that drive the AAN fast path into its tie handling: 4-level and
+    near-flat pixels give exact (2,2)-class and (4,4) ties and the rare whole-set
+    redo; stripes / checkerboards give large saturated coefficients.  Every
+    layout and both tables, fused RLE-tile variant included, vs the C oracle."""
+    rng = np.random.default_rng(hash(kind) % 2**32)
+    H, W = 8 * 160, 8 * 320
+    if kind == "levels4":
+        plane = (rng.integers(0, 4, (H, W)) * 85).astype(np.uint8)
+    elif kind == "nearflat":
+        plane = (128 + rng.integers(-4, 5, (H, W))).astype(np.uint8)
+    elif kind == "stripes":
+        plane = np.where((np.arange(W) // rng.integers(1, 4)) % 2 == 0, 255, 0).astype(np.uint8)[None].repeat(H, 0)
+        plane[rng.random((H, W)) < 0.01] = 128
+    else:
+        plane = (((np.arange(H)[:, None] + np.arange(W)[None]) % 2) * 255).astype(np.uint8)
+        plane ^= rng.integers(0, 2, (H, W), dtype=np.uint8)
+    d = device.to_device(plane)
+    for tab in (0, 1):
+        exp = orcc.dct_channel(plane, tab, threads=8)
+        for layout in (_lib.LAYOUT_RASTER_I32, _lib.LAYOUT_RASTER_I16, _lib.LAYOUT_ZIGZAG_I16):
+            got = device.to_host(transform.dct_channel_device(d, tab, layout))
+            if layout == _lib.LAYOUT_ZIGZAG_I16:
+                got = orc.merge_blocks(got[:, np.argsort(orc.ZZ8)].reshape(-1, 8, 8), (H, W))
+            np.testing.assert_array_equal(got.astype(np.int32), exp, err_msg=(kind, tab, layout))
+        # the fused variant (DCT + RLE tile records) writes the same coefficients
+        nblk = (H // 8) * (W // 8)
+        out = device.empty((nblk, 64), torch.int16)
+        ws = device.workspace(_lib.load().hic_rle_workspace_bytes(nblk, 64))
+        _lib.call("hic_dct_quant_rle_u8", device.ptr(d), H, W, W, tab, 15, device.ptr(out), device.ptr(ws),
+                  device.stream_ptr(), None, None)
+        got = orc.merge_blocks(device.to_host(out)[:, np.argsort(orc.ZZ8)].reshape(-1, 8, 8), (H, W))
+        np.testing.assert_array_equal(got.astype(np.int32), exp, err_msg=(kind, tab, "fused"))
+
+
 def test_bad_args():
     with pytest.raises(ValueError):
         transform.dct_channel(np.zeros((8, 8), np.uint8), model.QTables.JPEG_LUMINANCE, block_size=4)

@@ -10,6 +10,8 @@
 // the oracle's restatement (oracle/oracle.py), not against cv2 itself.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "hic_common.h"
 
 namespace hic {
@@ -222,10 +224,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kSegC == 8 
       hal_r = c.cr | c.cb << 8;
     }
   }
-  int hcr0[kSegR], hcr2[kSegR], hcb0[kSegR], hcb2[kSegR];
+  // Interior waves (a full segment clear of the image / shard top and bottom, a
+  // full strip that is neither the first nor the last) run a variant with no
+  // per-lane conditions: every row's Y store and every chroma store is decided at
+  // compile time, and the strip-edge halo comes in by v_cndmask.
+  const bool interior = ncr == kSegC && oyl0 + kSegC < dh_out && gy0 >= (in_row0 > 0 ? in_row0 : 0) &&
+                        gy0 + nr <= (in_row1 < H ? in_row1 : H) && gy0 + nr <= out_row0 + out_rows &&
+                        gy0 >= out_row0 && strip > 0 && q0 + 64 < nq;
+  auto body = [&](auto edge_tag) {
+    constexpr bool EDGE = decltype(edge_tag)::value;
+    int hcr0[kSegR], hcr2[kSegR], hcb0[kSegR], hcb2[kSegR];
 #pragma unroll
-  for (int r = 0; r < kSegR; ++r) {
-    if (r < nr) {
+    for (int r = 0; r < kSegR; ++r) {
+      if (EDGE && r >= nr) continue;
       const uint32_t w0 = raw[r][0], w1 = raw[r][1], w2 = raw[r][2];
       const int px[12] = {(int)(w0 & 255), (int)((w0 >> 8) & 255), (int)((w0 >> 16) & 255), (int)(w0 >> 24),
                           (int)(w1 & 255), (int)((w1 >> 8) & 255), (int)((w1 >> 16) & 255), (int)(w1 >> 24),
@@ -240,19 +251,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kSegC == 8 
         cb[k] = (int)c.cb;
       }
       const int gy = gy0 + r;
-      if (owner && gy >= yw0 && gy < yw1) *reinterpret_cast<uint32_t *>(Y + (int64_t)(gy - out_row0) * W + 4 * q) = yq;
+      if (EDGE) {
+        if (owner && gy >= yw0 && gy < yw1)
+          *reinterpret_cast<uint32_t *>(Y + (int64_t)(gy - out_row0) * W + 4 * q) = yq;
+      } else if (r >= 2 && r < 2 + 2 * kSegC) {
+        *reinterpret_cast<uint32_t *>(Y + (int64_t)(gy - out_row0) * W + 4 * q) = yq;
+      }
       // neighbours: pixels x-2, x-1 from the left quad, x+4 from the right quad
+      const uint32_t hl = (uint32_t)__builtin_amdgcn_readlane((int)hal_l, r);
+      const uint32_t hr = (uint32_t)__builtin_amdgcn_readlane((int)hal_r, r);
       uint32_t lft = shr1(pack4(cr[2], cr[3], cb[2], cb[3]));
       uint32_t rgt = shl1((uint32_t)cr[0] | (uint32_t)cb[0] << 8);
-      if (lane == 0) lft = (uint32_t)__builtin_amdgcn_readlane((int)hal_l, r);
-      if (lane == 63) rgt = (uint32_t)__builtin_amdgcn_readlane((int)hal_r, r);
-      if (q == 0) lft = pack4(cr[2], cr[1], cb[2], cb[1]);
-      if (q == nq - 1) rgt = (uint32_t)cr[2] | (uint32_t)cb[2] << 8;
+      lft = lane == 0 ? hl : lft;
+      rgt = lane == 63 ? hr : rgt;
+      if (EDGE) {
+        if (q == 0) lft = pack4(cr[2], cr[1], cb[2], cb[1]);
+        if (q == nq - 1) rgt = (uint32_t)cr[2] | (uint32_t)cb[2] << 8;
+      }
       hcr0[r] = (int)(lft & 255) + 4 * ((int)((lft >> 8) & 255) + cr[1]) + 6 * cr[0] + cr[2];
       hcb0[r] = (int)((lft >> 16) & 255) + 4 * ((int)(lft >> 24) + cb[1]) + 6 * cb[0] + cb[2];
       hcr2[r] = cr[0] + 4 * (cr[1] + cr[3]) + 6 * cr[2] + (int)(rgt & 255);
       hcb2[r] = cb[0] + 4 * (cb[1] + cb[3]) + 6 * cb[2] + (int)((rgt >> 8) & 255);
-      if (r >= 4 && r % 2 == 0 && owner) {  // chroma row k = r/2 - 2 is complete
+      if (r >= 4 && r % 2 == 0 && (!EDGE || owner)) {  // chroma row k = r/2 - 2 is complete
         const int a = r - 4, k = r / 2 - 2;
 #define HIC_V(h) ((((h)[a] + 4 * ((h)[a + 1] + (h)[a + 3]) + 6 * (h)[a + 2] + (h)[a + 4]) + 128) >> 8)
         const int64_t o = (int64_t)(oyl0 + k) * dw + 2 * q;
@@ -261,7 +281,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kSegC == 8 
 #undef HIC_V
       }
     }
-  }
+  };
+  if (interior)
+    body(std::false_type{});
+  else
+    body(std::true_type{});
 }
 
 __global__ void k_rgb_ycrcb(const uint8_t *__restrict__ rgb, int64_t npix, uint8_t *__restrict__ Y,

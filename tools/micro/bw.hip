@@ -36,6 +36,21 @@ __global__ __launch_bounds__(256) void k_r1w2(const uint4 *__restrict__ a, uint4
   }
 }
 
+// narrow stores: T per lane, consecutive lanes consecutive
+template <typename T>
+__global__ __launch_bounds__(256) void k_writeT(T *__restrict__ a, int64_t n) {
+  for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) a[i] = (T)i;
+}
+// dwordx3 loads at 12-byte lane stride (the colour kernel's pattern)
+__global__ __launch_bounds__(256) void k_read12(const uint8_t *__restrict__ a, int64_t n12, uint32_t *out) {
+  uint32_t acc = 0;
+  for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < n12; i += (int64_t)gridDim.x * 256) {
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(a + 12 * i);
+    acc ^= p[0] ^ p[1] ^ p[2];
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
 int main() {
   const int rot = 8;
   const size_t bytes = 256ull << 20;  // 256 MiB per buffer
@@ -75,6 +90,18 @@ int main() {
     });
     time("r1w2", 1.5 * bytes, [&](int r) {
       hipLaunchKernelGGL(k_r1w2, g, b, 0, 0, buf[r % rot], buf[(r + 4) % rot], n16 / 2);
+    });
+    time("write2", bytes, [&](int r) {
+      hipLaunchKernelGGL((k_writeT<uint16_t>), g, b, 0, 0, reinterpret_cast<uint16_t *>(buf[r % rot]), (int64_t)bytes / 2);
+    });
+    time("write4", bytes, [&](int r) {
+      hipLaunchKernelGGL((k_writeT<uint32_t>), g, b, 0, 0, reinterpret_cast<uint32_t *>(buf[r % rot]), (int64_t)bytes / 4);
+    });
+    time("write8", bytes, [&](int r) {
+      hipLaunchKernelGGL((k_writeT<uint64_t>), g, b, 0, 0, reinterpret_cast<uint64_t *>(buf[r % rot]), (int64_t)bytes / 8);
+    });
+    time("read12", bytes, [&](int r) {
+      hipLaunchKernelGGL(k_read12, g, b, 0, 0, reinterpret_cast<const uint8_t *>(buf[r % rot]), (int64_t)bytes / 12, o);
     });
   }
   return 0;

@@ -62,7 +62,7 @@ def main():
         wb = mean(w[k][2:] if len(w.get(k, [])) > 2 else w.get(k, [0.0]))
         res["kernels"][k] = {"fetch_counter_bytes": round(fb), "write_counter_bytes": round(wb),
                              "read_bytes_calibrated": round(fb / rf), "write_bytes_calibrated": round(wb / rw)}
-    lum = [k for k in res["kernels"] if k.startswith("k_dct_quant_2ph<0")]
+    lum = [k for k in res["kernels"] if k.startswith("k_dct_quant_2ph<0, 2, 15>")]
     if lum:
         r = res["kernels"][lum[0]]
         res["dct_lum_kernel"] = lum[0]

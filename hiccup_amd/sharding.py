@@ -52,12 +52,23 @@ def stitch_host(summaries, rank):
                     dtype=np.int64)
 
 
+def _all_gather(out_flat, inp, group=None):
+    """all_gather_into_tensor; gloo (CPU rehearsal of the multi-GPU path) cannot
+    gather device tensors, so there they are staged through host memory."""
+    if inp.is_cuda and dist.get_backend(group) == "gloo":
+        host = torch.empty(out_flat.shape, dtype=out_flat.dtype)
+        dist.all_gather_into_tensor(host, inp.detach().cpu().contiguous(), group=group)
+        out_flat.copy_(host)
+    else:
+        dist.all_gather_into_tensor(out_flat, inp.contiguous(), group=group)
+
+
 def exchange(summ_local, world, group=None):
     """All-gather every rank's (3, 4) channel summaries -> (world, 3, 4): the one
     collective of the sharded encode (RCCL on GPU tensors, gloo on CPU ones)."""
     shape = tuple(summ_local.shape)
     out = torch.empty((world * shape[0],) + shape[1:], dtype=summ_local.dtype, device=summ_local.device)
-    dist.all_gather_into_tensor(out, summ_local.contiguous(), group=group)
+    _all_gather(out, summ_local, group=group)
     return out.view((world,) + shape)
 
 
@@ -86,18 +97,33 @@ class ShardEncoder:
         enc.transform(rgb_rows, stream, in_row0=self.span[0], lum_events=lum_events)
         summ = enc.shard_summaries(stream)
         # the exchange step: 96 bytes per rank over RCCL
-        dist.all_gather_into_tensor(self.all_summ.view(self.world * 3, 4), summ, group=self.group)
+        _all_gather(self.all_summ.view(self.world * 3, 4), summ, group=self.group)
         s = device.stream_ptr(stream)
         for c in range(3):
             _lib.call("hic_rle_stitch", ctypes.c_void_p(self.all_summ.data_ptr() + 8 * 4 * c), self.world, self.rank,
                       12, device.ptr(self.stitch[c]), s)
         enc.entropy(stream, stitch=self.stitch)
-        dist.all_gather_into_tensor(self.all_counts.view(-1), enc.counts, group=self.group)
+        _all_gather(self.all_counts.view(-1), enc.counts, group=self.group)
 
     def offsets(self):
         """(this rank's symbol offset per channel, global totals) -- host ints (syncs)."""
         c = self.all_counts.cpu().numpy()
         return c[:self.rank].sum(0), c.sum(0)
+
+
+def _send(t, dst, group):
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        t = t.cpu()
+    dist.send(t, dst=dst, group=group)
+
+
+def _recv(t, src, group):
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        h = torch.empty(t.shape, dtype=t.dtype)
+        dist.recv(h, src=src, group=group)
+        t.copy_(h)
+    else:
+        dist.recv(t, src=src, group=group)
 
 
 def gather_streams(se, dst=0):
@@ -106,7 +132,7 @@ def gather_streams(se, dst=0):
     counts = se.all_counts.cpu().numpy()
     nblk = torch.tensor([se.enc.dc[k].numel() for k in CHANNELS], dtype=torch.int64, device=se.all_counts.device)
     all_nblk = torch.zeros((se.world, 3), dtype=torch.int64, device=nblk.device)
-    dist.all_gather_into_tensor(all_nblk.view(-1), nblk, group=se.group)
+    _all_gather(all_nblk.view(-1), nblk, group=se.group)
     all_nblk = all_nblk.cpu().numpy()
     out = {} if se.rank == dst else None
     for ci, k in enumerate(CHANNELS):
@@ -124,15 +150,13 @@ def gather_streams(se, dst=0):
                     V[so:so + n].copy_(enc.sym_val[k][:n])
                     D[bo:bo + nb].copy_(enc.dc[k])
                 else:
-                    dist.recv(L[so:so + n], src=r, group=se.group)
-                    dist.recv(V[so:so + n], src=r, group=se.group)
-                    dist.recv(D[bo:bo + nb], src=r, group=se.group)
+                    for t in (L[so:so + n], V[so:so + n], D[bo:bo + nb]):
+                        _recv(t, r, se.group)
                 so += n
                 bo += nb
             out[k] = (D.cpu().numpy(), L.cpu().numpy(), V.cpu().numpy())
         else:
             n = int(counts[se.rank, ci])
-            dist.send(enc.sym_len[k][:n].contiguous(), dst=dst, group=se.group)
-            dist.send(enc.sym_val[k][:n].contiguous(), dst=dst, group=se.group)
-            dist.send(enc.dc[k].contiguous(), dst=dst, group=se.group)
+            for t in (enc.sym_len[k][:n], enc.sym_val[k][:n], enc.dc[k]):
+                _send(t.contiguous(), dst, se.group)
     return out

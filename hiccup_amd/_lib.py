@@ -35,6 +35,12 @@ class RleJob16(ctypes.Structure):
                 ("sym_val", _vp), ("sym_cap", _i64), ("d_count", _vp), ("workspace", _vp)]
 
 
+class DctPlaneJob(ctypes.Structure):
+    """hic_dct_plane_job (include/hiccup_hip.h)."""
+    _fields_ = [("plane", _vp), ("H", _i64), ("W", _i64), ("stride", _i64), ("table_id", _int), ("out", _vp),
+                ("rle_workspace", _vp)]
+
+
 SIGNATURES = {
     "hic_abi_version": (_int, []),
     "hic_last_error": (_int, [ctypes.c_char_p, _sz]),
@@ -43,6 +49,7 @@ SIGNATURES = {
     "hic_dct_quant_u8": (_int, [_vp, _i64, _i64, _i64, _int, _int, _vp, _vp]),
     "hic_dct_quant_u8_timed": (_int, [_vp, _i64, _i64, _i64, _int, _int, _vp, _vp, _vp, _vp]),
     "hic_dct_quant_rle_u8": (_int, [_vp, _i64, _i64, _i64, _int, _int, _vp, _vp, _vp, _vp, _vp]),
+    "hic_dct_quant_rle_u8_batch": (_int, [_int, _vp, _int, _vp, _vp, _vp]),
     "hic_rle_encode_i16_tiles": (_int, [_vp, _i64, _int, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
     "hic_rle_shard_summary_tiles": (_int, [_vp, _i64, _vp, _vp, _vp]),
     "hic_rle_encode_i16_tiles_batch": (_int, [_int, _vp, _int, _vp]),

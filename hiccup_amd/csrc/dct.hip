@@ -244,46 +244,64 @@ __global__ __launch_bounds__(256) void k_dequant_idct(const void *__restrict__ c
   }
 }
 
-// Production forward kernel for aligned planes: one 8x8 block per lane, 64
-// consecutive raster-order blocks ("a set") per wave iteration, persistent grid
-// sized to the waves that fit at once.  dct_block_2ph (dct_core.h) writes the
-// quantized coefficients straight to their slot in an LDS stage, which is then
-// copied out so that every store instruction writes one contiguous 1 KiB segment
-// (zig-zag layout) or whole 16-byte row pieces (raster layouts).
-// TMF >= 0 (ZIGZAG_I16 only): also write the RLE hot path's tile record of every
-// set (a set is exactly one 64-block RLE tile, rle_core.h) -- the K1 pass of
-// hic_rle_encode_i16 fused into the epilogue; TMF = 15 specialises max_len 15.
-template <int TABLE, int LAYOUT, int TMF = -1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_dct_quant_2ph(const uint8_t *__restrict__ plane, int64_t stride, int W,
-                                                       int nbx, int nblk, int nsets, void *__restrict__ out,
-                                                       int M = 0, int64_t *__restrict__ tiles = nullptr,
-                                                       int path = 1) {
+// Production forward kernel for aligned planes, for up to three planes of one
+// quantisation table per launch (Cr + Cb of one image: one persistent grid over
+// both planes' sets keeps every SIMD busy, where a chroma plane alone leaves a
+// third of the waves idle).  One
+// 8x8 block per lane, 64 consecutive raster-order blocks ("a set" = one RLE tile)
+// per wave iteration; persistent grid sized to the waves that fit at once.
+// dct_block_aan (dct_core.h) writes the quantized coefficients straight to their
+// slot in an LDS stage, which is copied out so that every store instruction writes
+// one contiguous 1 KiB segment (zig-zag layout) or whole 16-byte row pieces
+// (raster layouts).  TMF >= 0 (ZIGZAG_I16 only): the set's RLE tile record
+// (rle_core.h) is written too -- the K1 pass of hic_rle_encode_i16 fused into the
+// epilogue; TMF = 15 specialises max_len 15.
+struct DctJob {
+  const uint8_t *plane;
+  int64_t stride;
+  void *out;
+  int64_t *tiles;
+  int W, nbx, nblk, nsets, set0, table;
+};
+struct DctJobs {
+  DctJob j[3];
+  int n, total_sets, M;
+};
+
+template <int TABLE, int LAYOUT, int TMF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_dct_planes(DctJobs jobs, int path) {
   __shared__ uint4 s_stage[4 * 64 * kStagePad];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nwaves = gridDim.x * 4;
-  const int set0 = blockIdx.x * 4 + wv;
+  const int g0 = blockIdx.x * 4 + wv;
   uint4 *st4 = s_stage + wv * 64 * kStagePad;
   int16_t *st = reinterpret_cast<int16_t *>(st4 + lane * kStagePad);
+  const int M = jobs.M;
 
-  auto load = [&](int set, uint2 (&w)[8]) {
+  auto job_of = [&](int g) {
+    int k = 0;
+    while (k + 1 < jobs.n && g >= jobs.j[k + 1].set0) ++k;
+    return k;
+  };
+  auto load = [&](const DctJob &J, int set, uint2 (&w)[8]) {
     const int blk = set * 64 + lane;
-    const int cblk = blk < nblk ? blk : nblk - 1;
-    const int bi = cblk / nbx, bj = cblk - bi * nbx;
-    const uint8_t *p = plane + (int64_t)bi * 8 * stride + bj * 8;
+    const int cblk = blk < J.nblk ? blk : J.nblk - 1;
+    const int bi = cblk / J.nbx, bj = cblk - bi * J.nbx;
+    const uint8_t *p = J.plane + (int64_t)bi * 8 * J.stride + bj * 8;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) w[r] = *reinterpret_cast<const uint2 *>(p + r * stride);
+    for (int r = 0; r < 8; ++r) w[r] = *reinterpret_cast<const uint2 *>(p + r * J.stride);
   };
   // stage -> output layout (+ the RLE tile record)
-  auto store = [&](int set) {
+  auto store = [&](const DctJob &J, int set) {
     __builtin_amdgcn_wave_barrier();
     const int blk = set * 64 + lane;
     if (LAYOUT == HIC_LAYOUT_ZIGZAG_I16) {
-      uint4 *o = reinterpret_cast<uint4 *>(static_cast<int16_t *>(out) + (int64_t)set * 64 * 64);
+      uint4 *o = reinterpret_cast<uint4 *>(static_cast<int16_t *>(J.out) + (int64_t)set * 64 * 64);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int b = 8 * k + (lane >> 3);
         const uint4 v = st4[b * kStagePad + (lane & 7)];
-        if (set * 64 + b < nblk) o[64 * k + lane] = v;
+        if (set * 64 + b < J.nblk) o[64 * k + lane] = v;
       }
       if (TMF >= 0) {
         uint32_t zw[32];
@@ -292,16 +310,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
           const uint4 t = st4[lane * kStagePad + k];
           zw[4 * k] = t.x; zw[4 * k + 1] = t.y; zw[4 * k + 2] = t.z; zw[4 * k + 3] = t.w;
         }
-        tile_record16<TMF>(zw, blk < nblk, blk, M, tiles + (int64_t)set * 3);
+        tile_record16<TMF>(zw, blk < J.nblk, blk, M, J.tiles + (int64_t)set * 3);
       }
-    } else if (blk < nblk) {
-      const int bi = blk / nbx, bj = blk - bi * nbx;
+    } else if (blk < J.nblk) {
+      const int bi = blk / J.nbx, bj = blk - bi * J.nbx;
       if (LAYOUT == HIC_LAYOUT_RASTER_I16) {
-        int16_t *o = static_cast<int16_t *>(out) + (int64_t)bi * 8 * W + bj * 8;
+        int16_t *o = static_cast<int16_t *>(J.out) + (int64_t)bi * 8 * J.W + bj * 8;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) *reinterpret_cast<uint4 *>(o + (int64_t)u * W) = st4[lane * kStagePad + u];
+        for (int u = 0; u < 8; ++u) *reinterpret_cast<uint4 *>(o + (int64_t)u * J.W) = st4[lane * kStagePad + u];
       } else {
-        int32_t *o = static_cast<int32_t *>(out) + (int64_t)bi * 8 * W + bj * 8;
+        int32_t *o = static_cast<int32_t *>(J.out) + (int64_t)bi * 8 * J.W + bj * 8;
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const uint4 t = st4[lane * kStagePad + u];
@@ -309,7 +327,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
           int q[8];
 #pragma unroll
           for (int v = 0; v < 8; ++v) q[v] = (int)(int16_t)(wd[v >> 1] >> (16 * (v & 1)));
-          int4 *row = reinterpret_cast<int4 *>(o + (int64_t)u * W);
+          int4 *row = reinterpret_cast<int4 *>(o + (int64_t)u * J.W);
           row[0] = make_int4(q[0], q[1], q[2], q[3]);
           row[1] = make_int4(q[4], q[5], q[6], q[7]);
         }
@@ -318,26 +336,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     __builtin_amdgcn_wave_barrier();
   };
 
-  // Main loop: the fast AAN path.  A set (64 blocks) with any coefficient inside
-  // the quantiser's tie window is remembered (bit i of `redo` = this wave's i-th
-  // set; the launcher keeps every wave at <= 64 sets) and redone after the loop
-  // on the exact pocketfft replica -- a separate code region, so the two paths
-  // do not share one register allocation.  path 0 (A/B tests): exact only;
-  // path 2: fast only (timing, not bit-exact).
+  // Main loop: the fast AAN path.  A set with any coefficient inside the
+  // quantiser's tie window is remembered (bit i of `redo` / `fix` = this wave's
+  // i-th set; the launcher keeps every wave at <= 64 sets) and handled after the
+  // loop -- a separate code region, so the paths do not share one register
+  // allocation.  path 0 (A/B tests): exact only; path 2: fast only (timing, not
+  // bit-exact).
   uint64_t redo = 0, fix = 0;
   int i = 0;
   if (path != 0) {
-    for (int set = set0; set < nsets; set += nwaves, ++i) {
+    for (int g = g0; g < jobs.total_sets; g += nwaves, ++i) {
+      const DctJob &J = jobs.j[job_of(g)];
+      const int set = g - J.set0;
       uint2 w[8];
-      load(set, w);
+      load(J, set, w);
       bool t26;
       const bool f = dct_block_aan<TABLE, LAYOUT>(w, st, &t26);
       if (__builtin_amdgcn_ballot_w64(f) != 0 && path == 1) redo |= 1ull << i;
       if (__builtin_amdgcn_ballot_w64(t26) != 0 && path == 1) fix |= 1ull << i;
-      store(set);
+      store(J, set);
     }
   } else {
-    for (int set = set0; set < nsets; set += nwaves, ++i) redo |= 1ull << i;
+    for (int g = g0; g < jobs.total_sets; g += nwaves, ++i) redo |= 1ull << i;
   }
   fix &= ~redo;
   // (2,2)-class exact ties: rewrite just those four coefficients of the set's
@@ -345,53 +365,57 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   while (fix) {
     const int k = __builtin_ctzll(fix);
     fix &= fix - 1;
-    const int set = set0 + k * nwaves;
+    const int g = g0 + k * nwaves;
+    const DctJob &J = jobs.j[job_of(g)];
+    const int set = g - J.set0;
     const int blk = set * 64 + lane;
     uint2 w[8];
-    load(set, w);
+    load(J, set, w);
     int q[4];
     dct_fix26<TABLE>(w, q);
-    if (blk < nblk) {
+    if (blk < J.nblk) {
       constexpr SlotOf<LAYOUT> kSlot{};
       constexpr int idx[4] = {18, 22, 50, 54};
       if (LAYOUT == HIC_LAYOUT_ZIGZAG_I16) {
-        int16_t *o = static_cast<int16_t *>(out) + (int64_t)blk * 64;
+        int16_t *o = static_cast<int16_t *>(J.out) + (int64_t)blk * 64;
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[kSlot.s[idx[j]]] = (int16_t)q[j];
       } else {
-        const int bi = blk / nbx, bj = blk - bi * nbx;
+        const int bi = blk / J.nbx, bj = blk - bi * J.nbx;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int64_t at = (int64_t)(bi * 8 + idx[j] / 8) * W + bj * 8 + idx[j] % 8;
+          const int64_t at = (int64_t)(bi * 8 + idx[j] / 8) * J.W + bj * 8 + idx[j] % 8;
           if (LAYOUT == HIC_LAYOUT_RASTER_I16)
-            static_cast<int16_t *>(out)[at] = (int16_t)q[j];
+            static_cast<int16_t *>(J.out)[at] = (int16_t)q[j];
           else
-            static_cast<int32_t *>(out)[at] = q[j];
+            static_cast<int32_t *>(J.out)[at] = q[j];
         }
       }
     }
     if (LAYOUT == HIC_LAYOUT_ZIGZAG_I16 && TMF >= 0) {
       uint32_t zw[32];
-      if (blk < nblk) {
-        const uint4 *b4 = reinterpret_cast<const uint4 *>(static_cast<const int16_t *>(out) + (int64_t)blk * 64);
+      if (blk < J.nblk) {
+        const uint4 *b4 = reinterpret_cast<const uint4 *>(static_cast<const int16_t *>(J.out) + (int64_t)blk * 64);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const uint4 t = b4[j];
           zw[4 * j] = t.x; zw[4 * j + 1] = t.y; zw[4 * j + 2] = t.z; zw[4 * j + 3] = t.w;
         }
       }
-      tile_record16<TMF>(zw, blk < nblk, blk, M, tiles + (int64_t)set * 3);
+      tile_record16<TMF>(zw, blk < J.nblk, blk, M, J.tiles + (int64_t)set * 3);
     }
   }
   // any other tie (rare): the whole set again on the exact pocketfft replica
   while (redo) {
     const int k = __builtin_ctzll(redo);
     redo &= redo - 1;
-    const int set = set0 + k * nwaves;
+    const int g = g0 + k * nwaves;
+    const DctJob &J = jobs.j[job_of(g)];
+    const int set = g - J.set0;
     uint2 w[8];
-    load(set, w);
+    load(J, set, w);
     dct_block_2ph<TABLE, LAYOUT>(w, st);
-    store(set);
+    store(J, set);
   }
 }
 
@@ -498,24 +522,42 @@ inline bool fwd_fast(int H, int W, int64_t stride, const void *plane, const void
   return (H % 8 == 0) && (W % 8 == 0) && (stride % 8 == 0) && aligned(plane, 8) && aligned(out, 16);
 }
 
-template <int TABLE, int LAYOUT, int TMF = -1>
+// Persistent launch of k_dct_planes over the jobs' sets (all fast-path planes).
+template <int TABLE, int LAYOUT, int TMF>
+int launch_planes(DctJobs &jobs, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+  int total = 0;
+  for (int k = 0; k < jobs.n; ++k) {
+    jobs.j[k].set0 = total;
+    total += jobs.j[k].nsets;
+  }
+  jobs.total_sets = total;
+  int cap = dct_waves_per_cu() * cu_count();
+  if (cap > 0 && (total + cap - 1) / cap > 64) cap = (total + 63) / 64;  // <= 64 sets per wave (redo mask)
+  const int waves = (cap == 0 || total < cap) ? total : cap;
+  const dim3 grid((waves + 3) / 4), block(256);
+  if (e0 || e1)
+    hipExtLaunchKernelGGL((k_dct_planes<TABLE, LAYOUT, TMF>), grid, block, 0, s, e0, e1, 0, jobs, dct_path());
+  else
+    hipLaunchKernelGGL((k_dct_planes<TABLE, LAYOUT, TMF>), grid, block, 0, s, jobs, dct_path());
+  return check_launch("k_dct_planes");
+}
+
+inline DctJob make_job(const uint8_t *plane, int H, int W, int64_t stride, int table, void *out, int64_t *tiles) {
+  const int nbx = (W + 7) / 8, nblk = nbx * ((H + 7) / 8);
+  return DctJob{plane, stride, out, tiles, W, nbx, nblk, (nblk + 63) / 64, 0, table};
+}
+
+template <int TABLE, int LAYOUT>
 int launch_fwd(const uint8_t *plane, int H, int W, int64_t stride, void *out, hipStream_t s, hipEvent_t e0,
-               hipEvent_t e1, int M = 0, int64_t *tiles = nullptr) {
+               hipEvent_t e1) {
   const int nbx = (W + 7) / 8, nby = (H + 7) / 8, nblk = nbx * nby;
   const bool fast = fwd_fast(H, W, stride, plane, out);
   const dim3 grid((nblk + 255) / 256), block(256);
   if (fast && dct_variant() == 3) {
-    const int nsets = (nblk + 63) / 64;
-    int cap = dct_waves_per_cu() * cu_count();
-    if (cap > 0 && (nsets + cap - 1) / cap > 64) cap = (nsets + 63) / 64;  // <= 64 sets per wave (redo mask)
-    const int waves = (cap == 0 || nsets < cap) ? nsets : cap;
-    if (e0 || e1)
-      hipExtLaunchKernelGGL((k_dct_quant_2ph<TABLE, LAYOUT, TMF>), dim3((waves + 3) / 4), block, 0, s, e0, e1, 0,
-                            plane, stride, W, nbx, nblk, nsets, out, M, tiles, dct_path());
-    else
-      hipLaunchKernelGGL((k_dct_quant_2ph<TABLE, LAYOUT, TMF>), dim3((waves + 3) / 4), block, 0, s, plane, stride, W,
-                         nbx, nblk, nsets, out, M, tiles, dct_path());
-    return check_launch("k_dct_quant_2ph");
+    DctJobs jobs{};
+    jobs.n = 1;
+    jobs.j[0] = make_job(plane, H, W, stride, TABLE, out, nullptr);
+    return launch_planes<TABLE, LAYOUT, -1>(jobs, s, e0, e1);
   } else if (fast) {
     hipLaunchKernelGGL((k_dct_quant<TABLE, LAYOUT, true>), grid, block, 0, s, plane, H, W, stride, nbx, nblk, out);
   } else if (e0 || e1)
@@ -578,28 +620,53 @@ extern "C" int hic_dct_quant_u8_timed(const uint8_t *plane, int64_t H, int64_t W
 extern "C" int hic_dct_quant_rle_u8(const uint8_t *plane, int64_t H, int64_t W, int64_t stride, int table_id,
                                     int max_len, int16_t *out, void *rle_workspace, void *stream, void *ev_start,
                                     void *ev_stop) {
-  if (!plane || !out || !rle_workspace) return arg_error("null pointer");
-  if (!dims_ok(H, W) || stride < W) return arg_error("plane shape / stride");
-  if (table_id != HIC_TABLE_LUMINANCE && table_id != HIC_TABLE_CHROMINANCE) return arg_error("table_id");
+  hic_dct_plane_job job{plane, H, W, stride, table_id, out, rle_workspace};
+  return hic_dct_quant_rle_u8_batch(1, &job, max_len, stream, ev_start, ev_stop);
+}
+
+extern "C" int hic_dct_quant_rle_u8_batch(int n, const hic_dct_plane_job *jobs, int max_len, void *stream,
+                                          void *ev_start, void *ev_stop) {
+  if (n < 1 || n > 3 || !jobs) return arg_error("1 <= n <= 3 planes");
   if (max_len < 1 || max_len > 256) return arg_error("max_len must be in [1, 256]");
   hipStream_t s = as_stream(stream);
-  const int h = (int)H, w = (int)W;
   const hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
-  int64_t *tiles = static_cast<int64_t *>(rle_workspace);
-  if (fwd_fast(h, w, stride, plane, out) && dct_variant() == 3) {
-    if (table_id == 0)
-      return max_len == 15 ? launch_fwd<0, HIC_LAYOUT_ZIGZAG_I16, 15>(plane, h, w, stride, out, s, e0, e1, 15, tiles)
-                           : launch_fwd<0, HIC_LAYOUT_ZIGZAG_I16, 0>(plane, h, w, stride, out, s, e0, e1, max_len,
-                                                                      tiles);
-    return max_len == 15 ? launch_fwd<1, HIC_LAYOUT_ZIGZAG_I16, 15>(plane, h, w, stride, out, s, e0, e1, 15, tiles)
-                         : launch_fwd<1, HIC_LAYOUT_ZIGZAG_I16, 0>(plane, h, w, stride, out, s, e0, e1, max_len,
-                                                                    tiles);
+  DctJobs fastj[2] = {};  // per quantisation table
+  for (int k = 0; k < n; ++k) {
+    const hic_dct_plane_job &a = jobs[k];
+    if (!a.plane || !a.out || !a.rle_workspace) return arg_error("plane %d: null pointer", k);
+    if (!dims_ok(a.H, a.W) || a.stride < a.W) return arg_error("plane %d: shape / stride", k);
+    if (a.table_id != HIC_TABLE_LUMINANCE && a.table_id != HIC_TABLE_CHROMINANCE) return arg_error("plane %d: table_id", k);
+    const int h = (int)a.H, w = (int)a.W;
+    int64_t *tiles = static_cast<int64_t *>(a.rle_workspace);
+    if (fwd_fast(h, w, a.stride, a.plane, a.out) && dct_variant() == 3) {
+      DctJobs &J = fastj[a.table_id];
+      J.j[J.n++] = make_job(a.plane, h, w, a.stride, a.table_id, a.out, tiles);
+      continue;
+    }
+    // ragged plane: pocketfft replica, then the stand-alone tile pass
+    const int e = a.table_id == 0 ? launch_fwd<0, HIC_LAYOUT_ZIGZAG_I16>(a.plane, h, w, a.stride, a.out, s, e0, e1)
+                                  : launch_fwd<1, HIC_LAYOUT_ZIGZAG_I16>(a.plane, h, w, a.stride, a.out, s, e0, e1);
+    if (e) return e;
+    if (int e2 = rle_tile16_launch(a.out, (int64_t)((h + 7) / 8) * ((w + 7) / 8), max_len, tiles, s)) return e2;
   }
-  const int e = table_id == 0 ? launch_fwd<0, HIC_LAYOUT_ZIGZAG_I16>(plane, h, w, stride, out, s, e0, e1)
-                              : launch_fwd<1, HIC_LAYOUT_ZIGZAG_I16>(plane, h, w, stride, out, s, e0, e1);
-  if (e) return e;
-  const int64_t nblk = (int64_t)((h + 7) / 8) * ((w + 7) / 8);
-  return rle_tile16_launch(out, nblk, max_len, tiles, s);
+  // one launch per table present; the events (if any) time the first of them
+  bool timed = false;
+  for (int t = 0; t < 2; ++t) {
+    DctJobs &J = fastj[t];
+    if (J.n == 0) continue;
+    J.M = max_len;
+    const hipEvent_t a0 = timed ? nullptr : e0, a1 = timed ? nullptr : e1;
+    timed = true;
+    int e;
+    if (t == 0)
+      e = max_len == 15 ? launch_planes<0, HIC_LAYOUT_ZIGZAG_I16, 15>(J, s, a0, a1)
+                        : launch_planes<0, HIC_LAYOUT_ZIGZAG_I16, 0>(J, s, a0, a1);
+    else
+      e = max_len == 15 ? launch_planes<1, HIC_LAYOUT_ZIGZAG_I16, 15>(J, s, a0, a1)
+                        : launch_planes<1, HIC_LAYOUT_ZIGZAG_I16, 0>(J, s, a0, a1);
+    if (e) return e;
+  }
+  return HIC_OK;
 }
 
 extern "C" int hic_dequant_idct_u8(const void *coef, int layout, int64_t H, int64_t W, int table_id,

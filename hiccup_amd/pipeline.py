@@ -5,8 +5,9 @@ half of codec.jpeg_encode (compression.py:16-39, codec.py:286-301) for one
 H x W x 3 uint8 image that already lives in HBM:
 
   1. hic_rgb_to_ycrcb420      RGB -> Y (H x W) + pyrDown'd Cr, Cb (H/2 x W/2)
-  2. hic_dct_quant_rle_u8 x 3 8x8 DCT + quantize + zig-zag -> int16 blocks (ZIGZAG_I16),
-                              with the RLE tile pass fused into the epilogue
+  2. hic_dct_quant_rle_u8_batch  8x8 DCT + quantize + zig-zag of the three planes in
+                              one launch -> int16 blocks (ZIGZAG_I16), with the RLE
+                              tile pass fused into the epilogue
   3. hic_rle_encode_i16_tiles_batch  DC DPCM + channel-wide AC RLE of all three
                               channels (one scan + one emit launch) -> (uint8 len, int16 val)
 
@@ -87,14 +88,17 @@ class Encoder:
         r0, r1 = self.rows
         _lib.call("hic_rgb_to_ycrcb420_rows", device.ptr(rgb), in_row0, rgb.shape[0], self.H, self.W, r0, r1 - r0,
                   device.ptr(self.y), device.ptr(self.cr), device.ptr(self.cb), s)
-        for k in CHANNELS:
+        # DCT + quantize + zig-zag of the three planes in ONE launch, with the RLE tile
+        # pass fused into its epilogue; lum_events (device.KernelEvents) receive the
+        # launch's own begin / end timestamps
+        jobs = (_lib.DctPlaneJob * 3)()
+        for i, k in enumerate(CHANNELS):
             h, w = self.shapes[k]
             p = self.planes[k]
-            # DCT + quantize + zig-zag with the RLE tile pass fused into its epilogue;
-            # lum_events (device.KernelEvents) receive the kernel's own timestamps
-            ev = (lum_events.start, lum_events.stop) if (lum_events is not None and k == "lum") else (None, None)
-            _lib.call("hic_dct_quant_rle_u8", device.ptr(p), h, w, p.stride(0), TABLES[k], self.max_len,
-                      device.ptr(self.coef[k]), device.ptr(self.ws[k]), s, *ev)
+            jobs[i] = _lib.DctPlaneJob(p.data_ptr(), h, w, p.stride(0), TABLES[k], self.coef[k].data_ptr(),
+                                       self.ws[k].data_ptr())
+        ev = (lum_events.start, lum_events.stop) if lum_events is not None else (None, None)
+        _lib.call("hic_dct_quant_rle_u8_batch", 3, jobs, self.max_len, s, *ev)
 
     def shard_summaries(self, stream=None):
         """Per-channel {trailing zeros, has nonzero, first DC, last DC} (sharded encode)."""

@@ -80,6 +80,21 @@ int hic_dct_quant_u8_timed(const uint8_t *plane, int64_t H, int64_t W, int64_t s
  * hic_rle_shard_summary_tiles).  Events as in hic_dct_quant_u8_timed (nullable). */
 int hic_dct_quant_rle_u8(const uint8_t *plane, int64_t H, int64_t W, int64_t stride, int table_id, int max_len,
                          int16_t *out, void *rle_workspace, void *stream, void *ev_start, void *ev_stop);
+/* hic_dct_quant_rle_u8 for up to 3 planes (the Y, Cr, Cb of one image): one
+ * launch per quantisation table, each a persistent grid over all its planes'
+ * 64-block sets.  Each job names its plane, table, ZIGZAG_I16 output and RLE
+ * workspace.  Events (nullable) time the first launch (the luminance one when
+ * the jobs are Y, Cr, Cb).  Ragged planes (H or W not a multiple of 8) take
+ * separate launches. */
+typedef struct {
+  const uint8_t *plane;
+  int64_t H, W, stride;
+  int table_id;
+  int16_t *out;
+  void *rle_workspace;
+} hic_dct_plane_job;
+int hic_dct_quant_rle_u8_batch(int n, const hic_dct_plane_job *jobs, int max_len, void *stream, void *ev_start,
+                               void *ev_stop);
 /* Timing events (hipEvent_t handles) for the *_timed entry points. */
 int hic_event_create(void **h_event);
 int hic_event_destroy(void *event);

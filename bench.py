@@ -85,9 +85,10 @@ def cpu_baseline(budget_s):
 
 
 def load_pmc_traffic():
-    """HBM bytes per luminance-DCT launch from the committed rocprofv3 PMC summary
-    (profiles/pmc_dct_lum.json, FETCH_SIZE doubled per MI355X_MICROARCH.md)."""
-    p = os.path.join(HERE, "profiles", "pmc_dct_lum.json")
+    """HBM bytes per 3-plane DCT launch from the committed rocprofv3 PMC summary
+    (profiles/pmc_dct.json: FETCH_SIZE / WRITE_SIZE calibrated on a kernel of known
+    traffic, MI355X_MICROARCH.md HBM section)."""
+    p = os.path.join(HERE, "profiles", "pmc_dct.json")
     if not os.path.exists(p):
         return None
     with open(p) as f:
@@ -129,7 +130,7 @@ def main():
     inputs = [torch.randint(0, 256, (in_rows, W8K, 3), dtype=torch.uint8, device="cuda", generator=g)
               for _ in range(nin)]
     enc0 = encs[0].enc if world > 1 else encs[0]
-    lum_px = enc0.shapes["lum"][0] * enc0.shapes["lum"][1]
+    dct_px = sum(h * w for h, w in enc0.shapes.values())  # Y + Cr + Cb: one DCT launch
     px_per_step_rank = enc0.pixels
 
     timed_events = []
@@ -139,12 +140,12 @@ def main():
         e = encs[i % len(encs)]
         x = inputs[i % nin]
         ev = None
-        # HIP events carrying the luminance DCT kernel's own begin/end timestamps, on
-        # every 4th timed step (a timestamped dispatch costs the stream a few us)
+        # HIP events carrying the DCT kernel's own begin/end timestamps, on every 4th
+        # timed step (a timestamped dispatch costs the stream a few us)
         if record and (i - args.warmup) % 4 == 0:
             ev = event_pool[len(timed_events)]
             timed_events.append(ev)
-        e.encode(x, lum_events=ev)
+        e.encode(x, dct_events=ev)
         if world > 1 and args.gather:
             sharding.gather_streams(e)
 
@@ -167,11 +168,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # ---- dominant kernel: luminance DCT+quantize+zig-zag.  Its launches inside the
-    # timed steps go through hic_dct_quant_u8_timed, which hands the two HIP events
-    # to hipExtLaunchKernelGGL: they hold that dispatch's begin / end timestamps.
+    # ---- roofline kernel: the DCT+quantize+zig-zag pass (one launch for the three
+    # planes).  hic_dct_quant_rle_u8_batch hands the two HIP events to
+    # hipExtLaunchKernelGGL: they hold that dispatch's begin / end timestamps.
     dct_us = float(np.mean([ev.elapsed_ms() for ev in timed_events])) * 1e3
-    dct_px = lum_px  # the timed launch is the luminance one
     achieved = dct_px * 3 / (dct_us * 1e-6) / 1e9  # u8 in + int16 out per pixel
 
     if rank == 0:
@@ -202,8 +202,8 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_dct_planes<lum,ZIGZAG_I16,15> (Y 4320x7680: AAN DCT + quantize + zig-zag + RLE "
-                          "tile records; Cr + Cb follow in one launch of the same kernel with the chroma table)",
+                "kernel": "k_dct_planes<-1,ZIGZAG_I16,15> (Y 4320x7680 + Cr, Cb 2160x3840 in one launch: "
+                          "AAN DCT + quantize + zig-zag + RLE tile records, per-plane table)",
                 "timed_launches": len(timed_events),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,

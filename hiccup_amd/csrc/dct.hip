@@ -244,12 +244,14 @@ __global__ __launch_bounds__(256) void k_dequant_idct(const void *__restrict__ c
   }
 }
 
-// Production forward kernel for aligned planes, for up to three planes of one
-// quantisation table per launch (Cr + Cb of one image: one persistent grid over
-// both planes' sets keeps every SIMD busy, where a chroma plane alone leaves a
-// third of the waves idle).  One
-// 8x8 block per lane, 64 consecutive raster-order blocks ("a set" = one RLE tile)
-// per wave iteration; persistent grid sized to the waves that fit at once.
+// Production forward kernel for aligned planes: up to three planes per launch
+// (Y, Cr, Cb of one image), one persistent grid over all their sets.  TABLE = -1:
+// each plane's quantisation table is read at run time (its constants become scalar
+// loads), so the three planes share one launch and one tail -- separate launches
+// per table left a third of the waves idle in each tail.  TABLE = 0 / 1: a
+// compile-time table (single-table callers).  One 8x8 block per lane, 64
+// consecutive raster-order blocks ("a set" = one RLE tile) per wave iteration;
+// persistent grid sized to the waves that fit at once.
 // dct_block_aan (dct_core.h) writes the quantized coefficients straight to their
 // slot in an LDS stage, which is copied out so that every store instruction writes
 // one contiguous 1 KiB segment (zig-zag layout) or whole 16-byte row pieces
@@ -271,7 +273,9 @@ struct DctJobs {
 template <int TABLE, int LAYOUT, int TMF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_dct_planes(DctJobs jobs, int path) {
   __shared__ uint4 s_stage[4 * 64 * kStagePad];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // wv is wave-uniform: keep it (and the set / job indices derived from it) in
+  // SGPRs, so the job fields are scalar loads, not vector loads on vmcnt
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nwaves = gridDim.x * 4;
   const int g0 = blockIdx.x * 4 + wv;
   uint4 *st4 = s_stage + wv * 64 * kStagePad;
@@ -351,7 +355,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
       uint2 w[8];
       load(J, set, w);
       bool t26;
-      const bool f = dct_block_aan<TABLE, LAYOUT>(w, st, &t26);
+      const bool f = dct_block_aan<TABLE, LAYOUT>(w, st, &t26, nullptr, J.table);
       if (__builtin_amdgcn_ballot_w64(f) != 0 && path == 1) redo |= 1ull << i;
       if (__builtin_amdgcn_ballot_w64(t26) != 0 && path == 1) fix |= 1ull << i;
       store(J, set);
@@ -372,7 +376,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     uint2 w[8];
     load(J, set, w);
     int q[4];
-    dct_fix26<TABLE>(w, q);
+    dct_fix26<TABLE>(w, q, J.table);
     if (blk < J.nblk) {
       constexpr SlotOf<LAYOUT> kSlot{};
       constexpr int idx[4] = {18, 22, 50, 54};
@@ -414,7 +418,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     const int set = g - J.set0;
     uint2 w[8];
     load(J, set, w);
-    dct_block_2ph<TABLE, LAYOUT>(w, st);
+    dct_block_2ph<TABLE, LAYOUT>(w, st, J.table);
     store(J, set);
   }
 }
@@ -535,10 +539,13 @@ int launch_planes(DctJobs &jobs, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   if (cap > 0 && (total + cap - 1) / cap > 64) cap = (total + 63) / 64;  // <= 64 sets per wave (redo mask)
   const int waves = (cap == 0 || total < cap) ? total : cap;
   const dim3 grid((waves + 3) / 4), block(256);
-  if (e0 || e1)
-    hipExtLaunchKernelGGL((k_dct_planes<TABLE, LAYOUT, TMF>), grid, block, 0, s, e0, e1, 0, jobs, dct_path());
-  else
-    hipLaunchKernelGGL((k_dct_planes<TABLE, LAYOUT, TMF>), grid, block, 0, s, jobs, dct_path());
+  auto go = [&](auto kernel) {
+    if (e0 || e1)
+      hipExtLaunchKernelGGL(kernel, grid, block, 0, s, e0, e1, 0, jobs, dct_path());
+    else
+      hipLaunchKernelGGL(kernel, grid, block, 0, s, jobs, dct_path());
+  };
+  go(k_dct_planes<TABLE, LAYOUT, TMF>);
   return check_launch("k_dct_planes");
 }
 
@@ -630,7 +637,13 @@ extern "C" int hic_dct_quant_rle_u8_batch(int n, const hic_dct_plane_job *jobs, 
   if (max_len < 1 || max_len > 256) return arg_error("max_len must be in [1, 256]");
   hipStream_t s = as_stream(stream);
   const hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
-  DctJobs fastj[2] = {};  // per quantisation table
+  // fast-path planes: one launch for all of them (the kernel reads each plane's
+  // table at run time); HIC_DCT_MERGE=0 (A/B knob): one launch per table
+  static const bool merge = [] {
+    const char *v = getenv("HIC_DCT_MERGE");
+    return !(v && v[0] == '0');
+  }();
+  DctJobs fastj[2] = {};
   for (int k = 0; k < n; ++k) {
     const hic_dct_plane_job &a = jobs[k];
     if (!a.plane || !a.out || !a.rle_workspace) return arg_error("plane %d: null pointer", k);
@@ -639,7 +652,7 @@ extern "C" int hic_dct_quant_rle_u8_batch(int n, const hic_dct_plane_job *jobs, 
     const int h = (int)a.H, w = (int)a.W;
     int64_t *tiles = static_cast<int64_t *>(a.rle_workspace);
     if (fwd_fast(h, w, a.stride, a.plane, a.out) && dct_variant() == 3) {
-      DctJobs &J = fastj[a.table_id];
+      DctJobs &J = fastj[merge ? 0 : a.table_id];
       J.j[J.n++] = make_job(a.plane, h, w, a.stride, a.table_id, a.out, tiles);
       continue;
     }
@@ -649,7 +662,7 @@ extern "C" int hic_dct_quant_rle_u8_batch(int n, const hic_dct_plane_job *jobs, 
     if (e) return e;
     if (int e2 = rle_tile16_launch(a.out, (int64_t)((h + 7) / 8) * ((w + 7) / 8), max_len, tiles, s)) return e2;
   }
-  // one launch per table present; the events (if any) time the first of them
+  // the events (if any) time the first launch
   bool timed = false;
   for (int t = 0; t < 2; ++t) {
     DctJobs &J = fastj[t];
@@ -658,7 +671,10 @@ extern "C" int hic_dct_quant_rle_u8_batch(int n, const hic_dct_plane_job *jobs, 
     const hipEvent_t a0 = timed ? nullptr : e0, a1 = timed ? nullptr : e1;
     timed = true;
     int e;
-    if (t == 0)
+    if (merge)
+      e = max_len == 15 ? launch_planes<-1, HIC_LAYOUT_ZIGZAG_I16, 15>(J, s, a0, a1)
+                        : launch_planes<-1, HIC_LAYOUT_ZIGZAG_I16, 0>(J, s, a0, a1);
+    else if (t == 0)
       e = max_len == 15 ? launch_planes<0, HIC_LAYOUT_ZIGZAG_I16, 15>(J, s, a0, a1)
                         : launch_planes<0, HIC_LAYOUT_ZIGZAG_I16, 0>(J, s, a0, a1);
     else

@@ -201,16 +201,22 @@ struct SlotOf {
   }
 };
 
+// TABLE >= 0: the table is a compile-time constant; TABLE == -1: it is `trt`
+// (wave-uniform at run time, so the constants become scalar loads).  The same
+// convention holds for every TABLE-templated block function below.
 template <int TABLE>
-__host__ __device__ __forceinline__ int quant_fast(double b, int i) {
-  if (pow2(kQ.d[TABLE][i])) return (int)__builtin_rint(b * kQ.r[TABLE][i]);  // exact product
+__host__ __device__ __forceinline__ int quant_fast(double b, int i, int trt = 0) {
+  constexpr int kT = TABLE >= 0 ? TABLE : 0;
+  const int t = TABLE >= 0 ? TABLE : trt;
+  if (TABLE >= 0 && pow2(kQ.d[kT][i])) return (int)__builtin_rint(b * kQ.r[kT][i]);  // exact product
   // one rounding of the exact product b*(1/D) to a multiple of 2^-19 (FMA: the
-  // tie test below is then about b*(1/D) itself, within 2^-53 relative of b/D)
-  const double t = __builtin_fma(b, kQ.r[TABLE][i], 0x1.8p33);
-  const int n = (int)(uint32_t)__builtin_bit_cast(unsigned long long, t);
+  // tie test below is then about b*(1/D) itself, within 2^-53 relative of b/D;
+  // a power-of-two D makes the product exact and the test exact too)
+  const double tt = __builtin_fma(b, kQ.r[t][i], 0x1.8p33);
+  const int n = (int)(uint32_t)__builtin_bit_cast(unsigned long long, tt);
   const int sft = n + (1 << 18);
   int q = sft >> 19;
-  if ((sft & 0x7FFFF) == 0) q = (int)__builtin_rint(b / kQ.d[TABLE][i]);
+  if ((sft & 0x7FFFF) == 0) q = (int)__builtin_rint(b / kQ.d[t][i]);
   return q;
 }
 
@@ -223,7 +229,7 @@ constexpr int kStagePad = 9;  // uint4 per block in the LDS stage (8 + 1 pad: co
 // outputs (1, 3, 5, 7) the odd columns.  Live state is ~half of a one-pass
 // block, at the cost of recomputing 4 integer sums per row.
 template <int TABLE, int LAYOUT>
-__host__ __device__ __forceinline__ void dct_block_2ph(uint2 (&w)[8], int16_t *st) {
+__host__ __device__ __forceinline__ void dct_block_2ph(uint2 (&w)[8], int16_t *st, int trt = 0) {
   constexpr SlotOf<LAYOUT> kSlot{};
   auto px = [&](int r, int n) -> int {
     return (int)(((n < 4 ? w[r].x : w[r].y) >> (8 * (n & 3))) & 0xFFu) - 128;
@@ -251,20 +257,20 @@ __host__ __device__ __forceinline__ void dct_block_2ph(uint2 (&w)[8], int16_t *s
       int b0;
       double b[8];
       dct8h_int(e0, b0, b);
-      st[kSlot.s[0]] = (int16_t)quant_fast<TABLE>((double)b0, 0);
+      st[kSlot.s[0]] = (int16_t)quant_fast<TABLE>((double)b0, 0, trt);
 #pragma unroll
-      for (int u = 1; u < 8; ++u) st[kSlot.s[u * 8]] = (int16_t)quant_fast<TABLE>(b[u], u * 8);
+      for (int u = 1; u < 8; ++u) st[kSlot.s[u * 8]] = (int16_t)quant_fast<TABLE>(b[u], u * 8, trt);
     }
     double b[8];
     dct8h(e2, b);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) st[kSlot.s[u * 8 + 2]] = (int16_t)quant_fast<TABLE>(b[u], u * 8 + 2);
+    for (int u = 0; u < 8; ++u) st[kSlot.s[u * 8 + 2]] = (int16_t)quant_fast<TABLE>(b[u], u * 8 + 2, trt);
     dct8h(e4, b);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) st[kSlot.s[u * 8 + 4]] = (int16_t)quant_fast<TABLE>(b[u], u * 8 + 4);
+    for (int u = 0; u < 8; ++u) st[kSlot.s[u * 8 + 4]] = (int16_t)quant_fast<TABLE>(b[u], u * 8 + 4, trt);
     dct8h(e6, b);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) st[kSlot.s[u * 8 + 6]] = (int16_t)quant_fast<TABLE>(b[u], u * 8 + 6);
+    for (int u = 0; u < 8; ++u) st[kSlot.s[u * 8 + 6]] = (int16_t)quant_fast<TABLE>(b[u], u * 8 + 6, trt);
   }
   // ---- phase B: odd row outputs -> odd columns.  Re-unpack the pixels (the asm
   // makes w opaque, so the compiler cannot keep 64 unpacked ints live across phases)
@@ -298,16 +304,16 @@ __host__ __device__ __forceinline__ void dct_block_2ph(uint2 (&w)[8], int16_t *s
     double b[8];
     dct8h(o1, b);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) st[kSlot.s[u * 8 + 1]] = (int16_t)quant_fast<TABLE>(b[u], u * 8 + 1);
+    for (int u = 0; u < 8; ++u) st[kSlot.s[u * 8 + 1]] = (int16_t)quant_fast<TABLE>(b[u], u * 8 + 1, trt);
     dct8h(o3, b);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) st[kSlot.s[u * 8 + 3]] = (int16_t)quant_fast<TABLE>(b[u], u * 8 + 3);
+    for (int u = 0; u < 8; ++u) st[kSlot.s[u * 8 + 3]] = (int16_t)quant_fast<TABLE>(b[u], u * 8 + 3, trt);
     dct8h(o5, b);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) st[kSlot.s[u * 8 + 5]] = (int16_t)quant_fast<TABLE>(b[u], u * 8 + 5);
+    for (int u = 0; u < 8; ++u) st[kSlot.s[u * 8 + 5]] = (int16_t)quant_fast<TABLE>(b[u], u * 8 + 5, trt);
     dct8h(o7, b);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) st[kSlot.s[u * 8 + 7]] = (int16_t)quant_fast<TABLE>(b[u], u * 8 + 7);
+    for (int u = 0; u < 8; ++u) st[kSlot.s[u * 8 + 7]] = (int16_t)quant_fast<TABLE>(b[u], u * 8 + 7, trt);
   }
 }
 
@@ -317,13 +323,12 @@ __host__ __device__ __forceinline__ void dct_block_2ph(uint2 (&w)[8], int16_t *s
 // the pocketfft replica.  Its outputs are y_k / S_k with S_0 = 2 and
 // S_k = 1 / cos(k*pi/16); the 2-D scale S_u S_v is folded into the quantiser
 // constant kRA = S_u S_v / T.  The fast result differs from pocketfft's float64
-// value only by rounding (both within ~1e-10 of the real DCT), so rint(y / T)
-// agrees wherever y / T is not within the quantiser's tie window (2^-20, four
-// orders above that error).  Lanes whose block has any coefficient inside the
-// window redo the block on the exact pocketfft path (dct_block_2ph).  The only
-// coefficients that can be EXACT ties are (0,0) (an integer) and (4,4) (an
-// integer times cos(pi/4)^2): both are computed here with pocketfft's own
-// operation sequence, so they never need the fallback.
+// value only by rounding, so rint(y / T) agrees wherever y / T is not within the
+// quantiser's tie window (2^-31 of a half-integer, see qfast).  A block with a
+// coefficient inside the window is reported to the caller: the (2,2) class apart
+// (dct_fix26), anything else for a redo on the exact pocketfft path
+// (dct_block_2ph).  (0,0) (an integer) and (4,4) (an integer times cos(pi/4)^2)
+// are computed here with pocketfft's own operation sequence.
 constexpr double kA1 = 0x1.6a09e667f3bcdp-1;  // cos(pi/4)
 constexpr double kA2 = 0x1.1517a7bdb3895p-1;  // cos(pi/8) - cos(3pi/8)
 constexpr double kA4 = 0x1.4e7ae9144f0fcp+0;  // cos(pi/8) + cos(3pi/8)
@@ -393,25 +398,32 @@ __host__ __device__ __forceinline__ void aan_odd(T x0, T x1, T x2, T x3, T x4, T
   o7 = z11 - z4;
 }
 
-// Fast quantiser: q = round(b * r).  t = fma(b, r, 1.5*2^22 + 1/2) rounds b*r + 1/2
-// to a multiple of 2^-30 (|b*r| < 2^21); bits 30.. of its bit pattern, less those
-// of the constant itself, are floor(b*r + 1/2).  The low 30 bits are zero exactly
-// when b*r lies within 2^-31 of a half-integer: `tie` keeps their minimum.  The
-// fast estimate of y/T is within 2^-41 of pocketfft's (tools/check/aan_err.hip,
-// 4M blocks incl. saturated patterns), three orders of magnitude inside the
-// window, so an unflagged q is pocketfft's q.
-constexpr double kQMagic = 0x1.8p22 + 0.5;
-constexpr uint32_t kQBase = (uint32_t)(__builtin_bit_cast(unsigned long long, kQMagic) >> 30);
+// Fast quantiser: q = round(b * r).  t = fma(b, r, 1.5*2^20 + 1/2 + 2^-30) rounds
+// b*r + 1/2 + 2^-30 to a multiple of 2^-32 (|b*r| < 2^19).  The high word of its bit
+// pattern is the constant's exponent over 2^19 + floor(b*r + 1/2 + 2^-30), so its
+// low 16 bits are q's (all an int16 output needs: no shift, no subtract); the low
+// word is the rounded fraction in units of 2^-32, offset by 4.  b*r + 1/2 within
+// 2^-31 of an integer (a quantiser tie) gives a low word of 2..6, and the 2^-30
+// offset can only change q where the fraction was within 2^-30 below an integer,
+// which gives 0..4: `tie` keeps the minimum low word, and any value <= kTieMax
+// flags the block.  The fast estimate of y/T is within 2^-41 of pocketfft's
+// (tools/check/aan_err.hip, 4M blocks incl. saturated patterns), three orders of
+// magnitude inside the window, so an unflagged q is pocketfft's q.
+constexpr double kQMagic = 0x1.8p20 + 0.5 + 0x1p-30;
+constexpr uint32_t kQHi = (uint32_t)(__builtin_bit_cast(unsigned long long, 0x1.8p20) >> 32);
+constexpr uint32_t kTieMax = 6;
 __host__ __device__ __forceinline__ int qfast(double b, double r, uint32_t &tie) {
   const unsigned long long t = __builtin_bit_cast(unsigned long long, __builtin_fma(b, r, kQMagic));
-  const uint32_t low = (uint32_t)t & 0x3FFFFFFFu;
-  tie = tie < low ? tie : low;
-  return (int)((uint32_t)(t >> 30) - kQBase);
+  const uint32_t lo = (uint32_t)t;
+  tie = tie < lo ? tie : lo;
+  return (int)((uint32_t)(t >> 32) - kQHi);
 }
 
 // One block on the fast path; returns true if it must be redone exactly.
 template <int TABLE, int LAYOUT>
-__host__ __device__ __forceinline__ bool dct_block_aan(uint2 (&w)[8], int16_t *st, bool *tie26_out = nullptr, double *dbg = nullptr) {
+__host__ __device__ __forceinline__ bool dct_block_aan(uint2 (&w)[8], int16_t *st, bool *tie26_out = nullptr,
+                                                       double *dbg = nullptr, int trt = 0) {
+  const int tb = TABLE >= 0 ? TABLE : trt;
   constexpr SlotOf<LAYOUT> kSlot{};
   // dbg (host error analysis only): b * kRA, i.e. this path's estimate of y / T
   // (2,2), (2,6), (6,2), (6,6): y = A + B*sqrt(2) with rational A, B, an exact tie
@@ -419,9 +431,9 @@ __host__ __device__ __forceinline__ bool dct_block_aan(uint2 (&w)[8], int16_t *s
   // (*tie26_out) for dct_fix26, which recomputes just these four coefficients.
   uint32_t tie26 = 0xFFFFFFFFu;
   auto qf = [&](double b, int i, uint32_t &t) {
-    if (dbg) dbg[i] = b * kRA[TABLE][i];
+    if (dbg) dbg[i] = b * kRA[tb][i];
     const bool c26 = (i == 18 || i == 22 || i == 50 || i == 54);
-    return qfast(b, kRA[TABLE][i], c26 ? tie26 : t);
+    return qfast(b, kRA[tb][i], c26 ? tie26 : t);
   };
   // raw bytes: the -128 offset of dct_channel only reaches row output 0 (the
   // DCT's other basis rows sum to zero), corrected there by -8 * 128 per row
@@ -444,7 +456,7 @@ __host__ __device__ __forceinline__ bool dct_block_aan(uint2 (&w)[8], int16_t *s
       double c[8];
       aan_even<int>(e0[0], e0[1], e0[2], e0[3], e0[4], e0[5], e0[6], e0[7], c0, c4, c[2], c[6]);
       aan_odd<int>(e0[0], e0[1], e0[2], e0[3], e0[4], e0[5], e0[6], e0[7], c[1], c[3], c[5], c[7]);
-      st[kSlot.s[0]] = (int16_t)quant_fast<TABLE>((double)c0, 0);
+      st[kSlot.s[0]] = (int16_t)quant_fast<TABLE>((double)c0, 0, trt);
       st[kSlot.s[32]] = (int16_t)qf((double)c4, 32, tie);
 #pragma unroll
       for (int u = 1; u < 8; ++u)
@@ -465,7 +477,7 @@ __host__ __device__ __forceinline__ bool dct_block_aan(uint2 (&w)[8], int16_t *s
       for (int r = 0; r < 8; ++r) y[r] = (double)e4[r] * TW3;  // pocketfft row output 4 (half scale)
       const double c1 = y[1] + y[2], c3 = y[3] + y[4], c5 = y[5] + y[6], H0 = y[0] + y[7];
       const double h1 = c1 + c5, T2 = H0 + c3;
-      st[kSlot.s[36]] = (int16_t)quant_fast<TABLE>((T2 - h1) * TW3, 36);
+      st[kSlot.s[36]] = (int16_t)quant_fast<TABLE>((T2 - h1) * TW3, 36, trt);
     }
     // columns 2, 6
 #pragma unroll
@@ -504,15 +516,15 @@ __host__ __device__ __forceinline__ bool dct_block_aan(uint2 (&w)[8], int16_t *s
       for (int u = 0; u < 8; ++u) st[kSlot.s[u * 8 + v]] = (int16_t)qf(c[u], u * 8 + v, tie);
     }
   }
-  if (tie26_out) *tie26_out = tie26 == 0;
-  return tie == 0;
+  if (tie26_out) *tie26_out = tie26 <= kTieMax;
+  return tie <= kTieMax;
 }
 
 // The four (2,2)-class coefficients with pocketfft's own operations (rows' outputs
 // 2 and 6, then columns 2 and 6), quantised exactly; q[] = raster (2,2), (2,6),
 // (6,2), (6,6).
 template <int TABLE>
-__host__ __device__ __forceinline__ void dct_fix26(const uint2 (&w)[8], int (&q)[4]) {
+__host__ __device__ __forceinline__ void dct_fix26(const uint2 (&w)[8], int (&q)[4], int trt = 0) {
   auto px = [&](int r, int n) -> int { return (int)(((n < 4 ? w[r].x : w[r].y) >> (8 * (n & 3))) & 0xFFu); };
   double y2[8], y6[8];
 #pragma unroll
@@ -533,8 +545,8 @@ __host__ __device__ __forceinline__ void dct_fix26(const uint2 (&w)[8], int (&q)
     const double T1 = (X[0] + X[7]) - (X[3] + X[4]), h2 = c2 - c6;
     const double D6 = T1 + h2, D2 = T1 - h2;
     const double P1 = TW1 * D6 + TW5 * D2, P2 = TW1 * D2 - TW5 * D6;
-    q[k] = quant_fast<TABLE>(P1 + P2, 16 + v);
-    q[2 + k] = quant_fast<TABLE>(P1 - P2, 48 + v);
+    q[k] = quant_fast<TABLE>(P1 + P2, 16 + v, trt);
+    q[2 + k] = quant_fast<TABLE>(P1 - P2, 48 + v, trt);
   }
 }
 

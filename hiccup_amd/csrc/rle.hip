@@ -673,7 +673,7 @@ __global__ __launch_bounds__(kScanT) void k_rle_scan16b(RleJobs16 jobs, uint32_t
         bool ok = false;
         for (int spin = 0; spin < (1 << 22) && !ok; ++spin) {
           int64_t f, l, c;
-          ok = get_granule(gran + 3 * q + 0, tag, f) & get_granule(gran + 3 * q + 1, tag, l) &
+          ok = (int)get_granule(gran + 3 * q + 0, tag, f) & (int)get_granule(gran + 3 * q + 1, tag, l) &
                get_granule(gran + 3 * q + 2, tag, c);
           if (ok) a = Agg{f, l, c};
           else __builtin_amdgcn_s_sleep(2);

@@ -97,6 +97,18 @@ __device__ __forceinline__ uint32_t zip16(uint32_t a, uint32_t b) {
   return spread(a) | (spread(b) << 1);
 }
 
+// v_pk_min_u16 (the compiler rewrites a vector min with 1 into compares)
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+#ifdef __HIP_DEVICE_COMPILE__
+  uint32_t r;
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+#else
+  const uint32_t lo = (a & 0xFFFFu) < (b & 0xFFFFu) ? (a & 0xFFFFu) : (b & 0xFFFFu);
+  const uint32_t hi = (a >> 16) < (b >> 16) ? (a >> 16) : (b >> 16);
+  return lo | hi << 16;
+#endif
+}
 // Nonzero mask of a zig-zag int16 block held as 32 packed dwords: bit s set iff
 // slot s != 0.  v_pk_min_u16(w, 1) turns each half into its 0/1 flag.
 __device__ __forceinline__ uint64_t nz_mask16(const uint32_t (&w)[32]) {
@@ -106,9 +118,7 @@ __device__ __forceinline__ uint64_t nz_mask16(const uint32_t (&w)[32]) {
     uint32_t acc = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-      const uint32_t x = w[16 * h + k];
-      const uint32_t f = ((x & 0xFFFFu) != 0 ? 1u : 0u) | ((x >> 16) != 0 ? 0x10000u : 0u);
-      acc |= f << k;
+      acc |= pk_min_u16(w[16 * h + k], 0x00010001u) << k;
     }
     lo[h] = acc & 0xFFFFu;  // even slots 32h + 2k
     hi[h] = acc >> 16;      // odd slots 32h + 2k + 1
@@ -191,11 +201,11 @@ __device__ __forceinline__ void tile_record16(const uint32_t (&w)[32], bool vali
   const int total = wave_last_i32(wave_incl_sum_i32(cnt));
   const int all_last = wave_last_i32(incl);
   const int64_t base = (b - lane) * 63;  // the tile's first AC element
-  if (first >= 0 && prev < 0) rec[0] = base + lane * 63 + first;
+  // rec[0]: the lane of the tile's first nonzero, or lane 0 (-1) in a tile without one
+  if (all_last < 0 ? lane == 0 : (first >= 0 && prev < 0)) rec[0] = all_last < 0 ? -1 : base + lane * 63 + first;
   if (lane == 0) {
     rec[1] = all_last >= 0 ? base + all_last : -1;
     rec[2] = total;
-    if (all_last < 0) rec[0] = -1;
   }
 }
 

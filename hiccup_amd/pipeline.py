@@ -78,7 +78,7 @@ class Encoder:
         """Image rows [in0, in1) this encoder reads: its rows plus the pyrDown halo."""
         return input_span(self.H, *self.rows)
 
-    def transform(self, rgb, stream=None, in_row0=None, lum_events=None):
+    def transform(self, rgb, stream=None, in_row0=None, dct_events=None):
         """Steps 1-2: colour + 4:2:0 + DCT/quantize/zig-zag of the three planes.
         rgb holds image rows [in_row0, in_row0 + rgb.shape[0]) (default: the
         whole image for an unsharded encoder, input_span() for a shard)."""
@@ -88,16 +88,16 @@ class Encoder:
         r0, r1 = self.rows
         _lib.call("hic_rgb_to_ycrcb420_rows", device.ptr(rgb), in_row0, rgb.shape[0], self.H, self.W, r0, r1 - r0,
                   device.ptr(self.y), device.ptr(self.cr), device.ptr(self.cb), s)
-        # DCT + quantize + zig-zag of the three planes in ONE launch, with the RLE tile
-        # pass fused into its epilogue; lum_events (device.KernelEvents) receive the
-        # launch's own begin / end timestamps
+        # DCT + quantize + zig-zag of the three planes in ONE launch (each plane with
+        # its own table), with the RLE tile pass fused into its epilogue; dct_events
+        # (device.KernelEvents) receive the launch's own begin / end timestamps
         jobs = (_lib.DctPlaneJob * 3)()
         for i, k in enumerate(CHANNELS):
             h, w = self.shapes[k]
             p = self.planes[k]
             jobs[i] = _lib.DctPlaneJob(p.data_ptr(), h, w, p.stride(0), TABLES[k], self.coef[k].data_ptr(),
                                        self.ws[k].data_ptr())
-        ev = (lum_events.start, lum_events.stop) if lum_events is not None else (None, None)
+        ev = (dct_events.start, dct_events.stop) if dct_events is not None else (None, None)
         _lib.call("hic_dct_quant_rle_u8_batch", 3, jobs, self.max_len, s, *ev)
 
     def shard_summaries(self, stream=None):
@@ -122,8 +122,8 @@ class Encoder:
                                     self.counts[i:i + 1].data_ptr(), self.ws[k].data_ptr())
         _lib.call("hic_rle_encode_i16_tiles_batch", 3, jobs, self.max_len, s)
 
-    def encode(self, rgb, stream=None, lum_events=None):
-        self.transform(rgb, stream, lum_events=lum_events)
+    def encode(self, rgb, stream=None, dct_events=None):
+        self.transform(rgb, stream, dct_events=dct_events)
         self.entropy(stream)
 
     def result(self):

@@ -91,10 +91,10 @@ class ShardEncoder:
     def pixels(self):
         return self.enc.pixels
 
-    def encode(self, rgb_rows, stream=None, lum_events=None):
+    def encode(self, rgb_rows, stream=None, dct_events=None):
         """rgb_rows: device uint8 tensor of image rows self.span (shard + halo)."""
         enc = self.enc
-        enc.transform(rgb_rows, stream, in_row0=self.span[0], lum_events=lum_events)
+        enc.transform(rgb_rows, stream, in_row0=self.span[0], dct_events=dct_events)
         summ = enc.shard_summaries(stream)
         # the exchange step: 96 bytes per rank over RCCL
         _all_gather(self.all_summ.view(self.world * 3, 4), summ, group=self.group)

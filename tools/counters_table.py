@@ -2,7 +2,7 @@
 import csv, re, sys, os, collections
 d = sys.argv[1]
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
-for sub in ("sq", "sq2", "fetch", "write"):
+for sub in sorted(os.listdir(d)):
     f = os.path.join(d, sub, "run_counter_collection.csv")
     if not os.path.exists(f):
         continue

@@ -1,5 +1,5 @@
 // Calibration for the DCT kernel's HBM counters (dev tool).
-// k_pattern reads an 8K uint8 plane with exactly k_dct_quant_2ph's access
+// k_pattern reads an 8K uint8 plane with exactly k_dct_planes' access
 // pattern: lane = one 8x8 block, 8 x 8-byte row loads.  It writes int16 [nblk][64]
 // with 16-B-per-lane streaming stores, and does no arithmetic.  Known bytes:
 // 1 B/px read, 2 B/px written.  rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE over this

@@ -1,11 +1,11 @@
 """Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (dev tool).
 
-usage: python tools/pmc_summary.py gpurun_out/prof_<tag> [profiles/pmc_dct_lum.json]
+usage: python tools/pmc_summary.py gpurun_out/prof_<tag> [profiles/pmc_dct.json]
 
-Reads <dir>/pmc_{FETCH,WRITE}_SIZE (8K luma DCT driver, tools/prof_dct.py) and
-<dir>/cal_{FETCH,WRITE}_SIZE (tools/micro/cal_traffic.hip: the DCT's exact
-access pattern with known bytes).  It then writes the per-launch HBM traffic of
-the luma DCT kernel.  Units: FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950,
+Reads <dir>/pmc_{FETCH,WRITE}_SIZE (the 8K 3-plane DCT driver, tools/prof_dct.py)
+and <dir>/cal_{FETCH,WRITE}_SIZE (tools/micro/cal_traffic.hip: the DCT's access
+pattern with known bytes).  It then writes the per-launch HBM traffic of the
+DCT kernel (Y + Cr + Cb in one launch).  Units: FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950,
 FETCH_SIZE reports half the bytes of wide streaming reads
 (MI355X_MICROARCH.md, HBM section).  Our read pattern is 8 B per lane, so the
 read factor is calibrated on cal_traffic rather than assumed.
@@ -42,14 +42,16 @@ def mean(v):
 def main():
     d = sys.argv[1]
     dst = sys.argv[2] if len(sys.argv) > 2 else None
-    px = H * W
-    res = {"source": d, "plane": [H, W], "algorithmic_read_bytes": px, "algorithmic_write_bytes": 2 * px}
+    cpx = H * W  # calibration kernel: one 8K plane
+    px = H * W + 2 * (H // 2) * (W // 2)  # the DCT launch: Y + Cr + Cb
+    res = {"source": d, "planes": [[H, W], [H // 2, W // 2], [H // 2, W // 2]], "algorithmic_read_bytes": px,
+           "algorithmic_write_bytes": 2 * px}
     cal_f = per_kernel(os.path.join(d, "cal_FETCH_SIZE"), "FETCH_SIZE")
     cal_w = per_kernel(os.path.join(d, "cal_WRITE_SIZE"), "WRITE_SIZE")
     kf = [k for k in cal_f if k.startswith("k_pattern")][0]
     kw = [k for k in cal_w if k.startswith("k_pattern")][0]
-    rf = mean(cal_f[kf][4:]) / px          # counter bytes per known read byte
-    rw = mean(cal_w[kw][4:]) / (2 * px)    # counter bytes per known written byte
+    rf = mean(cal_f[kf][4:]) / cpx          # counter bytes per known read byte
+    rw = mean(cal_w[kw][4:]) / (2 * cpx)    # counter bytes per known written byte
     res["calibration"] = {"kernel": "tools/micro/cal_traffic.hip k_pattern", "fetch_counter_per_byte": round(rf, 4),
                           "write_counter_per_byte": round(rw, 4)}
     f = per_kernel(os.path.join(d, "pmc_FETCH_SIZE"), "FETCH_SIZE")
@@ -62,10 +64,10 @@ def main():
         wb = mean(w[k][2:] if len(w.get(k, [])) > 2 else w.get(k, [0.0]))
         res["kernels"][k] = {"fetch_counter_bytes": round(fb), "write_counter_bytes": round(wb),
                              "read_bytes_calibrated": round(fb / rf), "write_bytes_calibrated": round(wb / rw)}
-    lum = [k for k in res["kernels"] if k.startswith("k_dct_quant_2ph<0, 2, 15>")]
-    if lum:
-        r = res["kernels"][lum[0]]
-        res["dct_lum_kernel"] = lum[0]
+    dk = [k for k in res["kernels"] if k.startswith("k_dct_planes<-1, 2, 15")]
+    if dk:
+        r = res["kernels"][dk[0]]
+        res["dct_kernel"] = dk[0]
         res["hbm_bytes_per_launch"] = r["read_bytes_calibrated"] + r["write_bytes_calibrated"]
     txt = json.dumps(res, indent=1)
     print(txt)

@@ -28,6 +28,6 @@ for sub in ("pmc_FETCH_SIZE", "pmc_WRITE_SIZE", "cal_FETCH_SIZE", "cal_WRITE_SIZ
         for r in keep:
             w.writerow({k: r[k] for k in fields})
 out = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "pmc_summary.py"), src,
-                      os.path.join("profiles", "pmc_dct_lum.json")], capture_output=True, text=True)
+                      os.path.join("profiles", "pmc_dct.json")], capture_output=True, text=True)
 print(out.stdout[-400:], out.stderr[-400:])
 print(json.loads(lines[-1])["roofline"])

@@ -272,20 +272,28 @@ struct DctJobs {
 
 template <int TABLE, int LAYOUT, int TMF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_dct_planes(DctJobs jobs, int path) {
-  __shared__ uint4 s_stage[4 * 64 * kStagePad];
+  __shared__ uint2 s_stage[4 * 64 * kStageU2];
   // wv is wave-uniform: keep it (and the set / job indices derived from it) in
   // SGPRs, so the job fields are scalar loads, not vector loads on vmcnt
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nwaves = gridDim.x * 4;
   const int g0 = blockIdx.x * 4 + wv;
-  uint4 *st4 = s_stage + wv * 64 * kStagePad;
-  int16_t *st = reinterpret_cast<int16_t *>(st4 + lane * kStagePad);
+  uint2 *st2 = s_stage + wv * 64 * kStageU2;
+  int16_t *st = reinterpret_cast<int16_t *>(st2 + lane * kStageU2);
+  // 16 B of block b's stage row, at 8-byte granularity (ds_read_b64 pairs)
+  auto st16 = [&](int b, int k) {
+    const uint2 lo = st2[b * kStageU2 + 2 * k], hi = st2[b * kStageU2 + 2 * k + 1];
+    return make_uint4(lo.x, lo.y, hi.x, hi.y);
+  };
   const int M = jobs.M;
 
+  // g is wave-uniform; readfirstlane keeps the job index in an SGPR (a VGPR index
+  // into the by-value kernel argument copies it to scratch)
   auto job_of = [&](int g) {
+    g = __builtin_amdgcn_readfirstlane(g);
     int k = 0;
     while (k + 1 < jobs.n && g >= jobs.j[k + 1].set0) ++k;
-    return k;
+    return __builtin_amdgcn_readfirstlane(k);
   };
   auto load = [&](const DctJob &J, int set, uint2 (&w)[8]) {
     const int blk = set * 64 + lane;
@@ -301,17 +309,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     const int blk = set * 64 + lane;
     if (LAYOUT == HIC_LAYOUT_ZIGZAG_I16) {
       uint4 *o = reinterpret_cast<uint4 *>(static_cast<int16_t *>(J.out) + (int64_t)set * 64 * 64);
+      auto sv = [&](int k) { return st16(8 * k + (lane >> 3), lane & 7); };
+      if (path & 128) {
+        // dev timing knob: no coefficient stores
+      } else if ((set + 1) * 64 <= J.nblk) {  // whole set: 8 unconditional 1 KiB stores
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int b = 8 * k + (lane >> 3);
-        const uint4 v = st4[b * kStagePad + (lane & 7)];
-        if (set * 64 + b < J.nblk) o[64 * k + lane] = v;
+        for (int h = 0; h < 2; ++h) {
+          const uint4 v0 = sv(4 * h), v1 = sv(4 * h + 1), v2 = sv(4 * h + 2), v3 = sv(4 * h + 3);
+          o[64 * (4 * h) + lane] = v0;
+          o[64 * (4 * h + 1) + lane] = v1;
+          o[64 * (4 * h + 2) + lane] = v2;
+          o[64 * (4 * h + 3) + lane] = v3;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (set * 64 + 8 * k + (lane >> 3) < J.nblk) o[64 * k + lane] = sv(k);
       }
-      if (TMF >= 0) {
+      if (TMF >= 0 && !(path & 32)) {
         uint32_t zw[32];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const uint4 t = st4[lane * kStagePad + k];
+          const uint4 t = st16(lane, k);
           zw[4 * k] = t.x; zw[4 * k + 1] = t.y; zw[4 * k + 2] = t.z; zw[4 * k + 3] = t.w;
         }
         tile_record16<TMF>(zw, blk < J.nblk, blk, M, J.tiles + (int64_t)set * 3);
@@ -321,12 +340,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
       if (LAYOUT == HIC_LAYOUT_RASTER_I16) {
         int16_t *o = static_cast<int16_t *>(J.out) + (int64_t)bi * 8 * J.W + bj * 8;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) *reinterpret_cast<uint4 *>(o + (int64_t)u * J.W) = st4[lane * kStagePad + u];
+        for (int u = 0; u < 8; ++u) *reinterpret_cast<uint4 *>(o + (int64_t)u * J.W) = st16(lane, u);
       } else {
         int32_t *o = static_cast<int32_t *>(J.out) + (int64_t)bi * 8 * J.W + bj * 8;
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const uint4 t = st4[lane * kStagePad + u];
+          const uint4 t = st16(lane, u);
           const uint32_t wd[4] = {t.x, t.y, t.z, t.w};
           int q[8];
 #pragma unroll
@@ -348,16 +367,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   // bit-exact).
   uint64_t redo = 0, fix = 0;
   int i = 0;
+  // dev (path & 256, results invalid): in-kernel clock stamps, MI355X_MICROARCH.md DVFS
+  const uint64_t ck0 = (path & 256) ? __builtin_amdgcn_s_memtime() : 0;
+  const uint64_t rt0 = (path & 256) ? __builtin_amdgcn_s_memrealtime() : 0;
   if (path != 0) {
+    // the job's fields stay in SGPRs and are reloaded only when g enters the next
+    // job (jobs are contiguous set ranges): no scalar loads on the per-set path
+    int kj = g0 < jobs.total_sets ? job_of(g0) : 0;
+    DctJob J = jobs.j[kj];
+    int next0 = kj + 1 < jobs.n ? jobs.j[kj + 1].set0 : jobs.total_sets;
     for (int g = g0; g < jobs.total_sets; g += nwaves, ++i) {
-      const DctJob &J = jobs.j[job_of(g)];
+      if (g >= next0) {
+        kj = job_of(g);
+        J = jobs.j[kj];
+        next0 = kj + 1 < jobs.n ? jobs.j[kj + 1].set0 : jobs.total_sets;
+      }
       const int set = g - J.set0;
       uint2 w[8];
-      load(J, set, w);
-      bool t26;
-      const bool f = dct_block_aan<TABLE, LAYOUT>(w, st, &t26, nullptr, J.table);
-      if (__builtin_amdgcn_ballot_w64(f) != 0 && path == 1) redo |= 1ull << i;
-      if (__builtin_amdgcn_ballot_w64(t26) != 0 && path == 1) fix |= 1ull << i;
+      if (path & 64) {  // dev timing knob: synthetic pixels, no HBM reads
+        const uint32_t h = (uint32_t)(g * 64 + lane) * 0x9E3779B1u;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) w[r] = make_uint2(h ^ (0x85EBCA6Bu * r), (h >> 7) ^ (0xC2B2AE35u * r));
+      } else {
+        load(J, set, w);
+      }
+      bool t26 = false, f = false;
+      if (path & 16) {  // dev timing knob: no DCT (pixels copied into the stage)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) reinterpret_cast<uint2 *>(st)[r] = w[r];
+      } else {
+        f = dct_block_aan<TABLE, LAYOUT>(w, st, &t26, nullptr, J.table);
+      }
+      if (__builtin_amdgcn_ballot_w64(f) != 0 && (path & 3) == 1) redo |= 1ull << i;
+      if (__builtin_amdgcn_ballot_w64(t26) != 0 && (path & 3) == 1) fix |= 1ull << i;
       store(J, set);
     }
   } else {
@@ -420,6 +462,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     load(J, set, w);
     dct_block_2ph<TABLE, LAYOUT>(w, st, J.table);
     store(J, set);
+  }
+  if ((path & 256) && lane == 0) {  // vector stores into job 0's output (invalid in this mode)
+    uint64_t *o = static_cast<uint64_t *>(jobs.j[0].out) + 4 * g0;
+    o[0] = ck0;
+    o[1] = rt0;
+    o[2] = __builtin_amdgcn_s_memtime();
+    o[3] = __builtin_amdgcn_s_memrealtime();
   }
 }
 
@@ -509,6 +558,11 @@ inline int dct_path() {
   if (v < 0) {
     const char *e = getenv("HIC_DCT_PATH");
     v = !e ? 1 : (e[0] == 'e') ? 0 : (e[0] == 'n') ? 2 : 1;
+    // dev timing knobs (results are NOT valid): 16 = no DCT (pixels copied into
+    // the stage), 32 = no RLE tile record, 64 = no pixel loads (synthetic
+    // pixels), 128 = no coefficient stores, 256 = per-wave clock stamps
+    const char *dbg = getenv("HIC_DCT_DBG");
+    if (v != 0 && dbg) v |= atoi(dbg) & 496;
   }
   return v;
 }

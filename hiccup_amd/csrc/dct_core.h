@@ -220,7 +220,12 @@ __host__ __device__ __forceinline__ int quant_fast(double b, int i, int trt = 0)
   return q;
 }
 
-constexpr int kStagePad = 9;  // uint4 per block in the LDS stage (8 + 1 pad: conflict-free)
+// LDS stage row of one block: 128 B of coefficients + 8 B pad (17 x 8 B).  The
+// quantiser writes it 2 B at a time (ds_write_b16, banks (a/4) mod 32): a 34-dword
+// lane stride puts a half-wave's 32 lanes on 16 banks, a 2-way conflict, which
+// costs a b16 store nothing (a 36-dword stride was 4-way, 2x); it is read back
+// 8 B at a time (ds_read_b64)
+constexpr int kStageU2 = 17;
 
 // One 8x8 block (this lane's eight 8-byte pixel rows) -> quantized int16
 // coefficients written to st[slot] in the order of LAYOUT (stage row of this lane).

@@ -51,6 +51,8 @@ def parse():
                     help="rehearsal on a 1-GPU box: every rank on cuda:0 (use with --dist-backend gloo)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=25.0)
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the BASELINE configs[1] / configs[4] side measurements (N=1 only)")
     return ap.parse_args()
 
 
@@ -82,6 +84,73 @@ def cpu_baseline(budget_s):
                       % (sample, elapsed),
             "reference_measured_in_build_container": "hiccup's own numpy path ~0.7 Mpix/s (8K 4:2:0 DCT+quantize, "
                                                      "BASELINE.md); its RLE is quadratic (infeasible at 8K)"}
+
+
+def extra_4k_luma(steps=20):
+    """BASELINE configs[1]: 4096 x 4096 random luminance, DCT + quantize + zig-zag on
+    one GPU (hic_dct_quant_u8_timed: the launch's own begin / end timestamps), with
+    >= 1.2 GB of rotating planes so every launch reads HBM, not the Infinity Cache."""
+    from hiccup_amd import _lib, device
+    n = 4096
+    rot = int(np.ceil(ROT_BYTES / (n * n * 3)))
+    g = torch.Generator(device="cuda")
+    g.manual_seed(2)
+    planes = [torch.randint(0, 256, (n, n), dtype=torch.uint8, device="cuda", generator=g) for _ in range(rot)]
+    outs = [device.empty((n * n // 64, 64), torch.int16) for _ in range(rot)]
+    evs = [device.KernelEvents() for _ in range(steps)]
+
+    def launch(i, ev=None):
+        p, o = planes[i % rot], outs[i % rot]
+        _lib.call("hic_dct_quant_u8_timed", device.ptr(p), n, n, n, _lib.TABLE_LUMINANCE, _lib.LAYOUT_ZIGZAG_I16,
+                  device.ptr(o), None, ev.start if ev else None, ev.stop if ev else None)
+
+    for i in range(3):
+        launch(i)
+    torch.cuda.synchronize()
+    for i in range(steps):
+        launch(3 + i, evs[i])
+    torch.cuda.synchronize()
+    us = float(np.mean([e.elapsed_ms() for e in evs])) * 1e3
+    gbs = n * n * 3 / (us * 1e-6) / 1e9
+    return {"workload": "4096x4096 uint8 luminance -> quantized int16 zig-zag blocks (BASELINE configs[1])",
+            "kernel": "k_dct_planes<0,ZIGZAG_I16,-1>", "avg_launch_us": round(us, 2),
+            "mpix_s": round(n * n / us, 1), "achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "algorithmic_bytes": n * n * 3, "timed_launches": steps}
+
+
+def extra_16k_roundtrip(steps=4):
+    """BASELINE configs[4] on one GPU: 16384 x 16384 random RGB, full encode (colour,
+    DCT/quantize/zig-zag, DPCM/RLE) then full decode (RLE expand, DC integrate,
+    izigzag, dequantize/IDCT, pyrUp, YCrCb -> RGB).  The symbol counts cross to the
+    host between the halves (the decoder sizes its workspace from them).  PSNR is
+    of the reconstruction against the input; its bit-exactness against the CPU
+    restatement is tests/test_gpu_codec.py::test_16k_roundtrip_vs_oracle."""
+    from hiccup_amd import pipeline
+    n = 16384
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    xs = [torch.randint(0, 256, (n, n, 3), dtype=torch.uint8, device="cuda", generator=g) for _ in range(2)]
+    enc, dec = pipeline.Encoder(n, n), pipeline.Decoder(n, n)
+
+    def trip(i):
+        enc.encode(xs[i % 2])
+        counts = enc.counts.cpu().tolist()
+        return dec.decode(enc.sym_len, enc.sym_val, counts, enc.dc)
+
+    trip(0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        out = trip(1 + i)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    x = xs[steps % 2]
+    mse = float(((out.float() - x.float()) ** 2).mean())
+    del xs, enc, dec
+    torch.cuda.empty_cache()
+    return {"workload": "16384x16384 RGB encode + decode round trip, 1 GPU (BASELINE configs[4] at N=1)",
+            "ms_per_roundtrip": round(dt * 1e3, 3), "mpix_s": round(n * n / dt / 1e6, 1),
+            "psnr_db_vs_input": round(10 * np.log10(255.0 ** 2 / mse), 3), "timed_roundtrips": steps}
 
 
 def load_pmc_traffic():
@@ -214,6 +283,8 @@ def main():
                 "avg_launch_us": round(dct_us, 2),
             },
         }
+        if not args.no_extras and world == 1:
+            out["extra_configs"] = {"4k_luma_dct": extra_4k_luma(), "16k_roundtrip": extra_16k_roundtrip()}
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args.cpu_budget_s)
         elif not args.no_cpu_baseline:

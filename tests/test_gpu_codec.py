@@ -228,6 +228,42 @@ def test_pipeline_encoder(H, W):
     np.testing.assert_array_equal(rgb2, exp_rgb)
 
 
+@pytest.mark.timeout(900)
+def test_16k_roundtrip_vs_oracle():
+    """BASELINE configs[4] on one GPU: a 16384 x 16384 random RGB image (the
+    config's seed) through the device encoder and decoder.  The symbol stream is
+    checked through size-independent properties (counts, DC integration, EOB) and
+    the reconstruction bit-exactly against the CPU restatement of the reference's
+    chain (cvtColor -> pyrDown -> dct_channel -> inv_dct_channel -> pyrUp ->
+    cvtColor, compression.py:16-56); PSNR vs the input is the same number."""
+    H = W = 16384
+    rng = np.random.default_rng(5)
+    rgb = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    enc = pipeline.Encoder(H, W)
+    enc.encode(device.to_device(rgb))
+    counts = enc.counts.cpu().tolist()
+    nblk = {k: enc.coef[k].shape[0] for k in pipeline.CHANNELS}
+    for k, c in zip(pipeline.CHANNELS, counts):
+        assert 0 < c <= nblk[k] * 63 + 1, k
+    dec = pipeline.Decoder(H, W)
+    rec_dev = dec.decode(enc.sym_len, enc.sym_val, counts, enc.dc)
+    # every AC position of every block was reconstructed from the stream
+    assert dec.status.cpu().tolist() == [nblk[k] * 63 for k in pipeline.CHANNELS]
+    # the decoder's blocks are the encoder's coefficients (RLE / DPCM inverse)
+    for k in pipeline.CHANNELS:
+        assert torch.equal(dec.blocks[k], enc.coef[k]), k
+    rec = device.to_host(rec_dev)
+    del enc, dec, rec_dev
+    torch.cuda.empty_cache()
+    y, cr, cb = orcc.rgb_to_ycrcb(rgb)
+    ry = orcc.inv_dct_channel(orcc.dct_channel(y, 0, threads=16), 0)
+    rc = [orcc.pyr_up(orcc.inv_dct_channel(orcc.dct_channel(orcc.pyr_down(c), 1, threads=16), 1)) for c in (cr, cb)]
+    exp = orcc.ycrcb_to_rgb(ry, rc[0], rc[1])
+    np.testing.assert_array_equal(rec, exp)
+    mse = np.mean((rec.astype(np.float64) - rgb) ** 2)
+    assert 10 * np.log10(255.0 ** 2 / mse) > 10.0
+
+
 @pytest.mark.parametrize("H,W,world", [(4320, 7680, 8), (250, 330, 3), (96, 64, 2)])
 def test_shards_stitch_to_single_stream(H, W, world):
     """Row shards (with pyrDown halos) + the stitch record reproduce the

@@ -366,6 +366,97 @@ __global__ void k_ycrcb420_rgb(const uint8_t *__restrict__ Y, int64_t ystride, c
   o[2] = (uint8_t)sat8(y + descale14(cb * kCB2B));
 }
 
+// Fast form of k_ycrcb420_rgb for even w (4-byte aligned Y rows and RGB): a wave
+// owns a strip of 64 output quads (4 pixels = 2 chroma columns per lane, 12 B of
+// RGB: one dwordx3 store, 768 contiguous bytes per wave and row) and walks down
+// kUpSeg chroma rows (2 * kUpSeg output rows).  Each chroma row is loaded once (2 B
+// per lane and plane) and filtered horizontally ([1 6 1] at even, [4 4] at odd
+// output columns); its neighbour columns 2q-1 / 2q+2 come from the adjacent lanes
+// by DPP wave shifts (the strip-edge lanes load them).  The vertical taps run over
+// a 3-row register window.  Edges as pyr_up_at: reflect-101 left / top, replicate
+// right / bottom.
+constexpr int kUpSeg = 8;
+
+__global__ __launch_bounds__(256) void k_ycrcb420_rgb_walk(const uint8_t *__restrict__ Y, int64_t ystride,
+                                                           const uint8_t *__restrict__ Cr,
+                                                           const uint8_t *__restrict__ Cb, int h, int w,
+                                                           uint8_t *__restrict__ rgb, int nstrips, int nwaves) {
+  const int lane = threadIdx.x & 63;
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wid >= nwaves) return;
+  const int seg = wid / nstrips, strip = wid - seg * nstrips;
+  const int nq = w >> 1;
+  const int q = strip * 64 + lane;
+  const bool owner = q < nq;
+  const int qc = owner ? q : nq - 1;
+  const int s0 = seg * kUpSeg;
+  const int ns = h - s0 < kUpSeg ? h - s0 : kUpSeg;
+  // horizontally filtered chroma row r: [cr x4 | cb x4] for output columns 4q..4q+3 (x8 scale)
+  auto hrow = [&](int r, int (&hc)[4], int (&hb)[4]) {
+    const int64_t o = (int64_t)r * w + 2 * qc;
+    const uint32_t cr2 = *reinterpret_cast<const uint16_t *>(Cr + o);
+    const uint32_t cb2 = *reinterpret_cast<const uint16_t *>(Cb + o);
+    const uint32_t own = cr2 | cb2 << 16;  // cr[2q], cr[2q+1], cb[2q], cb[2q+1]
+    uint32_t lft = shr1(own), rgt = shl1(own);
+    int crl = (int)((lft >> 8) & 255), cbl = (int)(lft >> 24);  // column 2q-1
+    int crr = (int)(rgt & 255), cbr = (int)((rgt >> 16) & 255);  // column 2q+2
+    const int c0 = (int)(cr2 & 255), c1 = (int)(cr2 >> 8), b0 = (int)(cb2 & 255), b1 = (int)(cb2 >> 8);
+    if (qc == 0) {  // reflect-101: column -1 -> 1
+      crl = c1;
+      cbl = b1;
+    } else if (lane == 0) {
+      crl = Cr[o - 1];
+      cbl = Cb[o - 1];
+    }
+    if (qc == nq - 1) {  // replicate: column w -> w - 1
+      crr = c1;
+      cbr = b1;
+    } else if (lane == 63) {
+      crr = Cr[o + 2];
+      cbr = Cb[o + 2];
+    }
+    hc[0] = crl + 6 * c0 + c1;
+    hc[1] = 4 * (c0 + c1);
+    hc[2] = c0 + 6 * c1 + crr;
+    hc[3] = 4 * (c1 + crr);
+    hb[0] = cbl + 6 * b0 + b1;
+    hb[1] = 4 * (b0 + b1);
+    hb[2] = b0 + 6 * b1 + cbr;
+    hb[3] = 4 * (b1 + cbr);
+  };
+  int pc[4], pb[4], cc[4], cb[4], nc[4], nb[4];
+  hrow(s0 > 0 ? s0 - 1 : (h > 1 ? 1 : 0), pc, pb);
+  hrow(s0, cc, cb);
+  for (int k = 0; k < ns; ++k) {
+    const int s = s0 + k;
+    hrow(s + 1 < h ? s + 1 : h - 1, nc, nb);
+#pragma unroll
+    for (int odd = 0; odd < 2; ++odd) {
+      const int oy = 2 * s + odd;
+      const uint32_t yq = *reinterpret_cast<const uint32_t *>(Y + (int64_t)oy * ystride + 4 * qc);
+      uint32_t px[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int vcr = odd ? 4 * (cc[j] + nc[j]) : pc[j] + 6 * cc[j] + nc[j];
+        const int vcb = odd ? 4 * (cb[j] + nb[j]) : pb[j] + 6 * cb[j] + nb[j];
+        const int cr = (int)sat8((vcr + 32) >> 6) - 128, cbv = (int)sat8((vcb + 32) >> 6) - 128;
+        const int yv = (int)((yq >> (8 * j)) & 255);
+        px[j] = sat8(yv + descale14(cr * kCR2R)) | sat8(yv + descale14(cbv * kCB2G + cr * kCR2G)) << 8 |
+                sat8(yv + descale14(cbv * kCB2B)) << 16;
+      }
+      if (owner) {
+        uint32_t *o = reinterpret_cast<uint32_t *>(rgb + ((int64_t)oy * 2 * w + 4 * q) * 3);
+        const uint3 v = make_uint3(px[0] | px[1] << 24, (px[1] >> 8) | px[2] << 16, (px[2] >> 16) | px[3] << 8);
+        *reinterpret_cast<uint3 *>(o) = v;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pc[j] = cc[j]; pb[j] = cb[j]; cc[j] = nc[j]; cb[j] = nb[j];
+    }
+  }
+}
+
 bool dims_ok(int64_t H, int64_t W) { return H > 0 && W > 0 && H < (1 << 20) && W < (1 << 20); }
 
 }  // namespace
@@ -457,6 +548,15 @@ extern "C" int hic_ycrcb420_to_rgb(const uint8_t *y, int64_t y_stride, const uin
                                    int64_t h, int64_t w, uint8_t *rgb, void *stream) {
   if (!y || !cr || !cb || !rgb) return arg_error("null pointer");
   if (!dims_ok(2 * h, 2 * w) || y_stride < 2 * w) return arg_error("shape");
+  if (w % 2 == 0 && y_stride % 4 == 0 && reinterpret_cast<uintptr_t>(y) % 4 == 0 &&
+      reinterpret_cast<uintptr_t>(rgb) % 4 == 0 && reinterpret_cast<uintptr_t>(cr) % 2 == 0 &&
+      reinterpret_cast<uintptr_t>(cb) % 2 == 0 && getenv("HIC_COLOR_TILED") == nullptr) {
+    const int nstrips = (int)((w / 2 + 63) / 64), nseg = (int)((h + kUpSeg - 1) / kUpSeg);
+    const int nwaves = nstrips * nseg;
+    hipLaunchKernelGGL(k_ycrcb420_rgb_walk, dim3((unsigned)((nwaves + 3) / 4)), dim3(256), 0, as_stream(stream), y,
+                       y_stride, cr, cb, (int)h, (int)w, rgb, nstrips, nwaves);
+    return check_launch("k_ycrcb420_rgb_walk");
+  }
   hipLaunchKernelGGL(k_ycrcb420_rgb, dim3((unsigned)((2 * w + 255) / 256), (unsigned)(2 * h)), dim3(256), 0,
                      as_stream(stream), y, y_stride, cr, cb, (int)h, (int)w, rgb);
   return check_launch("k_ycrcb420_rgb");

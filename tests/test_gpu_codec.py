@@ -164,6 +164,29 @@ def test_colour_kernels_vs_restatement(variant, monkeypatch):
     np.testing.assert_array_equal(transform.down_sample(np.full((4, 4), 2, np.uint8)), np.full((2, 2), 2, np.uint8))
 
 
+@pytest.mark.parametrize("variant", [{}, {"HIC_COLOR_TILED": "1"}])
+def test_decode_colour_vs_restatement(variant, monkeypatch):
+    """hic_ycrcb420_to_rgb (pyrUp of both chroma planes, crop of Y, YCrCb -> RGB:
+    compression.py:51-56, transform.py:151-158,269-277) against the restatement,
+    every shape of COLOUR_SHAPES plus a wide multi-strip plane."""
+    for k, v in variant.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(9)
+    for H, W in COLOUR_SHAPES + ((34, 16384 + 6),):
+        h, w = H // 2, W // 2
+        if h == 0 or w == 0:
+            continue
+        y = rng.integers(0, 256, (H, W), dtype=np.uint8)
+        cr = rng.integers(0, 256, (h, w), dtype=np.uint8)
+        cb = rng.integers(0, 256, (h, w), dtype=np.uint8)
+        yd, crd, cbd = (device.to_device(a) for a in (y, cr, cb))
+        out = device.empty((2 * h, 2 * w, 3), torch.uint8)
+        _lib.call("hic_ycrcb420_to_rgb", device.ptr(yd), yd.stride(0), device.ptr(crd), device.ptr(cbd), h, w,
+                  device.ptr(out), device.stream_ptr())
+        exp = orcc.ycrcb_to_rgb(y[:2 * h, :2 * w], orcc.pyr_up(cr), orcc.pyr_up(cb))
+        np.testing.assert_array_equal(device.to_host(out), exp, err_msg=str((H, W)))
+
+
 def test_jpeg_compression_roundtrip(golden_lenna):
     g = golden_lenna
     ci = compression.jpeg_compression(g["rgb"])

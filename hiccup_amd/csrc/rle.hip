@@ -833,14 +833,25 @@ __global__ __launch_bounds__(kTB) void k_rld_tile(const L_T *__restrict__ sym_le
 // In-place exclusive scan of n int64 values by one workgroup; returns total in *out_total.
 __global__ __launch_bounds__(kScanT) void k_scan_inplace(int64_t *__restrict__ v, int64_t n,
                                                          int64_t *__restrict__ out_total) {
+  // kScanK consecutive values per thread per pass: one workgroup-wide scan per
+  // kScanT * kScanK values
   __shared__ int64_t s_buf[32];
   int64_t run = 0;
-  for (int64_t c0 = 0; c0 < n; c0 += kScanT) {
-    const int64_t i = c0 + threadIdx.x;
-    const int64_t x = i < n ? v[i] : 0;
+  for (int64_t c0 = 0; c0 < n; c0 += (int64_t)kScanT * kScanK) {
+    const int64_t i0 = c0 + (int64_t)threadIdx.x * kScanK;
+    int64_t x[kScanK], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanK; ++k) {
+      x[k] = i0 + k < n ? v[i0 + k] : 0;
+      sum += x[k];
+    }
     int64_t tot;
-    const int64_t e = block_excl_sum<int64_t, kScanT>(x, s_buf, tot);
-    if (i < n) v[i] = run + e;
+    int64_t e = run + block_excl_sum<int64_t, kScanT>(sum, s_buf, tot);
+#pragma unroll
+    for (int k = 0; k < kScanK; ++k) {
+      if (i0 + k < n) v[i0 + k] = e;
+      e += x[k];
+    }
     run += tot;
   }
   if (threadIdx.x == 0) *out_total = run;
@@ -923,6 +934,177 @@ __global__ void k_last_sym(const L_T *__restrict__ sym_len, const V_T *__restric
                            int64_t *__restrict__ out) {
   out[0] = nsym > 0 ? (int64_t)sym_len[nsym - 1] : 1;
   out[1] = nsym > 0 ? (int64_t)sym_val[nsym - 1] : 1;
+}
+
+// ---------------------------------------------------------------------------
+// Hot-path decode (uint8 lengths, int16 values, 64-slot int16 blocks, AC stream
+// < 2^31 positions): every block is written exactly once, in 16-byte chunks.
+//  k_rld_tile16   per tile of 4096 symbols: sum of (len + 1)
+//  k_scan_inplace tile offsets
+//  k_dc_tile / k_scan_inplace / k_dc_values16: integrated DC values -> dcval[nblk]
+//  k_rld_blocks16 per symbol tile: the blocks its AC positions [P0, P1) touch are
+//                 assembled in an LDS window (zeros, the tile's values, and the DC
+//                 of blocks whose first AC lies in the tile), then copied out; the
+//                 two edge blocks shared with neighbour tiles element-wise
+//  k_rld_tail16   positions past the last symbol (EOB zero-fill) + their DCs
+constexpr int kDS = 16;            // symbols per thread
+constexpr int kDTS = kTB * kDS;    // symbols per tile
+constexpr int kWinBlk = 160;       // LDS window: blocks per pass (20 KiB)
+
+__global__ __launch_bounds__(kTB) void k_rld_tile16(const uint8_t *__restrict__ sym_len, int64_t nsym,
+                                                    int64_t *__restrict__ tile_sum) {
+  __shared__ int64_t s_buf[8];
+  const int64_t s0 = (int64_t)blockIdx.x * kDTS + (int64_t)threadIdx.x * kDS;
+  int acc = 0;
+  if (s0 + kDS <= nsym) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(sym_len + s0);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      acc += (int)((w[k] & 255) + ((w[k] >> 8) & 255) + ((w[k] >> 16) & 255) + (w[k] >> 24)) + 4;
+  } else {
+    for (int k = 0; k < kDS; ++k)
+      if (s0 + k < nsym) acc += (int)sym_len[s0 + k] + 1;
+  }
+  int64_t total;
+  block_excl_sum<int64_t, kTB>((int64_t)acc, s_buf, total);
+  if (threadIdx.x == 0) tile_sum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kTB) void k_dc_values16(const int32_t *__restrict__ diff, int64_t nblk,
+                                                     const int64_t *__restrict__ tile_off, int16_t *__restrict__ dcval) {
+  __shared__ int64_t s_buf[8];
+  const int64_t s0 = (int64_t)blockIdx.x * kTS + (int64_t)threadIdx.x * kSPT;
+  int64_t acc = 0;
+  int d[kSPT];
+#pragma unroll
+  for (int k = 0; k < kSPT; ++k) {
+    d[k] = s0 + k < nblk ? diff[s0 + k] : 0;
+    acc += d[k];
+  }
+  int64_t total;
+  int64_t run = tile_off[blockIdx.x] + block_excl_sum<int64_t, kTB>(acc, s_buf, total);
+#pragma unroll
+  for (int k = 0; k < kSPT; ++k)
+    if (s0 + k < nblk) {
+      run += d[k];
+      dcval[s0 + k] = (int16_t)run;
+    }
+}
+
+// element-wise write of the slots of block b that belong to AC range [lo, hi)
+// (slot 0, the DC, when the block's first AC position 63 b is in it)
+__device__ __forceinline__ void put_block_part(int16_t *__restrict__ blocks, int64_t b, int lo, int hi,
+                                               const int16_t *win, int16_t dc, int slot0, int nslot) {
+  const int f = (int)(b * 63);
+  for (int slot = slot0; slot < slot0 + nslot; ++slot) {
+    if (slot == 0) {
+      if (f >= lo && f < hi) blocks[b * 64] = dc;
+    } else {
+      const int p = f + slot - 1;
+      if (p >= lo && p < hi) blocks[b * 64 + slot] = win ? win[slot] : 0;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kTB) void k_rld_blocks16(const uint8_t *__restrict__ sym_len,
+                                                      const int16_t *__restrict__ sym_val, int64_t nsym,
+                                                      const int64_t *__restrict__ tile_off, int n_ac,
+                                                      const int16_t *__restrict__ dcval, int16_t *__restrict__ blocks) {
+  __shared__ uint4 s_win[kWinBlk * 8];
+  __shared__ int64_t s_buf[8];
+  int16_t *win = reinterpret_cast<int16_t *>(s_win);
+  const int tid = threadIdx.x;
+  const int64_t s0 = (int64_t)blockIdx.x * kDTS + (int64_t)tid * kDS;
+  int len[kDS], val[kDS];
+  if (s0 + kDS <= nsym) {
+    const uint4 l = *reinterpret_cast<const uint4 *>(sym_len + s0);
+    const uint4 v0 = *reinterpret_cast<const uint4 *>(sym_val + s0);
+    const uint4 v1 = *reinterpret_cast<const uint4 *>(sym_val + s0 + 8);
+    const uint32_t lw[4] = {l.x, l.y, l.z, l.w};
+    const uint32_t vw[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+    for (int k = 0; k < kDS; ++k) {
+      len[k] = (int)((lw[k >> 2] >> (8 * (k & 3))) & 255);
+      val[k] = (int)(int16_t)(vw[k >> 1] >> (16 * (k & 1)));
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kDS; ++k) {
+      len[k] = s0 + k < nsym ? (int)sym_len[s0 + k] : -1;  // -1: no symbol
+      val[k] = s0 + k < nsym ? (int)sym_val[s0 + k] : 0;
+    }
+  }
+  int acc = 0;
+#pragma unroll
+  for (int k = 0; k < kDS; ++k) acc += len[k] + 1;
+  int64_t tot64;
+  const int64_t P0l = tile_off[blockIdx.x];
+  const int64_t my = P0l + block_excl_sum<int64_t, kTB>((int64_t)acc, s_buf, tot64);
+  // positions fit int32 (the launcher checks n_ac < 2^31); clamp at n_ac
+  const int P0 = (int)(P0l < n_ac ? P0l : n_ac);
+  const int P1 = (int)(P0l + tot64 < n_ac ? P0l + tot64 : n_ac);
+  if (P1 <= P0) return;  // uniform
+  int pos[kDS];
+  {
+    int64_t q = my;
+#pragma unroll
+    for (int k = 0; k < kDS; ++k) {
+      q += len[k];
+      pos[k] = (len[k] >= 0 && q < n_ac) ? (int)q : -1;
+      ++q;
+    }
+  }
+  const int b_first = P0 / 63, b_last = (P1 - 1) / 63;
+  for (int wb0 = b_first; wb0 <= b_last; wb0 += kWinBlk) {
+    const int nb = b_last + 1 - wb0 < kWinBlk ? b_last + 1 - wb0 : kWinBlk;
+    for (int i = tid; i < nb * 8; i += kTB) s_win[i] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kDS; ++k) {
+      if (pos[k] >= 0) {
+        const int b = pos[k] / 63;
+        if (b >= wb0 && b < wb0 + nb) win[(b - wb0) * 64 + 1 + (pos[k] - b * 63)] = (int16_t)val[k];
+      }
+    }
+    for (int i = tid; i < nb; i += kTB) {
+      const int b = wb0 + i;
+      if (b * 63 >= P0) win[i * 64] = dcval[b];  // first AC of the block is ours (and < P1: b <= b_last)
+    }
+    __syncthreads();
+    for (int i = tid; i < nb * 8; i += kTB) {
+      const int bi = i >> 3, c = i & 7;
+      const int64_t b = wb0 + bi;
+      const int f = (int)(b * 63);
+      if (f >= P0 && f + 62 < P1) {
+        reinterpret_cast<uint4 *>(blocks + b * 64)[c] = s_win[i];
+      } else {
+        put_block_part(blocks, b, P0, P1, win + bi * 64, win[bi * 64], 8 * c, 8);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// positions [*total, n_ac): zeros (codec.decode_run_length's EOB fill), and the DC of
+// every block whose first AC lies there
+__global__ __launch_bounds__(kTB) void k_rld_tail16(const int64_t *__restrict__ total, int64_t nblk,
+                                                    const int16_t *__restrict__ dcval, int16_t *__restrict__ blocks) {
+  const int64_t n_ac = nblk * 63;
+  const int64_t t = *total < n_ac ? *total : n_ac;
+  if (t >= n_ac) return;
+  const int64_t b0 = t / 63;
+  const int64_t nchunk = (nblk - b0) * 8;
+  for (int64_t i = (int64_t)blockIdx.x * kTB + threadIdx.x; i < nchunk; i += (int64_t)gridDim.x * kTB) {
+    const int64_t b = b0 + (i >> 3);
+    const int c = (int)(i & 7);
+    if (b * 63 >= t) {
+      const int16_t dc = dcval[b];
+      reinterpret_cast<uint4 *>(blocks + b * 64)[c] = make_uint4(c == 0 ? (uint32_t)(uint16_t)dc : 0u, 0, 0, 0);
+    } else {
+      put_block_part(blocks, b, (int)t, (int)n_ac, nullptr, 0, 8 * c, 8);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1084,6 +1266,35 @@ int rle_decode(const L_T *sym_len, const V_T *sym_val, int64_t nsym, const int32
   return check_launch("k_rld_status");
 }
 
+// The hot-path decode (see k_rld_blocks16).  Workspace as hic_rld_workspace_bytes.
+int rle_decode_blocks16(const uint8_t *sym_len, const int16_t *sym_val, int64_t nsym, const int32_t *dc_diff,
+                        int64_t nblk, int16_t *blocks, int64_t *d_status, void *ws, hipStream_t s) {
+  const int64_t nts = (nsym + kDTS - 1) / kDTS, ntb = (nblk + kTS - 1) / kTS;
+  int64_t *w = static_cast<int64_t *>(ws);
+  // same int64 slots as rle_decode (its symbol tiles are smaller, so these fit)
+  int64_t *tsum = w, *dsum = w + (nsym + kTS - 1) / kTS + 1, *tot = dsum + ntb + 1, *last = tot + 2;
+  int16_t *dcval = reinterpret_cast<int16_t *>(last + 4);
+  if (nts > 0) {
+    hipLaunchKernelGGL(k_rld_tile16, dim3((unsigned)nts), dim3(kTB), 0, s, sym_len, nsym, tsum);
+    if (int e = check_launch("k_rld_tile16")) return e;
+  }
+  hipLaunchKernelGGL(k_scan_inplace, dim3(1), dim3(kScanT), 0, s, tsum, nts, tot);
+  hipLaunchKernelGGL(k_dc_tile, dim3((unsigned)ntb), dim3(kTB), 0, s, dc_diff, nblk, dsum);
+  hipLaunchKernelGGL(k_scan_inplace, dim3(1), dim3(kScanT), 0, s, dsum, ntb, tot + 1);
+  hipLaunchKernelGGL(k_dc_values16, dim3((unsigned)ntb), dim3(kTB), 0, s, dc_diff, nblk, dsum, dcval);
+  if (int e = check_launch("k_dc_values16")) return e;
+  if (nts > 0) {
+    hipLaunchKernelGGL(k_rld_blocks16, dim3((unsigned)nts), dim3(kTB), 0, s, sym_len, sym_val, nsym, tsum,
+                       (int)(nblk * 63), dcval, blocks);
+    if (int e = check_launch("k_rld_blocks16")) return e;
+  }
+  const int64_t tail_grid = cu_count() * 8 > 0 ? cu_count() * 8 : 1024;
+  hipLaunchKernelGGL(k_rld_tail16, dim3((unsigned)tail_grid), dim3(kTB), 0, s, tot, nblk, dcval, blocks);
+  hipLaunchKernelGGL((k_last_sym<uint8_t, int16_t>), dim3(1), dim3(1), 0, s, sym_len, sym_val, nsym, last);
+  hipLaunchKernelGGL(k_rld_status, dim3(1), dim3(1), 0, s, tot, last, nblk * 63, d_status);
+  return check_launch("k_rld_status");
+}
+
 }  // namespace
 }  // namespace hic
 
@@ -1198,13 +1409,21 @@ extern "C" int hic_rle_stitch(const int64_t *d_all_summaries, int world, int ran
 }
 
 extern "C" size_t hic_rld_workspace_bytes(int64_t nsym, int64_t nblk) {
-  return (size_t)((nsym + kTS - 1) / kTS + (nblk + kTS - 1) / kTS + 8) * sizeof(int64_t);
+  // tile sums (symbol tiles, DC tiles), totals, last symbol; then the hot path's
+  // integrated DC values (int16 x nblk)
+  return (size_t)((nsym + kTS - 1) / kTS + (nblk + kTS - 1) / kTS + 8) * sizeof(int64_t) +
+         (size_t)(nblk + 8) * sizeof(int16_t);
 }
 
 extern "C" int hic_rle_decode_i16(const uint8_t *sym_len, const int16_t *sym_val, int64_t nsym,
                                   const int32_t *dc_diff, int64_t nblk, int block_len, int16_t *blocks,
                                   int64_t *d_status, void *workspace, void *stream) {
   if (block_len < 2 || !dc_diff) return arg_error("block_len / dc_diff");
+  if (block_len == 64 && nblk > 0 && nblk * 63 < ((int64_t)1 << 31) && nsym >= 0 && sym_len && sym_val && blocks &&
+      d_status && workspace && reinterpret_cast<uintptr_t>(sym_len) % 16 == 0 &&
+      reinterpret_cast<uintptr_t>(sym_val) % 16 == 0 && reinterpret_cast<uintptr_t>(blocks) % 16 == 0 &&
+      getenv("HIC_RLD_GENERIC") == nullptr)
+    return rle_decode_blocks16(sym_len, sym_val, nsym, dc_diff, nblk, blocks, d_status, workspace, as_stream(stream));
   return rle_decode(sym_len, sym_val, nsym, dc_diff, nblk, block_geo(nblk, block_len), nblk * (block_len - 1), blocks,
                     d_status, workspace,
                     as_stream(stream));

@@ -52,6 +52,59 @@ def test_codectest_cases():
         codec.decode_run_length([], 5)
 
 
+def _decode_i16(L, V, dc, nblk, generic, monkeypatch):
+    if generic:
+        monkeypatch.setenv("HIC_RLD_GENERIC", "1")
+    else:
+        monkeypatch.delenv("HIC_RLD_GENERIC", raising=False)
+    lib = _lib.load()
+    Ld, Vd, dcd = (device.to_device(np.ascontiguousarray(a)) for a in (L.astype(np.uint8), V.astype(np.int16),
+                                                                        dc.astype(np.int32)))
+    blocks = torch.full((nblk, 64), -7, dtype=torch.int16, device="cuda")  # poison: every slot must be written
+    status = device.zeros((1,), torch.int64)
+    ws = device.workspace(lib.hic_rld_workspace_bytes(len(L), nblk))
+    _lib.call("hic_rle_decode_i16", device.ptr(Ld), device.ptr(Vd), len(L), device.ptr(dcd), nblk, 64,
+              device.ptr(blocks), device.ptr(status), device.ptr(ws), device.stream_ptr())
+    return device.to_host(blocks), int(status.cpu()[0])
+
+
+@pytest.mark.parametrize("kind", ["dense", "sparse", "zero", "last_only", "first_only", "striped", "no_eob"])
+def test_rle_decode_blocks_hot_path(kind, monkeypatch):
+    """hic_rle_decode_i16's block-assembling path (LDS windows over 4096-symbol
+    tiles, edge blocks shared between tiles, EOB tail fill) against the oracle's
+    streams (codec.py:55-113) and against the generic scatter path."""
+    rng = np.random.default_rng(len(kind))
+    nblk = 5000
+    zz = np.zeros((nblk, 64), np.int32)
+    if kind == "dense":
+        zz[:] = rng.integers(-40, 41, (nblk, 64))
+    elif kind == "sparse":  # runs far longer than a window, crossing tiles
+        m = rng.random((nblk, 64)) < 0.004
+        zz[m] = rng.integers(1, 9, m.sum())
+    elif kind == "last_only":
+        zz[-1, 63] = 5
+    elif kind == "first_only":
+        zz[0, 1] = -3
+    elif kind == "striped":  # dense bands between empty stretches
+        band = (np.arange(nblk) // 300) % 2 == 0
+        zz[band] = rng.integers(-3, 4, (band.sum(), 64))
+    elif kind == "no_eob":
+        zz[:] = rng.integers(-5, 6, (nblk, 64))
+    zz[:, 0] = rng.integers(-900, 900, nblk)
+    ac = zz[:, 1:].reshape(-1)
+    L, V = orcc.rle_encode(ac, 15)
+    if kind == "no_eob":  # a truncated stream: the remaining positions decode as zeros, status < n_ac
+        L, V = L[:-1000], V[:-1000]
+    dc = orcc.dpcm(zz[:, 0].copy())
+    got, st = _decode_i16(L, V, dc, nblk, False, monkeypatch)
+    ref, rst = _decode_i16(L, V, dc, nblk, True, monkeypatch)
+    np.testing.assert_array_equal(got, ref)
+    assert st == rst
+    if kind != "no_eob":
+        np.testing.assert_array_equal(got.astype(np.int32), zz)
+        assert st == nblk * 63
+
+
 def test_rle_long_carried_runs():
     """A nonzero after thousands of all-zero blocks: the cooperative filler path."""
     n = 63 * 5000

@@ -17,6 +17,10 @@ with open(os.path.join(dst, "bench_kernel_stats_%s.csv" % suf), "w", newline="")
         w.writerow(r)
 lines = [l for l in open(os.path.join(src, "bench.json.log")) if l.startswith("{")]
 open(os.path.join(dst, "bench_%s.json.log" % suf), "w").write(lines[-1])
+plain = os.path.join(src, "bench_plain.json.log")
+if os.path.exists(plain):
+    pl = [l for l in open(plain) if l.startswith("{")]
+    open(os.path.join(dst, "bench_full_%s.json.log" % suf), "w").write(pl[-1])
 for sub in ("pmc_FETCH_SIZE", "pmc_WRITE_SIZE", "cal_FETCH_SIZE", "cal_WRITE_SIZE"):
     p = os.path.join(src, sub, "run_counter_collection.csv")
     keep = [r for r in csv.DictReader(open(p)) if "hic::" in r["Kernel_Name"] or "k_pattern" in r["Kernel_Name"]]

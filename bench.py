@@ -49,6 +49,8 @@ def parse():
                     help="nccl (= RCCL) for the real multi-GPU run; gloo only to rehearse it")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank on cuda:0 (use with --dist-backend gloo)")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="HIP streams the consecutive images alternate over (each image's chain stays on one)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=25.0)
     ap.add_argument("--no-extras", action="store_true",
@@ -205,6 +207,13 @@ def main():
     timed_events = []
     event_pool = [device.KernelEvents() for _ in range((args.steps + 3) // 4)]
 
+    # consecutive images alternate over the streams (4 rotating encoders: an
+    # encoder's buffers are reused only by later work on its own stream when
+    # len(streams) divides 4)
+    assert 4 % args.streams == 0, "--streams must be 1, 2 or 4"
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(args.streams - 1)]
+    torch.cuda.synchronize()  # inputs / buffers were made on the current stream
+
     def step(i, record=False):
         e = encs[i % len(encs)]
         x = inputs[i % nin]
@@ -214,9 +223,10 @@ def main():
         if record and (i - args.warmup) % 4 == 0:
             ev = event_pool[len(timed_events)]
             timed_events.append(ev)
-        e.encode(x, dct_events=ev)
-        if world > 1 and args.gather:
-            sharding.gather_streams(e)
+        with torch.cuda.stream(streams[i % len(streams)]):
+            e.encode(x, dct_events=ev)
+            if world > 1 and args.gather:
+                sharding.gather_streams(e)
 
     for i in range(args.warmup):
         step(i)
@@ -241,6 +251,26 @@ def main():
     # planes).  hic_dct_quant_rle_u8_batch hands the two HIP events to
     # hipExtLaunchKernelGGL: they hold that dispatch's begin / end timestamps.
     dct_us = float(np.mean([ev.elapsed_ms() for ev in timed_events])) * 1e3
+    roof_note = "timed region (every 4th step)"
+    dct_us_overlapped = None
+    if len(streams) > 1:
+        # with images overlapped on several streams the DCT shares the chip with the
+        # other image's colour / emit kernels, so its launch duration is no longer
+        # its own: the roofline kernel is timed apart, on the same encoders and
+        # inputs, one stream, right after the timed region
+        dct_us_overlapped = dct_us
+        # as in the timed region: back-to-back steps, the DCT timestamped on every
+        # 4th (8 untimed steps first: the launches right after the overlapped region
+        # run 5-15 % slow in the kernel trace, profiles/r01/bench_s2_kernel_trace_v9)
+        iso = [device.KernelEvents() for _ in range(4)]
+        for j in range(24):
+            ev = iso[(j - 8) // 4] if j >= 8 and j % 4 == 0 else None
+            encs[j % len(encs)].encode(inputs[j % nin], dct_events=ev)
+        torch.cuda.synchronize()
+        dct_us = float(np.mean([ev.elapsed_ms() for ev in iso])) * 1e3
+        timed_events = iso
+        roof_note = ("16 single-stream steps (every 4th timestamped, after 8 untimed) right after the timed region; "
+                     "the timed region overlaps images on %d streams" % len(streams))
     achieved = dct_px * 3 / (dct_us * 1e-6) / 1e9  # u8 in + int16 out per pixel
 
     if rank == 0:
@@ -266,6 +296,7 @@ def main():
                 "image_hw": [H, W8K],
                 "per_rank_rows": in_rows if world == 1 else encs[0].rows[1] - encs[0].rows[0],
                 "mode": "single" if world == 1 else args.mode,
+                "streams": args.streams,
                 "gather_to_rank0": bool(args.gather and world > 1),
                 "parallelism": "dp%d tile-shard" % world,
             },
@@ -281,6 +312,8 @@ def main():
                 "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
                 "algorithmic_bytes": dct_px * 3,
                 "avg_launch_us": round(dct_us, 2),
+                "timed_over": roof_note,
+                "avg_launch_us_overlapped": None if dct_us_overlapped is None else round(dct_us_overlapped, 2),
             },
         }
         if not args.no_extras and world == 1:

@@ -372,3 +372,31 @@ def test_shards_stitch_to_single_stream(H, W, world):
         np.testing.assert_array_equal(zz, ref[k][0], err_msg=k)
         for j in (1, 2, 3):
             np.testing.assert_array_equal(np.concatenate([p[k][j] for p in parts]), ref[k][j], err_msg=(k, j))
+
+
+def test_two_stream_overlap_matches_single_stream():
+    """bench.py's default: consecutive images alternate over two HIP streams with 4
+    rotating encoders.  Every encoder's output after the overlapped run equals a
+    one-stream encode of the same image (no buffer shared across streams)."""
+    H, W = 1088, 1920
+    rng = np.random.default_rng(11)
+    imgs = [device.to_device(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)) for _ in range(3)]
+    encs = [pipeline.Encoder(H, W) for _ in range(4)]
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+    last = {}
+    for i in range(12):
+        with torch.cuda.stream(streams[i % 2]):
+            encs[i % 4].encode(imgs[i % 3])
+        last[i % 4] = i % 3
+    torch.cuda.synchronize()
+    ref = {}
+    for j in range(3):
+        e = pipeline.Encoder(H, W)
+        e.encode(imgs[j])
+        ref[j] = e.result()
+    for n, e in enumerate(encs):
+        got, exp = e.result(), ref[last[n]]
+        for k in pipeline.CHANNELS:
+            for a, b in zip(got[k], exp[k]):
+                np.testing.assert_array_equal(a, b, err_msg="%d %s" % (n, k))

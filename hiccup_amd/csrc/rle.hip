@@ -439,7 +439,7 @@ __global__ __launch_bounds__(256) void k_rle_tile16(const int16_t *__restrict__ 
 // by the whole wave.
 constexpr int kWSyms = 4096;  // staged symbols per wave (a dense tile has <= 64 * 63)
 
-template <int MF>
+template <int MF, bool NT>
 // w: this lane's block in registers; blk: the same block in global memory, read
 // for lane-varying coefficient indices (keeps w out of scratch).
 __device__ __forceinline__ void emit_tile16(const uint32_t (&w)[32], const int16_t *__restrict__ blk, bool valid,
@@ -553,8 +553,8 @@ __device__ __forceinline__ void emit_tile16(const uint32_t (&w)[32], const int16
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   HIC_PHASE(4);
   if (staged) {
-    copy_out_wave16<uint8_t>(s_len, lo, sym_len, o_tile, (int)total, cap);
-    copy_out_wave16<int16_t>(s_val, vo, sym_val, o_tile, (int)total, cap);
+    copy_out_wave16<uint8_t, NT>(s_len, lo, sym_len, o_tile, (int)total, cap);
+    copy_out_wave16<int16_t, NT>(s_val, vo, sym_val, o_tile, (int)total, cap);
     HIC_PHASE(5);
   } else {
     // long carried runs: the whole wave writes each lane's fillers
@@ -716,7 +716,7 @@ __global__ __launch_bounds__(kScanT) void k_rle_scan16b(RleJobs16 jobs, uint32_t
   if (s_fail && threadIdx.x == 0) *J.d_count = INT64_MIN;  // hand-off timed out: report, do not hang
 }
 
-template <int MF>
+template <int MF, bool NT>
 __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
   // per wave: kWSyms symbols + 16-byte alignment slack + the dummy slot
   __shared__ __attribute__((aligned(16))) uint8_t s_len_all[4][kWSyms + 32];
@@ -769,7 +769,7 @@ __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
       else
         J.dc_diff[b] = (J.stitch && J.stitch[2]) ? dc - (int)J.stitch[3] : dc;
     }
-    emit_tile16<MF>(cur.w, J.blocks + (b < J.nblk ? b : 0) * 64, b < J.nblk, b, J.nblk, M, cur.off, cur.prev,
+    emit_tile16<MF, NT>(cur.w, J.blocks + (b < J.nblk ? b : 0) * 64, b < J.nblk, b, J.nblk, M, cur.off, cur.prev,
                     s_len_all[wv], s_val_all[wv], J.sym_len, J.sym_val, J.cap);
     if (gn >= jobs.total_tiles) break;
     g = gn;
@@ -1205,10 +1205,19 @@ int encode_batch16(RleJobs16 &jobs, hipStream_t s) {
   const int64_t cap = 12 * (int64_t)cu_count();
   const int64_t waves = t0 < cap ? t0 : cap;
   const dim3 grid((unsigned)((waves + 3) / 4));
-  if (jobs.M == 15)
-    hipLaunchKernelGGL((k_rle_emit16b<15>), grid, dim3(256), 0, s, jobs);
+  // nontemporal symbol stores unless HIC_RLE_NT=0 (A/B knob)
+  static const bool nt = [] {
+    const char *e = getenv("HIC_RLE_NT");
+    return !(e && e[0] == '0');
+  }();
+  if (jobs.M == 15 && nt)
+    hipLaunchKernelGGL((k_rle_emit16b<15, true>), grid, dim3(256), 0, s, jobs);
+  else if (jobs.M == 15)
+    hipLaunchKernelGGL((k_rle_emit16b<15, false>), grid, dim3(256), 0, s, jobs);
+  else if (nt)
+    hipLaunchKernelGGL((k_rle_emit16b<0, true>), grid, dim3(256), 0, s, jobs);
   else
-    hipLaunchKernelGGL((k_rle_emit16b<0>), grid, dim3(256), 0, s, jobs);
+    hipLaunchKernelGGL((k_rle_emit16b<0, false>), grid, dim3(256), 0, s, jobs);
   return check_launch("k_rle_emit16b");
 }
 

@@ -248,7 +248,7 @@ __device__ __forceinline__ void copy_out_wave(const T *s, int a, T *__restrict__
 // g[o0 + e] (g 16-byte aligned), where a == o0 mod (16 / sizeof(T)): one
 // ds_read_b128 + global_store_dwordx4 per 16-byte chunk, element stores for the
 // partial chunks at either end and anything cut by the cap.
-template <typename T>
+template <typename T, bool NT = false>
 __device__ __forceinline__ void copy_out_wave16(const T *s, int a, T *__restrict__ g, int64_t o0, int n, int64_t cap) {
   constexpr int C = 16 / (int)sizeof(T);  // elements per chunk
   const int lane = threadIdx.x & 63;
@@ -257,8 +257,14 @@ __device__ __forceinline__ void copy_out_wave16(const T *s, int a, T *__restrict
   if (c1 > cap / C) c1 = cap / C;
   if (c1 < c0) c1 = c0;
   const int64_t sb = o0 - a;  // global element at s[0]
-  for (int64_t c = c0 + lane; c < c1; c += 64)
-    *reinterpret_cast<uint4 *>(g + c * C) = *reinterpret_cast<const uint4 *>(s + (int)(c * C - sb));
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  for (int64_t c = c0 + lane; c < c1; c += 64) {
+    const u32x4 v = *reinterpret_cast<const u32x4 *>(s + (int)(c * C - sb));
+    if (NT)  // nontemporal (nt): streaming output, no reuse in this launch
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(g + c * C));
+    else
+      *reinterpret_cast<u32x4 *>(g + c * C) = v;
+  }
   // head: [o0, c0*C); tail: [c1*C, o0+n) -- each at most C - 1 elements unless the cap cut
   const int64_t hend = c0 * C < o0 + n ? c0 * C : o0 + n;
   for (int64_t e = o0 + lane; e < hend; e += 64)

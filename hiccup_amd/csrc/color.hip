@@ -166,7 +166,15 @@ __device__ __forceinline__ uint32_t pack4(uint32_t b0, uint32_t b1, uint32_t b2,
   return b0 | b1 << 8 | b2 << 16 | b3 << 24;
 }
 
-template <int kSegC>
+template <typename T>
+__device__ __forceinline__ void st_plane(T *p, T v, bool nt) {
+  if (nt)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+
+template <int kSegC, bool NT = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kSegC == 8 ? 4 : 3))) void k_rgb_ycrcb420_walk(const uint8_t *__restrict__ rgb, int in_row0, int in_rows,
                                                            int H, int W, int out_row0, int out_rows,
                                                            uint8_t *__restrict__ Y, uint8_t *__restrict__ Cr,
@@ -253,9 +261,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kSegC == 8 
       const int gy = gy0 + r;
       if (EDGE) {
         if (owner && gy >= yw0 && gy < yw1)
-          *reinterpret_cast<uint32_t *>(Y + (int64_t)(gy - out_row0) * W + 4 * q) = yq;
+          st_plane(reinterpret_cast<uint32_t *>(Y + (int64_t)(gy - out_row0) * W + 4 * q), yq, NT);
       } else if (r >= 2 && r < 2 + 2 * kSegC) {
-        *reinterpret_cast<uint32_t *>(Y + (int64_t)(gy - out_row0) * W + 4 * q) = yq;
+        st_plane(reinterpret_cast<uint32_t *>(Y + (int64_t)(gy - out_row0) * W + 4 * q), yq, NT);
       }
       // neighbours: pixels x-2, x-1 from the left quad, x+4 from the right quad
       const uint32_t hl = (uint32_t)__builtin_amdgcn_readlane((int)hal_l, r);
@@ -276,8 +284,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kSegC == 8 
         const int a = r - 4, k = r / 2 - 2;
 #define HIC_V(h) ((((h)[a] + 4 * ((h)[a + 1] + (h)[a + 3]) + 6 * (h)[a + 2] + (h)[a + 4]) + 128) >> 8)
         const int64_t o = (int64_t)(oyl0 + k) * dw + 2 * q;
-        *reinterpret_cast<uint16_t *>(Cr + o) = (uint16_t)(sat8(HIC_V(hcr0)) | sat8(HIC_V(hcr2)) << 8);
-        *reinterpret_cast<uint16_t *>(Cb + o) = (uint16_t)(sat8(HIC_V(hcb0)) | sat8(HIC_V(hcb2)) << 8);
+        st_plane(reinterpret_cast<uint16_t *>(Cr + o), (uint16_t)(sat8(HIC_V(hcr0)) | sat8(HIC_V(hcr2)) << 8), NT);
+        st_plane(reinterpret_cast<uint16_t *>(Cb + o), (uint16_t)(sat8(HIC_V(hcb0)) | sat8(HIC_V(hcb2)) << 8), NT);
 #undef HIC_V
       }
     }
@@ -494,6 +502,10 @@ extern "C" int hic_rgb_to_ycrcb420_rows(const uint8_t *rgb_rows, int64_t in_row0
       hipLaunchKernelGGL(k_rgb_ycrcb420_walk<16>, grid, dim3(256), 0, as_stream(stream), rgb_rows, (int)in_row0,
                          (int)in_rows, (int)H, (int)W, (int)out_row0, (int)out_rows, y, cr, cb, (int)(c1 - c0),
                          nstrips, nwaves);
+    else if (const char *nt = getenv("HIC_COLOR_NT"); nt && nt[0] == '1')  // dev A/B: nontemporal plane stores
+      hipLaunchKernelGGL((k_rgb_ycrcb420_walk<8, true>), grid, dim3(256), 0, as_stream(stream), rgb_rows,
+                         (int)in_row0, (int)in_rows, (int)H, (int)W, (int)out_row0, (int)out_rows, y, cr, cb,
+                         (int)(c1 - c0), nstrips, nwaves);
     else
       hipLaunchKernelGGL(k_rgb_ycrcb420_walk<8>, grid, dim3(256), 0, as_stream(stream), rgb_rows, (int)in_row0,
                          (int)in_rows, (int)H, (int)W, (int)out_row0, (int)out_rows, y, cr, cb, (int)(c1 - c0),

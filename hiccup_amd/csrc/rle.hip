@@ -1007,6 +1007,7 @@ __device__ __forceinline__ void put_block_part(int16_t *__restrict__ blocks, int
   }
 }
 
+template <bool NT>
 __global__ __launch_bounds__(kTB) void k_rld_blocks16(const uint8_t *__restrict__ sym_len,
                                                       const int16_t *__restrict__ sym_val, int64_t nsym,
                                                       const int64_t *__restrict__ tile_off, int n_ac,
@@ -1077,7 +1078,14 @@ __global__ __launch_bounds__(kTB) void k_rld_blocks16(const uint8_t *__restrict_
       const int64_t b = wb0 + bi;
       const int f = (int)(b * 63);
       if (f >= P0 && f + 62 < P1) {
-        reinterpret_cast<uint4 *>(blocks + b * 64)[c] = s_win[i];
+        if (NT) {  // nontemporal: a 16K plane's blocks overflow every cache level
+          typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+          const uint4 t = s_win[i];
+          const u32x4 v = {t.x, t.y, t.z, t.w};
+          __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(blocks + b * 64) + c);
+        } else {
+          reinterpret_cast<uint4 *>(blocks + b * 64)[c] = s_win[i];
+        }
       } else {
         put_block_part(blocks, b, P0, P1, win + bi * 64, win[bi * 64], 8 * c, 8);
       }
@@ -1293,7 +1301,15 @@ int rle_decode_blocks16(const uint8_t *sym_len, const int16_t *sym_val, int64_t 
   hipLaunchKernelGGL(k_dc_values16, dim3((unsigned)ntb), dim3(kTB), 0, s, dc_diff, nblk, dsum, dcval);
   if (int e = check_launch("k_dc_values16")) return e;
   if (nts > 0) {
-    hipLaunchKernelGGL(k_rld_blocks16, dim3((unsigned)nts), dim3(kTB), 0, s, sym_len, sym_val, nsym, tsum,
+    static const bool nt = [] {  // HIC_RLD_NT=1: nontemporal block stores (dev A/B)
+      const char *e = getenv("HIC_RLD_NT");
+      return e && e[0] == '1';
+    }();
+    if (nt)
+      hipLaunchKernelGGL(k_rld_blocks16<true>, dim3((unsigned)nts), dim3(kTB), 0, s, sym_len, sym_val, nsym, tsum,
+                       (int)(nblk * 63), dcval, blocks);
+    else
+      hipLaunchKernelGGL(k_rld_blocks16<false>, dim3((unsigned)nts), dim3(kTB), 0, s, sym_len, sym_val, nsym, tsum,
                        (int)(nblk * 63), dcval, blocks);
     if (int e = check_launch("k_rld_blocks16")) return e;
   }

@@ -46,6 +46,8 @@ SIGNATURES = {
     "hic_last_error": (_int, [ctypes.c_char_p, _sz]),
     "hic_device_count": (_int, [ctypes.POINTER(_int)]),
     "hic_stream_sync": (_int, [_vp]),
+    "hic_set_knob": (_int, [_int, _int]),
+    "hic_get_knob": (_int, [_int, ctypes.POINTER(_int)]),
     "hic_dct_quant_u8": (_int, [_vp, _i64, _i64, _i64, _int, _int, _vp, _vp]),
     "hic_dct_quant_u8_timed": (_int, [_vp, _i64, _i64, _i64, _int, _int, _vp, _vp, _vp, _vp]),
     "hic_dct_quant_rle_u8": (_int, [_vp, _i64, _i64, _i64, _int, _int, _vp, _vp, _vp, _vp, _vp]),
@@ -131,3 +133,37 @@ def check(status, what=""):
 
 def call(name, *args):
     check(getattr(load(), name)(*args), name)
+
+
+# A/B knobs (include/hiccup_hip.h HIC_KNOB_*): every selectable path is bit-exact
+KNOBS = {"dct_path": 0, "dct_waves_per_cu": 1, "color_tiled": 2, "color_seg": 3, "color_nt": 4, "rle_nt": 5,
+         "rld_nt": 6, "rld_generic": 7, "dev": 8}
+DCT_PATH_F32, DCT_PATH_F64, DCT_PATH_F64_NOPF, DCT_PATH_EXACT = 3, 1, 2, 0
+
+
+def set_knob(name, value):
+    call("hic_set_knob", KNOBS[name], int(value))
+
+
+def get_knob(name):
+    v = _int(0)
+    call("hic_get_knob", KNOBS[name], ctypes.byref(v))
+    return v.value
+
+
+class knobs:
+    """Context manager: `with _lib.knobs(dct_path=0): ...` sets knobs, restoring
+    the defaults (-1) on exit."""
+
+    def __init__(self, **kw):
+        self.kw = kw
+
+    def __enter__(self):
+        for k, v in self.kw.items():
+            set_knob(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k in self.kw:
+            set_knob(k, -1)
+        return False

@@ -491,10 +491,9 @@ extern "C" int hic_rgb_to_ycrcb420_rows(const uint8_t *rgb_rows, int64_t in_row0
   if (in_row0 > need0 || in_row0 + in_rows < need1) return arg_error("input rows do not cover the pyrDown halo");
   if (c1 <= c0) return arg_error("no chroma rows in the output range");
   if (W % 4 == 0 && reinterpret_cast<uintptr_t>(cr) % 2 == 0 && reinterpret_cast<uintptr_t>(cb) % 2 == 0 &&
-      getenv("HIC_COLOR_TILED") == nullptr) {
+      knob(HIC_KNOB_COLOR_TILED) == 0) {
     const int nstrips = (int)((W / 4 + kStripQ - 1) / kStripQ);
-    const char *sv = getenv("HIC_COLOR_SEG");
-    const int segc = sv && atoi(sv) == 16 ? 16 : 8;
+    const int segc = knob(HIC_KNOB_COLOR_SEG) == 16 ? 16 : 8;
     const int nseg = (int)((c1 - c0 + segc - 1) / segc);
     const int nwaves = nstrips * nseg;
     const dim3 grid((unsigned)((nwaves + 3) / 4));
@@ -502,7 +501,7 @@ extern "C" int hic_rgb_to_ycrcb420_rows(const uint8_t *rgb_rows, int64_t in_row0
       hipLaunchKernelGGL(k_rgb_ycrcb420_walk<16>, grid, dim3(256), 0, as_stream(stream), rgb_rows, (int)in_row0,
                          (int)in_rows, (int)H, (int)W, (int)out_row0, (int)out_rows, y, cr, cb, (int)(c1 - c0),
                          nstrips, nwaves);
-    else if (const char *nt = getenv("HIC_COLOR_NT"); nt && nt[0] == '1')  // dev A/B: nontemporal plane stores
+    else if (knob(HIC_KNOB_COLOR_NT) == 1)  // A/B: nontemporal plane stores
       hipLaunchKernelGGL((k_rgb_ycrcb420_walk<8, true>), grid, dim3(256), 0, as_stream(stream), rgb_rows,
                          (int)in_row0, (int)in_rows, (int)H, (int)W, (int)out_row0, (int)out_rows, y, cr, cb,
                          (int)(c1 - c0), nstrips, nwaves);
@@ -562,7 +561,7 @@ extern "C" int hic_ycrcb420_to_rgb(const uint8_t *y, int64_t y_stride, const uin
   if (!dims_ok(2 * h, 2 * w) || y_stride < 2 * w) return arg_error("shape");
   if (w % 2 == 0 && y_stride % 4 == 0 && reinterpret_cast<uintptr_t>(y) % 4 == 0 &&
       reinterpret_cast<uintptr_t>(rgb) % 4 == 0 && reinterpret_cast<uintptr_t>(cr) % 2 == 0 &&
-      reinterpret_cast<uintptr_t>(cb) % 2 == 0 && getenv("HIC_COLOR_TILED") == nullptr) {
+      reinterpret_cast<uintptr_t>(cb) % 2 == 0 && knob(HIC_KNOB_COLOR_TILED) == 0) {
     const int nstrips = (int)((w / 2 + 63) / 64), nseg = (int)((h + kUpSeg - 1) / kUpSeg);
     const int nwaves = nstrips * nseg;
     hipLaunchKernelGGL(k_ycrcb420_rgb_walk, dim3((unsigned)((nwaves + 3) / 4)), dim3(256), 0, as_stream(stream), y,

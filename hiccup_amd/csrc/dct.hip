@@ -310,9 +310,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     if (LAYOUT == HIC_LAYOUT_ZIGZAG_I16) {
       uint4 *o = reinterpret_cast<uint4 *>(static_cast<int16_t *>(J.out) + (int64_t)set * 64 * 64);
       auto sv = [&](int k) { return st16(8 * k + (lane >> 3), lane & 7); };
-      if (path & 128) {
-        // dev timing knob: no coefficient stores
-      } else if ((set + 1) * 64 <= J.nblk && (path & 512)) {
+      if ((set + 1) * 64 <= J.nblk) {
         // nontemporal stores (the compiler's own nt encoding; an inline-asm sc1
         // store was faster but broke the sharded encode, see DESIGN)
 #pragma unroll
@@ -322,21 +320,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
           const u32x4 v = {t.x, t.y, t.z, t.w};
           __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(o + 64 * k + lane));
         }
-      } else if ((set + 1) * 64 <= J.nblk) {  // whole set: 8 unconditional 1 KiB stores
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const uint4 v0 = sv(4 * h), v1 = sv(4 * h + 1), v2 = sv(4 * h + 2), v3 = sv(4 * h + 3);
-          o[64 * (4 * h) + lane] = v0;
-          o[64 * (4 * h + 1) + lane] = v1;
-          o[64 * (4 * h + 2) + lane] = v2;
-          o[64 * (4 * h + 3) + lane] = v3;
-        }
       } else {
 #pragma unroll
         for (int k = 0; k < 8; ++k)
           if (set * 64 + 8 * k + (lane >> 3) < J.nblk) o[64 * k + lane] = sv(k);
       }
-      if (TMF >= 0 && !(path & 32)) {
+      if (TMF >= 0) {
         uint32_t zw[32];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -369,23 +358,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     __builtin_amdgcn_wave_barrier();
   };
 
-  // Main loop: the fast AAN path.  A set with any coefficient inside the
+  // Main loop: the float64 AAN path.  A set with any coefficient inside the
   // quantiser's tie window is remembered (bit i of `redo` / `fix` = this wave's
   // i-th set; the launcher keeps every wave at <= 64 sets) and handled after the
   // loop -- a separate code region, so the paths do not share one register
-  // allocation.  path 0 (A/B tests): exact only; path 2: fast only (timing, not
-  // bit-exact).
+  // allocation.  path 0 (A/B tests): exact replica only.
   uint64_t redo = 0, fix = 0;
   int i = 0;
-  // dev (path & 256, results invalid): in-kernel clock stamps, MI355X_MICROARCH.md DVFS
-  const uint64_t ck0 = (path & 256) ? __builtin_amdgcn_s_memtime() : 0;
-  const uint64_t rt0 = (path & 256) ? __builtin_amdgcn_s_memrealtime() : 0;
   if (path != 0) {
     // the job's fields stay in SGPRs and are reloaded only when g enters the next
     // job (jobs are contiguous set ranges): no scalar loads on the per-set path
     int kj = g0 < jobs.total_sets ? job_of(g0) : 0;
     DctJob J = jobs.j[kj];
     int next0 = kj + 1 < jobs.n ? jobs.j[kj + 1].set0 : jobs.total_sets;
+    // software pipeline (path 1): the next set's pixels load while this one computes
+    uint2 wn[8];
+    if (path == 1) load(J, g0 - J.set0, wn);
     for (int g = g0; g < jobs.total_sets; g += nwaves, ++i) {
       if (g >= next0) {
         kj = job_of(g);
@@ -394,22 +382,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
       }
       const int set = g - J.set0;
       uint2 w[8];
-      if (path & 64) {  // dev timing knob: synthetic pixels, no HBM reads
-        const uint32_t h = (uint32_t)(g * 64 + lane) * 0x9E3779B1u;
+      if (path == 1) {
 #pragma unroll
-        for (int r = 0; r < 8; ++r) w[r] = make_uint2(h ^ (0x85EBCA6Bu * r), (h >> 7) ^ (0xC2B2AE35u * r));
+        for (int r = 0; r < 8; ++r) w[r] = wn[r];
+        const int gn = g + nwaves;
+        if (gn < jobs.total_sets) {
+          const int kn = gn >= next0 ? job_of(gn) : kj;
+          load(jobs.j[kn], gn - jobs.j[kn].set0, wn);
+        }
       } else {
         load(J, set, w);
       }
-      bool t26 = false, f = false;
-      if (path & 16) {  // dev timing knob: no DCT (pixels copied into the stage)
-#pragma unroll
-        for (int r = 0; r < 8; ++r) reinterpret_cast<uint2 *>(st)[r] = w[r];
-      } else {
-        f = dct_block_aan<TABLE, LAYOUT>(w, st, &t26, nullptr, J.table);
-      }
-      if (__builtin_amdgcn_ballot_w64(f) != 0 && (path & 3) == 1) redo |= 1ull << i;
-      if (__builtin_amdgcn_ballot_w64(t26) != 0 && (path & 3) == 1) fix |= 1ull << i;
+      bool t26 = false;
+      const bool f = dct_block_aan<TABLE, LAYOUT>(w, st, &t26, nullptr, J.table);
+      if (__builtin_amdgcn_ballot_w64(f) != 0) redo |= 1ull << i;
+      if (__builtin_amdgcn_ballot_w64(t26) != 0) fix |= 1ull << i;
       store(J, set);
     }
   } else {
@@ -473,12 +460,362 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     dct_block_2ph<TABLE, LAYOUT>(w, st, J.table);
     store(J, set);
   }
-  if ((path & 256) && lane == 0) {  // vector stores into job 0's output (invalid in this mode)
-    uint64_t *o = static_cast<uint64_t *>(jobs.j[0].out) + 4 * g0;
-    o[0] = ck0;
-    o[1] = rt0;
-    o[2] = __builtin_amdgcn_s_memtime();
-    o[3] = __builtin_amdgcn_s_memrealtime();
+}
+
+// ---------------------------------------------------------------------------
+// Production forward kernel (aligned planes): the float32 fast path of
+// dct_core.h (dct_block_f32) with its two fallbacks.
+//  * tier 1: float32 AAN per block (one block per lane, 64 consecutive blocks =
+//    one set = one RLE tile per wave iteration), quantised with proven tie
+//    windows (dct_windows.h); a coefficient outside its window is final.
+//  * tier 2: every flagged coefficient (~0.03 per block on random data) is
+//    queued in LDS (block, plane, raster index) and resolved 64 at a time, one
+//    per lane, by resolve_coef (float64 dot product; pocketfft's own operations
+//    for (4,4) and the (2,2) class).  Deferred items patch the already stored
+//    coefficient in HBM.  A flagged coefficient whose candidates straddle zero
+//    ("zero-ambiguous") would change the set's RLE tile record, so such a set
+//    drains the queue before its store; items of the set being built then land
+//    in its LDS stage.
+//  * tier 3: a coefficient inside the float64 window that tier 2 cannot settle,
+//    or a set that overflows the queue, has its whole set recomputed after the
+//    main loop on the exact pocketfft replica (dct_block_2ph).
+// Coefficients go to an LDS stage at their output slot and leave in 1 KiB
+// contiguous (nontemporal) stores; the set's RLE tile record is computed from the
+// stage (TMF >= 0).  Persistent grid; each wave keeps <= 64 sets (redo mask).
+constexpr int kQCap = 32;  // queued items per wave (one resolve round)
+constexpr int kPSlots = 16;  // pixel slots per wave: 64 B copies of the flagged blocks' pixels
+
+__constant__ int8_t kZZInv[64] = {0,  2,  3,  9,  10, 20, 21, 35, 1,  4,  8,  11, 19, 22, 34, 36,
+                                  5,  7,  12, 18, 23, 33, 37, 48, 6,  13, 17, 24, 32, 38, 47, 49,
+                                  14, 16, 25, 31, 39, 46, 50, 57, 15, 26, 30, 40, 45, 51, 56, 58,
+                                  27, 29, 41, 44, 52, 55, 59, 62, 28, 42, 43, 53, 54, 60, 61, 63};
+
+// Wave-level pieces shared by the main loop and the cold paths.  `sj` is the
+// workgroup's LDS copy of the jobs (cold paths index it per lane).
+struct F32Wave {
+  const DctJob *sj;
+  uint2 *st2;  // this wave's stage: 64 rows of kStageU2 x 8 B
+  uint2 *qu;   // this wave's item queue: {block, plane << 16 | pixel slot << 8 | raster index}
+  uint4 *pix;  // this wave's pixel slots: 4 x 16 B per flagged block
+  const double *cm;      // LDS copies of the fallback's constants (cos2 table,
+  const uint8_t *qt;     // QT[2][64], kZZInv): per-lane lookups without memory latency
+  const int8_t *zz;
+  int lane, g0, nwaves, M;
+};
+
+__device__ __forceinline__ uint4 stage16(const uint2 *st2, int b, int k) {
+  const uint2 lo = st2[b * kStageU2 + 2 * k], hi = st2[b * kStageU2 + 2 * k + 1];
+  return make_uint4(lo.x, lo.y, hi.x, hi.y);
+}
+
+// stage -> output layout (+ the set's RLE tile record)
+template <int LAYOUT, int TMF>
+__device__ __forceinline__ void f32_store(const F32Wave &V, const DctJob &J, int set) {
+  const int lane = V.lane;
+  __builtin_amdgcn_wave_barrier();
+  const int blk = set * 64 + lane;
+  if (LAYOUT == HIC_LAYOUT_ZIGZAG_I16) {
+    uint4 *o = reinterpret_cast<uint4 *>(static_cast<int16_t *>(J.out) + (int64_t)set * 64 * 64);
+    auto sv = [&](int k) { return stage16(V.st2, 8 * k + (lane >> 3), lane & 7); };
+    if ((set + 1) * 64 <= J.nblk) {
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint4 t = sv(k);
+        const u32x4 v = {t.x, t.y, t.z, t.w};
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(o + 64 * k + lane));
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (set * 64 + 8 * k + (lane >> 3) < J.nblk) o[64 * k + lane] = sv(k);
+    }
+    if (TMF >= 0) {
+      uint32_t zw[32];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint4 t = stage16(V.st2, lane, k);
+        zw[4 * k] = t.x; zw[4 * k + 1] = t.y; zw[4 * k + 2] = t.z; zw[4 * k + 3] = t.w;
+      }
+      tile_record16<TMF>(zw, blk < J.nblk, blk, V.M, J.tiles + (int64_t)set * 3);
+    }
+  } else if (blk < J.nblk) {
+    const int bi = blk / J.nbx, bj = blk - bi * J.nbx;
+    if (LAYOUT == HIC_LAYOUT_RASTER_I16) {
+      int16_t *o = static_cast<int16_t *>(J.out) + (int64_t)bi * 8 * J.W + bj * 8;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) *reinterpret_cast<uint4 *>(o + (int64_t)u * J.W) = stage16(V.st2, lane, u);
+    } else {
+      int32_t *o = static_cast<int32_t *>(J.out) + (int64_t)bi * 8 * J.W + bj * 8;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const uint4 t = stage16(V.st2, lane, u);
+        const uint32_t wd[4] = {t.x, t.y, t.z, t.w};
+        int q[8];
+#pragma unroll
+        for (int v = 0; v < 8; ++v) q[v] = (int)(int16_t)(wd[v >> 1] >> (16 * (v & 1)));
+        int4 *row = reinterpret_cast<int4 *>(o + (int64_t)u * J.W);
+        row[0] = make_int4(q[0], q[1], q[2], q[3]);
+        row[1] = make_int4(q[4], q[5], q[6], q[7]);
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ void load_set(const DctJob &J, int set, int lane, uint2 (&w)[8]) {
+  const int blk = set * 64 + lane;
+  const int cblk = blk < J.nblk ? blk : J.nblk - 1;
+  const int bi = cblk / J.nbx, bj = cblk - bi * J.nbx;
+  const uint8_t *p = J.plane + (int64_t)bi * 8 * J.stride + bj * 8;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) w[r] = *reinterpret_cast<const uint2 *>(p + r * J.stride);
+}
+
+// Tier 2 (cold): resolve the n <= kQCap queued items, one per lane,
+// reading each block's pixels from its LDS slot (no memory latency).  (cur_kj,
+// cur_set): the set whose stage is not stored yet (-1: none); its items land in
+// the stage, earlier sets' items patch HBM.  Returns the wave's tier-3 bits.
+template <int LAYOUT>
+__device__ __forceinline__ uint64_t f32_round(const F32Wave &V, int n, int cur_kj, int cur_set) {
+  const int lane = V.lane;
+  const bool act = lane < n;
+  const uint2 it = act ? V.qu[lane] : make_uint2(0u, 0u);
+  const int blk = (int)it.x, kj = (int)(it.y >> 16), slot = (int)((it.y >> 8) & 0xFFu), i = (int)(it.y & 63u);
+  bool t3 = false;
+  if (act) {
+    const DctJob &J = V.sj[kj];
+    uint2 w[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 t = V.pix[slot * 4 + k];
+      w[2 * k] = make_uint2(t.x, t.y);
+      w[2 * k + 1] = make_uint2(t.z, t.w);
+    }
+    int q = 0;
+    if (resolve_coef(w, J.table, i, q, V.cm, V.qt)) {
+      const int zs = LAYOUT == HIC_LAYOUT_ZIGZAG_I16 ? (int)V.zz[i] : i;
+      if (kj == cur_kj && (blk >> 6) == cur_set) {
+        reinterpret_cast<int16_t *>(V.st2 + (blk & 63) * kStageU2)[zs] = (int16_t)q;
+      } else {
+        // this wave stored the set earlier; a wave's stores to one address complete
+        // in program order, so the patch lands after it (no fence: a wait here
+        // would also stall on the next set's prefetch)
+        if (LAYOUT == HIC_LAYOUT_ZIGZAG_I16) {
+          static_cast<int16_t *>(J.out)[(int64_t)blk * 64 + zs] = (int16_t)q;
+        } else {
+          const int bi = blk / J.nbx, bj = blk - bi * J.nbx;
+          const int64_t at = (int64_t)(bi * 8 + (i >> 3)) * J.W + bj * 8 + (i & 7);
+          if (LAYOUT == HIC_LAYOUT_RASTER_I16)
+            static_cast<int16_t *>(J.out)[at] = (int16_t)q;
+          else
+            static_cast<int32_t *>(J.out)[at] = q;
+        }
+      }
+    } else {
+      t3 = true;
+    }
+  }
+  uint64_t redo = 0;
+  uint64_t m = __builtin_amdgcn_ballot_w64(t3);
+  while (m) {  // rare: the item's whole set goes to the exact replica
+    const int l = __builtin_ctzll(m);
+    m &= m - 1;
+    const int kl = __builtin_amdgcn_readlane(kj, l), bl = __builtin_amdgcn_readlane(blk, l);
+    const int g = V.sj[kl].set0 + (bl >> 6);
+    redo |= 1ull << ((g - V.g0) / V.nwaves);
+  }
+  __builtin_amdgcn_wave_barrier();
+  return redo;
+}
+
+// Tier 3 (cold, out of line): set `set` of job kj on the exact pocketfft replica.
+template <int LAYOUT, int TMF>
+__device__ __attribute__((noinline)) void f32_exact_set(const F32Wave &V, int kj, int set) {
+  const DctJob &J = V.sj[kj];
+  uint2 w[8];
+  load_set(J, set, V.lane, w);
+  int16_t *st = reinterpret_cast<int16_t *>(V.st2 + V.lane * kStageU2);
+  if (J.table == 0)
+    dct_block_2ph<0, LAYOUT>(w, st);
+  else
+    dct_block_2ph<1, LAYOUT>(w, st);
+  f32_store<LAYOUT, TMF>(V, J, set);
+}
+
+// Queue this set's flagged coefficients (cold, after the block pass):
+// bit i of (fhi:flo) = raster index i of this lane's block is flagged.  Each
+// flagged block's pixels go to an LDS slot; its items {block, plane << 16 | slot
+// << 8 | i} to the queue.  Returns qn | ns << 8, or -1 if the queue or the slots
+// would overflow (the set then goes to tier 3).
+template <int LAYOUT>
+__device__ __forceinline__ int f32_enqueue(const F32Wave &V, int qn, int ns, int blk, int kj, uint32_t flo,
+                                                     uint32_t fhi, uint2 w0, uint2 w1, uint2 w2, uint2 w3, uint2 w4,
+                                                     uint2 w5, uint2 w6, uint2 w7) {
+  const bool has = (flo | fhi) != 0;
+  const uint64_t hm = __builtin_amdgcn_ballot_w64(has);
+  const int nb = __builtin_popcountll(hm);
+  int cnt = __builtin_popcountll(((uint64_t)fhi << 32) | flo);
+  // total items this set (wave sum of cnt)
+  int tot = 0;
+  for (uint64_t m = hm; m; m &= m - 1) tot += __builtin_amdgcn_readlane(cnt, __builtin_ctzll(m));
+  if (qn + tot > kQCap || ns + nb > kPSlots) return -1;
+  const int slot = ns + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
+  if (has) {
+    uint4 *p = V.pix + slot * 4;
+    p[0] = make_uint4(w0.x, w0.y, w1.x, w1.y);
+    p[1] = make_uint4(w2.x, w2.y, w3.x, w3.y);
+    p[2] = make_uint4(w4.x, w4.y, w5.x, w5.y);
+    p[3] = make_uint4(w6.x, w6.y, w7.x, w7.y);
+  }
+  uint64_t bits = ((uint64_t)fhi << 32) | flo;
+  while (__builtin_amdgcn_ballot_w64(bits != 0)) {  // one item per lane per pass
+    const bool on = bits != 0;
+    const uint64_t m = __builtin_amdgcn_ballot_w64(on);
+    if (on) {
+      const int i = __builtin_ctzll(bits);
+      bits &= bits - 1;
+      const int pos = qn + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      V.qu[pos] = make_uint2((uint32_t)blk, (uint32_t)(kj << 16 | slot << 8 | i));
+    }
+    qn += __builtin_popcountll(m);
+  }
+  __builtin_amdgcn_wave_barrier();
+  return qn | (ns + nb) << 8;
+}
+
+template <int LAYOUT, int TMF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_dct_f32(DctJobs jobs, int dev) {
+#ifdef HIC_DEV
+  // dev timing bits (results invalid): 1 drop tier 2, 2 no pre-store drains, 4 no
+  // stores, 8 no pixel loads, 16 no DCT, 32 queue but never resolve
+  const int dv = dev;
+#else
+  constexpr int dv = 0;
+  (void)dev;
+#endif
+  __shared__ uint2 s_stage[4 * 64 * kStageU2];
+  __shared__ uint2 s_queue[4 * kQCap];
+  __shared__ uint4 s_pix[4 * kPSlots * 4];
+  __shared__ DctJob s_jobs[3];
+  __shared__ double s_cm[64];
+  __shared__ uint8_t s_qt[128];
+  __shared__ int8_t s_zz[64];
+  if (threadIdx.x < 3) s_jobs[threadIdx.x] = jobs.j[threadIdx.x < jobs.n ? threadIdx.x : 0];
+  if (threadIdx.x < 64) s_cm[threadIdx.x] = cos2(kCm, threadIdx.x >> 3, threadIdx.x & 7);
+  if (threadIdx.x < 128) s_qt[threadIdx.x] = (uint8_t)QT[threadIdx.x >> 6][threadIdx.x & 63];
+  if (threadIdx.x < 64) s_zz[threadIdx.x] = kZZInv[threadIdx.x];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  F32Wave V;
+  V.sj = s_jobs;
+  V.st2 = s_stage + wv * 64 * kStageU2;
+  V.qu = s_queue + wv * kQCap;
+  V.pix = s_pix + wv * kPSlots * 4;
+  V.cm = s_cm;
+  V.qt = s_qt;
+  V.zz = s_zz;
+  V.lane = lane;
+  V.nwaves = gridDim.x * 4;
+  V.g0 = blockIdx.x * 4 + wv;
+  V.M = jobs.M;
+  const int g0 = V.g0, nwaves = V.nwaves;
+  int16_t *st = reinterpret_cast<int16_t *>(V.st2 + lane * kStageU2);
+  auto job_of = [&](int g) {
+    g = __builtin_amdgcn_readfirstlane(g);
+    int k = 0;
+    while (k + 1 < jobs.n && g >= jobs.j[k + 1].set0) ++k;
+    return __builtin_amdgcn_readfirstlane(k);
+  };
+
+  uint64_t redo = 0;
+  int qn = 0, ns = 0;  // queued items, used pixel slots (wave-uniform)
+  int k = 0;
+  if (g0 < jobs.total_sets) {
+    int kj = job_of(g0);
+    DctJob J = jobs.j[kj];
+    int next0 = kj + 1 < jobs.n ? jobs.j[kj + 1].set0 : jobs.total_sets;
+    // software pipeline: the next set's pixels are loaded while this one computes
+    uint2 wn[8];
+    if (dv & 8) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) wn[r] = make_uint2(0x9E3779B1u * (lane + r), 0x85EBCA6Bu * (lane ^ r));
+    } else {
+      load_set(J, g0 - J.set0, lane, wn);
+    }
+    for (int g = g0; g < jobs.total_sets; g += nwaves, ++k) {
+      if (g >= next0) {
+        kj = job_of(g);
+        J = jobs.j[kj];
+        next0 = kj + 1 < jobs.n ? jobs.j[kj + 1].set0 : jobs.total_sets;
+      }
+      const int set = g - J.set0;
+      uint2 w[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) w[r] = wn[r];
+      const int gn = g + nwaves;
+      if (gn < jobs.total_sets && !(dv & 8)) {
+        const int kn = gn >= next0 ? job_of(gn) : kj;
+        load_set(jobs.j[kn], gn - jobs.j[kn].set0, lane, wn);
+      }
+      const int blk = set * 64 + lane;
+      bool zamb = false;
+      // per column: one uniform branch on the wave's flags of its 8 coefficients;
+      // flagged raster indices collect in a per-lane 64-bit mask (bit u*8+v)
+      uint32_t flo = 0, fhi = 0;
+      bool zl = false;  // this lane has a zero-ambiguous flag: candidates rint(e) and
+                        // rint(e) +- 1 (toward d) straddle zero
+      auto sink = [&](int v, const float (&rr)[8], const float (&d)[8], const bool (&f)[8]) {
+        const bool any = f[0] | f[1] | f[2] | f[3] | f[4] | f[5] | f[6] | f[7];
+        if (__builtin_amdgcn_ballot_w64(any)) {
+          const uint32_t lo = (uint32_t)f[0] | (uint32_t)f[1] << 8 | (uint32_t)f[2] << 16 | (uint32_t)f[3] << 24;
+          const uint32_t hi = (uint32_t)f[4] | (uint32_t)f[5] << 8 | (uint32_t)f[6] << 16 | (uint32_t)f[7] << 24;
+          flo |= lo << v;
+          fhi |= hi << v;
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            zl |= f[u] && (rr[u] == 0.f || (rr[u] == 1.f && d[u] < 0.f) || (rr[u] == -1.f && d[u] > 0.f));
+        }
+      };
+      if (dv & 16) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) reinterpret_cast<uint2 *>(st)[r] = w[r];
+      } else if (J.table == 0) {
+        dct_block_f32<0, LAYOUT>(w, st, sink);
+      } else {
+        dct_block_f32<1, LAYOUT>(w, st, sink);
+      }
+      if (dv & 1) flo = fhi = 0;
+      const bool has = (flo | fhi) != 0;
+      if (__builtin_amdgcn_ballot_w64(has)) {
+        const int r = f32_enqueue<LAYOUT>(V, qn, ns, blk, kj, flo, fhi, w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7]);
+        if (r < 0) {  // overflow: this set's items are dropped and the whole set goes to tier 3
+          redo |= 1ull << k;
+        } else {
+          qn = __builtin_amdgcn_readfirstlane(r & 0xFF);
+          ns = __builtin_amdgcn_readfirstlane((r >> 8) & 0xFF);
+          zamb = __builtin_amdgcn_ballot_w64(zl) != 0 && !(dv & 2);
+        }
+      }
+      // resolve the queue before this set's store when a zero-ambiguous item needs
+      // it for the RLE tile record, or early enough that the next set finds room
+      // (one code site: items of this set land in its stage, older ones patch HBM)
+      if (dv & 32) qn = ns = 0, zamb = false;
+      if (zamb || qn > kQCap - 12 || ns > kPSlots - 6) {
+        redo |= f32_round<LAYOUT>(V, qn, kj, set);
+        qn = ns = 0;
+      }
+      if (!(dv & 4)) f32_store<LAYOUT, TMF>(V, J, set);
+    }
+  }
+  if (qn > 0) redo |= f32_round<LAYOUT>(V, qn, -1, -1);
+  // tier 3: whole sets on the exact pocketfft replica
+  while (redo) {
+    const int kk = __builtin_ctzll(redo);
+    redo &= redo - 1;
+    const int g = g0 + kk * nwaves;
+    const int kj = job_of(g);
+    f32_exact_set<LAYOUT, TMF>(V, kj, g - jobs.j[kj].set0);
   }
 }
 
@@ -545,50 +882,16 @@ __global__ void k_dequantize_i32(const int32_t *__restrict__ in, int64_t n, int 
 
 inline bool aligned(const void *p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
 
-// Dev/A-B knob (not part of the ABI contract): HIC_DCT_VARIANT=single forces the
-// one-lane-per-block kernel on aligned planes.
-// Persistent-grid size of the 2-phase kernel in waves per CU.  At 145 VGPRs a
-// SIMD holds 3 of its waves, so 12 per CU keeps the whole grid resident (16 left
-// a quarter of the waves for a second round).  HIC_DCT_WPC overrides (0 = one
-// wave per 64-block set, no persistence).
+// Forward-path selection (A/B tests only; every path is bit-exact): knob
+// "dct_path" 1 = float64 AAN fast path with the next set's pixels prefetched
+// (default), 2 = the same without the prefetch, 3 = float32 AAN + float64
+// fallback (k_dct_f32), 0 = the exact pocketfft replica for every block; "dct_waves_per_cu" = persistent grid
+// size (0 = one wave per set).  Set through hic_set_knob (common.hip); the
+// library reads no environment variables.
+inline int dct_path() { return knob(HIC_KNOB_DCT_PATH); }
 inline int dct_waves_per_cu() {
-  static int v = -1;
-  if (v < 0) {
-    const char *e = getenv("HIC_DCT_WPC");
-    v = e ? atoi(e) : 12;
-    if (v < 0) v = 12;
-  }
-  return v;
-}
-
-// HIC_DCT_VARIANT=single selects the one-pass single-lane kernel (A/B tests).
-// HIC_DCT_PATH=exact forces the pocketfft replica for every block (A/B tests).
-inline int dct_path() {
-  static int v = -1;
-  if (v < 0) {
-    const char *e = getenv("HIC_DCT_PATH");
-    v = !e ? 1 : (e[0] == 'e') ? 0 : (e[0] == 'n') ? 2 : 1;
-    // dev timing knobs (results are NOT valid): 16 = no DCT (pixels copied into
-    // the stage), 32 = no RLE tile record, 64 = no pixel loads (synthetic
-    // pixels), 128 = no coefficient stores, 256 = per-wave clock stamps
-    const char *dbg = getenv("HIC_DCT_DBG");
-    if (v != 0 && dbg) v |= atoi(dbg) & 496;
-    // nontemporal (nt) coefficient stores, the default: 4K luma 15.2 -> 12.4..13.4 us,
-    // 8K 3-plane pass unchanged within noise (43.7..44.0 -> 42.7..44.0 us);
-    // HIC_DCT_WT=0 turns them off (A/B)
-    const char *wt = getenv("HIC_DCT_WT");
-    if (v != 0 && !(wt && wt[0] == '0')) v |= 512;
-  }
-  return v;
-}
-
-inline int dct_variant() {
-  static int v = -1;
-  if (v < 0) {
-    const char *e = getenv("HIC_DCT_VARIANT");
-    v = (e && e[0] == 's' && e[1] == 'i') ? 1 : 3;
-  }
-  return v;
+  const int v = knob(HIC_KNOB_DCT_WAVES_PER_CU);
+  return v >= 0 ? v : (dct_path() == 3 ? 16 : 12);  // persistent waves per CU
 }
 
 inline bool fwd_fast(int H, int W, int64_t stride, const void *plane, const void *out) {
@@ -608,13 +911,18 @@ int launch_planes(DctJobs &jobs, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   if (cap > 0 && (total + cap - 1) / cap > 64) cap = (total + 63) / 64;  // <= 64 sets per wave (redo mask)
   const int waves = (cap == 0 || total < cap) ? total : cap;
   const dim3 grid((waves + 3) / 4), block(256);
-  auto go = [&](auto kernel) {
+  const int path = dct_path();
+  if (path == 3) {
     if (e0 || e1)
-      hipExtLaunchKernelGGL(kernel, grid, block, 0, s, e0, e1, 0, jobs, dct_path());
+      hipExtLaunchKernelGGL((k_dct_f32<LAYOUT, TMF>), grid, block, 0, s, e0, e1, 0, jobs, knob(HIC_KNOB_DEV));
     else
-      hipLaunchKernelGGL(kernel, grid, block, 0, s, jobs, dct_path());
-  };
-  go(k_dct_planes<TABLE, LAYOUT, TMF>);
+      hipLaunchKernelGGL((k_dct_f32<LAYOUT, TMF>), grid, block, 0, s, jobs, knob(HIC_KNOB_DEV));
+    return check_launch("k_dct_f32");
+  }
+  if (e0 || e1)
+    hipExtLaunchKernelGGL((k_dct_planes<TABLE, LAYOUT, TMF>), grid, block, 0, s, e0, e1, 0, jobs, path);
+  else
+    hipLaunchKernelGGL((k_dct_planes<TABLE, LAYOUT, TMF>), grid, block, 0, s, jobs, path);
   return check_launch("k_dct_planes");
 }
 
@@ -629,13 +937,11 @@ int launch_fwd(const uint8_t *plane, int H, int W, int64_t stride, void *out, hi
   const int nbx = (W + 7) / 8, nby = (H + 7) / 8, nblk = nbx * nby;
   const bool fast = fwd_fast(H, W, stride, plane, out);
   const dim3 grid((nblk + 255) / 256), block(256);
-  if (fast && dct_variant() == 3) {
+  if (fast) {
     DctJobs jobs{};
     jobs.n = 1;
     jobs.j[0] = make_job(plane, H, W, stride, TABLE, out, nullptr);
     return launch_planes<TABLE, LAYOUT, -1>(jobs, s, e0, e1);
-  } else if (fast) {
-    hipLaunchKernelGGL((k_dct_quant<TABLE, LAYOUT, true>), grid, block, 0, s, plane, H, W, stride, nbx, nblk, out);
   } else if (e0 || e1)
     hipExtLaunchKernelGGL((k_dct_quant<TABLE, LAYOUT, false>), grid, block, 0, s, e0, e1, 0, plane, H, W, stride, nbx,
                           nblk, out);
@@ -707,11 +1013,8 @@ extern "C" int hic_dct_quant_rle_u8_batch(int n, const hic_dct_plane_job *jobs, 
   hipStream_t s = as_stream(stream);
   const hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
   // fast-path planes: one launch for all of them (the kernel reads each plane's
-  // table at run time); HIC_DCT_MERGE=0 (A/B knob): one launch per table
-  static const bool merge = [] {
-    const char *v = getenv("HIC_DCT_MERGE");
-    return !(v && v[0] == '0');
-  }();
+  // table at run time)
+  const bool merge = true;
   DctJobs fastj[2] = {};
   for (int k = 0; k < n; ++k) {
     const hic_dct_plane_job &a = jobs[k];
@@ -720,7 +1023,7 @@ extern "C" int hic_dct_quant_rle_u8_batch(int n, const hic_dct_plane_job *jobs, 
     if (a.table_id != HIC_TABLE_LUMINANCE && a.table_id != HIC_TABLE_CHROMINANCE) return arg_error("plane %d: table_id", k);
     const int h = (int)a.H, w = (int)a.W;
     int64_t *tiles = static_cast<int64_t *>(a.rle_workspace);
-    if (fwd_fast(h, w, a.stride, a.plane, a.out) && dct_variant() == 3) {
+    if (fwd_fast(h, w, a.stride, a.plane, a.out)) {
       DctJobs &J = fastj[merge ? 0 : a.table_id];
       J.j[J.n++] = make_job(a.plane, h, w, a.stride, a.table_id, a.out, tiles);
       continue;

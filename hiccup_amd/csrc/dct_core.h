@@ -3,6 +3,7 @@
 // (encode.hip).  See dct.hip for the design notes and reference citations.
 #pragma once
 #include "hic_common.h"
+#include "dct_windows.h"
 
 namespace hic {
 namespace {
@@ -553,6 +554,247 @@ __host__ __device__ __forceinline__ void dct_fix26(const uint2 (&w)[8], int (&q)
     q[k] = quant_fast<TABLE>(P1 + P2, 16 + v, trt);
     q[2 + k] = quant_fast<TABLE>(P1 - P2, 48 + v, trt);
   }
+}
+
+
+// ---------------------------------------------------------------------------
+// Float32 fast path (production, aligned planes).  The AAN factorisation runs in
+// float32 on the raw pixel bytes (v_cvt_f32_ubyteN; the -128 offset of
+// dct_channel only reaches the DC, which is computed apart as an exact integer),
+// so its float work issues at the 32-bit rate and needs half the registers of the
+// float64 path.  Exactness rests on proven bounds, not on measurement
+// (tools/check/dct_bounds.py): for every (u, v) and table the
+// float32 estimate e = Y * R of y / T is within E1[t][u][v] (2^-10 .. 2^-16) of
+// the exact value, and pocketfft's own float64 y within EP of it.  The quantiser
+// takes q = rint(e) and d = e - q; |d| <= kThr32 = 1/2 - W1 with W1 > E1 + EP/T
+// + test rounding proves q == rint(fl(y_pf / T)), the reference's value.  A
+// coefficient with |d| > kThr32 ("flagged", ~0.03 per block on random data) is
+// handed to `flag`, which resolves it with the float64 fallback below.
+constexpr float kM32 = 0x1.8p23f;  // fl(e + kM32) = kM32 + rint(e); low 16 bits of the bits = q
+
+__host__ __device__ __forceinline__ void aan8_f32(const float (&x)[8], float (&o)[8]) {
+  // float32 roundings of the AAN constants (the bounds take |K - c| <= 2^-24 |c|)
+  constexpr float a1 = (float)kA1, a2 = (float)kA2, a4 = (float)kA4, a5 = (float)kA5;
+  const float s0 = x[0] + x[7], s1 = x[1] + x[6], s2 = x[2] + x[5], s3 = x[3] + x[4];
+  const float t10 = s0 + s3, t13 = s0 - s3, t11 = s1 + s2, t12 = s1 - s2;
+  o[0] = t10 + t11;
+  o[4] = t10 - t11;
+  const float wv = t12 + t13;
+  o[2] = __builtin_fmaf(a1, wv, t13);
+  o[6] = __builtin_fmaf(-a1, wv, t13);
+  const float d7 = x[0] - x[7], d6 = x[1] - x[6], d5 = x[2] - x[5], d4 = x[3] - x[4];
+  const float u10 = d4 + d5, u11 = d5 + d6, u12 = d6 + d7;
+  const float z5 = (u10 - u12) * a5;
+  const float z2 = __builtin_fmaf(a2, u10, z5), z4 = __builtin_fmaf(a4, u12, z5);
+  const float z11 = __builtin_fmaf(a1, u11, d7), z13 = __builtin_fmaf(-a1, u11, d7);
+  o[5] = z13 + z2;
+  o[3] = z13 - z2;
+  o[1] = z11 + z4;
+  o[7] = z11 - z4;
+}
+
+__host__ __device__ __forceinline__ float byte_f32(uint32_t w, int k) {
+  return (float)((w >> (8 * k)) & 0xFFu);  // v_cvt_f32_ubyte<k>
+}
+
+// The bit pattern's low 16 bits of fl(e + kM32) (== rint(e) mod 2^16).
+__host__ __device__ __forceinline__ uint32_t f32_bits(float f) { return __builtin_bit_cast(uint32_t, f); }
+
+// round-half-even(4 X / T[0][0]) for the centred pixel sum X (|X| <= 8192), in
+// integers: the DC is exact, and its ties (X = 2 mod 4 for T = 16) are real.
+template <int TABLE>
+__host__ __device__ __forceinline__ int dc_quant(int X) {
+  constexpr int T = QT[TABLE][0];
+  const int a = 8 * X + T;                        // 2 (4X) + T
+  const int q = (a >= 0 ? a : a - (2 * T - 1)) / (2 * T);  // floor(a / 2T)
+  return (a == q * 2 * T && (q & 1)) ? q - 1 : q;  // exact tie: to even
+}
+
+// Even (0, 2, 4, 6) or odd (1, 3, 5, 7) outputs of the AAN 8-point DCT-II.
+template <int PH>
+__host__ __device__ __forceinline__ void aan4_f32(const float (&x)[8], float (&o)[4]) {
+  constexpr float a1 = (float)kA1, a2 = (float)kA2, a4 = (float)kA4, a5 = (float)kA5;
+  if (PH == 0) {
+    const float s0 = x[0] + x[7], s1 = x[1] + x[6], s2 = x[2] + x[5], s3 = x[3] + x[4];
+    const float t10 = s0 + s3, t13 = s0 - s3, t11 = s1 + s2, t12 = s1 - s2;
+    const float wv = t12 + t13;
+    o[0] = t10 + t11;
+    o[1] = __builtin_fmaf(a1, wv, t13);   // output 2
+    o[2] = t10 - t11;                     // output 4
+    o[3] = __builtin_fmaf(-a1, wv, t13);  // output 6
+  } else {
+    const float d7 = x[0] - x[7], d6 = x[1] - x[6], d5 = x[2] - x[5], d4 = x[3] - x[4];
+    const float u10 = d4 + d5, u11 = d5 + d6, u12 = d6 + d7;
+    const float z5 = (u10 - u12) * a5;
+    const float z2 = __builtin_fmaf(a2, u10, z5), z4 = __builtin_fmaf(a4, u12, z5);
+    const float z11 = __builtin_fmaf(a1, u11, d7), z13 = __builtin_fmaf(-a1, u11, d7);
+    o[0] = z11 + z4;  // output 1
+    o[1] = z13 - z2;  // output 3
+    o[2] = z13 + z2;  // output 5
+    o[3] = z11 - z4;  // output 7
+  }
+}
+
+// One 8x8 block (this lane's raw pixel rows) -> quantized int16 coefficients at
+// st[slot] in the order of LAYOUT.  Two phases (even row outputs -> even
+// columns, then odd -> odd), so only half the row outputs are live at once.
+// After each column v, flag(v, rr, d, f) gets its 8 coefficients (u = 0..7):
+// rr = rint(e) as float, d = e - rr, f = (|d| > kThr32[TABLE][8u + v]); f[0] is
+// false for the DC, which is exact.
+template <int TABLE, int LAYOUT, typename Flag>
+__host__ __device__ __forceinline__ void dct_block_f32(const uint2 (&w)[8], int16_t *st, Flag &&flag) {
+  constexpr SlotOf<LAYOUT> kSlot{};
+#pragma unroll
+  for (int ph = 0; ph < 2; ++ph) {
+    uint2 wp[8];  // this phase's copy of the rows, opaque: the compiler must not keep
+                  // 64 unpacked pixels live from the even phase into the odd one
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      wp[r] = w[r];
+#ifdef __HIP_DEVICE_COMPILE__
+      asm volatile("" : "+v"(wp[r].x), "+v"(wp[r].y));
+#endif
+    }
+    float a[8][4];  // this phase's row outputs [row][k]: column v = 2k + ph
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const float x[8] = {byte_f32(wp[r].x, 0), byte_f32(wp[r].x, 1), byte_f32(wp[r].x, 2), byte_f32(wp[r].x, 3),
+                          byte_f32(wp[r].y, 0), byte_f32(wp[r].y, 1), byte_f32(wp[r].y, 2), byte_f32(wp[r].y, 3)};
+      if (ph == 0)
+        aan4_f32<0>(x, a[r]);
+      else
+        aan4_f32<1>(x, a[r]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int v = 2 * k + ph;
+      float c[8], Y[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) c[r] = a[r][k];
+      aan8_f32(c, Y);
+      float rr[8], d[8];
+      bool f[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = u * 8 + v;
+        if (i == 0) {
+          // DC: Y = the sum of the raw bytes (exact); y00 = 4 (Y - 64 * 128)
+          st[kSlot.s[0]] = (int16_t)dc_quant<TABLE>((int)Y[0] - 8192);
+          rr[0] = 0.f, d[0] = 0.f, f[0] = false;
+          continue;
+        }
+        const float R = kR32[TABLE][i];
+        const float t = __builtin_fmaf(Y[u], R, kM32);
+        const float nrr = kM32 - t;                    // -rint(e), exact
+        d[u] = __builtin_fmaf(Y[u], R, nrr);           // e - rint(e), |error| <= 2^-25
+        rr[u] = -nrr;
+        f[u] = __builtin_fabsf(d[u]) > kThr32[TABLE][i];
+        st[kSlot.s[i]] = (int16_t)(f32_bits(t) & 0xFFFFu);
+      }
+      flag(v, rr, d, f);
+    }
+  }
+}
+
+// Fallback: y_uv (full scale, as scipy's 2-D DCT-II of the centred block) in
+// float64 as a separable dot product, bounded by E2 (2^-34.5, dct_bounds.py).
+// u, v may differ per lane.  cm[m] = 2 cos(pi m / 16), m = 0..8, correctly
+// rounded; the 2 cos(pi k (2n+1) / 16) factors follow by symmetry (period 32,
+// cos(pi - a) = -cos(a)).  The caller passes cm from wherever is cheapest to read
+// per lane (LDS in the kernels).
+constexpr double kCm[9] = {2.0,
+                           0x1.f6297cff75cb0p+0,
+                           0x1.d906bcf328d46p+0,
+                           0x1.a9b66290ea1a3p+0,
+                           0x1.6a09e667f3bcdp+0,
+                           0x1.1c73b39ae68c8p+0,
+                           0x1.87de2a6aea963p-1,
+                           0x1.8f8b83c69a60bp-2,
+                           0.0};
+__host__ __device__ __forceinline__ double cos2(const double *cm, int k, int n) {
+  int m = (k * (2 * n + 1)) & 31;
+  if (m > 16) m = 32 - m;
+  const bool neg = m > 8;
+  const double c = cm[neg ? 16 - m : m];
+  return neg ? -c : c;
+}
+
+// ctab: nullptr -> computed from kCm; else the full table ctab[8k + n] = cos2(kCm, k, n)
+__host__ __device__ __forceinline__ double dct_coef_f64(const uint2 (&w)[8], int u, int v,
+                                                       const double *ctab = nullptr) {
+  double cv[8], cu[8];
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    cv[n] = ctab ? ctab[8 * v + n] : cos2(kCm, v, n);
+    cu[n] = ctab ? ctab[8 * u + n] : cos2(kCm, u, n);
+  }
+  double y = 0.0;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    auto px = [&](int n) -> double {
+      return (double)((int)(((n < 4 ? w[m].x : w[m].y) >> (8 * (n & 3))) & 0xFFu) - 128);
+    };
+    double r = px(0) * cv[0];
+#pragma unroll
+    for (int n = 1; n < 8; ++n) r = __builtin_fma(px(n), cv[n], r);
+    y = m == 0 ? r * cu[0] : __builtin_fma(r, cu[m], y);
+  }
+  return y;
+}
+
+// Quantise the fallback's y for raster index i of `table`: returns false (q unset)
+// when y / T is within 2^-kW2Log2 of a half-integer (the fallback's window; then
+// only the exact pocketfft replica decides).  p = y * (1/T) + 1/2 + 2^-30 is
+// rounded to a multiple of 2^-32 (|p| < 2^19 -> the fma's result lies in
+// [2^20, 2^21)); its low word is frac(p) in units of 2^-32.
+__host__ __device__ __forceinline__ bool quant_f64_window(double y, int T, int &q) {
+  static_assert(kW2Log2 == 30, "window constant below assumes 2^-30");
+  const double rT = 1.0 / (double)T;  // correctly rounded (IEEE division)
+  const unsigned long long t =
+      __builtin_bit_cast(unsigned long long, __builtin_fma(y, rT, 0x1.8p20 + 0.5 + 0x1p-30));
+  const uint32_t lo = (uint32_t)t;
+  q = (int)((uint32_t)(t >> 32) - kQHi);
+  // frac(y/T + 1/2 + 2^-30) < 2^-29 (+ 1 unit of the rounding): within 2^-30 of a tie
+  return lo > 9u;
+}
+
+
+// pocketfft's half-scaled y'[4][4] (row outputs 4 = an integer times TW3, then the
+// column pass's output-4 sequence): y44 is rational (2 x a pixel sum), so a tie
+// of the luminance table (T = 68: the sum = 17 mod 34) is decided by pocketfft's
+// roundings, which this reproduces.
+__host__ __device__ __forceinline__ double pf_y44(const uint2 (&w)[8]) {
+  double y[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    auto px = [&](int n) -> int { return (int)(((n < 4 ? w[r].x : w[r].y) >> (8 * (n & 3))) & 0xFFu); };
+    y[r] = (double)((px(0) + px(7) + px(3) + px(4)) - (px(1) + px(2) + px(5) + px(6))) * TW3;
+  }
+  const double c1 = y[1] + y[2], c3 = y[3] + y[4], c5 = y[5] + y[6], H0 = y[0] + y[7];
+  const double h1 = c1 + c5, T2 = H0 + c3;
+  return (T2 - h1) * TW3;
+}
+
+// Resolve AC coefficient i (raster) of this block exactly (table may differ per
+// lane).  The float64 estimate decides outside its window; inside it, the
+// coefficients whose y can be rational -- (4,4) and the (2,2) class, the only
+// ones that tie on non-adversarial data -- are recomputed with pocketfft's own
+// operation sequence.  Returns false if only the whole-block replica can decide.
+__host__ __device__ __forceinline__ bool resolve_coef(const uint2 (&w)[8], int table, int i, int &q,
+                                                     const double *ctab = nullptr, const uint8_t *qt = nullptr) {
+  const int T = qt ? (int)qt[table * 64 + i] : QT[table][i];
+  if (quant_f64_window(dct_coef_f64(w, i >> 3, i & 7, ctab), T, q)) return true;
+  if (i == 36) {
+    q = quant_fast<-1>(pf_y44(w), 36, table);
+    return true;
+  }
+  if (i == 18 || i == 22 || i == 50 || i == 54) {
+    int f[4];
+    dct_fix26<-1>(w, f, table);
+    q = i == 18 ? f[0] : i == 22 ? f[1] : i == 50 ? f[2] : f[3];
+    return true;
+  }
+  return false;
 }
 
 }  // namespace

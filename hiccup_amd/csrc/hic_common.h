@@ -13,6 +13,8 @@ namespace hic {
 
 // Per-thread last-error text (hic_last_error).
 void set_error(const char *fmt, ...);
+// Current value of an A/B knob (hic_set_knob; the default when unset).
+int knob(int k);
 
 inline int arg_error(const char *what) {
   set_error("invalid argument: %s", what);

@@ -1213,11 +1213,8 @@ int encode_batch16(RleJobs16 &jobs, hipStream_t s) {
   const int64_t cap = 12 * (int64_t)cu_count();
   const int64_t waves = t0 < cap ? t0 : cap;
   const dim3 grid((unsigned)((waves + 3) / 4));
-  // nontemporal symbol stores unless HIC_RLE_NT=0 (A/B knob)
-  static const bool nt = [] {
-    const char *e = getenv("HIC_RLE_NT");
-    return !(e && e[0] == '0');
-  }();
+  // nontemporal symbol stores unless knob RLE_NT = 0 (A/B)
+  const bool nt = knob(HIC_KNOB_RLE_NT) != 0;
   if (jobs.M == 15 && nt)
     hipLaunchKernelGGL((k_rle_emit16b<15, true>), grid, dim3(256), 0, s, jobs);
   else if (jobs.M == 15)
@@ -1301,10 +1298,7 @@ int rle_decode_blocks16(const uint8_t *sym_len, const int16_t *sym_val, int64_t 
   hipLaunchKernelGGL(k_dc_values16, dim3((unsigned)ntb), dim3(kTB), 0, s, dc_diff, nblk, dsum, dcval);
   if (int e = check_launch("k_dc_values16")) return e;
   if (nts > 0) {
-    static const bool nt = [] {  // HIC_RLD_NT=1: nontemporal block stores (dev A/B)
-      const char *e = getenv("HIC_RLD_NT");
-      return e && e[0] == '1';
-    }();
+    const bool nt = knob(HIC_KNOB_RLD_NT) == 1;  // A/B: nontemporal block stores
     if (nt)
       hipLaunchKernelGGL(k_rld_blocks16<true>, dim3((unsigned)nts), dim3(kTB), 0, s, sym_len, sym_val, nsym, tsum,
                        (int)(nblk * 63), dcval, blocks);
@@ -1447,7 +1441,7 @@ extern "C" int hic_rle_decode_i16(const uint8_t *sym_len, const int16_t *sym_val
   if (block_len == 64 && nblk > 0 && nblk * 63 < ((int64_t)1 << 31) && nsym >= 0 && sym_len && sym_val && blocks &&
       d_status && workspace && reinterpret_cast<uintptr_t>(sym_len) % 16 == 0 &&
       reinterpret_cast<uintptr_t>(sym_val) % 16 == 0 && reinterpret_cast<uintptr_t>(blocks) % 16 == 0 &&
-      getenv("HIC_RLD_GENERIC") == nullptr)
+      knob(HIC_KNOB_RLD_GENERIC) == 0)
     return rle_decode_blocks16(sym_len, sym_val, nsym, dc_diff, nblk, blocks, d_status, workspace, as_stream(stream));
   return rle_decode(sym_len, sym_val, nsym, dc_diff, nblk, block_geo(nblk, block_len), nblk * (block_len - 1), blocks,
                     d_status, workspace,

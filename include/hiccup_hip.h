@@ -58,6 +58,23 @@ int hic_abi_version(void);
 int hic_last_error(char *h_buf, size_t n);
 /* Number of visible HIP devices. */
 int hic_device_count(int *h_n);
+
+/* Code-path selection for A/B tests (not part of the reference's surface).
+ * Every selectable path is bit-exact: a knob never changes results, only which
+ * kernel variant computes them.  The library reads no environment variables.
+ * Values are process-wide; -1 restores the default. */
+#define HIC_KNOB_DCT_PATH 0         /* forward DCT: 1 float64 AAN (default), 2 the same unpipelined, 3 float32 AAN + float64 fallback, 0 exact replica */
+#define HIC_KNOB_DCT_WAVES_PER_CU 1 /* forward DCT persistent grid (waves per CU; 0 = one wave per set) */
+#define HIC_KNOB_COLOR_TILED 2      /* 1: LDS-tiled colour kernels instead of the wave-walk ones */
+#define HIC_KNOB_COLOR_SEG 3        /* wave-walk colour: chroma rows per segment (8 default, 16) */
+#define HIC_KNOB_COLOR_NT 4         /* 1: nontemporal plane stores in the colour kernel */
+#define HIC_KNOB_RLE_NT 5           /* 0: plain (not nontemporal) symbol stores in the RLE emit */
+#define HIC_KNOB_RLD_NT 6           /* 1: nontemporal block stores in the RLE decode */
+#define HIC_KNOB_RLD_GENERIC 7      /* 1: the generic (any block size) RLE decode */
+#define HIC_KNOB_DEV 8              /* dev builds only (-DHIC_DEV): timing bits that skip work; refused otherwise */
+#define HIC_KNOB_COUNT 9
+int hic_set_knob(int knob, int value);
+int hic_get_knob(int knob, int *h_value);
 /* Synchronises `stream`; returns HIC_ERR_HIP if an earlier async launch failed. */
 int hic_stream_sync(void *stream);
 

@@ -52,11 +52,12 @@ def test_codectest_cases():
         codec.decode_run_length([], 5)
 
 
-def _decode_i16(L, V, dc, nblk, generic, monkeypatch):
-    if generic:
-        monkeypatch.setenv("HIC_RLD_GENERIC", "1")
-    else:
-        monkeypatch.delenv("HIC_RLD_GENERIC", raising=False)
+def _decode_i16(L, V, dc, nblk, generic):
+    with _lib.knobs(rld_generic=1 if generic else 0):
+        return _decode_i16_call(L, V, dc, nblk)
+
+
+def _decode_i16_call(L, V, dc, nblk):
     lib = _lib.load()
     Ld, Vd, dcd = (device.to_device(np.ascontiguousarray(a)) for a in (L.astype(np.uint8), V.astype(np.int16),
                                                                         dc.astype(np.int32)))
@@ -96,8 +97,8 @@ def test_rle_decode_blocks_hot_path(kind, monkeypatch):
     if kind == "no_eob":  # a truncated stream: the remaining positions decode as zeros, status < n_ac
         L, V = L[:-1000], V[:-1000]
     dc = orcc.dpcm(zz[:, 0].copy())
-    got, st = _decode_i16(L, V, dc, nblk, False, monkeypatch)
-    ref, rst = _decode_i16(L, V, dc, nblk, True, monkeypatch)
+    got, st = _decode_i16(L, V, dc, nblk, False)
+    ref, rst = _decode_i16(L, V, dc, nblk, True)
     np.testing.assert_array_equal(got, ref)
     assert st == rst
     if kind != "no_eob":
@@ -197,10 +198,13 @@ COLOUR_SHAPES = ((64, 64), (37, 50), (130, 258), (2, 2), (3, 7), (1080, 1920), (
                  (33, 252), (35, 500), (71, 996), (64, 7680))
 
 
-@pytest.mark.parametrize("variant", [{}, {"HIC_COLOR_SEG": "16"}, {"HIC_COLOR_TILED": "1"}])
-def test_colour_kernels_vs_restatement(variant, monkeypatch):
-    for k, v in variant.items():
-        monkeypatch.setenv(k, v)
+@pytest.mark.parametrize("variant", [{}, {"color_seg": 16}, {"color_tiled": 1}])
+def test_colour_kernels_vs_restatement(variant):
+    with _lib.knobs(**variant):
+        _colour_kernels_vs_restatement()
+
+
+def _colour_kernels_vs_restatement():
     rng = np.random.default_rng(8)
     for H, W in COLOUR_SHAPES:
         rgb = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
@@ -217,13 +221,16 @@ def test_colour_kernels_vs_restatement(variant, monkeypatch):
     np.testing.assert_array_equal(transform.down_sample(np.full((4, 4), 2, np.uint8)), np.full((2, 2), 2, np.uint8))
 
 
-@pytest.mark.parametrize("variant", [{}, {"HIC_COLOR_TILED": "1"}])
-def test_decode_colour_vs_restatement(variant, monkeypatch):
+@pytest.mark.parametrize("variant", [{}, {"color_tiled": 1}])
+def test_decode_colour_vs_restatement(variant):
     """hic_ycrcb420_to_rgb (pyrUp of both chroma planes, crop of Y, YCrCb -> RGB:
     compression.py:51-56, transform.py:151-158,269-277) against the restatement,
     every shape of COLOUR_SHAPES plus a wide multi-strip plane."""
-    for k, v in variant.items():
-        monkeypatch.setenv(k, v)
+    with _lib.knobs(**variant):
+        _decode_colour_vs_restatement()
+
+
+def _decode_colour_vs_restatement():
     rng = np.random.default_rng(9)
     for H, W in COLOUR_SHAPES + ((34, 16384 + 6),):
         h, w = H // 2, W // 2

@@ -96,9 +96,16 @@ def test_layouts_roundtrip(layout, shape):
         np.testing.assert_array_equal(device.to_host(rec), orcc.inv_dct_channel(exp, tab))
 
 
+@pytest.mark.parametrize("path", [-1, _lib.DCT_PATH_F32])
 @pytest.mark.parametrize("H,W", [(4096, 4096), (4320, 7680)])
-def test_full_size_bit_exact(H, W):
-    """BASELINE configs 2/3 plane sizes, bit-exact against the C oracle (multi-threaded)."""
+def test_full_size_bit_exact(H, W, path):
+    """BASELINE configs 2/3 plane sizes, bit-exact against the C oracle (multi-threaded),
+    on the default forward path and on the float32 one."""
+    with _lib.knobs(dct_path=path):
+        _full_size_bit_exact(H, W)
+
+
+def _full_size_bit_exact(H, W):
     rng = np.random.default_rng(2)
     plane = rng.integers(0, 256, (H, W), dtype=np.uint8)
     exp = orcc.dct_channel(plane, 0, threads=16)
@@ -121,8 +128,14 @@ def test_tie_blocks_many():
         np.testing.assert_array_equal(transform.dct_channel(plane, QT[tab]), orcc.dct_channel(plane, tab, threads=8))
 
 
-@pytest.mark.parametrize("kind", ["levels4", "nearflat", "stripes", "checker"])
-def test_fast_path_structured_ties(kind):
+@pytest.mark.parametrize("path", [_lib.DCT_PATH_F32, _lib.DCT_PATH_F64, _lib.DCT_PATH_F64_NOPF, _lib.DCT_PATH_EXACT])
+@pytest.mark.parametrize("kind", ["levels4", "nearflat", "stripes", "checker", "blur"])
+def test_fast_path_structured_ties(kind, path):
+    with _lib.knobs(dct_path=path):
+        _structured_ties(kind)
+
+
+def _structured_ties(kind):
     """Planes that drive the AAN fast path into its tie handling: 4-level and
     near-flat pixels give exact (2,2)-class and (4,4) ties and the rare whole-set
     redo; stripes / checkerboards give large saturated coefficients.  Every
@@ -136,9 +149,11 @@ def test_fast_path_structured_ties(kind):
     elif kind == "stripes":
         plane = np.where((np.arange(W) // rng.integers(1, 4)) % 2 == 0, 255, 0).astype(np.uint8)[None].repeat(H, 0)
         plane[rng.random((H, W)) < 0.01] = 128
-    else:
+    elif kind == "checker":
         plane = (((np.arange(H)[:, None] + np.arange(W)[None]) % 2) * 255).astype(np.uint8)
         plane ^= rng.integers(0, 2, (H, W), dtype=np.uint8)
+    else:  # chroma-like: pyrDown of noise, many coefficients near +-1/2 (zero-ambiguous flags)
+        plane = orcc.pyr_down(rng.integers(0, 256, (2 * H, 2 * W), dtype=np.uint8))
     d = device.to_device(plane)
     for tab in (0, 1):
         exp = orcc.dct_channel(plane, tab, threads=8)

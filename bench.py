@@ -1,23 +1,25 @@
 #!/usr/bin/env python3
 """bench.py -- hiccup encode throughput on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[2], the 8K encode the metric is quoted on): a
+N = 1 (default; BASELINE configs[2], the 8K encode the metric is quoted on): a
 7680 x 4320 RGB uint8 image, already resident in HBM, through the full encode
 front end = compression.jpeg_compression + the zig-zag / DC / RLE half of
 codec.jpeg_encode:
   RGB -> YCrCb + 4:2:0 pyrDown  (1 fused kernel)
-  8x8 DCT + quantize + zig-zag   (3 planes, bit-exact float64)
-  DC DPCM + channel-wide AC RLE  (3 planes, 3 kernels each)
-One "step" encodes one such image per GPU.
+  8x8 DCT + quantize + zig-zag   (3 planes, one launch, bit-exact vs float64)
+  DC DPCM + channel-wide AC RLE  (3 planes, one scan + one emit launch)
+One "step" encodes one such image.
 
---gpus N > 1 (launched by torch.distributed.run, one process per GPU, RCCL):
-  --mode weak   (default): an (N*4320) x 7680 image, one 4320-row tile-shard per
-                rank; ranks all-gather their per-channel RLE/DC boundary
-                summaries (the only exchange the path needs), stitch, and emit
-                their slice of the single global symbol stream.
-  --mode strong: one 8K image split N ways.
-  --gather      also reassembles the whole stream on rank 0 (RCCL send/recv)
-                inside the timed region.
+--gpus N > 1 (BASELINE configs[3]): one process per GPU over RCCL.  `python
+bench.py --gpus N` starts the N ranks itself (torch.multiprocessing, before any
+GPU call in the parent); under torch.distributed.run it joins the given ranks.
+  --mode strong (default): ONE 8K image split N ways by block rows; each rank
+                 encodes its shard (colour with halo, DCT, its slice of the single
+                 DC/RLE stream after the 96-byte summary all-gather), then ONE
+                 grouped RCCL gather reassembles the whole image's coefficient
+                 blocks and DC stream on rank 0 (sharding.gather_coefficients).
+  --mode weak:   an (N*H) x W image, one H-row shard per rank (no gather).
+--workload 4k: 4096 x 4096 RGB instead of 7680 x 4320 (north_star's 4K point).
 value = pixels encoded by all ranks / max-over-ranks wall time of the K steps.
 """
 import argparse
@@ -43,8 +45,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--mode", choices=("weak", "strong"), default="weak")
-    ap.add_argument("--gather", action="store_true")
+    ap.add_argument("--mode", choices=("weak", "strong"), default="strong")
+    ap.add_argument("--workload", choices=("8k", "4k"), default="8k")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="strong mode: leave the coefficient blocks distributed (no RCCL gather to rank 0)")
+    ap.add_argument("--master-port", type=int, default=29541, help="self-launched N > 1 runs only")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                     help="nccl (= RCCL) for the real multi-GPU run; gloo only to rehearse it")
     ap.add_argument("--same-device", action="store_true",
@@ -58,32 +63,56 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(budget_s):
-    """The C oracle (scalar restatement of hiccup's CPU path, 1 thread) on a
-    bounded sample of the same workload: leading 8K rows until ~budget."""
+def _cpu_encode_band(rgb):
+    """hiccup's CPU encode path (restated in C: oracle/hiccup_oracle.c) on one band of
+    rows: colour + 4:2:0 pyrDown, DCT + quantize, zig-zag, DC DPCM, AC RLE."""
     import oracle.oracle_c as orcc
+    y, cr, cb = orcc.rgb_to_ycrcb(rgb)
+    for p, t in ((y, 0), (orcc.pyr_down(cr), 1), (orcc.pyr_down(cb), 1)):
+        zz = orcc.zigzag_blocks(orcc.dct_channel(p, t), 8)
+        orcc.dpcm(zz[:, 0].copy())
+        orcc.rle_encode(zz[:, 1:].reshape(-1), 15)
+
+
+def cpu_baseline(budget_s):
+    """The C restatement of hiccup's CPU path (oracle/; bit-identical to the GPU
+    path) on bounded samples of the same 8K workload, timed on this host: 1 thread
+    over 1088-row bands, then all usable cores, one 1088-row band per thread
+    (bands are independent through the transform; the cross-band DC / RLE stitch
+    the GPU shards do is a few words per band and is left out)."""
+    from concurrent.futures import ThreadPoolExecutor
+    rows = 1088  # 1/4 of the 8K frame (multiple of 16)
     rng = np.random.default_rng(3)
-    rows = 1088  # 1/4 of the 8K frame (multiple of 16); grown below if fast
-    done_px, elapsed = 0, 0.0
-    sample = None
-    while elapsed < budget_s * 0.5:
-        rgb = rng.integers(0, 256, (rows, W8K, 3), dtype=np.uint8)
+    band = rng.integers(0, 256, (rows, W8K, 3), dtype=np.uint8)
+    host = host_description()
+    # 1 thread: bands until ~budget/3
+    done, t_single = 0, 0.0
+    while t_single < budget_s / 3:
         t0 = time.perf_counter()
-        y, cr, cb = orcc.rgb_to_ycrcb(rgb)
-        for p, t in ((y, 0), (orcc.pyr_down(cr), 1), (orcc.pyr_down(cb), 1)):
-            q = orcc.dct_channel(p, t)
-            zz = orcc.zigzag_blocks(q, 8)
-            orcc.dpcm(zz[:, 0].copy())
-            orcc.rle_encode(zz[:, 1:].reshape(-1), 15)
-        dt = time.perf_counter() - t0
-        done_px += rows * W8K
-        elapsed += dt
-        sample = "%d x %d RGB rows of the 8K workload, %d pass(es), full encode chain" % (rows, W8K, 1)
-        if dt > budget_s * 0.5:
-            break
-    return {"value": round(done_px / elapsed / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "port",
-            "sample": "%s; %.1f s; oracle/hiccup_oracle.c (scalar restatement, bit-identical to the GPU path)"
-                      % (sample, elapsed),
+        _cpu_encode_band(band)
+        t_single += time.perf_counter() - t0
+        done += rows * W8K
+    single = done / t_single / 1e6
+    # all usable cores (capped by OMP_NUM_THREADS, the box's CPU share): one band per
+    # thread (ctypes releases the GIL in the C calls)
+    nt = max(1, host["usable_cpus"] or 1)
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        nt = min(nt, int(os.environ["OMP_NUM_THREADS"]))
+    host["threads_used"] = nt
+    bands = [rng.integers(0, 256, (rows, W8K, 3), dtype=np.uint8) for _ in range(min(nt, 64))]
+    with ThreadPoolExecutor(nt) as ex:
+        t0 = time.perf_counter()
+        list(ex.map(_cpu_encode_band, [bands[i % len(bands)] for i in range(nt)]))
+        t_all = time.perf_counter() - t0
+    multi = nt * rows * W8K / t_all / 1e6
+    return {"value": round(multi, 3), "unit": "Mpixels/s", "cores": nt, "kind": "port",
+            "sample": "%d threads x one %d x %d RGB band of the 8K workload each (%.1f s), full encode chain, "
+                      "oracle/hiccup_oracle.c (C restatement of hiccup's CPU path, bit-identical to the GPU path)"
+                      % (nt, rows, W8K, t_all),
+            "single_thread": {"value": round(single, 3), "cores": 1,
+                              "sample": "%d bands of %d x %d RGB, %.1f s" % (done // (rows * W8K), rows, W8K,
+                                                                             t_single)},
+            "host": host,
             "reference_measured_in_build_container": "hiccup's own numpy path ~0.7 Mpix/s (8K 4:2:0 DCT+quantize, "
                                                      "BASELINE.md); its RLE is quadratic (infeasible at 8K)"}
 
@@ -166,14 +195,55 @@ def load_pmc_traffic():
         return json.load(f)
 
 
+def host_description():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "usable_cpus": usable}
+
+
+def _spawn_worker(local, args_list, world, port):
+    """torch.multiprocessing entry: one rank of a self-launched N-GPU run."""
+    os.environ.update(RANK=str(local), LOCAL_RANK=str(local), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.argv = [sys.argv[0]] + list(args_list)
+    main()
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` without torch.distributed.run: start the N ranks here.
+    The parent makes no GPU call (device counting does not initialise HIP)."""
+    import torch.multiprocessing as mp
+    n = torch.cuda.device_count()
+    if n < args.gpus and not args.same_device:
+        raise SystemExit("--gpus %d: only %d visible GPUs (use --same-device --dist-backend gloo to rehearse)"
+                         % (args.gpus, n))
+    ctx = mp.start_processes(_spawn_worker, args=(sys.argv[1:], args.gpus, args.master_port), nprocs=args.gpus,
+                             join=False, start_method="spawn")
+    while not ctx.join():
+        pass
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1 and args.gpus > 1:
+        launch_ranks(args)
+        return
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and not (world == 1 and args.gpus == 1):
-        if world == 1:
-            raise SystemExit("--gpus %d needs torch.distributed.run --nproc-per-node %d" % (args.gpus, args.gpus))
     if args.same_device:
         local = 0
     torch.cuda.set_device(local)
@@ -186,19 +256,22 @@ def main():
     from hiccup_amd import device, pipeline, sharding
     device.require_gpu()
 
+    H0, W0 = (H8K, W8K) if args.workload == "8k" else (4096, 4096)
+    strong = world > 1 and args.mode == "strong"
+    gather = strong and not args.no_gather
     if world > 1:
-        H = H8K * world if args.mode == "weak" else H8K
-        make = lambda: sharding.ShardEncoder(H, W8K, rank=rank, world=world)  # noqa: E731
+        H = H0 * world if not strong else H0
+        make = lambda: sharding.ShardEncoder(H, W0, rank=rank, world=world, gather_to=0 if gather else None)  # noqa
     else:
-        H = H8K
-        make = lambda: pipeline.Encoder(H8K, W8K)  # noqa: E731
+        H = H0
+        make = lambda: pipeline.Encoder(H0, W0)  # noqa: E731
     encs = [make() for _ in range(4)]  # rotate outputs too (~1.2 GB)
     span = encs[0].span if world > 1 else (0, H)
     in_rows = span[1] - span[0]
-    nin = max(2, int(np.ceil(ROT_BYTES / (in_rows * W8K * 3))))
+    nin = max(2, int(np.ceil(ROT_BYTES / (in_rows * W0 * 3))))
     g = torch.Generator(device="cuda")
     g.manual_seed(3 + rank)
-    inputs = [torch.randint(0, 256, (in_rows, W8K, 3), dtype=torch.uint8, device="cuda", generator=g)
+    inputs = [torch.randint(0, 256, (in_rows, W0, 3), dtype=torch.uint8, device="cuda", generator=g)
               for _ in range(nin)]
     enc0 = encs[0].enc if world > 1 else encs[0]
     dct_px = sum(h * w for h, w in enc0.shapes.values())  # Y + Cr + Cb: one DCT launch
@@ -206,6 +279,7 @@ def main():
 
     timed_events = []
     event_pool = [device.KernelEvents() for _ in range((args.steps + 3) // 4)]
+    gather_ev = []  # (start, stop) torch events around each timed step's gather
 
     # consecutive images alternate over the streams (4 rotating encoders: an
     # encoder's buffers are reused only by later work on its own stream when
@@ -225,8 +299,14 @@ def main():
             timed_events.append(ev)
         with torch.cuda.stream(streams[i % len(streams)]):
             e.encode(x, dct_events=ev)
-            if world > 1 and args.gather:
-                sharding.gather_streams(e)
+            if gather:
+                if record:
+                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record()
+                e.gather_coefficients()
+                if record:
+                    b.record()
+                    gather_ev.append((a, b))
 
     for i in range(args.warmup):
         step(i)
@@ -246,6 +326,13 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # every step's symbol counts are valid (a failed step would report a negative count)
+    for e in encs:
+        counts = e.enc.counts if world > 1 else e.counts
+        for ci, c in enumerate(counts.cpu().tolist()):
+            pipeline.check_count(int(c), pipeline.CHANNELS[ci])
+            assert c > 0, "empty symbol stream"
+    gather_us = float(np.mean([a.elapsed_time(b) for a, b in gather_ev])) * 1e3 if gather_ev else None
 
     # ---- roofline kernel: the DCT+quantize+zig-zag pass (one launch for the three
     # planes).  hic_dct_quant_rle_u8_batch hands the two HIP events to
@@ -253,11 +340,11 @@ def main():
     dct_us = float(np.mean([ev.elapsed_ms() for ev in timed_events])) * 1e3
     roof_note = "timed region (every 4th step)"
     dct_us_overlapped = None
-    if len(streams) > 1:
-        # with images overlapped on several streams the DCT shares the chip with the
-        # other image's colour / emit kernels, so its launch duration is no longer
-        # its own: the roofline kernel is timed apart, on the same encoders and
-        # inputs, one stream, right after the timed region
+    if len(streams) > 1 or gather:
+        # with images overlapped on several streams (or a gather in the step) the DCT
+        # shares the chip with other kernels, so its launch duration is no longer its
+        # own: the roofline kernel is timed apart, on the same encoders and inputs,
+        # one stream, right after the timed region
         dct_us_overlapped = dct_us
         # as in the timed region: back-to-back steps, the DCT timestamped on every
         # 4th (8 untimed steps first: the launches right after the overlapped region
@@ -269,14 +356,26 @@ def main():
         torch.cuda.synchronize()
         dct_us = float(np.mean([ev.elapsed_ms() for ev in iso])) * 1e3
         timed_events = iso
-        roof_note = ("16 single-stream steps (every 4th timestamped, after 8 untimed) right after the timed region; "
-                     "the timed region overlaps images on %d streams" % len(streams))
+        roof_note = ("16 single-stream encodes (every 4th timestamped, after 8 untimed) right after the timed "
+                     "region; the timed region overlaps images on %d stream(s)%s"
+                     % (len(streams), " and gathers to rank 0" if gather else ""))
     achieved = dct_px * 3 / (dct_us * 1e-6) / 1e9  # u8 in + int16 out per pixel
 
     if rank == 0:
         total_px = px_per_step_rank * world * args.steps
         value = total_px / elapsed / 1e6
         pmc = load_pmc_traffic()
+        cfg_idx = 2 if world == 1 else 3
+        wl = ("%dx%d RGB -> YCrCb 4:2:0 full encode: colour+pyrDown, 8x8 DCT+quantize+zig-zag (3 planes), "
+              "DC DPCM + AC RLE (3 planes)" % (W0, H0))
+        if world > 1:
+            wl += ("; %s: %s, block-row tile shards over %d ranks%s"
+                   % ("BASELINE configs[3]" if (strong and args.workload == "8k") else "multi-GPU",
+                      "one image split N ways" if strong else "one %d-row shard per rank" % H0, world,
+                      ", one grouped RCCL gather of the coefficient blocks + DC stream to rank 0 per step"
+                      if gather else ""))
+        else:
+            wl = ("BASELINE configs[2]: " if args.workload == "8k" else "") + wl
         out = {
             "metric": "Mpixels/s encode (DCT+quantize+zig-zag) at 8K; % HBM roofline, 1/2/4/8 GPU",
             "value": round(value, 2),
@@ -286,30 +385,33 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak" if (world == 1 or args.mode == "weak") else "strong",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (uniform random uint8 RGB, resident in HBM)",
             "config": {
-                "workload": "7680x4320 RGB -> YCrCb 4:2:0 full encode: colour+pyrDown, 8x8 DCT+quantize+zig-zag "
-                            "(3 planes), DC DPCM + AC RLE (3 planes)",
-                "image_hw": [H, W8K],
+                "workload": wl,
+                "image_hw": [H, W0],
                 "per_rank_rows": in_rows if world == 1 else encs[0].rows[1] - encs[0].rows[0],
                 "mode": "single" if world == 1 else args.mode,
                 "streams": args.streams,
-                "gather_to_rank0": bool(args.gather and world > 1),
+                "gather_to_rank0": gather,
+                "gather_us_per_step": None if gather_us is None else round(gather_us, 2),
+                "dist_backend": None if world == 1 else args.dist_backend + (" (same device)" if args.same_device
+                                                                              else ""),
                 "parallelism": "dp%d tile-shard" % world,
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_dct_planes<-1,ZIGZAG_I16,15> (Y 4320x7680 + Cr, Cb 2160x3840 in one launch: "
+                "kernel": "k_dct_planes<-1,ZIGZAG_I16,15> (Y + Cr + Cb of the rank's image/shard in one launch: "
                           "AAN DCT + quantize + zig-zag + RLE tile records, per-plane table)",
                 "timed_launches": len(timed_events),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                "traffic": pmc.get("hbm_bytes_per_launch") if (pmc and world == 1 and args.workload == "8k")
+                else None,
                 "algorithmic_bytes": dct_px * 3,
                 "avg_launch_us": round(dct_us, 2),
                 "timed_over": roof_note,

@@ -713,7 +713,7 @@ __global__ __launch_bounds__(kScanT) void k_rle_scan16b(RleJobs16 jobs, uint32_t
     }
     *J.d_count = total <= J.cap ? total : -total;
   }
-  if (s_fail && threadIdx.x == 0) *J.d_count = INT64_MIN;  // hand-off timed out: report, do not hang
+  if (s_fail && threadIdx.x == 0) *J.d_count = HIC_COUNT_SCAN_TIMEOUT;  // hand-off timed out: report, do not hang
 }
 
 template <int MF, bool NT>

@@ -36,11 +36,29 @@ def input_span(H, r0, r1):
     return max(0, 2 * c0 - 2), max(r1, min(H, 2 * c1 + 2))
 
 
+# hic_rle_encode_* report failures through the count (include/hiccup_hip.h):
+# -(symbols needed) when the buffer is too small, HIC_COUNT_SCAN_TIMEOUT when a
+# cross-workgroup scan hand-off timed out (never expected; the stream is invalid)
+COUNT_SCAN_TIMEOUT = -(2 ** 63)
+
+
+def check_count(c, channel=""):
+    """Raise the error a negative symbol count stands for."""
+    if c >= 0:
+        return
+    if c == COUNT_SCAN_TIMEOUT:
+        raise _lib.HipError("RLE scan hand-off timed out (channel %s): the stream is invalid" % channel)
+    raise MemoryError("symbol buffer too small for channel %s: %d symbols needed" % (channel, -c))
+
+
 class Encoder:
     """rows=(r0, r1) makes this encoder one row-shard of an H x W image (r0 even;
     shards of one image split at multiples of 16 rows so chroma blocks align)."""
 
-    def __init__(self, H, W, max_len=15, rows=None):
+    def __init__(self, H, W, max_len=15, rows=None, out=None):
+        """out: optional {channel: (coef (n, 64) int16, dc (n,) int32)} device views the
+        encoder writes into (a gathering rank points them at its slice of the whole
+        image's buffers, so its own shard needs no copy)."""
         if H < 2 or W < 2:
             raise ValueError("image must be at least 2 x 2")
         device.require_gpu()
@@ -63,8 +81,13 @@ class Encoder:
         self.summaries = device.zeros((3, 4), torch.int64)
         for k in CHANNELS:
             n = _nblk(*self.shapes[k])
-            self.coef[k] = device.empty((n, 64), torch.int16)
-            self.dc[k] = device.empty((n,), torch.int32)
+            if out is not None:
+                self.coef[k], self.dc[k] = out[k]
+                if tuple(self.coef[k].shape) != (n, 64) or tuple(self.dc[k].shape) != (n,):
+                    raise ValueError("out[%s]: expected (%d, 64) / (%d,) views" % (k, n, n))
+            else:
+                self.coef[k] = device.empty((n, 64), torch.int16)
+                self.dc[k] = device.empty((n,), torch.int32)
             self.cap[k] = n * 63 + 1
             self.sym_len[k] = device.empty((self.cap[k],), torch.uint8)
             self.sym_val[k] = device.empty((self.cap[k],), torch.int16)
@@ -133,8 +156,7 @@ class Encoder:
         out = {}
         for i, k in enumerate(CHANNELS):
             c = int(counts[i])
-            if c < 0:
-                raise MemoryError("symbol buffer too small for channel %s" % k)
+            check_count(c, k)
             out[k] = (self.coef[k].cpu().numpy(), self.dc[k].cpu().numpy(), self.sym_len[k][:c].cpu().numpy(),
                       self.sym_val[k][:c].cpu().numpy())
         return out

@@ -12,8 +12,18 @@ step, and it is tiny: each rank all-gathers a 4-word summary per channel
 {carry zeros, emits EOB, has previous DC, previous DC} (hic_rle_stitch, on the
 device), and then emits exactly the symbols of its slice of the single-GPU
 stream.  A second all-gather of the per-channel symbol counts gives every rank its
-global offsets.  ``gather_streams`` optionally reassembles the coefficient stream
-on one rank (point-to-point RCCL sends into offset slices).
+global offsets.
+
+Reassembly on one rank (north_star's "single RCCL gather"): every rank's
+zig-zag coefficient blocks and DC differences are a contiguous slice of the whole
+image's (block-row shards, raster block order), and their sizes follow from the
+shard plan alone.  ``ShardEncoder.gather_coefficients`` therefore moves them with
+ONE grouped point-to-point batch (``dist.batch_isend_irecv``: an RCCL group of
+sends / receives on the encode stream) straight into the gathering rank's
+whole-image buffers -- no host synchronisation, no sizes exchanged first.  The
+gathering rank's own encoder writes into its slice of those buffers in place.
+``gather_streams`` (tests, tools) also collects the variable-length symbol
+streams; it needs the counts on the host.
 """
 import ctypes
 
@@ -72,16 +82,49 @@ def exchange(summ_local, world, group=None):
     return out.view((world,) + shape)
 
 
-class ShardEncoder:
-    """One rank's part of a tile-sharded encode of an H x W RGB image."""
+def block_ranges(H, W, world):
+    """{channel: [(b0, b1)] per rank}: each rank's blocks in the whole image's
+    raster block order (4:2:0 chroma planes are (H/2) x (W/2))."""
+    out = {}
+    for k in CHANNELS:
+        h, w = (H, W) if k == "lum" else (H // 2, W // 2)
+        nbx = -(-w // 8)
+        rr = []
+        for r0, r1 in plan(H, world):
+            if k == "lum":
+                a, b = r0, r1
+            else:
+                a, b = r0 // 2, min(h, r1 // 2)
+            rr.append(((a // 8) * nbx, -(-b // 8) * nbx))
+        out[k] = rr
+    return out
 
-    def __init__(self, H, W, rank=None, world=None, group=None, max_len=15):
+
+class ShardEncoder:
+    """One rank's part of a tile-sharded encode of an H x W RGB image.
+
+    gather_to: the rank that reassembles the whole image's coefficient blocks and
+    DC differences (gather_coefficients); None = no reassembly buffers."""
+
+    def __init__(self, H, W, rank=None, world=None, group=None, max_len=15, gather_to=None):
         self.rank = dist.get_rank(group) if rank is None else rank
         self.world = dist.get_world_size(group) if world is None else world
         self.group = group
         self.H, self.W = H, W
         self.rows = plan(H, self.world)[self.rank]
-        self.enc = pipeline.Encoder(H, W, max_len=max_len, rows=self.rows)
+        self.ranges = block_ranges(H, W, self.world)
+        self.gather_to = gather_to
+        out = None
+        if gather_to is not None and self.rank == gather_to:
+            # whole-image buffers; this rank's encoder writes its slice in place
+            self.full_coef, self.full_dc, out = {}, {}, {}
+            for k in CHANNELS:
+                n = self.ranges[k][-1][1]
+                self.full_coef[k] = device.empty((n, 64), torch.int16)
+                self.full_dc[k] = device.empty((n,), torch.int32)
+                b0, b1 = self.ranges[k][self.rank]
+                out[k] = (self.full_coef[k][b0:b1], self.full_dc[k][b0:b1])
+        self.enc = pipeline.Encoder(H, W, max_len=max_len, rows=self.rows, out=out)
         self.span = self.enc.input_span()
         self.all_summ = device.zeros((self.world, 3, 4), torch.int64)
         self.stitch = device.zeros((3, 4), torch.int64)
@@ -92,7 +135,15 @@ class ShardEncoder:
         return self.enc.pixels
 
     def encode(self, rgb_rows, stream=None, dct_events=None):
-        """rgb_rows: device uint8 tensor of image rows self.span (shard + halo)."""
+        """rgb_rows: device uint8 tensor of image rows self.span (shard + halo).
+        Everything, the collectives included, runs in order on `stream` (RCCL
+        enqueues on torch's current stream, so it is made current here)."""
+        if stream is not None:
+            with torch.cuda.stream(stream):
+                return self._encode(rgb_rows, stream, dct_events)
+        return self._encode(rgb_rows, None, dct_events)
+
+    def _encode(self, rgb_rows, stream, dct_events):
         enc = self.enc
         enc.transform(rgb_rows, stream, in_row0=self.span[0], dct_events=dct_events)
         summ = enc.shard_summaries(stream)
@@ -108,7 +159,62 @@ class ShardEncoder:
     def offsets(self):
         """(this rank's symbol offset per channel, global totals) -- host ints (syncs)."""
         c = self.all_counts.cpu().numpy()
+        for r in range(self.world):
+            for ci, k in enumerate(CHANNELS):
+                pipeline.check_count(int(c[r, ci]), "%s (rank %d)" % (k, r))
         return c[:self.rank].sum(0), c.sum(0)
+
+    def gather_coefficients(self, stream=None):
+        """Reassemble the whole image's zig-zag coefficient blocks and DC
+        differences on rank gather_to: one grouped batch of RCCL sends / receives on
+        `stream`, sized by the shard plan (no host sync).  Returns
+        {channel: (coef, dc)} whole-image device tensors on gather_to, None elsewhere."""
+        if self.gather_to is None:
+            raise ValueError("ShardEncoder(gather_to=...) was not set")
+        if stream is not None:
+            with torch.cuda.stream(stream):
+                return self._gather_coefficients()
+        return self._gather_coefficients()
+
+    def _gather_coefficients(self):
+        full = {k: (self.full_coef[k], self.full_dc[k]) for k in CHANNELS} if self.rank == self.gather_to else None
+        mine = {k: (self.enc.coef[k], self.enc.dc[k]) for k in CHANNELS}
+        gather_blocks(mine, full, self.ranges, self.rank, self.world, self.gather_to, self.group)
+        return full
+
+
+def gather_blocks(mine, full, ranges, rank, world, dst, group=None):
+    """The grouped gather itself (device-agnostic, so the CPU gloo tests run this
+    exact code): mine = {channel: (tensor, ...)} this rank's block slices; full =
+    {channel: (tensor, ...)} the whole-image tensors on dst (None elsewhere), the
+    same tuple layout, first dimension = blocks; ranges = block_ranges(...).  dst
+    receives every other rank's slices in place with ONE batch_isend_irecv group
+    (RCCL: sends / receives on the current stream, no host sync); dst's own slice
+    is expected to be written in place already.  gloo with device tensors (the
+    one-GPU rehearsal) stages through the host."""
+    ops, landing = [], []
+    gloo = dist.get_backend(group) == "gloo"
+    if rank == dst:
+        for r in range(world):
+            if r == dst:
+                continue
+            for k in CHANNELS:
+                b0, b1 = ranges[k][r]
+                for t in full[k]:
+                    t = t[b0:b1]
+                    buf = torch.empty(t.shape, dtype=t.dtype) if (gloo and t.is_cuda) else t
+                    ops.append(dist.P2POp(dist.irecv, buf, r, group=group))
+                    landing.append((t, buf))
+    else:
+        for k in CHANNELS:
+            for t in mine[k]:
+                t = t.contiguous()
+                ops.append(dist.P2POp(dist.isend, t.cpu() if (gloo and t.is_cuda) else t, dst, group=group))
+    for req in dist.batch_isend_irecv(ops) if ops else ():
+        req.wait()
+    for t, buf in landing:
+        if buf is not t:
+            t.copy_(buf)
 
 
 def _send(t, dst, group):
@@ -127,8 +233,10 @@ def _recv(t, src, group):
 
 
 def gather_streams(se, dst=0):
-    """Reassemble the global symbol / DC streams on rank `dst` (RCCL send/recv).
-    Returns {channel: (dc_diff, sym_len, sym_val)} host arrays on dst, None elsewhere."""
+    """Reassemble the global symbol / DC streams on rank `dst` (RCCL send/recv;
+    tests and tools: the counts cross to the host first).  Returns {channel:
+    (dc_diff, sym_len, sym_val)} host arrays on dst, None elsewhere."""
+    se.offsets()  # raises on a failed rank
     counts = se.all_counts.cpu().numpy()
     nblk = torch.tensor([se.enc.dc[k].numel() for k in CHANNELS], dtype=torch.int64, device=se.all_counts.device)
     all_nblk = torch.zeros((se.world, 3), dtype=torch.int64, device=nblk.device)

@@ -35,6 +35,7 @@ extern "C" {
 #define HIC_ERR_ARG (-1)      /* bad shape / pointer / enum: the reference asserts or raises */
 #define HIC_ERR_HIP (-2)      /* HIP runtime failure (launch, memcpy) */
 #define HIC_ERR_CAPACITY (-3) /* caller's output buffer too small */
+#define HIC_COUNT_SCAN_TIMEOUT INT64_MIN /* *d_count of an RLE encode whose scan hand-off timed out */
 
 /* model.QTables (model.py:25-27) -> quantization.table (quantization.py:14-37) */
 #define HIC_TABLE_LUMINANCE 0
@@ -183,7 +184,8 @@ int hic_izigzag_blocks_i32(const int32_t *blocks, int64_t H, int64_t W, int N, i
  *  Symbols are written SoA: sym_len[i] zeros followed by sym_val[i]; a trailing
  *  zero run becomes the single EOB (0,0); runs >= max_len are split into
  *  (max_len-1, 0) fillers (max_len 0 = no split, reference max_len=None).
- *  *d_count (device int64) receives the symbol count, or -(needed) if sym_cap was
+ *  *d_count (device int64) receives the symbol count, HIC_COUNT_SCAN_TIMEOUT if a
+ *  cross-workgroup scan hand-off timed out (never expected), or -(needed) if sym_cap was
  *  too small (nothing past sym_cap is written).
  *  Sharded use (tile-sharded image, one stream across ranks): d_stitch (device,
  *  int64[4] = {carry_zeros, emit_eob, has_prev_dc, prev_dc}) or NULL for a whole

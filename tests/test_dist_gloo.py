@@ -1,9 +1,10 @@
 """Multi-process (world_size 2 and 3, gloo on CPU) test of the tile-sharded
-encode's exchange step: each rank holds a block-row shard of the coefficient
+encode's exchange steps: each rank holds a block-row shard of the coefficient
 streams, all-gathers its channel summaries with sharding.exchange, derives its
 stitch record with sharding.stitch_host, run-length codes its slice, and rank 0
-reassembles the streams with point-to-point sends.  The result must equal the
-single-stream encode.  (Per-shard compute here is the CPU oracle -- test
+reassembles (a) the coefficient blocks + DC stream with sharding.gather_blocks --
+the same grouped batch_isend_irecv code the RCCL path runs -- and (b) the symbol
+streams with point-to-point sends.  Both must equal the single-stream encode.  (Per-shard compute here is the CPU oracle -- test
 infrastructure; the GPU kernels for the same steps are covered by
 tests/test_gpu_codec.py::test_shards_stitch_to_single_stream.)"""
 import os
@@ -69,6 +70,7 @@ def _worker(rank, world, port, H, W, results):
     try:
         zz = _zz_planes(_image(H, W))
         r0, r1 = sharding.plan(H, world)[rank]
+        ranges = sharding.block_ranges(H, W, world)
         mine = {}
         for k in pipeline.CHANNELS:
             nbx = -(-(W if k == "lum" else W // 2) // 8)
@@ -77,11 +79,30 @@ def _worker(rank, world, port, H, W, results):
             else:
                 c1 = min(H // 2, r1 // 2)
                 b0, b1 = (r0 // 16) * nbx, (-(-c1 // 8)) * nbx
+            assert ranges[k][rank] == (b0, b1)
             mine[k] = zz[k][b0:b1]
         summ = torch.tensor([_summary(mine[k]) for k in pipeline.CHANNELS], dtype=torch.int64)
         allsum = sharding.exchange(summ, world).numpy()
         enc = {k: _rle_stitched(mine[k], sharding.stitch_host(allsum[:, c], rank))
                for c, k in enumerate(pipeline.CHANNELS)}
+        # (a) the grouped coefficient / DC gather (sharding.gather_blocks)
+        parts = {k: (torch.from_numpy(np.ascontiguousarray(mine[k], dtype=np.int16)),
+                     torch.from_numpy(np.ascontiguousarray(enc[k][0], dtype=np.int32)))
+                 for k in pipeline.CHANNELS}
+        full = None
+        if rank == 0:
+            full = {k: (torch.full((len(zz[k]), 64), -7, dtype=torch.int16),
+                        torch.full((len(zz[k]),), -7, dtype=torch.int32)) for k in pipeline.CHANNELS}
+            for k in pipeline.CHANNELS:
+                b0, b1 = ranges[k][0]
+                full[k][0][b0:b1] = parts[k][0]
+                full[k][1][b0:b1] = parts[k][1]
+        sharding.gather_blocks(parts, full, ranges, rank, world, 0)
+        if rank == 0:
+            for k in pipeline.CHANNELS:
+                results["blocks_" + k] = bool(
+                    np.array_equal(full[k][0].numpy(), zz[k].astype(np.int16))
+                    and np.array_equal(full[k][1].numpy(), orc.dpcm(zz[k][:, 0].astype(np.int64)).astype(np.int32)))
         # reassemble on rank 0: sizes first, then point-to-point payloads
         sizes = torch.tensor([[len(enc[k][0]), len(enc[k][1])] for k in pipeline.CHANNELS], dtype=torch.int64)
         all_sizes = sharding.exchange(sizes, world).numpy()
@@ -112,9 +133,11 @@ def _worker(rank, world, port, H, W, results):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,H,W", [(2, 96, 80), (3, 130, 72)])
+@pytest.mark.parametrize("world,H,W", [(2, 96, 80), (3, 130, 72), (4, 160, 48)])
 def test_sharded_exchange_gloo(world, H, W):
     mgr = mp.Manager()
     results = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), H, W, results), nprocs=world, join=True)
-    assert dict(results) == {k: True for k in pipeline.CHANNELS}
+    exp = {k: True for k in pipeline.CHANNELS}
+    exp.update({"blocks_" + k: True for k in pipeline.CHANNELS})
+    assert dict(results) == exp

@@ -26,23 +26,28 @@ def _free_port():
     return p
 
 
-def _image(H, W):
+def _image(H, W, flat_rows=None):
     rng = np.random.default_rng(5)
     rgb = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
     rgb[H // 3: H // 3 + 48] = 128   # all-zero AC runs across a shard boundary
     rgb[:, : W // 5] = 40            # a flat band: long carried runs
+    if flat_rows:                    # a whole shard without any nonzero AC: the
+        rgb[flat_rows[0]:flat_rows[1]] = 128  # carried run chains through it
     return rgb
 
 
-def _rank(rank, world, port, H, W, out_path):
+def _rank(rank, world, port, H, W, flat_rows, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from hiccup_amd import device, pipeline, sharding
     torch.cuda.set_device(0)
-    rgb = _image(H, W)
-    se = sharding.ShardEncoder(H, W, rank=rank, world=world)
+    rgb = _image(H, W, flat_rows)
+    se = sharding.ShardEncoder(H, W, rank=rank, world=world, gather_to=0)
     a, b = se.span
-    se.encode(device.to_device(rgb[a:b]))
+    # a non-current stream: the collectives must follow it
+    s = torch.cuda.Stream()
+    se.encode(device.to_device(rgb[a:b]), stream=s)
+    blocks = se.gather_coefficients(stream=s)
     torch.cuda.synchronize()
     got = sharding.gather_streams(se)
     if rank == 0:
@@ -53,6 +58,9 @@ def _rank(rank, world, port, H, W, out_path):
         for k in pipeline.CHANNELS:
             D, L, V = got[k]
             ok &= np.array_equal(D, ref[k][1]) and np.array_equal(L, ref[k][2]) and np.array_equal(V, ref[k][3])
+            # the grouped gather's whole-image blocks / DC stream
+            ok &= np.array_equal(blocks[k][0].cpu().numpy(), ref[k][0])
+            ok &= np.array_equal(blocks[k][1].cpu().numpy(), ref[k][1])
         offs, tot = se.offsets()
         ok &= [int(x) for x in tot] == [len(ref[k][2]) for k in pipeline.CHANNELS]
         with open(out_path, "w") as f:
@@ -61,9 +69,10 @@ def _rank(rank, world, port, H, W, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,H,W", [(2, 256, 384), (3, 4320 // 4, 7680 // 2)])
-def test_sharded_encode_multiprocess(world, H, W):
+@pytest.mark.parametrize("world,H,W,flat", [(2, 256, 384, None), (3, 4320 // 4, 7680 // 2, None),
+                                            (3, 384, 256, (120, 264))])
+def test_sharded_encode_multiprocess(world, H, W, flat):
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "result")
-        mp.spawn(_rank, args=(world, _free_port(), H, W, out), nprocs=world, join=True)
+        mp.spawn(_rank, args=(world, _free_port(), H, W, flat, out), nprocs=world, join=True)
         assert open(out).read() == "ok"

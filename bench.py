@@ -59,7 +59,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=25.0)
     ap.add_argument("--no-extras", action="store_true",
-                    help="skip the BASELINE configs[1] / configs[4] side measurements (N=1 only)")
+                    help="skip the BASELINE configs[1] / configs[4] side measurements (at N > 1: configs[4], "
+                         "the sharded 16K round trip)")
     return ap.parse_args()
 
 
@@ -180,6 +181,59 @@ def extra_16k_roundtrip(steps=4):
     del xs, enc, dec
     torch.cuda.empty_cache()
     return {"workload": "16384x16384 RGB encode + decode round trip, 1 GPU (BASELINE configs[4] at N=1)",
+            "ms_per_roundtrip": round(dt * 1e3, 3), "mpix_s": round(n * n / dt / 1e6, 1),
+            "psnr_db_vs_input": round(10 * np.log10(255.0 ** 2 / mse), 3), "timed_roundtrips": steps}
+
+
+def extra_16k_roundtrip_sharded(rank, world, backend, steps=4):
+    """BASELINE configs[4] at N ranks: a 16384 x 16384 random RGB image tile-sharded
+    by block rows.  Each rank encodes its shard (ShardEncoder: colour with halo, DCT,
+    its slice of the single DC / RLE stream after the summary all-gather) and then
+    decodes its own slice (ShardDecoder: carried-zero skip, DC chain from the stitch
+    record, one chroma halo row per neighbour over the process group for pyrUp,
+    YCrCb -> RGB of its rows).  Each rank's symbol counts cross to its host between
+    the halves.  PSNR of the whole reconstruction vs the input (squared errors
+    summed over ranks); its bit-exactness vs the single-GPU decode is
+    tests/test_dist_gpu.py / test_gpu_codec.py::test_shards_stitch_to_single_stream."""
+    from hiccup_amd import sharding
+    n = 16384
+    se = sharding.ShardEncoder(n, n, rank=rank, world=world)
+    sd = sharding.ShardDecoder(n, n, rank=rank, world=world)
+    a, b = se.span
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5 + rank)
+    xs = [torch.randint(0, 256, (b - a, n, 3), dtype=torch.uint8, device="cuda", generator=g) for _ in range(2)]
+
+    def trip(i):
+        se.encode(xs[i % 2])
+        counts = se.enc.counts.cpu().tolist()
+        return sd.decode(se.enc.sym_len, se.enc.sym_val, counts, se.enc.dc, se.stitch)
+
+    trip(0)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        out = trip(1 + i)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    sd.check_status()
+    x = xs[steps % 2]
+    o0, o1 = sd.out_rows
+    sq = float(((out.float() - x[o0 - a:o1 - a].float()) ** 2).sum())
+    dev = "cuda" if backend == "nccl" else "cpu"
+    t = torch.tensor([dt, sq], dtype=torch.float64, device=dev)
+    tmax = t.clone()
+    dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    dt, mse = float(tmax[0].item()), float(t[1].item()) / (n * n * 3)
+    del xs, se, sd
+    torch.cuda.empty_cache()
+    return {"workload": "16384x16384 RGB encode + decode round trip, tile-sharded over %d ranks "
+                        "(BASELINE configs[4]; sharded encode + sharded decode with pyrUp halo exchange)" % world,
             "ms_per_roundtrip": round(dt * 1e3, 3), "mpix_s": round(n * n / dt / 1e6, 1),
             "psnr_db_vs_input": round(10 * np.log10(255.0 ** 2 / mse), 3), "timed_roundtrips": steps}
 
@@ -361,6 +415,14 @@ def main():
                      % (len(streams), " and gathers to rank 0" if gather else ""))
     achieved = dct_px * 3 / (dct_us * 1e-6) / 1e9  # u8 in + int16 out per pixel
 
+    per_rank_rows = in_rows if world == 1 else encs[0].rows[1] - encs[0].rows[0]
+    extra_sharded = None
+    if world > 1 and not args.no_extras:
+        # free the 8K run's buffers first (every rank holds ~1.2 GB of inputs)
+        del encs, inputs
+        torch.cuda.empty_cache()
+        extra_sharded = extra_16k_roundtrip_sharded(rank, world, args.dist_backend)
+
     if rank == 0:
         total_px = px_per_step_rank * world * args.steps
         value = total_px / elapsed / 1e6
@@ -392,7 +454,7 @@ def main():
             "config": {
                 "workload": wl,
                 "image_hw": [H, W0],
-                "per_rank_rows": in_rows if world == 1 else encs[0].rows[1] - encs[0].rows[0],
+                "per_rank_rows": per_rank_rows,
                 "mode": "single" if world == 1 else args.mode,
                 "streams": args.streams,
                 "gather_to_rank0": gather,
@@ -420,6 +482,8 @@ def main():
         }
         if not args.no_extras and world == 1:
             out["extra_configs"] = {"4k_luma_dct": extra_4k_luma(), "16k_roundtrip": extra_16k_roundtrip()}
+        if extra_sharded is not None:
+            out["extra_configs"] = {"16k_roundtrip": extra_sharded}
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args.cpu_budget_s)
         elif not args.no_cpu_baseline:

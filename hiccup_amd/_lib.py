@@ -69,6 +69,7 @@ SIGNATURES = {
     "hic_pyr_down_u8": (_int, [_vp, _i64, _i64, _vp, _i64, _i64, _vp]),
     "hic_pyr_up_u8": (_int, [_vp, _i64, _i64, _vp, _i64, _i64, _vp]),
     "hic_ycrcb420_to_rgb": (_int, [_vp, _i64, _vp, _vp, _i64, _i64, _vp, _vp]),
+    "hic_ycrcb420_to_rgb_rows": (_int, [_vp, _i64, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp]),
     "hic_zigzag_blocks_i32": (_int, [_vp, _i64, _i64, _int, _vp, _vp]),
     "hic_izigzag_blocks_i32": (_int, [_vp, _i64, _i64, _int, _vp, _vp]),
     "hic_rle_workspace_bytes": (_sz, [_i64, _int]),
@@ -81,6 +82,7 @@ SIGNATURES = {
     "hic_rle_stream_decode_i32": (_int, [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _vp]),
     "hic_rld_workspace_bytes": (_sz, [_i64, _i64]),
     "hic_rle_decode_i16": (_int, [_vp, _vp, _i64, _vp, _i64, _int, _vp, _vp, _vp, _vp]),
+    "hic_rle_decode_i16_shard": (_int, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
     "hic_rle_decode_i32": (_int, [_vp, _vp, _i64, _vp, _i64, _int, _vp, _vp, _vp, _vp]),
 }
 

@@ -338,7 +338,9 @@ __device__ __forceinline__ void up_taps(int o, int n, int (&idx)[3], int (&w)[3]
   }
 }
 
-__device__ __forceinline__ int pyr_up_at(const uint8_t *__restrict__ src, int H, int W, int oy, int ox) {
+// row0: the image row src's first row holds (a shard's buffer starts mid-image)
+__device__ __forceinline__ int pyr_up_at(const uint8_t *__restrict__ src, int H, int W, int oy, int ox,
+                                         int row0 = 0) {
   int iy[3], wy[3], ix[3], wx[3];
   up_taps(oy, H, iy, wy);
   up_taps(ox, W, ix, wx);
@@ -347,7 +349,7 @@ __device__ __forceinline__ int pyr_up_at(const uint8_t *__restrict__ src, int H,
   for (int a = 0; a < 3; ++a) {
     int row = 0;
 #pragma unroll
-    for (int b = 0; b < 3; ++b) row += wx[b] * src[(int64_t)iy[a] * W + ix[b]];
+    for (int b = 0; b < 3; ++b) row += wx[b] * src[(int64_t)(iy[a] - row0) * W + ix[b]];
     acc += wy[a] * row;
   }
   return (int)sat8((acc + 32) >> 6);
@@ -360,14 +362,16 @@ __global__ void k_pyr_up(const uint8_t *__restrict__ src, int H, int W, uint8_t 
   dst[(int64_t)oy * DW + ox] = (uint8_t)pyr_up_at(src, H, W, oy, ox);
 }
 
-// pyrUp(cr), pyrUp(cb) to 2h x 2w, crop y, cvtColor(YCrCb2RGB)
+// pyrUp(cr), pyrUp(cb) to 2h x 2w, crop y, cvtColor(YCrCb2RGB); output rows from
+// 2 sb on (Y and rgb point at row 2 sb), chroma buffers starting at image row c_row0
 __global__ void k_ycrcb420_rgb(const uint8_t *__restrict__ Y, int64_t ystride, const uint8_t *__restrict__ Cr,
-                               const uint8_t *__restrict__ Cb, int h, int w, uint8_t *__restrict__ rgb) {
-  const int ox = blockIdx.x * blockDim.x + threadIdx.x, oy = blockIdx.y;
-  if (ox >= 2 * w || oy >= 2 * h) return;
+                               const uint8_t *__restrict__ Cb, int h, int w, int sb, int c_row0,
+                               uint8_t *__restrict__ rgb) {
+  const int ox = blockIdx.x * blockDim.x + threadIdx.x, oy = blockIdx.y;  // oy: relative to 2 sb
+  if (ox >= 2 * w) return;
   const int y = Y[(int64_t)oy * ystride + ox];
-  const int cr = pyr_up_at(Cr, h, w, oy, ox) - 128;
-  const int cb = pyr_up_at(Cb, h, w, oy, ox) - 128;
+  const int cr = pyr_up_at(Cr, h, w, 2 * sb + oy, ox, c_row0) - 128;
+  const int cb = pyr_up_at(Cb, h, w, 2 * sb + oy, ox, c_row0) - 128;
   uint8_t *o = rgb + ((int64_t)oy * 2 * w + ox) * 3;
   o[0] = (uint8_t)sat8(y + descale14(cr * kCR2R));
   o[1] = (uint8_t)sat8(y + descale14(cb * kCB2G + cr * kCR2G));
@@ -385,9 +389,15 @@ __global__ void k_ycrcb420_rgb(const uint8_t *__restrict__ Y, int64_t ystride, c
 // right / bottom.
 constexpr int kUpSeg = 8;
 
+// Row-range form (a tile shard's decode, sharding.ShardDecoder): chroma rows
+// [sb, se) of an h-row image are produced, i.e. output rows [2 sb, 2 se); Y and rgb
+// point at output row 2 sb; Cr / Cb hold chroma rows from c_row0 on (the shard's
+// rows plus one halo row from each neighbour: rows sb - 1 and se are read when they
+// exist).  The whole image is sb = 0, se = h, c_row0 = 0.
 __global__ __launch_bounds__(256) void k_ycrcb420_rgb_walk(const uint8_t *__restrict__ Y, int64_t ystride,
                                                            const uint8_t *__restrict__ Cr,
                                                            const uint8_t *__restrict__ Cb, int h, int w,
+                                                           int sb, int se, int c_row0,
                                                            uint8_t *__restrict__ rgb, int nstrips, int nwaves) {
   const int lane = threadIdx.x & 63;
   const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -397,11 +407,11 @@ __global__ __launch_bounds__(256) void k_ycrcb420_rgb_walk(const uint8_t *__rest
   const int q = strip * 64 + lane;
   const bool owner = q < nq;
   const int qc = owner ? q : nq - 1;
-  const int s0 = seg * kUpSeg;
-  const int ns = h - s0 < kUpSeg ? h - s0 : kUpSeg;
+  const int s0 = sb + seg * kUpSeg;
+  const int ns = se - s0 < kUpSeg ? se - s0 : kUpSeg;
   // horizontally filtered chroma row r: [cr x4 | cb x4] for output columns 4q..4q+3 (x8 scale)
   auto hrow = [&](int r, int (&hc)[4], int (&hb)[4]) {
-    const int64_t o = (int64_t)r * w + 2 * qc;
+    const int64_t o = (int64_t)(r - c_row0) * w + 2 * qc;
     const uint32_t cr2 = *reinterpret_cast<const uint16_t *>(Cr + o);
     const uint32_t cb2 = *reinterpret_cast<const uint16_t *>(Cb + o);
     const uint32_t own = cr2 | cb2 << 16;  // cr[2q], cr[2q+1], cb[2q], cb[2q+1]
@@ -440,7 +450,7 @@ __global__ __launch_bounds__(256) void k_ycrcb420_rgb_walk(const uint8_t *__rest
     hrow(s + 1 < h ? s + 1 : h - 1, nc, nb);
 #pragma unroll
     for (int odd = 0; odd < 2; ++odd) {
-      const int oy = 2 * s + odd;
+      const int oy = 2 * (s - sb) + odd;  // output row, relative to 2 sb
       const uint32_t yq = *reinterpret_cast<const uint32_t *>(Y + (int64_t)oy * ystride + 4 * qc);
       uint32_t px[4];
 #pragma unroll
@@ -555,20 +565,31 @@ extern "C" int hic_pyr_up_u8(const uint8_t *src, int64_t H, int64_t W, uint8_t *
   return check_launch("k_pyr_up");
 }
 
+extern "C" int hic_ycrcb420_to_rgb_rows(const uint8_t *y, int64_t y_stride, const uint8_t *cr, const uint8_t *cb,
+                                        int64_t c_row0, int64_t c_rows, int64_t h, int64_t w, int64_t s0, int64_t s1,
+                                        uint8_t *rgb, void *stream) {
+  if (!y || !cr || !cb || !rgb) return arg_error("null pointer");
+  if (!dims_ok(2 * h, 2 * w) || y_stride < 2 * w) return arg_error("shape");
+  if (s0 < 0 || s1 > h || s1 <= s0) return arg_error("chroma row range");
+  // pyrUp reads chroma rows s0 - 1 .. s1 (clamped to the image)
+  const int64_t need0 = s0 > 0 ? s0 - 1 : 0, need1 = s1 < h ? s1 + 1 : h;
+  if (c_row0 > need0 || c_row0 + c_rows < need1) return arg_error("chroma rows do not cover the pyrUp halo");
+  if (w % 2 || y_stride % 4 || reinterpret_cast<uintptr_t>(y) % 4 || reinterpret_cast<uintptr_t>(rgb) % 4 ||
+      reinterpret_cast<uintptr_t>(cr) % 2 || reinterpret_cast<uintptr_t>(cb) % 2 || knob(HIC_KNOB_COLOR_TILED)) {
+    hipLaunchKernelGGL(k_ycrcb420_rgb, dim3((unsigned)((2 * w + 255) / 256), (unsigned)(2 * (s1 - s0))), dim3(256), 0,
+                       as_stream(stream), y, y_stride, cr, cb, (int)h, (int)w, (int)s0, (int)c_row0, rgb);
+    return check_launch("k_ycrcb420_rgb");
+  }
+  const int nstrips = (int)((w / 2 + 63) / 64), nseg = (int)((s1 - s0 + kUpSeg - 1) / kUpSeg);
+  const int nwaves = nstrips * nseg;
+  hipLaunchKernelGGL(k_ycrcb420_rgb_walk, dim3((unsigned)((nwaves + 3) / 4)), dim3(256), 0, as_stream(stream), y,
+                     y_stride, cr, cb, (int)h, (int)w, (int)s0, (int)s1, (int)c_row0, rgb, nstrips, nwaves);
+  return check_launch("k_ycrcb420_rgb_walk");
+}
+
 extern "C" int hic_ycrcb420_to_rgb(const uint8_t *y, int64_t y_stride, const uint8_t *cr, const uint8_t *cb,
                                    int64_t h, int64_t w, uint8_t *rgb, void *stream) {
   if (!y || !cr || !cb || !rgb) return arg_error("null pointer");
   if (!dims_ok(2 * h, 2 * w) || y_stride < 2 * w) return arg_error("shape");
-  if (w % 2 == 0 && y_stride % 4 == 0 && reinterpret_cast<uintptr_t>(y) % 4 == 0 &&
-      reinterpret_cast<uintptr_t>(rgb) % 4 == 0 && reinterpret_cast<uintptr_t>(cr) % 2 == 0 &&
-      reinterpret_cast<uintptr_t>(cb) % 2 == 0 && knob(HIC_KNOB_COLOR_TILED) == 0) {
-    const int nstrips = (int)((w / 2 + 63) / 64), nseg = (int)((h + kUpSeg - 1) / kUpSeg);
-    const int nwaves = nstrips * nseg;
-    hipLaunchKernelGGL(k_ycrcb420_rgb_walk, dim3((unsigned)((nwaves + 3) / 4)), dim3(256), 0, as_stream(stream), y,
-                       y_stride, cr, cb, (int)h, (int)w, rgb, nstrips, nwaves);
-    return check_launch("k_ycrcb420_rgb_walk");
-  }
-  hipLaunchKernelGGL(k_ycrcb420_rgb, dim3((unsigned)((2 * w + 255) / 256), (unsigned)(2 * h)), dim3(256), 0,
-                     as_stream(stream), y, y_stride, cr, cb, (int)h, (int)w, rgb);
-  return check_launch("k_ycrcb420_rgb");
+  return hic_ycrcb420_to_rgb_rows(y, y_stride, cr, cb, 0, h, h, w, 0, h, rgb, stream);
 }

@@ -922,11 +922,14 @@ __global__ __launch_bounds__(kTB) void k_dc_apply(const int32_t *__restrict__ di
 }
 
 __global__ void k_rld_status(const int64_t *__restrict__ total, const int64_t *__restrict__ last_sym, int64_t n_ac,
-                             int64_t *__restrict__ status) {
-  // codec.decode_run_length: EOB (last symbol (0,0)) zero-fills up to `length`
-  const int64_t t = *total;
+                             const int64_t *__restrict__ stitch, int64_t *__restrict__ status) {
+  // codec.decode_run_length: EOB (last symbol (0,0)) zero-fills up to `length`.  A
+  // shard that does not close the stream (stitch[1] == 0) ends in the zero run the
+  // next shard carries on, so it zero-fills too; its positions start `carry` early.
+  const int64_t t = *total - (stitch ? stitch[0] : 0);
   const bool eob = last_sym[0] == 0 && last_sym[1] == 0;
-  *status = (eob && t < n_ac) ? n_ac : t;
+  const bool open_end = stitch && stitch[1] == 0;
+  *status = ((eob || open_end) && t <= n_ac) ? n_ac : t;
 }
 
 template <typename L_T, typename V_T>
@@ -971,10 +974,14 @@ __global__ __launch_bounds__(kTB) void k_rld_tile16(const uint8_t *__restrict__ 
   if (threadIdx.x == 0) tile_sum[blockIdx.x] = total;
 }
 
+// stitch (a shard's hic_rle_stitch record, or null): the chain starts at the
+// previous shard's last DC instead of 0
 __global__ __launch_bounds__(kTB) void k_dc_values16(const int32_t *__restrict__ diff, int64_t nblk,
-                                                     const int64_t *__restrict__ tile_off, int16_t *__restrict__ dcval) {
+                                                     const int64_t *__restrict__ tile_off,
+                                                     const int64_t *__restrict__ stitch, int16_t *__restrict__ dcval) {
   __shared__ int64_t s_buf[8];
   const int64_t s0 = (int64_t)blockIdx.x * kTS + (int64_t)threadIdx.x * kSPT;
+  const int64_t base = (stitch && stitch[2]) ? stitch[3] : 0;
   int64_t acc = 0;
   int d[kSPT];
 #pragma unroll
@@ -983,7 +990,7 @@ __global__ __launch_bounds__(kTB) void k_dc_values16(const int32_t *__restrict__
     acc += d[k];
   }
   int64_t total;
-  int64_t run = tile_off[blockIdx.x] + block_excl_sum<int64_t, kTB>(acc, s_buf, total);
+  int64_t run = base + tile_off[blockIdx.x] + block_excl_sum<int64_t, kTB>(acc, s_buf, total);
 #pragma unroll
   for (int k = 0; k < kSPT; ++k)
     if (s0 + k < nblk) {
@@ -1011,6 +1018,7 @@ template <bool NT>
 __global__ __launch_bounds__(kTB) void k_rld_blocks16(const uint8_t *__restrict__ sym_len,
                                                       const int16_t *__restrict__ sym_val, int64_t nsym,
                                                       const int64_t *__restrict__ tile_off, int n_ac,
+                                                      const int64_t *__restrict__ stitch,
                                                       const int16_t *__restrict__ dcval, int16_t *__restrict__ blocks) {
   __shared__ uint4 s_win[kWinBlk * 8];
   __shared__ int64_t s_buf[8];
@@ -1040,11 +1048,15 @@ __global__ __launch_bounds__(kTB) void k_rld_blocks16(const uint8_t *__restrict_
 #pragma unroll
   for (int k = 0; k < kDS; ++k) acc += len[k] + 1;
   int64_t tot64;
-  const int64_t P0l = tile_off[blockIdx.x];
+  // a shard's stream starts `carry` zeros before its first block (the run it
+  // continues from the previous shards: hic_rle_stitch)
+  const int64_t skip = stitch ? stitch[0] : 0;
+  const int64_t P0l = tile_off[blockIdx.x] - skip;
   const int64_t my = P0l + block_excl_sum<int64_t, kTB>((int64_t)acc, s_buf, tot64);
-  // positions fit int32 (the launcher checks n_ac < 2^31); clamp at n_ac
-  const int P0 = (int)(P0l < n_ac ? P0l : n_ac);
-  const int P1 = (int)(P0l + tot64 < n_ac ? P0l + tot64 : n_ac);
+  // positions fit int32 (the launcher checks n_ac < 2^31); clamp to [0, n_ac]
+  const int64_t P1l = P0l + tot64;
+  const int P0 = (int)(P0l < 0 ? 0 : (P0l < n_ac ? P0l : n_ac));
+  const int P1 = (int)(P1l < 0 ? 0 : (P1l < n_ac ? P1l : n_ac));
   if (P1 <= P0) return;  // uniform
   int pos[kDS];
   {
@@ -1052,7 +1064,7 @@ __global__ __launch_bounds__(kTB) void k_rld_blocks16(const uint8_t *__restrict_
 #pragma unroll
     for (int k = 0; k < kDS; ++k) {
       q += len[k];
-      pos[k] = (len[k] >= 0 && q < n_ac) ? (int)q : -1;
+      pos[k] = (len[k] >= 0 && q >= 0 && q < n_ac) ? (int)q : -1;
       ++q;
     }
   }
@@ -1097,9 +1109,11 @@ __global__ __launch_bounds__(kTB) void k_rld_blocks16(const uint8_t *__restrict_
 // positions [*total, n_ac): zeros (codec.decode_run_length's EOB fill), and the DC of
 // every block whose first AC lies there
 __global__ __launch_bounds__(kTB) void k_rld_tail16(const int64_t *__restrict__ total, int64_t nblk,
+                                                    const int64_t *__restrict__ stitch,
                                                     const int16_t *__restrict__ dcval, int16_t *__restrict__ blocks) {
   const int64_t n_ac = nblk * 63;
-  const int64_t t = *total < n_ac ? *total : n_ac;
+  const int64_t tl = *total - (stitch ? stitch[0] : 0);
+  const int64_t t = tl < 0 ? 0 : (tl < n_ac ? tl : n_ac);
   if (t >= n_ac) return;
   const int64_t b0 = t / 63;
   const int64_t nchunk = (nblk - b0) * 8;
@@ -1276,13 +1290,14 @@ int rle_decode(const L_T *sym_len, const V_T *sym_val, int64_t nsym, const int32
     hipLaunchKernelGGL((k_dc_apply<T>), dim3((unsigned)ntb), dim3(kTB), 0, s, dc_diff, nblk, dsum, g.L, blocks);
   }
   hipLaunchKernelGGL((k_last_sym<L_T, V_T>), dim3(1), dim3(1), 0, s, sym_len, sym_val, nsym, last);
-  hipLaunchKernelGGL(k_rld_status, dim3(1), dim3(1), 0, s, tot, last, length, d_status);
+  hipLaunchKernelGGL(k_rld_status, dim3(1), dim3(1), 0, s, tot, last, length, nullptr, d_status);
   return check_launch("k_rld_status");
 }
 
 // The hot-path decode (see k_rld_blocks16).  Workspace as hic_rld_workspace_bytes.
 int rle_decode_blocks16(const uint8_t *sym_len, const int16_t *sym_val, int64_t nsym, const int32_t *dc_diff,
-                        int64_t nblk, int16_t *blocks, int64_t *d_status, void *ws, hipStream_t s) {
+                        int64_t nblk, const int64_t *stitch, int16_t *blocks, int64_t *d_status, void *ws,
+                        hipStream_t s) {
   const int64_t nts = (nsym + kDTS - 1) / kDTS, ntb = (nblk + kTS - 1) / kTS;
   int64_t *w = static_cast<int64_t *>(ws);
   // same int64 slots as rle_decode (its symbol tiles are smaller, so these fit)
@@ -1295,22 +1310,22 @@ int rle_decode_blocks16(const uint8_t *sym_len, const int16_t *sym_val, int64_t 
   hipLaunchKernelGGL(k_scan_inplace, dim3(1), dim3(kScanT), 0, s, tsum, nts, tot);
   hipLaunchKernelGGL(k_dc_tile, dim3((unsigned)ntb), dim3(kTB), 0, s, dc_diff, nblk, dsum);
   hipLaunchKernelGGL(k_scan_inplace, dim3(1), dim3(kScanT), 0, s, dsum, ntb, tot + 1);
-  hipLaunchKernelGGL(k_dc_values16, dim3((unsigned)ntb), dim3(kTB), 0, s, dc_diff, nblk, dsum, dcval);
+  hipLaunchKernelGGL(k_dc_values16, dim3((unsigned)ntb), dim3(kTB), 0, s, dc_diff, nblk, dsum, stitch, dcval);
   if (int e = check_launch("k_dc_values16")) return e;
   if (nts > 0) {
     const bool nt = knob(HIC_KNOB_RLD_NT) == 1;  // A/B: nontemporal block stores
     if (nt)
       hipLaunchKernelGGL(k_rld_blocks16<true>, dim3((unsigned)nts), dim3(kTB), 0, s, sym_len, sym_val, nsym, tsum,
-                       (int)(nblk * 63), dcval, blocks);
+                       (int)(nblk * 63), stitch, dcval, blocks);
     else
       hipLaunchKernelGGL(k_rld_blocks16<false>, dim3((unsigned)nts), dim3(kTB), 0, s, sym_len, sym_val, nsym, tsum,
-                       (int)(nblk * 63), dcval, blocks);
+                       (int)(nblk * 63), stitch, dcval, blocks);
     if (int e = check_launch("k_rld_blocks16")) return e;
   }
   const int64_t tail_grid = cu_count() * 8 > 0 ? cu_count() * 8 : 1024;
-  hipLaunchKernelGGL(k_rld_tail16, dim3((unsigned)tail_grid), dim3(kTB), 0, s, tot, nblk, dcval, blocks);
+  hipLaunchKernelGGL(k_rld_tail16, dim3((unsigned)tail_grid), dim3(kTB), 0, s, tot, nblk, stitch, dcval, blocks);
   hipLaunchKernelGGL((k_last_sym<uint8_t, int16_t>), dim3(1), dim3(1), 0, s, sym_len, sym_val, nsym, last);
-  hipLaunchKernelGGL(k_rld_status, dim3(1), dim3(1), 0, s, tot, last, nblk * 63, d_status);
+  hipLaunchKernelGGL(k_rld_status, dim3(1), dim3(1), 0, s, tot, last, nblk * 63, stitch, d_status);
   return check_launch("k_rld_status");
 }
 
@@ -1442,10 +1457,24 @@ extern "C" int hic_rle_decode_i16(const uint8_t *sym_len, const int16_t *sym_val
       d_status && workspace && reinterpret_cast<uintptr_t>(sym_len) % 16 == 0 &&
       reinterpret_cast<uintptr_t>(sym_val) % 16 == 0 && reinterpret_cast<uintptr_t>(blocks) % 16 == 0 &&
       knob(HIC_KNOB_RLD_GENERIC) == 0)
-    return rle_decode_blocks16(sym_len, sym_val, nsym, dc_diff, nblk, blocks, d_status, workspace, as_stream(stream));
+    return rle_decode_blocks16(sym_len, sym_val, nsym, dc_diff, nblk, nullptr, blocks, d_status, workspace,
+                               as_stream(stream));
   return rle_decode(sym_len, sym_val, nsym, dc_diff, nblk, block_geo(nblk, block_len), nblk * (block_len - 1), blocks,
                     d_status, workspace,
                     as_stream(stream));
+}
+
+extern "C" int hic_rle_decode_i16_shard(const uint8_t *sym_len, const int16_t *sym_val, int64_t nsym,
+                                        const int32_t *dc_diff, int64_t nblk, const int64_t *d_stitch,
+                                        int16_t *blocks, int64_t *d_status, void *workspace, void *stream) {
+  if (!sym_len || !sym_val || !dc_diff || !d_stitch || !blocks || !d_status || !workspace)
+    return arg_error("null pointer");
+  if (nblk <= 0 || nblk * 63 >= ((int64_t)1 << 31) || nsym < 0) return arg_error("nblk / nsym");
+  if (reinterpret_cast<uintptr_t>(sym_len) % 16 || reinterpret_cast<uintptr_t>(sym_val) % 16 ||
+      reinterpret_cast<uintptr_t>(blocks) % 16)
+    return arg_error("sym_len / sym_val / blocks must be 16-byte aligned");
+  return rle_decode_blocks16(sym_len, sym_val, nsym, dc_diff, nblk, d_stitch, blocks, d_status, workspace,
+                             as_stream(stream));
 }
 
 extern "C" int hic_rle_decode_i32(const int32_t *sym_len, const int32_t *sym_val, int64_t nsym,

@@ -88,7 +88,10 @@ class Encoder:
             else:
                 self.coef[k] = device.empty((n, 64), torch.int16)
                 self.dc[k] = device.empty((n,), torch.int32)
-            self.cap[k] = n * 63 + 1
+            # a shard's stream can open with the fillers of a zero run carried from every
+            # block before it (a flat previous shard): room for those too
+            lead = (r0 // (8 if k == "lum" else 16)) * -(-self.shapes[k][1] // 8)
+            self.cap[k] = n * 63 + 1 + (lead * 63 // max_len if max_len > 0 else 1)
             self.sym_len[k] = device.empty((self.cap[k],), torch.uint8)
             self.sym_val[k] = device.empty((self.cap[k],), torch.int16)
             self.ws[k] = device.workspace(lib.hic_rle_workspace_bytes(n, 64))
@@ -196,3 +199,12 @@ class Decoder:
         _lib.call("hic_ycrcb420_to_rgb", device.ptr(self.pix["lum"]), self.pix["lum"].stride(0),
                   device.ptr(self.pix["cr"]), device.ptr(self.pix["cb"]), h, w, device.ptr(self.rgb), s)
         return self.rgb
+
+    def check_status(self):
+        """Raise unless every channel's stream decoded to exactly its blocks' AC
+        positions (codec.jpeg_decode's length check, codec.py:418-419; syncs)."""
+        st = self.status.cpu().tolist()
+        for i, k in enumerate(CHANNELS):
+            want = self.blocks[k].shape[0] * 63
+            if st[i] != want:
+                raise ValueError("channel %s: stream covers %d AC positions, expected %d" % (k, st[i], want))

@@ -217,6 +217,140 @@ def gather_blocks(mine, full, ranges, rank, world, dst, group=None):
             t.copy_(buf)
 
 
+def exchange_halo_rows(planes, rank, world, group=None):
+    """pyrUp's halo for a row-sharded decode: every plane in `planes` is (buf, top,
+    n_own) -- buf holds this rank's n_own rows at [top, top + n_own), with one halo row
+    above (top = 1, rank > 0) and one below (row top + n_own, rank < world - 1).
+    Each rank sends its first own row up and its last own row down and receives its
+    halo rows, all in ONE batch_isend_irecv group (RCCL on the current stream; gloo
+    with device tensors stages through the host)."""
+    if world == 1:
+        return
+    ops, landing = [], []
+    gloo = dist.get_backend(group) == "gloo"
+
+    def send(t, peer):
+        t = t.contiguous()
+        ops.append(dist.P2POp(dist.isend, t.cpu() if (gloo and t.is_cuda) else t, peer, group=group))
+
+    def recv(t, peer):
+        buf = torch.empty(t.shape, dtype=t.dtype) if (gloo and t.is_cuda) else t
+        ops.append(dist.P2POp(dist.irecv, buf, peer, group=group))
+        landing.append((t, buf))
+
+    for buf, top, n_own in planes:
+        if rank > 0:
+            send(buf[top], rank - 1)
+            recv(buf[0], rank - 1)
+        if rank < world - 1:
+            send(buf[top + n_own - 1], rank + 1)
+            recv(buf[top + n_own], rank + 1)
+    for req in dist.batch_isend_irecv(ops):
+        req.wait()
+    for t, buf in landing:
+        if buf is not t:
+            t.copy_(buf)
+
+
+class ShardDecoder:
+    """One rank's part of a tile-sharded decode (codec.jpeg_decode's RLE / DC /
+    izigzag half + compression.jpeg_decompression, codec.py:397-425,
+    compression.py:42-56) of an H x W image encoded by ShardEncoders of the same
+    plan.  Each rank decodes its own slice of the channel streams (the stitch record
+    of its encode says where the slice starts: carried zeros, previous DC), runs the
+    inverse DCT on its block rows, exchanges one chroma row with each neighbour for
+    pyrUp and converts its rows to RGB: image rows [2 c0, 2 c1) (= the shard's rows
+    but for the last row of an odd-height image, as the whole-image decode)."""
+
+    def __init__(self, H, W, rank=None, world=None, group=None):
+        self.rank = dist.get_rank(group) if rank is None else rank
+        self.world = dist.get_world_size(group) if world is None else world
+        self.group = group
+        self.H, self.W = H, W
+        self.rows = plan(H, self.world)[self.rank]
+        r0, r1 = self.rows
+        self.h, self.w = H // 2, W // 2
+        self.c0, self.c1 = r0 // 2, min(self.h, r1 // 2)
+        if self.c1 <= self.c0:
+            raise ValueError("shard %r has no chroma rows" % (self.rows,))
+        self.top = 1 if self.c0 > 0 else 0
+        self.bot = 1 if self.c1 < self.h else 0
+        nc = self.c1 - self.c0
+        self.shapes = {"lum": (r1 - r0, W), "cr": (nc, self.w), "cb": (nc, self.w)}
+        self.blocks, self.status = {}, device.zeros((3,), torch.int64)
+        for k in CHANNELS:
+            self.blocks[k] = device.empty((pipeline._nblk(*self.shapes[k]), 64), torch.int16)
+        self.y = device.empty(self.shapes["lum"], torch.uint8)
+        self.cbuf = {k: device.empty((self.top + nc + self.bot, self.w), torch.uint8) for k in ("cr", "cb")}
+        self.rgb = device.empty((2 * nc, 2 * self.w, 3), torch.uint8)
+        self._ws = {}
+
+    @property
+    def out_rows(self):
+        """Image rows [a, b) of this rank's RGB output."""
+        return 2 * self.c0, 2 * self.c1
+
+    def decode(self, sym_len, sym_val, counts, dc, stitch, stream=None):
+        """sym_len / sym_val / dc: {channel: device tensor} this rank's slices (as its
+        ShardEncoder wrote them); counts: host ints per channel; stitch: (3, 4) int64
+        device tensor, the encode's hic_rle_stitch records.  Runs on `stream` (made
+        current for the halo exchange)."""
+        if stream is not None:
+            with torch.cuda.stream(stream):
+                return self._decode(sym_len, sym_val, counts, dc, stitch, stream)
+        return self._decode(sym_len, sym_val, counts, dc, stitch, None)
+
+    def _decode(self, sym_len, sym_val, counts, dc, stitch, stream):
+        self.planes(sym_len, sym_val, counts, dc, stitch, stream)
+        self.halo()
+        return self.colour(stream)
+
+    def halo_views(self):
+        """[(buf, top, n_own)] of the two chroma planes (exchange_halo_rows' layout)."""
+        return [(self.cbuf[k], self.top, self.c1 - self.c0) for k in ("cr", "cb")]
+
+    def halo(self):
+        """The exchange step: one chroma row to / from each neighbour (current stream)."""
+        exchange_halo_rows(self.halo_views(), self.rank, self.world, self.group)
+
+    def planes(self, sym_len, sym_val, counts, dc, stitch, stream=None):
+        """Stream slices -> blocks -> this rank's Y rows and chroma rows."""
+        s = device.stream_ptr(stream)
+        lib = _lib.load()
+        nc = self.c1 - self.c0
+        for i, k in enumerate(CHANNELS):
+            h, w = self.shapes[k]
+            n = self.blocks[k].shape[0]
+            nsym = int(counts[i])
+            pipeline.check_count(nsym, k)
+            need = lib.hic_rld_workspace_bytes(nsym, n)
+            if k not in self._ws or self._ws[k].numel() * 8 < need:
+                self._ws[k] = device.workspace(need)
+            _lib.call("hic_rle_decode_i16_shard", device.ptr(sym_len[k]), device.ptr(sym_val[k]), nsym,
+                      device.ptr(dc[k]), n, device.ptr(stitch[i]), device.ptr(self.blocks[k]),
+                      device.ptr(self.status[i:i + 1]), device.ptr(self._ws[k]), s)
+            out = self.y if k == "lum" else self.cbuf[k][self.top:self.top + nc]
+            _lib.call("hic_dequant_idct_u8", device.ptr(self.blocks[k]), _lib.LAYOUT_ZIGZAG_I16, h, w,
+                      pipeline.TABLES[k], device.ptr(out), out.stride(0), s)
+
+    def colour(self, stream=None):
+        """pyrUp (with the halo rows) + YCrCb -> RGB of this rank's rows."""
+        s = device.stream_ptr(stream)
+        cr, cb = self.cbuf["cr"], self.cbuf["cb"]
+        _lib.call("hic_ycrcb420_to_rgb_rows", device.ptr(self.y), self.y.stride(0), device.ptr(cr), device.ptr(cb),
+                  self.c0 - self.top, cr.shape[0], self.h, self.w, self.c0, self.c1, device.ptr(self.rgb), s)
+        return self.rgb
+
+    def check_status(self):
+        """Raise unless every channel's slice decoded to exactly its blocks (syncs)."""
+        st = self.status.cpu().tolist()
+        for i, k in enumerate(CHANNELS):
+            want = self.blocks[k].shape[0] * 63
+            if st[i] != want:
+                raise ValueError("rank %d channel %s: stream slice covers %d AC positions, expected %d"
+                                 % (self.rank, k, st[i], want))
+
+
 def _send(t, dst, group):
     if t.is_cuda and dist.get_backend(group) == "gloo":
         t = t.cpu()

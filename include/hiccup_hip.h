@@ -167,6 +167,15 @@ int hic_pyr_up_u8(const uint8_t *src, int64_t H, int64_t W, uint8_t *dst, int64_
  * transform.py:269-277), cvtColor(YCrCb2RGB) -> rgb (2h) x (2w) x 3. */
 int hic_ycrcb420_to_rgb(const uint8_t *y, int64_t y_stride, const uint8_t *cr, const uint8_t *cb,
                         int64_t h, int64_t w, uint8_t *rgb, void *stream);
+/* Row-range form of hic_ycrcb420_to_rgb for a tile shard's decode
+ * (compression.jpeg_decompression on rows of the image, compression.py:42-56):
+ * chroma rows [s0, s1) of the h x w chroma planes -> RGB rows [2 s0, 2 s1).
+ * y and rgb point at output row 2 s0; cr / cb hold c_rows chroma rows starting at
+ * image chroma row c_row0, which must cover the pyrUp halo [max(0, s0 - 1),
+ * min(h, s1 + 1)). */
+int hic_ycrcb420_to_rgb_rows(const uint8_t *y, int64_t y_stride, const uint8_t *cr, const uint8_t *cb,
+                             int64_t c_row0, int64_t c_rows, int64_t h, int64_t w, int64_t s0,
+                             int64_t s1, uint8_t *rgb, void *stream);
 
 /* ---- generic block split + zig-zag for any block size N (codec.jpeg_encode with
  *      settings.JPEG_BLOCK_SIZE != 8, codec.py:287-294; transform.zigzag):
@@ -249,6 +258,16 @@ size_t hic_rld_workspace_bytes(int64_t nsym, int64_t nblk);
 int hic_rle_decode_i16(const uint8_t *sym_len, const int16_t *sym_val, int64_t nsym,
                        const int32_t *dc_diff, int64_t nblk, int block_len, int16_t *blocks,
                        int64_t *d_status, void *workspace, void *stream);
+/* One tile shard's slice of the channel stream (the sharded decode of
+ * codec.jpeg_decode, codec.py:397-425): d_stitch is the shard's device record from
+ * hic_rle_stitch {carry zeros, closes the stream, has previous DC, previous DC}.
+ * The slice's first symbol continues a zero run that started `carry` positions
+ * before the shard's first block; the DC chain starts at the previous DC; a shard
+ * that does not close the stream ends in zeros.  *d_status = nblk * 63 for a
+ * consistent slice.  Hot-path form only (64-slot int16 blocks, 16-byte aligned). */
+int hic_rle_decode_i16_shard(const uint8_t *sym_len, const int16_t *sym_val, int64_t nsym,
+                             const int32_t *dc_diff, int64_t nblk, const int64_t *d_stitch,
+                             int16_t *blocks, int64_t *d_status, void *workspace, void *stream);
 int hic_rle_decode_i32(const int32_t *sym_len, const int32_t *sym_val, int64_t nsym,
                        const int32_t *dc_diff, int64_t nblk, int block_len, int32_t *blocks,
                        int64_t *d_status, void *workspace, void *stream);

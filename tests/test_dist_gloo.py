@@ -4,7 +4,10 @@ streams, all-gathers its channel summaries with sharding.exchange, derives its
 stitch record with sharding.stitch_host, run-length codes its slice, and rank 0
 reassembles (a) the coefficient blocks + DC stream with sharding.gather_blocks --
 the same grouped batch_isend_irecv code the RCCL path runs -- and (b) the symbol
-streams with point-to-point sends.  Both must equal the single-stream encode.  (Per-shard compute here is the CPU oracle -- test
+streams with point-to-point sends.  Both must equal the single-stream encode.
+(c) Each rank then decodes its own slice (sharded decode: carried-zero skip, DC
+chain from the stitch record, pyrUp halo rows from sharding.exchange_halo_rows)
+and its RGB rows must equal the whole-image decode's.  (Per-shard compute here is the CPU oracle -- test
 infrastructure; the GPU kernels for the same steps are covered by
 tests/test_gpu_codec.py::test_shards_stitch_to_single_stream.)"""
 import os
@@ -28,11 +31,13 @@ def _free_port():
     return p
 
 
-def _image(H, W):
+def _image(H, W, flat=None):
     rng = np.random.default_rng(42)
     rgb = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
     rgb[H // 3: H // 3 + 40] = 128  # zero runs crossing shard boundaries
     rgb[:, : W // 4] = 200
+    if flat:  # a whole shard with no nonzero luma AC: the carried run chains through it
+        rgb[flat[0]:flat[1]] = 128
     return rgb
 
 
@@ -63,12 +68,12 @@ def _rle_stitched(zz, st):
     return diff, L, V
 
 
-def _worker(rank, world, port, H, W, results):
+def _worker(rank, world, port, H, W, flat, results):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        zz = _zz_planes(_image(H, W))
+        zz = _zz_planes(_image(H, W, flat))
         r0, r1 = sharding.plan(H, world)[rank]
         ranges = sharding.block_ranges(H, W, world)
         mine = {}
@@ -103,6 +108,38 @@ def _worker(rank, world, port, H, W, results):
                 results["blocks_" + k] = bool(
                     np.array_equal(full[k][0].numpy(), zz[k].astype(np.int16))
                     and np.array_equal(full[k][1].numpy(), orc.dpcm(zz[k][:, 0].astype(np.int64)).astype(np.int32)))
+        # (c) the sharded decode: this rank's stream slice -> blocks (carried zeros
+        # skipped, DC chain from the previous shard), inverse DCT of its block rows,
+        # pyrUp halo rows from the neighbours (sharding.exchange_halo_rows, the code
+        # the RCCL path runs), colour of its rows == the whole-image decode's rows
+        h, w = H // 2, W // 2
+        c0, c1 = r0 // 2, min(h, r1 // 2)
+        top, bot = int(c0 > 0), int(c1 < h)
+        planes = {}
+        for c, k in enumerate(pipeline.CHANNELS):
+            st = sharding.stitch_host(allsum[:, c], rank)
+            diff, L, V = enc[k]
+            n = len(mine[k])
+            ac = orc.rle_decode_shard(L, V, int(st[0]), n * 63).reshape(n, 63)
+            dcs = np.cumsum(diff) + (int(st[3]) if st[2] else 0)
+            blocks = orc.izigzag_blocks(np.concatenate([dcs[:, None], ac], axis=1))
+            shape = (r1 - r0, W) if k == "lum" else (c1 - c0, w)
+            planes[k] = orc.inv_dct_channel(orc.merge_blocks(blocks, shape), 0 if k == "lum" else 1)
+        bufs = {}
+        for k in ("cr", "cb"):
+            b = torch.zeros((top + c1 - c0 + bot, w), dtype=torch.uint8)
+            b[top:top + c1 - c0] = torch.from_numpy(planes[k])
+            bufs[k] = b
+        sharding.exchange_halo_rows([(bufs[k], top, c1 - c0) for k in ("cr", "cb")], rank, world)
+        hl = bufs["cr"].shape[0]
+        yl = np.zeros((2 * hl, 2 * w), np.uint8)
+        yl[2 * top:2 * top + 2 * (c1 - c0)] = planes["lum"][:2 * (c1 - c0), :2 * w]
+        rgb_l = orc.ycrcb_to_rgb(yl, orc.pyr_up(bufs["cr"].numpy()), orc.pyr_up(bufs["cb"].numpy()))
+        mine_rgb = rgb_l[2 * top:2 * (top + c1 - c0)]
+        y_w, cr_w, cb_w = (orc.inv_dct_channel(orc.merge_blocks(orc.izigzag_blocks(zz[k]), sh), t) for k, sh, t in
+                           (("lum", (H, W), 0), ("cr", (h, w), 1), ("cb", (h, w), 1)))
+        whole = orc.ycrcb_to_rgb(y_w[:2 * h, :2 * w], orc.pyr_up(cr_w), orc.pyr_up(cb_w))
+        results["decode_%d" % rank] = bool(np.array_equal(mine_rgb, whole[2 * c0:2 * c1]))
         # reassemble on rank 0: sizes first, then point-to-point payloads
         sizes = torch.tensor([[len(enc[k][0]), len(enc[k][1])] for k in pipeline.CHANNELS], dtype=torch.int64)
         all_sizes = sharding.exchange(sizes, world).numpy()
@@ -133,11 +170,13 @@ def _worker(rank, world, port, H, W, results):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,H,W", [(2, 96, 80), (3, 130, 72), (4, 160, 48)])
-def test_sharded_exchange_gloo(world, H, W):
+@pytest.mark.parametrize("world,H,W,flat", [(2, 96, 80, None), (3, 130, 72, None), (4, 160, 48, None),
+                                            (3, 144, 64, (48, 96))])
+def test_sharded_exchange_gloo(world, H, W, flat):
     mgr = mp.Manager()
     results = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), H, W, results), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), H, W, flat, results), nprocs=world, join=True)
     exp = {k: True for k in pipeline.CHANNELS}
     exp.update({"blocks_" + k: True for k in pipeline.CHANNELS})
+    exp.update({"decode_%d" % r: True for r in range(world)})
     assert dict(results) == exp

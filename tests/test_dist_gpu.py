@@ -4,7 +4,9 @@ driver runs the real 8-GPU RCCL bench).  Each rank runs the HIP kernels on its
 row shard (ShardEncoder: colour with halo, fused DCT + RLE tile records,
 summaries, all-gather, device stitch, scan + emit), rank 0 reassembles the
 streams with gather_streams, and the result must equal the single-GPU encode of
-the whole image bit for bit."""
+the whole image bit for bit.  Each rank then decodes its own slice
+(ShardDecoder, halo rows over the process group) and its RGB rows must equal the
+single-GPU decode's."""
 import os
 import socket
 import tempfile
@@ -48,11 +50,22 @@ def _rank(rank, world, port, H, W, flat_rows, out_path):
     s = torch.cuda.Stream()
     se.encode(device.to_device(rgb[a:b]), stream=s)
     blocks = se.gather_coefficients(stream=s)
+    # the sharded decode of this rank's slice (halo rows exchanged with the neighbours)
+    sd = sharding.ShardDecoder(H, W, rank=rank, world=world)
     torch.cuda.synchronize()
+    mine = sd.decode(se.enc.sym_len, se.enc.sym_val, se.enc.counts.cpu().tolist(), se.enc.dc, se.stitch, stream=s)
+    torch.cuda.synchronize()
+    sd.check_status()
+    whole = pipeline.Encoder(H, W)
+    whole.encode(device.to_device(rgb))
+    wd = pipeline.Decoder(H, W)
+    exp = device.to_host(wd.decode(whole.sym_len, whole.sym_val, whole.counts.cpu().tolist(), whole.dc))
+    r0, r1 = sd.out_rows
+    dec_ok = np.array_equal(device.to_host(mine), exp[r0:r1])
+    oks = [None] * world
+    dist.all_gather_object(oks, bool(dec_ok))
     got = sharding.gather_streams(se)
     if rank == 0:
-        whole = pipeline.Encoder(H, W)
-        whole.encode(device.to_device(rgb))
         ref = whole.result()
         ok = True
         for k in pipeline.CHANNELS:
@@ -63,6 +76,7 @@ def _rank(rank, world, port, H, W, flat_rows, out_path):
             ok &= np.array_equal(blocks[k][1].cpu().numpy(), ref[k][1])
         offs, tot = se.offsets()
         ok &= [int(x) for x in tot] == [len(ref[k][2]) for k in pipeline.CHANNELS]
+        ok &= all(oks)
         with open(out_path, "w") as f:
             f.write("ok" if ok else "mismatch")
     dist.barrier()

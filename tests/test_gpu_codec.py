@@ -347,13 +347,20 @@ def test_16k_roundtrip_vs_oracle():
     assert 10 * np.log10(255.0 ** 2 / mse) > 10.0
 
 
-@pytest.mark.parametrize("H,W,world", [(4320, 7680, 8), (250, 330, 3), (96, 64, 2)])
-def test_shards_stitch_to_single_stream(H, W, world):
+@pytest.mark.parametrize("H,W,world,flat", [(4320, 7680, 8, None), (250, 330, 3, None), (96, 64, 2, None),
+                                            (144, 96, 3, (48, 96))])
+def test_shards_stitch_to_single_stream(H, W, world, flat):
     """Row shards (with pyrDown halos) + the stitch record reproduce the
-    single-GPU stream exactly (the multi-GPU path, simulated on one device)."""
+    single-GPU stream exactly, and each shard's decode of its own slice
+    (ShardDecoder: carried zeros skipped, DC chain from the stitch record, pyrUp
+    halo rows from the neighbours) reproduces its rows of the single-GPU decode
+    (the multi-GPU path, simulated on one device; flat = a shard with no nonzero
+    luma AC, so a carried run chains through it)."""
     rng = np.random.default_rng(W)
     rgb = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
     rgb[H // 3: H // 3 + 40] = 128  # zero runs that cross shard boundaries
+    if flat:
+        rgb[flat[0]:flat[1]] = 128
     whole = pipeline.Encoder(H, W)
     whole.encode(device.to_device(rgb))
     ref = whole.result()
@@ -365,6 +372,7 @@ def test_shards_stitch_to_single_stream(H, W, world):
         encs.append(e)
     summ = np.stack([e.shard_summaries().cpu().numpy() for e in encs])  # (world, 3, 4)
     allsum = device.to_device(summ)
+    stitches = []
     for r, e in enumerate(encs):
         st = device.zeros((3, 4), torch.int64)
         for c in range(3):
@@ -373,12 +381,33 @@ def test_shards_stitch_to_single_stream(H, W, world):
                       device.ptr(st[c]), device.stream_ptr())
             np.testing.assert_array_equal(st[c].cpu().numpy(), sharding.stitch_host(summ[:, c], r))
         e.entropy(stitch=st)
+        stitches.append(st)
     parts = [e.result() for e in encs]
     for k in pipeline.CHANNELS:
         zz = np.concatenate([p[k][0] for p in parts])
         np.testing.assert_array_equal(zz, ref[k][0], err_msg=k)
         for j in (1, 2, 3):
             np.testing.assert_array_equal(np.concatenate([p[k][j] for p in parts]), ref[k][j], err_msg=(k, j))
+    # sharded decode: every shard decodes its own slice; the halo rows are copied
+    # between the shards' buffers here (exchange_halo_rows does it over RCCL)
+    whole_dec = pipeline.Decoder(H, W)
+    exp = device.to_host(whole_dec.decode(whole.sym_len, whole.sym_val, whole.counts.cpu().tolist(), whole.dc))
+    decs = [sharding.ShardDecoder(H, W, rank=r, world=world) for r in range(world)]
+    for d, e, st in zip(decs, encs, stitches):
+        d.planes(e.sym_len, e.sym_val, e.counts.cpu().tolist(), e.dc, st)
+    for r, d in enumerate(decs):
+        for (buf, top, n), k in zip(d.halo_views(), ("cr", "cb")):
+            if r > 0:
+                pb, pt, pn = decs[r - 1].halo_views()[0 if k == "cr" else 1]
+                buf[0].copy_(pb[pt + pn - 1])
+            if r < world - 1:
+                nb, nt, _ = decs[r + 1].halo_views()[0 if k == "cr" else 1]
+                buf[top + n].copy_(nb[nt])
+    for r, d in enumerate(decs):
+        got = device.to_host(d.colour())
+        d.check_status()
+        a, b = d.out_rows
+        np.testing.assert_array_equal(got, exp[a:b], err_msg="rank %d" % r)
 
 
 def test_two_stream_overlap_matches_single_stream():

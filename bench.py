@@ -56,6 +56,10 @@ def parse():
                     help="rehearsal on a 1-GPU box: every rank on cuda:0 (use with --dist-backend gloo)")
     ap.add_argument("--streams", type=int, default=2,
                     help="HIP streams the consecutive images alternate over (each image's chain stays on one)")
+    ap.add_argument("--unfused", action="store_true",
+                    help="A/B: colour and DCT as two kernels (the planes round-trip HBM) instead of hic_encode420_u8")
+    ap.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
+                    help="A/B: set a library knob (hiccup_amd._lib.KNOBS; every knob is bit-exact)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=25.0)
     ap.add_argument("--no-extras", action="store_true",
@@ -307,18 +311,22 @@ def main():
         else:
             dist.init_process_group("gloo")
 
-    from hiccup_amd import device, pipeline, sharding
+    from hiccup_amd import _lib, device, pipeline, sharding
     device.require_gpu()
+    for kv in args.knob:
+        name, _, val = kv.partition("=")
+        _lib.set_knob(name, int(val))
 
     H0, W0 = (H8K, W8K) if args.workload == "8k" else (4096, 4096)
     strong = world > 1 and args.mode == "strong"
     gather = strong and not args.no_gather
     if world > 1:
         H = H0 * world if not strong else H0
-        make = lambda: sharding.ShardEncoder(H, W0, rank=rank, world=world, gather_to=0 if gather else None)  # noqa
+        make = lambda: sharding.ShardEncoder(H, W0, rank=rank, world=world, gather_to=0 if gather else None,  # noqa
+                                             fused=False if args.unfused else None)
     else:
         H = H0
-        make = lambda: pipeline.Encoder(H0, W0)  # noqa: E731
+        make = lambda: pipeline.Encoder(H0, W0, fused=False if args.unfused else None)  # noqa: E731
     encs = [make() for _ in range(4)]  # rotate outputs too (~1.2 GB)
     span = encs[0].span if world > 1 else (0, H)
     in_rows = span[1] - span[0]
@@ -330,6 +338,7 @@ def main():
     enc0 = encs[0].enc if world > 1 else encs[0]
     dct_px = sum(h * w for h, w in enc0.shapes.values())  # Y + Cr + Cb: one DCT launch
     px_per_step_rank = enc0.pixels
+    fused = enc0.fused
 
     timed_events = []
     event_pool = [device.KernelEvents() for _ in range((args.steps + 3) // 4)]
@@ -413,13 +422,17 @@ def main():
         roof_note = ("16 single-stream encodes (every 4th timestamped, after 8 untimed) right after the timed "
                      "region; the timed region overlaps images on %d stream(s)%s"
                      % (len(streams), " and gathers to rank 0" if gather else ""))
-    achieved = dct_px * 3 / (dct_us * 1e-6) / 1e9  # u8 in + int16 out per pixel
+    # algorithmic bytes of the timed launch: the two-kernel chain's DCT reads 1 B and
+    # writes 2 B per plane pixel; the fused kernel reads the RGB (3 B per image
+    # pixel) and writes the same coefficients
+    roof_bytes = dct_px * 2 + (px_per_step_rank * 3 if fused else dct_px)
+    achieved = roof_bytes / (dct_us * 1e-6) / 1e9
 
     per_rank_rows = in_rows if world == 1 else encs[0].rows[1] - encs[0].rows[0]
     extra_sharded = None
     if world > 1 and not args.no_extras:
         # free the 8K run's buffers first (every rank holds ~1.2 GB of inputs)
-        del encs, inputs
+        del encs, inputs, enc0
         torch.cuda.empty_cache()
         extra_sharded = extra_16k_roundtrip_sharded(rank, world, args.dist_backend)
 
@@ -465,16 +478,21 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_dct_planes<-1,ZIGZAG_I16,15> (Y + Cr + Cb of the rank's image/shard in one launch: "
-                          "AAN DCT + quantize + zig-zag + RLE tile records, per-plane table)",
+                "kernel": ("k_encode420<15> (RGB -> YCrCb + 4:2:0 pyrDown + AAN DCT + quantize + zig-zag + RLE "
+                           "tile records of the rank's image/shard in one launch; algorithmic bytes = 3 B RGB read + "
+                           "2 B int16 written per Y / Cr / Cb coefficient)" if fused else
+                           "k_dct_planes<-1,ZIGZAG_I16,15> (Y + Cr + Cb of the rank's image/shard in one launch: "
+                           "AAN DCT + quantize + zig-zag + RLE tile records, per-plane table; 1 B read + 2 B "
+                           "written per plane pixel)"),
                 "timed_launches": len(timed_events),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": pmc.get("hbm_bytes_per_launch") if (pmc and world == 1 and args.workload == "8k")
+                "traffic": pmc.get("hbm_bytes_per_launch") if (pmc and world == 1 and args.workload == "8k"
+                                                                and pmc.get("kernel_fused", False) == fused)
                 else None,
-                "algorithmic_bytes": dct_px * 3,
+                "algorithmic_bytes": roof_bytes,
                 "avg_launch_us": round(dct_us, 2),
                 "timed_over": roof_note,
                 "avg_launch_us_overlapped": None if dct_us_overlapped is None else round(dct_us_overlapped, 2),

@@ -1,0 +1,374 @@
+// encode.hip -- the fused 4:2:0 encoder front end for MI355X (gfx950): one pass
+// over the RGB image computes cvtColor(RGB2YCrCb), pyrDown of Cr / Cb, the 8x8
+// DCT + quantize + transposed zig-zag of all three planes and the planes' RLE
+// tile records.  The Y / Cr / Cb planes never exist in HBM.
+//
+// Reference: compression.jpeg_compression (compression.py:16-39) = cv2.cvtColor
+// (:21) + transform.down_sample (pyrDown, transform.py:151-157) + dct_channel x3
+// (transform.py:182-193), and the zig-zag / tile pass of codec.jpeg_encode
+// (codec.py:286-301, transform.py:106-148).  Bit-exact with the unfused chain
+// (color.hip + dct.hip): the same colour arithmetic (color_core.h, OpenCV 8U
+// restatement, PARITY UNPINNED), the same float64 AAN DCT with exact tie
+// handling (dct_core.h), the same tile records (rle_core.h).
+//
+// Work unit: a "strip" of 512 pixel columns x 16 image rows.  Lane l owns pixel
+// columns [8 l, 8 l + 8) of the strip, i.e. Y block column l of the strip's two
+// block rows (a 64-block RLE tile each, W % 512 == 0) and half of chroma block
+// column l / 2.  One wave per unit:
+//   1. colour: 19 RGB rows (the 16 rows + the 2 + 1 rows of pyrDown's vertical
+//      taps), 24 B per lane per row (1.5 KiB contiguous per wave-row); Y of rows
+//      0..15 stays in registers (two 8x8 blocks per lane); Cr / Cb per pixel, the
+//      horizontal [1 4 6 4 1] at even columns with the neighbour pixels by DPP
+//      wave shifts (the strip's edge pixels converted once per unit, one row per
+//      lane, and read back by v_readlane), the vertical taps over a 5-row window
+//      -> 8 chroma rows x 4 columns per lane and plane;
+//   2. DCT of Y block row 0 and row 1 (lane = block): coefficients to the LDS
+//      stage at their zig-zag slot, copied out in 1 KiB nontemporal stores, the
+//      tile record from the stage;
+//   3. chroma: the colour stage left the chroma rows in a 4 KiB LDS area per wave;
+//      chroma block m of Cr is read into lane m and of Cb into lane 32 + m (a
+//      block spans the columns of lanes 2m, 2m + 1), one DCT pass with the
+//      chrominance table, 4 KiB of Cr and 4 KiB of Cb blocks out, and two 32-block
+//      half-tile records (hic_rle_job16.records_per_tile = 2).
+// Exact-tie fallbacks (dct_block_2ph, dct_fix26) run in place on the pixels still
+// in registers: a unit never revisits HBM.
+// RGB traffic: 19/16 of the image (the vertical halo rows are re-read by the unit
+// above / below); coefficient writes 3 B per pixel.
+#include "color_core.h"
+#include "dct_core.h"
+#include "rle_core.h"
+
+namespace hic {
+namespace {
+
+struct Enc420 {
+  const uint8_t *rgb;  // image rows [in_row0, in_row0 + in_rows), W * 3 bytes each
+  int in_row0, in_rows, H, W, out_row0, out_rows;
+  int16_t *coef[3];  // ZIGZAG_I16 blocks of the shard's Y, Cr, Cb planes
+  int64_t *rec[3];   // tile records: Y per 64-block tile, Cr / Cb per 32-block half tile
+  int M;
+  int nstrips, nunits;
+};
+
+constexpr int kZZ = HIC_LAYOUT_ZIGZAG_I16;
+
+// Exact fallbacks, out of line (cold; by-value pixel rows keep them in VGPRs).
+template <int TABLE>
+__device__ __attribute__((noinline)) void enc_exact_block(uint2 w0, uint2 w1, uint2 w2, uint2 w3, uint2 w4, uint2 w5,
+                                                          uint2 w6, uint2 w7, int16_t *st) {
+  uint2 w[8] = {w0, w1, w2, w3, w4, w5, w6, w7};
+  dct_block_2ph<TABLE, kZZ>(w, st);
+}
+template <int TABLE>
+__device__ __attribute__((noinline)) void enc_fix26_block(uint2 w0, uint2 w1, uint2 w2, uint2 w3, uint2 w4, uint2 w5,
+                                                          uint2 w6, uint2 w7, int16_t *st) {
+  const uint2 w[8] = {w0, w1, w2, w3, w4, w5, w6, w7};
+  int q[4];
+  dct_fix26<TABLE>(w, q);
+  constexpr SlotOf<kZZ> kSlot{};
+  st[kSlot.s[18]] = (int16_t)q[0];
+  st[kSlot.s[22]] = (int16_t)q[1];
+  st[kSlot.s[50]] = (int16_t)q[2];
+  st[kSlot.s[54]] = (int16_t)q[3];
+}
+
+// One block per lane -> quantized zig-zag coefficients in this lane's stage row,
+// exact in every case (fast AAN path; the rare tie sets fall back in place).
+template <int TABLE>
+__device__ __forceinline__ void enc_dct(uint2 (&w)[8], int16_t *st) {
+#if defined(HIC_DEV) && defined(HIC_ENC_DEV) && (HIC_ENC_DEV & 1)
+  // dev timing (results invalid): no DCT, the pixels go to the stage
+#pragma unroll
+  for (int r = 0; r < 8; ++r) reinterpret_cast<uint2 *>(st)[r] = w[r];
+  return;
+#endif
+  bool t26 = false;
+  const bool f = dct_block_aan<TABLE, kZZ>(w, st, &t26);
+  if (__builtin_amdgcn_ballot_w64(f)) {
+    enc_exact_block<TABLE>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], st);
+  } else if (__builtin_amdgcn_ballot_w64(t26)) {
+    enc_fix26_block<TABLE>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], st);
+  }
+}
+
+// 16 B chunk k of stage row b
+__device__ __forceinline__ uint4 enc_st16(const uint2 *st2, int b, int k) {
+  const uint2 lo = st2[b * kStageU2 + 2 * k], hi = st2[b * kStageU2 + 2 * k + 1];
+  return make_uint4(lo.x, lo.y, hi.x, hi.y);
+}
+
+// stage rows 0..31 -> o_lo (32 blocks), rows 32..63 -> o_hi: 1 KiB per store
+// instruction, nontemporal (the coefficients are not re-read by this kernel)
+__device__ __forceinline__ void enc_store(const uint2 *st2, int lane, int16_t *o_lo, int16_t *o_hi) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint4 t = enc_st16(st2, 8 * k + (lane >> 3), lane & 7);
+    const u32x4 v = {t.x, t.y, t.z, t.w};
+    u32x4 *o = reinterpret_cast<u32x4 *>(k < 4 ? o_lo : o_hi) + 64 * (k & 3) + lane;
+    __builtin_nontemporal_store(v, o);
+  }
+}
+
+__device__ __forceinline__ void enc_stage_row(const uint2 *st2, int lane, uint32_t (&zw)[32]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint4 t = enc_st16(st2, lane, k);
+    zw[4 * k] = t.x; zw[4 * k + 1] = t.y; zw[4 * k + 2] = t.z; zw[4 * k + 3] = t.w;
+  }
+}
+
+// Packed 16-bit helpers: both chroma planes in one dword (Cr low half, Cb high
+// half); pyrDown's sums stay below 2^16 (horizontal <= 16 * 255, vertical + 128 <=
+// 65408), so v_pk_*_u16 does both planes at once.
+__device__ __forceinline__ uint32_t pk_add16(uint32_t a, uint32_t b) {
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  const u16x2 r = __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b);
+  return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ uint32_t pk_mad16(uint32_t a, unsigned short k, uint32_t c) {  // a * k + c per half
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  const u16x2 r = __builtin_bit_cast(u16x2, a) * (u16x2){k, k} + __builtin_bit_cast(u16x2, c);
+  return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ uint32_t pk_shr8(uint32_t a) {
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  const u16x2 r = __builtin_bit_cast(u16x2, a) >> (u16x2){8, 8};
+  return __builtin_bit_cast(uint32_t, r);
+}
+// [1 4 6 4 1] over five packed taps
+__device__ __forceinline__ uint32_t pk_taps5(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e) {
+  return pk_mad16(c, 6, pk_mad16(pk_add16(b, d), 4, pk_add16(a, e)));
+}
+
+// Colour stage of one unit (image rows y0 .. y0 + 15 of strip s): Y rows -> yq,
+// pyrDown'd chroma rows (4 columns per lane, packed bytes) -> the wave's LDS chroma
+// area s_chroma[plane][row][lane] (so chroma block m's row i is the 8 bytes at
+// s_chroma[plane][i][2m]).
+__device__ __forceinline__ void enc_colour(const Enc420 &E, int y0, int s, int lane, uint2 (&yq)[16],
+                                           uint32_t *s_chroma) {
+  const int W = E.W, H = E.H;
+  const int in_row1 = E.in_row0 + E.in_rows;
+  const int xs = 512 * s, x0 = xs + 8 * lane;
+  auto src_row = [&](int rr) {  // rr: row relative to y0 (-2 .. 16)
+    int sy = refl101(y0 + rr, H);
+    sy = sy < E.in_row0 ? E.in_row0 : (sy >= in_row1 ? in_row1 - 1 : sy);
+    return E.rgb + (int64_t)(sy - E.in_row0) * W * 3;
+  };
+  // the strip's edge pixels, packed (cr | cb << 16): lane r converts row r - 2's
+  // x = xs - 2, xs - 1 (left neighbour strip) and x = xs + 512 (right one)
+  uint32_t hal_l2 = 0, hal_l1 = 0, hal_r = 0;
+  if (lane < 19) {
+    const uint8_t *row = src_row(lane - 2);
+    if (xs >= 2) {
+      const uint8_t *p = row + 3 * (xs - 2);
+      const YCC a = rgb2ycc(p[0], p[1], p[2]), b = rgb2ycc(p[3], p[4], p[5]);
+      hal_l2 = a.cr | a.cb << 16;
+      hal_l1 = b.cr | b.cb << 16;
+    }
+    if (xs + 512 < W) {
+      const uint8_t *p = row + 3 * (xs + 512);
+      const YCC c = rgb2ycc(p[0], p[1], p[2]);
+      hal_r = c.cr | c.cb << 16;
+    }
+  }
+  const bool left_border = s == 0, right_border = xs + 512 >= W;
+  uint32_t h[19][4];  // horizontal pyrDown sums of input row r, chroma column j (packed)
+  // rows stream through a ring of kLA + 1 loads in flight (sched_barrier keeps the
+  // compiler from hoisting all 19 rows' loads: 114 VGPRs)
+#ifndef HIC_ENC_LA
+#define HIC_ENC_LA 6
+#endif
+  constexpr int kLA = HIC_ENC_LA;
+  uint2 ring[kLA + 1][3];
+  auto load_row = [&](int r, uint2 (&d)[3]) {
+    const uint2 *p = reinterpret_cast<const uint2 *>(src_row(r - 2) + 3 * x0);
+    d[0] = p[0];
+    d[1] = p[1];
+    d[2] = p[2];
+  };
+#pragma unroll
+  for (int r = 0; r < kLA; ++r) load_row(r, ring[r]);
+#pragma unroll
+  for (int r = 0; r < 19; ++r) {
+    if (r + kLA < 19) load_row(r + kLA, ring[(r + kLA) % (kLA + 1)]);
+    const uint2 q0 = ring[r % (kLA + 1)][0], q1 = ring[r % (kLA + 1)][1], q2 = ring[r % (kLA + 1)][2];
+    const uint32_t wd[6] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y};
+    auto byte = [&](int i) { return (int)((wd[i >> 2] >> (8 * (i & 3))) & 255u); };
+    uint32_t c[8], y[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const YCC v = rgb2ycc(byte(3 * k), byte(3 * k + 1), byte(3 * k + 2));
+      y[k] = v.y;
+      c[k] = v.cr | v.cb << 16;
+    }
+    if (r >= 2 && r < 18) yq[r - 2] = make_uint2(pack4(y[0], y[1], y[2], y[3]), pack4(y[4], y[5], y[6], y[7]));
+    // neighbour pixels x0 - 2, x0 - 1 (left lane) and x0 + 8 (right lane)
+    uint32_t l2 = shr1(c[6]), l1 = shr1(c[7]), r0 = shl1(c[0]);
+    if (lane == 0) {  // reflect-101 at the image's left border: x = -2, -1 -> 2, 1
+      l2 = left_border ? c[2] : (uint32_t)__builtin_amdgcn_readlane((int)hal_l2, r);
+      l1 = left_border ? c[1] : (uint32_t)__builtin_amdgcn_readlane((int)hal_l1, r);
+    }
+    if (lane == 63)  // right border: x = W -> W - 2
+      r0 = right_border ? c[6] : (uint32_t)__builtin_amdgcn_readlane((int)hal_r, r);
+    h[r][0] = pk_taps5(l2, l1, c[0], c[1], c[2]);
+    h[r][1] = pk_taps5(c[0], c[1], c[2], c[3], c[4]);
+    h[r][2] = pk_taps5(c[2], c[3], c[4], c[5], c[6]);
+    h[r][3] = pk_taps5(c[4], c[5], c[6], c[7], r0);
+    if (r >= 4 && r % 2 == 0) {  // chroma row i = r / 2 - 2 has all five input rows
+      const int a = r - 4, i = r / 2 - 2;
+      uint32_t v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)  // (sum + 128) >> 8 <= 255: no saturation needed
+        v[j] = pk_shr8(pk_add16(pk_taps5(h[a][j], h[a + 1][j], h[a + 2][j], h[a + 3][j], h[a + 4][j]),
+                                0x00800080u));
+      // bytes: x01 = (cr0, cr1, cb0, cb1), x23 = (cr2, cr3, cb2, cb3)
+      const uint32_t x01 = __builtin_amdgcn_perm(v[1], v[0], 0x06020400u);
+      const uint32_t x23 = __builtin_amdgcn_perm(v[3], v[2], 0x06020400u);
+      s_chroma[i * 64 + lane] = __builtin_amdgcn_perm(x23, x01, 0x05040100u);
+      s_chroma[512 + i * 64 + lane] = __builtin_amdgcn_perm(x23, x01, 0x07060302u);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int TMF>
+__device__ __forceinline__ void encode420_unit(const Enc420 &E);
+
+// Two register budgets (knob "encode_waves", A/B): 2 waves per SIMD (default: up
+// to 256 VGPRs, no spills; 63.7 us per 8K launch) or 3 (<= 168 VGPRs: the Y passes
+// spill ~80 dwords per unit; 76 us)
+template <int TMF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_encode420(Enc420 E) {
+  encode420_unit<TMF>(E);
+}
+template <int TMF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_encode420_w2(Enc420 E) {
+  encode420_unit<TMF>(E);
+}
+
+template <int TMF>
+__device__ __forceinline__ void encode420_unit(const Enc420 &E) {
+  __shared__ uint2 s_stage[4 * 64 * kStageU2];
+  __shared__ uint32_t s_chroma_all[4][2 * 8 * 64];
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wv);
+  if (g >= E.nunits) return;  // wave-uniform
+  uint2 *st2 = s_stage + wv * 64 * kStageU2;
+  uint32_t *s_chroma = s_chroma_all[wv];
+  int16_t *st = reinterpret_cast<int16_t *>(st2 + lane * kStageU2);
+  const int u = g / E.nstrips, s = g - u * E.nstrips;
+  const int y0 = E.out_row0 + 16 * u;
+  const int nbx = E.W >> 3, nbxc = E.W >> 4;
+
+  uint2 yq[16];
+#if defined(HIC_DEV) && defined(HIC_ENC_DEV) && (HIC_ENC_DEV & 2)
+  // dev timing (results invalid): no colour stage, synthetic pixels
+#pragma unroll
+  for (int r = 0; r < 16; ++r) yq[r] = make_uint2(0x9E3779B1u * (lane + r + g), 0x85EBCA6Bu * (lane ^ r ^ g));
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s_chroma[i * 64 + lane] = 0x01000193u * (lane + i + g);
+#else
+  enc_colour(E, y0, s, lane, yq, s_chroma);
+#endif
+
+  // ---- Y: block rows 2u and 2u + 1, blocks 64 s .. 64 s + 63 (one RLE tile each)
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int br = 0; br < 2; ++br) {
+    uint2 w[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) w[r] = yq[8 * br + r];
+    enc_dct<0>(w, st);
+    __builtin_amdgcn_wave_barrier();
+    const int64_t b0 = (int64_t)(2 * u + br) * nbx + 64 * s;
+    int16_t *o = E.coef[0] + b0 * 64;
+    enc_store(st2, lane, o, o + 32 * 64);
+    if (TMF >= 0 && E.rec[0]) {
+      uint32_t zw[32];
+      enc_stage_row(st2, lane, zw);
+      tile_record16<TMF>(zw, true, b0 + lane, E.M, E.rec[0] + (b0 >> 6) * 3);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  // ---- chroma: block m of Cr -> lane m, of Cb -> lane 32 + m (block m spans the
+  // chroma columns of lanes 2m and 2m + 1 of this strip), read from the LDS area
+  {
+    __builtin_amdgcn_wave_barrier();
+    const uint2 *sc = reinterpret_cast<const uint2 *>(s_chroma + (lane >> 5) * 512) + (lane & 31);
+    uint2 w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = sc[i * 32];
+    enc_dct<1>(w, st);
+    __builtin_amdgcn_wave_barrier();
+    const int64_t b0 = (int64_t)u * nbxc + 32 * s;
+    enc_store(st2, lane, E.coef[1] + b0 * 64, E.coef[2] + b0 * 64);
+    if (TMF >= 0 && E.rec[1]) {
+      uint32_t zw[32];
+      enc_stage_row(st2, lane, zw);
+      tile_record16_half<TMF>(zw, b0, E.M, E.rec[1] + (b0 >> 5) * 3, E.rec[2] + (b0 >> 5) * 3);
+    }
+  }
+}
+
+}  // namespace
+}  // namespace hic
+
+using namespace hic;
+
+extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, int64_t H, int64_t W,
+                                int64_t out_row0, int64_t out_rows, int16_t *coef_y, int16_t *coef_cr,
+                                int16_t *coef_cb, void *ws_y, void *ws_cr, void *ws_cb, int max_len, void *stream,
+                                void *ev_start, void *ev_stop) {
+  if (!rgb_rows || !coef_y || !coef_cr || !coef_cb) return arg_error("null pointer");
+  if (H < 16 || W < 512 || H >= (1 << 20) || W >= (1 << 20)) return arg_error("image shape");
+  if (W % 512 || H % 16) return arg_error("hic_encode420_u8 needs W %% 512 == 0 and H %% 16 == 0");
+  if (out_row0 < 0 || out_rows < 16 || out_row0 % 16 || out_rows % 16 || out_row0 + out_rows > H)
+    return arg_error("output row range (multiples of 16)");
+  const int64_t need0 = out_row0 >= 2 ? out_row0 - 2 : 0;
+  const int64_t need1 = out_row0 + out_rows + 1 < H ? out_row0 + out_rows + 1 : H;
+  if (in_row0 > need0 || in_row0 + in_rows < need1) return arg_error("input rows do not cover the pyrDown halo");
+  if (reinterpret_cast<uintptr_t>(rgb_rows) % 8) return arg_error("rgb must be 8-byte aligned");
+  if ((reinterpret_cast<uintptr_t>(coef_y) | reinterpret_cast<uintptr_t>(coef_cr) |
+       reinterpret_cast<uintptr_t>(coef_cb)) % 16)
+    return arg_error("coefficient buffers must be 16-byte aligned");
+  const bool recs = ws_y && ws_cr && ws_cb;
+  if ((ws_y || ws_cr || ws_cb) && !recs) return arg_error("workspaces: all three or none");
+  if (recs && (max_len < 0 || max_len > 256)) return arg_error("max_len");
+  Enc420 E{};
+  E.rgb = rgb_rows;
+  E.in_row0 = (int)in_row0;
+  E.in_rows = (int)in_rows;
+  E.H = (int)H;
+  E.W = (int)W;
+  E.out_row0 = (int)out_row0;
+  E.out_rows = (int)out_rows;
+  E.coef[0] = coef_y;
+  E.coef[1] = coef_cr;
+  E.coef[2] = coef_cb;
+  E.rec[0] = static_cast<int64_t *>(ws_y);
+  E.rec[1] = static_cast<int64_t *>(ws_cr);
+  E.rec[2] = static_cast<int64_t *>(ws_cb);
+  E.M = max_len;
+  E.nstrips = (int)(W / 512);
+  E.nunits = E.nstrips * (int)(out_rows / 16);
+  // one wave per unit (no persistent loop: units are the same size, and the
+  // hardware's dispatch balances the tail better than a fixed split)
+  const dim3 grid((unsigned)((E.nunits + 3) / 4)), block(256);
+  hipStream_t s = as_stream(stream);
+  hipEvent_t e0 = static_cast<hipEvent_t>(ev_start), e1 = static_cast<hipEvent_t>(ev_stop);
+  auto launch = [&](auto kern) {
+    if (e0 || e1)
+      hipExtLaunchKernelGGL(kern, grid, block, 0, s, e0, e1, 0, E);
+    else
+      hipLaunchKernelGGL(kern, grid, block, 0, s, E);
+  };
+  const bool w2 = knob(HIC_KNOB_ENCODE_WAVES) == 2;
+  if (max_len == 15)
+    w2 ? launch(k_encode420_w2<15>) : launch(k_encode420<15>);
+  else
+    w2 ? launch(k_encode420_w2<0>) : launch(k_encode420<0>);
+  return check_launch("k_encode420");
+}

@@ -586,9 +586,11 @@ struct RleJob16 {
   int16_t *sym_val;
   int64_t cap;
   int64_t *d_count;
-  int64_t *ws;     // tile records [3 * ntiles] then offsets [2 * ntiles]
+  int64_t *ws;     // tile records [3 * nrec] then offsets [2 * nrec]
   int64_t ntiles;
   int64_t tile0;   // first global tile index of this job
+  int64_t nrec;    // records: one per 64-block tile, or one per 32-block half tile (rshift 1)
+  int rshift;      // log2(records per 64-block tile)
 };
 struct RleJobs16 {
   RleJob16 j[kMaxJobs];
@@ -623,14 +625,14 @@ __global__ __launch_bounds__(kScanT) void k_rle_scan16b(RleJobs16 jobs, uint32_t
   // workgroup -> (job, partition)
   int jb = 0;
   int64_t p = blockIdx.x;
-  while (jb + 1 < jobs.n && p >= (jobs.j[jb].ntiles + kScanT - 1) / kScanT) {
-    p -= (jobs.j[jb].ntiles + kScanT - 1) / kScanT;
+  while (jb + 1 < jobs.n && p >= (jobs.j[jb].nrec + kScanT - 1) / kScanT) {
+    p -= (jobs.j[jb].nrec + kScanT - 1) / kScanT;
     ++jb;
   }
   const RleJob16 &J = jobs.j[jb];
   const int M = jobs.M;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t nt = J.ntiles, np = (nt + kScanT - 1) / kScanT;
+  const int64_t nt = J.nrec, np = (nt + kScanT - 1) / kScanT;
   const int64_t *tiles = J.ws;
   int64_t *offs = J.ws + 3 * nt;
   uint64_t *gran = reinterpret_cast<uint64_t *>(J.ws + 5 * nt);  // 3 per partition
@@ -746,9 +748,10 @@ __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
 #pragma unroll
       for (int k = 0; k < 32; ++k) n.w[k] = 0;
     }
-    const int64_t *offs = J.ws + 3 * J.ntiles;
-    n.off = offs[t * 2 + 0];
-    n.prev = offs[t * 2 + 1];
+    // the tile's first record (a 64-block tile may carry two 32-block records)
+    const int64_t *offs = J.ws + 3 * J.nrec;
+    n.off = offs[(t << J.rshift) * 2 + 0];
+    n.prev = offs[(t << J.rshift) * 2 + 1];
     n.pdc = (lane == 0 && b > 0 && b <= J.nblk) ? (int)J.blocks[(b - 1) * 64] : 0;
   };
   Next cur;
@@ -1213,6 +1216,7 @@ int encode_batch16(RleJobs16 &jobs, hipStream_t s) {
     // stream positions and counts travel as int32 through the scan's hand-off
     if (jobs.j[k].nblk > (int64_t)INT32_MAX / 63) return arg_error("nblk too large (AC stream >= 2^31)");
     jobs.j[k].ntiles = ntiles16(jobs.j[k].nblk);
+    jobs.j[k].nrec = (jobs.j[k].nblk * (1 << jobs.j[k].rshift) + kWT - 1) / kWT;
     jobs.j[k].tile0 = t0;
     t0 += jobs.j[k].ntiles;
   }
@@ -1220,7 +1224,7 @@ int encode_batch16(RleJobs16 &jobs, hipStream_t s) {
   static std::atomic<uint32_t> epoch{0};
   const uint32_t ep = (epoch.fetch_add(1) % ((1u << 30) - 1)) + 1;  // never 0 (zeroed workspace)
   int64_t nparts = 0;
-  for (int k = 0; k < jobs.n; ++k) nparts += (jobs.j[k].ntiles + kScanT - 1) / kScanT;
+  for (int k = 0; k < jobs.n; ++k) nparts += (jobs.j[k].nrec + kScanT - 1) / kScanT;
   hipLaunchKernelGGL(k_rle_scan16b, dim3((unsigned)nparts), dim3(kScanT), 0, s, jobs, ep);
   if (int e = check_launch("k_rle_scan16b")) return e;
   // persistent: 3 workgroups (12 waves) per CU fit the 51 KB LDS stage and the registers
@@ -1245,7 +1249,8 @@ int encode_from_tiles16(const int16_t *blocks, int64_t nblk, int M, const int64_
   RleJobs16 jobs{};
   jobs.n = 1;
   jobs.M = M;
-  jobs.j[0] = RleJob16{blocks, nblk, stitch, dc_diff, sym_len, sym_val, cap, d_count, static_cast<int64_t *>(ws), 0, 0};
+  jobs.j[0] = RleJob16{blocks, nblk, stitch, dc_diff, sym_len, sym_val, cap, d_count, static_cast<int64_t *>(ws), 0, 0,
+                       0, 0};
   return encode_batch16(jobs, s);
 }
 
@@ -1342,8 +1347,10 @@ int rle_tile16_launch(const int16_t *blocks, int64_t nblk, int max_len, int64_t 
 using namespace hic;
 
 extern "C" size_t hic_rle_workspace_bytes(int64_t nblk, int block_len) {
-  (void)block_len;  // sized for the hot path's 64-block tiles (>= the generic 256-block tiles)
-  const int64_t n = nblk > 0 ? nblk : 1, nt = (n + kWT - 1) / kWT;
+  (void)block_len;
+  // sized for the hot path's 32-block half-tile records (hic_encode420_u8's chroma;
+  // >= its 64-block tiles and the generic 256-block tiles)
+  const int64_t n = nblk > 0 ? nblk : 1, nt = (n + kWT / 2 - 1) / (kWT / 2);
   // tile records (3), offsets (2) per tile; 3 hand-off granules per scan partition
   return (size_t)(5 * nt + 3 * ((nt + kScanT - 1) / kScanT) + 8) * sizeof(int64_t);
 }
@@ -1399,19 +1406,28 @@ extern "C" int hic_rle_encode_i16_tiles_batch(int n, const hic_rle_job16 *jobs, 
       return arg_error("job %d: null pointer", k);
     if (a.nblk <= 0) return arg_error("job %d: nblk", k);
     if (reinterpret_cast<uintptr_t>(a.blocks) & 15) return arg_error("job %d: blocks must be 16-byte aligned", k);
+    if (a.records_per_tile != 0 && a.records_per_tile != 1 && a.records_per_tile != 2)
+      return arg_error("job %d: records_per_tile must be 1 or 2", k);
     J.j[k] = RleJob16{a.blocks, a.nblk, a.d_stitch, a.dc_diff, a.sym_len, a.sym_val, a.sym_cap, a.d_count,
-                      static_cast<int64_t *>(a.workspace), 0, 0};
+                      static_cast<int64_t *>(a.workspace), 0, 0, 0, a.records_per_tile == 2 ? 1 : 0};
   }
   return encode_batch16(J, as_stream(stream));
 }
 
-extern "C" int hic_rle_shard_summary_tiles(const int16_t *blocks, int64_t nblk, void *workspace, int64_t *d_summary,
-                                           void *stream) {
+extern "C" int hic_rle_shard_summary_records(const int16_t *blocks, int64_t nblk, int records_per_tile,
+                                             void *workspace, int64_t *d_summary, void *stream) {
   if (!blocks || !workspace || !d_summary) return arg_error("null pointer");
   if (nblk <= 0) return arg_error("nblk");
+  if (records_per_tile != 1 && records_per_tile != 2) return arg_error("records_per_tile must be 1 or 2");
   hipLaunchKernelGGL((k_rle_summary<int16_t>), dim3(1), dim3(kTB), 0, as_stream(stream), blocks, nblk,
-                     block_geo(nblk, 64), static_cast<const int64_t *>(workspace), ntiles16(nblk), d_summary);
+                     block_geo(nblk, 64), static_cast<const int64_t *>(workspace),
+                     (nblk * records_per_tile + kWT - 1) / kWT, d_summary);
   return check_launch("k_rle_summary");
+}
+
+extern "C" int hic_rle_shard_summary_tiles(const int16_t *blocks, int64_t nblk, void *workspace, int64_t *d_summary,
+                                           void *stream) {
+  return hic_rle_shard_summary_records(blocks, nblk, 1, workspace, d_summary, stream);
 }
 
 extern "C" int hic_rle_encode_i32(const int32_t *blocks, int64_t nblk, int block_len, int max_len,

@@ -244,6 +244,55 @@ __device__ __forceinline__ void copy_out_wave(const T *s, int a, T *__restrict__
   for (int64_t ew = (i1 > w0 ? i1 : w0 + (w0 < i0 ? 1 : 0)) + lane; ew < w1; ew += 64) edge(ew);
 }
 
+// 32-lane segmented int32 inclusive scans (lanes 0-31 and 32-63 independent): the
+// wave scans without their last step (row_bcast:31 joins the two halves).
+__device__ __forceinline__ int seg32_incl_sum_i32(int v) {
+  v += dpp_i32<0x111>(0, v);
+  v += dpp_i32<0x112>(0, v);
+  v += dpp_i32<0x114>(0, v);
+  v += dpp_i32<0x118>(0, v);
+  v += dpp_i32<0x142, 0xA>(0, v);
+  return v;
+}
+__device__ __forceinline__ int seg32_incl_max_i32(int v) {
+  constexpr int I = -2147483647 - 1;
+  v = max(v, dpp_i32<0x111>(I, v));
+  v = max(v, dpp_i32<0x112>(I, v));
+  v = max(v, dpp_i32<0x114>(I, v));
+  v = max(v, dpp_i32<0x118>(I, v));
+  v = max(v, dpp_i32<0x142, 0xA>(I, v));
+  return v;
+}
+
+// Two half-tile records at once: lanes 0-31 hold blocks b0 .. b0 + 31 of one stream
+// (record -> rec_lo), lanes 32-63 the same block indices of another stream (->
+// rec_hi); each record covers 32 blocks (a 64-block tile's two halves combine as
+// the scan's agg_combine does).  Same fields as tile_record16.
+template <int MF>
+__device__ __forceinline__ void tile_record16_half(const uint32_t (&w)[32], int64_t b0, int M,
+                                                   int64_t *__restrict__ rec_lo, int64_t *__restrict__ rec_hi) {
+  const int lane = threadIdx.x & 63, sl = lane & 31;
+  int first = -1, last = -1, nsym = 0;
+  summarize16<MF>(w, M, first, last, nsym);
+  const int lastr = last >= 0 ? sl * 63 + last : -1;
+  const int incl = seg32_incl_max_i32(lastr);
+  int prev = wave_shr1_i32(-1, incl);
+  if (sl == 0) prev = -1;
+  int cnt = nsym;
+  if (first >= 0 && prev >= 0) cnt += syms_for_run(sl * 63 + first - prev - 1, M);
+  const int icnt = seg32_incl_sum_i32(cnt);
+  const int tot_lo = __builtin_amdgcn_readlane(icnt, 31), tot_hi = __builtin_amdgcn_readlane(icnt, 63);
+  const int all_lo = __builtin_amdgcn_readlane(incl, 31), all_hi = __builtin_amdgcn_readlane(incl, 63);
+  const int all_last = lane < 32 ? all_lo : all_hi, total = lane < 32 ? tot_lo : tot_hi;
+  int64_t *rec = lane < 32 ? rec_lo : rec_hi;
+  const int64_t base = b0 * 63;
+  if (all_last < 0 ? sl == 0 : (first >= 0 && prev < 0)) rec[0] = all_last < 0 ? -1 : base + sl * 63 + first;
+  if (sl == 0) {
+    rec[1] = all_last >= 0 ? base + all_last : -1;
+    rec[2] = total;
+  }
+}
+
 // Copy n elements from LDS (element e at s[a + e], s 16-byte aligned) to global
 // g[o0 + e] (g 16-byte aligned), where a == o0 mod (16 / sizeof(T)): one
 // ds_read_b128 + global_store_dwordx4 per 16-byte chunk, element stores for the

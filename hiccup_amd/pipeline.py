@@ -4,6 +4,10 @@
 half of codec.jpeg_encode (compression.py:16-39, codec.py:286-301) for one
 H x W x 3 uint8 image that already lives in HBM:
 
+  1+2. hic_encode420_u8       (W % 512 == 0, H % 16 == 0) colour + 4:2:0 pyrDown +
+                              8x8 DCT + quantize + zig-zag of the three planes + the
+                              RLE tile records in ONE launch; the planes never reach
+                              HBM.  Otherwise two launches:
   1. hic_rgb_to_ycrcb420      RGB -> Y (H x W) + pyrDown'd Cr, Cb (H/2 x W/2)
   2. hic_dct_quant_rle_u8_batch  8x8 DCT + quantize + zig-zag of the three planes in
                               one launch -> int16 blocks (ZIGZAG_I16), with the RLE
@@ -55,10 +59,13 @@ class Encoder:
     """rows=(r0, r1) makes this encoder one row-shard of an H x W image (r0 even;
     shards of one image split at multiples of 16 rows so chroma blocks align)."""
 
-    def __init__(self, H, W, max_len=15, rows=None, out=None):
+    def __init__(self, H, W, max_len=15, rows=None, out=None, fused=None):
         """out: optional {channel: (coef (n, 64) int16, dc (n,) int32)} device views the
         encoder writes into (a gathering rank points them at its slice of the whole
-        image's buffers, so its own shard needs no copy)."""
+        image's buffers, so its own shard needs no copy).
+        fused: colour + 4:2:0 + DCT in one kernel (hic_encode420_u8, the planes never
+        reach HBM); None = whenever the shape allows it (W % 512 == 0, H and the row
+        range multiples of 16), False = the two-kernel chain (colour, then DCT)."""
         if H < 2 or W < 2:
             raise ValueError("image must be at least 2 x 2")
         device.require_gpu()
@@ -67,14 +74,24 @@ class Encoder:
         if r0 % 2 or not (0 <= r0 < r1 <= H):
             raise ValueError("bad row range %r" % ((r0, r1),))
         self.rows = (r0, r1)
+        can_fuse = W % 512 == 0 and H % 16 == 0 and r0 % 16 == 0 and r1 % 16 == 0
+        if fused and not can_fuse:
+            raise ValueError("the fused encoder needs W % 512 == 0 and H, rows multiples of 16")
+        self.fused = can_fuse if fused is None else bool(fused)
         c0, c1 = r0 // 2, min(H // 2, r1 // 2)
         self.shapes = {"lum": (r1 - r0, W), "cr": (c1 - c0, W // 2), "cb": (c1 - c0, W // 2)}
         ys, cs = self.shapes["lum"], self.shapes["cr"]
         lib = _lib.load()
-        self.y = device.empty(ys, torch.uint8)
-        self.cr = device.empty(cs, torch.uint8)
-        self.cb = device.empty(cs, torch.uint8)
+        # the planes exist only on the two-kernel path
+        self.y = self.cr = self.cb = None
+        if not self.fused:
+            self.y = device.empty(ys, torch.uint8)
+            self.cr = device.empty(cs, torch.uint8)
+            self.cb = device.empty(cs, torch.uint8)
         self.planes = {"lum": self.y, "cr": self.cr, "cb": self.cb}
+        # tile records per 64-block tile: the fused kernel writes chroma records per
+        # 32-block half tile
+        self.rpt = {"lum": 1, "cr": 2 if self.fused else 1, "cb": 2 if self.fused else 1}
         self.coef, self.dc, self.sym_len, self.sym_val, self.ws = {}, {}, {}, {}, {}
         self.cap = {}
         self.counts = device.zeros((3,), torch.int64)
@@ -112,6 +129,14 @@ class Encoder:
         if in_row0 is None:
             in_row0 = 0 if self.rows == (0, self.H) else self.input_span()[0]
         r0, r1 = self.rows
+        ev = (dct_events.start, dct_events.stop) if dct_events is not None else (None, None)
+        if self.fused:
+            # colour + pyrDown + DCT/quantize/zig-zag of the three planes + RLE tile
+            # records in ONE launch (dct_events time it)
+            _lib.call("hic_encode420_u8", device.ptr(rgb), in_row0, rgb.shape[0], self.H, self.W, r0, r1 - r0,
+                      *[device.ptr(self.coef[k]) for k in CHANNELS], *[device.ptr(self.ws[k]) for k in CHANNELS],
+                      self.max_len, s, *ev)
+            return
         _lib.call("hic_rgb_to_ycrcb420_rows", device.ptr(rgb), in_row0, rgb.shape[0], self.H, self.W, r0, r1 - r0,
                   device.ptr(self.y), device.ptr(self.cr), device.ptr(self.cb), s)
         # DCT + quantize + zig-zag of the three planes in ONE launch (each plane with
@@ -123,7 +148,6 @@ class Encoder:
             p = self.planes[k]
             jobs[i] = _lib.DctPlaneJob(p.data_ptr(), h, w, p.stride(0), TABLES[k], self.coef[k].data_ptr(),
                                        self.ws[k].data_ptr())
-        ev = (dct_events.start, dct_events.stop) if dct_events is not None else (None, None)
         _lib.call("hic_dct_quant_rle_u8_batch", 3, jobs, self.max_len, s, *ev)
 
     def shard_summaries(self, stream=None):
@@ -131,7 +155,7 @@ class Encoder:
         s = device.stream_ptr(stream)
         for i, k in enumerate(CHANNELS):
             n = self.coef[k].shape[0]
-            _lib.call("hic_rle_shard_summary_tiles", device.ptr(self.coef[k]), n, device.ptr(self.ws[k]),
+            _lib.call("hic_rle_shard_summary_records", device.ptr(self.coef[k]), n, self.rpt[k], device.ptr(self.ws[k]),
                       device.ptr(self.summaries[i]), s)
         return self.summaries
 
@@ -145,7 +169,7 @@ class Encoder:
             jobs[i] = _lib.RleJob16(self.coef[k].data_ptr(), self.coef[k].shape[0],
                                     stitch[i].data_ptr() if stitch is not None else None, self.dc[k].data_ptr(),
                                     self.sym_len[k].data_ptr(), self.sym_val[k].data_ptr(), self.cap[k],
-                                    self.counts[i:i + 1].data_ptr(), self.ws[k].data_ptr())
+                                    self.counts[i:i + 1].data_ptr(), self.ws[k].data_ptr(), self.rpt[k])
         _lib.call("hic_rle_encode_i16_tiles_batch", 3, jobs, self.max_len, s)
 
     def encode(self, rgb, stream=None, dct_events=None):

@@ -106,7 +106,7 @@ class ShardEncoder:
     gather_to: the rank that reassembles the whole image's coefficient blocks and
     DC differences (gather_coefficients); None = no reassembly buffers."""
 
-    def __init__(self, H, W, rank=None, world=None, group=None, max_len=15, gather_to=None):
+    def __init__(self, H, W, rank=None, world=None, group=None, max_len=15, gather_to=None, fused=None):
         self.rank = dist.get_rank(group) if rank is None else rank
         self.world = dist.get_world_size(group) if world is None else world
         self.group = group
@@ -124,7 +124,7 @@ class ShardEncoder:
                 self.full_dc[k] = device.empty((n,), torch.int32)
                 b0, b1 = self.ranges[k][self.rank]
                 out[k] = (self.full_coef[k][b0:b1], self.full_dc[k][b0:b1])
-        self.enc = pipeline.Encoder(H, W, max_len=max_len, rows=self.rows, out=out)
+        self.enc = pipeline.Encoder(H, W, max_len=max_len, rows=self.rows, out=out, fused=fused)
         self.span = self.enc.input_span()
         self.all_summ = device.zeros((self.world, 3, 4), torch.int64)
         self.stitch = device.zeros((3, 4), torch.int64)

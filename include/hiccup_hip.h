@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define HIC_ABI_VERSION 1
+#define HIC_ABI_VERSION 2
 
 #define HIC_OK 0
 #define HIC_ERR_ARG (-1)      /* bad shape / pointer / enum: the reference asserts or raises */
@@ -73,7 +73,8 @@ int hic_device_count(int *h_n);
 #define HIC_KNOB_RLD_NT 6           /* 1: nontemporal block stores in the RLE decode */
 #define HIC_KNOB_RLD_GENERIC 7      /* 1: the generic (any block size) RLE decode */
 #define HIC_KNOB_DEV 8              /* dev builds only (-DHIC_DEV): timing bits that skip work; refused otherwise */
-#define HIC_KNOB_COUNT 9
+#define HIC_KNOB_ENCODE_WAVES 9     /* hic_encode420_u8: register budget for 2 (default) or 3 waves per SIMD */
+#define HIC_KNOB_COUNT 10
 int hic_set_knob(int knob, int value);
 int hic_get_knob(int knob, int *h_value);
 /* Synchronises `stream`; returns HIC_ERR_HIP if an earlier async launch failed. */
@@ -113,6 +114,25 @@ typedef struct {
 } hic_dct_plane_job;
 int hic_dct_quant_rle_u8_batch(int n, const hic_dct_plane_job *jobs, int max_len, void *stream, void *ev_start,
                                void *ev_stop);
+/* ---- fused 4:2:0 encode front end: replaces compression.jpeg_compression's
+ *      cvtColor(RGB2YCrCb) + pyrDown(Cr), pyrDown(Cb) + dct_channel x3
+ *      (compression.py:16-39, transform.py:151-157,182-193) and the zig-zag of
+ *      codec.jpeg_encode (codec.py:286-301), in ONE kernel: the planes never reach
+ *      HBM.  Output identical to hic_rgb_to_ycrcb420_rows + hic_dct_quant_rle_u8_batch.
+ *  rgb_rows: image rows [in_row0, in_row0 + in_rows) of an H x W x 3 uint8 image
+ *  (8-byte aligned), covering output rows [out_row0, out_row0 + out_rows) plus the
+ *  pyrDown halo (2 rows above, 1 below, clamped to the image).  W % 512 == 0,
+ *  H % 16 == 0, out_row0 / out_rows multiples of 16.
+ *  coef_*: ZIGZAG_I16 blocks of the output rows' Y ((out_rows/8) x (W/8) blocks) and
+ *  Cr / Cb ((out_rows/16) x (W/16)).  ws_* (all or none): RLE workspaces that
+ *  receive the tile records for hic_rle_encode_i16_tiles_batch -- Y one per
+ *  64-block tile (records_per_tile 1), Cr / Cb one per 32-block half tile
+ *  (records_per_tile 2); max_len as there.  ev_start / ev_stop (optional): events
+ *  carrying the launch's own begin / end timestamps. */
+int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, int64_t H, int64_t W,
+                     int64_t out_row0, int64_t out_rows, int16_t *coef_y, int16_t *coef_cr, int16_t *coef_cb,
+                     void *ws_y, void *ws_cr, void *ws_cb, int max_len, void *stream, void *ev_start,
+                     void *ev_stop);
 /* Timing events (hipEvent_t handles) for the *_timed entry points. */
 int hic_event_create(void **h_event);
 int hic_event_destroy(void *event);
@@ -226,11 +246,16 @@ typedef struct {
   int64_t sym_cap;
   int64_t *d_count;
   void *workspace;
+  int64_t records_per_tile; /* 0 or 1: one tile record per 64 blocks (hic_dct_quant_rle_u8);
+                               2: one per 32 blocks (hic_encode420_u8's chroma planes) */
 } hic_rle_job16;
 int hic_rle_encode_i16_tiles_batch(int n, const hic_rle_job16 *jobs, int max_len, void *stream);
 /* hic_rle_shard_summary_i16 from the tile records of hic_dct_quant_rle_u8. */
 int hic_rle_shard_summary_tiles(const int16_t *blocks, int64_t nblk, void *workspace, int64_t *d_summary,
                                 void *stream);
+/* The same for records_per_tile 1 or 2 (hic_encode420_u8's chroma records). */
+int hic_rle_shard_summary_records(const int16_t *blocks, int64_t nblk, int records_per_tile,
+                                  void *workspace, int64_t *d_summary, void *stream);
 int hic_rle_shard_summary_i32(const int32_t *blocks, int64_t nblk, int block_len,
                               void *workspace, int64_t *d_summary, void *stream);
 int hic_rle_encode_i32(const int32_t *blocks, int64_t nblk, int block_len, int max_len,

@@ -34,7 +34,7 @@ def test_ctypes_signatures_match_header():
     for name, args in decl.items():
         nargs = 0 if args.strip() == "void" else len([a for a in args.split(",") if a.strip()])
         assert nargs == len(_lib.SIGNATURES[name][1]), name
-    assert _lib.load().hic_abi_version() == 1
+    assert _lib.load().hic_abi_version() == 2
 
 
 def test_last_error_roundtrip():

@@ -273,15 +273,18 @@ def _oracle_encode(rgb):
     return out
 
 
-@pytest.mark.parametrize("H,W", [(64, 96), (4320, 7680), (250, 330), (512, 768)])
+@pytest.mark.parametrize("H,W", [(64, 96), (4320, 7680), (250, 330), (512, 768), (512, 1024), (272, 1536)])
 def test_pipeline_encoder(H, W):
+    """The device encoder vs the C oracle; widths % 512 == 0 (with H % 16 == 0) run
+    the fused kernel (hic_encode420_u8), the others the two-kernel chain."""
     rng = np.random.default_rng(H)
     rgb = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
-    if H == 250:
+    if H in (250, 272):
         rgb[:, :100] = 128  # flat region: all-zero AC blocks, long runs
     if H == 512:  # few grey levels: exact quantiser ties on the fast DCT path
         rgb = (rng.integers(0, 4, (H, W, 1)) * 85).astype(np.uint8).repeat(3, 2)
     enc = pipeline.Encoder(H, W)
+    assert enc.fused == (W % 512 == 0 and H % 16 == 0)
     enc.encode(device.to_device(rgb))
     got = enc.result()
     exp = _oracle_encode(rgb)
@@ -309,6 +312,46 @@ def test_pipeline_encoder(H, W):
     h, w = H // 2, W // 2
     exp_rgb = orcc.ycrcb_to_rgb(rec["lum"][:2 * h, :2 * w], orcc.pyr_up(rec["cr"]), orcc.pyr_up(rec["cb"]))
     np.testing.assert_array_equal(rgb2, exp_rgb)
+
+
+def _structured_rgb(kind, H, W, seed):
+    rng = np.random.default_rng(seed)
+    if kind == "random":
+        return rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    if kind == "levels":  # 4 grey levels: exact ties at DC / (4,4) / the (2,2) class
+        return (rng.integers(0, 4, (H, W, 1)) * 85).astype(np.uint8).repeat(3, 2)
+    if kind == "colour_levels":  # 2 levels per channel independently
+        return (rng.integers(0, 2, (H, W, 3)) * 255).astype(np.uint8)
+    if kind == "blocks":  # constant 8x8 blocks and symmetric 2x2 patterns
+        b = rng.integers(0, 256, (H // 8, W // 8, 3), dtype=np.uint8)
+        img = b.repeat(8, 0).repeat(8, 1)
+        img[::2, ::2] = 255 - img[::2, ::2]
+        return img
+    if kind == "flat":  # all-zero AC runs spanning whole strips and unit rows
+        img = np.full((H, W, 3), 128, np.uint8)
+        img[H // 2:H // 2 + 3, W // 3] = 7
+        return img
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind", ["random", "levels", "colour_levels", "blocks", "flat"])
+@pytest.mark.parametrize("H,W", [(16, 512), (144, 2048), (1088, 1536)])
+def test_fused_encoder_matches_two_kernel_chain(kind, H, W):
+    """hic_encode420_u8 (colour + pyrDown + DCT + tile records in one kernel, exact
+    tie fallbacks in place) == the two-kernel chain (hic_rgb_to_ycrcb420 +
+    hic_dct_quant_rle_u8_batch, deferred fallbacks), symbols and DC streams included
+    (the fused chroma records are 32-block half tiles)."""
+    rgb = _structured_rgb(kind, H, W, H + W)
+    x = device.to_device(rgb)
+    got, exp = pipeline.Encoder(H, W, fused=True), pipeline.Encoder(H, W, fused=False)
+    got.encode(x)
+    exp.encode(x)
+    a, b = got.result(), exp.result()
+    for k in pipeline.CHANNELS:
+        for j, what in enumerate(("coef", "dc", "sym_len", "sym_val")):
+            np.testing.assert_array_equal(a[k][j], b[k][j], err_msg="%s %s" % (k, what))
+    # the shard summaries read the half-tile records
+    np.testing.assert_array_equal(got.shard_summaries().cpu().numpy(), exp.shard_summaries().cpu().numpy())
 
 
 @pytest.mark.timeout(900)

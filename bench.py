@@ -395,6 +395,7 @@ def main():
         for ci, c in enumerate(counts.cpu().tolist()):
             pipeline.check_count(int(c), pipeline.CHANNELS[ci])
             assert c > 0, "empty symbol stream"
+    symbols = [int(c) for c in (encs[0].enc.counts if world > 1 else encs[0].counts).cpu().tolist()]
     gather_us = float(np.mean([a.elapsed_time(b) for a, b in gather_ev])) * 1e3 if gather_ev else None
 
     # ---- roofline kernel: the DCT+quantize+zig-zag pass (one launch for the three
@@ -472,6 +473,7 @@ def main():
                 "streams": args.streams,
                 "gather_to_rank0": gather,
                 "gather_us_per_step": None if gather_us is None else round(gather_us, 2),
+                "symbols_per_image_rank0": symbols,
                 "dist_backend": None if world == 1 else args.dist_backend + (" (same device)" if args.same_device
                                                                               else ""),
                 "parallelism": "dp%d tile-shard" % world,

@@ -7,7 +7,7 @@ namespace hic {
 static thread_local char g_last_error[512] = "";
 
 // hic_set_knob values (-1 = default; read by the launchers on every call)
-static int g_knobs[HIC_KNOB_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+static int g_knobs[HIC_KNOB_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 int knob(int k) {
   const int v = g_knobs[k];
   if (v >= 0) return v;
@@ -16,6 +16,7 @@ int knob(int k) {
     case HIC_KNOB_COLOR_SEG: return 8;
     case HIC_KNOB_RLE_NT: return 1;
     case HIC_KNOB_ENCODE_WAVES: return 2;
+    case HIC_KNOB_ENCODE_NT: return 0;
     default: return k == HIC_KNOB_DCT_WAVES_PER_CU ? -1 : 0;
   }
 }

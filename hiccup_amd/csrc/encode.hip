@@ -99,6 +99,7 @@ __device__ __forceinline__ uint4 enc_st16(const uint2 *st2, int b, int k) {
 
 // stage rows 0..31 -> o_lo (32 blocks), rows 32..63 -> o_hi: 1 KiB per store
 // instruction, nontemporal (the coefficients are not re-read by this kernel)
+template <bool NT>
 __device__ __forceinline__ void enc_store(const uint2 *st2, int lane, int16_t *o_lo, int16_t *o_hi) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
@@ -106,7 +107,10 @@ __device__ __forceinline__ void enc_store(const uint2 *st2, int lane, int16_t *o
     const uint4 t = enc_st16(st2, 8 * k + (lane >> 3), lane & 7);
     const u32x4 v = {t.x, t.y, t.z, t.w};
     u32x4 *o = reinterpret_cast<u32x4 *>(k < 4 ? o_lo : o_hi) + 64 * (k & 3) + lane;
-    __builtin_nontemporal_store(v, o);
+    if (NT)
+      __builtin_nontemporal_store(v, o);
+    else
+      *o = v;
   }
 }
 
@@ -232,22 +236,25 @@ __device__ __forceinline__ void enc_colour(const Enc420 &E, int y0, int s, int l
   }
 }
 
-template <int TMF>
+template <int TMF, bool NT>
 __device__ __forceinline__ void encode420_unit(const Enc420 &E);
 
 // Two register budgets (knob "encode_waves", A/B): 2 waves per SIMD (default: up
 // to 256 VGPRs, no spills; 63.7 us per 8K launch) or 3 (<= 168 VGPRs: the Y passes
 // spill ~80 dwords per unit; 76 us)
-template <int TMF>
+// NT: nontemporal coefficient stores (knob "encode_nt" = 1).  Default 0: plain
+// stores, so part of the coefficients is still in the Infinity Cache when the RLE
+// emit re-reads them (emit 59.7 -> 54.7 us; 8K encode +2-4 %, scripts/gpu_r2i.sh)
+template <int TMF, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_encode420(Enc420 E) {
-  encode420_unit<TMF>(E);
+  encode420_unit<TMF, NT>(E);
 }
-template <int TMF>
+template <int TMF, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_encode420_w2(Enc420 E) {
-  encode420_unit<TMF>(E);
+  encode420_unit<TMF, NT>(E);
 }
 
-template <int TMF>
+template <int TMF, bool NT>
 __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
   __shared__ uint2 s_stage[4 * 64 * kStageU2];
   __shared__ uint32_t s_chroma_all[4][2 * 8 * 64];
@@ -283,7 +290,7 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
     __builtin_amdgcn_wave_barrier();
     const int64_t b0 = (int64_t)(2 * u + br) * nbx + 64 * s;
     int16_t *o = E.coef[0] + b0 * 64;
-    enc_store(st2, lane, o, o + 32 * 64);
+    enc_store<NT>(st2, lane, o, o + 32 * 64);
     if (TMF >= 0 && E.rec[0]) {
       uint32_t zw[32];
       enc_stage_row(st2, lane, zw);
@@ -304,7 +311,7 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
     enc_dct<1>(w, st);
     __builtin_amdgcn_wave_barrier();
     const int64_t b0 = (int64_t)u * nbxc + 32 * s;
-    enc_store(st2, lane, E.coef[1] + b0 * 64, E.coef[2] + b0 * 64);
+    enc_store<NT>(st2, lane, E.coef[1] + b0 * 64, E.coef[2] + b0 * 64);
     if (TMF >= 0 && E.rec[1]) {
       uint32_t zw[32];
       enc_stage_row(st2, lane, zw);
@@ -365,10 +372,17 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
     else
       hipLaunchKernelGGL(kern, grid, block, 0, s, E);
   };
-  const bool w2 = knob(HIC_KNOB_ENCODE_WAVES) == 2;
-  if (max_len == 15)
-    w2 ? launch(k_encode420_w2<15>) : launch(k_encode420<15>);
-  else
-    w2 ? launch(k_encode420_w2<0>) : launch(k_encode420<0>);
+  const bool w2 = knob(HIC_KNOB_ENCODE_WAVES) == 2, nt = knob(HIC_KNOB_ENCODE_NT) != 0;
+  if (max_len == 15) {
+    if (nt)
+      w2 ? launch(k_encode420_w2<15, true>) : launch(k_encode420<15, true>);
+    else
+      w2 ? launch(k_encode420_w2<15, false>) : launch(k_encode420<15, false>);
+  } else {
+    if (nt)
+      w2 ? launch(k_encode420_w2<0, true>) : launch(k_encode420<0, true>);
+    else
+      w2 ? launch(k_encode420_w2<0, false>) : launch(k_encode420<0, false>);
+  }
   return check_launch("k_encode420");
 }

@@ -468,41 +468,47 @@ __device__ __forceinline__ void emit_tile16(const uint32_t (&w)[32], const int16
   // stage offsets congruent to the output position mod 16 bytes (16-byte copy-out)
   const int lo = (int)(o_tile & 15), vo = (int)(o_tile & 7);
   int64_t nf0 = 0;  // fillers of a long carried run written by the whole wave (unstaged)
+  const bool dense = nsym == __builtin_popcountll(ac) - 1;  // no run >= max_len inside the block
   if (first >= 0) {
     int64_t o = o_thr;
-    {
-      const int64_t nf = div_run(run0, M);
-      const int64_t rem = run0 - nf * M;
-      if (staged) {
-        int r = (int)(o - o_tile);
-        for (int64_t k = 0; k < nf; ++k, ++r) {
-          s_len[lo + r] = (uint8_t)(M - 1);
-          s_val[vo + r] = 0;
-        }
+    const int64_t nf = div_run(run0, M);
+    const int rem = (int)(run0 - nf * M);
+    if (staged) {
+      // the carried run's fillers, then (dense case) every nonzero from the first on
+      // in one branch-free pass over the block's registers -- no reload of the
+      // first value from memory, so nothing here waits on the next tile's prefetch
+      int r = (int)(o - o_tile);
+      for (int64_t k = 0; k < nf; ++k, ++r) {
+        s_len[lo + r] = (uint8_t)(M - 1);
+        s_val[vo + r] = 0;
+      }
+      o += nf;
+      if (!dense) {
         s_len[lo + r] = (uint8_t)rem;
         s_val[vo + r] = blk[1 + first];
-      } else {
-        nf0 = nf;
-        if (o + nf < cap) {
-          sym_len[o + nf] = (uint8_t)rem;
-          sym_val[o + nf] = blk[1 + first];
-        }
+        ++o;
+      }
+    } else {
+      nf0 = nf;
+      if (o + nf < cap) {
+        sym_len[o + nf] = (uint8_t)rem;
+        sym_val[o + nf] = blk[1 + first];
       }
       o += nf + 1;
     }
-    if (staged && nsym == __builtin_popcountll(ac) - 1) {
-      // no run inside the block reaches max_len (the dense case): one symbol per
-      // nonzero after the first, branch-free -- a zero coefficient writes to the
-      // stage's dummy slot and does not advance r
+    if (staged && dense) {
+      // one symbol per nonzero from the first (whose run is the carried one's
+      // remainder), branch-free -- a zero coefficient writes to the stage's dummy
+      // slot and does not advance r
       int r = (int)(o - o_tile) + lo;  // stage index of the next symbol (len array)
       const int dv = vo - lo;          // val index = len index + dv
       int pl = first;
 #pragma unroll
-      for (int j = 1; j < 63; ++j) {
+      for (int j = 0; j < 63; ++j) {
         const int v = zz_ac(w, j);
-        const bool nz = (v != 0) & (j > first);
-        s_len[nz ? r : kWSyms + 16] = (uint8_t)(j - pl - 1);  // dummy slots lie past every
-        s_val[nz ? r + dv : kWSyms + 24] = (int16_t)v;         // real one (lo, vo < 16)
+        const bool nz = (v != 0) & (j >= first);
+        s_len[nz ? r : kWSyms + 16] = (uint8_t)(j == first ? rem : j - pl - 1);  // dummy slots lie past
+        s_val[nz ? r + dv : kWSyms + 24] = (int16_t)v;  // every real one (lo, vo < 16)
         r += nz ? 1 : 0;
         pl = nz ? j : pl;
       }
@@ -548,9 +554,8 @@ __device__ __forceinline__ void emit_tile16(const uint32_t (&w)[32], const int16
   }
   __builtin_amdgcn_wave_barrier();
   HIC_PHASE(3);
-  // the persistent caller's prefetch of its next tile must not hold the copy-out:
-  // wait for every outstanding vector-memory op here, once per tile
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // (no vmcnt drain here: the copy-out reads only this wave's LDS stage, so the
+  // next tile's prefetch stays in flight across it)
   HIC_PHASE(4);
   if (staged) {
     copy_out_wave16<uint8_t, NT>(s_len, lo, sym_len, o_tile, (int)total, cap);

@@ -162,11 +162,6 @@ def encode_channel(plane, bs=None):
     return dc.cpu().numpy(), Ls[:count].cpu().numpy(), Vs[:count].cpu().numpy()
 
 
-def _huff_from_keys(keys):
-    uniq, counts = huffman.first_appearance_counts(keys)
-    return huffman.HuffmanTree.construct_from_counts(uniq, counts)
-
-
 def huffman_encode(huff):
     return hic.PayloadStringP(hic.TupP, [hic.TupP(v, c) for v, c in huff.encode_table()])
 
@@ -184,17 +179,25 @@ def huffman_data_decode(data, tree):
 
 
 def jpeg_encode(compressed):
-    """codec.py:275-334: CompressedImage -> HicImage (9 tables, 9 bit strings, 2 shapes)."""
+    """codec.py:275-334: CompressedImage -> HicImage (9 tables, 9 bit strings, 2 shapes).
+    Everything but the nine trees runs on the GPU: split + zig-zag, DC DPCM, AC RLE
+    (encode_channel_device), the key histograms in first-appearance order and the
+    bit packing of the coded streams (huffman.DeviceStream, csrc/huffman.hip)."""
     utils.debug_msg("Starting JPEG encoding")
     bs = settings.JPEG_BLOCK_SIZE
-    streams = utils.dict_map(compressed.as_dict, lambda k, v: encode_channel(v, bs))
-    trees = {}
-    for k, (dc, L, V) in streams.items():
-        trees[k] = (_huff_from_keys(dc), _huff_from_keys(V), _huff_from_keys(L))
     chans = ("lum", "cr", "cb")
-    tables = [huffman_encode(trees[k][j]) for j in range(3) for k in chans]
-    keysets = {0: 0, 1: 2, 2: 1}  # tree j encodes stream keysets[j] (dc, values, lengths)
-    data = [hic.BitStringP(trees[k][j].encode_keys(streams[k][keysets[j]])) for j in range(3) for k in chans]
+    streams = {}
+    for k, v in compressed.as_dict.items():
+        p = _i32(v, "coefficient plane")
+        if p.ndim != 2:
+            raise ValueError("expected a 2-D coefficient plane")
+        dc, Ls, Vs, cnt = encode_channel_device(device.to_device(p), p.shape[0], p.shape[1], bs)
+        count = int(device.to_host(cnt)[0])
+        # trees per channel: DC differences, AC values, AC lengths (codec.py:304-313)
+        streams[k] = (huffman.DeviceStream(dc), huffman.DeviceStream(Vs[:count]), huffman.DeviceStream(Ls[:count]))
+    # each tree codes the stream it was built from (codec.py:310-330)
+    tables = [huffman_encode(streams[k][j].tree) for j in range(3) for k in chans]
+    data = [hic.BitStringP.from_packed(*streams[k][j].packed()) for j in range(3) for k in chans]
     shape = compressed.shape
     payloads = tables + data + [hic.TupP(shape[0][0], shape[0][1]), hic.TupP(shape[1][0], shape[1][1])]
     return hic.HicImage.jpeg_image(payloads)

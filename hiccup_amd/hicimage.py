@@ -6,6 +6,8 @@ objects only (never loads foreign files with anything but this format).
 """
 import pickle
 
+import numpy as np
+
 from . import iohelper as io
 from . import model, utils
 
@@ -45,20 +47,42 @@ class TupP(Payload):
 
 
 class BitStringP(Payload):
-    """Huffman-coded data as a '0'/'1' string, stored byte-padded."""
+    """Huffman-coded data as a '0'/'1' string, stored byte-padded.  A stream packed
+    on the GPU (from_packed) keeps its bytes; the string is made on first use."""
 
     @classmethod
     def from_bytes(cls, b):
         return cls(io.padded_bytes_2_bs(b))
 
+    @classmethod
+    def from_packed(cls, packed, nbits):
+        """packed: uint8 array, nbits bits MSB-first (hic_huffman_pack's output)."""
+        obj = cls(None)
+        obj._packed, obj._nbits = np.asarray(packed, dtype=np.uint8), int(nbits)
+        return obj
+
     def __init__(self, string):
-        self.payload = string
+        self._payload = string
+        self._packed = None
+        self._nbits = None
+
+    @property
+    def payload(self):
+        if self._payload is None:
+            bits = np.unpackbits(self._packed[:-(-self._nbits // 8)])[:self._nbits]
+            self._payload = (bits + ord("0")).astype(np.uint8).tobytes().decode("ascii")
+        return self._payload
 
     def __eq__(self, other):
         return type(self) == type(other) and self.payload == other.payload
 
     @property
     def byte_stream(self):
+        if self._payload is None:  # io.padded_bs_2_bytes on the packed bits
+            padding = 8 - self._nbits % 8
+            body = self._packed[:self._nbits // 8 + 1] if self._nbits % 8 else self._packed[:self._nbits // 8]
+            body = np.concatenate([body, np.zeros(1 if padding == 8 else 0, np.uint8)])
+            return bytes([padding]) + body.tobytes()
         return io.padded_bs_2_bytes(self.payload)
 
 

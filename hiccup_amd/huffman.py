@@ -10,12 +10,18 @@ root -> leaf with left = "1", right = "0"; a one-symbol alphabet gets the code
 
 Encoding is vectorised (a code lookup per distinct key, then one join) instead
 of the reference's per-symbol parent walk (huffman.py:131-142).
+
+Device half (codec.jpeg_encode's hot loops, csrc/huffman.hip): the key histogram
+in first-appearance order (``device_counts``) and the bit packing of a coded
+stream (``HuffmanTree.encode_device``); only the tree (a heap over the distinct
+keys) is built here.
 """
 import heapq
 
 import numpy as np
+import torch
 
-from . import utils
+from . import _lib, device, utils
 
 
 class HuffmanTree:
@@ -200,6 +206,40 @@ class HuffmanTree:
         table = np.array([codes[int(k)] for k in uniq], dtype=object)
         return "".join(table[inv].tolist())
 
+    def code_table(self, key_min, nbins):
+        """(code bits uint64, code lengths uint8) for keys key_min .. key_min + nbins - 1
+        (0 / 0 for keys not in the tree), the table hic_huffman_pack reads."""
+        bits = np.zeros(nbins, dtype=np.uint64)
+        lens = np.zeros(nbins, dtype=np.uint8)
+        for k, code in self.codes().items():
+            if len(code) > 64:
+                raise ValueError("Huffman code longer than 64 bits")
+            bits[int(k) - key_min] = int(code, 2)
+            lens[int(k) - key_min] = len(code)
+        return bits, lens
+
+    def encode_device(self, keys_dev, n, key_min, nbins, counts, stream=None):
+        """encode_data of a device key stream (uint8 / int16 / int32 tensor of n keys
+        in [key_min, key_min + nbins), with counts the per-bin histogram), packed on
+        the GPU: returns (packed uint8 numpy array, number of bits), MSB-first --
+        the bits io.padded_bs_2_bytes stores after its pad-length byte."""
+        if n == 0:
+            return np.zeros(0, np.uint8), 0
+        bits, lens = self.code_table(key_min, nbins)
+        total = int(np.sum(np.asarray(counts, dtype=np.int64) * lens.astype(np.int64)))
+        nbytes = max(4, -(-total // 32) * 4)
+        out = device.empty((nbytes,), torch.uint8)
+        nbits = device.empty((1,), torch.int64)
+        ws = device.workspace(_lib.load().hic_huffman_pack_workspace_bytes(n))
+        cb, cl = device.to_device(bits.view(np.int64)), device.to_device(lens)
+        _lib.call("hic_huffman_pack", device.ptr(keys_dev), keys_dev.element_size(), n, key_min, nbins, device.ptr(cb),
+                  device.ptr(cl), device.ptr(out), nbytes, device.ptr(nbits), device.ptr(ws),
+                  device.stream_ptr(stream))
+        nb = int(nbits.cpu()[0])
+        if nb != total:
+            raise RuntimeError("packed %d bits, the histogram says %d" % (nb, total))
+        return out[:-(-nb // 8)].cpu().numpy(), nb
+
     def decode_data(self, bits):
         out = []
         node = self.root
@@ -222,3 +262,58 @@ def first_appearance_counts(keys):
     uniq, first, counts = np.unique(keys, return_index=True, return_counts=True)
     order = np.argsort(first, kind="stable")
     return [int(k) for k in uniq[order]], counts[order]
+
+
+# ------------------------------------------------------------------ device half
+def device_key_range(keys_dev, n=None, stream=None):
+    """(min, max) of a device key stream (hic_key_range; syncs)."""
+    n = keys_dev.numel() if n is None else n
+    mm = device.empty((2,), torch.int32)
+    _lib.call("hic_key_range", device.ptr(keys_dev), keys_dev.element_size(), n, device.ptr(mm),
+              device.stream_ptr(stream))
+    lo, hi = (int(x) for x in mm.cpu().tolist())
+    return lo, hi
+
+
+def device_counts_raw(keys_dev, n, key_min, nbins, stream=None):
+    """Per-bin (counts, first index) host arrays of hic_key_histogram (syncs)."""
+    counts = device.empty((nbins,), torch.int32)
+    first = device.empty((nbins,), torch.int32)
+    _lib.call("hic_key_histogram", device.ptr(keys_dev), keys_dev.element_size(), n, key_min, nbins,
+              device.ptr(counts), device.ptr(first), device.stream_ptr(stream))
+    return counts.cpu().numpy().view(np.uint32), first.cpu().numpy().view(np.uint32)
+
+
+class DeviceStream:
+    """One key stream on the device with its GPU histogram: the Huffman tree
+    (construct_from_data's, huffman.py:20-28: leaves in first-appearance order) and
+    the packed bits of encode_data (huffman.py:131-142)."""
+
+    def __init__(self, keys_dev, n=None, stream=None):
+        self.keys, self.n, self.stream = keys_dev, keys_dev.numel() if n is None else int(n), stream
+        if self.n == 0:
+            raise ValueError("empty key stream")
+        self.lo, hi = device_key_range(keys_dev, self.n, stream)
+        self.nbins = hi - self.lo + 1
+        self.counts, first = device_counts_raw(keys_dev, self.n, self.lo, self.nbins, stream)
+        present = np.flatnonzero(self.counts)
+        order = present[np.argsort(first[present], kind="stable")]
+        self.keys_in_order = [int(self.lo + b) for b in order]
+        self.tree = HuffmanTree.construct_from_counts(self.keys_in_order, self.counts[order].astype(np.int64))
+
+    def packed(self):
+        return self.tree.encode_device(self.keys, self.n, self.lo, self.nbins, self.counts, self.stream)
+
+
+def device_counts(keys_dev, n=None, stream=None):
+    """first_appearance_counts of a device key stream: (keys in first-appearance
+    order, counts) from the GPU histogram (utils.group_by's order, which the tree's
+    ties follow: huffman.py:20-28)."""
+    n = keys_dev.numel() if n is None else n
+    if n == 0:
+        return [], np.zeros(0, np.int64)
+    lo, hi = device_key_range(keys_dev, n, stream)
+    counts, first = device_counts_raw(keys_dev, n, lo, hi - lo + 1, stream)
+    present = np.flatnonzero(counts)
+    order = present[np.argsort(first[present], kind="stable")]
+    return [int(lo + b) for b in order], counts[order].astype(np.int64)

@@ -176,6 +176,29 @@ class Encoder:
         self.transform(rgb, stream, dct_events=dct_events)
         self.entropy(stream)
 
+    def hic_image(self, stream=None):
+        """codec.jpeg_encode of this encode, from the device streams: the nine Huffman
+        trees from GPU key histograms, the nine bit strings packed on the GPU
+        (huffman.DeviceStream); == codec.jpeg_encode(the encoded CompressedImage)
+        for an unsharded encoder (syncs)."""
+        from . import hicimage as hic
+        from . import huffman
+        if self.rows != (0, self.H):
+            raise ValueError("hic_image needs the whole image (an unsharded encoder)")
+        counts = self.counts.cpu().tolist()
+        streams = {}
+        for i, k in enumerate(CHANNELS):
+            check_count(int(counts[i]), k)
+            c = int(counts[i])
+            streams[k] = (huffman.DeviceStream(self.dc[k], stream=stream),
+                          huffman.DeviceStream(self.sym_val[k][:c], stream=stream),
+                          huffman.DeviceStream(self.sym_len[k][:c], stream=stream))
+        tables = [hic.PayloadStringP(hic.TupP, [hic.TupP(v, c) for v, c in streams[k][j].tree.encode_table()])
+                  for j in range(3) for k in CHANNELS]
+        data = [hic.BitStringP.from_packed(*streams[k][j].packed()) for j in range(3) for k in CHANNELS]
+        (h, w), (hc, wc) = self.shapes["lum"], self.shapes["cr"]
+        return hic.HicImage.jpeg_image(tables + data + [hic.TupP(h, w), hic.TupP(hc, wc)])
+
     def result(self):
         """Host copies: {channel: (zigzag blocks, dc_diff, sym_len, sym_val)} (syncs)."""
         device.sync()

@@ -305,6 +305,28 @@ int hic_rle_stream_decode_i32(const int32_t *sym_len, const int32_t *sym_val, in
                               int64_t length, int32_t *out, int64_t out_cap, int64_t *d_status,
                               void *workspace, void *stream);
 
+/* ---- Huffman back end, device half (codec.jpeg_encode's trees and bit strings,
+ *      codec.py:304-334; huffman.py:11-58,131-142; iohelper.py:35-56).  The trees
+ *      (a heap over the distinct keys) are built on the host.
+ *  keys: int8 (key_bytes 1, unsigned), int16 (2) or int32 (4) device streams.
+ *  hic_key_range: d_minmax (device int32[2]) = {min, max} of the n keys.
+ *  hic_key_histogram: for key k in [key_min, key_min + nbins): d_counts[k - key_min]
+ *    (uint32) = its count and d_first[...] = the index of its first appearance
+ *    (0xFFFFFFFF if absent) -- utils.group_by's order, which the tree's ties follow.
+ *  hic_huffman_pack: symbol i gets code d_code_bits[k] (right-aligned, <= 64 bits)
+ *    of length d_code_len[k]; out (zeroed here) receives the concatenated codes
+ *    MSB-first (the bit string of encode_data, as iohelper packs it after its
+ *    pad-length byte); *d_nbits = the total bits.  out_bytes (multiple of 4) must
+ *    hold ceil(total / 32) words (sum of count x length); words past it are not
+ *    written.  workspace >= hic_huffman_pack_workspace_bytes(n). */
+int hic_key_range(const void *keys, int key_bytes, int64_t n, int32_t *d_minmax, void *stream);
+int hic_key_histogram(const void *keys, int key_bytes, int64_t n, int32_t key_min, int32_t nbins,
+                      uint32_t *d_counts, uint32_t *d_first, void *stream);
+size_t hic_huffman_pack_workspace_bytes(int64_t n);
+int hic_huffman_pack(const void *keys, int key_bytes, int64_t n, int32_t key_min, int32_t nbins,
+                     const uint64_t *d_code_bits, const uint8_t *d_code_len, uint8_t *out,
+                     int64_t out_bytes, int64_t *d_nbits, void *workspace, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

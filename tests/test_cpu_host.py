@@ -168,3 +168,17 @@ def test_shard_plan_and_stitch():
     assert sharding.stitch_host(s, 0).tolist() == [0, 0, 0, 0]
     assert sharding.stitch_host(s, 1).tolist() == [3, 0, 1, 6]
     assert sharding.stitch_host(s, 2).tolist() == [66, 1, 1, 1]
+
+
+def test_bitstring_packed_matches_string_form():
+    """BitStringP.from_packed (the GPU packer's output) gives the same payload and
+    container bytes as the '0'/'1' string form (iohelper.padded_bs_2_bytes)."""
+    import numpy as np
+    rng = np.random.default_rng(7)
+    for nbits in [0, 1, 3, 7, 8, 9, 15, 16, 17, 64, 1001]:
+        bits = rng.integers(0, 2, nbits).astype(np.uint8)
+        packed = np.packbits(bits) if nbits else np.zeros(0, np.uint8)
+        s = "".join("1" if b else "0" for b in bits)
+        a, b = hicimage.BitStringP.from_packed(packed, nbits), hicimage.BitStringP(s)
+        assert a.byte_stream == b.byte_stream == iohelper.padded_bs_2_bytes(s), nbits
+        assert a.payload == s and a == b

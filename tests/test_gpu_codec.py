@@ -479,3 +479,60 @@ def test_two_stream_overlap_matches_single_stream():
         for k in pipeline.CHANNELS:
             for a, b in zip(got[k], exp[k]):
                 np.testing.assert_array_equal(a, b, err_msg="%d %s" % (n, k))
+
+
+@pytest.mark.parametrize("dtype,kind", [(np.uint8, "lengths"), (np.int16, "values"), (np.int32, "dc"),
+                                        (np.int16, "single"), (np.int32, "skewed"), (np.uint8, "tail")])
+def test_huffman_device_vs_host(dtype, kind):
+    """GPU histogram (first-appearance order) + GPU bit packing == the host tree
+    builder and string encoder (huffman.py, pinned against the reference's golden
+    tables and bit strings in test_cpu_host / test_jpeg_encode_golden)."""
+    from hiccup_amd import huffman
+    rng = np.random.default_rng(hash(kind) % 1000)
+    n = 300_001
+    if kind == "lengths":
+        keys = rng.integers(0, 15, n)
+    elif kind == "values":
+        keys = np.round(rng.laplace(0, 40, n)).clip(-3277, 3277)
+    elif kind == "dc":
+        keys = rng.integers(-4096, 4097, n)
+    elif kind == "single":
+        keys = np.full(n, -7)
+    elif kind == "skewed":  # deep trees: long codes
+        keys = (rng.geometric(0.5, n) - 1) * 3 - 40
+    else:  # a few rare keys at the end of the stream
+        keys = np.concatenate([rng.integers(0, 3, n - 5), [200, 201, 250, 255, 0]])
+    keys = keys.astype(dtype)
+    ds = huffman.DeviceStream(device.to_device(keys))
+    uniq, counts = huffman.first_appearance_counts(keys)
+    assert ds.keys_in_order == uniq
+    host = huffman.HuffmanTree.construct_from_counts(uniq, counts)
+    assert ds.tree.encode_table() == host.encode_table()
+    packed, nbits = ds.packed()
+    bits = host.encode_keys(keys)
+    assert nbits == len(bits)
+    got = hicimage.BitStringP.from_packed(packed, nbits)
+    assert got.payload == bits
+    assert got.byte_stream == hicimage.BitStringP(bits).byte_stream
+
+
+def test_encoder_hic_image_equals_jpeg_encode():
+    """pipeline.Encoder.hic_image (GPU streams + GPU Huffman) == codec.jpeg_encode of
+    the same quantized planes (the reference's encode path on its own output)."""
+    H, W = 272, 1024
+    rng = np.random.default_rng(3)
+    rgb = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    rgb[:, :300] = 90
+    enc = pipeline.Encoder(H, W)
+    enc.encode(device.to_device(rgb))
+    hic = enc.hic_image()
+    res = enc.result()
+    planes = {}
+    for k, (h, w) in enc.shapes.items():
+        zz = res[k][0].astype(np.int32)
+        planes[k] = orc.merge_blocks(zz[:, np.argsort(orc.ZZ8)].reshape(-1, 8, 8), (h, w))
+    ref = codec.jpeg_encode(model.CompressedImage(planes["lum"], planes["cr"], planes["cb"]))
+    assert len(hic.payloads) == len(ref.payloads) == 20
+    for i, (a, b) in enumerate(zip(hic.payloads, ref.payloads)):
+        assert a == b, i
+    assert hic.byte_stream() == ref.byte_stream()

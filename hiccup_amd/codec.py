@@ -162,8 +162,12 @@ def encode_channel(plane, bs=None):
     return dc.cpu().numpy(), Ls[:count].cpu().numpy(), Vs[:count].cpu().numpy()
 
 
-def huffman_encode(huff):
-    return hic.PayloadStringP(hic.TupP, [hic.TupP(v, c) for v, c in huff.encode_table()])
+def huffman_encode(huff, key_type=None):
+    """A tree's table payload; key_type: the scalar type its keys have in the
+    reference (numpy integers of the plane's dtype for the DC trees, whose keys come
+    from the plane itself; Python ints for the RLE trees) -- it shows in the bytes."""
+    kt = key_type or (lambda v: v)
+    return hic.PayloadStringP(hic.TupP, [hic.TupP(kt(v), c) for v, c in huff.encode_table()])
 
 
 def huffman_decode(data):
@@ -186,8 +190,11 @@ def jpeg_encode(compressed):
     utils.debug_msg("Starting JPEG encoding")
     bs = settings.JPEG_BLOCK_SIZE
     chans = ("lum", "cr", "cb")
-    streams = {}
+    streams, dc_type = {}, {}
     for k, v in compressed.as_dict.items():
+        # the reference's DC keys are elements of the plane (utils.differences over
+        # block[0][0]): numpy scalars of its dtype
+        dc_type[k] = np.asarray(v).dtype.type
         p = _i32(v, "coefficient plane")
         if p.ndim != 2:
             raise ValueError("expected a 2-D coefficient plane")
@@ -196,7 +203,7 @@ def jpeg_encode(compressed):
         # trees per channel: DC differences, AC values, AC lengths (codec.py:304-313)
         streams[k] = (huffman.DeviceStream(dc), huffman.DeviceStream(Vs[:count]), huffman.DeviceStream(Ls[:count]))
     # each tree codes the stream it was built from (codec.py:310-330)
-    tables = [huffman_encode(streams[k][j].tree) for j in range(3) for k in chans]
+    tables = [huffman_encode(streams[k][j].tree, dc_type[k] if j == 0 else int) for j in range(3) for k in chans]
     data = [hic.BitStringP.from_packed(*streams[k][j].packed()) for j in range(3) for k in chans]
     shape = compressed.shape
     payloads = tables + data + [hic.TupP(shape[0][0], shape[0][1]), hic.TupP(shape[1][0], shape[1][1])]

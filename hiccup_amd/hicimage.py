@@ -1,15 +1,58 @@
 """HIC container (mirrors hiccup/hicimage.py:14-183), JPEG flavour.
 
 Host-side "next" row: the payload list jpeg_encode
-returns.  Serialisation uses pickle of plain tuples/bytes of THIS package's own
-objects only (never loads foreign files with anything but this format).
+returns.  Byte format = the reference's: a Huffman table (PayloadStringP) is a
+pickle of {"type": <the payload CLASS>, "data": [...]} whose class reference reads
+``hiccup.hicimage.TupP`` (hicimage.py:117-121), so files written here load in the
+reference and the reference's files load here (pinned byte-for-byte by
+tests/golden/hicimage_cases.npz).  Loading never runs arbitrary pickles: a
+restricted unpickler admits only the three payload classes (as the reference
+names them, or by this module's name) and numpy's scalar reconstruction (the
+reference's DC tables hold numpy integers).
 """
+import io as _bio
 import pickle
 
 import numpy as np
 
 from . import iohelper as io
 from . import model, utils
+
+_REF_MODULE = "hiccup.hicimage"  # the module the reference's pickles name
+
+
+class _SafeUnpickler(pickle.Unpickler):
+    _NUMPY = {("numpy._core.multiarray", "scalar"), ("numpy.core.multiarray", "scalar"), ("numpy", "dtype")}
+
+    def find_class(self, module, name):
+        if module in (_REF_MODULE, __name__) and name in _PAYLOAD_TYPES:
+            return _PAYLOAD_TYPES[name]
+        if (module, name) in self._NUMPY:
+            return super().find_class(module, name)
+        raise pickle.UnpicklingError("refusing to load %s.%s from a HIC file" % (module, name))
+
+
+def _loads(b):
+    return _SafeUnpickler(_bio.BytesIO(bytes(b))).load()
+
+
+class _RefPickler(pickle._Pickler):
+    """Writes this module's payload classes as the reference names them."""
+
+    def save_global(self, obj, name=None):
+        if isinstance(obj, type) and _PAYLOAD_TYPES.get(obj.__name__) is obj:
+            self.save(_REF_MODULE)
+            self.save(obj.__name__)
+            self.write(pickle.STACK_GLOBAL)
+            self.memoize(obj)
+            return
+        super().save_global(obj, name)
+
+
+def _dumps(obj):
+    f = _bio.BytesIO()
+    _RefPickler(f, protocol=pickle.DEFAULT_PROTOCOL).dump(obj)
+    return f.getvalue()
 
 
 class Payload:
@@ -27,7 +70,7 @@ class TupP(Payload):
 
     @classmethod
     def from_bytes(cls, b):
-        t = pickle.loads(b)
+        t = _loads(b)
         return cls(t[0], t[1])
 
     def __init__(self, n1, n2):
@@ -107,12 +150,10 @@ class PlainStringP(Payload):
 class PayloadStringP(Payload):
     """A group of payloads of one type (a Huffman table)."""
 
-    _TYPES = {"TupP": TupP, "BitStringP": BitStringP, "PlainStringP": PlainStringP}
-
     @classmethod
     def from_bytes(cls, b):
-        d = pickle.loads(b)
-        t = cls._TYPES[d["type"]]
+        d = _loads(b)
+        t = d["type"] if isinstance(d["type"], type) else _PAYLOAD_TYPES[d["type"]]  # (round-1 files: a name)
         return cls(t, [t.from_bytes(x) for x in d["data"]])
 
     def __init__(self, t, payloads):
@@ -124,7 +165,10 @@ class PayloadStringP(Payload):
 
     @property
     def byte_stream(self):
-        return pickle.dumps({"type": self.t.__name__, "data": [p.byte_stream for p in self.payloads]})
+        return _dumps({"type": self.t, "data": [p.byte_stream for p in self.payloads]})
+
+
+_PAYLOAD_TYPES = {"TupP": TupP, "BitStringP": BitStringP, "PlainStringP": PlainStringP}
 
 
 class HicImage:
@@ -149,7 +193,7 @@ class HicImage:
     @classmethod
     def from_file(cls, path):
         with open(path, "rb") as f:
-            raw = pickle.load(f)
+            raw = _loads(f.read())
         assert raw is not None
         return cls.from_bytes(raw)
 

@@ -22,6 +22,7 @@ an encoder one tile-shard of a larger image (see sharding.py).
 """
 import ctypes
 
+import numpy as np
 import torch
 
 from . import _lib, device
@@ -193,7 +194,9 @@ class Encoder:
             streams[k] = (huffman.DeviceStream(self.dc[k], stream=stream),
                           huffman.DeviceStream(self.sym_val[k][:c], stream=stream),
                           huffman.DeviceStream(self.sym_len[k][:c], stream=stream))
-        tables = [hic.PayloadStringP(hic.TupP, [hic.TupP(v, c) for v, c in streams[k][j].tree.encode_table()])
+        # DC keys as the reference holds them (numpy int32: dct_channel's dtype)
+        tables = [hic.PayloadStringP(hic.TupP, [hic.TupP(np.int32(v) if j == 0 else int(v), c)
+                                                for v, c in streams[k][j].tree.encode_table()])
                   for j in range(3) for k in CHANNELS]
         data = [hic.BitStringP.from_packed(*streams[k][j].packed()) for j in range(3) for k in CHANNELS]
         (h, w), (hc, wc) = self.shapes["lum"], self.shapes["cr"]

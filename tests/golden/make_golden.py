@@ -299,8 +299,35 @@ def lenna():
     print("lenna done")
 
 
+def hicimage_cases():
+    """The reference's container payload bytes (hicimage.py:31-121): the nine
+    Huffman tables (PayloadStringP: a pickle naming the payload CLASS), the two
+    shape TupPs and the settings PlainStringP of jpeg_encode on codec case
+    inputs.  BitStringP bytes need the absent ``bitstring`` package, so they are not
+    recorded here (their format is pinned by iohelpertest.py's vectors)."""
+    import hiccup.hicimage as hicimage
+    rng = np.random.default_rng(11)
+    d = {}
+    settings.JPEG_BLOCK_SIZE = 8
+    y = transform.dct_channel(rng.integers(0, 256, (32, 48), dtype=np.uint8), LUM)
+    cr = transform.dct_channel(rng.integers(90, 170, (16, 24), dtype=np.uint8), CHR)
+    cb = transform.dct_channel(rng.integers(100, 140, (16, 24), dtype=np.uint8), CHR)
+    hic = codec.jpeg_encode(model.CompressedImage(y, cr, cb))
+    for k, ch in enumerate(("lum", "cr", "cb")):
+        d["in_" + ch] = np.asarray(hic is not None and {"lum": y, "cr": cr, "cb": cb}[ch]).astype(np.int64)
+    for i in list(range(9)) + [18, 19]:
+        d["payload_%02d" % i] = np.frombuffer(hic.payloads[i].byte_stream, dtype=np.uint8)
+    d["settings_0"] = np.frombuffer(hic.settings[0].byte_stream, dtype=np.uint8)
+    d["pickle_protocol"] = np.int64(__import__("pickle").DEFAULT_PROTOCOL)
+    assert isinstance(hic.payloads[0], hicimage.PayloadStringP)
+    np.savez_compressed(out("hicimage_cases.npz"), **d)
+    print("hicimage cases:", len(d))
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["tables", "transform", "rle", "codec", "lenna"]
+    which = sys.argv[1:] or ["tables", "transform", "rle", "codec", "lenna", "hicimage"]
+    if "hicimage" in which:
+        hicimage_cases()
     if "tables" in which:
         zigzag_tables()
     if "transform" in which:

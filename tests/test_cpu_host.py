@@ -182,3 +182,38 @@ def test_bitstring_packed_matches_string_form():
         a, b = hicimage.BitStringP.from_packed(packed, nbits), hicimage.BitStringP(s)
         assert a.byte_stream == b.byte_stream == iohelper.padded_bs_2_bytes(s), nbits
         assert a.payload == s and a == b
+
+
+def test_container_bytes_match_reference():
+    """The reference's own container bytes (tests/golden/hicimage_cases.npz, written
+    by hiccup.hicimage under this Python): our loader reads them (the class
+    reference hiccup.hicimage.TupP and numpy scalars, nothing else), re-serialises
+    them byte for byte, and the tables built here from the same planes are the
+    same bytes (hicimage.py:117-121, codec.py:304-334)."""
+    import numpy as np
+    import pickle
+    import oracle.oracle as orc
+    from hiccup_amd import codec
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "hicimage_cases.npz"))
+    assert int(g["pickle_protocol"]) == pickle.DEFAULT_PROTOCOL
+    for i in list(range(9)) + [18, 19]:
+        raw = bytes(g["payload_%02d" % i])
+        p = (hicimage.TupP if i >= 18 else hicimage.PayloadStringP).from_bytes(raw)
+        assert p.byte_stream == raw, i
+    assert hicimage.PlainStringP.from_bytes(bytes(g["settings_0"])).payload == "JPEG"
+    for c, ch in enumerate(("lum", "cr", "cb")):
+        plane = g["in_" + ch].astype(np.int32)
+        zz = orc.zigzag_blocks(orc.split_blocks(plane)).astype(np.int64)
+        dc = orc.dpcm(zz[:, 0])
+        L, V = orc.rle_encode(zz[:, 1:].reshape(-1), 15)
+        for j, (keys, kt) in enumerate(((dc, np.int32), (V, int), (L, int))):
+            uniq, counts = huffman.first_appearance_counts(keys)
+            tree = huffman.HuffmanTree.construct_from_counts(uniq, counts)
+            assert codec.huffman_encode(tree, kt).byte_stream == bytes(g["payload_%02d" % (3 * j + c)]), (ch, j)
+
+
+def test_container_refuses_foreign_pickles():
+    import pickle
+    evil = pickle.dumps({"type": os.system, "data": []})
+    with pytest.raises(pickle.UnpicklingError):
+        hicimage.PayloadStringP.from_bytes(evil)

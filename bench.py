@@ -154,6 +154,46 @@ def extra_4k_luma(steps=20):
             "algorithmic_bytes": n * n * 3, "timed_launches": steps}
 
 
+def extra_8k_plane_dct(steps=24):
+    """The north_star's DCT+quantize pass on its own: k_dct_planes over the 8K Y +
+    Cr + Cb planes (4320 x 7680 + 2 x 2160 x 3840 uint8 -> int16 zig-zag blocks +
+    RLE tile records, one launch, the two-kernel chain's second kernel), rotating
+    >= 1.2 GB of planes, timed by the launch's own events.  Algorithmic bytes 3 B
+    per plane pixel (1 read + 2 written)."""
+    from hiccup_amd import _lib, device
+    shapes = [(H8K, W8K, 0), (H8K // 2, W8K // 2, 1), (H8K // 2, W8K // 2, 1)]
+    px = sum(h * w for h, w, _ in shapes)
+    rot = int(np.ceil(ROT_BYTES / (px * 3)))
+    g = torch.Generator(device="cuda")
+    g.manual_seed(4)
+    sets = []
+    for _ in range(rot):
+        planes, outs, wss = [], [], []
+        jobs = (_lib.DctPlaneJob * 3)()
+        for i, (h, w, t) in enumerate(shapes):
+            nblk = (h // 8) * (w // 8)
+            planes.append(torch.randint(0, 256, (h, w), dtype=torch.uint8, device="cuda", generator=g))
+            outs.append(device.empty((nblk, 64), torch.int16))
+            wss.append(device.workspace(_lib.load().hic_rle_workspace_bytes(nblk, 64)))
+            jobs[i] = _lib.DctPlaneJob(planes[i].data_ptr(), h, w, w, t, outs[i].data_ptr(), wss[i].data_ptr())
+        sets.append((planes, outs, wss, jobs))
+    evs = [device.KernelEvents() for _ in range(steps)]
+    for i in range(4):
+        _lib.call("hic_dct_quant_rle_u8_batch", 3, sets[i % rot][3], 15, device.stream_ptr(), None, None)
+    for i, e in enumerate(evs):
+        _lib.call("hic_dct_quant_rle_u8_batch", 3, sets[(4 + i) % rot][3], 15, device.stream_ptr(), e.start, e.stop)
+    torch.cuda.synchronize()
+    us = float(np.median([e.elapsed_ms() for e in evs])) * 1e3
+    gbs = px * 3 / (us * 1e-6) / 1e9
+    del sets
+    torch.cuda.empty_cache()
+    return {"workload": "8K Y + Cr + Cb planes -> quantized int16 zig-zag blocks + RLE tile records (k_dct_planes, "
+                        "the DCT+quantize pass without the colour stage)",
+            "kernel": "k_dct_planes<-1,ZIGZAG_I16,15>", "median_launch_us": round(us, 2),
+            "achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes": px * 3,
+            "timed_launches": steps}
+
+
 def extra_16k_roundtrip(steps=4):
     """BASELINE configs[4] on one GPU: 16384 x 16384 random RGB, full encode (colour,
     DCT/quantize/zig-zag, DPCM/RLE) then full decode (RLE expand, DC integrate,
@@ -242,11 +282,12 @@ def extra_16k_roundtrip_sharded(rank, world, backend, steps=4):
             "psnr_db_vs_input": round(10 * np.log10(255.0 ** 2 / mse), 3), "timed_roundtrips": steps}
 
 
-def load_pmc_traffic():
-    """HBM bytes per 3-plane DCT launch from the committed rocprofv3 PMC summary
-    (profiles/pmc_dct.json: FETCH_SIZE / WRITE_SIZE calibrated on a kernel of known
-    traffic, MI355X_MICROARCH.md HBM section)."""
-    p = os.path.join(HERE, "profiles", "pmc_dct.json")
+def load_pmc_traffic(fused):
+    """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC
+    summary (profiles/pmc_encode.json for the fused encoder, profiles/pmc_dct.json
+    for the two-kernel chain's DCT: FETCH_SIZE / WRITE_SIZE calibrated on kernels of
+    known traffic with the same access pattern, MI355X_MICROARCH.md HBM section)."""
+    p = os.path.join(HERE, "profiles", "pmc_encode.json" if fused else "pmc_dct.json")
     if not os.path.exists(p):
         return None
     with open(p) as f:
@@ -440,7 +481,7 @@ def main():
     if rank == 0:
         total_px = px_per_step_rank * world * args.steps
         value = total_px / elapsed / 1e6
-        pmc = load_pmc_traffic()
+        pmc = load_pmc_traffic(fused)
         cfg_idx = 2 if world == 1 else 3
         wl = ("%dx%d RGB -> YCrCb 4:2:0 full encode: colour+pyrDown, 8x8 DCT+quantize+zig-zag (3 planes), "
               "DC DPCM + AC RLE (3 planes)" % (W0, H0))
@@ -491,8 +532,7 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": pmc.get("hbm_bytes_per_launch") if (pmc and world == 1 and args.workload == "8k"
-                                                                and pmc.get("kernel_fused", False) == fused)
+                "traffic": pmc.get("hbm_bytes_per_launch") if (pmc and world == 1 and args.workload == "8k")
                 else None,
                 "algorithmic_bytes": roof_bytes,
                 "avg_launch_us": round(dct_us, 2),
@@ -501,7 +541,8 @@ def main():
             },
         }
         if not args.no_extras and world == 1:
-            out["extra_configs"] = {"4k_luma_dct": extra_4k_luma(), "16k_roundtrip": extra_16k_roundtrip()}
+            out["extra_configs"] = {"4k_luma_dct": extra_4k_luma(), "8k_plane_dct": extra_8k_plane_dct(),
+                                    "16k_roundtrip": extra_16k_roundtrip()}
         if extra_sharded is not None:
             out["extra_configs"] = {"16k_roundtrip": extra_sharded}
         if not args.no_cpu_baseline and world == 1:

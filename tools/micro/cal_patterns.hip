@@ -20,15 +20,28 @@ __device__ __forceinline__ void put(uint8_t *out, int64_t i16, u32x4 v) {
   __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(out) + i16);
 }
 
-// n = bytes read (multiple of 1536 * 64); writes n / 3 bytes
-__global__ __launch_bounds__(256) void k_cal_rgb24(const uint8_t *__restrict__ in, int64_t n, uint8_t *__restrict__ out) {
-  const int lane = threadIdx.x & 63;
-  const int64_t rows = n / 1536, nw = (int64_t)gridDim.x * 4;
-  for (int64_t r = blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += nw) {
-    const uint2 *p = reinterpret_cast<const uint2 *>(in + r * 1536 + 24 * lane);
+// k_encode420's geometry: an H x W RGB image (W % 512 == 0) in units of 16 rows x
+// 512 pixels, one wave per unit, lane l reading 24 B at 24 l of each of the unit's
+// rows (here without the pyrDown halo rows, so every byte is read once); writes a
+// sixth of the bytes read
+__global__ __launch_bounds__(256) void k_cal_rgb24(const uint8_t *__restrict__ in, int H, int W,
+                                                   uint8_t *__restrict__ out) {
+  const int lane = threadIdx.x & 63, ns = W / 512;
+  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= ns * (H / 16)) return;
+  const int u = g / ns, s = g - u * ns;
+  const int64_t pitch = (int64_t)W * 3;
+  uint32_t acc[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const uint2 *p = reinterpret_cast<const uint2 *>(in + (int64_t)(16 * u + r) * pitch + 1536 * s + 24 * lane);
     const uint2 a = p[0], b = p[1], c = p[2];
-    // 512 B written per 1536 B read: lanes 0..31 store 16 B each
-    if (lane < 32) put(out, r * 32 + lane, (u32x4){a.x ^ c.y, a.y, b.x, b.y ^ c.x});
+    acc[r & 3] ^= a.x ^ b.y;
+    acc[(r + 1) & 3] ^= a.y ^ c.x;
+    acc[(r + 2) & 3] ^= b.x ^ c.y;
+    if ((r & 3) == 3) {  // 16 B per lane per 4 rows = 1/6 of the 24 B x 4 read
+      put(out, ((int64_t)g * 4 + (r >> 2)) * 64 + lane, (u32x4){acc[0], acc[1], acc[2], acc[3]});
+    }
   }
 }
 
@@ -87,12 +100,13 @@ int main() {
   const int n = 12;
   const char *names[4] = {"k_cal_rgb24", "k_cal_blk8", "k_cal_q12", "k_cal_d16"};
   const double rd[4] = {(double)nrgb, (double)nplane, (double)nrgb, (double)nrgb};
-  const double wr[4] = {(double)nrgb / 3, 2.0 * nplane, (double)nrgb, (double)nrgb};
+  const double wr[4] = {(double)nrgb / 6, 2.0 * nplane, (double)nrgb, (double)nrgb};
   for (int k = 0; k < 4; ++k) {
     float tot = 0;
     for (int i = 0; i < n; ++i) {
       hipEventRecord(s);
-      if (k == 0) hipLaunchKernelGGL(k_cal_rgb24, grid, block, 0, 0, in[i % rot], nrgb, out[i % rot]);
+      if (k == 0)
+        hipLaunchKernelGGL(k_cal_rgb24, dim3((W / 512) * (H / 16) / 4), block, 0, 0, in[i % rot], H, W, out[i % rot]);
       if (k == 1) hipLaunchKernelGGL(k_cal_blk8, grid, block, 0, 0, in[i % rot], W, (int)(nplane / 64), out[i % rot]);
       if (k == 2) hipLaunchKernelGGL(k_cal_q12, grid, block, 0, 0, in[i % rot], nrgb, out[i % rot]);
       if (k == 3) hipLaunchKernelGGL(k_cal_d16, grid, block, 0, 0, in[i % rot], nrgb, out[i % rot]);

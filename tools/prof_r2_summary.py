@@ -20,6 +20,13 @@ def short(name):
     return m.group(1) if m else name[:40]
 
 
+def pattern_of(k):
+    for p, cal in PATTERN.items():
+        if k.startswith(p):
+            return cal
+    return "k_cal_d16"
+
+
 def per_kernel(path, counter):
     out = collections.defaultdict(list)
     with open(os.path.join(path, "run_counter_collection.csv")) as fh:
@@ -62,10 +69,10 @@ def main():
             continue
         e = dict(stats[k])
         if k in f:
-            cal = factors.get(PATTERN.get(k, "k_cal_d16"))
+            cal = factors.get(pattern_of(k))
             fb, wb = mean(f[k]) * 1024, mean(w[k]) * 1024
             e.update({"fetch_counter_bytes": round(fb), "write_counter_bytes": round(wb),
-                      "calibrated_with": PATTERN.get(k, "k_cal_d16")})
+                      "calibrated_with": pattern_of(k)})
             if cal:
                 e["read_bytes"] = round(fb / cal["fetch_counter_per_byte"])
                 e["write_bytes"] = round(wb / cal["write_counter_per_byte"])

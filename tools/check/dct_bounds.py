@@ -11,8 +11,10 @@ An integer combination below 2^24 (f32) / 2^53 (f64) is exact.  A constant c
 stored as K contributes |a| * |K - c|; |K - c| <= 1 ulp(c) is assumed for the
 pocketfft twiddles (they are not all correctly rounded), 1/2 ulp for ours.
 
-Three estimates of y/T are bounded (y = scipy.fftpack 2-D DCT-II of the centred
+Four estimates of y/T are bounded (y = scipy.fftpack 2-D DCT-II of the centred
 block, T the quantisation table entry):
+  E64[t][u][v] the float64 AAN fast path (dct_core.h dct_block_aan: the production
+               path of k_dct_planes and k_encode420)
   E1[t][u][v]  the float32 AAN fast path (dct_core.h dct_block_f32)
   E2[u][v]     the float64 separable dot product of the fallback (dct_coef_f64)
   EP[u][v]     pocketfft's own float64 result (the reference), vs the exact y
@@ -195,6 +197,52 @@ def E2():
     return out
 
 
+# ---- float64 AAN (dct_core.h aan_even / aan_odd / dct_block_aan, the production
+# fast path): integer prefix on raw bytes (exact), then float64 with separate
+# multiply and add where the source has them (z1, z3) and explicit fmas (z2, z4)
+A1d, A2d, A4d, A5d = A1, A2, A4, A5
+
+
+def aan64_even(x):
+    s0, s1, s2, s3 = x[0] + x[7], x[1] + x[6], x[2] + x[5], x[3] + x[4]
+    t10, t13, t11, t12 = s0 + s3, s0 - s3, s1 + s2, s1 - s2
+    z1 = (t12 + t13).mul(A1d)
+    return t10 + t11, t13 + z1, t10 - t11, t13 - z1  # outputs 0, 2, 4, 6
+
+
+def aan64_odd(x):
+    d7, d6, d5, d4 = x[0] - x[7], x[1] - x[6], x[2] - x[5], x[3] - x[4]
+    u10, u11, u12 = d4 + d5, d5 + d6, d6 + d7
+    z5 = (u10 - u12).mul(A5d)
+    z2, z4 = u10.fma(A2d, z5), u12.fma(A4d, z5)
+    z3 = u11.mul(A1d)
+    z11, z13 = d7 + z3, d7 - z3
+    return z11 + z4, z13 - z2, z13 + z2, z11 - z4  # outputs 1, 3, 5, 7
+
+
+def aan64(x):
+    e, o = aan64_even(x), aan64_odd(x)
+    return [e[0], o[0], e[1], o[1], e[2], o[2], e[3], o[3]]
+
+
+def E64():
+    """|b * kRA - y / T| of dct_block_aan for every (t, u, v) but (0,0) and (4,4)
+    (computed exactly there), b the AAN output, kRA = fl64(S_u S_v / T)."""
+    c = Ctx(2.0 ** -53, 2.0 ** 53, True, 2.0 ** -53)
+    px = pixels(c)
+    rows = [aan64(px[m]) for m in range(8)]
+    out = np.zeros((2, 8, 8))
+    for v in range(8):
+        col = aan64([rows[m][v] for m in range(8)])
+        for u in range(8):
+            n = col[u]
+            for t in range(2):
+                R = aan_scale(u) * aan_scale(v) / QT[t][8 * u + v]
+                dR = 2.0 ** -53 * R  # kRA correctly rounded
+                out[t, u, v] = (R + dR) * n.E + n.mag() * dR
+    return out
+
+
 def windows():
     e1, e2, ep = E1(), E2(), EP()
     W1 = np.zeros((2, 8, 8))
@@ -257,3 +305,16 @@ if __name__ == "__main__":
     print("log2 E2 (y):\n", np.log2(e2))
     print("log2 EP (y):\n", np.log2(ep))
     print("max W2 = 2^%.2f" % math.log2(W2.max()))
+    # the float64 fast path: qfast rounds b * kRA + 1/2 + 2^-30 to a multiple of 2^-32
+    # (2^-33 error) and flags a low word <= 6, so an unflagged value lies more than
+    # 2.5 * 2^-32 (above) / 4 * 2^-32 (below) from the next integer; its rint equals
+    # rint(fl(y_pf / T)) if the estimate's error + pocketfft's + the division's stays
+    # below that margin
+    e64 = E64()
+    for t in range(2):
+        T = np.array(QT[t], float).reshape(8, 8)
+        tot = e64[t] + ep / T + 2.0 ** -33 + 2.0 ** -41
+        tot[0, 0] = tot[4, 4] = 0.0  # exact paths
+        print("table", t, "float64 AAN: max |estimate - y_pf/T| + roundings = 2^%.2f  (margin 2.5 * 2^-32 = 2^%.2f)"
+              % (math.log2(tot.max()), math.log2(2.5 * 2.0 ** -32)))
+        assert tot.max() < 2.5 * 2.0 ** -32

@@ -7,7 +7,7 @@ namespace hic {
 static thread_local char g_last_error[512] = "";
 
 // hic_set_knob values (-1 = default; read by the launchers on every call)
-static int g_knobs[HIC_KNOB_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+static int g_knobs[HIC_KNOB_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 int knob(int k) {
   const int v = g_knobs[k];
   if (v >= 0) return v;

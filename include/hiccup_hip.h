@@ -75,7 +75,8 @@ int hic_device_count(int *h_n);
 #define HIC_KNOB_DEV 8              /* dev builds only (-DHIC_DEV): timing bits that skip work; refused otherwise */
 #define HIC_KNOB_ENCODE_WAVES 9     /* hic_encode420_u8: register budget for 2 (default) or 3 waves per SIMD */
 #define HIC_KNOB_ENCODE_NT 10       /* hic_encode420_u8: 1 = nontemporal coefficient stores (default 0: cached) */
-#define HIC_KNOB_COUNT 11
+#define HIC_KNOB_ENCODE_DCT 11      /* hic_encode420_u8: 1 = float32 AAN DCT with proven windows + in-place fallbacks (default 0: float64) */
+#define HIC_KNOB_COUNT 12
 int hic_set_knob(int knob, int value);
 int hic_get_knob(int knob, int *h_value);
 /* Synchronises `stream`; returns HIC_ERR_HIP if an earlier async launch failed. */

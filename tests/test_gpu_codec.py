@@ -334,9 +334,11 @@ def _structured_rgb(kind, H, W, seed):
     raise ValueError(kind)
 
 
+@pytest.mark.parametrize("variant", [{}, {"encode_dct": 1}, {"encode_waves": 3}, {"encode_dct": 1, "encode_waves": 3},
+                                     {"encode_nt": 1}])
 @pytest.mark.parametrize("kind", ["random", "levels", "colour_levels", "blocks", "flat"])
 @pytest.mark.parametrize("H,W", [(16, 512), (144, 2048), (1088, 1536)])
-def test_fused_encoder_matches_two_kernel_chain(kind, H, W):
+def test_fused_encoder_matches_two_kernel_chain(kind, H, W, variant):
     """hic_encode420_u8 (colour + pyrDown + DCT + tile records in one kernel, exact
     tie fallbacks in place) == the two-kernel chain (hic_rgb_to_ycrcb420 +
     hic_dct_quant_rle_u8_batch, deferred fallbacks), symbols and DC streams included
@@ -344,7 +346,8 @@ def test_fused_encoder_matches_two_kernel_chain(kind, H, W):
     rgb = _structured_rgb(kind, H, W, H + W)
     x = device.to_device(rgb)
     got, exp = pipeline.Encoder(H, W, fused=True), pipeline.Encoder(H, W, fused=False)
-    got.encode(x)
+    with _lib.knobs(**variant):  # every fused-kernel variant is bit-exact
+        got.encode(x)
     exp.encode(x)
     a, b = got.result(), exp.result()
     for k in pipeline.CHANNELS:

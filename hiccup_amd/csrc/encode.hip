@@ -91,6 +91,65 @@ __device__ __forceinline__ void enc_dct(uint2 (&w)[8], int16_t *st) {
   }
 }
 
+// Float32 AAN variant (knob "encode_dct" = 1): dct_block_f32 (dct_core.h) with the
+// proven float32 tie windows (dct_windows.h, tools/check/dct_bounds.py E1); a
+// flagged coefficient (~0.03 per block on random data) is resolved in place by
+// resolve_coef (float64 dot product, then pocketfft's own operations for the
+// rational classes), a coefficient that stays ambiguous sends the block to the
+// exact replica.  Out of line: the flagged lanes only.  Measured slower than the
+// float64 path (104-111 vs 65-72 us at 8K, profiles/r02/ab_fused_f32.log): the
+// out-of-line resolve costs more than the float32 arithmetic saves.
+template <int TABLE>
+__device__ __attribute__((noinline)) bool enc_resolve(uint2 w0, uint2 w1, uint2 w2, uint2 w3, uint2 w4, uint2 w5,
+                                                      uint2 w6, uint2 w7, uint32_t mlo, uint32_t mhi, int16_t *st) {
+  const uint2 w[8] = {w0, w1, w2, w3, w4, w5, w6, w7};
+  constexpr SlotOf<kZZ> kSlot{};
+  uint64_t m = ((uint64_t)mhi << 32) | mlo;
+  bool ok = true;
+  while (m) {
+    const int i = __builtin_ctzll(m);
+    m &= m - 1;
+    int q = 0;
+    if (resolve_coef(w, TABLE, i, q))
+      st[kSlot.s[i]] = (int16_t)q;
+    else
+      ok = false;
+  }
+  return ok;
+}
+
+template <int TABLE>
+__device__ __forceinline__ void enc_dct_f32(uint2 (&w)[8], int16_t *st) {
+  uint32_t mlo = 0, mhi = 0;
+  auto sink = [&](int v, const float (&rr)[8], const float (&d)[8], const bool (&f)[8]) {
+    (void)rr;
+    (void)d;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = u * 8 + v;
+      if (i < 32)
+        mlo |= (uint32_t)f[u] << i;
+      else
+        mhi |= (uint32_t)f[u] << (i - 32);
+    }
+  };
+  dct_block_f32<TABLE, kZZ>(w, st, sink);
+  const bool has = (mlo | mhi) != 0;
+  if (__builtin_amdgcn_ballot_w64(has)) {
+    bool ok = true;
+    if (has) ok = enc_resolve<TABLE>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], mlo, mhi, st);
+    if (__builtin_amdgcn_ballot_w64(!ok)) enc_exact_block<TABLE>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], st);
+  }
+}
+
+template <int TABLE, bool F32>
+__device__ __forceinline__ void enc_dct_any(uint2 (&w)[8], int16_t *st) {
+  if (F32)
+    enc_dct_f32<TABLE>(w, st);
+  else
+    enc_dct<TABLE>(w, st);
+}
+
 // 16 B chunk k of stage row b
 __device__ __forceinline__ uint4 enc_st16(const uint2 *st2, int b, int k) {
   const uint2 lo = st2[b * kStageU2 + 2 * k], hi = st2[b * kStageU2 + 2 * k + 1];
@@ -236,7 +295,7 @@ __device__ __forceinline__ void enc_colour(const Enc420 &E, int y0, int s, int l
   }
 }
 
-template <int TMF, bool NT>
+template <int TMF, bool NT, bool F32>
 __device__ __forceinline__ void encode420_unit(const Enc420 &E);
 
 // Two register budgets (knob "encode_waves", A/B): 2 waves per SIMD (default: up
@@ -245,16 +304,17 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E);
 // NT: nontemporal coefficient stores (knob "encode_nt" = 1).  Default 0: plain
 // stores, so part of the coefficients is still in the Infinity Cache when the RLE
 // emit re-reads them (emit 59.7 -> 54.7 us; 8K encode +2-4 %, scripts/gpu_r2i.sh)
-template <int TMF, bool NT>
+// F32: the float32 DCT variant (knob "encode_dct" = 1, enc_dct_f32)
+template <int TMF, bool NT, bool F32>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_encode420(Enc420 E) {
-  encode420_unit<TMF, NT>(E);
+  encode420_unit<TMF, NT, F32>(E);
 }
-template <int TMF, bool NT>
+template <int TMF, bool NT, bool F32>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_encode420_w2(Enc420 E) {
-  encode420_unit<TMF, NT>(E);
+  encode420_unit<TMF, NT, F32>(E);
 }
 
-template <int TMF, bool NT>
+template <int TMF, bool NT, bool F32>
 __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
   __shared__ uint2 s_stage[4 * 64 * kStageU2];
   __shared__ uint32_t s_chroma_all[4][2 * 8 * 64];
@@ -286,7 +346,7 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
     uint2 w[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) w[r] = yq[8 * br + r];
-    enc_dct<0>(w, st);
+    enc_dct_any<0, F32>(w, st);
     __builtin_amdgcn_wave_barrier();
     const int64_t b0 = (int64_t)(2 * u + br) * nbx + 64 * s;
     int16_t *o = E.coef[0] + b0 * 64;
@@ -308,7 +368,7 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
     uint2 w[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = sc[i * 32];
-    enc_dct<1>(w, st);
+    enc_dct_any<1, F32>(w, st);
     __builtin_amdgcn_wave_barrier();
     const int64_t b0 = (int64_t)u * nbxc + 32 * s;
     enc_store<NT>(st2, lane, E.coef[1] + b0 * 64, E.coef[2] + b0 * 64);
@@ -373,16 +433,20 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
       hipLaunchKernelGGL(kern, grid, block, 0, s, E);
   };
   const bool w2 = knob(HIC_KNOB_ENCODE_WAVES) == 2, nt = knob(HIC_KNOB_ENCODE_NT) != 0;
+  const bool f32 = knob(HIC_KNOB_ENCODE_DCT) == 1;
+  // variants: {2, 3} waves per SIMD x {float64, float32} DCT x {cached, nontemporal}
+  // stores (the last at 2 waves and float64 only) x {max_len 15, any}
+#define HIC_ENC_VARIANTS(M)                                                 \
+  if (nt && w2 && !f32) launch(k_encode420_w2<M, true, false>);             \
+  else if (w2 && f32) launch(k_encode420_w2<M, false, true>);               \
+  else if (w2) launch(k_encode420_w2<M, false, false>);                     \
+  else if (f32) launch(k_encode420<M, false, true>);                        \
+  else launch(k_encode420<M, false, false>)
   if (max_len == 15) {
-    if (nt)
-      w2 ? launch(k_encode420_w2<15, true>) : launch(k_encode420<15, true>);
-    else
-      w2 ? launch(k_encode420_w2<15, false>) : launch(k_encode420<15, false>);
+    HIC_ENC_VARIANTS(15);
   } else {
-    if (nt)
-      w2 ? launch(k_encode420_w2<0, true>) : launch(k_encode420<0, true>);
-    else
-      w2 ? launch(k_encode420_w2<0, false>) : launch(k_encode420<0, false>);
+    HIC_ENC_VARIANTS(0);
   }
+#undef HIC_ENC_VARIANTS
   return check_launch("k_encode420");
 }

@@ -470,6 +470,28 @@ def main():
     roof_bytes = dct_px * 2 + (px_per_step_rank * 3 if fused else dct_px)
     achieved = roof_bytes / (dct_us * 1e-6) / 1e9
 
+    # context for the gathered strong-scaling line: the same steps with the stream
+    # left distributed (no gather), timed the same way -- the sharded encode itself
+    # scales; the gather into rank 0 is bound by rank 0's xGMI links
+    no_gather = None
+    if gather:
+        dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for i in range(args.steps):
+            with torch.cuda.stream(streams[i % len(streams)]):
+                encs[i % len(encs)].encode(inputs[i % nin])
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t = torch.tensor([time.perf_counter() - t1], dtype=torch.float64,
+                         device="cuda" if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ng = float(t.item())
+        no_gather = {"value": round(px_per_step_rank * world * args.steps / ng / 1e6, 2),
+                     "ms_per_step": round(ng / args.steps * 1e3, 4),
+                     "note": "same sharded encode and steps with the stream left distributed on the ranks "
+                             "(no gather); not the headline value"}
     per_rank_rows = in_rows if world == 1 else encs[0].rows[1] - encs[0].rows[0]
     extra_sharded = None
     if world > 1 and not args.no_extras:
@@ -514,6 +536,7 @@ def main():
                 "streams": args.streams,
                 "gather_to_rank0": gather,
                 "gather_us_per_step": None if gather_us is None else round(gather_us, 2),
+                "without_gather": no_gather,
                 "symbols_per_image_rank0": symbols,
                 "dist_backend": None if world == 1 else args.dist_backend + (" (same device)" if args.same_device
                                                                               else ""),

@@ -183,59 +183,139 @@ __device__ __forceinline__ void enc_stage_row(const uint2 *st2, int lane, uint32
 
 // Packed 16-bit helpers: both chroma planes in one dword (Cr low half, Cb high
 // half); pyrDown's sums stay below 2^16 (horizontal <= 16 * 255, vertical + 128 <=
-// 65408), so v_pk_*_u16 does both planes at once.
+// 65408), so v_pk_*_u16 does both planes at once.  The multipliers arrive as
+// opaque registers (opq): a literal 4 is strength-reduced to a shift + an add.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pk_add16(uint32_t a, uint32_t b) {
-  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-  const u16x2 r = __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b);
-  return __builtin_bit_cast(uint32_t, r);
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
 }
-__device__ __forceinline__ uint32_t pk_mad16(uint32_t a, unsigned short k, uint32_t c) {  // a * k + c per half
-  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-  const u16x2 r = __builtin_bit_cast(u16x2, a) * (u16x2){k, k} + __builtin_bit_cast(u16x2, c);
-  return __builtin_bit_cast(uint32_t, r);
+__device__ __forceinline__ uint32_t pk_mad16(uint32_t a, uint32_t k, uint32_t c) {  // a * k + c per half
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) * __builtin_bit_cast(u16x2, k) +
+                                          __builtin_bit_cast(u16x2, c));
 }
-__device__ __forceinline__ uint32_t pk_shr8(uint32_t a) {
-  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-  const u16x2 r = __builtin_bit_cast(u16x2, a) >> (u16x2){8, 8};
-  return __builtin_bit_cast(uint32_t, r);
+__device__ __forceinline__ uint32_t opq(uint32_t k) {
+  asm volatile("" : "+s"(k));
+  return k;
 }
-// [1 4 6 4 1] over five packed taps
-__device__ __forceinline__ uint32_t pk_taps5(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e) {
-  return pk_mad16(c, 6, pk_mad16(pk_add16(b, d), 4, pk_add16(a, e)));
+// [1 4 6 4 1] over five packed taps (k4 = 4 | 4 << 16, k6 = 6 | 6 << 16)
+__device__ __forceinline__ uint32_t pk_taps5(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e, uint32_t k4,
+                                             uint32_t k6) {
+  return pk_mad16(c, k6, pk_mad16(pk_add16(b, d), k4, pk_add16(a, e)));
+}
+
+// cvtColor RGB2YCrCb of the 8 pixels in 24 RGB bytes wd[0..5]: color_core.h's
+// rgb2ycc restated for the dot-product unit (equal on all 2^24 inputs,
+// tools/check/colour_dot4.py):
+//   4 (4899 r + 9617 g + 1868 b) + 2^15 = 256 (rgb . HI) + (rgb . LO) + 2^15, HI / LO
+//   the high / low bytes of the 4x coefficients: two v_dot4_u32_u8, the second
+//   accumulating the first >> 8, leave y = descale14(4899 r + ...) in byte 1 (Yh);
+//   Cr = sat8(descale14((r - y) 11682 + 2^21)) is byte 2 of
+//   clamp((r - y) 46728 + 4 (2^21 + 2^13), 0, 2^24 - 1), likewise Cb, and one
+//   v_perm packs Cr | Cb << 16 (c).
+// Pixel k's bytes start at 3k: pixels 0, 4 (byte 0 of a dword) and 3, 7 (byte 1)
+// are read in place, pixels 1, 2, 5, 6 through v_alignbyte.
+constexpr uint32_t kYLo = 140u | 68u << 8 | 48u << 16, kYHi = 76u | 150u << 8 | 29u << 16;
+constexpr int kCr4 = 4 * kYCRI, kCb4 = 4 * kYCBI, kCC4 = 4 * ((128 << 14) + (1 << 13));
+struct YccK {  // dot4 weights in SGPRs (VOP3P takes no literals), addends in VGPRs
+  uint32_t lo0, lo1, hi0, hi1, acc, cc4;
+};
+// Stage by stage over the 8 pixels (a v_dot4 result read by the next instruction
+// costs wait states: independent pixels fill them)
+__device__ __forceinline__ void ycc8(const uint32_t (&wd)[6], const YccK &K, uint32_t (&Yh)[8], uint32_t (&c)[8]) {
+  uint32_t x[8], L[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int q = k & 3, d0 = (k >> 2) * 3;
+    x[k] = q == 0 ? wd[d0]
+           : q == 1 ? __builtin_amdgcn_alignbyte(wd[d0 + 1], wd[d0], 3)
+           : q == 2 ? __builtin_amdgcn_alignbyte(wd[d0 + 2], wd[d0 + 1], 2)
+                    : wd[d0 + 2];
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) L[k] = __builtin_amdgcn_udot4(x[k], (k & 3) == 3 ? K.lo1 : K.lo0, K.acc, false);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) Yh[k] = __builtin_amdgcn_udot4(x[k], (k & 3) == 3 ? K.hi1 : K.hi0, L[k] >> 8, false);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int sh = (k & 3) == 3 ? 8 : 0;
+    const int y = (int)((Yh[k] >> 8) & 255u);
+    const int r = (int)((x[k] >> sh) & 255u), b = (int)((x[k] >> (sh + 16)) & 255u);
+    // opaque addend: a literal one is split off into a v_add after the clamp
+    int vr = (r - y) * kCr4 + (int)K.cc4, vb = (b - y) * kCb4 + (int)K.cc4;
+    vr = vr < 0 ? 0 : (vr > 0xFFFFFF ? 0xFFFFFF : vr);
+    vb = vb < 0 ? 0 : (vb > 0xFFFFFF ? 0xFFFFFF : vb);
+    c[k] = __builtin_amdgcn_perm((uint32_t)vb, (uint32_t)vr, 0x07060302u);
+  }
+}
+// bytes 1 of Yh[k0 .. k0 + 3] -> one dword of four Y bytes
+__device__ __forceinline__ uint32_t ypack4(const uint32_t (&Yh)[8], int k0) {
+  const uint32_t lo = __builtin_amdgcn_perm(Yh[k0 + 1], Yh[k0], 0x0C0C0501u);
+  const uint32_t hi = __builtin_amdgcn_perm(Yh[k0 + 3], Yh[k0 + 2], 0x0C0C0501u);
+  return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+}
+
+__device__ __forceinline__ uint32_t opv(uint32_t k) {  // a constant held in a VGPR
+  asm volatile("" : "+v"(k));
+  return k;
+}
+// v's value in lane L replaced by s (v_writelane_b32: no builtin in this compiler)
+template <int L>
+__device__ __forceinline__ uint32_t set_lane(uint32_t v, int s) {
+  asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(s), "n"(L));
+  return v;
+}
+// wave shifts for the horizontal taps (the edge lane is overwritten by v_writelane)
+__device__ __forceinline__ uint32_t wshr1(uint32_t v) {  // lane i <- lane i - 1
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t wshl1(uint32_t v) {  // lane i <- lane i + 1
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xF, 0xF, true);
 }
 
 // Colour stage of one unit (image rows y0 .. y0 + 15 of strip s): Y rows -> yq,
 // pyrDown'd chroma rows (4 columns per lane, packed bytes) -> the wave's LDS chroma
 // area s_chroma[plane][row][lane] (so chroma block m's row i is the 8 bytes at
-// s_chroma[plane][i][2m]).
+// s_chroma[plane][i][2m]).  Row r's 24 B per lane come from a buffer load whose
+// row offset is a scalar (no per-row address arithmetic on the vector unit); the
+// strip-edge pixels (the neighbour strips', or reflect-101's at the image border)
+// are converted once up front and written into lane 0 / 63 with v_writelane.
 __device__ __forceinline__ void enc_colour(const Enc420 &E, int y0, int s, int lane, uint2 (&yq)[16],
                                            uint32_t *s_chroma) {
-  const int W = E.W, H = E.H;
+  const int W = E.W, H = E.H, pitch = 3 * W;
   const int in_row1 = E.in_row0 + E.in_rows;
-  const int xs = 512 * s, x0 = xs + 8 * lane;
-  auto src_row = [&](int rr) {  // rr: row relative to y0 (-2 .. 16)
-    int sy = refl101(y0 + rr, H);
+  const int xs = 512 * s;
+  // byte offset of image row y0 + rr (rr in -2 .. 16) in the input rows, computed
+  // by lane rr + 2 (read back per row by v_readlane): one reflect-101 step
+  // suffices (y0 + 16 <= H, H >= 16), then the shard's clamp
+  int roff = 0;
+  {
+    int sy = y0 + lane - 2;
+    sy = sy < 0 ? -sy : (sy >= H ? 2 * H - 2 - sy : sy);
     sy = sy < E.in_row0 ? E.in_row0 : (sy >= in_row1 ? in_row1 - 1 : sy);
-    return E.rgb + (int64_t)(sy - E.in_row0) * W * 3;
-  };
-  // the strip's edge pixels, packed (cr | cb << 16): lane r converts row r - 2's
-  // x = xs - 2, xs - 1 (left neighbour strip) and x = xs + 512 (right one)
+    roff = (sy - E.in_row0) * pitch;
+  }
+  // edge pixels, packed (cr | cb << 16): lane r converts row r - 2's x = xs - 2,
+  // xs - 1 (or 2, 1 at the left border) and x = xs + 512 (or W - 2 at the right)
   uint32_t hal_l2 = 0, hal_l1 = 0, hal_r = 0;
   if (lane < 19) {
-    const uint8_t *row = src_row(lane - 2);
-    if (xs >= 2) {
-      const uint8_t *p = row + 3 * (xs - 2);
-      const YCC a = rgb2ycc(p[0], p[1], p[2]), b = rgb2ycc(p[3], p[4], p[5]);
-      hal_l2 = a.cr | a.cb << 16;
-      hal_l1 = b.cr | b.cb << 16;
-    }
-    if (xs + 512 < W) {
-      const uint8_t *p = row + 3 * (xs + 512);
-      const YCC c = rgb2ycc(p[0], p[1], p[2]);
-      hal_r = c.cr | c.cb << 16;
-    }
+    const uint8_t *row = E.rgb + roff;
+    const int xl = xs >= 2 ? xs - 2 : 2, xl1 = xs >= 2 ? xs - 1 : 1, xr = xs + 512 < W ? xs + 512 : W - 2;
+    const YCC a = rgb2ycc(row[3 * xl], row[3 * xl + 1], row[3 * xl + 2]);
+    const YCC b = rgb2ycc(row[3 * xl1], row[3 * xl1 + 1], row[3 * xl1 + 2]);
+    const YCC c = rgb2ycc(row[3 * xr], row[3 * xr + 1], row[3 * xr + 2]);
+    hal_l2 = a.cr | a.cb << 16;
+    hal_l1 = b.cr | b.cb << 16;
+    hal_r = c.cr | c.cb << 16;
   }
-  const bool left_border = s == 0, right_border = xs + 512 >= W;
+  const uint64_t base = reinterpret_cast<uint64_t>(E.rgb) + 3 * xs;
+  const uint32_t base_lo = __builtin_amdgcn_readfirstlane((uint32_t)base),
+                 base_hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void *>((uint64_t)base_hi << 32 | base_lo), 0,
+      __builtin_amdgcn_readfirstlane(E.in_rows * pitch - 3 * xs), 0x00020000);
+  const int voff = 24 * lane;
+  const YccK K{opq(kYLo), opq(kYLo << 8), opq(kYHi), opq(kYHi << 8), opv(32768u), opv((uint32_t)kCC4)};
+  const uint32_t k4 = opq(0x00040004u), k6 = opq(0x00060006u), k128 = opq(0x00800080u);
   uint32_t h[19][4];  // horizontal pyrDown sums of input row r, chroma column j (packed)
   // rows stream through a ring of kLA + 1 loads in flight (sched_barrier keeps the
   // compiler from hoisting all 19 rows' loads: 114 VGPRs)
@@ -243,51 +323,43 @@ __device__ __forceinline__ void enc_colour(const Enc420 &E, int y0, int s, int l
 #define HIC_ENC_LA 6
 #endif
   constexpr int kLA = HIC_ENC_LA;
-  uint2 ring[kLA + 1][3];
-  auto load_row = [&](int r, uint2 (&d)[3]) {
-    const uint2 *p = reinterpret_cast<const uint2 *>(src_row(r - 2) + 3 * x0);
-    d[0] = p[0];
-    d[1] = p[1];
-    d[2] = p[2];
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  u32x4 ring_a[kLA + 1];
+  u32x2 ring_b[kLA + 1];
+  auto load_row = [&](int r, int slot) {
+    const int so = __builtin_amdgcn_readlane(roff, r);
+    ring_a[slot] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, so, 0);
+    ring_b[slot] = __builtin_amdgcn_raw_buffer_load_b64(rsrc, voff + 16, so, 0);
   };
 #pragma unroll
-  for (int r = 0; r < kLA; ++r) load_row(r, ring[r]);
+  for (int r = 0; r < kLA; ++r) load_row(r, r);
 #pragma unroll
   for (int r = 0; r < 19; ++r) {
-    if (r + kLA < 19) load_row(r + kLA, ring[(r + kLA) % (kLA + 1)]);
-    const uint2 q0 = ring[r % (kLA + 1)][0], q1 = ring[r % (kLA + 1)][1], q2 = ring[r % (kLA + 1)][2];
-    const uint32_t wd[6] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y};
-    auto byte = [&](int i) { return (int)((wd[i >> 2] >> (8 * (i & 3))) & 255u); };
-    uint32_t c[8], y[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const YCC v = rgb2ycc(byte(3 * k), byte(3 * k + 1), byte(3 * k + 2));
-      y[k] = v.y;
-      c[k] = v.cr | v.cb << 16;
-    }
-    if (r >= 2 && r < 18) yq[r - 2] = make_uint2(pack4(y[0], y[1], y[2], y[3]), pack4(y[4], y[5], y[6], y[7]));
+    if (r + kLA < 19) load_row(r + kLA, (r + kLA) % (kLA + 1));
+    const u32x4 qa = ring_a[r % (kLA + 1)];
+    const u32x2 qb = ring_b[r % (kLA + 1)];
+    const uint32_t wd[6] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y};
+    uint32_t Yh[8], c[8];
+    ycc8(wd, K, Yh, c);
+    if (r >= 2 && r < 18) yq[r - 2] = make_uint2(ypack4(Yh, 0), ypack4(Yh, 4));
     // neighbour pixels x0 - 2, x0 - 1 (left lane) and x0 + 8 (right lane)
-    uint32_t l2 = shr1(c[6]), l1 = shr1(c[7]), r0 = shl1(c[0]);
-    if (lane == 0) {  // reflect-101 at the image's left border: x = -2, -1 -> 2, 1
-      l2 = left_border ? c[2] : (uint32_t)__builtin_amdgcn_readlane((int)hal_l2, r);
-      l1 = left_border ? c[1] : (uint32_t)__builtin_amdgcn_readlane((int)hal_l1, r);
-    }
-    if (lane == 63)  // right border: x = W -> W - 2
-      r0 = right_border ? c[6] : (uint32_t)__builtin_amdgcn_readlane((int)hal_r, r);
-    h[r][0] = pk_taps5(l2, l1, c[0], c[1], c[2]);
-    h[r][1] = pk_taps5(c[0], c[1], c[2], c[3], c[4]);
-    h[r][2] = pk_taps5(c[2], c[3], c[4], c[5], c[6]);
-    h[r][3] = pk_taps5(c[4], c[5], c[6], c[7], r0);
+    const uint32_t l2 = set_lane<0>(wshr1(c[6]), __builtin_amdgcn_readlane((int)hal_l2, r));
+    const uint32_t l1 = set_lane<0>(wshr1(c[7]), __builtin_amdgcn_readlane((int)hal_l1, r));
+    const uint32_t r0 = set_lane<63>(wshl1(c[0]), __builtin_amdgcn_readlane((int)hal_r, r));
+    h[r][0] = pk_taps5(l2, l1, c[0], c[1], c[2], k4, k6);
+    h[r][1] = pk_taps5(c[0], c[1], c[2], c[3], c[4], k4, k6);
+    h[r][2] = pk_taps5(c[2], c[3], c[4], c[5], c[6], k4, k6);
+    h[r][3] = pk_taps5(c[4], c[5], c[6], c[7], r0, k4, k6);
     if (r >= 4 && r % 2 == 0) {  // chroma row i = r / 2 - 2 has all five input rows
       const int a = r - 4, i = r / 2 - 2;
       uint32_t v[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)  // (sum + 128) >> 8 <= 255: no saturation needed
-        v[j] = pk_shr8(pk_add16(pk_taps5(h[a][j], h[a + 1][j], h[a + 2][j], h[a + 3][j], h[a + 4][j]),
-                                0x00800080u));
-      // bytes: x01 = (cr0, cr1, cb0, cb1), x23 = (cr2, cr3, cb2, cb3)
-      const uint32_t x01 = __builtin_amdgcn_perm(v[1], v[0], 0x06020400u);
-      const uint32_t x23 = __builtin_amdgcn_perm(v[3], v[2], 0x06020400u);
+      for (int j = 0; j < 4; ++j)  // sum + 128 < 2^16: (sum + 128) >> 8 is the high byte
+        v[j] = pk_add16(pk_taps5(h[a][j], h[a + 1][j], h[a + 2][j], h[a + 3][j], h[a + 4][j], k4, k6), k128);
+      // high bytes: x01 = (cr0, cr1, cb0, cb1), x23 = (cr2, cr3, cb2, cb3)
+      const uint32_t x01 = __builtin_amdgcn_perm(v[1], v[0], 0x07030501u);
+      const uint32_t x23 = __builtin_amdgcn_perm(v[3], v[2], 0x07030501u);
       s_chroma[i * 64 + lane] = __builtin_amdgcn_perm(x23, x01, 0x05040100u);
       s_chroma[512 + i * 64 + lane] = __builtin_amdgcn_perm(x23, x01, 0x07060302u);
     }
@@ -324,7 +396,7 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
   uint2 *st2 = s_stage + wv * 64 * kStageU2;
   uint32_t *s_chroma = s_chroma_all[wv];
   int16_t *st = reinterpret_cast<int16_t *>(st2 + lane * kStageU2);
-  const int u = g / E.nstrips, s = g - u * E.nstrips;
+  const int u = __builtin_amdgcn_readfirstlane(g / E.nstrips), s = __builtin_amdgcn_readfirstlane(g - u * E.nstrips);
   const int y0 = E.out_row0 + 16 * u;
   const int nbx = E.W >> 3, nbxc = E.W >> 4;
 
@@ -398,6 +470,8 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
   const int64_t need1 = out_row0 + out_rows + 1 < H ? out_row0 + out_rows + 1 : H;
   if (in_row0 > need0 || in_row0 + in_rows < need1) return arg_error("input rows do not cover the pyrDown halo");
   if (reinterpret_cast<uintptr_t>(rgb_rows) % 8) return arg_error("rgb must be 8-byte aligned");
+  // the RGB rows are read through a buffer resource with 32-bit offsets
+  if (in_rows * W * 3 > INT32_MAX) return arg_error("hic_encode420_u8: input rows exceed 2 GiB (use the unfused chain)");
   if ((reinterpret_cast<uintptr_t>(coef_y) | reinterpret_cast<uintptr_t>(coef_cr) |
        reinterpret_cast<uintptr_t>(coef_cb)) % 16)
     return arg_error("coefficient buffers must be 16-byte aligned");

@@ -217,3 +217,14 @@ def test_container_refuses_foreign_pickles():
     evil = pickle.dumps({"type": os.system, "data": []})
     with pytest.raises(pickle.UnpicklingError):
         hicimage.PayloadStringP.from_bytes(evil)
+
+
+def test_fused_colour_arithmetic_exhaustive():
+    """encode.hip's dot4 restatement of RGB2YCrCb equals the oracle on all 2^24
+    RGB triples (tools/check/colour_dot4.py)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "colour_dot4", os.path.join(os.path.dirname(__file__), "..", "tools", "check", "colour_dot4.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    assert mod.check()

@@ -272,100 +272,119 @@ __device__ __forceinline__ uint32_t wshl1(uint32_t v) {  // lane i <- lane i + 1
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xF, 0xF, true);
 }
 
-// Colour stage of one unit (image rows y0 .. y0 + 15 of strip s): Y rows -> yq,
-// pyrDown'd chroma rows (4 columns per lane, packed bytes) -> the wave's LDS chroma
-// area s_chroma[plane][row][lane] (so chroma block m's row i is the 8 bytes at
-// s_chroma[plane][i][2m]).  Row r's 24 B per lane come from a buffer load whose
-// row offset is a scalar (no per-row address arithmetic on the vector unit); the
-// strip-edge pixels (the neighbour strips', or reflect-101's at the image border)
-// are converted once up front and written into lane 0 / 63 with v_writelane.
-__device__ __forceinline__ void enc_colour(const Enc420 &E, int y0, int s, int lane, uint2 (&yq)[16],
-                                           uint32_t *s_chroma) {
-  const int W = E.W, H = E.H, pitch = 3 * W;
-  const int in_row1 = E.in_row0 + E.in_rows;
-  const int xs = 512 * s;
-  // byte offset of image row y0 + rr (rr in -2 .. 16) in the input rows, computed
-  // by lane rr + 2 (read back per row by v_readlane): one reflect-101 step
-  // suffices (y0 + 16 <= H, H >= 16), then the shard's clamp
-  int roff = 0;
-  {
-    int sy = y0 + lane - 2;
-    sy = sy < 0 ? -sy : (sy >= H ? 2 * H - 2 - sy : sy);
-    sy = sy < E.in_row0 ? E.in_row0 : (sy >= in_row1 ? in_row1 - 1 : sy);
-    roff = (sy - E.in_row0) * pitch;
-  }
-  // edge pixels, packed (cr | cb << 16): lane r converts row r - 2's x = xs - 2,
-  // xs - 1 (or 2, 1 at the left border) and x = xs + 512 (or W - 2 at the right)
-  uint32_t hal_l2 = 0, hal_l1 = 0, hal_r = 0;
-  if (lane < 19) {
-    const uint8_t *row = E.rgb + roff;
-    const int xl = xs >= 2 ? xs - 2 : 2, xl1 = xs >= 2 ? xs - 1 : 1, xr = xs + 512 < W ? xs + 512 : W - 2;
-    const YCC a = rgb2ycc(row[3 * xl], row[3 * xl + 1], row[3 * xl + 2]);
-    const YCC b = rgb2ycc(row[3 * xl1], row[3 * xl1 + 1], row[3 * xl1 + 2]);
-    const YCC c = rgb2ycc(row[3 * xr], row[3 * xr + 1], row[3 * xr + 2]);
-    hal_l2 = a.cr | a.cb << 16;
-    hal_l1 = b.cr | b.cb << 16;
-    hal_r = c.cr | c.cb << 16;
-  }
-  const uint64_t base = reinterpret_cast<uint64_t>(E.rgb) + 3 * xs;
-  const uint32_t base_lo = __builtin_amdgcn_readfirstlane((uint32_t)base),
-                 base_hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<void *>((uint64_t)base_hi << 32 | base_lo), 0,
-      __builtin_amdgcn_readfirstlane(E.in_rows * pitch - 3 * xs), 0x00020000);
-  const int voff = 24 * lane;
-  const YccK K{opq(kYLo), opq(kYLo << 8), opq(kYHi), opq(kYHi << 8), opv(32768u), opv((uint32_t)kCC4)};
-  const uint32_t k4 = opq(0x00040004u), k6 = opq(0x00060006u), k128 = opq(0x00800080u);
-  uint32_t h[19][4];  // horizontal pyrDown sums of input row r, chroma column j (packed)
-  // rows stream through a ring of kLA + 1 loads in flight (sched_barrier keeps the
-  // compiler from hoisting all 19 rows' loads: 114 VGPRs)
+// Colour stage of one unit (image rows y0 .. y0 + 15 of strip s), run in two row
+// ranges around the DCT of Y block row 0 (rows() below): Y rows -> yq, pyrDown'd
+// chroma rows (4 columns per lane, packed bytes) -> the wave's LDS chroma area
+// s_chroma[plane][row][lane] (so chroma block m's row i is the 8 bytes at
+// s_chroma[plane][i][2m]).  Input row r (image row y0 + r - 2) arrives by a buffer
+// load whose row offset is a scalar (no per-row address arithmetic on the vector
+// unit); the strip-edge pixels (the neighbour strips', or reflect-101's at the
+// image border) are converted once up front and written into lane 0 / 63 by
+// v_writelane.
 #ifndef HIC_ENC_LA
 #define HIC_ENC_LA 6
 #endif
-  constexpr int kLA = HIC_ENC_LA;
+struct EncColour {
+  // rows stream through a ring of kLA + 1 loads in flight (sched_barrier keeps the
+  // compiler from hoisting all 19 rows' loads: 114 VGPRs)
+  static constexpr int kLA = HIC_ENC_LA;
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  int lane, roff, voff;
+  uint32_t hal_l2, hal_l1, hal_r;
+  __amdgpu_buffer_rsrc_t rsrc;
+  YccK K;
+  uint32_t k4, k6, k128;
   u32x4 ring_a[kLA + 1];
   u32x2 ring_b[kLA + 1];
-  auto load_row = [&](int r, int slot) {
+  uint32_t h[19][4];  // horizontal pyrDown sums of input row r, chroma column j (packed)
+
+#ifndef HIC_ENC_LOAD_AUX
+#define HIC_ENC_LOAD_AUX 0
+#endif
+  __device__ __forceinline__ void load_row(int r) {
     const int so = __builtin_amdgcn_readlane(roff, r);
-    ring_a[slot] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, so, 0);
-    ring_b[slot] = __builtin_amdgcn_raw_buffer_load_b64(rsrc, voff + 16, so, 0);
-  };
-#pragma unroll
-  for (int r = 0; r < kLA; ++r) load_row(r, r);
-#pragma unroll
-  for (int r = 0; r < 19; ++r) {
-    if (r + kLA < 19) load_row(r + kLA, (r + kLA) % (kLA + 1));
-    const u32x4 qa = ring_a[r % (kLA + 1)];
-    const u32x2 qb = ring_b[r % (kLA + 1)];
-    const uint32_t wd[6] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y};
-    uint32_t Yh[8], c[8];
-    ycc8(wd, K, Yh, c);
-    if (r >= 2 && r < 18) yq[r - 2] = make_uint2(ypack4(Yh, 0), ypack4(Yh, 4));
-    // neighbour pixels x0 - 2, x0 - 1 (left lane) and x0 + 8 (right lane)
-    const uint32_t l2 = set_lane<0>(wshr1(c[6]), __builtin_amdgcn_readlane((int)hal_l2, r));
-    const uint32_t l1 = set_lane<0>(wshr1(c[7]), __builtin_amdgcn_readlane((int)hal_l1, r));
-    const uint32_t r0 = set_lane<63>(wshl1(c[0]), __builtin_amdgcn_readlane((int)hal_r, r));
-    h[r][0] = pk_taps5(l2, l1, c[0], c[1], c[2], k4, k6);
-    h[r][1] = pk_taps5(c[0], c[1], c[2], c[3], c[4], k4, k6);
-    h[r][2] = pk_taps5(c[2], c[3], c[4], c[5], c[6], k4, k6);
-    h[r][3] = pk_taps5(c[4], c[5], c[6], c[7], r0, k4, k6);
-    if (r >= 4 && r % 2 == 0) {  // chroma row i = r / 2 - 2 has all five input rows
-      const int a = r - 4, i = r / 2 - 2;
-      uint32_t v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)  // sum + 128 < 2^16: (sum + 128) >> 8 is the high byte
-        v[j] = pk_add16(pk_taps5(h[a][j], h[a + 1][j], h[a + 2][j], h[a + 3][j], h[a + 4][j], k4, k6), k128);
-      // high bytes: x01 = (cr0, cr1, cb0, cb1), x23 = (cr2, cr3, cb2, cb3)
-      const uint32_t x01 = __builtin_amdgcn_perm(v[1], v[0], 0x07030501u);
-      const uint32_t x23 = __builtin_amdgcn_perm(v[3], v[2], 0x07030501u);
-      s_chroma[i * 64 + lane] = __builtin_amdgcn_perm(x23, x01, 0x05040100u);
-      s_chroma[512 + i * 64 + lane] = __builtin_amdgcn_perm(x23, x01, 0x07060302u);
-    }
-    __builtin_amdgcn_sched_barrier(0);
+    ring_a[r % (kLA + 1)] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, so, HIC_ENC_LOAD_AUX);
+    ring_b[r % (kLA + 1)] = __builtin_amdgcn_raw_buffer_load_b64(rsrc, voff + 16, so, HIC_ENC_LOAD_AUX);
   }
-}
+
+  __device__ __forceinline__ void init(const Enc420 &E, int y0, int s, int lane_) {
+    lane = lane_;
+    const int W = E.W, H = E.H, pitch = 3 * W;
+    const int in_row1 = E.in_row0 + E.in_rows;
+    const int xs = 512 * s;
+    // byte offset of input row rr (image row y0 + rr - 2, rr = 0 .. 18) in the input
+    // rows, computed by lane rr (read back per row by v_readlane): one reflect-101
+    // step suffices (y0 + 16 <= H, H >= 16), then the shard's clamp
+    {
+      int sy = y0 + lane - 2;
+      sy = sy < 0 ? -sy : (sy >= H ? 2 * H - 2 - sy : sy);
+      sy = sy < E.in_row0 ? E.in_row0 : (sy >= in_row1 ? in_row1 - 1 : sy);
+      roff = (sy - E.in_row0) * pitch;
+    }
+    // edge pixels, packed (cr | cb << 16): lane r converts input row r's x = xs - 2,
+    // xs - 1 (or 2, 1 at the left border) and x = xs + 512 (or W - 2 at the right)
+    hal_l2 = hal_l1 = hal_r = 0;
+    if (lane < 19) {
+      const uint8_t *row = E.rgb + roff;
+      const int xl = xs >= 2 ? xs - 2 : 2, xl1 = xs >= 2 ? xs - 1 : 1, xr = xs + 512 < W ? xs + 512 : W - 2;
+      const YCC a = rgb2ycc(row[3 * xl], row[3 * xl + 1], row[3 * xl + 2]);
+      const YCC b = rgb2ycc(row[3 * xl1], row[3 * xl1 + 1], row[3 * xl1 + 2]);
+      const YCC c = rgb2ycc(row[3 * xr], row[3 * xr + 1], row[3 * xr + 2]);
+      hal_l2 = a.cr | a.cb << 16;
+      hal_l1 = b.cr | b.cb << 16;
+      hal_r = c.cr | c.cb << 16;
+    }
+    const uint64_t base = reinterpret_cast<uint64_t>(E.rgb) + 3 * xs;
+    const uint32_t base_lo = __builtin_amdgcn_readfirstlane((uint32_t)base),
+                   base_hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+    rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>((uint64_t)base_hi << 32 | base_lo), 0,
+                                             __builtin_amdgcn_readfirstlane(E.in_rows * pitch - 3 * xs), 0x00020000);
+    voff = 24 * lane;
+    K = YccK{opq(kYLo), opq(kYLo << 8), opq(kYHi), opq(kYHi << 8), opv(32768u), opv((uint32_t)kCC4)};
+    k4 = opq(0x00040004u);
+    k6 = opq(0x00060006u);
+    k128 = opq(0x00800080u);
+#pragma unroll
+    for (int r = 0; r < kLA; ++r) load_row(r);
+  }
+
+  // input rows R0 .. R1 - 1
+  template <int R0, int R1>
+  __device__ __forceinline__ void rows(uint2 (&yq)[16], uint32_t *s_chroma) {
+#pragma unroll
+    for (int r = R0; r < R1; ++r) {
+      if (r + kLA < 19) load_row(r + kLA);
+      const u32x4 qa = ring_a[r % (kLA + 1)];
+      const u32x2 qb = ring_b[r % (kLA + 1)];
+      const uint32_t wd[6] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y};
+      uint32_t Yh[8], c[8];
+      ycc8(wd, K, Yh, c);
+      if (r >= 2 && r < 18) yq[r - 2] = make_uint2(ypack4(Yh, 0), ypack4(Yh, 4));
+      // neighbour pixels x0 - 2, x0 - 1 (left lane) and x0 + 8 (right lane)
+      const uint32_t l2 = set_lane<0>(wshr1(c[6]), __builtin_amdgcn_readlane((int)hal_l2, r));
+      const uint32_t l1 = set_lane<0>(wshr1(c[7]), __builtin_amdgcn_readlane((int)hal_l1, r));
+      const uint32_t r0 = set_lane<63>(wshl1(c[0]), __builtin_amdgcn_readlane((int)hal_r, r));
+      h[r][0] = pk_taps5(l2, l1, c[0], c[1], c[2], k4, k6);
+      h[r][1] = pk_taps5(c[0], c[1], c[2], c[3], c[4], k4, k6);
+      h[r][2] = pk_taps5(c[2], c[3], c[4], c[5], c[6], k4, k6);
+      h[r][3] = pk_taps5(c[4], c[5], c[6], c[7], r0, k4, k6);
+      if (r >= 4 && r % 2 == 0) {  // chroma row i = r / 2 - 2 has all five input rows
+        const int a = r - 4, i = r / 2 - 2;
+        uint32_t v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)  // sum + 128 < 2^16: (sum + 128) >> 8 is the high byte
+          v[j] = pk_add16(pk_taps5(h[a][j], h[a + 1][j], h[a + 2][j], h[a + 3][j], h[a + 4][j], k4, k6), k128);
+        // high bytes: x01 = (cr0, cr1, cb0, cb1), x23 = (cr2, cr3, cb2, cb3)
+        const uint32_t x01 = __builtin_amdgcn_perm(v[1], v[0], 0x07030501u);
+        const uint32_t x23 = __builtin_amdgcn_perm(v[3], v[2], 0x07030501u);
+        s_chroma[i * 64 + lane] = __builtin_amdgcn_perm(x23, x01, 0x05040100u);
+        s_chroma[512 + i * 64 + lane] = __builtin_amdgcn_perm(x23, x01, 0x07060302u);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+};
 
 template <int TMF, bool NT, bool F32>
 __device__ __forceinline__ void encode420_unit(const Enc420 &E);
@@ -401,20 +420,8 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
   const int nbx = E.W >> 3, nbxc = E.W >> 4;
 
   uint2 yq[16];
-#if defined(HIC_DEV) && defined(HIC_ENC_DEV) && (HIC_ENC_DEV & 2)
-  // dev timing (results invalid): no colour stage, synthetic pixels
-#pragma unroll
-  for (int r = 0; r < 16; ++r) yq[r] = make_uint2(0x9E3779B1u * (lane + r + g), 0x85EBCA6Bu * (lane ^ r ^ g));
-#pragma unroll
-  for (int i = 0; i < 16; ++i) s_chroma[i * 64 + lane] = 0x01000193u * (lane + i + g);
-#else
-  enc_colour(E, y0, s, lane, yq, s_chroma);
-#endif
-
-  // ---- Y: block rows 2u and 2u + 1, blocks 64 s .. 64 s + 63 (one RLE tile each)
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int br = 0; br < 2; ++br) {
+  // Y block row br: blocks 64 s .. 64 s + 63 of block row 2u + br (one RLE tile)
+  auto y_blocks = [&](int br) {
     uint2 w[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) w[r] = yq[8 * br + r];
@@ -430,7 +437,36 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_sched_barrier(0);
+  };
+#if defined(HIC_DEV) && defined(HIC_ENC_DEV) && (HIC_ENC_DEV & 2)
+  // dev timing (results invalid): no colour stage, synthetic pixels
+#pragma unroll
+  for (int r = 0; r < 16; ++r) yq[r] = make_uint2(0x9E3779B1u * (lane + r + g), 0x85EBCA6Bu * (lane ^ r ^ g));
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s_chroma[i * 64 + lane] = 0x01000193u * (lane + i + g);
+  y_blocks(0);
+  y_blocks(1);
+#else
+#ifndef HIC_ENC_SPLIT
+#define HIC_ENC_SPLIT 10
+#endif
+  // Y block row 0 (image rows y0 .. y0 + 7 = input rows 2 .. 9) is transformed
+  // between the colour stage's two row ranges: the loads of input rows 10 ..
+  // 9 + kLA are in flight under its DCT instead of exposed at the unit's start only
+  EncColour C;
+  C.init(E, y0, s, lane);
+  C.rows<0, HIC_ENC_SPLIT>(yq, s_chroma);
+  __builtin_amdgcn_sched_barrier(0);
+  if (HIC_ENC_SPLIT < 19) {
+    y_blocks(0);
+    C.rows<HIC_ENC_SPLIT, 19>(yq, s_chroma);
+    __builtin_amdgcn_sched_barrier(0);
+    y_blocks(1);
+  } else {
+    y_blocks(0);
+    y_blocks(1);
   }
+#endif
 
   // ---- chroma: block m of Cr -> lane m, of Cb -> lane 32 + m (block m spans the
   // chroma columns of lanes 2m and 2m + 1 of this strip), read from the LDS area

@@ -723,6 +723,9 @@ __global__ __launch_bounds__(kScanT) void k_rle_scan16b(RleJobs16 jobs, uint32_t
   if (s_fail && threadIdx.x == 0) *J.d_count = HIC_COUNT_SCAN_TIMEOUT;  // hand-off timed out: report, do not hang
 }
 
+#ifndef HIC_EMIT_COAL
+#define HIC_EMIT_COAL 1
+#endif
 template <int MF, bool NT>
 __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
   // per wave: kWSyms symbols + 16-byte alignment slack + the dummy slot
@@ -747,12 +750,27 @@ __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
     const RleJob16 &J = jobs.j[job_of(gt)];
     const int64_t t = gt - J.tile0;
     const int64_t b = t * kWT + lane;
+#if HIC_EMIT_COAL
+    // coalesced: 16-B chunk c = 64 k + lane of the tile (block c / 8, part c % 8)
+    // into w[4k .. 4k + 3]; transposed to one block per lane through LDS (to_lanes)
+    {
+      const int64_t b0 = t * kWT;
+      const uint4 *q = reinterpret_cast<const uint4 *>(J.blocks + b0 * 64);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const bool ok = b0 + 8 * k + (lane >> 3) < J.nblk;
+        const uint4 v = ok ? q[64 * k + lane] : make_uint4(0, 0, 0, 0);
+        n.w[4 * k] = v.x; n.w[4 * k + 1] = v.y; n.w[4 * k + 2] = v.z; n.w[4 * k + 3] = v.w;
+      }
+    }
+#else
     if (b < J.nblk) {
       load_block16(J.blocks, b, n.w);
     } else {
 #pragma unroll
       for (int k = 0; k < 32; ++k) n.w[k] = 0;
     }
+#endif
     // the tile's first record (a 64-block tile may carry two 32-block records)
     const int64_t *offs = J.ws + 3 * J.nrec;
     n.off = offs[(t << J.rshift) * 2 + 0];
@@ -767,6 +785,27 @@ __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
     if (gn < jobs.total_tiles) fetch(gn, nxt);
     const RleJob16 &J = jobs.j[job_of(g)];
     const int64_t b = (g - J.tile0) * kWT + lane;
+#if HIC_EMIT_COAL
+    {
+      // transpose through the wave's symbol-value stage (free until this tile's
+      // emit): chunk (block bb, part p) at 16-B slot 8 bb + (p ^ (bb & 7)) -- the
+      // stores are 1 KiB contiguous, the loads (block = lane) hit 8 distinct
+      // 16-B bank groups per 8 lanes
+      uint4 *sx = reinterpret_cast<uint4 *>(s_val_all[wv]);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int c = 64 * k + lane, bb = c >> 3, pp = c & 7;
+        sx[8 * bb + (pp ^ (bb & 7))] = make_uint4(cur.w[4 * k], cur.w[4 * k + 1], cur.w[4 * k + 2], cur.w[4 * k + 3]);
+      }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint4 v = sx[8 * lane + (k ^ (lane & 7))];
+        cur.w[4 * k] = v.x; cur.w[4 * k + 1] = v.y; cur.w[4 * k + 2] = v.z; cur.w[4 * k + 3] = v.w;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+#endif
     // DC differences: the previous block's DC comes from the neighbouring lane
     const int dc = (int)(int16_t)(cur.w[0] & 0xFFFFu);
     int pdc = __shfl_up(dc, 1, 64);

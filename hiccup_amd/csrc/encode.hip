@@ -536,11 +536,14 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
   const dim3 grid((unsigned)((E.nunits + 3) / 4)), block(256);
   hipStream_t s = as_stream(stream);
   hipEvent_t e0 = static_cast<hipEvent_t>(ev_start), e1 = static_cast<hipEvent_t>(ev_stop);
+  // knob encode_lds_pad: reserve extra LDS per workgroup (fewer encode workgroups
+  // per CU, room for a kernel of another stream beside them)
+  const size_t pad = (size_t)knob(HIC_KNOB_ENCODE_LDS_PAD) * 1024;
   auto launch = [&](auto kern) {
     if (e0 || e1)
-      hipExtLaunchKernelGGL(kern, grid, block, 0, s, e0, e1, 0, E);
+      hipExtLaunchKernelGGL(kern, grid, block, pad, s, e0, e1, 0, E);
     else
-      hipLaunchKernelGGL(kern, grid, block, 0, s, E);
+      hipLaunchKernelGGL(kern, grid, block, pad, s, E);
   };
   const bool w2 = knob(HIC_KNOB_ENCODE_WAVES) == 2, nt = knob(HIC_KNOB_ENCODE_NT) != 0;
   const bool f32 = knob(HIC_KNOB_ENCODE_DCT) == 1;

@@ -16,15 +16,16 @@
 // block rows (a 64-block RLE tile each, W % 512 == 0) and half of chroma block
 // column l / 2.  One wave per unit:
 //   1. colour: 19 RGB rows (the 16 rows + the 2 + 1 rows of pyrDown's vertical
-//      taps), 24 B per lane per row (1.5 KiB contiguous per wave-row); Y of rows
-//      0..15 stays in registers (two 8x8 blocks per lane); Cr / Cb per pixel, the
-//      horizontal [1 4 6 4 1] at even columns with the neighbour pixels by DPP
-//      wave shifts (the strip's edge pixels converted once per unit, one row per
-//      lane, and read back by v_readlane), the vertical taps over a 5-row window
-//      -> 8 chroma rows x 4 columns per lane and plane;
-//   2. DCT of Y block row 0 and row 1 (lane = block): coefficients to the LDS
-//      stage at their zig-zag slot, copied out in 1 KiB nontemporal stores, the
-//      tile record from the stage;
+//      taps), 24 B per lane per row (1.5 KiB contiguous per wave-row, buffer loads
+//      at a scalar row offset); YCC by v_dot4 (ycc8); Y of rows 0..15 stays in
+//      registers (two 8x8 blocks per lane); Cr / Cb per pixel, the horizontal
+//      [1 4 6 4 1] at even columns with the neighbour pixels by DPP wave shifts
+//      (the strip's edge pixels converted once per unit, one row per lane, and
+//      written into lane 0 / 63 by v_writelane), the vertical taps over a 5-row
+//      window -> 8 chroma rows x 4 columns per lane and plane;
+//   2. DCT of Y block row 0 (between the colour rows 0..9 and 10..18) and row 1
+//      (lane = block): coefficients to the LDS stage at their zig-zag slot,
+//      copied out in 1 KiB stores, the tile record from the stage;
 //   3. chroma: the colour stage left the chroma rows in a 4 KiB LDS area per wave;
 //      chroma block m of Cr is read into lane m and of Cb into lane 32 + m (a
 //      block spans the columns of lanes 2m, 2m + 1), one DCT pass with the

@@ -497,19 +497,33 @@ __device__ __forceinline__ void emit_tile16(const uint32_t (&w)[32], const int16
       o += nf + 1;
     }
     if (staged && dense) {
-      // one symbol per nonzero from the first (whose run is the carried one's
-      // remainder), branch-free -- a zero coefficient writes to the stage's dummy
-      // slot and does not advance r
-      int r = (int)(o - o_tile) + lo;  // stage index of the next symbol (len array)
-      const int dv = vo - lo;          // val index = len index + dv
-      int pl = first;
+      // one symbol per nonzero from the first, branch-free: a zero coefficient
+      // writes to the stage's dummy slot and does not advance r.  The first
+      // nonzero needs no case of its own: with pl = first - 1 - rem its run
+      // j - pl - 1 is the carried run's remainder, and no coefficient before it
+      // is nonzero.  One index serves both arrays (val index = len index + dv), so
+      // a coefficient costs a compare, a subtract, two selects, an address and a
+      // carry-add.
+      typedef __attribute__((address_space(3))) uint8_t lds_u8;
+      typedef __attribute__((address_space(3))) int16_t lds_i16;
+      // LDS byte addresses: len slot = la, val slot = 2 la + vshift
+      const uint32_t lbase = (uint32_t)(uintptr_t)(lds_u8 *)s_len;
+      const uint32_t vshift = (uint32_t)(uintptr_t)(lds_i16 *)s_val + 2u * (uint32_t)(vo - lo) - 2u * lbase;
+      // dummy slot past every real one: len kWSyms + 16 > lo + kWSyms - 1, val
+      // kWSyms + 16 + vo - lo > vo + kWSyms - 1 (lo, vo < 16), both inside the stage
+      const uint32_t ldummy = lbase + kWSyms + 16;
+      uint32_t la = lbase + (uint32_t)((int)(o - o_tile) + lo);  // next symbol's len slot
+      int pl = first - 1 - rem;
 #pragma unroll
       for (int j = 0; j < 63; ++j) {
         const int v = zz_ac(w, j);
-        const bool nz = (v != 0) & (j >= first);
-        s_len[nz ? r : kWSyms + 16] = (uint8_t)(j == first ? rem : j - pl - 1);  // dummy slots lie past
-        s_val[nz ? r + dv : kWSyms + 24] = (int16_t)v;  // every real one (lo, vo < 16)
-        r += nz ? 1 : 0;
+        const bool nz = v != 0;
+        const uint32_t a = nz ? la : ldummy;
+        *(lds_u8 *)(uintptr_t)a = (uint8_t)(j - pl - 1);
+        uint32_t va;  // 2 a + vshift in one instruction (the compiler splits it in two)
+        asm("v_lshl_add_u32 %0, %1, 1, %2" : "=v"(va) : "v"(a), "v"(vshift));
+        *(lds_i16 *)(uintptr_t)va = (int16_t)v;
+        la += nz ? 1u : 0u;
         pl = nz ? j : pl;
       }
     } else if (staged) {

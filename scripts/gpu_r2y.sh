@@ -1,4 +1,4 @@
-# emit dense pass at 7 VALU per coefficient: full GPU suite, emit kernel stats, bench
+# emit: dense pass, unrolled copy-out with uniform tile offsets: full GPU suite, emit kernel stats, bench
 set -u
 run() { timeout -k 10 "$@"; rc=$?; echo "rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi; }
 mkdir -p gpurun_out

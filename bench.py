@@ -154,14 +154,17 @@ def extra_4k_luma(steps=20):
             "algorithmic_bytes": n * n * 3, "timed_launches": steps}
 
 
-def extra_8k_plane_dct(steps=24):
+def extra_8k_plane_dct(steps=24, luma_only=False):
     """The north_star's DCT+quantize pass on its own: k_dct_planes over the 8K Y +
     Cr + Cb planes (4320 x 7680 + 2 x 2160 x 3840 uint8 -> int16 zig-zag blocks +
-    RLE tile records, one launch, the two-kernel chain's second kernel), rotating
-    >= 1.2 GB of planes, timed by the launch's own events.  Algorithmic bytes 3 B
-    per plane pixel (1 read + 2 written)."""
+    RLE tile records, one launch, the two-kernel chain's second kernel), or over the
+    8K luminance plane alone (luma_only: SURVEY.md section 8(d)'s measurement point
+    for north_star's >= 0.70 target, 99.5 MB, <= 17.8 us), rotating >= 1.2 GB of
+    planes, timed by the launch's own events.  Algorithmic bytes 3 B per plane
+    pixel (1 read + 2 written); read_only_frac counts the 1 B read alone."""
     from hiccup_amd import _lib, device
-    shapes = [(H8K, W8K, 0), (H8K // 2, W8K // 2, 1), (H8K // 2, W8K // 2, 1)]
+    shapes = [(H8K, W8K, 0)] if luma_only else [(H8K, W8K, 0), (H8K // 2, W8K // 2, 1), (H8K // 2, W8K // 2, 1)]
+    n = len(shapes)
     px = sum(h * w for h, w, _ in shapes)
     rot = int(np.ceil(ROT_BYTES / (px * 3)))
     g = torch.Generator(device="cuda")
@@ -169,7 +172,7 @@ def extra_8k_plane_dct(steps=24):
     sets = []
     for _ in range(rot):
         planes, outs, wss = [], [], []
-        jobs = (_lib.DctPlaneJob * 3)()
+        jobs = (_lib.DctPlaneJob * n)()
         for i, (h, w, t) in enumerate(shapes):
             nblk = (h // 8) * (w // 8)
             planes.append(torch.randint(0, 256, (h, w), dtype=torch.uint8, device="cuda", generator=g))
@@ -179,19 +182,23 @@ def extra_8k_plane_dct(steps=24):
         sets.append((planes, outs, wss, jobs))
     evs = [device.KernelEvents() for _ in range(steps)]
     for i in range(4):
-        _lib.call("hic_dct_quant_rle_u8_batch", 3, sets[i % rot][3], 15, device.stream_ptr(), None, None)
+        _lib.call("hic_dct_quant_rle_u8_batch", n, sets[i % rot][3], 15, device.stream_ptr(), None, None)
     for i, e in enumerate(evs):
-        _lib.call("hic_dct_quant_rle_u8_batch", 3, sets[(4 + i) % rot][3], 15, device.stream_ptr(), e.start, e.stop)
+        _lib.call("hic_dct_quant_rle_u8_batch", n, sets[(4 + i) % rot][3], 15, device.stream_ptr(), e.start, e.stop)
     torch.cuda.synchronize()
     us = float(np.median([e.elapsed_ms() for e in evs])) * 1e3
     gbs = px * 3 / (us * 1e-6) / 1e9
     del sets
     torch.cuda.empty_cache()
-    return {"workload": "8K Y + Cr + Cb planes -> quantized int16 zig-zag blocks + RLE tile records (k_dct_planes, "
-                        "the DCT+quantize pass without the colour stage)",
-            "kernel": "k_dct_planes<-1,ZIGZAG_I16,15>", "median_launch_us": round(us, 2),
-            "achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes": px * 3,
-            "timed_launches": steps}
+    out = {"workload": ("8K luminance plane (4320 x 7680 uint8) -> quantized int16 zig-zag blocks + RLE tile "
+                        "records: SURVEY.md 8(d)'s measurement point for north_star's >= 0.70 target "
+                        "(<= 17.8 us for 99.5 MB)" if luma_only else
+                        "8K Y + Cr + Cb planes -> quantized int16 zig-zag blocks + RLE tile records (k_dct_planes, "
+                        "the DCT+quantize pass without the colour stage)"),
+           "kernel": "k_dct_planes<-1,ZIGZAG_I16,15>", "median_launch_us": round(us, 2),
+           "achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes": px * 3,
+           "read_only_frac": round(px / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4), "timed_launches": steps}
+    return out
 
 
 def extra_16k_roundtrip(steps=4):
@@ -565,6 +572,7 @@ def main():
         }
         if not args.no_extras and world == 1:
             out["extra_configs"] = {"4k_luma_dct": extra_4k_luma(), "8k_plane_dct": extra_8k_plane_dct(),
+                                     "8k_luma_dct": extra_8k_plane_dct(luma_only=True),
                                     "16k_roundtrip": extra_16k_roundtrip()}
         if extra_sharded is not None:
             out["extra_configs"] = {"16k_roundtrip": extra_sharded}

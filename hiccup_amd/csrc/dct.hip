@@ -270,8 +270,12 @@ struct DctJobs {
   int n, total_sets, M;
 };
 
+#ifndef HIC_DCT_WPE
+#define HIC_DCT_WPE 3  // register budget: waves per SIMD (3: <= 168 VGPRs)
+#endif
 template <int TABLE, int LAYOUT, int TMF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_dct_planes(DctJobs jobs, int path) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DCT_WPE))) void k_dct_planes(DctJobs jobs,
+                                                                                                       int path) {
   __shared__ uint2 s_stage[4 * 64 * kStageU2];
   // wv is wave-uniform: keep it (and the set / job indices derived from it) in
   // SGPRs, so the job fields are scalar loads, not vector loads on vmcnt
@@ -891,7 +895,10 @@ inline bool aligned(const void *p, uintptr_t a) { return (reinterpret_cast<uintp
 inline int dct_path() { return knob(HIC_KNOB_DCT_PATH); }
 inline int dct_waves_per_cu() {
   const int v = knob(HIC_KNOB_DCT_WAVES_PER_CU);
-  return v >= 0 ? v : (dct_path() == 3 ? 16 : 12);  // persistent waves per CU
+  // float64 path: one wave per set (the hardware's dispatch balances the tail:
+  // 8K planes 37.6 us vs 40.0-40.6 for 12 persistent waves per CU, luma equal;
+  // scripts/gpu_r2ad.sh); the float32 path keeps its persistent queue
+  return v >= 0 ? v : (dct_path() == 3 ? 16 : 0);
 }
 
 inline bool fwd_fast(int H, int W, int64_t stride, const void *plane, const void *out) {

@@ -1286,7 +1286,10 @@ int encode_batch16(RleJobs16 &jobs, hipStream_t s) {
   hipLaunchKernelGGL(k_rle_scan16b, dim3((unsigned)nparts), dim3(kScanT), 0, s, jobs, ep);
   if (int e = check_launch("k_rle_scan16b")) return e;
   // persistent: 3 workgroups (12 waves) per CU fit the 51 KB LDS stage and the registers
-  const int64_t cap = 12 * (int64_t)cu_count();
+#ifndef HIC_EMIT_WPC
+#define HIC_EMIT_WPC 12
+#endif
+  const int64_t cap = HIC_EMIT_WPC > 0 ? HIC_EMIT_WPC * (int64_t)cu_count() : INT64_MAX;
   const int64_t waves = t0 < cap ? t0 : cap;
   const dim3 grid((unsigned)((waves + 3) / 4));
   // nontemporal symbol stores unless knob RLE_NT = 0 (A/B)

@@ -42,7 +42,19 @@ __global__ __launch_bounds__(256) void k_rate(double *out, unsigned long long *c
   if (K == 8) asm volatile("v_cvt_f32_i32 %0, %1" : "=v"(f[i]) : "v"(v[i]));                           \
   if (K == 9) asm volatile("v_lshl_add_u64 %0, %0, 1, %0" : "+v"(d[i]));                               \
   if (K == 10) asm volatile("v_mov_b64 %0, %1" : "=v"(d[i]) : "v"(d[(i + 1) & 7]));                    \
-  if (K == 11) asm volatile("v_pk_fma_f32 %0, %0, %0, %0" : "+v"(d[i]));
+  if (K == 11) asm volatile("v_pk_fma_f32 %0, %0, %0, %0" : "+v"(d[i]));                              \
+  if (K == 12) asm volatile("v_fmac_f32 %0, %1, %1" : "+v"(f[i]) : "v"((float)c));                     \
+  if (K == 13) asm volatile("v_sub_u32 %0, %0, %1" : "+v"(v[i]) : "v"(lane));                           \
+  if (K == 14) asm volatile("v_lshlrev_b32 %0, 1, %0" : "+v"(v[i]));                                    \
+  if (K == 15) asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(v[i]) : "v"(lane));                       \
+  if (K == 16) asm volatile("v_perm_b32 %0, %0, %1, %1" : "+v"(v[i]) : "v"(lane));                      \
+  if (K == 17) asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(v[i]) : "v"(lane));                        \
+  if (K == 18) asm volatile("v_med3_i32 %0, %0, %1, %1" : "+v"(v[i]) : "v"(lane));                      \
+  if (K == 19) asm volatile("v_add3_u32 %0, %0, %1, %1" : "+v"(v[i]) : "v"(lane));                      \
+  if (K == 20) asm volatile("v_add_u32_e64 %0, %0, %1" : "+v"(v[i]) : "v"(lane));                       \
+  if (K == 21) asm volatile("v_sub_u32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD" : "+v"(v[i]) : "v"(lane)); \
+  if (K == 22) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(v[i]) : "v"(lane));                 \
+  if (K == 23) asm volatile("v_pk_mad_u16 %0, %0, %1, %1" : "+v"(v[i]) : "v"(lane));
     CHAIN8(OPK)
 #undef OPK
   }
@@ -67,19 +79,22 @@ int main() {
   hipEvent_t s, e;
   hipEventCreate(&s);
   hipEventCreate(&e);
-  const char *names[12] = {"v_add_f64", "v_fma_f64", "v_mul_f64", "v_cvt_f64_i32", "v_add_u32", "v_mad_u32_u24",
+  const char *names[24] = {"v_add_f64", "v_fma_f64", "v_mul_f64", "v_cvt_f64_i32", "v_add_u32", "v_mad_u32_u24",
                            "v_dot4_u32_u8", "v_fma_f32", "v_cvt_f32_i32", "v_lshl_add_u64", "v_mov_b64",
-                           "v_pk_fma_f32"};
-  for (int wps : {1, 2, 4}) {  // waves per SIMD: workgroups of 4 waves, wps per CU
+                           "v_pk_fma_f32", "v_fmac_f32", "v_sub_u32", "v_lshlrev_b32", "v_mul_u32_u24",
+                           "v_perm_b32", "v_pk_add_u16", "v_med3_i32", "v_add3_u32", "v_add_u32_e64",
+                           "v_sub_u32_sdwa", "v_cndmask_b32", "v_pk_mad_u16"};
+  for (int wps : {2, 4}) {  // waves per SIMD: workgroups of 4 waves, wps per CU
     const int blocks = cus * wps;
-    for (int k = 0; k < 12; ++k) {
+    for (int k = 0; k < 24; ++k) {
       float best = 1e9;
       unsigned long long h[2] = {0, 0};
       for (int rep = 0; rep < 3; ++rep) {
         hipEventRecord(s);
 #define L(K) \
   if (k == K) hipLaunchKernelGGL(k_rate<K>, dim3(blocks), dim3(256), 0, 0, out, clk, rep);
-        L(0) L(1) L(2) L(3) L(4) L(5) L(6) L(7) L(8) L(9) L(10) L(11)
+        L(0) L(1) L(2) L(3) L(4) L(5) L(6) L(7) L(8) L(9) L(10) L(11) L(12) L(13) L(14) L(15) L(16) L(17)
+        L(18) L(19) L(20) L(21) L(22) L(23)
 #undef L
         hipEventRecord(e);
         hipEventSynchronize(e);

@@ -51,6 +51,20 @@ extern "C" int hic_stream_sync(void *stream) {
   return hic::hip_status(hipStreamSynchronize(hic::as_stream(stream)), "hipStreamSynchronize");
 }
 
+extern "C" int hic_stream_create_cu_mask(const uint32_t *h_mask, int nwords, void **h_stream) {
+  if (!h_mask || !h_stream || nwords <= 0) return hic::arg_error("null pointer / mask size");
+  hipStream_t s = nullptr;
+  const int rc = hic::hip_status(hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, h_mask),
+                                 "hipExtStreamCreateWithCUMask");
+  *h_stream = rc == HIC_OK ? (void *)s : nullptr;
+  return rc;
+}
+
+extern "C" int hic_stream_destroy(void *stream) {
+  if (!stream) return hic::arg_error("null stream");
+  return hic::hip_status(hipStreamDestroy((hipStream_t)stream), "hipStreamDestroy");
+}
+
 extern "C" int hic_event_create(void **h_event) {
   if (!h_event) return hic::arg_error("null pointer");
   hipEvent_t e = nullptr;

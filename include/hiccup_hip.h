@@ -82,6 +82,11 @@ int hic_set_knob(int knob, int value);
 int hic_get_knob(int knob, int *h_value);
 /* Synchronises `stream`; returns HIC_ERR_HIP if an earlier async launch failed. */
 int hic_stream_sync(void *stream);
+/* A stream whose kernels run only on the CUs set in h_mask (nwords 32-bit words,
+ * bit c = CU c; hipExtStreamCreateWithCUMask): the producer / consumer CU split
+ * of bench.py --cu-split.  Destroy with hic_stream_destroy. */
+int hic_stream_create_cu_mask(const uint32_t *h_mask, int nwords, void **h_stream);
+int hic_stream_destroy(void *stream);
 
 /* ---- forward transform: replaces transform.dct_channel (transform.py:182-193) =
  *      offset -128 (:186), split_matrix/pad (:33-42), dct2 (:67-84, scipy pocketfft

@@ -186,11 +186,11 @@ def jpeg_encode(compressed):
     """codec.py:275-334: CompressedImage -> HicImage (9 tables, 9 bit strings, 2 shapes).
     Everything but the nine trees runs on the GPU: split + zig-zag, DC DPCM, AC RLE
     (encode_channel_device), the key histograms in first-appearance order and the
-    bit packing of the coded streams (huffman.DeviceStream, csrc/huffman.hip)."""
+    bit packing of the coded streams (huffman.DeviceStreams, csrc/huffman.hip)."""
     utils.debug_msg("Starting JPEG encoding")
     bs = settings.JPEG_BLOCK_SIZE
     chans = ("lum", "cr", "cb")
-    streams, dc_type = {}, {}
+    keys, dc_type = {}, {}
     for k, v in compressed.as_dict.items():
         # the reference's DC keys are elements of the plane (utils.differences over
         # block[0][0]): numpy scalars of its dtype
@@ -201,10 +201,13 @@ def jpeg_encode(compressed):
         dc, Ls, Vs, cnt = encode_channel_device(device.to_device(p), p.shape[0], p.shape[1], bs)
         count = int(device.to_host(cnt)[0])
         # trees per channel: DC differences, AC values, AC lengths (codec.py:304-313)
-        streams[k] = (huffman.DeviceStream(dc), huffman.DeviceStream(Vs[:count]), huffman.DeviceStream(Ls[:count]))
-    # each tree codes the stream it was built from (codec.py:310-330)
-    tables = [huffman_encode(streams[k][j].tree, dc_type[k] if j == 0 else int) for j in range(3) for k in chans]
-    data = [hic.BitStringP.from_packed(*streams[k][j].packed()) for j in range(3) for k in chans]
+        keys[k] = ((dc, dc.numel()), (Vs, count), (Ls, count))
+    # the nine streams in payload order (codec.py:310-330); each tree codes the
+    # stream it was built from
+    order = [(k, j) for j in range(3) for k in chans]
+    ds = huffman.DeviceStreams([keys[k][j] for k, j in order])
+    tables = [huffman_encode(ds.trees[i], dc_type[k] if j == 0 else int) for i, (k, j) in enumerate(order)]
+    data = [hic.BitStringP.from_packed(*pk) for pk in ds.packed()]
     shape = compressed.shape
     payloads = tables + data + [hic.TupP(shape[0][0], shape[0][1]), hic.TupP(shape[1][0], shape[1][1])]
     return hic.HicImage.jpeg_image(payloads)

@@ -16,6 +16,7 @@ in first-appearance order (``device_counts``) and the bit packing of a coded
 stream (``HuffmanTree.encode_device``); only the tree (a heap over the distinct
 keys) is built here.
 """
+import ctypes
 import heapq
 
 import numpy as np
@@ -164,6 +165,7 @@ class HuffmanTree:
         self.data = data
         self.key_func = key_func
         self._codes = None
+        self._by_leaf = None
 
     # ------------------------------------------------------------ codes
     @staticmethod
@@ -176,10 +178,29 @@ class HuffmanTree:
             node = parent
         return "".join(reversed(bits))
 
+    def _leaf_codes(self):
+        """{id(leaf): code string}, every leaf's path in ONE walk down from the root
+        ("1" = left child, as _code_of reads it bottom-up); cached."""
+        if self._by_leaf is None:
+            out = {}
+            stack = [(self.root, "")]
+            while stack:
+                node, code = stack.pop()
+                if node is None:  # a singleton root's empty right side
+                    continue
+                if node.is_leaf:
+                    out[id(node)] = code
+                    continue
+                stack.append((node.left, code + "1"))
+                stack.append((node.right, code + "0"))
+            self._by_leaf = out
+        return self._by_leaf
+
     def codes(self):
         """{key: code string} for every leaf."""
         if self._codes is None:
-            self._codes = dict((leaf.value, self._code_of(leaf)) for leaf in self.leaves)
+            by_leaf = self._leaf_codes()
+            self._codes = dict((leaf.value, by_leaf[id(leaf)]) for leaf in self.leaves)
         return self._codes
 
     def get_leaf(self, value):
@@ -189,7 +210,8 @@ class HuffmanTree:
         return s + self._code_of(path[0]) if path else s
 
     def encode_table(self):
-        return [(leaf.value, self._code_of(leaf)) for leaf in self.leaves]
+        by_leaf = self._leaf_codes()
+        return [(leaf.value, by_leaf[id(leaf)]) for leaf in self.leaves]
 
     def encode_data(self, data=None):
         data = self.data if data is None else data
@@ -317,3 +339,76 @@ def device_counts(keys_dev, n=None, stream=None):
     present = np.flatnonzero(counts)
     order = present[np.argsort(first[present], kind="stable")]
     return [int(lo + b) for b in order], counts[order].astype(np.int64)
+
+
+class DeviceStreams:
+    """Several device key streams at once (the nine of codec.jpeg_encode): the same
+    trees and packed bits as one DeviceStream each, with the host round trips
+    batched -- one copy back for all key ranges, one for all histograms, one upload
+    of all code tables, one copy back for every stream's bits -- instead of five
+    synchronising copies per stream."""
+
+    def __init__(self, keys_list, stream=None):
+        self.keys = [k for k, _ in keys_list]
+        self.n = [int(n) for _, n in keys_list]
+        self.stream = stream
+        if min(self.n) == 0:
+            raise ValueError("empty key stream")
+        lib = _lib.load()
+        s = device.stream_ptr(stream)
+        m = len(self.keys)
+        mm = device.empty((m, 2), torch.int32)
+        for i, (k, n) in enumerate(zip(self.keys, self.n)):
+            _lib.call("hic_key_range", device.ptr(k), k.element_size(), n, device.ptr(mm[i]), s)
+        rng = mm.cpu().numpy()
+        self.lo = [int(a) for a, _ in rng]
+        self.nbins = [int(b) - int(a) + 1 for a, b in rng]
+        off = np.concatenate([[0], np.cumsum(self.nbins)]).astype(np.int64)
+        counts = device.empty((int(off[-1]),), torch.int32)
+        first = device.empty((int(off[-1]),), torch.int32)
+        for i, (k, n) in enumerate(zip(self.keys, self.n)):
+            _lib.call("hic_key_histogram", device.ptr(k), k.element_size(), n, self.lo[i], self.nbins[i],
+                      ctypes.c_void_p(counts.data_ptr() + 4 * int(off[i])),
+                      ctypes.c_void_p(first.data_ptr() + 4 * int(off[i])), s)
+        c_all = counts.cpu().numpy().view(np.uint32)
+        f_all = first.cpu().numpy().view(np.uint32)
+        self.counts, self.trees = [], []
+        for i in range(m):
+            c = c_all[off[i]:off[i + 1]]
+            f = f_all[off[i]:off[i + 1]]
+            present = np.flatnonzero(c)
+            order = present[np.argsort(f[present], kind="stable")]
+            self.counts.append(c)
+            self.trees.append(HuffmanTree.construct_from_counts([int(self.lo[i] + b) for b in order],
+                                                                c[order].astype(np.int64)))
+        self._lib = lib
+
+    def packed(self):
+        """[(packed uint8 numpy array, number of bits)] per stream (hic_huffman_pack)."""
+        m = len(self.keys)
+        s = device.stream_ptr(self.stream)
+        tabs = [t.code_table(lo, nb) for t, lo, nb in zip(self.trees, self.lo, self.nbins)]
+        totals = [int(np.sum(np.asarray(c, dtype=np.int64) * l.astype(np.int64)))
+                  for c, (_, l) in zip(self.counts, tabs)]
+        nbytes = [max(4, -(-t // 32) * 4) for t in totals]
+        boff = np.concatenate([[0], np.cumsum(nbytes)]).astype(np.int64)
+        toff = np.concatenate([[0], np.cumsum(self.nbins)]).astype(np.int64)
+        cb = device.to_device(np.concatenate([b for b, _ in tabs]).view(np.int64))
+        cl = device.to_device(np.concatenate([l for _, l in tabs]))
+        out = device.empty((int(boff[-1]),), torch.uint8)
+        nbits = device.empty((m,), torch.int64)
+        ws = device.workspace(self._lib.hic_huffman_pack_workspace_bytes(max(self.n)))
+        for i, (k, n) in enumerate(zip(self.keys, self.n)):
+            # one workspace serves the launches in turn: they run in order on the stream
+            _lib.call("hic_huffman_pack", device.ptr(k), k.element_size(), n, self.lo[i], self.nbins[i],
+                      ctypes.c_void_p(cb.data_ptr() + 8 * int(toff[i])), ctypes.c_void_p(cl.data_ptr() + int(toff[i])),
+                      ctypes.c_void_p(out.data_ptr() + int(boff[i])), nbytes[i],
+                      ctypes.c_void_p(nbits.data_ptr() + 8 * i), device.ptr(ws), s)
+        nb = nbits.cpu().numpy()
+        host = out.cpu().numpy()
+        res = []
+        for i in range(m):
+            if int(nb[i]) != totals[i]:
+                raise RuntimeError("stream %d: packed %d bits, the histogram says %d" % (i, int(nb[i]), totals[i]))
+            res.append((host[boff[i]:boff[i] + -(-int(nb[i]) // 8)], int(nb[i])))
+        return res

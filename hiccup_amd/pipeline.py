@@ -180,25 +180,26 @@ class Encoder:
     def hic_image(self, stream=None):
         """codec.jpeg_encode of this encode, from the device streams: the nine Huffman
         trees from GPU key histograms, the nine bit strings packed on the GPU
-        (huffman.DeviceStream); == codec.jpeg_encode(the encoded CompressedImage)
+        (huffman.DeviceStreams); == codec.jpeg_encode(the encoded CompressedImage)
         for an unsharded encoder (syncs)."""
         from . import hicimage as hic
         from . import huffman
         if self.rows != (0, self.H):
             raise ValueError("hic_image needs the whole image (an unsharded encoder)")
         counts = self.counts.cpu().tolist()
-        streams = {}
+        keys = {}
         for i, k in enumerate(CHANNELS):
             check_count(int(counts[i]), k)
             c = int(counts[i])
-            streams[k] = (huffman.DeviceStream(self.dc[k], stream=stream),
-                          huffman.DeviceStream(self.sym_val[k][:c], stream=stream),
-                          huffman.DeviceStream(self.sym_len[k][:c], stream=stream))
+            keys[k] = ((self.dc[k], self.dc[k].numel()), (self.sym_val[k], c), (self.sym_len[k], c))
+        # the nine streams in payload order, their host round trips batched
+        order = [(k, j) for j in range(3) for k in CHANNELS]
+        ds = huffman.DeviceStreams([keys[k][j] for k, j in order], stream=stream)
         # DC keys as the reference holds them (numpy int32: dct_channel's dtype)
         tables = [hic.PayloadStringP(hic.TupP, [hic.TupP(np.int32(v) if j == 0 else int(v), c)
-                                                for v, c in streams[k][j].tree.encode_table()])
-                  for j in range(3) for k in CHANNELS]
-        data = [hic.BitStringP.from_packed(*streams[k][j].packed()) for j in range(3) for k in CHANNELS]
+                                                for v, c in ds.trees[i].encode_table()])
+                  for i, (k, j) in enumerate(order)]
+        data = [hic.BitStringP.from_packed(*pk) for pk in ds.packed()]
         (h, w), (hc, wc) = self.shapes["lum"], self.shapes["cr"]
         return hic.HicImage.jpeg_image(tables + data + [hic.TupP(h, w), hic.TupP(hc, wc)])
 

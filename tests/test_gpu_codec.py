@@ -519,6 +519,28 @@ def test_huffman_device_vs_host(dtype, kind):
     assert got.byte_stream == hicimage.BitStringP(bits).byte_stream
 
 
+def test_huffman_device_streams_batch_equals_single():
+    """huffman.DeviceStreams (the batched form codec.jpeg_encode and
+    Encoder.hic_image use) == one DeviceStream per stream: trees and packed bits,
+    over streams of mixed key widths, lengths and alphabets."""
+    from hiccup_amd import huffman
+    rng = np.random.default_rng(11)
+    raw = [rng.integers(0, 15, 70_001).astype(np.uint8), np.round(rng.laplace(0, 30, 123_457)).astype(np.int16),
+           rng.integers(-2000, 2001, 9_999).astype(np.int32), np.full(17, 5, np.int16),
+           ((rng.geometric(0.4, 50_000) - 1) * 2).astype(np.int32), rng.integers(0, 2, 3).astype(np.uint8)]
+    devs = [device.to_device(k) for k in raw]
+    # a stream given as a prefix of a longer buffer (the symbol buffers' form)
+    devs.append(device.to_device(np.concatenate([raw[1], raw[1][:100]])))
+    lens = [k.size for k in raw] + [raw[1].size]
+    ds = huffman.DeviceStreams(list(zip(devs, lens)))
+    packs = ds.packed()
+    for i, (d, n) in enumerate(zip(devs, lens)):
+        one = huffman.DeviceStream(d, n)
+        assert ds.trees[i].encode_table() == one.tree.encode_table(), i
+        p1, b1 = one.packed()
+        assert packs[i][1] == b1 and np.array_equal(packs[i][0], p1), i
+
+
 def test_encoder_hic_image_equals_jpeg_encode():
     """pipeline.Encoder.hic_image (GPU streams + GPU Huffman) == codec.jpeg_encode of
     the same quantized planes (the reference's encode path on its own output)."""

@@ -75,9 +75,13 @@ class Encoder:
         if r0 % 2 or not (0 <= r0 < r1 <= H):
             raise ValueError("bad row range %r" % ((r0, r1),))
         self.rows = (r0, r1)
-        can_fuse = W % 512 == 0 and H % 16 == 0 and r0 % 16 == 0 and r1 % 16 == 0
+        a, b = input_span(H, r0, r1)
+        # (hic_encode420_u8 reads the input rows through 32-bit buffer offsets)
+        can_fuse = (W % 512 == 0 and H % 16 == 0 and r0 % 16 == 0 and r1 % 16 == 0
+                    and (b - a) * W * 3 <= 2**31 - 1)
         if fused and not can_fuse:
-            raise ValueError("the fused encoder needs W % 512 == 0 and H, rows multiples of 16")
+            raise ValueError("the fused encoder needs W % 512 == 0, H and rows multiples of 16, "
+                             "and < 2 GiB of input rows")
         self.fused = can_fuse if fused is None else bool(fused)
         c0, c1 = r0 // 2, min(H // 2, r1 // 2)
         self.shapes = {"lum": (r1 - r0, W), "cr": (c1 - c0, W // 2), "cb": (c1 - c0, W // 2)}

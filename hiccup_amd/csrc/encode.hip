@@ -48,7 +48,7 @@ struct Enc420 {
   int16_t *coef[3];  // ZIGZAG_I16 blocks of the shard's Y, Cr, Cb planes
   int64_t *rec[3];   // tile records: Y per 64-block tile, Cr / Cb per 32-block half tile
   int M;
-  int nstrips, nunits;
+  int nstrips, nunits;  // nunits: waves (HIC_ENC_VG unit rows each)
 };
 
 constexpr int kZZ = HIC_LAYOUT_ZIGZAG_I16;
@@ -285,6 +285,9 @@ __device__ __forceinline__ uint32_t wshl1(uint32_t v) {  // lane i <- lane i + 1
 #ifndef HIC_ENC_LA
 #define HIC_ENC_LA 6
 #endif
+// NR input rows: 19 for one 16-row unit, 35 for two vertically adjacent units
+// (VG = 2: the second unit reuses the first's bottom halo rows).
+template <int NR>
 struct EncColour {
   // rows stream through a ring of kLA + 1 loads in flight (sched_barrier keeps the
   // compiler from hoisting all 19 rows' loads: 114 VGPRs)
@@ -298,7 +301,7 @@ struct EncColour {
   uint32_t k4, k6, k128;
   u32x4 ring_a[kLA + 1];
   u32x2 ring_b[kLA + 1];
-  uint32_t h[19][4];  // horizontal pyrDown sums of input row r, chroma column j (packed)
+  uint32_t h[NR][4];  // horizontal pyrDown sums of input row r, chroma column j (packed)
 
 #ifndef HIC_ENC_LOAD_AUX
 #define HIC_ENC_LOAD_AUX 0
@@ -314,9 +317,11 @@ struct EncColour {
     const int W = E.W, H = E.H, pitch = 3 * W;
     const int in_row1 = E.in_row0 + E.in_rows;
     const int xs = 512 * s;
-    // byte offset of input row rr (image row y0 + rr - 2, rr = 0 .. 18) in the input
-    // rows, computed by lane rr (read back per row by v_readlane): one reflect-101
-    // step suffices (y0 + 16 <= H, H >= 16), then the shard's clamp
+    // byte offset of input row rr (image row y0 + rr - 2, rr = 0 .. NR - 1) in the
+    // input rows, computed by lane rr (read back per row by v_readlane): one
+    // reflect-101 step suffices for every row a unit uses (its last row <= H, H >=
+    // 16), then the shard's clamp (which also keeps the rows of a missing second
+    // unit, loaded ahead but never used, inside the buffer)
     {
       int sy = y0 + lane - 2;
       sy = sy < 0 ? -sy : (sy >= H ? 2 * H - 2 - sy : sy);
@@ -326,7 +331,7 @@ struct EncColour {
     // edge pixels, packed (cr | cb << 16): lane r converts input row r's x = xs - 2,
     // xs - 1 (or 2, 1 at the left border) and x = xs + 512 (or W - 2 at the right)
     hal_l2 = hal_l1 = hal_r = 0;
-    if (lane < 19) {
+    if (lane < NR) {
       const uint8_t *row = E.rgb + roff;
       const int xl = xs >= 2 ? xs - 2 : 2, xl1 = xs >= 2 ? xs - 1 : 1, xr = xs + 512 < W ? xs + 512 : W - 2;
       const YCC a = rgb2ycc(row[3 * xl], row[3 * xl + 1], row[3 * xl + 2]);
@@ -355,13 +360,15 @@ struct EncColour {
   __device__ __forceinline__ void rows(uint2 (&yq)[16], uint32_t *s_chroma) {
 #pragma unroll
     for (int r = R0; r < R1; ++r) {
-      if (r + kLA < 19) load_row(r + kLA);
+      if (r + kLA < NR) load_row(r + kLA);
       const u32x4 qa = ring_a[r % (kLA + 1)];
       const u32x2 qb = ring_b[r % (kLA + 1)];
       const uint32_t wd[6] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y};
       uint32_t Yh[8], c[8];
       ycc8(wd, K, Yh, c);
-      if (r >= 2 && r < 18) yq[r - 2] = make_uint2(ypack4(Yh, 0), ypack4(Yh, 4));
+      // Y rows of the unit(s): input rows 2 .. NR - 2, slot (r - 2) mod 16 (a slot is
+      // refilled only after the DCT of its block row has read it)
+      if (r >= 2 && r <= NR - 2) yq[(r - 2) & 15] = make_uint2(ypack4(Yh, 0), ypack4(Yh, 4));
       // neighbour pixels x0 - 2, x0 - 1 (left lane) and x0 + 8 (right lane)
       const uint32_t l2 = set_lane<0>(wshr1(c[6]), __builtin_amdgcn_readlane((int)hal_l2, r));
       const uint32_t l1 = set_lane<0>(wshr1(c[7]), __builtin_amdgcn_readlane((int)hal_l1, r));
@@ -379,14 +386,18 @@ struct EncColour {
         // high bytes: x01 = (cr0, cr1, cb0, cb1), x23 = (cr2, cr3, cb2, cb3)
         const uint32_t x01 = __builtin_amdgcn_perm(v[1], v[0], 0x07030501u);
         const uint32_t x23 = __builtin_amdgcn_perm(v[3], v[2], 0x07030501u);
-        s_chroma[i * 64 + lane] = __builtin_amdgcn_perm(x23, x01, 0x05040100u);
-        s_chroma[512 + i * 64 + lane] = __builtin_amdgcn_perm(x23, x01, 0x07060302u);
+        s_chroma[(i & 7) * 64 + lane] = __builtin_amdgcn_perm(x23, x01, 0x05040100u);
+        s_chroma[512 + (i & 7) * 64 + lane] = __builtin_amdgcn_perm(x23, x01, 0x07060302u);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
   }
 };
 
+#ifndef HIC_ENC_VG
+#define HIC_ENC_VG 1  // 16-row units per wave (2: two vertically adjacent units, 35 input rows
+                      // for 32; measured 61-65 vs 60-63 us: no gain, scripts/gpu_r2ah.sh)
+#endif
 template <int TMF, bool NT, bool F32>
 __device__ __forceinline__ void encode420_unit(const Enc420 &E);
 
@@ -416,13 +427,18 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
   uint2 *st2 = s_stage + wv * 64 * kStageU2;
   uint32_t *s_chroma = s_chroma_all[wv];
   int16_t *st = reinterpret_cast<int16_t *>(st2 + lane * kStageU2);
-  const int u = __builtin_amdgcn_readfirstlane(g / E.nstrips), s = __builtin_amdgcn_readfirstlane(g - u * E.nstrips);
-  const int y0 = E.out_row0 + 16 * u;
+  // wave g: strip s, unit rows u0 .. u0 + HIC_ENC_VG - 1 (the last wave of a strip
+  // may have one unit row only)
+  const int p = __builtin_amdgcn_readfirstlane(g / E.nstrips), s = __builtin_amdgcn_readfirstlane(g - p * E.nstrips);
+  const int u0 = HIC_ENC_VG * p;
+  const int y0 = E.out_row0 + 16 * u0;
+  const bool has2 = HIC_ENC_VG == 2 && 16 * (u0 + 1) < E.out_rows;
   const int nbx = E.W >> 3, nbxc = E.W >> 4;
 
   uint2 yq[16];
-  // Y block row br: blocks 64 s .. 64 s + 63 of block row 2u + br (one RLE tile)
-  auto y_blocks = [&](int br) {
+  // Y block row br of unit u: blocks 64 s .. 64 s + 63 of block row 2u + br (one
+  // RLE tile), from yq slots 8 br .. 8 br + 7
+  auto y_blocks = [&](int u, int br) {
     uint2 w[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) w[r] = yq[8 * br + r];
@@ -439,39 +455,9 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
-#if defined(HIC_DEV) && defined(HIC_ENC_DEV) && (HIC_ENC_DEV & 2)
-  // dev timing (results invalid): no colour stage, synthetic pixels
-#pragma unroll
-  for (int r = 0; r < 16; ++r) yq[r] = make_uint2(0x9E3779B1u * (lane + r + g), 0x85EBCA6Bu * (lane ^ r ^ g));
-#pragma unroll
-  for (int i = 0; i < 16; ++i) s_chroma[i * 64 + lane] = 0x01000193u * (lane + i + g);
-  y_blocks(0);
-  y_blocks(1);
-#else
-#ifndef HIC_ENC_SPLIT
-#define HIC_ENC_SPLIT 10
-#endif
-  // Y block row 0 (image rows y0 .. y0 + 7 = input rows 2 .. 9) is transformed
-  // between the colour stage's two row ranges: the loads of input rows 10 ..
-  // 9 + kLA are in flight under its DCT instead of exposed at the unit's start only
-  EncColour C;
-  C.init(E, y0, s, lane);
-  C.rows<0, HIC_ENC_SPLIT>(yq, s_chroma);
-  __builtin_amdgcn_sched_barrier(0);
-  if (HIC_ENC_SPLIT < 19) {
-    y_blocks(0);
-    C.rows<HIC_ENC_SPLIT, 19>(yq, s_chroma);
-    __builtin_amdgcn_sched_barrier(0);
-    y_blocks(1);
-  } else {
-    y_blocks(0);
-    y_blocks(1);
-  }
-#endif
-
-  // ---- chroma: block m of Cr -> lane m, of Cb -> lane 32 + m (block m spans the
-  // chroma columns of lanes 2m and 2m + 1 of this strip), read from the LDS area
-  {
+  // chroma of unit u: block m of Cr -> lane m, of Cb -> lane 32 + m (block m spans
+  // the chroma columns of lanes 2m and 2m + 1 of this strip), read from the LDS area
+  auto c_blocks = [&](int u) {
     __builtin_amdgcn_wave_barrier();
     const uint2 *sc = reinterpret_cast<const uint2 *>(s_chroma + (lane >> 5) * 512) + (lane & 31);
     uint2 w[8];
@@ -486,7 +472,47 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
       enc_stage_row(st2, lane, zw);
       tile_record16_half<TMF>(zw, b0, E.M, E.rec[1] + (b0 >> 5) * 3, E.rec[2] + (b0 >> 5) * 3);
     }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+#if defined(HIC_DEV) && defined(HIC_ENC_DEV) && (HIC_ENC_DEV & 2)
+  // dev timing (results invalid): no colour stage, synthetic pixels
+  for (int k = 0; k < (has2 ? 2 : 1); ++k) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) yq[r] = make_uint2(0x9E3779B1u * (lane + r + g), 0x85EBCA6Bu * (lane ^ r ^ g));
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s_chroma[i * 64 + lane] = 0x01000193u * (lane + i + g);
+    y_blocks(u0 + k, 0);
+    y_blocks(u0 + k, 1);
+    c_blocks(u0 + k);
   }
+#else
+  // Each unit's Y block row 0 is transformed between the colour rows that complete
+  // it and the rest, so the loads of the following rows are in flight under its
+  // DCT.  With two units per wave (HIC_ENC_VG = 2) the second unit reuses the
+  // first one's bottom halo rows: 35 converted input rows for 32 image rows,
+  // against 2 x 19.
+  EncColour<HIC_ENC_VG == 2 ? 35 : 19> C;
+  C.init(E, y0, s, lane);
+  C.template rows<0, 10>(yq, s_chroma);  // input rows 2 .. 9 = unit u0's Y block row 0
+  __builtin_amdgcn_sched_barrier(0);
+  y_blocks(u0, 0);
+  C.template rows<10, 19>(yq, s_chroma);
+  __builtin_amdgcn_sched_barrier(0);
+  y_blocks(u0, 1);
+  c_blocks(u0);  // before the second unit's chroma rows reuse the LDS area
+  if constexpr (HIC_ENC_VG == 2) {
+    if (has2) {
+    C.template rows<19, 26>(yq, s_chroma);  // input rows 18 .. 25 = unit u0 + 1's Y block row 0
+    __builtin_amdgcn_sched_barrier(0);
+    y_blocks(u0 + 1, 0);
+    C.template rows<26, 35>(yq, s_chroma);
+    __builtin_amdgcn_sched_barrier(0);
+    y_blocks(u0 + 1, 1);
+    c_blocks(u0 + 1);
+    }
+  }
+#endif
 }
 
 }  // namespace
@@ -531,7 +557,7 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
   E.rec[2] = static_cast<int64_t *>(ws_cb);
   E.M = max_len;
   E.nstrips = (int)(W / 512);
-  E.nunits = E.nstrips * (int)(out_rows / 16);
+  E.nunits = E.nstrips * (int)((out_rows / 16 + HIC_ENC_VG - 1) / HIC_ENC_VG);  // waves
   // one wave per unit (no persistent loop: units are the same size, and the
   // hardware's dispatch balances the tail better than a fixed split)
   const dim3 grid((unsigned)((E.nunits + 3) / 4)), block(256);

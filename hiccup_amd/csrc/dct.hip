@@ -893,12 +893,14 @@ inline bool aligned(const void *p, uintptr_t a) { return (reinterpret_cast<uintp
 // size (0 = one wave per set).  Set through hic_set_knob (common.hip); the
 // library reads no environment variables.
 inline int dct_path() { return knob(HIC_KNOB_DCT_PATH); }
-inline int dct_waves_per_cu() {
+inline int dct_waves_per_cu(int njobs) {
   const int v = knob(HIC_KNOB_DCT_WAVES_PER_CU);
-  // float64 path: one wave per set (the hardware's dispatch balances the tail:
-  // 8K planes 37.6 us vs 40.0-40.6 for 12 persistent waves per CU, luma equal;
-  // scripts/gpu_r2ad.sh); the float32 path keeps its persistent queue
-  return v >= 0 ? v : (dct_path() == 3 ? 16 : 0);
+  // float64 path: one wave per set for a multi-plane launch (the hardware's dispatch
+  // balances the planes' mixed tail: 8K Y + Cr + Cb 37.5 us vs 39.7 for 12
+  // persistent waves per CU), 12 persistent waves per CU for one plane (4K luma
+  // 13.4 vs 13.8 us, 8K luma 27.4 vs 27.8; scripts/gpu_r2aj.sh); the float32 path
+  // keeps its persistent queue
+  return v >= 0 ? v : (dct_path() == 3 ? 16 : (njobs > 1 ? 0 : 12));
 }
 
 inline bool fwd_fast(int H, int W, int64_t stride, const void *plane, const void *out) {
@@ -914,7 +916,7 @@ int launch_planes(DctJobs &jobs, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     total += jobs.j[k].nsets;
   }
   jobs.total_sets = total;
-  int cap = dct_waves_per_cu() * cu_count();
+  int cap = dct_waves_per_cu(jobs.n) * cu_count();
   if (cap > 0 && (total + cap - 1) / cap > 64) cap = (total + 63) / 64;  // <= 64 sets per wave (redo mask)
   const int waves = (cap == 0 || total < cap) ? total : cap;
   const dim3 grid((waves + 3) / 4), block(256);

@@ -17,8 +17,10 @@ def main():
         with _lib.knobs(**kw):
             a = bench.extra_8k_plane_dct()
             b = bench.extra_8k_plane_dct(luma_only=True)
-        print("%-28s %-24s planes %7.2f us (%.3f)  luma %7.2f us (%.3f)" % (
-            lib, label, a["median_launch_us"], a["frac"], b["median_launch_us"], b["frac"]), flush=True)
+            c = bench.extra_4k_luma()
+        print("%-28s %-24s planes %7.2f us (%.3f)  luma %7.2f us (%.3f)  4k %7.2f us (%.3f)" % (
+            lib, label, a["median_launch_us"], a["frac"], b["median_launch_us"], b["frac"], c["avg_launch_us"],
+            c["frac"]), flush=True)
 
 
 if __name__ == "__main__":

@@ -394,6 +394,9 @@ struct EncColour {
   }
 };
 
+#ifndef HIC_ENC_WPB
+#define HIC_ENC_WPB 4  // waves per workgroup
+#endif
 #ifndef HIC_ENC_VG
 #define HIC_ENC_VG 1  // 16-row units per wave (2: two vertically adjacent units, 35 input rows
                       // for 32; measured 61-65 vs 60-63 us: no gain, scripts/gpu_r2ah.sh)
@@ -409,20 +412,20 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E);
 // emit re-reads them (emit 59.7 -> 54.7 us; 8K encode +2-4 %, scripts/gpu_r2i.sh)
 // F32: the float32 DCT variant (knob "encode_dct" = 1, enc_dct_f32)
 template <int TMF, bool NT, bool F32>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_encode420(Enc420 E) {
+__global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_eu(3))) void k_encode420(Enc420 E) {
   encode420_unit<TMF, NT, F32>(E);
 }
 template <int TMF, bool NT, bool F32>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_encode420_w2(Enc420 E) {
+__global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_eu(2))) void k_encode420_w2(Enc420 E) {
   encode420_unit<TMF, NT, F32>(E);
 }
 
 template <int TMF, bool NT, bool F32>
 __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
-  __shared__ uint2 s_stage[4 * 64 * kStageU2];
-  __shared__ uint32_t s_chroma_all[4][2 * 8 * 64];
+  __shared__ uint2 s_stage[HIC_ENC_WPB * 64 * kStageU2];
+  __shared__ uint32_t s_chroma_all[HIC_ENC_WPB][2 * 8 * 64];
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wv);
+  const int g = __builtin_amdgcn_readfirstlane(blockIdx.x * HIC_ENC_WPB + wv);
   if (g >= E.nunits) return;  // wave-uniform
   uint2 *st2 = s_stage + wv * 64 * kStageU2;
   uint32_t *s_chroma = s_chroma_all[wv];
@@ -560,7 +563,7 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
   E.nunits = E.nstrips * (int)((out_rows / 16 + HIC_ENC_VG - 1) / HIC_ENC_VG);  // waves
   // one wave per unit (no persistent loop: units are the same size, and the
   // hardware's dispatch balances the tail better than a fixed split)
-  const dim3 grid((unsigned)((E.nunits + 3) / 4)), block(256);
+  const dim3 grid((unsigned)((E.nunits + HIC_ENC_WPB - 1) / HIC_ENC_WPB)), block(64 * HIC_ENC_WPB);
   hipStream_t s = as_stream(stream);
   hipEvent_t e0 = static_cast<hipEvent_t>(ev_start), e1 = static_cast<hipEvent_t>(ev_stop);
   // knob encode_lds_pad: reserve extra LDS per workgroup (fewer encode workgroups

@@ -918,6 +918,56 @@ __global__ __launch_bounds__(kScanT) void k_scan_inplace(int64_t *__restrict__ v
   if (threadIdx.x == 0) *out_total = run;
 }
 
+// Multi-workgroup form of k_scan_inplace for long sequences (a 16K luma plane has
+// ~65k symbol tiles, 8 serial passes of the one-workgroup scan, ~56 us): one
+// workgroup per kScanT * kScanK chunk sums its chunk into part[chunk]; part is
+// scanned by k_scan_inplace; each chunk is then scanned from its offset.
+__global__ __launch_bounds__(kScanT) void k_scan_chunk_sum(const int64_t *__restrict__ v, int64_t n,
+                                                           int64_t *__restrict__ part) {
+  __shared__ int64_t s_buf[32];
+  const int64_t i0 = (int64_t)blockIdx.x * kScanT * kScanK + (int64_t)threadIdx.x * kScanK;
+  int64_t sum = 0;
+#pragma unroll
+  for (int k = 0; k < kScanK; ++k) sum += i0 + k < n ? v[i0 + k] : 0;
+  int64_t tot;
+  block_excl_sum<int64_t, kScanT>(sum, s_buf, tot);
+  if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kScanT) void k_scan_chunk_apply(int64_t *__restrict__ v, int64_t n,
+                                                             const int64_t *__restrict__ part) {
+  __shared__ int64_t s_buf[32];
+  const int64_t i0 = (int64_t)blockIdx.x * kScanT * kScanK + (int64_t)threadIdx.x * kScanK;
+  int64_t x[kScanK], sum = 0;
+#pragma unroll
+  for (int k = 0; k < kScanK; ++k) {
+    x[k] = i0 + k < n ? v[i0 + k] : 0;
+    sum += x[k];
+  }
+  int64_t tot;
+  int64_t e = part[blockIdx.x] + block_excl_sum<int64_t, kScanT>(sum, s_buf, tot);
+#pragma unroll
+  for (int k = 0; k < kScanK; ++k) {
+    if (i0 + k < n) v[i0 + k] = e;
+    e += x[k];
+  }
+}
+
+// Exclusive scan of v[0, n) in place, total to *out_total.  `part` needs
+// ceil(n / (kScanT * kScanK)) int64 slots when n exceeds one chunk (else unused).
+int scan_inplace(int64_t *v, int64_t n, int64_t *out_total, int64_t *part, hipStream_t s) {
+  constexpr int64_t kChunk = (int64_t)kScanT * kScanK;
+  if (n <= kChunk || !part) {
+    hipLaunchKernelGGL(k_scan_inplace, dim3(1), dim3(kScanT), 0, s, v, n, out_total);
+    return check_launch("k_scan_inplace");
+  }
+  const int64_t g = (n + kChunk - 1) / kChunk;
+  hipLaunchKernelGGL(k_scan_chunk_sum, dim3((unsigned)g), dim3(kScanT), 0, s, v, n, part);
+  hipLaunchKernelGGL(k_scan_inplace, dim3(1), dim3(kScanT), 0, s, part, g, out_total);
+  hipLaunchKernelGGL(k_scan_chunk_apply, dim3((unsigned)g), dim3(kScanT), 0, s, v, n, part);
+  return check_launch("k_scan_chunk_apply");
+}
+
 template <typename L_T, typename V_T, typename T>
 __global__ __launch_bounds__(kTB) void k_rld_scatter(const L_T *__restrict__ sym_len, const V_T *__restrict__ sym_val,
                                                      int64_t nsym, const int64_t *__restrict__ tile_off, StreamGeo g,
@@ -1373,7 +1423,9 @@ int rle_decode_blocks16(const uint8_t *sym_len, const int16_t *sym_val, int64_t 
     hipLaunchKernelGGL(k_rld_tile16, dim3((unsigned)nts), dim3(kTB), 0, s, sym_len, nsym, tsum);
     if (int e = check_launch("k_rld_tile16")) return e;
   }
-  hipLaunchKernelGGL(k_scan_inplace, dim3(1), dim3(kScanT), 0, s, tsum, nts, tot);
+  // chunk partials in the tsum slots past nts (the region is sized for kTS tiles,
+  // twice the count of kDTS tiles, so ceil(nts / 8192) <= nts slots are free there)
+  if (int e = scan_inplace(tsum, nts, tot, tsum + nts, s)) return e;
   hipLaunchKernelGGL(k_dc_tile, dim3((unsigned)ntb), dim3(kTB), 0, s, dc_diff, nblk, dsum);
   hipLaunchKernelGGL(k_scan_inplace, dim3(1), dim3(kScanT), 0, s, dsum, ntb, tot + 1);
   hipLaunchKernelGGL(k_dc_values16, dim3((unsigned)ntb), dim3(kTB), 0, s, dc_diff, nblk, dsum, stitch, dcval);

@@ -69,15 +69,18 @@ def _decode_i16_call(L, V, dc, nblk):
     return device.to_host(blocks), int(status.cpu()[0])
 
 
-@pytest.mark.parametrize("kind", ["dense", "sparse", "zero", "last_only", "first_only", "striped", "no_eob"])
+@pytest.mark.parametrize("kind", ["dense", "sparse", "zero", "last_only", "first_only", "striped", "no_eob",
+                                  "dense_long"])
 def test_rle_decode_blocks_hot_path(kind, monkeypatch):
     """hic_rle_decode_i16's block-assembling path (LDS windows over 4096-symbol
     tiles, edge blocks shared between tiles, EOB tail fill) against the oracle's
-    streams (codec.py:55-113) and against the generic scatter path."""
+    streams (codec.py:55-113) and against the generic scatter path.  dense_long:
+    37.8M symbols, 9.2k symbol tiles, past one 8192-tile chunk of the tile-offset
+    scan, so the multi-workgroup scan runs."""
     rng = np.random.default_rng(len(kind))
-    nblk = 5000
+    nblk = 600_000 if kind == "dense_long" else 5000
     zz = np.zeros((nblk, 64), np.int32)
-    if kind == "dense":
+    if kind in ("dense", "dense_long"):
         zz[:] = rng.integers(-40, 41, (nblk, 64))
     elif kind == "sparse":  # runs far longer than a window, crossing tiles
         m = rng.random((nblk, 64)) < 0.004

@@ -347,7 +347,47 @@ __global__ void k_ycrcb420_rgb(const uint8_t *__restrict__ Y, int64_t ystride, c
 // by DPP wave shifts (the strip-edge lanes load them).  The vertical taps run over
 // a 3-row register window.  Edges as pyr_up_at: reflect-101 left / top, replicate
 // right / bottom.
+//
+// Arithmetic (VALU-bound before: 37 ops and 2 quarter-rate multiplies per pixel):
+// Cr and Cb travel as one packed pair (cr | cb << 16) through both filters
+// (v_pk_mad_u16 / v_pk_add_u16, mod 2^16); every horizontal value carries a bias
+// of -1020, so the vertical sum (weights 8 x 8) is v + 32 - 8192, in [-8160,
+// 8160], and one v_pk_ashrrev_i16 by 6 gives both (cr - 128, cb - 128) exactly as
+// sat8((v + 32) >> 6) - 128 (v <= 64 * 255, no saturation).  Each colour channel
+// is then one v_dot2_i32_i16 of that pair with (kCR2x, kCB2x) accumulated onto
+// y << 14 | 8192: y + descale14(...) == (y * 2^14 + 8192 + ...) >> 14 since
+// y * 2^14 is a multiple of 2^14.  ~18 VALU per pixel.
 constexpr int kUpSeg = 8;
+
+typedef unsigned short u16x2c __attribute__((ext_vector_type(2)));
+typedef short s16x2c __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2c, a) + __builtin_bit_cast(u16x2c, b));
+}
+__device__ __forceinline__ uint32_t pk_mad_u16(uint32_t a, uint32_t k, uint32_t c) {  // a * k + c per half
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2c, a) * __builtin_bit_cast(u16x2c, k) +
+                                          __builtin_bit_cast(u16x2c, c));
+}
+__device__ __forceinline__ uint32_t pk_sra6(uint32_t a) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2c, a) >> (short)6);
+}
+// acc + lo(crcb) * lo(k) + hi(crcb) * hi(k), signed 16-bit halves; the
+// three-operand form (k in an SGPR), so no copy of acc per channel
+__device__ __forceinline__ int ycc_dot(uint32_t crcb, uint32_t k, int acc) {
+  int d;
+  asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(crcb), "s"(k), "v"(acc));
+  return d;
+}
+__device__ __forceinline__ uint32_t sreg(uint32_t k) {  // opaque wave-uniform constant
+  asm volatile("" : "+s"(k));
+  return k;
+}
+// low 16 bits: sat8(a >> 14) | sat8(b >> 14) << 8 (gfx950 v_ashr_pk_u8_i32)
+__device__ __forceinline__ uint32_t sat_pk2(int a, int b) {
+  uint32_t d;
+  asm("v_ashr_pk_u8_i32 %0, %1, %2, 14" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
 
 // Row-range form (a tile shard's decode, sharding.ShardDecoder): chroma rows
 // [sb, se) of an h-row image are produced, i.e. output rows [2 sb, 2 se); Y and rgb
@@ -360,7 +400,8 @@ __global__ __launch_bounds__(256) void k_ycrcb420_rgb_walk(const uint8_t *__rest
                                                            int sb, int se, int c_row0,
                                                            uint8_t *__restrict__ rgb, int nstrips, int nwaves) {
   const int lane = threadIdx.x & 63;
-  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // wave-uniform (readfirstlane): row offsets and the loop count stay scalar
+  const int wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (wid >= nwaves) return;
   const int seg = wid / nstrips, strip = wid - seg * nstrips;
   const int nq = w >> 1;
@@ -369,69 +410,99 @@ __global__ __launch_bounds__(256) void k_ycrcb420_rgb_walk(const uint8_t *__rest
   const int qc = owner ? q : nq - 1;
   const int s0 = sb + seg * kUpSeg;
   const int ns = se - s0 < kUpSeg ? se - s0 : kUpSeg;
-  // horizontally filtered chroma row r: [cr x4 | cb x4] for output columns 4q..4q+3 (x8 scale)
-  auto hrow = [&](int r, int (&hc)[4], int (&hb)[4]) {
-    const int64_t o = (int64_t)(r - c_row0) * w + 2 * qc;
-    const uint32_t cr2 = *reinterpret_cast<const uint16_t *>(Cr + o);
-    const uint32_t cb2 = *reinterpret_cast<const uint16_t *>(Cb + o);
-    const uint32_t own = cr2 | cb2 << 16;  // cr[2q], cr[2q+1], cb[2q], cb[2q+1]
-    uint32_t lft = shr1(own), rgt = shl1(own);
-    int crl = (int)((lft >> 8) & 255), cbl = (int)(lft >> 24);  // column 2q-1
-    int crr = (int)(rgt & 255), cbr = (int)((rgt >> 16) & 255);  // column 2q+2
-    const int c0 = (int)(cr2 & 255), c1 = (int)(cr2 >> 8), b0 = (int)(cb2 & 255), b1 = (int)(cb2 >> 8);
-    if (qc == 0) {  // reflect-101: column -1 -> 1
-      crl = c1;
-      cbl = b1;
-    } else if (lane == 0) {
-      crl = Cr[o - 1];
-      cbl = Cb[o - 1];
-    }
-    if (qc == nq - 1) {  // replicate: column w -> w - 1
-      crr = c1;
-      cbr = b1;
-    } else if (lane == 63) {
-      crr = Cr[o + 2];
-      cbr = Cb[o + 2];
-    }
-    hc[0] = crl + 6 * c0 + c1;
-    hc[1] = 4 * (c0 + c1);
-    hc[2] = c0 + 6 * c1 + crr;
-    hc[3] = 4 * (c1 + crr);
-    hb[0] = cbl + 6 * b0 + b1;
-    hb[1] = 4 * (b0 + b1);
-    hb[2] = b0 + 6 * b1 + cbr;
-    hb[3] = 4 * (b1 + cbr);
+  constexpr uint32_t K4 = 0x00040004u, K6 = 0x00060006u;
+  constexpr uint32_t KB = 0xFC04FC04u;  // -1020 per half
+  // (kCR2x | kCB2x << 16) in SGPRs: the three-operand v_dot2_i32_i16 then needs no
+  // accumulator copies (its two-operand form with a literal does)
+  const uint32_t kr = sreg((uint32_t)(uint16_t)kCR2R), kg = sreg((uint32_t)(uint16_t)kCR2G | (uint32_t)kCB2G << 16),
+                 kb = sreg((uint32_t)kCB2B << 16);
+  // row bases wave-uniform (scalar), lane offsets 32-bit.  Every lane also loads one
+  // more chroma pair: lane 0 the pair left of its own (column 2q-1), lane 63 the pair
+  // right of it (column 2q+2), the others a clamped dummy -- no divergent branch,
+  // so the loads of row s+2 and of the next two Y rows are issued a whole
+  // iteration before their use (software pipelining; each wave otherwise waits
+  // out every load)
+  const uint32_t qo = 2u * (uint32_t)qc;
+  const uint32_t qe = lane == 0 ? (qo >= 2 ? qo - 2 : 0) : (qo + 2 <= (uint32_t)w - 2 ? qo + 2 : (uint32_t)w - 2);
+  const uint32_t esel = lane == 0 ? 0x0C050C01u : 0x0C040C00u;
+  struct Raw {
+    uint32_t cr, cb, cre, cbe;
   };
-  int pc[4], pb[4], cc[4], cb[4], nc[4], nb[4];
-  hrow(s0 > 0 ? s0 - 1 : (h > 1 ? 1 : 0), pc, pb);
-  hrow(s0, cc, cb);
+  auto fetch = [&](int r) {
+    const int64_t ro = (int64_t)(r - c_row0) * w;
+    const uint8_t *crr = Cr + ro, *cbr = Cb + ro;
+    Raw x;
+    x.cr = *reinterpret_cast<const uint16_t *>(crr + qo);
+    x.cb = *reinterpret_cast<const uint16_t *>(cbr + qo);
+    x.cre = *reinterpret_cast<const uint16_t *>(crr + qe);
+    x.cbe = *reinterpret_cast<const uint16_t *>(cbr + qe);
+    return x;
+  };
+  // horizontally filtered chroma row, packed (cr | cb << 16) + bias, for output
+  // columns 4q .. 4q+3 (x8 scale)
+  auto filter = [&](const Raw &x, uint32_t (&hv)[4]) {
+    const uint32_t p0 = __builtin_amdgcn_perm(x.cb, x.cr, 0x0C040C00u);  // column 2q:   cr | cb << 16
+    const uint32_t p1 = __builtin_amdgcn_perm(x.cb, x.cr, 0x0C050C01u);  // column 2q+1
+    const uint32_t e = __builtin_amdgcn_perm(x.cbe, x.cre, esel);        // 2q-1 (lane 0) / 2q+2 (lane 63)
+    uint32_t l = shr1(p1), rr = shl1(p0);                                // columns 2q-1, 2q+2
+    l = lane == 0 ? e : l;
+    rr = lane == 63 ? e : rr;
+    l = qc == 0 ? p1 : l;        // reflect-101: column -1 -> 1
+    rr = qc == nq - 1 ? p1 : rr;  // replicate: column w -> w - 1
+    hv[0] = pk_mad_u16(p0, K6, pk_add_u16(l, pk_add_u16(p1, KB)));
+    hv[1] = pk_mad_u16(pk_add_u16(p0, p1), K4, KB);
+    hv[2] = pk_mad_u16(p1, K6, pk_add_u16(rr, pk_add_u16(p0, KB)));
+    hv[3] = pk_mad_u16(pk_add_u16(p1, rr), K4, KB);
+  };
+  auto yrow = [&](int oy) {  // output row oy (relative to 2 sb): 4 Y bytes
+    return *reinterpret_cast<const uint32_t *>(Y + (int64_t)oy * ystride + 2 * qo);
+  };
+  uint32_t pv[4], cv[4], nv[4];
+  filter(fetch(s0 > 0 ? s0 - 1 : (h > 1 ? 1 : 0)), pv);
+  filter(fetch(s0), cv);
+  Raw rn = fetch(s0 + 1 < h ? s0 + 1 : h - 1);
+  uint32_t yq[2] = {yrow(2 * (s0 - sb)), yrow(2 * (s0 - sb) + 1)};
   for (int k = 0; k < ns; ++k) {
     const int s = s0 + k;
-    hrow(s + 1 < h ? s + 1 : h - 1, nc, nb);
+    filter(rn, nv);
+    // prefetch for iteration k + 1 (rows inside the shard's halo: s + 2 <= se)
+    uint32_t yn[2] = {yq[0], yq[1]};
+    if (k + 1 < ns) {
+      rn = fetch(s + 2 < h ? s + 2 : h - 1);
+      yn[0] = yrow(2 * (s + 1 - sb));
+      yn[1] = yrow(2 * (s + 1 - sb) + 1);
+    }
 #pragma unroll
     for (int odd = 0; odd < 2; ++odd) {
       const int oy = 2 * (s - sb) + odd;  // output row, relative to 2 sb
-      const uint32_t yq = *reinterpret_cast<const uint32_t *>(Y + (int64_t)oy * ystride + 4 * qc);
-      uint32_t px[4];
+      int R[4], G[4], B[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int vcr = odd ? 4 * (cc[j] + nc[j]) : pc[j] + 6 * cc[j] + nc[j];
-        const int vcb = odd ? 4 * (cb[j] + nb[j]) : pb[j] + 6 * cb[j] + nb[j];
-        const int cr = (int)sat8((vcr + 32) >> 6) - 128, cbv = (int)sat8((vcb + 32) >> 6) - 128;
-        const int yv = (int)((yq >> (8 * j)) & 255);
-        px[j] = sat8(yv + descale14(cr * kCR2R)) | sat8(yv + descale14(cbv * kCB2G + cr * kCR2G)) << 8 |
-                sat8(yv + descale14(cbv * kCB2B)) << 16;
+        const uint32_t v = odd ? pk_mad_u16(pk_add_u16(cv[j], nv[j]), K4, 0) : pk_mad_u16(cv[j], K6, pk_add_u16(pv[j], nv[j]));
+        const uint32_t crcb = pk_sra6(v);  // (cr - 128, cb - 128), signed
+        const int acc = (int)(((yq[odd] >> (8 * j)) & 255) << 14 | 8192);
+        R[j] = ycc_dot(crcb, kr, acc);
+        G[j] = ycc_dot(crcb, kg, acc);
+        B[j] = ycc_dot(crcb, kb, acc);
       }
       if (owner) {
-        uint32_t *o = reinterpret_cast<uint32_t *>(rgb + ((int64_t)oy * 2 * w + 4 * q) * 3);
-        const uint3 v = make_uint3(px[0] | px[1] << 24, (px[1] >> 8) | px[2] << 16, (px[2] >> 16) | px[3] << 8);
+        uint32_t *o = reinterpret_cast<uint32_t *>(rgb + (int64_t)oy * 6 * w + 12u * (uint32_t)q);
+        // sat8(x >> 14) of channel pairs, two bytes per v_ashr_pk_u8_i32; its upper
+        // half is not relied on (the halves are joined by v_perm)
+        auto join = [](uint32_t lo, uint32_t hi) { return __builtin_amdgcn_perm(hi, lo, 0x05040100u); };
+        const uint3 v = make_uint3(join(sat_pk2(R[0], G[0]), sat_pk2(B[0], R[1])),
+                                   join(sat_pk2(G[1], B[1]), sat_pk2(R[2], G[2])),
+                                   join(sat_pk2(B[2], R[3]), sat_pk2(G[3], B[3])));
         *reinterpret_cast<uint3 *>(o) = v;
       }
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      pc[j] = cc[j]; pb[j] = cb[j]; cc[j] = nc[j]; cb[j] = nb[j];
+      pv[j] = cv[j];
+      cv[j] = nv[j];
     }
+    yq[0] = yn[0];
+    yq[1] = yn[1];
   }
 }
 

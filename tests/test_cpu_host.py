@@ -228,3 +228,15 @@ def test_fused_colour_arithmetic_exhaustive():
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     assert mod.check()
+
+
+def test_decode_colour_arithmetic_exhaustive():
+    """color.hip's decode colour arithmetic (packed biased pyrUp sums, v_dot2 per
+    channel) equals the oracle's pyrUp rounding and YCrCb2RGB on every input
+    (tools/check/colour_decode_dot2.py)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "colour_decode_dot2", os.path.join(os.path.dirname(__file__), "..", "tools", "check", "colour_decode_dot2.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    assert mod.check()

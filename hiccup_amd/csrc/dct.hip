@@ -144,6 +144,20 @@ __global__ __launch_bounds__(256) void k_dct_quant(const uint8_t *__restrict__ p
 }
 
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ double sreg_f64(double k) {  // opaque wave-uniform constant
+  asm volatile("" : "+s"(k));
+  return k;
+}
+__device__ __forceinline__ double vreg_f64(double k) {
+  asm volatile("" : "+v"(k));
+  return k;
+}
+__device__ __forceinline__ double fma_scale_add(double y, double k_s, double c_v) {  // fl(y * k + c), one rounding
+  double d;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(y), "s"(k_s), "v"(c_v));
+  return d;
+}
+
 template <int TABLE, int LAYOUT, bool FAST>
 __global__ __launch_bounds__(256) void k_dequant_idct(const void *__restrict__ coef, int H, int W,
                                                       int nbx, int nblk, uint8_t *__restrict__ out,
@@ -213,7 +227,11 @@ __global__ __launch_bounds__(256) void k_dequant_idct(const void *__restrict__ c
     for (int v = 0; v < 8; ++v) c[v] = q[u * 8 + v] * QT[TABLE][u * 8 + v];
     idct8<int>(c, a[u]);
   }
-  // column pass, /256 (exact) + 128, truncate toward zero, wrap mod 256
+  // column pass, /256 (exact) + 128, truncate toward zero, wrap mod 256.  The
+  // constants live in registers (2^-8 an SGPR pair, 128 a VGPR pair) for a
+  // three-address v_fma_f64: LLVM's v_fmac_f64 form overwrote its accumulator,
+  // so it re-materialised 128.0 (two v_mov_b32) before each of the 64 fmas
+  const double k2m8 = sreg_f64(0x1p-8), k128 = vreg_f64(128.0);
   uint32_t px[16];  // row r: bytes v = 0..3 in px[2r], 4..7 in px[2r+1]
 #pragma unroll
   for (int k = 0; k < 16; ++k) px[k] = 0;
@@ -225,15 +243,15 @@ __global__ __launch_bounds__(256) void k_dequant_idct(const void *__restrict__ c
     idct8<double>(xc, yv);
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-      const double p = __builtin_fma(yv[r], 0x1p-8, 128.0);  // == fl(y/256 + 128): y*2^-8 exact
+      const double p = fma_scale_add(yv[r], k2m8, k128);  // == fl(y/256 + 128): y*2^-8 exact
       const uint32_t b = (uint32_t)__double2int_rz(p) & 0xFFu;
       px[2 * r + (v >> 2)] |= b << (8 * (v & 3));
     }
   }
   if (FAST) {
+    uint8_t *o = out + (int64_t)y0 * ostride + x0;  // one 64-bit multiply; rows step by the uniform stride
 #pragma unroll
-    for (int r = 0; r < 8; ++r)
-      *reinterpret_cast<uint2 *>(out + (int64_t)(y0 + r) * ostride + x0) = make_uint2(px[2 * r], px[2 * r + 1]);
+    for (int r = 0; r < 8; ++r) *reinterpret_cast<uint2 *>(o + r * ostride) = make_uint2(px[2 * r], px[2 * r + 1]);
   } else {
 #pragma unroll
     for (int r = 0; r < 8; ++r)

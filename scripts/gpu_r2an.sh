@@ -1,4 +1,4 @@
-# dequant + IDCT: three-address fma epilogue and hoisted row addresses vs the previous build
+# dequant + IDCT: persistent LDS-DMA prefetching zig-zag kernel vs the previous build
 set -u
 run() { timeout -k 10 "$@"; rc=$?; echo "rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi; }
 mkdir -p gpurun_out

@@ -126,6 +126,77 @@ __global__ __launch_bounds__(256) void k_rgb_ycrcb420(const uint8_t *__restrict_
 // itself (x = -2, -1 -> 2, 1; x = W -> W - 2).
 constexpr int kStripQ = 64;
 
+typedef unsigned short u16x2c __attribute__((ext_vector_type(2)));
+typedef short s16x2c __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2c, a) + __builtin_bit_cast(u16x2c, b));
+}
+__device__ __forceinline__ uint32_t pk_mad_u16(uint32_t a, uint32_t k, uint32_t c) {  // a * k + c per half
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2c, a) * __builtin_bit_cast(u16x2c, k) +
+                                          __builtin_bit_cast(u16x2c, c));
+}
+__device__ __forceinline__ uint32_t pk_sra6(uint32_t a) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2c, a) >> (short)6);
+}
+// acc + lo(crcb) * lo(k) + hi(crcb) * hi(k), signed 16-bit halves; the
+// three-operand form (k in an SGPR), so no copy of acc per channel
+__device__ __forceinline__ int ycc_dot(uint32_t crcb, uint32_t k, int acc) {
+  int d;
+  asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(crcb), "s"(k), "v"(acc));
+  return d;
+}
+__device__ __forceinline__ uint32_t sreg(uint32_t k) {  // opaque wave-uniform constant
+  asm volatile("" : "+s"(k));
+  return k;
+}
+// low 16 bits: sat8(a >> 14) | sat8(b >> 14) << 8 (gfx950 v_ashr_pk_u8_i32)
+__device__ __forceinline__ uint32_t sat_pk2(int a, int b) {
+  uint32_t d;
+  asm("v_ashr_pk_u8_i32 %0, %1, %2, 14" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+
+
+// [1 4 6 4 1] over five packed taps (k4 = 4 | 4 << 16, k6 = 6 | 6 << 16, registers:
+// a literal 4 is strength-reduced to a shift and an add)
+__device__ __forceinline__ uint32_t pk_taps5(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e, uint32_t k4,
+                                             uint32_t k6) {
+  return pk_mad_u16(c, k6, pk_mad_u16(pk_add_u16(b, d), k4, pk_add_u16(a, e)));
+}
+__device__ __forceinline__ uint32_t vreg(uint32_t k) {  // a constant held in a VGPR
+  asm volatile("" : "+v"(k));
+  return k;
+}
+
+// cvtColor RGB2YCrCb of the 4 pixels in 12 RGB bytes w[0..2] on the dot-product
+// unit -- the fused encoder's ycc8 (encode.hip) for 4 pixels, equal to rgb2ycc on
+// all 2^24 inputs (tools/check/colour_dot4.py): y in byte 1 of Yh[k], c[k] = Cr |
+// Cb << 16.
+constexpr uint32_t kYLo4 = 140u | 68u << 8 | 48u << 16, kYHi4 = 76u | 150u << 8 | 29u << 16;
+constexpr int kCr4x = 4 * kYCRI, kCb4x = 4 * kYCBI, kCC4x = 4 * ((128 << 14) + (1 << 13));
+struct YccK4 {
+  uint32_t lo0, lo1, hi0, hi1, acc, cc4;
+};
+__device__ __forceinline__ void ycc4(uint32_t w0, uint32_t w1, uint32_t w2, const YccK4 &K, uint32_t (&Yh)[4],
+                                     uint32_t (&c)[4]) {
+  const uint32_t x[4] = {w0, __builtin_amdgcn_alignbyte(w1, w0, 3), __builtin_amdgcn_alignbyte(w2, w1, 2), w2};
+  uint32_t L[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) L[k] = __builtin_amdgcn_udot4(x[k], k == 3 ? K.lo1 : K.lo0, K.acc, false);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) Yh[k] = __builtin_amdgcn_udot4(x[k], k == 3 ? K.hi1 : K.hi0, L[k] >> 8, false);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int sh = k == 3 ? 8 : 0;
+    const int y = (int)((Yh[k] >> 8) & 255u);
+    const int r = (int)((x[k] >> sh) & 255u), b = (int)((x[k] >> (sh + 16)) & 255u);
+    int vr = (r - y) * kCr4x + (int)K.cc4, vb = (b - y) * kCb4x + (int)K.cc4;
+    vr = vr < 0 ? 0 : (vr > 0xFFFFFF ? 0xFFFFFF : vr);
+    vb = vb < 0 ? 0 : (vb > 0xFFFFFF ? 0xFFFFFF : vb);
+    c[k] = __builtin_amdgcn_perm((uint32_t)vb, (uint32_t)vr, 0x07060302u);
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ void st_plane(T *p, T v, bool nt) {
   if (nt)
@@ -176,22 +247,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kSegC == 8 
       raw[r][2] = p[2];
     }
   }
-  // halo of row `lane`: left = (cr, cr, cb, cb) of x0-2, x0-1; right = (cr, cb) of x0+256
-  uint32_t hal_l = 0, hal_r = 0;
+  // halo of row `lane`, packed Cr | Cb << 16: x0-2, x0-1 (left) and x0+256 (right)
+  uint32_t hal_l2 = 0, hal_l1 = 0, hal_r = 0;
   if (lane < nr) {
     const uint8_t *row = src_row(lane);
     const int x0 = 4 * q0;
     if (x0 >= 2) {
       const uint8_t *p = row + 3 * (x0 - 2);
       const YCC a = rgb2ycc(p[0], p[1], p[2]), b = rgb2ycc(p[3], p[4], p[5]);
-      hal_l = pack4(a.cr, b.cr, a.cb, b.cb);
+      hal_l2 = a.cr | a.cb << 16;
+      hal_l1 = b.cr | b.cb << 16;
     }
     if (x0 + 256 < W) {
       const uint8_t *p = row + 3 * (x0 + 256);
       const YCC c = rgb2ycc(p[0], p[1], p[2]);
-      hal_r = c.cr | c.cb << 8;
+      hal_r = c.cr | c.cb << 16;
     }
   }
+  const YccK4 K{sreg(kYLo4), sreg(kYLo4 << 8), sreg(kYHi4), sreg(kYHi4 << 8), vreg(32768u), vreg((uint32_t)kCC4x)};
+  const uint32_t k4 = sreg(0x00040004u), k6 = sreg(0x00060006u), k128 = 0x00800080u;
   // Interior waves (a full segment clear of the image / shard top and bottom, a
   // full strip that is neither the first nor the last) run a variant with no
   // per-lane conditions: every row's Y store and every chroma store is decided at
@@ -201,23 +275,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kSegC == 8 
                         gy0 >= out_row0 && strip > 0 && q0 + 64 < nq;
   auto body = [&](auto edge_tag) {
     constexpr bool EDGE = decltype(edge_tag)::value;
-    int hcr0[kSegR], hcr2[kSegR], hcb0[kSegR], hcb2[kSegR];
+    // horizontally filtered rows, packed Cr | Cb << 16: chroma columns 2q (h0) and
+    // 2q+1 (h2); one v_pk op filters both planes (sums <= 16 * 255, and the
+    // vertical pass's <= 65280 + 128 fits 16 bits too)
+    uint32_t h0[kSegR], h2[kSegR];
 #pragma unroll
     for (int r = 0; r < kSegR; ++r) {
       if (EDGE && r >= nr) continue;
-      const uint32_t w0 = raw[r][0], w1 = raw[r][1], w2 = raw[r][2];
-      const int px[12] = {(int)(w0 & 255), (int)((w0 >> 8) & 255), (int)((w0 >> 16) & 255), (int)(w0 >> 24),
-                          (int)(w1 & 255), (int)((w1 >> 8) & 255), (int)((w1 >> 16) & 255), (int)(w1 >> 24),
-                          (int)(w2 & 255), (int)((w2 >> 8) & 255), (int)((w2 >> 16) & 255), (int)(w2 >> 24)};
-      int cr[4], cb[4];
-      uint32_t yq = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const YCC c = rgb2ycc(px[3 * k], px[3 * k + 1], px[3 * k + 2]);
-        yq |= c.y << (8 * k);
-        cr[k] = (int)c.cr;
-        cb[k] = (int)c.cb;
-      }
+      uint32_t Yh[4], c[4];
+      ycc4(raw[r][0], raw[r][1], raw[r][2], K, Yh, c);
+      const uint32_t yq = __builtin_amdgcn_perm(__builtin_amdgcn_perm(Yh[3], Yh[2], 0x0C0C0501u),
+                                                __builtin_amdgcn_perm(Yh[1], Yh[0], 0x0C0C0501u), 0x05040100u);
       const int gy = gy0 + r;
       if (EDGE) {
         if (owner && gy >= yw0 && gy < yw1)
@@ -226,27 +294,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kSegC == 8 
         st_plane(reinterpret_cast<uint32_t *>(Y + (int64_t)(gy - out_row0) * W + 4 * q), yq, NT);
       }
       // neighbours: pixels x-2, x-1 from the left quad, x+4 from the right quad
-      const uint32_t hl = (uint32_t)__builtin_amdgcn_readlane((int)hal_l, r);
-      const uint32_t hr = (uint32_t)__builtin_amdgcn_readlane((int)hal_r, r);
-      uint32_t lft = shr1(pack4(cr[2], cr[3], cb[2], cb[3]));
-      uint32_t rgt = shl1((uint32_t)cr[0] | (uint32_t)cb[0] << 8);
-      lft = lane == 0 ? hl : lft;
-      rgt = lane == 63 ? hr : rgt;
+      uint32_t l2 = shr1(c[2]), l1 = shr1(c[3]), rt = shl1(c[0]);
+      l2 = lane == 0 ? (uint32_t)__builtin_amdgcn_readlane((int)hal_l2, r) : l2;
+      l1 = lane == 0 ? (uint32_t)__builtin_amdgcn_readlane((int)hal_l1, r) : l1;
+      rt = lane == 63 ? (uint32_t)__builtin_amdgcn_readlane((int)hal_r, r) : rt;
       if (EDGE) {
-        if (q == 0) lft = pack4(cr[2], cr[1], cb[2], cb[1]);
-        if (q == nq - 1) rgt = (uint32_t)cr[2] | (uint32_t)cb[2] << 8;
+        if (q == 0) {  // reflect-101: x-2 -> x+2, x-1 -> x+1
+          l2 = c[2];
+          l1 = c[1];
+        }
+        if (q == nq - 1) rt = c[2];  // x+4 = W -> W-2
       }
-      hcr0[r] = (int)(lft & 255) + 4 * ((int)((lft >> 8) & 255) + cr[1]) + 6 * cr[0] + cr[2];
-      hcb0[r] = (int)((lft >> 16) & 255) + 4 * ((int)(lft >> 24) + cb[1]) + 6 * cb[0] + cb[2];
-      hcr2[r] = cr[0] + 4 * (cr[1] + cr[3]) + 6 * cr[2] + (int)(rgt & 255);
-      hcb2[r] = cb[0] + 4 * (cb[1] + cb[3]) + 6 * cb[2] + (int)((rgt >> 8) & 255);
+      h0[r] = pk_taps5(l2, l1, c[0], c[1], c[2], k4, k6);
+      h2[r] = pk_taps5(c[0], c[1], c[2], c[3], rt, k4, k6);
       if (r >= 4 && r % 2 == 0 && (!EDGE || owner)) {  // chroma row k = r/2 - 2 is complete
         const int a = r - 4, k = r / 2 - 2;
-#define HIC_V(h) ((((h)[a] + 4 * ((h)[a + 1] + (h)[a + 3]) + 6 * (h)[a + 2] + (h)[a + 4]) + 128) >> 8)
+        const uint32_t v0 = pk_add_u16(pk_taps5(h0[a], h0[a + 1], h0[a + 2], h0[a + 3], h0[a + 4], k4, k6), k128);
+        const uint32_t v2 = pk_add_u16(pk_taps5(h2[a], h2[a + 1], h2[a + 2], h2[a + 3], h2[a + 4], k4, k6), k128);
         const int64_t o = (int64_t)(oyl0 + k) * dw + 2 * q;
-        st_plane(reinterpret_cast<uint16_t *>(Cr + o), (uint16_t)(sat8(HIC_V(hcr0)) | sat8(HIC_V(hcr2)) << 8), NT);
-        st_plane(reinterpret_cast<uint16_t *>(Cb + o), (uint16_t)(sat8(HIC_V(hcb0)) | sat8(HIC_V(hcb2)) << 8), NT);
-#undef HIC_V
+        // (v + 128) >> 8 = the high byte of each half (<= 255: no saturation)
+        st_plane(reinterpret_cast<uint16_t *>(Cr + o), (uint16_t)__builtin_amdgcn_perm(v2, v0, 0x0C0C0501u), NT);
+        st_plane(reinterpret_cast<uint16_t *>(Cb + o), (uint16_t)__builtin_amdgcn_perm(v2, v0, 0x0C0C0703u), NT);
       }
     }
   };
@@ -358,36 +426,6 @@ __global__ void k_ycrcb420_rgb(const uint8_t *__restrict__ Y, int64_t ystride, c
 // y << 14 | 8192: y + descale14(...) == (y * 2^14 + 8192 + ...) >> 14 since
 // y * 2^14 is a multiple of 2^14.  ~18 VALU per pixel.
 constexpr int kUpSeg = 8;
-
-typedef unsigned short u16x2c __attribute__((ext_vector_type(2)));
-typedef short s16x2c __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b) {
-  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2c, a) + __builtin_bit_cast(u16x2c, b));
-}
-__device__ __forceinline__ uint32_t pk_mad_u16(uint32_t a, uint32_t k, uint32_t c) {  // a * k + c per half
-  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2c, a) * __builtin_bit_cast(u16x2c, k) +
-                                          __builtin_bit_cast(u16x2c, c));
-}
-__device__ __forceinline__ uint32_t pk_sra6(uint32_t a) {
-  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2c, a) >> (short)6);
-}
-// acc + lo(crcb) * lo(k) + hi(crcb) * hi(k), signed 16-bit halves; the
-// three-operand form (k in an SGPR), so no copy of acc per channel
-__device__ __forceinline__ int ycc_dot(uint32_t crcb, uint32_t k, int acc) {
-  int d;
-  asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(crcb), "s"(k), "v"(acc));
-  return d;
-}
-__device__ __forceinline__ uint32_t sreg(uint32_t k) {  // opaque wave-uniform constant
-  asm volatile("" : "+s"(k));
-  return k;
-}
-// low 16 bits: sat8(a >> 14) | sat8(b >> 14) << 8 (gfx950 v_ashr_pk_u8_i32)
-__device__ __forceinline__ uint32_t sat_pk2(int a, int b) {
-  uint32_t d;
-  asm("v_ashr_pk_u8_i32 %0, %1, %2, 14" : "=v"(d) : "v"(a), "v"(b));
-  return d;
-}
 
 // Row-range form (a tile shard's decode, sharding.ShardDecoder): chroma rows
 // [sb, se) of an h-row image are produced, i.e. output rows [2 sb, 2 se); Y and rgb

@@ -15,9 +15,14 @@ bench.py --gpus N` starts the N ranks itself (torch.multiprocessing, before any
 GPU call in the parent); under torch.distributed.run it joins the given ranks.
   --mode strong (default): ONE 8K image split N ways by block rows; each rank
                  encodes its shard (colour with halo, DCT, its slice of the single
-                 DC/RLE stream after the 96-byte summary all-gather), then ONE
-                 grouped RCCL gather reassembles the whole image's coefficient
-                 blocks and DC stream on rank 0 (sharding.gather_coefficients).
+                 DC/RLE stream after the 96-byte summary all-gather); each image's
+                 coefficient blocks and DC stream are then reassembled on one rank
+                 by an RCCL gather.  Image j of each group of N consecutive images
+                 lands on rank j, and the group's N gathers go out as ONE grouped
+                 batch (sharding.gather_coefficients_group) on a process group of
+                 their own: every xGMI link carries data in both directions, where
+                 N gathers into rank 0 would queue on its 7 ingress links, and the
+                 next group's encodes run beside the exchange.
   --mode weak:   an (N*H) x W image, one H-row shard per rank (no gather).
 --workload 4k: 4096 x 4096 RGB instead of 7680 x 4320 (north_star's 4K point).
 value = pixels encoded by all ranks / max-over-ranks wall time of the K steps.
@@ -48,7 +53,7 @@ def parse():
     ap.add_argument("--mode", choices=("weak", "strong"), default="strong")
     ap.add_argument("--workload", choices=("8k", "4k"), default="8k")
     ap.add_argument("--no-gather", action="store_true",
-                    help="strong mode: leave the coefficient blocks distributed (no RCCL gather to rank 0)")
+                    help="strong mode: leave the coefficient blocks distributed (no RCCL gather)")
     ap.add_argument("--master-port", type=int, default=29541, help="self-launched N > 1 runs only")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                     help="nccl (= RCCL) for the real multi-GPU run; gloo only to rehearse it")
@@ -371,14 +376,24 @@ def main():
     H0, W0 = (H8K, W8K) if args.workload == "8k" else (4096, 4096)
     strong = world > 1 and args.mode == "strong"
     gather = strong and not args.no_gather
+    # strong mode with the gather: image j of each group of `world` consecutive
+    # images is gathered to rank j, the group's gathers in ONE grouped RCCL batch on
+    # a process group of their own (its own RCCL stream, so the next group's
+    # encodes -- and their 96-byte summary all-gathers -- run beside it); 2 x world
+    # encoders, so a group's buffers are reused only after the group before it
+    n_enc = max(4, 2 * world) if gather else 4
+    xgroup = dist.new_group(list(range(world))) if gather else None
+    if xgroup is not None:
+        dist.barrier(group=xgroup)  # its communicator is set up before any timing
     if world > 1:
         H = H0 * world if not strong else H0
-        make = lambda: sharding.ShardEncoder(H, W0, rank=rank, world=world, gather_to=0 if gather else None,  # noqa
-                                             fused=False if args.unfused else None)
+        make = lambda j: sharding.ShardEncoder(H, W0, rank=rank, world=world,  # noqa: E731
+                                               gather_to=j % world if gather else None,
+                                               fused=False if args.unfused else None)
     else:
         H = H0
-        make = lambda: pipeline.Encoder(H0, W0, fused=False if args.unfused else None)  # noqa: E731
-    encs = [make() for _ in range(4)]  # rotate outputs too (~1.2 GB)
+        make = lambda j: pipeline.Encoder(H0, W0, fused=False if args.unfused else None)  # noqa: E731
+    encs = [make(j) for j in range(n_enc)]  # rotate outputs too (~1.2 GB per 4)
     span = encs[0].span if world > 1 else (0, H)
     in_rows = span[1] - span[0]
     nin = max(2, int(np.ceil(ROT_BYTES / (in_rows * W0 * 3))))
@@ -412,6 +427,34 @@ def main():
         e_done = [torch.cuda.Event() for _ in encs]
         e_used = [False] * len(encs)
 
+    exch_done = [None] * len(encs)  # event: the gather of the encoder's last image completed
+    pending = []  # (encoder index, stream) encoded, not yet gathered
+
+    def flush(record=False):
+        """The pending images' gathers as one grouped batch (image j of the group to
+        rank j), after all of their encodes, on the last image's stream."""
+        if not pending:
+            return
+        s_x = pending[-1][1]
+        for _, s_o in pending:
+            if s_o is not s_x:
+                ev_o = torch.cuda.Event()
+                ev_o.record(s_o)
+                s_x.wait_event(ev_o)
+        with torch.cuda.stream(s_x):
+            if record:
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+            sharding.gather_coefficients_group([encs[j] for j, _ in pending], group=xgroup)
+            done = torch.cuda.Event()
+            done.record()
+            if record:
+                b.record()
+                gather_ev.append((a, b, len(pending)))
+        for j, _ in pending:
+            exch_done[j] = done
+        pending.clear()
+
     def step(i, record=False):
         e = encs[i % len(encs)]
         x = inputs[i % nin]
@@ -434,19 +477,21 @@ def main():
                 e_done[k].record(s_b)
             e_used[k] = True
             return
-        with torch.cuda.stream(streams[i % len(streams)]):
+        st = streams[i % len(streams)]
+        j = i % len(encs)
+        if exch_done[j] is not None:
+            st.wait_event(exch_done[j])  # this encoder's previous image has left
+        with torch.cuda.stream(st):
             e.encode(x, dct_events=ev)
-            if gather:
-                if record:
-                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    a.record()
-                e.gather_coefficients()
-                if record:
-                    b.record()
-                    gather_ev.append((a, b))
+        if gather:
+            pending.append((j, st))
+            if len(pending) == world:
+                flush(record)
 
     for i in range(args.warmup):
         step(i)
+    if gather:
+        flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -454,6 +499,8 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i, record=True)
+    if gather:
+        flush(True)  # a last, partial group: every timed image is gathered
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -470,7 +517,9 @@ def main():
             pipeline.check_count(int(c), pipeline.CHANNELS[ci])
             assert c > 0, "empty symbol stream"
     symbols = [int(c) for c in (encs[0].enc.counts if world > 1 else encs[0].counts).cpu().tolist()]
-    gather_us = float(np.mean([a.elapsed_time(b) for a, b in gather_ev])) * 1e3 if gather_ev else None
+    # per image: each grouped batch's span / the images it carried
+    gather_us = (float(sum(a.elapsed_time(b) for a, b, _ in gather_ev) / sum(n for _, _, n in gather_ev)) * 1e3
+                 if gather_ev else None)
 
     # ---- roofline kernel: the DCT+quantize+zig-zag pass (one launch for the three
     # planes).  hic_dct_quant_rle_u8_batch hands the two HIP events to
@@ -496,7 +545,7 @@ def main():
         timed_events = iso
         roof_note = ("16 single-stream encodes (every 4th timestamped, after 8 untimed) right after the timed "
                      "region; the timed region overlaps images on %d stream(s)%s"
-                     % (len(streams), " and gathers to rank 0" if gather else ""))
+                     % (len(streams), " and grouped gathers" if gather else ""))
     # algorithmic bytes of the timed launch: the two-kernel chain's DCT reads 1 B and
     # writes 2 B per plane pixel; the fused kernel reads the RGB (3 B per image
     # pixel) and writes the same coefficients
@@ -505,7 +554,7 @@ def main():
 
     # context for the gathered strong-scaling line: the same steps with the stream
     # left distributed (no gather), timed the same way -- the sharded encode itself
-    # scales; the gather into rank 0 is bound by rank 0's xGMI links
+    # scales; the gathers are bound by the xGMI links
     no_gather = None
     if gather:
         dist.barrier()
@@ -544,7 +593,8 @@ def main():
             wl += ("; %s: %s, block-row tile shards over %d ranks%s"
                    % ("BASELINE configs[3]" if (strong and args.workload == "8k") else "multi-GPU",
                       "one image split N ways" if strong else "one %d-row shard per rank" % H0, world,
-                      ", one grouped RCCL gather of the coefficient blocks + DC stream to rank 0 per step"
+                      ", each image's coefficient blocks + DC stream gathered to one rank (image j of each "
+                      "group of %d to rank j, the group's gathers in one grouped RCCL batch)" % world
                       if gather else ""))
         else:
             wl = ("BASELINE configs[2]: " if args.workload == "8k" else "") + wl
@@ -568,8 +618,9 @@ def main():
                 "mode": "single" if world == 1 else args.mode,
                 "streams": args.streams,
                 "cu_split": args.cu_split if cu_split else None,
-                "gather_to_rank0": gather,
-                "gather_us_per_step": None if gather_us is None else round(gather_us, 2),
+                "gather": "image j of each group of %d to rank j, one grouped RCCL batch per group" % world
+                          if gather else None,
+                "gather_us_per_image": None if gather_us is None else round(gather_us, 2),
                 "without_gather": no_gather,
                 "symbols_per_image_rank0": symbols,
                 "dist_backend": None if world == 1 else args.dist_backend + (" (same device)" if args.same_device

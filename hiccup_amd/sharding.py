@@ -177,10 +177,28 @@ class ShardEncoder:
         return self._gather_coefficients()
 
     def _gather_coefficients(self):
+        mine, full, ranges, dst = self.gather_item()
+        gather_blocks(mine, full, ranges, self.rank, self.world, dst, self.group)
+        return full
+
+    def gather_item(self):
+        """(mine, full, ranges, dst) of this encoder's gather, for gather_blocks_group."""
+        if self.gather_to is None:
+            raise ValueError("ShardEncoder(gather_to=...) was not set")
         full = {k: (self.full_coef[k], self.full_dc[k]) for k in CHANNELS} if self.rank == self.gather_to else None
         mine = {k: (self.enc.coef[k], self.enc.dc[k]) for k in CHANNELS}
-        gather_blocks(mine, full, self.ranges, self.rank, self.world, self.gather_to, self.group)
-        return full
+        return mine, full, self.ranges, self.gather_to
+
+
+def gather_coefficients_group(encoders, group=None):
+    """The gathers of several ShardEncoders (one image each, typically with
+    different gather_to ranks) in ONE grouped RCCL batch on the current stream
+    (gather_blocks_group).  Returns each encoder's whole-image {channel: (coef, dc)}
+    on its gather_to rank, None elsewhere."""
+    items = [e.gather_item() for e in encoders]
+    e0 = encoders[0]
+    gather_blocks_group(items, e0.rank, e0.world, group if group is not None else e0.group)
+    return [it[1] for it in items]
 
 
 def gather_blocks(mine, full, ranges, rank, world, dst, group=None):
@@ -192,24 +210,36 @@ def gather_blocks(mine, full, ranges, rank, world, dst, group=None):
     (RCCL: sends / receives on the current stream, no host sync); dst's own slice
     is expected to be written in place already.  gloo with device tensors (the
     one-GPU rehearsal) stages through the host."""
+    gather_blocks_group([(mine, full, ranges, dst)], rank, world, group)
+
+
+def gather_blocks_group(items, rank, world, group=None):
+    """Several images' gathers in ONE batch_isend_irecv group: items = [(mine,
+    full, ranges, dst)] as gather_blocks, each with its own destination.  With the
+    destinations spread over the ranks (image j of a group of N lands on rank j)
+    every rank both sends and receives, so all xGMI links carry data in both
+    directions at once -- N gathers into one rank would queue on that rank's 7
+    ingress links.  Every rank lists the items in the same order (a sender's and a
+    receiver's operations pair up per peer in posting order)."""
     ops, landing = [], []
     gloo = dist.get_backend(group) == "gloo"
-    if rank == dst:
-        for r in range(world):
-            if r == dst:
-                continue
+    for mine, full, ranges, dst in items:
+        if rank == dst:
+            for r in range(world):
+                if r == dst:
+                    continue
+                for k in CHANNELS:
+                    b0, b1 = ranges[k][r]
+                    for t in full[k]:
+                        t = t[b0:b1]
+                        buf = torch.empty(t.shape, dtype=t.dtype) if (gloo and t.is_cuda) else t
+                        ops.append(dist.P2POp(dist.irecv, buf, r, group=group))
+                        landing.append((t, buf))
+        else:
             for k in CHANNELS:
-                b0, b1 = ranges[k][r]
-                for t in full[k]:
-                    t = t[b0:b1]
-                    buf = torch.empty(t.shape, dtype=t.dtype) if (gloo and t.is_cuda) else t
-                    ops.append(dist.P2POp(dist.irecv, buf, r, group=group))
-                    landing.append((t, buf))
-    else:
-        for k in CHANNELS:
-            for t in mine[k]:
-                t = t.contiguous()
-                ops.append(dist.P2POp(dist.isend, t.cpu() if (gloo and t.is_cuda) else t, dst, group=group))
+                for t in mine[k]:
+                    t = t.contiguous()
+                    ops.append(dist.P2POp(dist.isend, t.cpu() if (gloo and t.is_cuda) else t, dst, group=group))
     for req in dist.batch_isend_irecv(ops) if ops else ():
         req.wait()
     for t, buf in landing:

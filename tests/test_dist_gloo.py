@@ -3,7 +3,9 @@ encode's exchange steps: each rank holds a block-row shard of the coefficient
 streams, all-gathers its channel summaries with sharding.exchange, derives its
 stitch record with sharding.stitch_host, run-length codes its slice, and rank 0
 reassembles (a) the coefficient blocks + DC stream with sharding.gather_blocks --
-the same grouped batch_isend_irecv code the RCCL path runs -- and (b) the symbol
+the same grouped batch_isend_irecv code the RCCL path runs; (a') a group of
+`world` images' gathers, image j to rank j, goes out as one batch
+(sharding.gather_blocks_group, the bench's exchange) -- and (b) the symbol
 streams with point-to-point sends.  Both must equal the single-stream encode.
 (c) Each rank then decodes its own slice (sharded decode: carried-zero skip, DC
 chain from the stitch record, pyrUp halo rows from sharding.exchange_halo_rows)
@@ -108,6 +110,26 @@ def _worker(rank, world, port, H, W, flat, results):
                 results["blocks_" + k] = bool(
                     np.array_equal(full[k][0].numpy(), zz[k].astype(np.int16))
                     and np.array_equal(full[k][1].numpy(), orc.dpcm(zz[k][:, 0].astype(np.int64)).astype(np.int32)))
+        # (a') one group of `world` images' gathers, image j to rank j
+        # (sharding.gather_blocks_group, the bench's multi-GPU exchange)
+        items = []
+        for j in range(world):
+            pj = {k: (parts[k][0] + j, parts[k][1] - j) for k in pipeline.CHANNELS}
+            fj = None
+            if rank == j:
+                fj = {k: (torch.full((len(zz[k]), 64), -7, dtype=torch.int16),
+                          torch.full((len(zz[k]),), -7, dtype=torch.int32)) for k in pipeline.CHANNELS}
+                for k in pipeline.CHANNELS:
+                    b0, b1 = ranges[k][rank]
+                    fj[k][0][b0:b1] = pj[k][0]
+                    fj[k][1][b0:b1] = pj[k][1]
+            items.append((pj, fj, ranges, j))
+        sharding.gather_blocks_group(items, rank, world)
+        fj = items[rank][1]
+        results["group_%d" % rank] = all(
+            np.array_equal(fj[k][0].numpy(), zz[k].astype(np.int16) + rank)
+            and np.array_equal(fj[k][1].numpy(), orc.dpcm(zz[k][:, 0].astype(np.int64)).astype(np.int32) - rank)
+            for k in pipeline.CHANNELS)
         # (c) the sharded decode: this rank's stream slice -> blocks (carried zeros
         # skipped, DC chain from the previous shard), inverse DCT of its block rows,
         # pyrUp halo rows from the neighbours (sharding.exchange_halo_rows, the code
@@ -179,4 +201,5 @@ def test_sharded_exchange_gloo(world, H, W, flat):
     exp = {k: True for k in pipeline.CHANNELS}
     exp.update({"blocks_" + k: True for k in pipeline.CHANNELS})
     exp.update({"decode_%d" % r: True for r in range(world)})
+    exp.update({"group_%d" % r: True for r in range(world)})
     assert dict(results) == exp

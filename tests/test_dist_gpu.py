@@ -6,7 +6,9 @@ summaries, all-gather, device stitch, scan + emit), rank 0 reassembles the
 streams with gather_streams, and the result must equal the single-GPU encode of
 the whole image bit for bit.  Each rank then decodes its own slice
 (ShardDecoder, halo rows over the process group) and its RGB rows must equal the
-single-GPU decode's."""
+single-GPU decode's.  Finally `world` images are encoded and gathered as the
+bench's strong mode does it (image j to rank j, one grouped batch), and each
+rank's received image must equal its single-GPU encode."""
 import os
 import socket
 import tempfile
@@ -79,6 +81,28 @@ def _rank(rank, world, port, H, W, flat_rows, out_path):
         ok &= all(oks)
         with open(out_path, "w") as f:
             f.write("ok" if ok else "mismatch")
+    # the bench's grouped exchange: `world` different images, image j gathered to
+    # rank j, all in one batch (sharding.gather_coefficients_group) on a process
+    # group of its own; each rank checks the image it received
+    xgroup = dist.new_group(list(range(world)))
+    imgs = [np.roll(rgb, 8 * j, axis=1) for j in range(world)]
+    ses = [sharding.ShardEncoder(H, W, rank=rank, world=world, gather_to=j) for j in range(world)]
+    for se_j, img in zip(ses, imgs):
+        se_j.encode(device.to_device(img[a:b]), stream=s)
+    with torch.cuda.stream(s):
+        fulls = sharding.gather_coefficients_group(ses, group=xgroup)
+    torch.cuda.synchronize()
+    mine_ref = pipeline.Encoder(H, W)
+    mine_ref.encode(device.to_device(imgs[rank]))
+    ref = mine_ref.result()
+    gok = all(np.array_equal(fulls[rank][k][0].cpu().numpy(), ref[k][0]) and
+              np.array_equal(fulls[rank][k][1].cpu().numpy(), ref[k][1]) for k in pipeline.CHANNELS)
+    gok &= all(fulls[j] is None for j in range(world) if j != rank)
+    goks = [None] * world
+    dist.all_gather_object(goks, bool(gok))
+    if rank == 0 and not all(goks):
+        with open(out_path, "w") as f:
+            f.write("grouped gather mismatch %s" % goks)
     dist.barrier()
     dist.destroy_process_group()
 

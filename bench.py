@@ -22,7 +22,9 @@ GPU call in the parent); under torch.distributed.run it joins the given ranks.
                  batch (sharding.gather_coefficients_group) on a process group of
                  their own: every xGMI link carries data in both directions, where
                  N gathers into rank 0 would queue on its 7 ingress links, and the
-                 next group's encodes run beside the exchange.
+                 next group's encodes run beside the exchange.  The group's
+                 encodes batch their exchange steps (sharding.encode_group: one
+                 summary all-gather and one count all-gather per group).
   --mode weak:   an (N*H) x W image, one H-row shard per rank (no gather).
 --workload 4k: 4096 x 4096 RGB instead of 7680 x 4320 (north_star's 4K point).
 value = pixels encoded by all ranks / max-over-ranks wall time of the K steps.
@@ -428,30 +430,34 @@ def main():
         e_used = [False] * len(encs)
 
     exch_done = [None] * len(encs)  # event: the gather of the encoder's last image completed
-    pending = []  # (encoder index, stream) encoded, not yet gathered
+    pending = []  # (encoder index, input, DCT events) of the group being collected
+    n_groups = [0]
 
     def flush(record=False):
-        """The pending images' gathers as one grouped batch (image j of the group to
-        rank j), after all of their encodes, on the last image's stream."""
+        """The pending images (a group of up to N): their sharded encodes with the
+        exchange steps batched (sharding.encode_group), then their gathers as one
+        grouped batch (image j of the group to rank j), on the group's stream
+        (groups alternate over the streams)."""
         if not pending:
             return
-        s_x = pending[-1][1]
-        for _, s_o in pending:
-            if s_o is not s_x:
-                ev_o = torch.cuda.Event()
-                ev_o.record(s_o)
-                s_x.wait_event(ev_o)
-        with torch.cuda.stream(s_x):
+        st = streams[n_groups[0] % len(streams)]
+        n_groups[0] += 1
+        for j, _, _ in pending:
+            if exch_done[j] is not None:
+                st.wait_event(exch_done[j])  # the encoder's previous image has left
+        with torch.cuda.stream(st):
+            group_encs = [encs[j] for j, _, _ in pending]
+            sharding.encode_group(group_encs, [x for _, x, _ in pending], st, [ev for _, _, ev in pending])
             if record:
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record()
-            sharding.gather_coefficients_group([encs[j] for j, _ in pending], group=xgroup)
+            sharding.gather_coefficients_group(group_encs, group=xgroup)
             done = torch.cuda.Event()
             done.record()
             if record:
                 b.record()
                 gather_ev.append((a, b, len(pending)))
-        for j, _ in pending:
+        for j, _, _ in pending:
             exch_done[j] = done
         pending.clear()
 
@@ -477,16 +483,13 @@ def main():
                 e_done[k].record(s_b)
             e_used[k] = True
             return
-        st = streams[i % len(streams)]
-        j = i % len(encs)
-        if exch_done[j] is not None:
-            st.wait_event(exch_done[j])  # this encoder's previous image has left
-        with torch.cuda.stream(st):
-            e.encode(x, dct_events=ev)
         if gather:
-            pending.append((j, st))
+            pending.append((i % len(encs), x, ev))
             if len(pending) == world:
                 flush(record)
+            return
+        with torch.cuda.stream(streams[i % len(streams)]):
+            e.encode(x, dct_events=ev)
 
     for i in range(args.warmup):
         step(i)
@@ -560,9 +563,10 @@ def main():
         dist.barrier()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        for i in range(args.steps):
-            with torch.cuda.stream(streams[i % len(streams)]):
-                encs[i % len(encs)].encode(inputs[i % nin])
+        for g0 in range(0, args.steps, world):  # the same groups, encode_group only
+            idx = list(range(g0, min(g0 + world, args.steps)))
+            sharding.encode_group([encs[i % len(encs)] for i in idx], [inputs[i % nin] for i in idx],
+                                  streams[((g0 // world) % 2) % len(streams)])
         torch.cuda.synchronize()
         dist.barrier()
         torch.cuda.synchronize()

@@ -190,6 +190,43 @@ class ShardEncoder:
         return mine, full, self.ranges, self.gather_to
 
 
+def encode_group(encoders, rgb_rows_list, stream=None, dct_events=None):
+    """The sharded encodes of several images (one ShardEncoder each, same plan)
+    with their exchange steps batched: every image's transform and channel
+    summaries, ONE all-gather of all the summaries (n x 96 bytes per rank), the
+    stitch records and entropy coding of every image, ONE all-gather of all the
+    symbol counts.  Two small collectives per group instead of two per image: at N
+    GPUs each is a latency-bound RCCL all-gather, which would otherwise bound the
+    per-image time.  Equal, image by image, to ShardEncoder.encode.  dct_events:
+    None or one entry (None or device.KernelEvents) per image."""
+    if stream is not None:
+        with torch.cuda.stream(stream):
+            return _encode_group(encoders, rgb_rows_list, stream, dct_events)
+    return _encode_group(encoders, rgb_rows_list, None, dct_events)
+
+
+def _encode_group(encoders, rgb_rows_list, stream, dct_events):
+    e0 = encoders[0]
+    n, world = len(encoders), e0.world
+    summs = []
+    for i, (se, x) in enumerate(zip(encoders, rgb_rows_list)):
+        se.enc.transform(x, stream, in_row0=se.span[0], dct_events=dct_events[i] if dct_events else None)
+        summs.append(se.enc.shard_summaries(stream))
+    allsumm = torch.empty((world, n, 3, 4), dtype=torch.int64, device=summs[0].device)
+    _all_gather(allsumm.view(world * n * 3, 4), torch.stack(summs).view(n * 3, 4), group=e0.group)
+    s = device.stream_ptr(stream)
+    for i, se in enumerate(encoders):
+        se.all_summ.copy_(allsumm[:, i])
+        for c in range(3):
+            _lib.call("hic_rle_stitch", ctypes.c_void_p(se.all_summ.data_ptr() + 8 * 4 * c), world, se.rank, 12,
+                      device.ptr(se.stitch[c]), s)
+        se.enc.entropy(stream, stitch=se.stitch)
+    allcounts = torch.empty((world, n, 3), dtype=torch.int64, device=summs[0].device)
+    _all_gather(allcounts.view(-1), torch.stack([se.enc.counts for se in encoders]).view(-1), group=e0.group)
+    for i, se in enumerate(encoders):
+        se.all_counts.copy_(allcounts[:, i])
+
+
 def gather_coefficients_group(encoders, group=None):
     """The gathers of several ShardEncoders (one image each, typically with
     different gather_to ranks) in ONE grouped RCCL batch on the current stream

@@ -87,17 +87,26 @@ def _rank(rank, world, port, H, W, flat_rows, out_path):
     xgroup = dist.new_group(list(range(world)))
     imgs = [np.roll(rgb, 8 * j, axis=1) for j in range(world)]
     ses = [sharding.ShardEncoder(H, W, rank=rank, world=world, gather_to=j) for j in range(world)]
-    for se_j, img in zip(ses, imgs):
-        se_j.encode(device.to_device(img[a:b]), stream=s)
+    # the group's exchange steps batched: one summary and one count all-gather
+    sharding.encode_group(ses, [device.to_device(img[a:b]) for img in imgs], stream=s)
     with torch.cuda.stream(s):
         fulls = sharding.gather_coefficients_group(ses, group=xgroup)
     torch.cuda.synchronize()
-    mine_ref = pipeline.Encoder(H, W)
-    mine_ref.encode(device.to_device(imgs[rank]))
-    ref = mine_ref.result()
+    refs = []
+    for img in imgs:
+        w_enc = pipeline.Encoder(H, W)
+        w_enc.encode(device.to_device(img))
+        refs.append(w_enc.result())
+    ref = refs[rank]
     gok = all(np.array_equal(fulls[rank][k][0].cpu().numpy(), ref[k][0]) and
               np.array_equal(fulls[rank][k][1].cpu().numpy(), ref[k][1]) for k in pipeline.CHANNELS)
     gok &= all(fulls[j] is None for j in range(world) if j != rank)
+    # every image's symbol stream (stitched per image inside the batched group)
+    for j in range(world):
+        got_j = sharding.gather_streams(ses[j])
+        if rank == 0:
+            gok &= all(np.array_equal(got_j[k][0], refs[j][k][1]) and np.array_equal(got_j[k][1], refs[j][k][2])
+                       and np.array_equal(got_j[k][2], refs[j][k][3]) for k in pipeline.CHANNELS)
     goks = [None] * world
     dist.all_gather_object(goks, bool(gok))
     if rank == 0 and not all(goks):

@@ -268,14 +268,14 @@ def gather_blocks_group(items, rank, world, group=None):
                 for k in CHANNELS:
                     b0, b1 = ranges[k][r]
                     for t in full[k]:
-                        t = t[b0:b1]
+                        t = _wire(t[b0:b1])
                         buf = torch.empty(t.shape, dtype=t.dtype) if (gloo and t.is_cuda) else t
                         ops.append(dist.P2POp(dist.irecv, buf, r, group=group))
                         landing.append((t, buf))
         else:
             for k in CHANNELS:
                 for t in mine[k]:
-                    t = t.contiguous()
+                    t = _wire(t.contiguous())
                     ops.append(dist.P2POp(dist.isend, t.cpu() if (gloo and t.is_cuda) else t, dst, group=group))
     for req in dist.batch_isend_irecv(ops) if ops else ():
         req.wait()
@@ -297,10 +297,11 @@ def exchange_halo_rows(planes, rank, world, group=None):
     gloo = dist.get_backend(group) == "gloo"
 
     def send(t, peer):
-        t = t.contiguous()
+        t = _wire(t.contiguous())
         ops.append(dist.P2POp(dist.isend, t.cpu() if (gloo and t.is_cuda) else t, peer, group=group))
 
     def recv(t, peer):
+        t = _wire(t)
         buf = torch.empty(t.shape, dtype=t.dtype) if (gloo and t.is_cuda) else t
         ops.append(dist.P2POp(dist.irecv, buf, peer, group=group))
         landing.append((t, buf))
@@ -418,13 +419,26 @@ class ShardDecoder:
                                  % (self.rank, k, st[i], want))
 
 
+def _wire(t):
+    """The bytes of a contiguous tensor, as the uint8 view every point-to-point
+    transfer moves: torch's NCCL (= RCCL) process group refuses int16 tensors
+    ("data type is not supported for NCCL process group: Short"), and the
+    coefficient blocks and symbol lengths are int16.  A receive into the view lands
+    in the tensor itself."""
+    if not t.is_contiguous():
+        raise ValueError("point-to-point transfers need contiguous tensors")
+    return t if t.dtype == torch.uint8 else t.view(torch.uint8)
+
+
 def _send(t, dst, group):
+    t = _wire(t)
     if t.is_cuda and dist.get_backend(group) == "gloo":
         t = t.cpu()
     dist.send(t, dst=dst, group=group)
 
 
 def _recv(t, src, group):
+    t = _wire(t)
     if t.is_cuda and dist.get_backend(group) == "gloo":
         h = torch.empty(t.shape, dtype=t.dtype)
         dist.recv(h, src=src, group=group)

@@ -123,3 +123,56 @@ def test_sharded_encode_multiprocess(world, H, W, flat):
         out = os.path.join(d, "result")
         mp.spawn(_rank, args=(world, _free_port(), H, W, flat, out), nprocs=world, join=True)
         assert open(out).read() == "ok"
+
+
+def _rccl_rank(rank, port, H, W, out_path):
+    """RCCL itself on the one-GPU box: a world-size-1 nccl process group (RCCL refuses
+    two ranks on one device) through the sharded encode's collectives (the summary
+    and count all-gathers of encode_group, ShardEncoder.offsets) and the grouped
+    P2P batch of the gather, here as sends / receives to self (through the byte
+    views sharding._wire gives every transfer: the NCCL process group refuses int16)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    from hiccup_amd import device, pipeline, sharding
+    assert dist.get_backend() == "nccl"
+    rgb = _image(H, W)
+    xgroup = dist.new_group([0])
+    se = sharding.ShardEncoder(H, W, rank=0, world=1, gather_to=0)
+    s = torch.cuda.Stream()
+    sharding.encode_group([se], [device.to_device(rgb)], stream=s)
+    with torch.cuda.stream(s):
+        fulls = sharding.gather_coefficients_group([se], group=xgroup)
+        # the gather's P2P batch shape (P2POp pairs in one batch_isend_irecv group on
+        # the current stream), rank to itself: every channel's blocks and DC stream
+        copies, ops = [], []
+        for k in pipeline.CHANNELS:
+            for t in fulls[0][k]:
+                dst = torch.empty_like(t)
+                ops += [dist.P2POp(dist.isend, sharding._wire(t.contiguous()), 0, group=xgroup),
+                        dist.P2POp(dist.irecv, sharding._wire(dst), 0, group=xgroup)]
+                copies.append((t, dst))
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    torch.cuda.synchronize()
+    whole = pipeline.Encoder(H, W)
+    whole.encode(device.to_device(rgb))
+    ref = whole.result()
+    ok = all(np.array_equal(fulls[0][k][0].cpu().numpy(), ref[k][0]) and
+             np.array_equal(fulls[0][k][1].cpu().numpy(), ref[k][1]) for k in pipeline.CHANNELS)
+    ok &= all(torch.equal(a, b) for a, b in copies)
+    got = sharding.gather_streams(se)
+    ok &= all(np.array_equal(got[k][0], ref[k][1]) and np.array_equal(got[k][1], ref[k][2]) and
+              np.array_equal(got[k][2], ref[k][3]) for k in pipeline.CHANNELS)
+    offs, tot = se.offsets()
+    ok &= [int(x) for x in tot] == [len(ref[k][2]) for k in pipeline.CHANNELS]
+    with open(out_path, "w") as f:
+        f.write("ok" if ok else "mismatch")
+    dist.destroy_process_group()
+
+
+def test_rccl_world1_exchange():
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "result")
+        mp.spawn(_rccl_rank, args=(_free_port(), 256, 1024, out), nprocs=1, join=True)
+        assert open(out).read() == "ok"

@@ -7,7 +7,7 @@ namespace hic {
 static thread_local char g_last_error[512] = "";
 
 // hic_set_knob values (-1 = default; read by the launchers on every call)
-static int g_knobs[HIC_KNOB_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+static int g_knobs[HIC_KNOB_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 int knob(int k) {
   const int v = g_knobs[k];
   if (v >= 0) return v;
@@ -91,6 +91,7 @@ extern "C" int hic_set_knob(int k, int value) {
     return hic::arg_error("dct path %d (0 exact, 1 float64 AAN, 2 float64 AAN unpipelined, 3 float32)", value);
   if (k == HIC_KNOB_COLOR_SEG && value != -1 && value != 8 && value != 16) return hic::arg_error("colour segment");
   if (k == HIC_KNOB_ENCODE_WAVES && value != -1 && value != 2 && value != 3) return hic::arg_error("encode waves");
+  if (k == HIC_KNOB_ENCODE_XCD && value != -1 && value != 0 && value != 1) return hic::arg_error("encode xcd");
   if (k == HIC_KNOB_ENCODE_LDS_PAD && value > 64) return hic::arg_error("encode LDS pad %d KiB (0..64)", value);
   if (value < -1) return hic::arg_error("knob value %d", value);
 #ifndef HIC_DEV

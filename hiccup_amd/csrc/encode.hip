@@ -49,6 +49,7 @@ struct Enc420 {
   int64_t *rec[3];   // tile records: Y per 64-block tile, Cr / Cb per 32-block half tile
   int M;
   int nstrips, nunits;  // nunits: waves (HIC_ENC_VG unit rows each)
+  int xcd;              // 1: workgroups remapped to a contiguous band of units per XCD
 };
 
 constexpr int kZZ = HIC_LAYOUT_ZIGZAG_I16;
@@ -425,7 +426,18 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
   __shared__ uint2 s_stage[HIC_ENC_WPB * 64 * kStageU2];
   __shared__ uint32_t s_chroma_all[HIC_ENC_WPB][2 * 8 * 64];
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g = __builtin_amdgcn_readfirstlane(blockIdx.x * HIC_ENC_WPB + wv);
+  // Workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8 share one,
+  // MI355X_MICROARCH.md "Workgroup dispatch"; for speed only, any placement is
+  // correct).  E.xcd: block b takes logical workgroup L so that each XCD's blocks
+  // are one contiguous run of units in raster order, i.e. a band of unit rows: the
+  // pyrDown halo rows a unit shares with the unit row above / below are then read
+  // by the same XCD at about the same time and served by its L2.
+  int b = blockIdx.x;
+  if (E.xcd) {
+    const int nwg = gridDim.x, per = nwg >> 3, rem = nwg & 7, x = b & 7, i = b >> 3;
+    b = x < rem ? x * (per + 1) + i : rem * (per + 1) + (x - rem) * per + i;
+  }
+  const int g = __builtin_amdgcn_readfirstlane(b * HIC_ENC_WPB + wv);
   if (g >= E.nunits) return;  // wave-uniform
   uint2 *st2 = s_stage + wv * 64 * kStageU2;
   uint32_t *s_chroma = s_chroma_all[wv];
@@ -561,6 +573,7 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
   E.M = max_len;
   E.nstrips = (int)(W / 512);
   E.nunits = E.nstrips * (int)((out_rows / 16 + HIC_ENC_VG - 1) / HIC_ENC_VG);  // waves
+  E.xcd = knob(HIC_KNOB_ENCODE_XCD) == 1;
   // one wave per unit (no persistent loop: units are the same size, and the
   // hardware's dispatch balances the tail better than a fixed split)
   const dim3 grid((unsigned)((E.nunits + HIC_ENC_WPB - 1) / HIC_ENC_WPB)), block(64 * HIC_ENC_WPB);

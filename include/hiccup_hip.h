@@ -77,7 +77,8 @@ int hic_device_count(int *h_n);
 #define HIC_KNOB_ENCODE_NT 10       /* hic_encode420_u8: 1 = nontemporal coefficient stores (default 0: cached) */
 #define HIC_KNOB_ENCODE_DCT 11      /* hic_encode420_u8: 1 = float32 AAN DCT with proven windows + in-place fallbacks (default 0: float64) */
 #define HIC_KNOB_ENCODE_LDS_PAD 12  /* hic_encode420_u8: KiB of extra LDS per workgroup (0..64; 40 leaves one encode workgroup per CU, the rest of the CU to a concurrent kernel) */
-#define HIC_KNOB_COUNT 13
+#define HIC_KNOB_ENCODE_XCD 13     /* hic_encode420_u8: 1 = each XCD takes a contiguous band of unit rows (pyrDown halo rows re-read from its own L2), 0 = dispatch order */
+#define HIC_KNOB_COUNT 14
 int hic_set_knob(int knob, int value);
 int hic_get_knob(int knob, int *h_value);
 /* Synchronises `stream`; returns HIC_ERR_HIP if an earlier async launch failed. */

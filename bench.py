@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--workload", choices=("8k", "4k"), default="8k")
     ap.add_argument("--no-gather", action="store_true",
                     help="strong mode: leave the coefficient blocks distributed (no RCCL gather)")
+    ap.add_argument("--transport", choices=("torch", "c-abi"), default="torch",
+                    help="strong mode's gather: torch.distributed P2P batch (default) or the C-ABI's own RCCL "
+                         "communicator (hic_gather_*, sharding.RcclGather; nccl backend only)")
     ap.add_argument("--master-port", type=int, default=29541, help="self-launched N > 1 runs only")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                     help="nccl (= RCCL) for the real multi-GPU run; gloo only to rehearse it")
@@ -387,6 +390,11 @@ def main():
     xgroup = dist.new_group(list(range(world))) if gather else None
     if xgroup is not None:
         dist.barrier(group=xgroup)  # its communicator is set up before any timing
+    rgather = None
+    if gather and args.transport == "c-abi":
+        if args.dist_backend != "nccl":
+            raise SystemExit("--transport c-abi needs --dist-backend nccl (one GPU per rank)")
+        rgather = sharding.RcclGather()
     if world > 1:
         H = H0 * world if not strong else H0
         make = lambda j: sharding.ShardEncoder(H, W0, rank=rank, world=world,  # noqa: E731
@@ -451,7 +459,10 @@ def main():
             if record:
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record()
-            sharding.gather_coefficients_group(group_encs, group=xgroup)
+            if rgather is not None:
+                rgather.gather_encoders(group_encs, st)
+            else:
+                sharding.gather_coefficients_group(group_encs, group=xgroup)
             done = torch.cuda.Event()
             done.record()
             if record:
@@ -622,7 +633,8 @@ def main():
                 "mode": "single" if world == 1 else args.mode,
                 "streams": args.streams,
                 "cu_split": args.cu_split if cu_split else None,
-                "gather": "image j of each group of %d to rank j, one grouped RCCL batch per group" % world
+                "gather": "image j of each group of %d to rank j, one grouped RCCL batch per group (%s)"
+                          % (world, "torch.distributed P2P" if rgather is None else "C-ABI hic_gather_bytes")
                           if gather else None,
                 "gather_us_per_image": None if gather_us is None else round(gather_us, 2),
                 "without_gather": no_gather,
@@ -663,6 +675,9 @@ def main():
         elif not args.no_cpu_baseline:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
+    if rgather is not None:
+        torch.cuda.synchronize()
+        rgather.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -94,7 +94,15 @@ SIGNATURES = {
     "hic_rle_decode_i16": (_int, [_vp, _vp, _i64, _vp, _i64, _int, _vp, _vp, _vp, _vp]),
     "hic_rle_decode_i16_shard": (_int, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
     "hic_rle_decode_i32": (_int, [_vp, _vp, _i64, _vp, _i64, _int, _vp, _vp, _vp, _vp]),
+    "hic_gather_unique_id": (_int, [_vp]),
+    "hic_gather_comm_init": (_int, [_vp, _vp, _int, _int]),
+    "hic_gather_comm_info": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int)]),
+    "hic_gather_comm_destroy": (_int, [_vp]),
+    "hic_gather_group_begin": (_int, []),
+    "hic_gather_group_end": (_int, []),
+    "hic_gather_bytes": (_int, [_vp, _vp, _i64, _vp, _vp, _vp, _int, _vp]),
 }
+GATHER_ID_BYTES = 128
 
 
 class HipUnavailable(RuntimeError):

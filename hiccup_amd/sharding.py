@@ -284,6 +284,61 @@ def gather_blocks_group(items, rank, world, group=None):
             t.copy_(buf)
 
 
+class RcclGather:
+    """The gather through the C-ABI (hic_gather_*, include/hiccup_hip.h): an RCCL
+    communicator of the process group's ranks, made by the library itself (rank
+    0's id crosses over the process group), and gather_blocks_group's transfer as
+    hic_gather_bytes calls inside ONE hic_gather_group_begin / _end.  The same
+    exchange as gather_blocks_group for a caller that binds the C-ABI directly;
+    the caller must have selected its GPU (torch.cuda.set_device)."""
+
+    def __init__(self, group=None):
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        uid = ctypes.create_string_buffer(_lib.GATHER_ID_BYTES)
+        if self.rank == 0:
+            _lib.call("hic_gather_unique_id", uid)
+        box = [uid.raw if self.rank == 0 else None]
+        dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        uid = ctypes.create_string_buffer(box[0], _lib.GATHER_ID_BYTES)
+        self.comm = ctypes.c_void_p()
+        _lib.call("hic_gather_comm_init", ctypes.byref(self.comm), uid, self.world, self.rank)
+
+    def close(self):
+        if self.comm:
+            _lib.call("hic_gather_comm_destroy", self.comm)
+            self.comm = ctypes.c_void_p()
+
+    def gather_group(self, items, stream=None):
+        """items = [(mine, full, ranges, dst)] as gather_blocks_group (every
+        rank lists them in the same order); on the given (or current) stream."""
+        s = device.stream_ptr(stream)
+        I64 = ctypes.c_int64 * self.world
+        _lib.call("hic_gather_group_begin")
+        try:
+            for mine, full, ranges, dst in items:
+                for k in CHANNELS:
+                    for ti, t in enumerate(mine[k]):
+                        row = t.stride(0) * t.element_size()  # bytes per block
+                        t = _wire(t)
+                        offs = I64(*[ranges[k][r][0] * row for r in range(self.world)])
+                        nbytes = I64(*[(ranges[k][r][1] - ranges[k][r][0]) * row for r in range(self.world)])
+                        if self.rank == dst:
+                            f = full[k][ti]
+                            _lib.call("hic_gather_bytes", self.comm, device.ptr(t), t.numel(), device.ptr(f), offs,
+                                      nbytes, dst, s)
+                        else:
+                            _lib.call("hic_gather_bytes", self.comm, device.ptr(t), t.numel(), None, None, None,
+                                      dst, s)
+        finally:
+            _lib.call("hic_gather_group_end")
+
+    def gather_encoders(self, encoders, stream=None):
+        """gather_coefficients_group through the C-ABI."""
+        items = [e.gather_item() for e in encoders]
+        self.gather_group(items, stream)
+        return [it[1] for it in items]
+
+
 def exchange_halo_rows(planes, rank, world, group=None):
     """pyrUp's halo for a row-sharded decode: every plane in `planes` is (buf, top,
     n_own) -- buf holds this rank's n_own rows at [top, top + n_own), with one halo row

@@ -335,6 +335,33 @@ int hic_huffman_pack(const void *keys, int key_bytes, int64_t n, int32_t key_min
                      const uint64_t *d_code_bits, const uint8_t *d_code_len, uint8_t *out,
                      int64_t out_bytes, int64_t *d_nbits, void *workspace, void *stream);
 
+/* ---- Multi-GPU gather over RCCL (SURVEY.md section 8(b) hic_gather_*; the
+ *      whole-image buffers it reassembles are what codec.jpeg_encode consumes,
+ *      codec.py:275-334, after compression.jpeg_compression, compression.py:16-39,
+ *      which the tile-sharded encode splits over the ranks).  One rank per GPU;
+ *      RCCL is opened at run time (librccl.so.1), the other entry points do not
+ *      need it.
+ *  hic_gather_unique_id: one rank makes the communicator id (HIC_GATHER_ID_BYTES
+ *    host bytes) and hands it to the others by any host channel.
+ *  hic_gather_comm_init: collective over the `world` ranks, after the caller has
+ *    selected its GPU (hipSetDevice); *h_comm is an opaque handle.
+ *  hic_gather_bytes: a variable-size gather: every rank's d_send (send_bytes)
+ *    lands at d_recv + h_recv_offsets[rank] on `root` (h_recv_bytes[rank] bytes;
+ *    root-only arguments, NULL elsewhere).  The root's own slice is copied unless
+ *    d_send already is that address.  One RCCL group of sends / receives on
+ *    `stream`; no host synchronisation.
+ *  hic_gather_group_begin / _end: gathers posted between them (e.g. image j of a
+ *    group of N to root j) go out as ONE RCCL group. */
+#define HIC_GATHER_ID_BYTES 128
+int hic_gather_unique_id(uint8_t *h_id);
+int hic_gather_comm_init(void **h_comm, const uint8_t *h_id, int world, int rank);
+int hic_gather_comm_info(void *comm, int *h_world, int *h_rank);
+int hic_gather_comm_destroy(void *comm);
+int hic_gather_group_begin(void);
+int hic_gather_group_end(void);
+int hic_gather_bytes(void *comm, const void *d_send, int64_t send_bytes, void *d_recv,
+                     const int64_t *h_recv_offsets, const int64_t *h_recv_bytes, int root, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -166,6 +166,34 @@ def _rccl_rank(rank, port, H, W, out_path):
               np.array_equal(got[k][2], ref[k][3]) for k in pipeline.CHANNELS)
     offs, tot = se.offsets()
     ok &= [int(x) for x in tot] == [len(ref[k][2]) for k in pipeline.CHANNELS]
+    # the same gather through the C-ABI (hic_gather_*: the library's own RCCL
+    # communicator), into fresh whole-image buffers, and a root slice that is not in
+    # place (hic_gather_bytes copies it)
+    import ctypes
+    from hiccup_amd import _lib
+    g = sharding.RcclGather(group=xgroup)
+    w, r = ctypes.c_int(), ctypes.c_int()
+    _lib.call("hic_gather_comm_info", g.comm, ctypes.byref(w), ctypes.byref(r))
+    ok &= (w.value, r.value) == (1, 0)
+    se2 = sharding.ShardEncoder(H, W, rank=0, world=1, gather_to=0)
+    se2.encode(device.to_device(rgb))
+    full2 = g.gather_encoders([se2])[0]
+    src = torch.arange(1000, dtype=torch.int16, device="cuda")
+    dst = torch.zeros(1300, dtype=torch.int16, device="cuda")
+    I64 = ctypes.c_int64 * 1
+    _lib.call("hic_gather_bytes", g.comm, device.ptr(src), 2000, device.ptr(dst), I64(600), I64(2000), 0,
+              device.stream_ptr())
+    torch.cuda.synchronize()
+    ok &= all(np.array_equal(full2[k][0].cpu().numpy(), ref[k][0]) and np.array_equal(full2[k][1].cpu().numpy(),
+                                                                                        ref[k][1])
+              for k in pipeline.CHANNELS)
+    ok &= torch.equal(dst[300:1300], src) and int(dst[:300].abs().sum()) == 0
+    try:  # argument errors come back as HIC_ERR_ARG
+        _lib.call("hic_gather_bytes", g.comm, device.ptr(src), 2000, device.ptr(dst), I64(0), I64(10), 0, None)
+        ok = False
+    except ValueError:
+        pass
+    g.close()
     with open(out_path, "w") as f:
         f.write("ok" if ok else "mismatch")
     dist.destroy_process_group()

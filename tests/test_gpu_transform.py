@@ -4,6 +4,8 @@ Small cases are compared with the golden fixtures the reference itself produced
 (tests/golden/make_golden.py); full 4K / 8K planes are compared bit-exactly with
 the C oracle (oracle/hiccup_oracle.c, pinned against the same fixtures).
 """
+import zlib
+
 import numpy as np
 import pytest
 import torch
@@ -96,7 +98,7 @@ def test_layouts_roundtrip(layout, shape):
         np.testing.assert_array_equal(device.to_host(rec), orcc.inv_dct_channel(exp, tab))
 
 
-@pytest.mark.parametrize("path", [-1, _lib.DCT_PATH_F32])
+@pytest.mark.parametrize("path", [-1, _lib.DCT_PATH_F64, _lib.DCT_PATH_F32])
 @pytest.mark.parametrize("H,W", [(4096, 4096), (4320, 7680)])
 def test_full_size_bit_exact(H, W, path):
     """BASELINE configs 2/3 plane sizes, bit-exact against the C oracle (multi-threaded),
@@ -128,32 +130,41 @@ def test_tie_blocks_many():
         np.testing.assert_array_equal(transform.dct_channel(plane, QT[tab]), orcc.dct_channel(plane, tab, threads=8))
 
 
-@pytest.mark.parametrize("path", [_lib.DCT_PATH_F32, _lib.DCT_PATH_F64, _lib.DCT_PATH_F64_NOPF, _lib.DCT_PATH_EXACT])
+@pytest.mark.parametrize("path", [_lib.DCT_PATH_PK, _lib.DCT_PATH_F32, _lib.DCT_PATH_F64, _lib.DCT_PATH_F64_NOPF,
+                                  _lib.DCT_PATH_EXACT])
 @pytest.mark.parametrize("kind", ["levels4", "nearflat", "stripes", "checker", "blur"])
 def test_fast_path_structured_ties(kind, path):
     with _lib.knobs(dct_path=path):
         _structured_ties(kind)
 
 
+def _structured_plane(kind, H, W):
+    rng = np.random.default_rng(zlib.crc32(kind.encode()))
+    if kind == "random":
+        return rng.integers(0, 256, (H, W), dtype=np.uint8)
+    if kind == "levels4":
+        return (rng.integers(0, 4, (H, W)) * 85).astype(np.uint8)
+    if kind == "nearflat":
+        return (128 + rng.integers(-4, 5, (H, W))).astype(np.uint8)
+    if kind == "stripes":
+        plane = np.where((np.arange(W) // rng.integers(1, 4)) % 2 == 0, 255, 0).astype(np.uint8)[None].repeat(H, 0)
+        plane[rng.random((H, W)) < 0.01] = 128
+        return plane
+    if kind == "checker":
+        plane = (((np.arange(H)[:, None] + np.arange(W)[None]) % 2) * 255).astype(np.uint8)
+        plane ^= rng.integers(0, 2, (H, W), dtype=np.uint8)
+        return plane
+    # else ("blur"): chroma-like: pyrDown of noise, many coefficients near +-1/2
+    return orcc.pyr_down(rng.integers(0, 256, (2 * H, 2 * W), dtype=np.uint8))
+
+
 def _structured_ties(kind):
-    """Planes that drive the AAN fast path into its tie handling: 4-level and
+    """Planes that drive the AAN fast paths into their tie handling: 4-level and
     near-flat pixels give exact (2,2)-class and (4,4) ties and the rare whole-set
     redo; stripes / checkerboards give large saturated coefficients.  Every
     layout and both tables, fused RLE-tile variant included, vs the C oracle."""
-    rng = np.random.default_rng(hash(kind) % 2**32)
     H, W = 8 * 160, 8 * 320
-    if kind == "levels4":
-        plane = (rng.integers(0, 4, (H, W)) * 85).astype(np.uint8)
-    elif kind == "nearflat":
-        plane = (128 + rng.integers(-4, 5, (H, W))).astype(np.uint8)
-    elif kind == "stripes":
-        plane = np.where((np.arange(W) // rng.integers(1, 4)) % 2 == 0, 255, 0).astype(np.uint8)[None].repeat(H, 0)
-        plane[rng.random((H, W)) < 0.01] = 128
-    elif kind == "checker":
-        plane = (((np.arange(H)[:, None] + np.arange(W)[None]) % 2) * 255).astype(np.uint8)
-        plane ^= rng.integers(0, 2, (H, W), dtype=np.uint8)
-    else:  # chroma-like: pyrDown of noise, many coefficients near +-1/2 (zero-ambiguous flags)
-        plane = orcc.pyr_down(rng.integers(0, 256, (2 * H, 2 * W), dtype=np.uint8))
+    plane = _structured_plane(kind, H, W)
     d = device.to_device(plane)
     for tab in (0, 1):
         exp = orcc.dct_channel(plane, tab, threads=8)
@@ -183,3 +194,77 @@ def test_bad_args():
         _lib.call("hic_dct_quant_u8", device.ptr(dev), 8, 8, 8, 7, 0, device.ptr(out), device.stream_ptr())
     with pytest.raises(ValueError):
         _lib.call("hic_dct_quant_u8", device.ptr(dev), 8, 8, 8, 0, 9, device.ptr(out), device.stream_ptr())
+
+
+@pytest.mark.parametrize("path", [_lib.DCT_PATH_PK, _lib.DCT_PATH_F64])
+@pytest.mark.parametrize("kind", ["random", "levels4", "nearflat", "blur"])
+@pytest.mark.parametrize("H,W", [(8, 16), (8 * 61, 16 * 7), (8 * 33, 8 * 130), (8 * 160, 8 * 320)])
+def test_plane_dct_rle_records(kind, path, H, W):
+    """The plane DCT's fused RLE tile records (k_dct_pk: two 64-block tiles per
+    128-block set, partial last sets included) drive the channel RLE: symbols and DC
+    differences of hic_dct_quant_rle_u8 + hic_rle_encode_i16_tiles_batch equal the
+    C oracle's run_length_coding / differential_coding (codec.py:47-99)."""
+    plane = _structured_plane(kind, H, W)
+    d = device.to_device(plane)
+    nblk = (H // 8) * (W // 8)
+    lib = _lib.load()
+    for tab in (0, 1):
+        exp = orcc.zigzag_blocks(orcc.dct_channel(plane, tab), 8)
+        eL, eV = orcc.rle_encode(exp[:, 1:].reshape(-1), 15)
+        out = device.empty((nblk, 64), torch.int16)
+        ws = device.workspace(lib.hic_rle_workspace_bytes(nblk, 64))
+        with _lib.knobs(dct_path=path):
+            _lib.call("hic_dct_quant_rle_u8", device.ptr(d), H, W, W, tab, 15, device.ptr(out), device.ptr(ws),
+                      device.stream_ptr(), None, None)
+        cap = nblk * 63 + 1
+        L, V = device.empty((cap,), torch.uint8), device.empty((cap,), torch.int16)
+        dc, cnt = device.empty((nblk,), torch.int32), device.zeros((1,), torch.int64)
+        job = (_lib.RleJob16 * 1)()
+        job[0] = _lib.RleJob16(out.data_ptr(), nblk, None, dc.data_ptr(), L.data_ptr(), V.data_ptr(), cap,
+                               cnt.data_ptr(), ws.data_ptr(), 1)
+        _lib.call("hic_rle_encode_i16_tiles_batch", 1, job, 15, device.stream_ptr())
+        np.testing.assert_array_equal(device.to_host(out).astype(np.int32), exp, err_msg=(kind, tab))
+        c = int(cnt.cpu().item())
+        assert c == len(eL), (kind, tab, c, len(eL))
+        np.testing.assert_array_equal(device.to_host(L[:c]).astype(np.int32), eL, err_msg=(kind, tab))
+        np.testing.assert_array_equal(device.to_host(V[:c]).astype(np.int32), eV, err_msg=(kind, tab))
+        np.testing.assert_array_equal(device.to_host(dc), orcc.dpcm(exp[:, 0].copy()), err_msg=(kind, tab))
+
+
+@pytest.mark.parametrize("waves_per_cu", [-1, 1])
+@pytest.mark.parametrize("kind", ["random", "levels4"])
+def test_plane_batch_three_planes(kind, waves_per_cu):
+    """hic_dct_quant_rle_u8_batch over BASELINE configs[2]'s three planes (8K Y +
+    two 4K chroma) in one launch, the production packed path: with few persistent
+    waves each wave's deferred tie queue mixes sets of different planes (and
+    tables).  Coefficients, DC differences and symbols vs the C oracle."""
+    shapes = [(4320, 7680, 0), (2160, 3840, 1), (2160, 3840, 1)]
+    lib = _lib.load()
+    planes, outs, wss = [], [], []
+    jobs = (_lib.DctPlaneJob * 3)()
+    for i, (h, w, t) in enumerate(shapes):
+        p = _structured_plane(kind, h, w) if i == 0 else np.ascontiguousarray(_structured_plane(kind, h, w)[::-1])
+        nblk = (h // 8) * (w // 8)
+        planes.append((p, device.to_device(p)))
+        outs.append(device.empty((nblk, 64), torch.int16))
+        wss.append(device.workspace(lib.hic_rle_workspace_bytes(nblk, 64)))
+        jobs[i] = _lib.DctPlaneJob(planes[i][1].data_ptr(), h, w, w, t, outs[i].data_ptr(), wss[i].data_ptr())
+    with _lib.knobs(dct_waves_per_cu=waves_per_cu):
+        _lib.call("hic_dct_quant_rle_u8_batch", 3, jobs, 15, device.stream_ptr(), None, None)
+    for i, (h, w, t) in enumerate(shapes):
+        nblk = (h // 8) * (w // 8)
+        exp = orcc.zigzag_blocks(orcc.dct_channel(planes[i][0], t, threads=16), 8)
+        np.testing.assert_array_equal(device.to_host(outs[i]).astype(np.int32), exp, err_msg=(kind, i))
+        cap = nblk * 63 + 1
+        L, V = device.empty((cap,), torch.uint8), device.empty((cap,), torch.int16)
+        dc, cnt = device.empty((nblk,), torch.int32), device.zeros((1,), torch.int64)
+        job = (_lib.RleJob16 * 1)()
+        job[0] = _lib.RleJob16(outs[i].data_ptr(), nblk, None, dc.data_ptr(), L.data_ptr(), V.data_ptr(), cap,
+                               cnt.data_ptr(), wss[i].data_ptr(), 1)
+        _lib.call("hic_rle_encode_i16_tiles_batch", 1, job, 15, device.stream_ptr())
+        eL, eV = orcc.rle_encode(exp[:, 1:].reshape(-1), 15)
+        c = int(cnt.cpu().item())
+        assert c == len(eL), (kind, i, c, len(eL))
+        np.testing.assert_array_equal(device.to_host(L[:c]).astype(np.int32), eL, err_msg=(kind, i))
+        np.testing.assert_array_equal(device.to_host(V[:c]).astype(np.int32), eV, err_msg=(kind, i))
+        np.testing.assert_array_equal(device.to_host(dc), orcc.dpcm(exp[:, 0].copy()), err_msg=(kind, i))

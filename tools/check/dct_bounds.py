@@ -274,6 +274,7 @@ def emit(path):
     lines.append("// fast-path flag threshold: |d| > kThr32 flags (d = Y*R - rint(Y*R));")
     lines.append("// kThr32 = float32 rounded down of 1/2 - W1, W1 = E1 + EP/T + 2^-24 + 2^-40")
     lines.append("constexpr float kThr32[2][64] = {")
+    thr = [[], []]
     for t in range(2):
         vals = []
         for i in range(64):
@@ -281,6 +282,20 @@ def emit(path):
             if float(th) > 0.5 - W1[t].flat[i]:
                 th = np.nextafter(th, np.float32(0))
             vals.append(float(th))
+        thr[t] = vals
+        lines.append("    {" + ", ".join(v.hex() + "f" for v in vals) + "},")
+    lines.append("};")
+    # the packed path tests d^2 > c instead of |d| > thr: c must not exceed thr^2, so
+    # every |d| > thr is still flagged (fl(c - d*d) in one fma has d*d's exact sign)
+    lines.append("// packed-path threshold: d*d > kThr32Sq flags; kThr32Sq = float32 rounded down of kThr32^2")
+    lines.append("constexpr float kThr32Sq[2][64] = {")
+    for t in range(2):
+        vals = []
+        for th in thr[t]:
+            sq = np.float32(th * th)
+            if float(sq) > th * th:  # float64 th*th is exact (24-bit th)
+                sq = np.nextafter(sq, np.float32(0))
+            vals.append(float(sq))
         lines.append("    {" + ", ".join(v.hex() + "f" for v in vals) + "},")
     lines.append("};")
     m2 = float(W2.max())

@@ -58,6 +58,25 @@ __global__ __launch_bounds__(256) void k_blk16(const uint8_t *__restrict__ plane
   }
 }
 
+// lane = two blocks, each lane stores its own 2 x 128 B (16 x 16 B at its block
+// addresses: every store instruction touches 64 lines, 16 B each), no LDS stage
+template <bool NT>
+__global__ __launch_bounds__(256) void k_blk16_lane(const uint8_t *__restrict__ plane, int W, int nsets2,
+                                                    uint8_t *__restrict__ out) {
+  const int lane = threadIdx.x & 63, nbx = W / 8;
+  for (int set = blockIdx.x * 4 + (threadIdx.x >> 6); set < nsets2; set += gridDim.x * 4) {
+    const int b = set * 128 + 2 * lane, by = b / nbx, bx = b - by * nbx;
+    const uint8_t *p = plane + (int64_t)by * 8 * W + bx * 8;
+    uint4 w[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) w[r] = *reinterpret_cast<const uint4 *>(p + (int64_t)r * W);
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      put<NT>(out, ((int64_t)set * 128 + 2 * lane) * 8 + u,
+              (u32x4){w[u & 7].x, w[u & 7].y ^ u, w[(u + 1) & 7].z, w[(u + 3) & 7].w});
+  }
+}
+
 // a wave reads 8 rows x 1 KiB (128 blocks of one block row; the row's last chunk
 // is 512 B, 64 blocks), lane = 16 B of a row; the chunk's coefficients are written
 // 1 KiB per instruction
@@ -116,6 +135,9 @@ int main() {
       {"blk16 1w", 2, (nsets2 + 3) / 4}, {"blk16 persist 16/CU", 2, cus * 4},
       {"rows16 1w", 3, ((H / 8) * ((W + 1023) / 1024) + 3) / 4}, {"rows16 persist 16/CU", 3, cus * 4},
       {"stream 1:2", 4, cus * 8},
+      {"blk16_lane nt 1w", 5, (nsets2 + 3) / 4}, {"blk16_lane nt persist 8/CU", 5, cus * 2},
+      {"blk16_lane plain 1w", 6, (nsets2 + 3) / 4}, {"blk16_lane plain persist 8/CU", 6, cus * 2},
+      {"blk16 persist 8/CU", 2, cus * 2},
   };
   const int n = 14;
   for (const V &v : vs) {
@@ -128,6 +150,8 @@ int main() {
       if (v.kind == 2) hipLaunchKernelGGL(k_blk16, g, b, 0, 0, in[i % rot], W, nsets2, out[i % rot]);
       if (v.kind == 3) hipLaunchKernelGGL(k_rows16, g, b, 0, 0, in[i % rot], W, H, out[i % rot]);
       if (v.kind == 4) hipLaunchKernelGGL(k_stream, g, b, 0, 0, in[i % rot], np, out[i % rot]);
+      if (v.kind == 5) hipLaunchKernelGGL(k_blk16_lane<true>, g, b, 0, 0, in[i % rot], W, nsets2, out[i % rot]);
+      if (v.kind == 6) hipLaunchKernelGGL(k_blk16_lane<false>, g, b, 0, 0, in[i % rot], W, nsets2, out[i % rot]);
       (void)hipEventRecord(e);
       (void)hipEventSynchronize(e);
       float ms;

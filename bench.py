@@ -45,13 +45,12 @@ sys.path.insert(0, HERE)
 H8K, W8K = 4320, 7680
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 XGMI_LINK_GBS = 153.0  # per xGMI link of an MI355X (7 per GPU), the figure given with this build
-ROT_BYTES = 1.2e9
-# measured memory-only floors (no arithmetic) of the two roofline kernels' byte
-# mixes on MI355X: profiles/r02/micro_plane_patterns.log (8K luma DCT pass: the
-# linear stream of 33 MB in / 66 MB out) and profiles/r02/micro_rgb_rows.log (the
-# fused encoder's 19 RGB rows + 24 KiB of stores per unit)
-LUMA_PASS_FLOOR_US = 20.8
-FUSED_FLOOR_US = 43.0      # rotate >= 1.2 GB of inputs: defeats the 256 MiB Infinity Cache
+ROT_BYTES = 1.2e9          # rotate >= 1.2 GB of inputs: defeats the 256 MiB Infinity Cache
+# the fused encoder's memory-only floor (19 RGB rows + 24 KiB of stores per unit, no
+# arithmetic) from the committed micro-benchmark log profiles/r02/micro_rgb_rows.log
+# (tools/micro/rgb_rows.hip) -- NOT measured in the bench run; the plane pass's floor
+# and the device-copy rate are (measure_floors)
+FUSED_FLOOR_US_MICRO = 43.0
 
 
 def parse():
@@ -212,7 +211,7 @@ def extra_4k_rgb_encode(steps=40, n_streams=2):
             "timed_images": steps}
 
 
-def extra_8k_plane_dct(steps=24, luma_only=False):
+def extra_8k_plane_dct(steps=24, luma_only=False, floor_us=None):
     """The north_star's DCT+quantize pass on its own: k_dct_planes over the 8K Y +
     Cr + Cb planes (4320 x 7680 + 2 x 2160 x 3840 uint8 -> int16 zig-zag blocks +
     RLE tile records, one launch, the two-kernel chain's second kernel), or over the
@@ -256,11 +255,77 @@ def extra_8k_plane_dct(steps=24, luma_only=False):
            "kernel": "k_dct_planes<-1,ZIGZAG_I16,15>", "median_launch_us": round(us, 2),
            "achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes": px * 3,
            "read_only_frac": round(px / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4), "timed_launches": steps}
-    if luma_only:
-        # the byte mix's own floor on this hardware: a linear stream of 33 MB in and
-        # 66 MB out, no arithmetic (tools/micro/plane_patterns.hip)
-        out["memory_floor_us_measured"] = LUMA_PASS_FLOOR_US
-        out["frac_of_measured_floor"] = round(LUMA_PASS_FLOOR_US / us, 4)
+    if luma_only and floor_us:
+        # the pass's own byte pattern without the DCT, measured in this run
+        # (measure_floors: hic_probe_plane on the same plane size)
+        out["memory_floor_us_measured"] = floor_us
+        out["frac_of_measured_floor"] = round(floor_us / us, 4)
+    return out
+
+
+def measure_floors(steps=20):
+    """In-run memory floors (hic_probe_copy / hic_probe_plane, memory-only probes in
+    the product library), each timed by the launches' own HIP events over >= 1.2 GB
+    of rotating buffers:
+      device_copy_gbs: a streaming device copy (read + write bytes / time);
+      luma_pattern:    the forward plane pass's own byte pattern without the DCT
+                       (8x8 block loads, LDS stage, 1 KiB nontemporal stores, 1 B
+                       read + 2 B written per pixel), on 1x / 2x / 4x the 8K luma
+                       plane per launch -- whether the pass's floor is the access
+                       pattern or the per-launch ramp and tail."""
+    from hiccup_amd import _lib, device
+    out = {}
+    nbytes = 256 << 20
+    nbuf = int(np.ceil(ROT_BYTES / (2 * nbytes)))
+    bufs = [(device.empty((nbytes,), torch.uint8), device.empty((nbytes,), torch.uint8)) for _ in range(nbuf)]
+    for a, _ in bufs:
+        a.fill_(7)
+    evs = [device.KernelEvents() for _ in range(steps)]
+
+    def timed(launch):
+        for i in range(steps + 3):
+            ev = evs[i - 3] if i >= 3 else None
+            launch(i, ev.start if ev else None, ev.stop if ev else None)
+        torch.cuda.synchronize()
+        return float(np.median([e.elapsed_ms() for e in evs])) * 1e3
+
+    # the best of three grid sizes (the probes claim a floor, so they get the best
+    # configuration this run finds)
+    per = {}
+    for wpc in (8, 16, 32):
+        per[wpc] = timed(lambda i, e0, e1: _lib.call("hic_probe_copy", device.ptr(bufs[i % nbuf][0]),
+                                                     device.ptr(bufs[i % nbuf][1]), nbytes, wpc,
+                                                     device.stream_ptr(), e0, e1))
+    best = min(per, key=per.get)
+    us = per[best]
+    out["device_copy_gbs"] = round(2 * nbytes / (us * 1e-6) / 1e9, 1)
+    out["device_copy"] = {"bytes_per_launch": nbytes, "median_launch_us": round(us, 2), "waves_per_cu": best,
+                          "frac_of_8tbs": round(2 * nbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                          "us_by_waves_per_cu": {k: round(v, 2) for k, v in per.items()}}
+    del bufs
+    torch.cuda.empty_cache()
+    pat = {}
+    for mult in (1, 2, 4):
+        h, w = H8K * mult, W8K
+        px = h * w
+        rot = max(2, int(np.ceil(ROT_BYTES / (3 * px))))
+        g = torch.Generator(device="cuda")
+        g.manual_seed(9)
+        planes = [torch.randint(0, 256, (h, w), dtype=torch.uint8, device="cuda", generator=g) for _ in range(rot)]
+        outs = [device.empty((px // 64, 64), torch.int16) for _ in range(rot)]
+        per = {}
+        for wpc in (12, 16):
+            per[wpc] = timed(lambda i, e0, e1: _lib.call("hic_probe_plane", device.ptr(planes[i % rot]), h, w,
+                                                         device.ptr(outs[i % rot]), wpc, device.stream_ptr(), e0, e1))
+        best = min(per, key=per.get)
+        us = per[best]
+        pat["%dx" % mult] = {"plane_hw": [h, w], "bytes_per_launch": 3 * px, "median_launch_us": round(us, 2),
+                             "waves_per_cu": best, "us_by_waves_per_cu": {k: round(v, 2) for k, v in per.items()},
+                             "gbs": round(3 * px / (us * 1e-6) / 1e9, 1),
+                             "frac_of_8tbs": round(3 * px / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+        del planes, outs
+        torch.cuda.empty_cache()
+    out["luma_pattern"] = pat
     return out
 
 
@@ -729,14 +794,21 @@ def main():
                 "avg_launch_us": round(dct_us, 2),
                 "timed_over": roof_note,
                 "avg_launch_us_overlapped": None if dct_us_overlapped is None else round(dct_us_overlapped, 2),
-                "memory_floor_us_measured": FUSED_FLOOR_US if (fused and args.workload == "8k" and world == 1)
+                "memory_floor_us_micro": FUSED_FLOOR_US_MICRO if (fused and args.workload == "8k" and world == 1)
                 else None,
+                "memory_floor_source": "profiles/r02/micro_rgb_rows.log (committed micro log, not this run)",
             },
         }
+        if world == 1:
+            floors = measure_floors()
+            out["memory_floors"] = floors
+            out["roofline"]["device_copy_gbs"] = floors["device_copy_gbs"]
+            out["roofline"]["frac_of_device_copy"] = round(achieved / floors["device_copy_gbs"], 4)
         if not args.no_extras and world == 1:
             out["extra_configs"] = {"4k_rgb_encode": extra_4k_rgb_encode(),
                                     "4k_luma_dct": extra_4k_luma(), "8k_plane_dct": extra_8k_plane_dct(),
-                                     "8k_luma_dct": extra_8k_plane_dct(luma_only=True),
+                                    "8k_luma_dct": extra_8k_plane_dct(
+                                        luma_only=True, floor_us=floors["luma_pattern"]["1x"]["median_launch_us"]),
                                     "16k_roundtrip": extra_16k_roundtrip()}
         if extra_sharded is not None:
             out["extra_configs"] = {"16k_roundtrip": extra_sharded}

@@ -47,6 +47,8 @@ SIGNATURES = {
     "hic_device_count": (_int, [ctypes.POINTER(_int)]),
     "hic_stream_sync": (_int, [_vp]),
     "hic_stream_create_cu_mask": (_int, [_vp, _int, _vp]),
+    "hic_probe_copy": (_int, [_vp, _vp, _i64, _int, _vp, _vp, _vp]),
+    "hic_probe_plane": (_int, [_vp, _i64, _i64, _vp, _int, _vp, _vp, _vp]),
     "hic_stream_destroy": (_int, [_vp]),
     "hic_set_knob": (_int, [_int, _int]),
     "hic_get_knob": (_int, [_int, ctypes.POINTER(_int)]),

@@ -12,7 +12,7 @@ int knob(int k) {
   const int v = g_knobs[k];
   if (v >= 0) return v;
   switch (k) {
-    case HIC_KNOB_DCT_PATH: return 4;
+    case HIC_KNOB_DCT_PATH: return 1;
     case HIC_KNOB_COLOR_SEG: return 8;
     case HIC_KNOB_RLE_NT: return 1;
     case HIC_KNOB_ENCODE_WAVES: return 2;

@@ -864,8 +864,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
 //    patches.  A coefficient that resolve_coef cannot settle recomputes its block on
 //    the exact pocketfft replica (and marks the tile); a set whose flags overflow
 //    the queue runs its flagged blocks on the replica before its store.
-constexpr int kPkQCap = 32;    // deferred items per wave (each with its block's 64 B of pixels)
-constexpr int kPkQFlush = 20;  // flush after a set once this many are queued
+constexpr int kPkQCap = 48;    // deferred items per wave (each with its block's 64 B of pixels)
+constexpr int kPkQFlush = 36;  // flush after a set once this many are queued
 
 __device__ __forceinline__ void pk_load(const DctJob &J, int set, int lane, uint2 (&w)[8]) {
   int blk = set * 64 + lane;
@@ -891,7 +891,7 @@ __device__ __attribute__((noinline)) void pk_exact_block(const uint8_t *plane, i
     dct_block_2ph<1, HIC_LAYOUT_ZIGZAG_I16>(w, st);
 }
 
-// Flush (cold): resolve the n <= 32 queued items, one per lane.  Item =
+// Flush (cold): resolve the n <= 48 queued items, one per lane.  Item =
 // {wave set index k (g = g0 + k nwaves), lane << 26 | flag bit << 20 | provisional
 // q} + its block's 8 pixel rows (qp, 4 x 16 B), so no HBM reads.  Returns the
 // wave's dirty-tile mask (bit k: set k's record must be rebuilt).

@@ -858,9 +858,13 @@ __host__ __device__ __forceinline__ int pk_flag_index(int b) {
 }
 
 // Fallback: y_uv (full scale, as scipy's 2-D DCT-II of the centred block) in
-// float64 as a separable dot product, bounded by E2 (2^-34.5, dct_bounds.py).
-// u, v may differ per lane.  cm[m] = 2 cos(pi m / 16), m = 0..8, correctly
-// rounded; the 2 cos(pi k (2n+1) / 16) factors follow by symmetry (period 32,
+// float64, bounded by E2 (dct_bounds.py).  Separable and folded by symmetry
+// (C_k(7 - n) = (-1)^k C_k(n), C_k(n) = 2 cos(pi k (2n + 1) / 16)):
+//   r_m = sum_{n<4} C_v(n) a_mn,  a_mn = x_mn + (-1)^v x_m,7-n (centred; an exact
+//         integer), as one multiply and three fmas;
+//   y   = sum_{m<4} C_u(m) b_m,   b_m = r_m + (-1)^u r_7-m (one rounded add),
+// 40 float64 operations instead of 72.  u, v may differ per lane.  cm[m] = 2 cos(pi
+// m / 16), m = 0..8, correctly rounded; the factors follow by symmetry (period 32,
 // cos(pi - a) = -cos(a)).  The caller passes cm from wherever is cheapest to read
 // per lane (LDS in the kernels).
 constexpr double kCm[9] = {2.0,
@@ -883,23 +887,26 @@ __host__ __device__ __forceinline__ double cos2(const double *cm, int k, int n) 
 // ctab: nullptr -> computed from kCm; else the full table ctab[8k + n] = cos2(kCm, k, n)
 __host__ __device__ __forceinline__ double dct_coef_f64(const uint2 (&w)[8], int u, int v,
                                                        const double *ctab = nullptr) {
-  double cv[8], cu[8];
+  double cv[4], cu[4];
 #pragma unroll
-  for (int n = 0; n < 8; ++n) {
+  for (int n = 0; n < 4; ++n) {
     cv[n] = ctab ? ctab[8 * v + n] : cos2(kCm, v, n);
     cu[n] = ctab ? ctab[8 * u + n] : cos2(kCm, u, n);
   }
-  double y = 0.0;
+  const int sv = (v & 1) ? -1 : 1, ov = (v & 1) ? 0 : 256;  // a = x_n + sv x_{7-n} - ov (raw bytes)
+  double r[8];
 #pragma unroll
   for (int m = 0; m < 8; ++m) {
-    auto px = [&](int n) -> double {
-      return (double)((int)(((n < 4 ? w[m].x : w[m].y) >> (8 * (n & 3))) & 0xFFu) - 128);
-    };
-    double r = px(0) * cv[0];
+    auto px = [&](int n) -> int { return (int)(((n < 4 ? w[m].x : w[m].y) >> (8 * (n & 3))) & 0xFFu); };
+    double acc = (double)(px(0) + sv * px(7) - ov) * cv[0];
 #pragma unroll
-    for (int n = 1; n < 8; ++n) r = __builtin_fma(px(n), cv[n], r);
-    y = m == 0 ? r * cu[0] : __builtin_fma(r, cu[m], y);
+    for (int n = 1; n < 4; ++n) acc = __builtin_fma((double)(px(n) + sv * px(7 - n) - ov), cv[n], acc);
+    r[m] = acc;
   }
+  const bool uo = (u & 1) != 0;
+  double y = (uo ? r[0] - r[7] : r[0] + r[7]) * cu[0];
+#pragma unroll
+  for (int m = 1; m < 4; ++m) y = __builtin_fma(uo ? r[m] - r[7 - m] : r[m] + r[7 - m], cu[m], y);
   return y;
 }
 

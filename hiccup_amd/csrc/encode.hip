@@ -144,9 +144,85 @@ __device__ __forceinline__ void enc_dct_f32(uint2 (&w)[8], int16_t *st) {
   }
 }
 
-template <int TABLE, bool F32>
-__device__ __forceinline__ void enc_dct_any(uint2 (&w)[8], int16_t *st) {
-  if (F32)
+// Packed float32 variant (knob "encode_dct" = 2): dct_block_pk (dct_core.h: two
+// transforms of the block per v_pk op, (4,4) ties decided in place), the proven
+// float32 windows.  The flagged coefficients (~0.03 per block on random data) are
+// resolved inline before the stage leaves: compacted into a per-wave LDS list
+// {owner lane, flag bit}, one item per lane, the owner's pixel rows fetched by
+// ds_bpermute (no LDS copy), resolve_coef (float64 dot product, pocketfft's own
+// operations for the rational classes), the result written into the owner's stage
+// row.  No call: an out-of-line resolve made every live register of this kernel
+// cross scratch.  A coefficient that stays ambiguous (or a list overflow) sends
+// the owner's block to the exact replica (out of line; never seen on natural data).
+constexpr int kEncQCap = 64;
+
+__device__ __forceinline__ uint32_t enc_bperm(int src_lane, uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
+}
+
+template <int TABLE>
+__device__ __forceinline__ void enc_dct_pk(uint2 (&w)[8], int16_t *st, uint2 *st2, uint32_t *qlist, const double *cm,
+                                           const uint8_t *qt) {
+  constexpr SlotOf<kZZ> kSlot{};
+  uint32_t f0 = 0, f1 = 0;
+  dct_block_pk<TABLE>(w, st, f0, f1);
+  const int lane = threadIdx.x & 63;
+  uint64_t bits = ((uint64_t)f1 << 32) | f0;
+#if defined(HIC_DEV) && defined(HIC_ENC_DEV) && (HIC_ENC_DEV & 4)
+  bits = 0;  // dev timing (results invalid): flags dropped, no resolve
+#endif
+  if (!__builtin_amdgcn_ballot_w64(bits != 0)) return;
+  const bool mine = bits != 0;
+  int n = 0;
+  bool over = false;
+  for (;;) {  // compact: one flag per lane per pass
+    const bool has = bits != 0;
+    const uint64_t m = __builtin_amdgcn_ballot_w64(has);
+    if (!m) break;
+    if (has) {
+      const int b = __builtin_ctzll(bits);
+      bits &= bits - 1;
+      const int pos = n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (pos < kEncQCap) qlist[pos] = (uint32_t)(lane << 8 | b);
+    }
+    n += __builtin_popcountll(m);
+  }
+  if (n > kEncQCap) {
+    over = true;
+    n = kEncQCap;
+  }
+  __builtin_amdgcn_wave_barrier();
+  // one round (n <= 64): lane j resolves item j
+  const uint32_t it = lane < n ? qlist[lane] : 0u;
+  const int owner = (int)(it >> 8);
+  uint2 wo[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) wo[r] = make_uint2(enc_bperm(owner, w[r].x), enc_bperm(owner, w[r].y));
+  bool fail = false;
+  if (lane < n) {
+    const int i = pk_flag_index((int)(it & 63u));
+    int q = 0;
+    if (resolve_coef(wo, TABLE, i, q, cm, qt))  // cos / table lookups from LDS, not select chains
+      reinterpret_cast<int16_t *>(st2 + owner * kStageU2)[kSlot.s[i]] = (int16_t)q;
+    else
+      fail = true;
+  }
+  // owners of an unresolved item (or of any item, after an overflow): exact replica
+  const uint64_t fm = __builtin_amdgcn_ballot_w64(fail);
+  bool redo = over && mine;
+  for (uint64_t mm = fm; mm; mm &= mm - 1) redo |= __builtin_amdgcn_readlane(owner, __builtin_ctzll(mm)) == lane;
+  __builtin_amdgcn_wave_barrier();
+  if (__builtin_amdgcn_ballot_w64(redo))
+    if (redo) enc_exact_block<TABLE>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], st);
+}
+
+// DM: the DCT variant (0 float64 AAN, 1 scalar float32, 2 packed float32)
+template <int TABLE, int DM>
+__device__ __forceinline__ void enc_dct_any(uint2 (&w)[8], int16_t *st, uint2 *st2, uint32_t *qlist, const double *cm,
+                                            const uint8_t *qt) {
+  if (DM == 2)
+    enc_dct_pk<TABLE>(w, st, st2, qlist, cm, qt);
+  else if (DM == 1)
     enc_dct_f32<TABLE>(w, st);
   else
     enc_dct<TABLE>(w, st);
@@ -402,7 +478,7 @@ struct EncColour {
 #define HIC_ENC_VG 1  // 16-row units per wave (2: two vertically adjacent units, 35 input rows
                       // for 32; measured 61-65 vs 60-63 us: no gain, scripts/gpu_r2ah.sh)
 #endif
-template <int TMF, bool NT, bool F32>
+template <int TMF, bool NT, int DM>
 __device__ __forceinline__ void encode420_unit(const Enc420 &E);
 
 // Two register budgets (knob "encode_waves", A/B): 2 waves per SIMD (default: up
@@ -411,20 +487,28 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E);
 // NT: nontemporal coefficient stores (knob "encode_nt" = 1).  Default 0: plain
 // stores, so part of the coefficients is still in the Infinity Cache when the RLE
 // emit re-reads them (emit 59.7 -> 54.7 us; 8K encode +2-4 %, scripts/gpu_r2i.sh)
-// F32: the float32 DCT variant (knob "encode_dct" = 1, enc_dct_f32)
-template <int TMF, bool NT, bool F32>
+// DM: the DCT variant (knob "encode_dct": 0 float64 AAN, 1 scalar float32 enc_dct_f32, 2 packed float32 enc_dct_pk)
+template <int TMF, bool NT, int DM>
 __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_eu(3))) void k_encode420(Enc420 E) {
-  encode420_unit<TMF, NT, F32>(E);
+  encode420_unit<TMF, NT, DM>(E);
 }
-template <int TMF, bool NT, bool F32>
+template <int TMF, bool NT, int DM>
 __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_eu(2))) void k_encode420_w2(Enc420 E) {
-  encode420_unit<TMF, NT, F32>(E);
+  encode420_unit<TMF, NT, DM>(E);
 }
 
-template <int TMF, bool NT, bool F32>
+template <int TMF, bool NT, int DM>
 __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
   __shared__ uint2 s_stage[HIC_ENC_WPB * 64 * kStageU2];
   __shared__ uint32_t s_chroma_all[HIC_ENC_WPB][2 * 8 * 64];
+  __shared__ uint32_t s_qlist_all[HIC_ENC_WPB][DM == 2 ? kEncQCap : 1];
+  __shared__ double s_cm[DM == 2 ? 64 : 1];    // the fallback's cos2 table and QT (per-lane lookups)
+  __shared__ uint8_t s_qt[DM == 2 ? 128 : 1];
+  if (DM == 2) {
+    if (threadIdx.x < 64) s_cm[threadIdx.x] = cos2(kCm, threadIdx.x >> 3, threadIdx.x & 7);
+    if (threadIdx.x < 128) s_qt[threadIdx.x] = (uint8_t)QT[threadIdx.x >> 6][threadIdx.x & 63];
+    __syncthreads();
+  }
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // Workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8 share one,
   // MI355X_MICROARCH.md "Workgroup dispatch"; for speed only, any placement is
@@ -441,6 +525,7 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
   if (g >= E.nunits) return;  // wave-uniform
   uint2 *st2 = s_stage + wv * 64 * kStageU2;
   uint32_t *s_chroma = s_chroma_all[wv];
+  uint32_t *s_qlist = s_qlist_all[wv];
   int16_t *st = reinterpret_cast<int16_t *>(st2 + lane * kStageU2);
   // wave g: strip s, unit rows u0 .. u0 + HIC_ENC_VG - 1 (the last wave of a strip
   // may have one unit row only)
@@ -457,7 +542,7 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
     uint2 w[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) w[r] = yq[8 * br + r];
-    enc_dct_any<0, F32>(w, st);
+    enc_dct_any<0, DM>(w, st, st2, s_qlist, s_cm, s_qt);
     __builtin_amdgcn_wave_barrier();
     const int64_t b0 = (int64_t)(2 * u + br) * nbx + 64 * s;
     int16_t *o = E.coef[0] + b0 * 64;
@@ -478,7 +563,7 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
     uint2 w[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = sc[i * 32];
-    enc_dct_any<1, F32>(w, st);
+    enc_dct_any<1, DM>(w, st, st2, s_qlist, s_cm, s_qt);
     __builtin_amdgcn_wave_barrier();
     const int64_t b0 = (int64_t)u * nbxc + 32 * s;
     enc_store<NT>(st2, lane, E.coef[1] + b0 * 64, E.coef[2] + b0 * 64);
@@ -607,15 +692,17 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
       hipLaunchKernelGGL(kern, grid, block, pad, s, E);
   };
   const bool w2 = knob(HIC_KNOB_ENCODE_WAVES) == 2, nt = knob(HIC_KNOB_ENCODE_NT) != 0;
-  const bool f32 = knob(HIC_KNOB_ENCODE_DCT) == 1;
-  // variants: {2, 3} waves per SIMD x {float64, float32} DCT x {cached, nontemporal}
-  // stores (the last at 2 waves and float64 only) x {max_len 15, any}
+  const int dm = knob(HIC_KNOB_ENCODE_DCT);
+  // variants: {2, 3} waves per SIMD x {float64, float32, packed float32} DCT x
+  // {cached, nontemporal} stores (the last at 2 waves and float64 only) x {max_len 15, any}
 #define HIC_ENC_VARIANTS(M)                                                 \
-  if (nt && w2 && !f32) launch(k_encode420_w2<M, true, false>);             \
-  else if (w2 && f32) launch(k_encode420_w2<M, false, true>);               \
-  else if (w2) launch(k_encode420_w2<M, false, false>);                     \
-  else if (f32) launch(k_encode420<M, false, true>);                        \
-  else launch(k_encode420<M, false, false>)
+  if (nt && w2 && dm == 0) launch(k_encode420_w2<M, true, 0>);              \
+  else if (w2 && dm == 2) launch(k_encode420_w2<M, false, 2>);              \
+  else if (w2 && dm == 1) launch(k_encode420_w2<M, false, 1>);              \
+  else if (w2) launch(k_encode420_w2<M, false, 0>);                         \
+  else if (dm == 2) launch(k_encode420<M, false, 2>);                       \
+  else if (dm == 1) launch(k_encode420<M, false, 1>);                       \
+  else launch(k_encode420<M, false, 0>)
   if (max_len == 15) {
     HIC_ENC_VARIANTS(15);
   } else {

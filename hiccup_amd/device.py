@@ -1,6 +1,7 @@
 """Device plumbing: PyTorch-ROCm provides HBM allocations and the HIP stream;
 the compute is entirely in libhiccup_hip.so.  No CPU fallback: without a HIP
 device every entry point raises ``HipUnavailable``."""
+import contextlib
 import ctypes
 
 import numpy as np
@@ -25,6 +26,13 @@ def require_gpu():
 def stream_ptr(stream=None):
     s = stream if stream is not None else torch.cuda.current_stream()
     return ctypes.c_void_p(s.cuda_stream)
+
+
+def on_stream(stream=None):
+    """Context that makes `stream` torch's current stream (a no-op for None): the
+    allocations made inside belong to it, and host reads (.cpu()) wait for the
+    kernels launched on it."""
+    return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
 
 
 def ptr(t):

@@ -247,6 +247,10 @@ class HuffmanTree:
         the bits io.padded_bs_2_bytes stores after its pad-length byte."""
         if n == 0:
             return np.zeros(0, np.uint8), 0
+        with device.on_stream(stream):
+            return self._encode_device(keys_dev, n, key_min, nbins, counts, stream)
+
+    def _encode_device(self, keys_dev, n, key_min, nbins, counts, stream):
         bits, lens = self.code_table(key_min, nbins)
         total = int(np.sum(np.asarray(counts, dtype=np.int64) * lens.astype(np.int64)))
         nbytes = max(4, -(-total // 32) * 4)
@@ -290,20 +294,22 @@ def first_appearance_counts(keys):
 def device_key_range(keys_dev, n=None, stream=None):
     """(min, max) of a device key stream (hic_key_range; syncs)."""
     n = keys_dev.numel() if n is None else n
-    mm = device.empty((2,), torch.int32)
-    _lib.call("hic_key_range", device.ptr(keys_dev), keys_dev.element_size(), n, device.ptr(mm),
-              device.stream_ptr(stream))
-    lo, hi = (int(x) for x in mm.cpu().tolist())
+    with device.on_stream(stream):
+        mm = device.empty((2,), torch.int32)
+        _lib.call("hic_key_range", device.ptr(keys_dev), keys_dev.element_size(), n, device.ptr(mm),
+                  device.stream_ptr(stream))
+        lo, hi = (int(x) for x in mm.cpu().tolist())
     return lo, hi
 
 
 def device_counts_raw(keys_dev, n, key_min, nbins, stream=None):
     """Per-bin (counts, first index) host arrays of hic_key_histogram (syncs)."""
-    counts = device.empty((nbins,), torch.int32)
-    first = device.empty((nbins,), torch.int32)
-    _lib.call("hic_key_histogram", device.ptr(keys_dev), keys_dev.element_size(), n, key_min, nbins,
-              device.ptr(counts), device.ptr(first), device.stream_ptr(stream))
-    return counts.cpu().numpy().view(np.uint32), first.cpu().numpy().view(np.uint32)
+    with device.on_stream(stream):
+        counts = device.empty((nbins,), torch.int32)
+        first = device.empty((nbins,), torch.int32)
+        _lib.call("hic_key_histogram", device.ptr(keys_dev), keys_dev.element_size(), n, key_min, nbins,
+                  device.ptr(counts), device.ptr(first), device.stream_ptr(stream))
+        return counts.cpu().numpy().view(np.uint32), first.cpu().numpy().view(np.uint32)
 
 
 class DeviceStream:
@@ -349,11 +355,18 @@ class DeviceStreams:
     synchronising copies per stream."""
 
     def __init__(self, keys_list, stream=None):
+        """stream: the stream the keys were produced on (None: the current one); every
+        launch, allocation and host read here runs on it."""
         self.keys = [k for k, _ in keys_list]
         self.n = [int(n) for _, n in keys_list]
         self.stream = stream
         if min(self.n) == 0:
             raise ValueError("empty key stream")
+        with device.on_stream(stream):
+            self._histograms()
+
+    def _histograms(self):
+        stream = self.stream
         lib = _lib.load()
         s = device.stream_ptr(stream)
         m = len(self.keys)
@@ -385,6 +398,10 @@ class DeviceStreams:
 
     def packed(self):
         """[(packed uint8 numpy array, number of bits)] per stream (hic_huffman_pack)."""
+        with device.on_stream(self.stream):
+            return self._packed()
+
+    def _packed(self):
         m = len(self.keys)
         s = device.stream_ptr(self.stream)
         tabs = [t.code_table(lo, nb) for t, lo, nb in zip(self.trees, self.lo, self.nbins)]

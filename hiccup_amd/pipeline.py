@@ -190,6 +190,12 @@ class Encoder:
         from . import huffman
         if self.rows != (0, self.H):
             raise ValueError("hic_image needs the whole image (an unsharded encoder)")
+        with device.on_stream(stream):  # the counts and histograms are read after the stream's kernels
+            return self._hic_image(stream)
+
+    def _hic_image(self, stream):
+        from . import hicimage as hic
+        from . import huffman
         counts = self.counts.cpu().tolist()
         keys = {}
         for i, k in enumerate(CHANNELS):

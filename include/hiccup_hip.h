@@ -64,7 +64,7 @@ int hic_device_count(int *h_n);
  * Every selectable path is bit-exact: a knob never changes results, only which
  * kernel variant computes them.  The library reads no environment variables.
  * Values are process-wide; -1 restores the default. */
-#define HIC_KNOB_DCT_PATH 0         /* forward DCT: 4 packed-float32 pair AAN + exact queue (default; aligned planes, W % 16 == 0), 1 float64 AAN, 2 the same unpipelined, 3 scalar float32 AAN + float64 fallback, 0 exact replica */
+#define HIC_KNOB_DCT_PATH 0         /* forward DCT: 1 float64 AAN (default), 4 packed-float32 AAN + deferred exact queue (aligned planes), 2 float64 AAN unpipelined, 3 scalar float32 AAN + float64 fallback, 0 exact replica */
 #define HIC_KNOB_DCT_WAVES_PER_CU 1 /* forward DCT persistent grid (waves per CU; 0 = one wave per set) */
 #define HIC_KNOB_COLOR_TILED 2      /* 1: LDS-tiled colour kernels instead of the wave-walk ones */
 #define HIC_KNOB_COLOR_SEG 3        /* wave-walk colour: chroma rows per segment (8 default, 16) */
@@ -75,7 +75,7 @@ int hic_device_count(int *h_n);
 #define HIC_KNOB_DEV 8              /* dev builds only (-DHIC_DEV): timing bits that skip work; refused otherwise */
 #define HIC_KNOB_ENCODE_WAVES 9     /* hic_encode420_u8: register budget for 2 (default) or 3 waves per SIMD */
 #define HIC_KNOB_ENCODE_NT 10       /* hic_encode420_u8: 1 = nontemporal coefficient stores (default 0: cached) */
-#define HIC_KNOB_ENCODE_DCT 11      /* hic_encode420_u8: 1 = float32 AAN DCT with proven windows + in-place fallbacks (default 0: float64) */
+#define HIC_KNOB_ENCODE_DCT 11      /* hic_encode420_u8: 1 = scalar float32 AAN DCT, 2 = packed float32 AAN DCT (proven windows + in-place fallbacks; default 0: float64) */
 #define HIC_KNOB_ENCODE_LDS_PAD 12  /* hic_encode420_u8: KiB of extra LDS per workgroup (0..64; 40 leaves one encode workgroup per CU, the rest of the CU to a concurrent kernel) */
 #define HIC_KNOB_ENCODE_XCD 13     /* hic_encode420_u8: 1 = each XCD takes a contiguous band of unit rows (pyrDown halo rows re-read from its own L2), 0 = dispatch order */
 #define HIC_KNOB_COUNT 14
@@ -88,6 +88,22 @@ int hic_stream_sync(void *stream);
  * of bench.py --cu-split.  Destroy with hic_stream_destroy. */
 int hic_stream_create_cu_mask(const uint32_t *h_mask, int nwords, void **h_stream);
 int hic_stream_destroy(void *stream);
+
+/* ---- measurement probes (bench.py; no reference counterpart: SURVEY.md 8(d) asks
+ *      for the box's device-copy bandwidth beside the roofline).  Memory-only, no
+ *      arithmetic; ev_start / ev_stop (hipEvent_t or NULL) receive the launch's own
+ *      begin / end timestamps.
+ *  hic_probe_copy: dst[0, bytes) = src[0, bytes) (16-byte aligned, bytes % 16 == 0),
+ *    16 B per lane loads, nontemporal stores: the streaming copy rate.
+ *  hic_probe_plane: the forward plane pass's byte pattern without the DCT: a uint8
+ *    H x W plane (pitch W, multiples of 8) read as 8x8 blocks (one per lane), 128 B
+ *    per block written to out (nblk x 64 int16) through the LDS stage and 1 KiB
+ *    nontemporal stores of k_dct_pk, persistent grid: the pass's memory floor.
+ *  waves_per_cu: persistent grid size (0 = default: 16 for the copy, 12 for the plane). */
+int hic_probe_copy(const void *src, void *dst, int64_t bytes, int waves_per_cu, void *stream, void *ev_start,
+                   void *ev_stop);
+int hic_probe_plane(const uint8_t *plane, int64_t H, int64_t W, int16_t *out, int waves_per_cu, void *stream,
+                    void *ev_start, void *ev_stop);
 
 /* ---- forward transform: replaces transform.dct_channel (transform.py:182-193) =
  *      offset -128 (:186), split_matrix/pad (:33-42), dct2 (:67-84, scipy pocketfft

@@ -338,6 +338,7 @@ def _structured_rgb(kind, H, W, seed):
 
 
 @pytest.mark.parametrize("variant", [{}, {"encode_dct": 1}, {"encode_waves": 3}, {"encode_dct": 1, "encode_waves": 3},
+                                     {"encode_dct": 2}, {"encode_dct": 2, "encode_waves": 3}, {"encode_dct": 2, "encode_waves": 2},
                                      {"encode_nt": 1}, {"encode_xcd": 0}, {"encode_xcd": 1}])
 @pytest.mark.parametrize("kind", ["random", "levels", "colour_levels", "blocks", "flat"])
 @pytest.mark.parametrize("H,W", [(16, 512), (144, 2048), (1088, 1536)])
@@ -564,3 +565,22 @@ def test_encoder_hic_image_equals_jpeg_encode():
     for i, (a, b) in enumerate(zip(hic.payloads, ref.payloads)):
         assert a == b, i
     assert hic.byte_stream() == ref.byte_stream()
+
+
+def test_encoder_hic_image_on_side_stream():
+    """The whole encode + hic_image on a non-current stream: the histograms, key
+    ranges, code tables and packed bits are read after that stream's kernels, and
+    the temporaries live on it.  A large image gives the reads a chance
+    to overtake an unsynchronised stream.  == the same on the current stream."""
+    H, W = 2160, 3840
+    rng = np.random.default_rng(31)
+    rgb = device.to_device(rng.integers(0, 256, (H, W, 3), dtype=np.uint8))
+    ref_enc = pipeline.Encoder(H, W)
+    ref_enc.encode(rgb)
+    ref = ref_enc.hic_image()
+    side = torch.cuda.Stream()
+    enc = pipeline.Encoder(H, W)
+    torch.cuda.synchronize()  # the encoder's zero-filled workspaces were written on the current stream
+    enc.encode(rgb, stream=side)
+    got = enc.hic_image(stream=side)
+    assert got.byte_stream() == ref.byte_stream()

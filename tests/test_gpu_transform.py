@@ -98,11 +98,11 @@ def test_layouts_roundtrip(layout, shape):
         np.testing.assert_array_equal(device.to_host(rec), orcc.inv_dct_channel(exp, tab))
 
 
-@pytest.mark.parametrize("path", [-1, _lib.DCT_PATH_F64, _lib.DCT_PATH_F32])
+@pytest.mark.parametrize("path", [-1, _lib.DCT_PATH_PK, _lib.DCT_PATH_F32])
 @pytest.mark.parametrize("H,W", [(4096, 4096), (4320, 7680)])
 def test_full_size_bit_exact(H, W, path):
     """BASELINE configs 2/3 plane sizes, bit-exact against the C oracle (multi-threaded),
-    on the default forward path and on the float32 one."""
+    on the default (float64) forward path, the packed float32 one and the scalar float32 one."""
     with _lib.knobs(dct_path=path):
         _full_size_bit_exact(H, W)
 
@@ -235,7 +235,7 @@ def test_plane_dct_rle_records(kind, path, H, W):
 @pytest.mark.parametrize("kind", ["random", "levels4"])
 def test_plane_batch_three_planes(kind, waves_per_cu):
     """hic_dct_quant_rle_u8_batch over BASELINE configs[2]'s three planes (8K Y +
-    two 4K chroma) in one launch, the production packed path: with few persistent
+    two 4K chroma) in one launch on the packed path (DCT_PATH_PK): with few persistent
     waves each wave's deferred tie queue mixes sets of different planes (and
     tables).  Coefficients, DC differences and symbols vs the C oracle."""
     shapes = [(4320, 7680, 0), (2160, 3840, 1), (2160, 3840, 1)]
@@ -249,7 +249,7 @@ def test_plane_batch_three_planes(kind, waves_per_cu):
         outs.append(device.empty((nblk, 64), torch.int16))
         wss.append(device.workspace(lib.hic_rle_workspace_bytes(nblk, 64)))
         jobs[i] = _lib.DctPlaneJob(planes[i][1].data_ptr(), h, w, w, t, outs[i].data_ptr(), wss[i].data_ptr())
-    with _lib.knobs(dct_waves_per_cu=waves_per_cu):
+    with _lib.knobs(dct_waves_per_cu=waves_per_cu, dct_path=_lib.DCT_PATH_PK):
         _lib.call("hic_dct_quant_rle_u8_batch", 3, jobs, 15, device.stream_ptr(), None, None)
     for i, (h, w, t) in enumerate(shapes):
         nblk = (h // 8) * (w // 8)
@@ -268,3 +268,25 @@ def test_plane_batch_three_planes(kind, waves_per_cu):
         np.testing.assert_array_equal(device.to_host(L[:c]).astype(np.int32), eL, err_msg=(kind, i))
         np.testing.assert_array_equal(device.to_host(V[:c]).astype(np.int32), eV, err_msg=(kind, i))
         np.testing.assert_array_equal(device.to_host(dc), orcc.dpcm(exp[:, 0].copy()), err_msg=(kind, i))
+
+
+def test_measurement_probes():
+    """bench.py's in-run floors: hic_probe_copy copies; hic_probe_plane writes each 8x8
+    block's 64 pixel bytes then the same rows with their halves swapped (128 B per
+    block, block order) -- it moves the plane pass's bytes, including a partial set."""
+    lib_src = np.random.default_rng(5).integers(0, 256, 1 << 16, dtype=np.uint8)
+    a, b = device.to_device(lib_src), device.empty((1 << 16,), torch.uint8)
+    _lib.call("hic_probe_copy", device.ptr(a), device.ptr(b), 1 << 16, 0, device.stream_ptr(), None, None)
+    np.testing.assert_array_equal(device.to_host(b), lib_src)
+    H, W = 8 * 9, 8 * 15  # 135 blocks: two full sets and a partial one
+    plane = np.random.default_rng(6).integers(0, 256, (H, W), dtype=np.uint8)
+    out = device.empty((135, 64), torch.int16)
+    _lib.call("hic_probe_plane", device.ptr(device.to_device(plane)), H, W, device.ptr(out), 0, device.stream_ptr(),
+              None, None)
+    got = device.to_host(out).view(np.uint8).reshape(135, 128)
+    blocks = plane.reshape(9, 8, 15, 8).swapaxes(1, 2).reshape(135, 8, 8)
+    np.testing.assert_array_equal(got[:, :64], blocks.reshape(135, 64))
+    swapped = blocks.reshape(135, 8, 2, 4)[:, :, ::-1, :].reshape(135, 64)
+    np.testing.assert_array_equal(got[:, 64:], swapped)
+    with pytest.raises(ValueError):
+        _lib.call("hic_probe_copy", device.ptr(a), device.ptr(b), 17, 0, device.stream_ptr(), None, None)

@@ -175,8 +175,9 @@ def EP():
     return out
 
 
-# ---- float64 fallback (dct_core.h dct_coef_f64): r_m = sum_n C_v(n) x_mn (fma chain),
-# y = sum_m C_u(m) r_m (fma chain), C_k(n) = 2 cos(pi k (2n+1) / 16)
+# ---- float64 fallback (dct_core.h dct_coef_f64), folded by symmetry:
+# r_m = sum_{n<4} C_v(n) a_mn (a multiply, then an fma chain), a_mn = x_mn +- x_m,7-n
+# (an exact integer); y = sum_{m<4} C_u(m) b_m, b_m = r_m +- r_7-m (rounded add)
 def E2():
     c = Ctx(2.0 ** -53, 2.0 ** 53, False, 2.0 ** -53)
     px = pixels(c)
@@ -186,13 +187,15 @@ def E2():
         for v in range(8):
             r = []
             for m in range(8):
-                acc = px[m][0].mul(C(v, 0))
-                for n in range(1, 8):
-                    acc = px[m][n].fma(C(v, n), acc)
+                a = [px[m][n] + px[m][7 - n] if v % 2 == 0 else px[m][n] - px[m][7 - n] for n in range(4)]
+                acc = a[0].mul(C(v, 0))
+                for n in range(1, 4):
+                    acc = a[n].fma(C(v, n), acc)
                 r.append(acc)
-            acc = r[0].mul(C(u, 0))
-            for m in range(1, 8):
-                acc = r[m].fma(C(u, m), acc)
+            b = [r[m] + r[7 - m] if u % 2 == 0 else r[m] - r[7 - m] for m in range(4)]
+            acc = b[0].mul(C(u, 0))
+            for m in range(1, 4):
+                acc = b[m].fma(C(u, m), acc)
             out[u, v] = acc.E
     return out
 

@@ -173,18 +173,17 @@ def extra_4k_luma(steps=20):
             "algorithmic_bytes": n * n * 3, "timed_launches": steps}
 
 
-def extra_4k_rgb_encode(steps=40, n_streams=2):
-    """north_star's 4K point on one GPU: 4096 x 4096 random RGB through the same
-    full encode as the headline (fused colour + DCT/quantize/zig-zag, DC DPCM + AC
-    RLE), consecutive images alternating over `n_streams` streams, >= 1.2 GB of
-    rotating inputs, wall time of `steps` images between two synchronisations."""
+def extra_rgb_encode(H=4096, W=4096, steps=40, n_streams=2, fused=None):
+    """A full RGB encode on one GPU (fused colour + DCT/quantize/zig-zag, DC DPCM +
+    AC RLE; fused=False: the two-kernel chain), consecutive images alternating over
+    `n_streams` streams, >= 1.2 GB of rotating inputs, wall time of `steps` images
+    between two synchronisations."""
     from hiccup_amd import pipeline
-    n = 4096
-    nin = int(np.ceil(ROT_BYTES / (n * n * 3)))
+    nin = int(np.ceil(ROT_BYTES / (H * W * 3)))
     g = torch.Generator(device="cuda")
     g.manual_seed(6)
-    xs = [torch.randint(0, 256, (n, n, 3), dtype=torch.uint8, device="cuda", generator=g) for _ in range(nin)]
-    encs = [pipeline.Encoder(n, n) for _ in range(4)]
+    xs = [torch.randint(0, 256, (H, W, 3), dtype=torch.uint8, device="cuda", generator=g) for _ in range(nin)]
+    encs = [pipeline.Encoder(H, W, fused=fused) for _ in range(4)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(n_streams - 1)]
     torch.cuda.synchronize()
 
@@ -202,13 +201,29 @@ def extra_4k_rgb_encode(steps=40, n_streams=2):
     for e in encs:
         for ci, c in enumerate(e.counts.cpu().tolist()):
             pipeline.check_count(int(c), pipeline.CHANNELS[ci])
-    fused = encs[0].fused
+    used = encs[0].fused
     del xs, encs
     torch.cuda.empty_cache()
-    return {"workload": "4096x4096 RGB -> YCrCb 4:2:0 full encode (the headline's chain at north_star's 4K point), "
-                        "1 GPU, %d streams" % n_streams,
-            "fused": fused, "ms_per_image": round(dt * 1e3, 4), "mpix_s": round(n * n / dt / 1e6, 1),
-            "timed_images": steps}
+    return {"fused": used, "ms_per_image": round(dt * 1e3, 4), "mpix_s": round(H * W / dt / 1e6, 1),
+            "timed_images": steps, "streams": n_streams}
+
+
+def extra_4k_rgb_encode(steps=40, n_streams=2):
+    """north_star's 4K point on one GPU: 4096 x 4096 random RGB, the headline's chain."""
+    out = {"workload": "4096x4096 RGB -> YCrCb 4:2:0 full encode (the headline's chain at north_star's 4K point), "
+                       "1 GPU, %d streams" % n_streams}
+    out.update(extra_rgb_encode(4096, 4096, steps, n_streams))
+    return out
+
+
+def extra_uhd_rgb_encode(steps=40, n_streams=2):
+    """3840 x 2160 (UHD: W % 512 != 0, the fused kernel's ragged last strip) full
+    encode, fused against the two-kernel chain on the same inputs."""
+    out = {"workload": "3840x2160 RGB -> YCrCb 4:2:0 full encode, 1 GPU, %d streams (fused: ragged last strip, "
+                       "tile records by a tile pass; chain: colour kernel + plane DCT)" % n_streams}
+    out["fused"] = extra_rgb_encode(2160, 3840, steps, n_streams)
+    out["two_kernel_chain"] = extra_rgb_encode(2160, 3840, steps, n_streams, fused=False)
+    return out
 
 
 def extra_8k_plane_dct(steps=24, luma_only=False, floor_us=None):
@@ -362,6 +377,43 @@ def extra_16k_roundtrip(steps=4):
     return {"workload": "16384x16384 RGB encode + decode round trip, 1 GPU (BASELINE configs[4] at N=1)",
             "ms_per_roundtrip": round(dt * 1e3, 3), "mpix_s": round(n * n / dt / 1e6, 1),
             "psnr_db_vs_input": round(10 * np.log10(255.0 ** 2 / mse), 3), "timed_roundtrips": steps}
+
+
+def extra_8k_jpeg_decode(steps=3):
+    """codec.jpeg_decode of a real 8K .hic, end to end from its bytes: container
+    parse, the nine trees from the tables (host), the nine Huffman streams decoded
+    on the GPU (hic_huffman_decode), RLE decode + DC integration + izigzag on the
+    GPU, the float64 planes copied back (the reference's CompressedImage).  The
+    .hic comes from the GPU encoder on a random 8K RGB image."""
+    from hiccup_amd import codec, device, hicimage, pipeline
+    g = torch.Generator(device="cuda")
+    g.manual_seed(9)
+    x = torch.randint(0, 256, (H8K, W8K, 3), dtype=torch.uint8, device="cuda", generator=g)
+    enc = pipeline.Encoder(H8K, W8K)
+    enc.encode(x)
+    raw = enc.hic_image().byte_stream
+    symbols = int(sum(enc.counts.cpu().tolist()) * 2 + sum(enc.dc[k].numel() for k in pipeline.CHANNELS))
+    want = device.to_host(enc.coef["lum"][:, 0])
+    del x
+    t_parse, t_dec = [], []
+    for _ in range(steps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        img = hicimage.HicImage.from_bytes(raw)
+        t1 = time.perf_counter()
+        out = codec.jpeg_decode(img)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        t_parse.append(t1 - t0)
+        t_dec.append(t2 - t1)
+    lum = out.as_dict["lum"]
+    # the decoded DC coefficients equal the encoder's (full parity: tests/test_gpu_codec.py)
+    ok = bool(np.array_equal(lum[::8, ::8].reshape(-1), want.astype(np.float64)))
+    ms = lambda v: round(float(np.median(v[1:])) * 1e3, 1)  # noqa: E731
+    return {"workload": "codec.jpeg_decode of an 8K (7680x4320) .hic from bytes (GPU Huffman + RLE decode)",
+            "hic_bytes": len(raw), "symbols": symbols, "ms_parse": ms(t_parse), "ms_jpeg_decode": ms(t_dec),
+            "msym_s": round(symbols / float(np.median(t_dec[1:])) / 1e6, 1), "dc_matches_encoder": ok,
+            "timed_decodes": steps}
 
 
 def extra_16k_roundtrip_sharded(rank, world, backend, steps=4):
@@ -806,9 +858,11 @@ def main():
             out["roofline"]["frac_of_device_copy"] = round(achieved / floors["device_copy_gbs"], 4)
         if not args.no_extras and world == 1:
             out["extra_configs"] = {"4k_rgb_encode": extra_4k_rgb_encode(),
+                                    "3840x2160_rgb_encode": extra_uhd_rgb_encode(),
                                     "4k_luma_dct": extra_4k_luma(), "8k_plane_dct": extra_8k_plane_dct(),
                                     "8k_luma_dct": extra_8k_plane_dct(
                                         luma_only=True, floor_us=floors["luma_pattern"]["1x"]["median_launch_us"]),
+                                    "8k_jpeg_decode": extra_8k_jpeg_decode(),
                                     "16k_roundtrip": extra_16k_roundtrip()}
         if extra_sharded is not None:
             out["extra_configs"] = {"16k_roundtrip": extra_sharded}

@@ -214,46 +214,77 @@ def jpeg_encode(compressed):
 
 
 def jpeg_decode(hic_image):
-    """codec.py:337-426: HicImage -> CompressedImage (float64 planes)."""
+    """codec.py:337-426: HicImage -> CompressedImage (float64 planes).  The nine
+    coded streams are decoded on the GPU (hic_huffman_decode, in the reference's
+    order: DC, AC values, AC lengths, codec.py:372-388) and stay there for the RLE
+    decode, DC integration and izigzag (hic_rle_decode_i32, hic_izigzag_blocks_i32);
+    only the nine trees (from the tables) are built on the host."""
     utils.debug_msg("JPEG decode")
     assert hic_image.hic_type == model.Compression.JPEG
     p = hic_image.payloads
     chans = ("lum", "cr", "cb")
+    trees = [huffman_decode(p[i]) for i in range(9)]
+    streams = [_huffman_stream_device(p[9 + i], trees[i]) for i in range(9)]
     shapes = {"lum": p[18].numbers, "cr": p[19].numbers, "cb": p[19].numbers}
     bs = settings.JPEG_BLOCK_SIZE
     sub_length = bs * bs - 1
     out = {}
     for c, k in enumerate(chans):
-        dc = huffman_data_decode(p[9 + c], huffman_decode(p[c]))
-        vals = huffman_data_decode(p[12 + c], huffman_decode(p[3 + c]))
-        lens = huffman_data_decode(p[15 + c], huffman_decode(p[6 + c]))
-        n = min(len(vals), len(lens))  # zip() in codec.py:399-400
-        vals, lens = vals[:n], lens[:n]
-        # the reference's assertions (utils.group_tuples, codec.py:418), evaluated up front
-        total = int(np.sum(np.asarray(lens, dtype=np.int64) + 1))
-        eob = n > 0 and lens[-1] == 0 and vals[-1] == 0
-        ac_length = utils.size(shapes[k]) - len(dc)
-        decoded = max(total, ac_length) if eob else total
+        dc, vals, lens = streams[c], streams[3 + c], streams[6 + c]
+        n = min(vals[1], lens[1])  # zip() in codec.py:399-400
         if n == 0:
             raise TypeError("reduce() of empty iterable with no initial value")
         if sub_length == 0:
             raise ZeroDivisionError("integer division or modulo by zero")
-        assert decoded % sub_length == 0
-        assert decoded // sub_length == len(dc)
-        out[k] = _decode_channel(dc, lens, vals, shapes[k], bs)
+        out[k] = _decode_channel(dc, lens, vals, n, shapes[k], bs)
     return model.CompressedImage.from_dict(out)
 
 
-def _decode_channel(dc, lens, vals, shape, bs):
-    nblk, L = len(dc), bs * bs
+def _huffman_stream_device(payload, tree):
+    """huffman_data_decode on the GPU: (int32 device tensor, count).  Streams whose
+    tree holds a leaf that is not an int32 (a table with unused codes decodes them
+    to None) go through the values on the host, where the reference's arithmetic on
+    them fails the same way."""
+    packed, nbits = payload.packed_bits()
+    if tree.root.is_leaf:  # no edges: the reference's walk fails on the first bit
+        tree.decode_data("1" if nbits else "")
+        return device.to_device(np.zeros(1, np.int32)), 0
+    buf = np.zeros(-(-max(int(nbits), 1) // 32) * 4, np.uint8)
+    body = np.asarray(packed, dtype=np.uint8)[:-(-int(nbits) // 8)]
+    buf[:body.size] = body
+    d, n, ints = tree.decode_device(device.to_device(buf), nbits)
+    if not ints:
+        leaves = tree.flat()[1]
+        vals = _i32([leaves[i].value for i in device.to_host(d[:n]).tolist()], "decoded values")
+        return device.to_device(vals if n else np.zeros(1, np.int32)), n
+    return d, n
+
+
+def _decode_channel(dc, lens, vals, n, shape, bs):
+    """The RLE decode + DC integration + izigzag of one channel from its decoded
+    streams (device int32 tensors with counts), with codec.py:418's assertions."""
+    (Dd, nblk), (Ld, _), (Vd, _) = dc, lens, vals
+    L, sub = bs * bs, bs * bs - 1
     H, W = int(shape[0]), int(shape[1])
+    if nblk == 0:  # decoded // sub_length == 0 needs decoded == 0; n > 0 symbols cover >= 1
+        raise AssertionError()
+    if H * W != nblk * L:
+        # ac_length (codec.py:403) differs from nblk * sub: evaluate the assertion
+        # on the symbols themselves (a malformed file; never the encoder's output)
+        lh, vh = device.to_host(Ld[:n]).astype(np.int64), device.to_host(Vd[:n])
+        total = int(np.sum(lh + 1))
+        decoded = max(total, H * W - nblk) if (lh[-1] == 0 and vh[-1] == 0) else total
+        assert decoded % sub == 0
+        assert decoded // sub == nblk
     blocks = device.empty((nblk, L), torch.int32)
     status = device.empty((1,), torch.int64)
-    Ld, Vd, Dd = device.to_device(_i32(lens, "lengths")), device.to_device(_i32(vals, "values")), \
-        device.to_device(_i32(dc, "dc"))
-    ws = device.workspace(_lib.load().hic_rld_workspace_bytes(len(lens), nblk))
-    _lib.call("hic_rle_decode_i32", device.ptr(Ld), device.ptr(Vd), len(lens), device.ptr(Dd), nblk, L,
+    ws = device.workspace(_lib.load().hic_rld_workspace_bytes(n, nblk))
+    _lib.call("hic_rle_decode_i32", device.ptr(Ld), device.ptr(Vd), n, device.ptr(Dd), nblk, L,
               device.ptr(blocks), device.ptr(status), device.ptr(ws), device.stream_ptr())
+    if H * W == nblk * L:
+        # status = max(total, nblk * sub) after an EOB, else total (k_rld_status):
+        # codec.py:418's two assertions hold exactly when it is nblk * sub
+        assert int(status.cpu()[0]) == nblk * sub
     raster = device.zeros((H, W), torch.int32)
     _lib.call("hic_izigzag_blocks_i32", device.ptr(blocks), H, W, bs, device.ptr(raster), device.stream_ptr())
     return device.to_host(raster).astype(np.float64)

@@ -13,8 +13,12 @@
 //
 // Work unit: a "strip" of 512 pixel columns x 16 image rows.  Lane l owns pixel
 // columns [8 l, 8 l + 8) of the strip, i.e. Y block column l of the strip's two
-// block rows (a 64-block RLE tile each, W % 512 == 0) and half of chroma block
-// column l / 2.  One wave per unit:
+// block rows (a 64-block RLE tile each when W % 512 == 0) and half of chroma block
+// column l / 2.  Any W % 16 == 0: the last strip is ragged (W mod 512 columns;
+// its lanes past W compute on whatever the loads return and store nothing, the
+// right-border pixel goes to its last lane); its block rows then straddle RLE
+// tiles, so the tile records come from a tile pass after the launch.  One wave
+// per unit:
 //   1. colour: 19 RGB rows (the 16 rows + the 2 + 1 rows of pyrDown's vertical
 //      taps), 24 B per lane per row (1.5 KiB contiguous per wave-row, buffer loads
 //      at a scalar row offset); YCC by v_dot4 (ycc8); Y of rows 0..15 stays in
@@ -49,6 +53,7 @@ struct Enc420 {
   int64_t *rec[3];   // tile records: Y per 64-block tile, Cr / Cb per 32-block half tile
   int M;
   int nstrips, nunits;  // nunits: waves (HIC_ENC_VG unit rows each)
+  int wlast;            // pixel columns of the last strip (16 .. 512)
   int xcd;              // 1: workgroups remapped to a contiguous band of units per XCD
 };
 
@@ -235,15 +240,20 @@ __device__ __forceinline__ uint4 enc_st16(const uint2 *st2, int b, int k) {
 }
 
 // stage rows 0..31 -> o_lo (32 blocks), rows 32..63 -> o_hi: 1 KiB per store
-// instruction, nontemporal (the coefficients are not re-read by this kernel)
+// instruction, nontemporal (the coefficients are not re-read by this kernel).
+// n_lo / n_hi (wave-uniform): blocks of o_lo / o_hi that exist (32 but in a
+// ragged strip)
 template <bool NT>
-__device__ __forceinline__ void enc_store(const uint2 *st2, int lane, int16_t *o_lo, int16_t *o_hi) {
+__device__ __forceinline__ void enc_store(const uint2 *st2, int lane, int16_t *o_lo, int16_t *o_hi, int n_lo = 32,
+                                          int n_hi = 32) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const bool full = (n_lo & n_hi) == 32;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const uint4 t = enc_st16(st2, 8 * k + (lane >> 3), lane & 7);
     const u32x4 v = {t.x, t.y, t.z, t.w};
     u32x4 *o = reinterpret_cast<u32x4 *>(k < 4 ? o_lo : o_hi) + 64 * (k & 3) + lane;
+    if (!full && 8 * (k & 3) + (lane >> 3) >= (k < 4 ? n_lo : n_hi)) continue;
     if (NT)
       __builtin_nontemporal_store(v, o);
     else
@@ -342,6 +352,11 @@ __device__ __forceinline__ uint32_t set_lane(uint32_t v, int s) {
   asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(s), "n"(L));
   return v;
 }
+// the same with a wave-uniform lane index (writelane cannot take the value and the
+// lane from two SGPRs: one constant-bus read per instruction)
+__device__ __forceinline__ uint32_t set_lane_s(uint32_t v, int s, int lane, int l) {
+  return lane == l ? (uint32_t)s : v;
+}
 // wave shifts for the horizontal taps (the edge lane is overwritten by v_writelane)
 __device__ __forceinline__ uint32_t wshr1(uint32_t v) {  // lane i <- lane i - 1
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xF, 0xF, true);
@@ -371,7 +386,7 @@ struct EncColour {
   static constexpr int kLA = HIC_ENC_LA;
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-  int lane, roff, voff;
+  int lane, roff, voff, rlane;  // rlane: the strip's last lane (63 but in a ragged strip)
   uint32_t hal_l2, hal_l1, hal_r;
   __amdgpu_buffer_rsrc_t rsrc;
   YccK K;
@@ -389,8 +404,9 @@ struct EncColour {
     ring_b[r % (kLA + 1)] = __builtin_amdgcn_raw_buffer_load_b64(rsrc, voff + 16, so, HIC_ENC_LOAD_AUX);
   }
 
-  __device__ __forceinline__ void init(const Enc420 &E, int y0, int s, int lane_) {
+  __device__ __forceinline__ void init(const Enc420 &E, int y0, int s, int lane_, int nb) {
     lane = lane_;
+    rlane = __builtin_amdgcn_readfirstlane(nb - 1);
     const int W = E.W, H = E.H, pitch = 3 * W;
     const int in_row1 = E.in_row0 + E.in_rows;
     const int xs = 512 * s;
@@ -406,7 +422,8 @@ struct EncColour {
       roff = (sy - E.in_row0) * pitch;
     }
     // edge pixels, packed (cr | cb << 16): lane r converts input row r's x = xs - 2,
-    // xs - 1 (or 2, 1 at the left border) and x = xs + 512 (or W - 2 at the right)
+    // xs - 1 (or 2, 1 at the left border) and x = xs + 512 (or W - 2 at the right,
+    // also for a ragged last strip)
     hal_l2 = hal_l1 = hal_r = 0;
     if (lane < NR) {
       const uint8_t *row = E.rgb + roff;
@@ -449,7 +466,7 @@ struct EncColour {
       // neighbour pixels x0 - 2, x0 - 1 (left lane) and x0 + 8 (right lane)
       const uint32_t l2 = set_lane<0>(wshr1(c[6]), __builtin_amdgcn_readlane((int)hal_l2, r));
       const uint32_t l1 = set_lane<0>(wshr1(c[7]), __builtin_amdgcn_readlane((int)hal_l1, r));
-      const uint32_t r0 = set_lane<63>(wshl1(c[0]), __builtin_amdgcn_readlane((int)hal_r, r));
+      const uint32_t r0 = set_lane_s(wshl1(c[0]), __builtin_amdgcn_readlane((int)hal_r, r), lane, rlane);
       h[r][0] = pk_taps5(l2, l1, c[0], c[1], c[2], k4, k6);
       h[r][1] = pk_taps5(c[0], c[1], c[2], c[3], c[4], k4, k6);
       h[r][2] = pk_taps5(c[2], c[3], c[4], c[5], c[6], k4, k6);
@@ -532,6 +549,8 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
   const int p = __builtin_amdgcn_readfirstlane(g / E.nstrips), s = __builtin_amdgcn_readfirstlane(g - p * E.nstrips);
   const int u0 = HIC_ENC_VG * p;
   const int y0 = E.out_row0 + 16 * u0;
+  // Y blocks of this strip's block rows (64 but in a ragged last strip)
+  const int nb = __builtin_amdgcn_readfirstlane(s == E.nstrips - 1 ? E.wlast >> 3 : 64);
   const bool has2 = HIC_ENC_VG == 2 && 16 * (u0 + 1) < E.out_rows;
   const int nbx = E.W >> 3, nbxc = E.W >> 4;
 
@@ -546,7 +565,7 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
     __builtin_amdgcn_wave_barrier();
     const int64_t b0 = (int64_t)(2 * u + br) * nbx + 64 * s;
     int16_t *o = E.coef[0] + b0 * 64;
-    enc_store<NT>(st2, lane, o, o + 32 * 64);
+    enc_store<NT>(st2, lane, o, o + 32 * 64, nb < 32 ? nb : 32, nb > 32 ? nb - 32 : 0);
     if (TMF >= 0 && E.rec[0]) {
       uint32_t zw[32];
       enc_stage_row(st2, lane, zw);
@@ -566,7 +585,7 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
     enc_dct_any<1, DM>(w, st, st2, s_qlist, s_cm, s_qt);
     __builtin_amdgcn_wave_barrier();
     const int64_t b0 = (int64_t)u * nbxc + 32 * s;
-    enc_store<NT>(st2, lane, E.coef[1] + b0 * 64, E.coef[2] + b0 * 64);
+    enc_store<NT>(st2, lane, E.coef[1] + b0 * 64, E.coef[2] + b0 * 64, nb >> 1, nb >> 1);
     if (TMF >= 0 && E.rec[1]) {
       uint32_t zw[32];
       enc_stage_row(st2, lane, zw);
@@ -608,7 +627,7 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
   using PD = std::integral_constant<short, HIC_ENC_PRIO_D>;
   EncColour<HIC_ENC_VG == 2 ? 35 : 19> C;
   prio(PC{});
-  C.init(E, y0, s, lane);
+  C.init(E, y0, s, lane, nb);
   C.template rows<0, 10>(yq, s_chroma);  // input rows 2 .. 9 = unit u0's Y block row 0
   __builtin_amdgcn_sched_barrier(0);
   prio(PD{});
@@ -643,8 +662,8 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
                                 int16_t *coef_cb, void *ws_y, void *ws_cr, void *ws_cb, int max_len, void *stream,
                                 void *ev_start, void *ev_stop) {
   if (!rgb_rows || !coef_y || !coef_cr || !coef_cb) return arg_error("null pointer");
-  if (H < 16 || W < 512 || H >= (1 << 20) || W >= (1 << 20)) return arg_error("image shape");
-  if (W % 512 || H % 16) return arg_error("hic_encode420_u8 needs W %% 512 == 0 and H %% 16 == 0");
+  if (H < 16 || W < 16 || H >= (1 << 20) || W >= (1 << 20)) return arg_error("image shape");
+  if (W % 16 || H % 16) return arg_error("hic_encode420_u8 needs W %% 16 == 0 and H %% 16 == 0");
   if (out_row0 < 0 || out_rows < 16 || out_row0 % 16 || out_rows % 16 || out_row0 + out_rows > H)
     return arg_error("output row range (multiples of 16)");
   const int64_t need0 = out_row0 >= 2 ? out_row0 - 2 : 0;
@@ -670,11 +689,14 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
   E.coef[0] = coef_y;
   E.coef[1] = coef_cr;
   E.coef[2] = coef_cb;
-  E.rec[0] = static_cast<int64_t *>(ws_y);
-  E.rec[1] = static_cast<int64_t *>(ws_cr);
-  E.rec[2] = static_cast<int64_t *>(ws_cb);
+  // ragged last strip: the records come from a tile pass after the launch
+  const bool aligned = W % 512 == 0;
+  E.rec[0] = aligned ? static_cast<int64_t *>(ws_y) : nullptr;
+  E.rec[1] = aligned ? static_cast<int64_t *>(ws_cr) : nullptr;
+  E.rec[2] = aligned ? static_cast<int64_t *>(ws_cb) : nullptr;
   E.M = max_len;
-  E.nstrips = (int)(W / 512);
+  E.nstrips = (int)((W + 511) / 512);
+  E.wlast = (int)(W - 512 * (int64_t)(E.nstrips - 1));
   E.nunits = E.nstrips * (int)((out_rows / 16 + HIC_ENC_VG - 1) / HIC_ENC_VG);  // waves
   E.xcd = knob(HIC_KNOB_ENCODE_XCD) == 1;
   // one wave per unit (no persistent loop: units are the same size, and the
@@ -709,5 +731,12 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
     HIC_ENC_VARIANTS(0);
   }
 #undef HIC_ENC_VARIANTS
-  return check_launch("k_encode420");
+  if (int e = check_launch("k_encode420")) return e;
+  if (recs && !aligned) {  // one record per 64-block tile, all three planes
+    const int64_t ny = (out_rows / 8) * (W / 8), nc = (out_rows / 16) * (W / 16);
+    if (int e = rle_tile16_launch(coef_y, ny, max_len, static_cast<int64_t *>(ws_y), s)) return e;
+    if (int e = rle_tile16_launch(coef_cr, nc, max_len, static_cast<int64_t *>(ws_cr), s)) return e;
+    if (int e = rle_tile16_launch(coef_cb, nc, max_len, static_cast<int64_t *>(ws_cb), s)) return e;
+  }
+  return HIC_OK;
 }

@@ -1,0 +1,406 @@
+// huffdec.hip -- Huffman decode of a packed bit stream on the GPU: the inverse of
+// hic_huffman_pack, i.e. HuffmanTree.decode_data (hiccup/huffman.py:149-178) over
+// the bit strings codec.jpeg_decode reads from the .hic payloads (codec.py:372-388).
+//
+// The reference walks the tree one bit at a time ('1' = left, '0' = right), emits
+// a leaf's value and restarts at the root; trailing bits that do not finish a code
+// are dropped, and a step into a missing child (a one-leaf encoding tree's empty
+// right side) raises.  The stream has no markers, so it is cut into fixed
+// subsequences of kSub bits, one per thread, decoded speculatively from their
+// nominal first bit; Huffman codes resynchronise within a few codewords, so after
+// the exit bit of subsequence i is handed to i+1 and only changed subsequences
+// re-decode (a handful of rounds), every subsequence starts on a codeword boundary.
+// A prefix sum over the per-subsequence symbol counts then places each one's
+// output and a second decode writes the symbols.
+//
+//   tree:  child[2n] / child[2n+1] = node n's '1' / '0' child: >= 0 an internal
+//          node, -1 missing, <= -2 leaf (-2 - leaf index); node 0 is the root
+//   LUT:   the first kLutBits bits from the root: 4096 entries held in LDS,
+//          [3:0] bits consumed - 1, [5:4] kind (0 leaf reached, 1 still internal
+//          after kLutBits bits, 2 missing child), [31:8] leaf / node index
+//   codes longer than kLutBits finish with a bit walk over child[] (global)
+#include <vector>
+
+#include "hic_common.h"
+
+namespace hic {
+namespace {
+
+constexpr int kLutBits = 12, kLut = 1 << kLutBits;
+constexpr int kSub = 1024;      // bits per subsequence (one thread each)
+constexpr int kDT = 256;        // threads per workgroup
+constexpr int kMaxRounds = 24;  // resynchronisation rounds before the serial chain
+constexpr int64_t kEnd = INT64_MAX;  // exit of a subsequence that reached the stream end
+
+enum : uint32_t { kLeaf = 0, kNode = 1, kMissing = 2 };
+
+// 64-bit MSB-aligned window over big-endian 32-bit words (the stream's bytes are
+// MSB-first); words past the buffer read as zero.
+struct BitReader {
+  const uint32_t *w;
+  int64_t nwords, wi;
+  uint64_t acc;
+  int nacc;
+  __device__ uint32_t load(int64_t i) const { return i < nwords ? __builtin_bswap32(w[i]) : 0u; }
+  __device__ void refill() {
+    if (nacc <= 32) {
+      acc |= (uint64_t)load(wi++) << (32 - nacc);
+      nacc += 32;
+    }
+  }
+  __device__ void init(const uint32_t *words, int64_t nw, int64_t p) {
+    w = words;
+    nwords = nw;
+    wi = p >> 5;
+    const int off = (int)(p & 31);
+    acc = (uint64_t)load(wi++) << (32 + off);
+    nacc = 32 - off;
+    refill();
+  }
+  __device__ uint32_t peek(int k) const { return (uint32_t)(acc >> (64 - k)); }
+  __device__ void skip(int k) {
+    acc <<= k;
+    nacc -= k;
+    refill();
+  }
+};
+
+// One symbol at bit p: 0 decoded (sym = leaf index), 1 stream end (no complete
+// code before nbits), 2 missing child (the reference's AttributeError).
+__device__ __forceinline__ int next_symbol(BitReader &br, int64_t &p, int64_t nbits, const uint32_t *lut,
+                                           const int32_t *__restrict__ child, int &sym) {
+  if (p >= nbits) return 1;
+  const uint32_t e = lut[br.peek(kLutBits)];
+  const int len = (int)(e & 15) + 1;
+  const uint32_t kind = (e >> 4) & 3;
+  if (kind == kLeaf) {
+    if (p + len > nbits) return 1;
+    br.skip(len);
+    p += len;
+    sym = (int)(e >> 8);
+    return 0;
+  }
+  if (kind == kMissing) return p + len > nbits ? 1 : 2;
+  if (p + kLutBits > nbits) return 1;
+  br.skip(kLutBits);
+  p += kLutBits;
+  int node = (int)(e >> 8);
+  for (;;) {
+    if (p >= nbits) return 1;
+    const int c = child[2 * node + 1 - (int)br.peek(1)];
+    if (c == -1) return 2;
+    br.skip(1);
+    ++p;
+    if (c < 0) {
+      sym = -2 - c;
+      return 0;
+    }
+    node = c;
+  }
+}
+
+struct DecGeo {
+  const uint32_t *words;
+  int64_t nwords, nbits, nsub;
+  const uint32_t *lut;  // global copy (the kernels stage it in LDS)
+  const int32_t *child;
+};
+
+// Symbols starting in [start, end): count and the first codeword start >= end
+// (kEnd at the stream end or after a missing child: nothing follows).
+__device__ void count_sub(const DecGeo &g, const uint32_t *lut, int64_t start, int64_t end, int64_t &exit,
+                          int32_t &count) {
+  count = 0;
+  exit = start;
+  if (start >= end) return;
+  BitReader br;
+  br.init(g.words, g.nwords, start);
+  int64_t p = start;
+  int sym;
+  while (p < end) {
+    if (next_symbol(br, p, g.nbits, lut, g.child, sym) != 0) {
+      exit = kEnd;
+      return;
+    }
+    ++count;
+  }
+  exit = p;
+}
+
+__device__ void stage_lut(const uint32_t *__restrict__ lut, uint32_t *s_lut) {
+  for (int i = threadIdx.x; i < kLut; i += kDT) s_lut[i] = lut[i];
+  __syncthreads();
+}
+
+// round 0: every subsequence from its nominal first bit
+__global__ __launch_bounds__(kDT) void k_hd_count(DecGeo g, int64_t *__restrict__ start, int64_t *__restrict__ exit,
+                                                  int32_t *__restrict__ cnt) {
+  __shared__ uint32_t s_lut[kLut];
+  stage_lut(g.lut, s_lut);
+  const int64_t i = (int64_t)blockIdx.x * kDT + threadIdx.x;
+  if (i >= g.nsub) return;
+  int64_t e;
+  int32_t c;
+  count_sub(g, s_lut, i * kSub, (i + 1) * kSub, e, c);
+  start[i] = i * kSub;
+  exit[i] = e;
+  cnt[i] = c;
+}
+
+// one resynchronisation round: subsequence i starts where i-1 exited last round
+__global__ __launch_bounds__(kDT) void k_hd_sync(DecGeo g, int64_t *__restrict__ start,
+                                                 const int64_t *__restrict__ exit_in, int64_t *__restrict__ exit_out,
+                                                 int32_t *__restrict__ cnt, int32_t *__restrict__ changed) {
+  __shared__ uint32_t s_lut[kLut];
+  stage_lut(g.lut, s_lut);
+  const int64_t i = (int64_t)blockIdx.x * kDT + threadIdx.x;
+  if (i >= g.nsub) return;
+  const int64_t s = i == 0 ? 0 : exit_in[i - 1];
+  if (s == start[i]) {
+    exit_out[i] = exit_in[i];
+    return;
+  }
+  int64_t e;
+  int32_t c;
+  count_sub(g, s_lut, s, (i + 1) * kSub, e, c);
+  start[i] = s;
+  exit_out[i] = e;
+  cnt[i] = c;
+  *changed = 1;
+}
+
+// the serial chain for streams that do not resynchronise (e.g. equal-length codes
+// whose length does not divide kSub): one thread walks the boundaries in order
+__global__ void k_hd_chain(DecGeo g, int64_t *__restrict__ start, int64_t *__restrict__ exit,
+                           int32_t *__restrict__ cnt) {
+  for (int64_t i = 1; i < g.nsub; ++i) {
+    const int64_t s = exit[i - 1];
+    if (s == start[i]) continue;
+    int64_t e;
+    int32_t c;
+    count_sub(g, g.lut, s, (i + 1) * kSub, e, c);
+    start[i] = s;
+    exit[i] = e;
+    cnt[i] = c;
+  }
+}
+
+__device__ __forceinline__ int64_t blk_excl(int64_t v, int64_t *s_w, int64_t &total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int64_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t o = __shfl_up(x, d, 64);
+    if (lane >= d) x += o;
+  }
+  if (lane == 63) s_w[wv] = x;
+  __syncthreads();
+  int64_t pre = 0;
+  total = 0;
+#pragma unroll
+  for (int k = 0; k < kDT / 64; ++k) {
+    pre += k < wv ? s_w[k] : 0;
+    total += s_w[k];
+  }
+  __syncthreads();
+  return pre + x - v;
+}
+
+__global__ __launch_bounds__(kDT) void k_hd_bsum(const int32_t *__restrict__ cnt, int64_t nsub,
+                                                 int64_t *__restrict__ bsum) {
+  __shared__ int64_t s_w[kDT / 64];
+  const int64_t i = (int64_t)blockIdx.x * kDT + threadIdx.x;
+  int64_t tot;
+  blk_excl(i < nsub ? cnt[i] : 0, s_w, tot);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+// in-place exclusive scan of n int64 by one workgroup; *total = the sum
+__global__ __launch_bounds__(kDT) void k_hd_scan(int64_t *__restrict__ v, int64_t n, int64_t *__restrict__ total) {
+  __shared__ int64_t s_w[kDT / 64];
+  int64_t run = 0;
+  for (int64_t c0 = 0; c0 < n; c0 += kDT) {
+    const int64_t i = c0 + threadIdx.x;
+    const int64_t x = i < n ? v[i] : 0;
+    int64_t tot;
+    const int64_t e = run + blk_excl(x, s_w, tot);
+    if (i < n) v[i] = e;
+    run += tot;
+  }
+  if (threadIdx.x == 0) *total = run;
+}
+
+// the output pass: symbols of subsequence i at its offset, as leaf values (or
+// leaf indices when values is null); err = the first bit of a symbol that walks
+// into a missing child (min over the stream)
+__global__ __launch_bounds__(kDT) void k_hd_emit(DecGeo g, const int64_t *__restrict__ start,
+                                                 const int32_t *__restrict__ cnt, const int64_t *__restrict__ boff,
+                                                 const int32_t *__restrict__ values, int32_t *__restrict__ out,
+                                                 int64_t out_cap, unsigned long long *__restrict__ err) {
+  __shared__ uint32_t s_lut[kLut];
+  __shared__ int64_t s_w[kDT / 64];
+  stage_lut(g.lut, s_lut);
+  const int64_t i = (int64_t)blockIdx.x * kDT + threadIdx.x;
+  int64_t tot;
+  const int64_t o = boff[blockIdx.x] + blk_excl(i < g.nsub ? cnt[i] : 0, s_w, tot);
+  if (i >= g.nsub) return;
+  const int64_t s = start[i], end = (i + 1) * kSub;
+  if (s >= end) return;
+  BitReader br;
+  br.init(g.words, g.nwords, s);
+  int64_t p = s, k = o;
+  int sym;
+  while (p < end) {
+    const int64_t at = p;
+    const int r = next_symbol(br, p, g.nbits, s_lut, g.child, sym);
+    if (r == 2) atomicMin(err, (unsigned long long)at);
+    if (r != 0) break;
+    if (k < out_cap) out[k] = values ? values[sym] : sym;
+    ++k;
+  }
+}
+
+struct DecWs {
+  uint32_t *lut;
+  int32_t *child, *values, *cnt, *changed;
+  int64_t *start, *exit_a, *exit_b, *bsum, *total;
+  unsigned long long *err;
+};
+
+DecWs carve(void *ws, int64_t nsub, int32_t nnodes, int32_t nleaves) {
+  char *p = static_cast<char *>(ws);
+  auto take = [&](size_t bytes) {
+    char *q = p;
+    p += round_up((int64_t)bytes, 256);
+    return q;
+  };
+  DecWs w;
+  const int64_t nblk = ceil_div(nsub, kDT);
+  w.lut = reinterpret_cast<uint32_t *>(take(kLut * 4));
+  w.child = reinterpret_cast<int32_t *>(take((size_t)2 * nnodes * 4));
+  w.values = reinterpret_cast<int32_t *>(take((size_t)(nleaves > 0 ? nleaves : 1) * 4));
+  w.start = reinterpret_cast<int64_t *>(take((size_t)nsub * 8));
+  w.exit_a = reinterpret_cast<int64_t *>(take((size_t)nsub * 8));
+  w.exit_b = reinterpret_cast<int64_t *>(take((size_t)nsub * 8));
+  w.cnt = reinterpret_cast<int32_t *>(take((size_t)nsub * 4));
+  w.bsum = reinterpret_cast<int64_t *>(take((size_t)(nblk + 1) * 8));
+  w.total = reinterpret_cast<int64_t *>(take(16));  // {symbols, first error bit}: one read back
+  w.err = reinterpret_cast<unsigned long long *>(w.total + 1);
+  w.changed = reinterpret_cast<int32_t *>(take(4));
+  return w;
+}
+
+}  // namespace
+}  // namespace hic
+
+using namespace hic;
+
+extern "C" size_t hic_huffman_decode_workspace_bytes(int64_t nbits, int32_t nnodes, int32_t nleaves) {
+  if (nbits < 0 || nnodes < 0 || nleaves < 0) return 0;
+  const int64_t nsub = ceil_div(nbits, kSub) > 0 ? ceil_div(nbits, kSub) : 1;
+  const int64_t nblk = ceil_div(nsub, kDT);
+  const int64_t r = 256;
+  return (size_t)(round_up(kLut * 4, r) + round_up(2LL * nnodes * 4, r) + round_up((nleaves > 0 ? nleaves : 1) * 4LL, r) +
+                  3 * round_up(nsub * 8, r) + round_up(nsub * 4, r) + round_up((nblk + 1) * 8, r) + 2 * r);
+}
+
+extern "C" int hic_huffman_decode(const uint8_t *d_bits, int64_t nbits, const int32_t *h_child, int32_t nnodes,
+                                  const int32_t *h_values, int32_t nleaves, int32_t *d_out, int64_t out_cap,
+                                  int64_t *h_count, void *workspace, void *stream) {
+  if (!h_child || !h_count || !workspace || (nbits > 0 && (!d_bits || !d_out)))
+    return arg_error("null pointer");
+  if (nbits < 0 || out_cap < 0) return arg_error("nbits / out_cap");
+  if (reinterpret_cast<uintptr_t>(d_bits) % 4) return arg_error("d_bits must be 4-byte aligned");
+  if (nnodes < 1 || nnodes >= (1 << 24) || nleaves < 1 || nleaves >= (1 << 24))
+    return arg_error("tree size (1 <= nodes, leaves < 2^24)");
+  // a tree: indices in range, every node but the root the child of exactly one node
+  std::vector<uint8_t> seen((size_t)nnodes + nleaves, 0);
+  for (int64_t k = 0; k < 2LL * nnodes; ++k) {
+    const int32_t c = h_child[k];
+    if (c == -1) continue;
+    const int64_t slot = c >= 0 ? c : (int64_t)nnodes + (-2 - (int64_t)c);
+    if ((c >= 0 && (c == 0 || c >= nnodes)) || (c < -1 && -2 - (int64_t)c >= nleaves) || seen[slot]++)
+      return arg_error("child[%lld] = %d is not a tree edge", (long long)k, c);
+  }
+  // the kLutBits-bit lookup table from the root
+  std::vector<uint32_t> lut(kLut);
+  for (int v = 0; v < kLut; ++v) {
+    int node = 0;
+    uint32_t e = ((uint32_t)(kLutBits - 1)) | (kNode << 4);
+    for (int k = 0; k < kLutBits; ++k) {
+      const int c = h_child[2 * node + 1 - ((v >> (kLutBits - 1 - k)) & 1)];
+      if (c == -1) {
+        e = (uint32_t)k | (kMissing << 4);
+        break;
+      }
+      if (c < 0) {
+        e = (uint32_t)k | (kLeaf << 4) | ((uint32_t)(-2 - c) << 8);
+        break;
+      }
+      node = c;
+      e = ((uint32_t)(kLutBits - 1)) | (kNode << 4) | ((uint32_t)node << 8);
+    }
+    lut[v] = e;
+  }
+  const hipStream_t s = as_stream(stream);
+  const int64_t nsub = ceil_div(nbits, kSub) > 0 ? ceil_div(nbits, kSub) : 1;
+  DecWs w = carve(workspace, nsub, nnodes, nleaves);
+  *h_count = 0;
+  if (nbits == 0) return HIC_OK;
+  if (int e = hip_status(hipMemcpyAsync(w.lut, lut.data(), kLut * 4, hipMemcpyHostToDevice, s), "hipMemcpyAsync"))
+    return e;
+  if (int e = hip_status(hipMemcpyAsync(w.child, h_child, (size_t)2 * nnodes * 4, hipMemcpyHostToDevice, s),
+                         "hipMemcpyAsync"))
+    return e;
+  if (h_values)
+    if (int e = hip_status(hipMemcpyAsync(w.values, h_values, (size_t)nleaves * 4, hipMemcpyHostToDevice, s),
+                           "hipMemcpyAsync"))
+      return e;
+  // the host tables are locals / the caller's: wait for the uploads before anything can return
+  if (int e = hip_status(hipStreamSynchronize(s), "hipStreamSynchronize")) return e;
+  if (int e = hip_status(hipMemsetAsync(w.err, 0xFF, 8, s), "hipMemsetAsync")) return e;
+  DecGeo g{reinterpret_cast<const uint32_t *>(d_bits), ceil_div(nbits, 32), nbits, nsub, w.lut, w.child};
+  const dim3 grid((unsigned)ceil_div(nsub, kDT)), block(kDT);
+  hipLaunchKernelGGL(k_hd_count, grid, block, 0, s, g, w.start, w.exit_a, w.cnt);
+  if (int e = check_launch("k_hd_count")) return e;
+  int64_t *ein = w.exit_a, *eout = w.exit_b;
+  bool synced = nsub == 1;
+  for (int round = 0; !synced && round < kMaxRounds; ++round) {
+    if (int e = hip_status(hipMemsetAsync(w.changed, 0, 4, s), "hipMemsetAsync")) return e;
+    hipLaunchKernelGGL(k_hd_sync, grid, block, 0, s, g, w.start, ein, eout, w.cnt, w.changed);
+    if (int e = check_launch("k_hd_sync")) return e;
+    int32_t changed = 0;
+    if (int e = hip_status(hipMemcpyAsync(&changed, w.changed, 4, hipMemcpyDeviceToHost, s), "hipMemcpyAsync"))
+      return e;
+    if (int e = hip_status(hipStreamSynchronize(s), "hipStreamSynchronize")) return e;
+    int64_t *t = ein;
+    ein = eout;
+    eout = t;
+    synced = changed == 0;
+  }
+  if (!synced) {
+    hipLaunchKernelGGL(k_hd_chain, dim3(1), dim3(1), 0, s, g, w.start, ein, w.cnt);
+    if (int e = check_launch("k_hd_chain")) return e;
+  }
+  hipLaunchKernelGGL(k_hd_bsum, grid, block, 0, s, w.cnt, nsub, w.bsum);
+  hipLaunchKernelGGL(k_hd_scan, dim3(1), block, 0, s, w.bsum, (int64_t)grid.x, w.total);
+  hipLaunchKernelGGL(k_hd_emit, grid, block, 0, s, g, w.start, w.cnt, w.bsum, h_values ? w.values : nullptr, d_out,
+                     out_cap, w.err);
+  if (int e = check_launch("k_hd_emit")) return e;
+  int64_t host[2];
+  if (int e = hip_status(hipMemcpyAsync(host, w.total, 16, hipMemcpyDeviceToHost, s), "hipMemcpyAsync")) return e;
+  if (int e = hip_status(hipStreamSynchronize(s), "hipStreamSynchronize")) return e;
+  const unsigned long long err = (unsigned long long)host[1];
+  if (err != ~0ULL) {
+    // the symbols before the failing one are in d_out; *h_count says how many
+    *h_count = host[0];
+    set_error("Huffman walk stepped into a missing child at bit %llu", err);
+    return HIC_ERR_ARG;
+  }
+  *h_count = host[0];
+  if (host[0] > out_cap) {
+    set_error("decoded %lld symbols, out_cap %lld", (long long)host[0], (long long)out_cap);
+    return HIC_ERR_CAPACITY;
+  }
+  return HIC_OK;
+}

@@ -95,7 +95,17 @@ class BitStringP(Payload):
 
     @classmethod
     def from_bytes(cls, b):
-        return cls(io.padded_bytes_2_bs(b))
+        """io.padded_bytes_2_bs's bits, kept packed (the '0'/'1' string is made on
+        first use of .payload): byte 0 = pad length p, then the body, whose last p
+        bits are padding."""
+        b = bytes(b)
+        if len(b) == 0:  # padded_bytes_2_bs indexes byte 0
+            raise IndexError("index out of range")
+        n = io.padded_bits_length(len(b), b[0])
+        body = np.zeros(-(-n // 8), dtype=np.uint8)  # bits past the body are zero
+        m = min(body.size, len(b) - 1)
+        body[:m] = np.frombuffer(b[1:1 + m], dtype=np.uint8)
+        return cls.from_packed(body, n)
 
     @classmethod
     def from_packed(cls, packed, nbits):
@@ -108,6 +118,13 @@ class BitStringP(Payload):
         self._payload = string
         self._packed = None
         self._nbits = None
+
+    def packed_bits(self):
+        """(uint8 array, nbits): the bits MSB-first, as hic_huffman_decode reads them."""
+        if self._packed is None:
+            bits = np.frombuffer(self._payload.encode("ascii"), dtype=np.uint8) - ord("0")
+            return np.packbits(bits), bits.size
+        return self._packed, self._nbits
 
     @property
     def payload(self):
@@ -125,6 +142,9 @@ class BitStringP(Payload):
             padding = 8 - self._nbits % 8
             body = self._packed[:self._nbits // 8 + 1] if self._nbits % 8 else self._packed[:self._nbits // 8]
             body = np.concatenate([body, np.zeros(1 if padding == 8 else 0, np.uint8)])
+            if padding != 8:  # the pad bits are zero (bytes read from a file may carry others)
+                body = body.copy()
+                body[-1] &= (0xFF << padding) & 0xFF
             return bytes([padding]) + body.tobytes()
         return io.padded_bs_2_bytes(self.payload)
 

@@ -266,6 +266,71 @@ class HuffmanTree:
             raise RuntimeError("packed %d bits, the histogram says %d" % (nb, total))
         return out[:-(-nb // 8)].cpu().numpy(), nb
 
+    def flat(self):
+        """The tree as hic_huffman_decode takes it: (child int32[2 * nodes], leaf nodes
+        in index order).  child[2n] / child[2n + 1] = node n's left ('1') / right ('0')
+        child: >= 0 internal, -1 none, <= -2 the leaf -2 - c; node 0 is the root."""
+        if getattr(self, "_flat", None) is None:
+            if self.root.is_leaf:
+                raise ValueError("a one-node tree decodes nothing")
+            child, leaves, index = [], [], {id(self.root): 0}
+            order = [self.root]
+            for node in order:  # breadth first; order grows as internal nodes appear
+                for c in (node.left, node.right):
+                    if c is None:
+                        child.append(-1)
+                    elif c.is_leaf:
+                        child.append(-2 - len(leaves))
+                        leaves.append(c)
+                    else:
+                        index[id(c)] = len(order)
+                        child.append(len(order))
+                        order.append(c)
+            self._flat = (np.asarray(child, dtype=np.int32), leaves)
+        return self._flat
+
+    def decode_device(self, bits_dev, nbits, out=None, stream=None):
+        """decode_data of a packed MSB-first stream on the device (hic_huffman_decode):
+        bits_dev a 4-byte-aligned uint8 tensor, nbits the stream length.  Returns
+        (int32 device tensor of the decoded values, count); leaves whose value is not
+        an int32 (None, from a table with unused codes) decode to their leaf index
+        and ``self.flat()[1]`` maps them back (see decode_packed)."""
+        child, leaves = self.flat()
+        vals = [l.value for l in leaves]
+        ints = all(isinstance(v, (int, np.integer)) and -2 ** 31 <= int(v) < 2 ** 31 for v in vals)
+        h_vals = np.asarray([int(v) for v in vals], dtype=np.int32) if ints else None
+        lib = _lib.load()
+        with device.on_stream(stream):
+            if out is None:
+                out = device.empty((max(int(nbits), 1),), torch.int32)
+            ws = device.workspace(lib.hic_huffman_decode_workspace_bytes(int(nbits), len(child) // 2, len(leaves)))
+            count = ctypes.c_int64(0)
+            st = lib.hic_huffman_decode(device.ptr(bits_dev) if nbits else None, int(nbits),
+                                        child.ctypes.data_as(ctypes.c_void_p), len(child) // 2,
+                                        h_vals.ctypes.data_as(ctypes.c_void_p) if ints else None, len(leaves),
+                                        device.ptr(out), out.numel(), ctypes.byref(count), device.ptr(ws),
+                                        device.stream_ptr(stream))
+            if st == _lib.HIC_ERR_ARG and "missing child" in _lib.last_error():
+                # the reference's reduce steps into None: huffman.py:155-161
+                raise AttributeError("'NoneType' object has no attribute 'is_leaf'")
+            _lib.check(st, "hic_huffman_decode")
+        return out, int(count.value), ints
+
+    def decode_packed(self, packed, nbits, stream=None):
+        """decode_data of a packed MSB-first stream (numpy uint8) through the GPU
+        decoder: the list of leaf values."""
+        if self.root.is_leaf:  # no edges: the reference fails on the first bit
+            return self.decode_data("1" if nbits else "")
+        buf = np.zeros(-(-max(int(nbits), 1) // 32) * 4, np.uint8)
+        body = np.asarray(packed, dtype=np.uint8)[:-(-int(nbits) // 8)]
+        buf[:body.size] = body
+        out, n, ints = self.decode_device(device.to_device(buf), nbits, stream=stream)
+        got = device.to_host(out[:n])
+        if ints:
+            return got.tolist()
+        leaves = self.flat()[1]
+        return [leaves[i].value for i in got.tolist()]
+
     def decode_data(self, bits):
         out = []
         node = self.root

@@ -22,9 +22,20 @@ def padded_bs_2_bytes(s):
     return bytes([padding]) + (int(bits, 2).to_bytes(len(bits) // 8, "big") if bits else b"")
 
 
+def padded_bits_length(nbytes, pad_byte):
+    """How many bits padded_bytes_2_bs keeps of an nbytes-byte buffer whose first
+    byte is pad_byte: iohelper.py:51-56 reads it as a SIGNED 8-bit int p, shifts the
+    whole buffer left by 8 bits (zero fill) and slices ``bin[:-p-8]`` -- Python
+    slice semantics, so p >= -8 drops p + 8 bits from the end while p < -8 keeps
+    the first -p - 8.  Bits past the body read as zero."""
+    p = pad_byte - 256 if pad_byte >= 128 else pad_byte
+    total, stop = 8 * nbytes, -p - 8
+    return max(0, total + stop) if stop < 0 else min(stop, total)
+
+
 def padded_bytes_2_bs(bites):
     bites = bytes(bites)
-    padding = bites[0]
     body = bites[1:]
+    n = padded_bits_length(len(bites), bites[0])
     bits = bin(int.from_bytes(body, "big"))[2:].zfill(8 * len(body)) if body else ""
-    return bits[:len(bits) - padding]
+    return (bits + "0" * 8)[:n]

@@ -4,7 +4,7 @@
 half of codec.jpeg_encode (compression.py:16-39, codec.py:286-301) for one
 H x W x 3 uint8 image that already lives in HBM:
 
-  1+2. hic_encode420_u8       (W % 512 == 0, H % 16 == 0) colour + 4:2:0 pyrDown +
+  1+2. hic_encode420_u8       (W % 16 == 0, H % 16 == 0) colour + 4:2:0 pyrDown +
                               8x8 DCT + quantize + zig-zag of the three planes + the
                               RLE tile records in ONE launch; the planes never reach
                               HBM.  Otherwise two launches:
@@ -65,8 +65,8 @@ class Encoder:
         encoder writes into (a gathering rank points them at its slice of the whole
         image's buffers, so its own shard needs no copy).
         fused: colour + 4:2:0 + DCT in one kernel (hic_encode420_u8, the planes never
-        reach HBM); None = whenever the shape allows it (W % 512 == 0, H and the row
-        range multiples of 16), False = the two-kernel chain (colour, then DCT)."""
+        reach HBM); None = whenever the shape allows it (W, H and the row range
+        multiples of 16), False = the two-kernel chain (colour, then DCT)."""
         if H < 2 or W < 2:
             raise ValueError("image must be at least 2 x 2")
         device.require_gpu()
@@ -77,10 +77,10 @@ class Encoder:
         self.rows = (r0, r1)
         a, b = input_span(H, r0, r1)
         # (hic_encode420_u8 reads the input rows through 32-bit buffer offsets)
-        can_fuse = (W % 512 == 0 and H % 16 == 0 and r0 % 16 == 0 and r1 % 16 == 0
+        can_fuse = (W % 16 == 0 and H % 16 == 0 and r0 % 16 == 0 and r1 % 16 == 0
                     and (b - a) * W * 3 <= 2**31 - 1)
         if fused and not can_fuse:
-            raise ValueError("the fused encoder needs W % 512 == 0, H and rows multiples of 16, "
+            raise ValueError("the fused encoder needs W, H and rows multiples of 16, "
                              "and < 2 GiB of input rows")
         self.fused = can_fuse if fused is None else bool(fused)
         c0, c1 = r0 // 2, min(H // 2, r1 // 2)
@@ -96,7 +96,9 @@ class Encoder:
         self.planes = {"lum": self.y, "cr": self.cr, "cb": self.cb}
         # tile records per 64-block tile: the fused kernel writes chroma records per
         # 32-block half tile
-        self.rpt = {"lum": 1, "cr": 2 if self.fused else 1, "cb": 2 if self.fused else 1}
+        # (W % 512 == 0; a ragged last strip gets one record per 64-block tile)
+        half = self.fused and W % 512 == 0
+        self.rpt = {"lum": 1, "cr": 2 if half else 1, "cb": 2 if half else 1}
         self.coef, self.dc, self.sym_len, self.sym_val, self.ws = {}, {}, {}, {}, {}
         self.cap = {}
         self.counts = device.zeros((3,), torch.int64)

@@ -146,14 +146,16 @@ int hic_dct_quant_rle_u8_batch(int n, const hic_dct_plane_job *jobs, int max_len
  *      HBM.  Output identical to hic_rgb_to_ycrcb420_rows + hic_dct_quant_rle_u8_batch.
  *  rgb_rows: image rows [in_row0, in_row0 + in_rows) of an H x W x 3 uint8 image
  *  (8-byte aligned), covering output rows [out_row0, out_row0 + out_rows) plus the
- *  pyrDown halo (2 rows above, 1 below, clamped to the image).  W % 512 == 0,
+ *  pyrDown halo (2 rows above, 1 below, clamped to the image).  W % 16 == 0,
  *  H % 16 == 0, out_row0 / out_rows multiples of 16.
  *  coef_*: ZIGZAG_I16 blocks of the output rows' Y ((out_rows/8) x (W/8) blocks) and
  *  Cr / Cb ((out_rows/16) x (W/16)).  ws_* (all or none): RLE workspaces that
  *  receive the tile records for hic_rle_encode_i16_tiles_batch -- Y one per
- *  64-block tile (records_per_tile 1), Cr / Cb one per 32-block half tile
- *  (records_per_tile 2); max_len as there.  ev_start / ev_stop (optional): events
- *  carrying the launch's own begin / end timestamps. */
+ *  64-block tile (records_per_tile 1); Cr / Cb one per 32-block half tile
+ *  (records_per_tile 2) when W % 512 == 0, else one per 64-block tile
+ *  (records_per_tile 1: a tile pass after the launch); max_len as there.
+ *  ev_start / ev_stop (optional): events carrying the fused launch's own begin /
+ *  end timestamps. */
 int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, int64_t H, int64_t W,
                      int64_t out_row0, int64_t out_rows, int16_t *coef_y, int16_t *coef_cr, int16_t *coef_cb,
                      void *ws_y, void *ws_cr, void *ws_cb, int max_len, void *stream, void *ev_start,
@@ -350,6 +352,22 @@ size_t hic_huffman_pack_workspace_bytes(int64_t n);
 int hic_huffman_pack(const void *keys, int key_bytes, int64_t n, int32_t key_min, int32_t nbins,
                      const uint64_t *d_code_bits, const uint8_t *d_code_len, uint8_t *out,
                      int64_t out_bytes, int64_t *d_nbits, void *workspace, void *stream);
+/* hic_huffman_decode: HuffmanTree.decode_data (huffman.py:149-178) of the nbits-bit
+ *    MSB-first stream at d_bits (4-byte aligned; the payload bytes after
+ *    iohelper's pad-length byte, iohelper.py:35-56) -- codec.jpeg_decode's nine
+ *    huffman_data_decode calls (codec.py:372-388).  The tree is a host array:
+ *    h_child[2n] / h_child[2n + 1] = node n's '1' (left) / '0' (right) child, >= 0
+ *    an internal node, -1 none, <= -2 the leaf -2 - c; node 0 is the root.  Symbol
+ *    k gets d_out[k] = h_values[leaf] (h_values null: the leaf index).  Trailing
+ *    bits that finish no code are dropped, as the reference's reduce does.
+ *    *h_count = symbols decoded.  Synchronises the stream.  HIC_ERR_ARG when a code
+ *    walks into a missing child (the reference's AttributeError; *h_count = the
+ *    symbols before it), HIC_ERR_CAPACITY when *h_count > out_cap (nbits is always
+ *    enough).  workspace >= hic_huffman_decode_workspace_bytes(nbits, nnodes, nleaves). */
+size_t hic_huffman_decode_workspace_bytes(int64_t nbits, int32_t nnodes, int32_t nleaves);
+int hic_huffman_decode(const uint8_t *d_bits, int64_t nbits, const int32_t *h_child, int32_t nnodes,
+                       const int32_t *h_values, int32_t nleaves, int32_t *d_out, int64_t out_cap,
+                       int64_t *h_count, void *workspace, void *stream);
 
 /* ---- Multi-GPU gather over RCCL (SURVEY.md section 8(b) hic_gather_*; the
  *      whole-image buffers it reassembles are what codec.jpeg_encode consumes,

@@ -258,3 +258,75 @@ def test_wire_views_are_byte_views_of_the_tensor():
     assert sharding._wire(b) is b
     with pytest.raises(ValueError):
         sharding._wire(t[:, ::2])
+
+
+def _ref_padded_bytes_2_bs(b):
+    """iohelper.py:51-56 restated with bitstring's semantics: the first byte read
+    as a signed int p, the whole buffer shifted left 8 bits (zero fill, same
+    length), then ``bin[:-p-8]``."""
+    p = b[0] - 256 if b[0] >= 128 else b[0]
+    bits = "".join(format(x, "08b") for x in b)
+    shifted = bits[8:] + "0" * 8
+    return shifted[:-p - 8]
+
+
+def test_padded_bytes_every_pad_byte():
+    """padded_bytes_2_bs and BitStringP.from_bytes (which keeps the bits packed for
+    the GPU decoder) agree with the reference's slicing for every pad byte,
+    including the signed and out-of-range ones a foreign file could hold."""
+    rng = np.random.default_rng(5)
+    for nbody in range(0, 5):
+        body = bytes(rng.integers(0, 256, nbody, dtype=np.uint8).tolist())
+        for pad in range(256):
+            b = bytes([pad]) + body
+            want = _ref_padded_bytes_2_bs(b)
+            assert iohelper.padded_bytes_2_bs(b) == want, (nbody, pad)
+            bsp = hicimage.BitStringP.from_bytes(b)
+            packed, nbits = bsp.packed_bits()
+            assert nbits == len(want), (nbody, pad)
+            assert np.unpackbits(np.asarray(packed, np.uint8))[:nbits].tolist() == [int(c) for c in want]
+            assert bsp.payload == want
+            # re-serialising gives what the reference writes for those bits
+            assert bsp.byte_stream == iohelper.padded_bs_2_bytes(want), (nbody, pad)
+
+
+def _walk_flat(child, leaves, bits):
+    """decode_data over the flat arrays hic_huffman_decode takes (the kernel's
+    semantics, restated bit by bit)."""
+    out, node = [], 0
+    for ch in bits:
+        c = child[2 * node + (0 if ch == "1" else 1)]
+        if c == -1:
+            raise AttributeError("missing child")
+        if c < 0:
+            out.append(leaves[-2 - c].value)
+            node = 0
+        else:
+            node = c
+    return out
+
+
+def test_huffman_flat_tree_matches_walk(golden_codec):
+    """HuffmanTree.flat() (the decode kernel's tree) decodes the golden bit strings
+    to the golden keys, for trees rebuilt from the tables and built from the data."""
+    g = golden_codec
+    for name in _names(g, "bs_"):
+        for ch in ("lum", "cr", "cb"):
+            for kind, key in (("dc", "dc"), ("av", "acv"), ("al", "acl")):
+                keys = g["%s_%s_%s" % (key, ch, name)]
+                table = list(zip(g["%shv_%s_%s" % (kind, ch, name)].tolist(),
+                                 g["%shc_%s_%s" % (kind, ch, name)].tolist()))
+                bits = str(g["%sb_%s_%s" % (kind, ch, name)])
+                for tree in (huffman.HuffmanTree.construct_from_coding(table),
+                             huffman.HuffmanTree.construct_from_counts(*huffman.first_appearance_counts(keys))):
+                    child, leaves = tree.flat()
+                    assert child.dtype == np.int32 and child.size % 2 == 0
+                    assert _walk_flat(child.tolist(), leaves, bits) == keys.tolist()
+    # a one-leaf encoding tree: its empty '0' side is a missing child
+    t = huffman.HuffmanTree.construct_from_data([7, 7, 7])
+    child, leaves = t.flat()
+    assert child.tolist() == [-2, -1] and leaves[0].value == 7
+    with pytest.raises(AttributeError):
+        _walk_flat(child.tolist(), leaves, "10")
+    with pytest.raises(AttributeError):
+        t.decode_data("10")

@@ -276,10 +276,12 @@ def _oracle_encode(rgb):
     return out
 
 
-@pytest.mark.parametrize("H,W", [(64, 96), (4320, 7680), (250, 330), (512, 768), (512, 1024), (272, 1536)])
+@pytest.mark.parametrize("H,W", [(64, 96), (4320, 7680), (250, 330), (512, 768), (512, 1024), (272, 1536),
+                                 (2160, 3840), (1088, 1920), (32, 16)])
 def test_pipeline_encoder(H, W):
-    """The device encoder vs the C oracle; widths % 512 == 0 (with H % 16 == 0) run
-    the fused kernel (hic_encode420_u8), the others the two-kernel chain."""
+    """The device encoder vs the C oracle; W and H multiples of 16 run the fused
+    kernel (hic_encode420_u8; W % 512 != 0: a ragged last strip), the others the
+    two-kernel chain."""
     rng = np.random.default_rng(H)
     rgb = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
     if H in (250, 272):
@@ -287,7 +289,7 @@ def test_pipeline_encoder(H, W):
     if H == 512:  # few grey levels: exact quantiser ties on the fast DCT path
         rgb = (rng.integers(0, 4, (H, W, 1)) * 85).astype(np.uint8).repeat(3, 2)
     enc = pipeline.Encoder(H, W)
-    assert enc.fused == (W % 512 == 0 and H % 16 == 0)
+    assert enc.fused == (W % 16 == 0 and H % 16 == 0)
     enc.encode(device.to_device(rgb))
     got = enc.result()
     exp = _oracle_encode(rgb)
@@ -361,6 +363,17 @@ def test_fused_encoder_matches_two_kernel_chain(kind, H, W, variant):
     np.testing.assert_array_equal(got.shard_summaries().cpu().numpy(), exp.shard_summaries().cpu().numpy())
 
 
+@pytest.mark.parametrize("variant", [{}, {"encode_dct": 2}, {"encode_waves": 3}, {"encode_nt": 1}])
+@pytest.mark.parametrize("kind", ["random", "levels", "blocks", "flat"])
+@pytest.mark.parametrize("H,W", [(2160, 3840), (1088, 1920), (32, 528), (48, 16), (16, 1040)])
+def test_fused_encoder_ragged_matches_chain(kind, H, W, variant):
+    """Widths that are not a multiple of 512: the fused kernel's last strip is
+    ragged (lanes past W store nothing, the right-border pixel goes to the strip's
+    last lane) and its tile records come from a tile pass -- symbols, DC and shard
+    summaries equal the two-kernel chain's."""
+    test_fused_encoder_matches_two_kernel_chain(kind, H, W, variant)
+
+
 @pytest.mark.timeout(900)
 def test_16k_roundtrip_vs_oracle():
     """BASELINE configs[4] on one GPU: a 16384 x 16384 random RGB image (the
@@ -398,7 +411,7 @@ def test_16k_roundtrip_vs_oracle():
 
 
 @pytest.mark.parametrize("H,W,world,flat", [(4320, 7680, 8, None), (250, 330, 3, None), (96, 64, 2, None),
-                                            (144, 96, 3, (48, 96))])
+                                            (144, 96, 3, (48, 96)), (2160, 3840, 3, None)])
 def test_shards_stitch_to_single_stream(H, W, world, flat):
     """Row shards (with pyrDown halos) + the stitch record reproduce the
     single-GPU stream exactly, and each shard's decode of its own slice
@@ -521,6 +534,82 @@ def test_huffman_device_vs_host(dtype, kind):
     got = hicimage.BitStringP.from_packed(packed, nbits)
     assert got.payload == bits
     assert got.byte_stream == hicimage.BitStringP(bits).byte_stream
+
+
+@pytest.mark.parametrize("kind", ["lengths", "values", "dc", "single", "skewed", "tail", "equal8"])
+def test_huffman_decode_device(kind):
+    """hic_huffman_decode (speculative subsequences + resynchronisation + the
+    serial chain) == the reference's bit walk (decode_data), on trees rebuilt from
+    the tables as jpeg_decode builds them: short codes, codes past the 12-bit
+    lookup (skewed), a one-symbol table, and equal 3-bit codes that never
+    resynchronise on 1024-bit subsequences (equal8: the chain path)."""
+    from hiccup_amd import huffman
+    rng = np.random.default_rng(len(kind))
+    n = 200_003
+    if kind == "lengths":
+        keys = rng.integers(0, 15, n)
+    elif kind == "values":
+        keys = np.round(rng.laplace(0, 40, n)).clip(-3277, 3277)
+    elif kind == "dc":
+        keys = rng.integers(-4096, 4097, n)
+    elif kind == "single":
+        keys = np.full(n, -7)
+    elif kind == "skewed":
+        keys = (rng.geometric(0.35, n) - 1) * 3 - 40
+    elif kind == "equal8":
+        keys = rng.integers(0, 8, n)
+    else:
+        keys = np.concatenate([rng.integers(0, 3, n - 5), [200, 201, 250, 255, 0]])
+    keys = keys.astype(np.int32)
+    ds = huffman.DeviceStream(device.to_device(keys))
+    packed, nbits = ds.packed()
+    codes = ds.tree.codes()
+    if kind == "skewed":
+        assert max(len(c) for c in codes.values()) > 12
+    if kind == "equal8":
+        assert set(len(c) for c in codes.values()) == {3}
+    dec = huffman.HuffmanTree.construct_from_coding(ds.tree.encode_table())
+    assert dec.decode_packed(packed, nbits) == keys.tolist()
+    # trailing bits that finish no code are dropped (the reference's reduce)
+    ends = np.cumsum([len(codes[int(k)]) for k in keys])
+    for cut in (1, 2, 5):
+        m = int(np.searchsorted(ends, nbits - cut, side="right"))
+        assert dec.decode_packed(packed, nbits - cut) == keys[:m].tolist()
+
+
+def test_huffman_decode_device_edges():
+    """Empty and one-bit streams, a table whose unused codes decode to None, a
+    one-leaf encoding tree's missing '0' child (AttributeError, as the reference's
+    walk raises), and a stream too short for one subsequence."""
+    from hiccup_amd import huffman
+    t = huffman.HuffmanTree.construct_from_coding([(5, "1")])  # "0" decodes to None
+    for bits in ["", "1", "0", "10", "0110", "1" * 3000 + "0" * 77]:
+        bsp = hicimage.BitStringP(bits)
+        assert t.decode_packed(*bsp.packed_bits()) == t.decode_data(bits), bits
+    single = huffman.HuffmanTree.construct_from_data([3, 3, 3])
+    assert single.decode_packed(*hicimage.BitStringP("111").packed_bits()) == [3, 3, 3]
+    with pytest.raises(AttributeError):
+        single.decode_packed(*hicimage.BitStringP("1" * 5000 + "0" + "1" * 5000).packed_bits())
+    tree = huffman.HuffmanTree.construct_from_data([1, 2, 2, 3, 3, 3, 4, 4, 4, 4])
+    for bits in ["001", "0010001", "01" * 700 + "0"]:
+        assert tree.decode_packed(*hicimage.BitStringP(bits).packed_bits()) == tree.decode_data(bits)
+
+
+def test_huffman_decode_device_full_size():
+    """An 8K-sized AC value stream (22 M symbols, Laplace keys): GPU pack then GPU
+    decode returns the keys (compared on the device)."""
+    from hiccup_amd import huffman
+    rng = np.random.default_rng(8)
+    n = 22_000_000
+    keys = device.to_device(np.round(rng.laplace(0, 6, n)).clip(-2047, 2047).astype(np.int32))
+    ds = huffman.DeviceStream(keys)
+    packed, nbits = ds.packed()
+    dec = huffman.HuffmanTree.construct_from_coding(ds.tree.encode_table())
+    buf = np.zeros(-(-nbits // 32) * 4, np.uint8)
+    buf[:packed.size] = packed
+    out, cnt, ints = dec.decode_device(device.to_device(buf), nbits)
+    assert ints and cnt == n
+    assert torch.equal(out[:n], keys)
 
 
 def test_huffman_device_streams_batch_equals_single():

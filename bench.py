@@ -14,17 +14,20 @@ One "step" encodes one such image.
 bench.py --gpus N` starts the N ranks itself (torch.multiprocessing, before any
 GPU call in the parent); under torch.distributed.run it joins the given ranks.
   --mode strong (default): ONE 8K image split N ways by block rows; each rank
-                 encodes its shard (colour with halo, DCT, its slice of the single
-                 DC/RLE stream after the 96-byte summary all-gather); each image's
-                 coefficient blocks and DC stream are then reassembled on one rank
-                 by an RCCL gather.  Image j of each group of N consecutive images
-                 lands on rank j, and the group's N gathers go out as ONE grouped
-                 batch (sharding.gather_coefficients_group) on a process group of
-                 their own: every xGMI link carries data in both directions, where
-                 N gathers into rank 0 would queue on its 7 ingress links, and the
-                 next group's encodes run beside the exchange.  The group's
-                 encodes batch their exchange steps (sharding.encode_group: one
-                 summary all-gather and one count all-gather per group).
+                 transforms its shard (colour with halo, DCT + quantize + zig-zag +
+                 RLE tile records) and ships its blocks in the lossless 13-bit wire
+                 format (hic_wire_pack_i16, 81.7 MB per 8K image with the records)
+                 to the image's gathering rank, which unpacks them and runs the
+                 scan + emit of the whole image: each timed image ends as ONE
+                 encoded stream (codec.jpeg_encode's DC / RLE symbols) on one rank.
+                 Image j of each group of N consecutive images lands on rank j, and
+                 the group's N gathers go out as ONE grouped batch
+                 (sharding.gather_streams_group) on a process group of their own:
+                 every xGMI link carries data in both directions, where N gathers
+                 into rank 0 would queue on its 7 ingress links.
+                 --gather-kind blocks: round 2's exchange instead (each rank codes
+                 its slice of the stream after a summary all-gather; the int16
+                 blocks + DC are gathered, the symbol slices stay distributed).
   --mode weak:   an (N*H) x W image, one H-row shard per rank (no gather).
 --workload 4k: 4096 x 4096 RGB instead of 7680 x 4320 (north_star's 4K point).
 value = pixels encoded by all ranks / max-over-ranks wall time of the K steps.
@@ -61,6 +64,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--mode", choices=("weak", "strong"), default="strong")
     ap.add_argument("--workload", choices=("8k", "4k"), default="8k")
+    ap.add_argument("--gather-kind", choices=("stream", "blocks"), default="stream",
+                    help="strong mode: 'stream' = wire-format blocks to the gathering rank, which codes the whole "
+                         "stream (default); 'blocks' = per-shard stream slices + int16 block gather (round 2)")
     ap.add_argument("--no-gather", action="store_true",
                     help="strong mode: leave the coefficient blocks distributed (no RCCL gather)")
     ap.add_argument("--transport", choices=("torch", "c-abi"), default="torch",
@@ -575,6 +581,7 @@ def main():
         H = H0 * world if not strong else H0
         make = lambda j: sharding.ShardEncoder(H, W0, rank=rank, world=world,  # noqa: E731
                                                gather_to=j % world if gather else None,
+                                               gather_kind=args.gather_kind if gather else "blocks",
                                                fused=False if args.unfused else None)
     else:
         H = H0
@@ -635,7 +642,9 @@ def main():
             if record:
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record()
-            if rgather is not None:
+            if args.gather_kind == "stream":
+                sharding.gather_streams_group(group_encs, group=xgroup, rccl=rgather, stream=st)
+            elif rgather is not None:
                 rgather.gather_encoders(group_encs, st)
             else:
                 sharding.gather_coefficients_group(group_encs, group=xgroup)
@@ -700,13 +709,28 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    # every step's symbol counts are valid (a failed step would report a negative count)
+    # every step's symbol counts are valid (a failed step would report a negative count);
+    # in stream-gather mode the streams live on the gathering ranks
+    stream_gather = gather and args.gather_kind == "stream"
+
+    def counts_of(e):
+        if world == 1:
+            return e.counts
+        if stream_gather:
+            return e.whole.counts if e.whole is not None else None
+        return e.enc.counts
+
     for e in encs:
-        counts = e.enc.counts if world > 1 else e.counts
+        counts = counts_of(e)
+        if counts is None:
+            continue
         for ci, c in enumerate(counts.cpu().tolist()):
             pipeline.check_count(int(c), pipeline.CHANNELS[ci])
             assert c > 0, "empty symbol stream"
-    symbols = [int(c) for c in (encs[0].enc.counts if world > 1 else encs[0].counts).cpu().tolist()]
+    mine = [e for e in encs if counts_of(e) is not None]
+    symbols = [int(c) for c in counts_of(mine[0]).cpu().tolist()] if mine else None
+    wire_flags = [int(e.wire_flag.item()) for e in encs if stream_gather]
+    assert not any(wire_flags), "a coefficient outside the 13-bit wire range"
     # per image: each grouped batch's span / the images it carried
     gather_us = (float(sum(a.elapsed_time(b) for a, b, _ in gather_ev) / sum(n for _, _, n in gather_ev)) * 1e3
                  if gather_ev else None)
@@ -718,7 +742,8 @@ def main():
     # given (7 links x ~153 GB/s per MI355X), not a measurement.
     gather_link = None
     if gather_ev and world > 1:
-        img_bytes = sum(encs[0].ranges[k][-1][1] * (64 * 2 + 4) for k in pipeline.CHANNELS)
+        img_bytes = (encs[0].wire_bytes if stream_gather else
+                     sum(encs[0].ranges[k][-1][1] * (64 * 2 + 4) for k in pipeline.CHANNELS))
         span_us = float(np.mean([a.elapsed_time(b) for a, b, n in gather_ev if n == world] or
                                 [a.elapsed_time(b) for a, b, _ in gather_ev])) * 1e3
         per_link = img_bytes / world / (span_us * 1e-6) / 1e9
@@ -762,7 +787,7 @@ def main():
     # left distributed (no gather), timed the same way -- the sharded encode itself
     # scales; the gathers are bound by the xGMI links
     no_gather = None
-    if gather:
+    if gather and not stream_gather:
         dist.barrier()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
@@ -800,8 +825,11 @@ def main():
             wl += ("; %s: %s, block-row tile shards over %d ranks%s"
                    % ("BASELINE configs[3]" if (strong and args.workload == "8k") else "multi-GPU",
                       "one image split N ways" if strong else "one %d-row shard per rank" % H0, world,
-                      ", each image's coefficient blocks + DC stream gathered to one rank (image j of each "
-                      "group of %d to rank j, the group's gathers in one grouped RCCL batch)" % world
+                      (", each image's blocks gathered to one rank in the 13-bit wire format with their RLE "
+                       "tile records, where the whole image's DC / RLE stream is coded (image j of each group of "
+                       "%d to rank j, the group's gathers in one grouped RCCL batch)" % world) if stream_gather else
+                      (", each image's coefficient blocks + DC stream gathered to one rank (image j of each "
+                       "group of %d to rank j, the group's gathers in one grouped RCCL batch)" % world)
                       if gather else ""))
         else:
             wl = ("BASELINE configs[2]: " if args.workload == "8k" else "") + wl
@@ -828,10 +856,16 @@ def main():
                 "gather": "image j of each group of %d to rank j, one grouped RCCL batch per group (%s)"
                           % (world, "torch.distributed P2P" if rgather is None else "C-ABI hic_gather_bytes")
                           if gather else None,
+                "gather_kind": args.gather_kind if gather else None,
+                "gather_bytes_per_image": (encs[0].wire_bytes if stream_gather else
+                                           sum(encs[0].ranges[k][-1][1] * (64 * 2 + 4) for k in pipeline.CHANNELS))
+                if gather else None,
                 "gather_us_per_image": None if gather_us is None else round(gather_us, 2),
                 "gather_link": gather_link,
                 "without_gather": no_gather,
                 "symbols_per_image_rank0": symbols,
+                "stream_ends_on": "the gathering rank (whole-image scan + emit)" if stream_gather else
+                ("every rank holds its slice" if world > 1 else "this GPU"),
                 "dist_backend": None if world == 1 else args.dist_backend + (" (same device)" if args.same_device
                                                                               else ""),
                 "parallelism": "dp%d tile-shard" % world,

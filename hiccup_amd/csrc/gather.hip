@@ -145,6 +145,7 @@ extern "C" int hic_gather_bytes(void *comm, const void *d_send, int64_t send_byt
   if (int rc = need_rccl(r)) return rc;
   const hipStream_t s = as_stream(stream);
   if (c->rank != root) {
+    if (send_bytes == 0) return HIC_OK;  // the root posts no receive for an empty slice
     if (int rc = rccl_status(r, r->group_start(), "ncclGroupStart")) return rc;
     const int rc = rccl_status(r, r->send(d_send, (size_t)send_bytes, ncclUint8, root, c->comm, s), "ncclSend");
     const int rc2 = rccl_status(r, r->group_end(), "ncclGroupEnd");

@@ -1507,6 +1507,15 @@ extern "C" int hic_rle_encode_i16_tiles(const int16_t *blocks, int64_t nblk, int
                              as_stream(stream));
 }
 
+extern "C" int hic_rle_tile_records_i16(const int16_t *blocks, int64_t nblk, int max_len, void *workspace,
+                                        void *stream) {
+  if (!blocks || !workspace) return arg_error("null pointer");
+  if (nblk <= 0) return arg_error("nblk");
+  if (max_len < 1 || max_len > 256) return arg_error("max_len must be in [1, 256] for uint8 symbol lengths");
+  if (reinterpret_cast<uintptr_t>(blocks) & 15) return arg_error("blocks must be 16-byte aligned");
+  return launch_tile16(blocks, nblk, max_len, static_cast<int64_t *>(workspace), as_stream(stream));
+}
+
 extern "C" int hic_rle_encode_i16_tiles_batch(int n, const hic_rle_job16 *jobs, int max_len, void *stream) {
   if (n < 1 || n > kMaxJobs || !jobs) return arg_error("1 <= n <= %d jobs", kMaxJobs);
   if (max_len < 1 || max_len > 256) return arg_error("max_len must be in [1, 256] for uint8 symbol lengths");

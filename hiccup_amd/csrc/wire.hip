@@ -1,0 +1,200 @@
+// wire.hip -- the gather's lossless wire format for quantized zig-zag blocks
+// (DESIGN.md section 6): a block's DC as 16 bits and its 63 AC slots as 13-bit
+// two's complement, 835 bits per block, packed back to back, so a 64-block tile
+// is exactly 1670 32-bit words, stored at a stride of 1672 (6688 B against 8192 B
+// of int16 blocks; 16-byte aligned tiles).  Bit i of a tile is bit (i & 31) of its
+// word i >> 5 (LSB first).
+//
+// Why 13 bits lose nothing: an AC coefficient of hiccup's orthonormal 8x8 DCT-II
+// (transform.py:67-84) of pixels - 128 is bounded by 128 * (sum |c_u(x)|) *
+// (sum |c_v(y)|) <= 128 * 4 * 4 = 2048 (every 1-D basis entry is at most 1/2 in
+// magnitude), and the quantizer divides by a table entry >= 1
+// (quantization.py:47-52), so |q| <= 2048 < 4096.  The pack kernel still checks
+// every value and raises *d_flag for one outside [-4096, 4095] (the caller then
+// sends the raw blocks).  The DC (a 16-bit zig-zag slot) is carried whole.
+//
+//  hic_wire_pack_i16:   nblk blocks (64 int16, ZIGZAG_I16) -> ceil(nblk / 64) tiles
+//  hic_wire_unpack_i16: the inverse (blocks past nblk in the last tile dropped)
+//  hic_rle_records_rebase: a shard's RLE tile records moved into the whole
+//                       image's record array (positions + pos_shift), so the
+//                       gathering rank runs the scan + emit without a tile pass
+#include "hic_common.h"
+
+namespace hic {
+namespace {
+
+constexpr int kBlkBits = 16 + 63 * 13;        // 835
+constexpr int kTileWords = 64 * kBlkBits / 32;  // 1670
+constexpr int kTileStride = 1672;              // words per tile on the wire (16-byte multiple)
+constexpr int kWPB = 4;                        // waves per workgroup
+static_assert(64 * kBlkBits % 32 == 0 && kTileWords <= kTileStride, "a tile is whole words");
+
+// pack: lane j = block j of the wave's tile; its 835 bits are ORed into the LDS
+// tile at bit 835 j (the two words a lane shares with its neighbours need the OR)
+__global__ __launch_bounds__(64 * kWPB) void k_wire_pack(const int16_t *__restrict__ blocks, int64_t nblk,
+                                                         uint32_t *__restrict__ out, int *__restrict__ flag) {
+  __shared__ uint32_t s_tile[kWPB][kTileStride];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t ntiles = (nblk + 63) / 64;
+  const int64_t t = (int64_t)blockIdx.x * kWPB + wv;
+  if (t >= ntiles) return;  // wave-uniform
+  uint32_t *st = s_tile[wv];
+  for (int i = lane; i < kTileStride; i += 64) st[i] = 0;
+  __builtin_amdgcn_wave_barrier();
+  const int64_t b = t * 64 + lane;
+  uint32_t w[32];
+  if (b < nblk) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(blocks + b * 64);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint4 v = q[k];
+      w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 32; ++k) w[k] = 0;
+  }
+  // stream the fields into 32-bit words: acc holds `n` pending bits (LSB first)
+  const int bit0 = lane * kBlkBits;
+  int wi = bit0 >> 5, n = bit0 & 31;
+  uint64_t acc = 0;
+  bool bad = false;
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    const int v = (int)(int16_t)((w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
+    uint32_t f;
+    int nb;
+    if (i == 0) {
+      f = (uint32_t)v & 0xFFFFu;
+      nb = 16;
+    } else {
+      bad |= v < -4096 || v > 4095;
+      f = (uint32_t)v & 0x1FFFu;
+      nb = 13;
+    }
+    acc |= (uint64_t)f << n;
+    n += nb;
+    if (n >= 32) {
+      atomicOr(&st[wi], (uint32_t)acc);  // first / last word: shared with a neighbour
+      ++wi;
+      acc >>= 32;
+      n -= 32;
+    }
+  }
+  if (n > 0) atomicOr(&st[wi], (uint32_t)acc);
+  if (bad) *flag = 1;
+  __builtin_amdgcn_wave_barrier();
+  // copy out: 418 16-byte chunks (the last two words are zero padding)
+  uint4 *o = reinterpret_cast<uint4 *>(out + t * kTileStride);
+  for (int c = lane; c < kTileStride / 4; c += 64)
+    o[c] = make_uint4(st[4 * c], st[4 * c + 1], st[4 * c + 2], st[4 * c + 3]);
+}
+
+// unpack: the tile into LDS (coalesced), lane j extracts block j into its stage
+// row, the stage leaves as 1 KiB stores
+constexpr int kRowU4 = 9;  // 144 B stage rows (128 B + pad)
+__global__ __launch_bounds__(64 * kWPB) void k_wire_unpack(const uint32_t *__restrict__ wire, int64_t nblk,
+                                                           int16_t *__restrict__ blocks) {
+  __shared__ uint32_t s_tile[kWPB][kTileStride];
+  __shared__ uint4 s_stage[kWPB][64 * kRowU4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t ntiles = (nblk + 63) / 64;
+  const int64_t t = (int64_t)blockIdx.x * kWPB + wv;
+  if (t >= ntiles) return;
+  uint32_t *st = s_tile[wv];
+  const uint4 *src = reinterpret_cast<const uint4 *>(wire + t * kTileStride);
+  for (int c = lane; c < kTileStride / 4; c += 64) {
+    const uint4 v = src[c];
+    st[4 * c] = v.x; st[4 * c + 1] = v.y; st[4 * c + 2] = v.z; st[4 * c + 3] = v.w;
+  }
+  __builtin_amdgcn_wave_barrier();
+  const int bit0 = lane * kBlkBits;
+  int wi = bit0 >> 5, n = 0;
+  uint64_t acc = 0;
+  {
+    const int ph = bit0 & 31;
+    acc = (uint64_t)st[wi++] >> ph;
+    n = 32 - ph;
+  }
+  uint32_t w[32];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    const int nb = i == 0 ? 16 : 13;
+    if (n < nb) {
+      acc |= (uint64_t)st[wi++] << n;
+      n += 32;
+    }
+    int v;
+    if (i == 0)
+      v = (int)(int16_t)(acc & 0xFFFFu);
+    else
+      v = ((int)(acc & 0x1FFFu) ^ 0x1000) - 0x1000;  // sign-extend 13 bits
+    acc >>= nb;
+    n -= nb;
+    if (i & 1)
+      w[i >> 1] |= ((uint32_t)v & 0xFFFFu) << 16;
+    else
+      w[i >> 1] = (uint32_t)v & 0xFFFFu;
+  }
+  uint4 *row = s_stage[wv] + lane * kRowU4;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) row[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+  __builtin_amdgcn_wave_barrier();
+  // chunk c = 64 k + lane: block c / 8, 16-byte part c % 8
+  uint4 *o = reinterpret_cast<uint4 *>(blocks + t * 64 * 64);
+  const int64_t nvalid = nblk - t * 64;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = 64 * k + lane, bb = c >> 3;
+    if (bb < nvalid) o[c] = s_stage[wv][bb * kRowU4 + (c & 7)];
+  }
+}
+
+__global__ void k_records_rebase(const int64_t *__restrict__ src, int64_t nrec, int64_t shift,
+                                 int64_t *__restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nrec) return;
+  const int64_t f = src[3 * i], l = src[3 * i + 1];
+  dst[3 * i] = f >= 0 ? f + shift : f;
+  dst[3 * i + 1] = l >= 0 ? l + shift : l;
+  dst[3 * i + 2] = src[3 * i + 2];
+}
+
+}  // namespace
+}  // namespace hic
+
+using namespace hic;
+
+extern "C" size_t hic_wire_bytes(int64_t nblk) { return nblk <= 0 ? 0 : (size_t)((nblk + 63) / 64) * kTileStride * 4; }
+
+extern "C" int hic_wire_pack_i16(const int16_t *blocks, int64_t nblk, uint8_t *wire, int *d_flag, void *stream) {
+  if (!blocks || !wire || !d_flag) return arg_error("null pointer");
+  if (nblk <= 0) return arg_error("nblk");
+  if ((reinterpret_cast<uintptr_t>(blocks) | reinterpret_cast<uintptr_t>(wire)) % 16)
+    return arg_error("blocks and wire must be 16-byte aligned");
+  const int64_t ntiles = (nblk + 63) / 64;
+  hipLaunchKernelGGL(k_wire_pack, dim3((unsigned)((ntiles + kWPB - 1) / kWPB)), dim3(64 * kWPB), 0, as_stream(stream),
+                     blocks, nblk, reinterpret_cast<uint32_t *>(wire), d_flag);
+  return check_launch("k_wire_pack");
+}
+
+extern "C" int hic_wire_unpack_i16(const uint8_t *wire, int64_t nblk, int16_t *blocks, void *stream) {
+  if (!blocks || !wire) return arg_error("null pointer");
+  if (nblk <= 0) return arg_error("nblk");
+  if ((reinterpret_cast<uintptr_t>(blocks) | reinterpret_cast<uintptr_t>(wire)) % 16)
+    return arg_error("blocks and wire must be 16-byte aligned");
+  const int64_t ntiles = (nblk + 63) / 64;
+  hipLaunchKernelGGL(k_wire_unpack, dim3((unsigned)((ntiles + kWPB - 1) / kWPB)), dim3(64 * kWPB), 0,
+                     as_stream(stream), reinterpret_cast<const uint32_t *>(wire), nblk, blocks);
+  return check_launch("k_wire_unpack");
+}
+
+extern "C" int hic_rle_records_rebase(const int64_t *d_src, int64_t nrec, int64_t pos_shift, int64_t *d_dst,
+                                      void *stream) {
+  if (!d_src || !d_dst) return arg_error("null pointer");
+  if (nrec < 0 || pos_shift < 0) return arg_error("nrec / pos_shift");
+  if (nrec == 0) return HIC_OK;
+  hipLaunchKernelGGL(k_records_rebase, dim3((unsigned)((nrec + 255) / 256)), dim3(256), 0, as_stream(stream), d_src,
+                     nrec, pos_shift, d_dst);
+  return check_launch("k_records_rebase");
+}

@@ -100,13 +100,54 @@ def block_ranges(H, W, world):
     return out
 
 
+REC_BYTES = 24  # one RLE tile record: 3 int64
+
+
+def wire_ranges(ranges, rpt, records):
+    """{channel: [(o0, o1)]}: rank r's byte segment of the whole image's wire buffer
+    -- its blocks in the wire format (hic_wire_bytes) followed, when `records`, by
+    its RLE tile records already rebased to whole-image positions (REC_BYTES each,
+    rpt records per 64 blocks, padded to a multiple of 16 bytes)."""
+    lib = _lib.load()
+    out = {}
+    for k in CHANNELS:
+        o, rr = 0, []
+        for b0, b1 in ranges[k]:
+            n = b1 - b0
+            # (the records padded to 16 bytes: every segment starts 16-byte aligned)
+            size = lib.hic_wire_bytes(n) + (-(-(-(-n * rpt[k] // 64) * REC_BYTES) // 16) * 16 if records else 0)
+            rr.append((o, o + size))
+            o += size
+        out[k] = rr
+    return out
+
+
+def records_aligned(ranges, rpt):
+    """Every shard starts on a record boundary of the whole image (its records can
+    be rebased instead of recomputed): W % 512 == 0 on the fused path."""
+    return all((b0 * rpt[k]) % 64 == 0 for k in CHANNELS for b0, _ in ranges[k])
+
+
 class ShardEncoder:
     """One rank's part of a tile-sharded encode of an H x W RGB image.
 
-    gather_to: the rank that reassembles the whole image's coefficient blocks and
-    DC differences (gather_coefficients); None = no reassembly buffers."""
+    gather_to: the rank that reassembles the image; None = no reassembly buffers.
+    gather_kind "blocks": every rank entropy-codes its slice of the stream
+    (summaries, stitch, scan + emit) and gather_to collects the whole image's
+    coefficient blocks and DC differences (gather_coefficients).
+    gather_kind "stream": the ranks only transform; each ships its blocks in the
+    lossless 13-bit wire format (hic_wire_pack_i16) plus its rebased RLE tile
+    records to gather_to, which unpacks them and runs the scan + emit of the whole
+    image -- codec.jpeg_encode's single stream (codec.py:55-99,286-301) ends on
+    gather_to (self.whole.sym_len / sym_val / dc / counts), with no host sync and
+    no per-shard entropy pass.  See stream_item / pack / finish."""
 
-    def __init__(self, H, W, rank=None, world=None, group=None, max_len=15, gather_to=None, fused=None):
+    def __init__(self, H, W, rank=None, world=None, group=None, max_len=15, gather_to=None, fused=None,
+                 gather_kind="blocks"):
+        if gather_kind not in ("blocks", "stream"):
+            raise ValueError("gather_kind must be 'blocks' or 'stream'")
+        if gather_kind == "stream" and gather_to is None:
+            raise ValueError("gather_kind 'stream' needs gather_to")
         self.rank = dist.get_rank(group) if rank is None else rank
         self.world = dist.get_world_size(group) if world is None else world
         self.group = group
@@ -114,14 +155,23 @@ class ShardEncoder:
         self.rows = plan(H, self.world)[self.rank]
         self.ranges = block_ranges(H, W, self.world)
         self.gather_to = gather_to
+        self.gather_kind = gather_kind
+        self.whole = None
         out = None
         if gather_to is not None and self.rank == gather_to:
-            # whole-image buffers; this rank's encoder writes its slice in place
-            self.full_coef, self.full_dc, out = {}, {}, {}
+            if gather_kind == "stream":
+                # the whole image's entropy stage lives here: its buffers are the
+                # landing zone, this rank's encoder writes its slice in place
+                self.whole = pipeline.Encoder(H, W, max_len=max_len, fused=fused)
+                self.full_coef, self.full_dc = self.whole.coef, self.whole.dc
+            else:
+                self.full_coef, self.full_dc = {}, {}
+                for k in CHANNELS:
+                    n = self.ranges[k][-1][1]
+                    self.full_coef[k] = device.empty((n, 64), torch.int16)
+                    self.full_dc[k] = device.empty((n,), torch.int32)
+            out = {}
             for k in CHANNELS:
-                n = self.ranges[k][-1][1]
-                self.full_coef[k] = device.empty((n, 64), torch.int16)
-                self.full_dc[k] = device.empty((n,), torch.int32)
                 b0, b1 = self.ranges[k][self.rank]
                 out[k] = (self.full_coef[k][b0:b1], self.full_dc[k][b0:b1])
         self.enc = pipeline.Encoder(H, W, max_len=max_len, rows=self.rows, out=out, fused=fused)
@@ -129,6 +179,78 @@ class ShardEncoder:
         self.all_summ = device.zeros((self.world, 3, 4), torch.int64)
         self.stitch = device.zeros((3, 4), torch.int64)
         self.all_counts = device.zeros((self.world, 3), torch.int64)
+        if gather_kind == "stream":
+            self.records = records_aligned(self.ranges, self.enc.rpt)
+            self.wranges = wire_ranges(self.ranges, self.enc.rpt, self.records)
+            self.wire_flag = device.zeros((1,), torch.int32)
+            if self.rank == gather_to:
+                self.wire_full = {k: device.empty((self.wranges[k][-1][1],), torch.uint8) for k in CHANNELS}
+                self.wire_send = None
+            else:
+                self.wire_full = None
+                self.wire_send = {k: device.empty((self.wranges[k][self.rank][1] - self.wranges[k][self.rank][0],),
+                                                  torch.uint8) for k in CHANNELS}
+
+    @property
+    def wire_bytes(self):
+        """Bytes of one image on the wire (every rank's segments, all channels)."""
+        return sum(self.wranges[k][-1][1] for k in CHANNELS) if self.gather_kind == "stream" else None
+
+    def pack(self, stream=None):
+        """gather_kind "stream", a rank other than gather_to: this rank's blocks into
+        the wire format and its tile records, rebased, behind them (on `stream`)."""
+        s = device.stream_ptr(stream)
+        lib = _lib.load()
+        for k in CHANNELS:
+            b0, b1 = self.ranges[k][self.rank]
+            n = b1 - b0
+            w = self.wire_send[k]
+            wb = lib.hic_wire_bytes(n)
+            _lib.call("hic_wire_pack_i16", device.ptr(self.enc.coef[k]), n, device.ptr(w), device.ptr(self.wire_flag), s)
+            if self.records:
+                nrec = -(-n * self.enc.rpt[k] // 64)
+                _lib.call("hic_rle_records_rebase", device.ptr(self.enc.ws[k]), nrec, b0 * 63,
+                          ctypes.c_void_p(w.data_ptr() + wb), s)
+
+    def stream_item(self):
+        """(mine, full, ranges, dst) of this image's wire gather for
+        gather_blocks_group / RcclGather.gather_group (byte tensors, byte ranges)."""
+        if self.wire_send is not None:
+            mine, full = {k: (self.wire_send[k],) for k in CHANNELS}, None
+        else:  # gather_to: its own segment is never sent (the C-ABI sees it in place)
+            mine = {k: (self.wire_full[k][slice(*self.wranges[k][self.rank])],) for k in CHANNELS}
+            full = {k: (self.wire_full[k],) for k in CHANNELS}
+        return mine, full, self.wranges, self.gather_to
+
+    def finish(self, stream=None):
+        """gather_to, after the wire gather: every other rank's blocks unpacked into
+        the whole image, the tile records placed (or, when the shards do not start
+        on record boundaries, recomputed by a tile pass), then the whole image's
+        scan + emit (one stream, no stitch).  On `stream`."""
+        s = device.stream_ptr(stream)
+        lib = _lib.load()
+        whole = self.whole
+        for k in CHANNELS:
+            rpt = whole.rpt[k]
+            for r in range(self.world):
+                b0, b1 = self.ranges[k][r]
+                n = b1 - b0
+                nrec = -(-n * rpt // 64)
+                dst_rec = ctypes.c_void_p(whole.ws[k].data_ptr() + (b0 * rpt // 64) * REC_BYTES)
+                if r == self.rank:
+                    if self.records:
+                        _lib.call("hic_rle_records_rebase", device.ptr(self.enc.ws[k]), nrec, b0 * 63, dst_rec, s)
+                    continue
+                o0, _ = self.wranges[k][r]
+                seg = ctypes.c_void_p(self.wire_full[k].data_ptr() + o0)
+                _lib.call("hic_wire_unpack_i16", seg, n, device.ptr(whole.coef[k][b0:b1]), s)
+                if self.records:
+                    src = ctypes.c_void_p(self.wire_full[k].data_ptr() + o0 + lib.hic_wire_bytes(n))
+                    _lib.call("hic_rle_records_rebase", src, nrec, 0, dst_rec, s)
+            if not self.records:
+                _lib.call("hic_rle_tile_records_i16", device.ptr(whole.coef[k]), whole.coef[k].shape[0],
+                          whole.max_len, device.ptr(whole.ws[k]), s)
+        whole.entropy(stream)
 
     @property
     def pixels(self):
@@ -208,6 +330,11 @@ def encode_group(encoders, rgb_rows_list, stream=None, dct_events=None):
 def _encode_group(encoders, rgb_rows_list, stream, dct_events):
     e0 = encoders[0]
     n, world = len(encoders), e0.world
+    if all(se.gather_kind == "stream" for se in encoders):
+        # the entropy stage runs on the gathering rank (gather_streams_group)
+        for i, (se, x) in enumerate(zip(encoders, rgb_rows_list)):
+            se.enc.transform(x, stream, in_row0=se.span[0], dct_events=dct_events[i] if dct_events else None)
+        return
     summs = []
     for i, (se, x) in enumerate(zip(encoders, rgb_rows_list)):
         se.enc.transform(x, stream, in_row0=se.span[0], dct_events=dct_events[i] if dct_events else None)
@@ -236,6 +363,30 @@ def gather_coefficients_group(encoders, group=None):
     e0 = encoders[0]
     gather_blocks_group(items, e0.rank, e0.world, group if group is not None else e0.group)
     return [it[1] for it in items]
+
+
+def gather_streams_group(encoders, group=None, rccl=None, stream=None):
+    """gather_kind "stream": the wire gathers of several images (image j to rank j)
+    in ONE grouped batch, then each receiving rank's unpack + scan + emit, all on
+    `stream` (default: the current one) with no host sync.  rccl: a RcclGather to
+    move the bytes through the C-ABI instead of torch.distributed.  Returns each
+    encoder's whole-image pipeline.Encoder (its stream) on its gather_to rank, None
+    elsewhere."""
+    st = stream if stream is not None else torch.cuda.current_stream()
+    with torch.cuda.stream(st):
+        for e in encoders:
+            if e.rank != e.gather_to:
+                e.pack(st)
+        items = [e.stream_item() for e in encoders]
+        e0 = encoders[0]
+        if rccl is not None:
+            rccl.gather_group(items, st)
+        else:
+            gather_blocks_group(items, e0.rank, e0.world, group if group is not None else e0.group)
+        for e in encoders:
+            if e.rank == e.gather_to:
+                e.finish(st)
+    return [e.whole for e in encoders]
 
 
 def gather_blocks(mine, full, ranges, rank, world, dst, group=None):
@@ -313,6 +464,16 @@ class RcclGather:
         rank lists them in the same order); on the given (or current) stream."""
         s = device.stream_ptr(stream)
         I64 = ctypes.c_int64 * self.world
+        # every item's layout checked before the RCCL group opens (a failure inside
+        # it would leave the peers' halves of the group posted)
+        for mine, full, ranges, dst in items:
+            if not 0 <= dst < self.world:
+                raise ValueError("gather root %d of world %d" % (dst, self.world))
+            for k in CHANNELS:
+                if len(ranges[k]) != self.world or any(b < a for a, b in ranges[k]):
+                    raise ValueError("channel %s: bad receive layout %r" % (k, ranges[k]))
+                if self.rank == dst and (full is None or len(full[k]) != len(mine[k])):
+                    raise ValueError("channel %s: the root needs a receive buffer per sent tensor" % k)
         _lib.call("hic_gather_group_begin")
         try:
             for mine, full, ranges, dst in items:

@@ -261,6 +261,10 @@ int hic_rle_encode_i16(const int16_t *blocks, int64_t nblk, int block_len, int m
 int hic_rle_encode_i16_tiles(const int16_t *blocks, int64_t nblk, int max_len, const int64_t *d_stitch,
                              int32_t *dc_diff, uint8_t *sym_len, int16_t *sym_val, int64_t sym_cap,
                              int64_t *d_count, void *workspace, void *stream);
+/* The tile records hic_rle_encode_i16_tiles reads (one per 64-block tile, into
+ * `workspace`) of int16 zig-zag blocks of 64 (16-byte aligned) that a transform
+ * did not record: codec.run_length_coding's per-tile state (codec.py:55-99). */
+int hic_rle_tile_records_i16(const int16_t *blocks, int64_t nblk, int max_len, void *workspace, void *stream);
 /* hic_rle_encode_i16_tiles for up to 4 streams (e.g. the Y, Cr, Cb planes of one
  * image) in two launches in total; all with the same max_len. */
 typedef struct {
@@ -368,6 +372,27 @@ size_t hic_huffman_decode_workspace_bytes(int64_t nbits, int32_t nnodes, int32_t
 int hic_huffman_decode(const uint8_t *d_bits, int64_t nbits, const int32_t *h_child, int32_t nnodes,
                        const int32_t *h_values, int32_t nleaves, int32_t *d_out, int64_t out_cap,
                        int64_t *h_count, void *workspace, void *stream);
+
+/* ---- the gather's wire format (no reference counterpart: the bytes that carry a
+ *      shard's quantized zig-zag blocks -- codec.jpeg_encode's input after
+ *      dct_channel, codec.py:286-301 -- to the gathering rank, losslessly).  A block
+ *      is 835 bits: the DC slot as 16 bits, the 63 AC slots as 13-bit two's
+ *      complement (|q| <= 2048 for hiccup's orthonormal DCT and tables >= 1); a
+ *      64-block tile is 1670 little-endian 32-bit words.
+ *  hic_wire_bytes: the wire size of nblk blocks (whole tiles).
+ *  hic_wire_pack_i16: blocks (nblk x 64 int16, 16-byte aligned) -> wire; *d_flag
+ *    (device int, caller-zeroed) becomes 1 if an AC value lies outside 13 bits
+ *    (then the wire is not lossless: send the raw blocks).
+ *  hic_wire_unpack_i16: wire -> blocks (the inverse; nblk as packed).
+ *  hic_rle_records_rebase: nrec RLE tile records (3 int64: first / last nonzero
+ *    stream position or -1, symbol count) copied to d_dst with pos_shift added to
+ *    the positions: a shard's records placed in the whole image's record array
+ *    (pos_shift = the shard's first block x 63; its records must start on a
+ *    record boundary of the whole image). */
+size_t hic_wire_bytes(int64_t nblk);
+int hic_wire_pack_i16(const int16_t *blocks, int64_t nblk, uint8_t *wire, int *d_flag, void *stream);
+int hic_wire_unpack_i16(const uint8_t *wire, int64_t nblk, int16_t *blocks, void *stream);
+int hic_rle_records_rebase(const int64_t *d_src, int64_t nrec, int64_t pos_shift, int64_t *d_dst, void *stream);
 
 /* ---- Multi-GPU gather over RCCL (SURVEY.md section 8(b) hic_gather_*; the
  *      whole-image buffers it reassembles are what codec.jpeg_encode consumes,

@@ -5,7 +5,9 @@ stitch record with sharding.stitch_host, run-length codes its slice, and rank 0
 reassembles (a) the coefficient blocks + DC stream with sharding.gather_blocks --
 the same grouped batch_isend_irecv code the RCCL path runs; (a') a group of
 `world` images' gathers, image j to rank j, goes out as one batch
-(sharding.gather_blocks_group, the bench's exchange) -- and (b) the symbol
+(sharding.gather_blocks_group, the bench's exchange); (a'') the stream gather:
+blocks in the 13-bit wire format (tests/wire_host.py) to the receiving rank, which
+codes the whole stream -- and (b) the symbol
 streams with point-to-point sends.  Both must equal the single-stream encode.
 (c) Each rank then decodes its own slice (sharded decode: carried-zero skip, DC
 chain from the stitch record, pyrUp halo rows from sharding.exchange_halo_rows)
@@ -70,6 +72,19 @@ def _rle_stitched(zz, st):
     return diff, L, V
 
 
+def _wire_ranges_host(ranges):
+    """sharding.wire_ranges without records and without the library (CPU test)."""
+    import wire_host
+    out = {}
+    for k in pipeline.CHANNELS:
+        o, rr = 0, []
+        for b0, b1 in ranges[k]:
+            rr.append((o, o + wire_host.wire_bytes(b1 - b0)))
+            o = rr[-1][1]
+        out[k] = rr
+    return out
+
+
 def _worker(rank, world, port, H, W, flat, results):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -130,6 +145,43 @@ def _worker(rank, world, port, H, W, flat, results):
             np.array_equal(fj[k][0].numpy(), zz[k].astype(np.int16) + rank)
             and np.array_equal(fj[k][1].numpy(), orc.dpcm(zz[k][:, 0].astype(np.int64)).astype(np.int32) - rank)
             for k in pipeline.CHANNELS)
+        # (a'') the stream gather (gather_kind "stream", the bench's default): every
+        # rank ships its blocks in the 13-bit wire format (host restatement of
+        # hic_wire_pack_i16) into the byte ranges of sharding.wire_ranges, image j to
+        # rank j in one batch (sharding.gather_blocks_group, the code the GPU path
+        # runs); the receiver unpacks, codes the WHOLE stream and must get the
+        # single-stream encode
+        import wire_host
+        rpt = {k: 1 for k in pipeline.CHANNELS}
+        wr = sharding.wire_ranges(ranges, rpt, False)  # hic_wire_bytes: host code, no GPU
+        assert wr == _wire_ranges_host(ranges)
+        items = []
+        for j in range(world):
+            mine_w = {k: (torch.from_numpy(wire_host.pack(mine[k] + j if j else mine[k]).copy()),)
+                      for k in pipeline.CHANNELS}
+            full_w = ({k: (torch.zeros(wr[k][-1][1], dtype=torch.uint8),) for k in pipeline.CHANNELS}
+                      if rank == j else None)
+            items.append((mine_w, full_w, wr, j))
+        sharding.gather_blocks_group(items, rank, world)
+        full_w = items[rank][1]
+        ok = True
+        for k in pipeline.CHANNELS:
+            parts = []
+            for r in range(world):
+                b0, b1 = ranges[k][r]
+                if r == rank:
+                    parts.append(mine[k] + rank if rank else mine[k])
+                else:
+                    o0, o1 = wr[k][r]
+                    parts.append(wire_host.unpack(full_w[k][0][o0:o1].numpy(), b1 - b0).astype(np.int64))
+            whole = np.concatenate(parts)
+            want = zz[k] + rank if rank else zz[k]
+            ok &= np.array_equal(whole, want)
+            L, V = orc.rle_encode(whole[:, 1:].reshape(-1), 15)
+            eL, eV = orc.rle_encode(want[:, 1:].reshape(-1), 15)
+            ok &= np.array_equal(L, eL) and np.array_equal(V, eV)
+            ok &= np.array_equal(orc.dpcm(whole[:, 0]), orc.dpcm(want[:, 0]))
+        results["stream_%d" % rank] = bool(ok)
         # (c) the sharded decode: this rank's stream slice -> blocks (carried zeros
         # skipped, DC chain from the previous shard), inverse DCT of its block rows,
         # pyrUp halo rows from the neighbours (sharding.exchange_halo_rows, the code
@@ -202,4 +254,5 @@ def test_sharded_exchange_gloo(world, H, W, flat):
     exp.update({"blocks_" + k: True for k in pipeline.CHANNELS})
     exp.update({"decode_%d" % r: True for r in range(world)})
     exp.update({"group_%d" % r: True for r in range(world)})
+    exp.update({"stream_%d" % r: True for r in range(world)})
     assert dict(results) == exp

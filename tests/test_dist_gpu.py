@@ -8,7 +8,9 @@ the whole image bit for bit.  Each rank then decodes its own slice
 (ShardDecoder, halo rows over the process group) and its RGB rows must equal the
 single-GPU decode's.  Finally `world` images are encoded and gathered as the
 bench's strong mode does it (image j to rank j, one grouped batch), and each
-rank's received image must equal its single-GPU encode."""
+rank's received image must equal its single-GPU encode: the int16 block gather
+(gather_kind "blocks") and the stream gather (gather_kind "stream": wire-format
+blocks + rebased tile records, the whole stream coded on the receiving rank)."""
 import os
 import socket
 import tempfile
@@ -107,6 +109,18 @@ def _rank(rank, world, port, H, W, flat_rows, out_path):
         if rank == 0:
             gok &= all(np.array_equal(got_j[k][0], refs[j][k][1]) and np.array_equal(got_j[k][1], refs[j][k][2])
                        and np.array_equal(got_j[k][2], refs[j][k][3]) for k in pipeline.CHANNELS)
+    # the stream gather (the bench's default): ranks only transform, ship wire-format
+    # blocks + rebased tile records; the receiving rank codes the whole stream
+    sss = [sharding.ShardEncoder(H, W, rank=rank, world=world, gather_to=j, gather_kind="stream")
+           for j in range(world)]
+    sharding.encode_group(sss, [device.to_device(img[a:b]) for img in imgs], stream=s)
+    wholes = sharding.gather_streams_group(sss, group=xgroup, stream=s)
+    torch.cuda.synchronize()
+    got_w = wholes[rank].result()
+    gok &= all(np.array_equal(got_w[k][i], ref[k][i]) for k in pipeline.CHANNELS for i in range(4))
+    gok &= all(wholes[j] is None for j in range(world) if j != rank)
+    gok &= all(int(e.wire_flag.item()) == 0 for e in sss)
+    gok &= sss[rank].records == sharding.records_aligned(sss[rank].ranges, sss[rank].enc.rpt)
     goks = [None] * world
     dist.all_gather_object(goks, bool(gok))
     if rank == 0 and not all(goks):
@@ -117,7 +131,8 @@ def _rank(rank, world, port, H, W, flat_rows, out_path):
 
 
 @pytest.mark.parametrize("world,H,W,flat", [(2, 256, 384, None), (3, 4320 // 4, 7680 // 2, None),
-                                            (3, 384, 256, (120, 264))])
+                                            (3, 384, 256, (120, 264)), (2, 256, 1024, None),
+                                            (3, 4320 // 4, 7680, None)])
 def test_sharded_encode_multiprocess(world, H, W, flat):
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "result")
@@ -193,6 +208,14 @@ def _rccl_rank(rank, port, H, W, out_path):
         ok = False
     except ValueError:
         pass
+    # the stream gather through the C-ABI transport (world 1: the whole image is
+    # this rank's own shard; its records are rebased, the whole stream coded here)
+    ss = sharding.ShardEncoder(H, W, rank=0, world=1, gather_to=0, gather_kind="stream")
+    sharding.encode_group([ss], [device.to_device(rgb)], stream=s)
+    whole_s = sharding.gather_streams_group([ss], group=xgroup, rccl=g, stream=s)[0]
+    torch.cuda.synchronize()
+    got_s = whole_s.result()
+    ok &= all(np.array_equal(got_s[k][i], ref[k][i]) for k in pipeline.CHANNELS for i in range(4))
     g.close()
     with open(out_path, "w") as f:
         f.write("ok" if ok else "mismatch")

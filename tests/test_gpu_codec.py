@@ -612,6 +612,44 @@ def test_huffman_decode_device_full_size():
     assert torch.equal(out[:n], keys)
 
 
+@pytest.mark.parametrize("nblk", [1, 63, 64, 65, 777, 129600])
+def test_wire_pack_unpack(nblk):
+    """The gather's wire format: hic_wire_pack_i16 == the host restatement
+    (tests/wire_host.py, which the CPU gloo test of the stream gather uses),
+    unpack inverts it, the 13-bit range check raises the flag, and
+    hic_rle_records_rebase shifts record positions (-1 kept)."""
+    import wire_host
+    rng = np.random.default_rng(nblk)
+    blocks = rng.integers(-4096, 4096, (nblk, 64)).astype(np.int16)
+    blocks[:, 0] = rng.integers(-32768, 32768, nblk)
+    blocks[rng.random((nblk, 64)) < 0.5] = 0
+    lib = _lib.load()
+    nb = lib.hic_wire_bytes(nblk)
+    assert nb == wire_host.wire_bytes(nblk)
+    b = device.to_device(blocks)
+    wire = device.empty((nb,), torch.uint8)
+    flag = device.zeros((1,), torch.int32)
+    _lib.call("hic_wire_pack_i16", device.ptr(b), nblk, device.ptr(wire), device.ptr(flag), device.stream_ptr())
+    got = device.to_host(wire)
+    np.testing.assert_array_equal(got, wire_host.pack(blocks))
+    assert int(flag.item()) == 0
+    back = device.empty((nblk, 64), torch.int16)
+    _lib.call("hic_wire_unpack_i16", device.ptr(wire), nblk, device.ptr(back), device.stream_ptr())
+    np.testing.assert_array_equal(device.to_host(back), blocks)
+    bad = blocks.copy()
+    bad[nblk // 2, 7] = 4096
+    _lib.call("hic_wire_pack_i16", device.ptr(device.to_device(bad)), nblk, device.ptr(wire), device.ptr(flag),
+              device.stream_ptr())
+    assert int(flag.item()) == 1
+    rec = rng.integers(-1, 10 ** 6, (nblk, 3)).astype(np.int64)
+    out = device.empty((nblk, 3), torch.int64)
+    _lib.call("hic_rle_records_rebase", device.ptr(device.to_device(rec)), nblk, 1234567, device.ptr(out),
+              device.stream_ptr())
+    exp = rec.copy()
+    exp[:, :2] = np.where(rec[:, :2] >= 0, rec[:, :2] + 1234567, rec[:, :2])
+    np.testing.assert_array_equal(device.to_host(out), exp)
+
+
 def test_huffman_device_streams_batch_equals_single():
     """huffman.DeviceStreams (the batched form codec.jpeg_encode and
     Encoder.hic_image use) == one DeviceStream per stream: trees and packed bits,

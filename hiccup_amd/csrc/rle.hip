@@ -616,6 +616,7 @@ struct RleJobs16 {
   int n;
   int M;
   int64_t total_tiles;
+  uint32_t epoch;  // the scan launch's hand-off epoch (its failure granule's tag)
 };
 
 // Multi-workgroup scan for the batched hot path: each channel's tiles are cut
@@ -734,7 +735,10 @@ __global__ __launch_bounds__(kScanT) void k_rle_scan16b(RleJobs16 jobs, uint32_t
     }
     *J.d_count = total <= J.cap ? total : -total;
   }
-  if (s_fail && threadIdx.x == 0) *J.d_count = HIC_COUNT_SCAN_TIMEOUT;  // hand-off timed out: report, do not hang
+  // a hand-off that timed out is reported, not waited for: a tagged failure granule
+  // after the partitions' ones, folded into *d_count by the emit (which runs after
+  // every partition's write, so the report cannot be overwritten by a total)
+  if (s_fail && threadIdx.x == 0) put_granule(gran + 3 * np, 1, tag);
 }
 
 #ifndef HIC_EMIT_COAL
@@ -748,6 +752,13 @@ __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   const int M = jobs.M;
+  if (blockIdx.x == 0 && threadIdx.x < jobs.n) {  // the scan's failure report (sticky)
+    const RleJob16 &J = jobs.j[threadIdx.x];
+    const int64_t np = (J.nrec + kScanT - 1) / kScanT;
+    int64_t f;
+    if (get_granule(reinterpret_cast<const uint64_t *>(J.ws + 5 * J.nrec) + 3 * np, (jobs.epoch << 2) | 1u, f))
+      *J.d_count = HIC_COUNT_SCAN_TIMEOUT;
+  }
   int64_t g = (int64_t)blockIdx.x * 4 + wv;
   if (g >= jobs.total_tiles) return;  // wave-uniform
   struct Next {
@@ -1333,6 +1344,7 @@ int encode_batch16(RleJobs16 &jobs, hipStream_t s) {
   const uint32_t ep = (epoch.fetch_add(1) % ((1u << 30) - 1)) + 1;  // never 0 (zeroed workspace)
   int64_t nparts = 0;
   for (int k = 0; k < jobs.n; ++k) nparts += (jobs.j[k].nrec + kScanT - 1) / kScanT;
+  jobs.epoch = ep;
   hipLaunchKernelGGL(k_rle_scan16b, dim3((unsigned)nparts), dim3(kScanT), 0, s, jobs, ep);
   if (int e = check_launch("k_rle_scan16b")) return e;
   // persistent: 3 workgroups (12 waves) per CU fit the 51 KB LDS stage and the registers

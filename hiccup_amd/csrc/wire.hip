@@ -5,13 +5,13 @@
 // of int16 blocks; 16-byte aligned tiles).  Bit i of a tile is bit (i & 31) of its
 // word i >> 5 (LSB first).
 //
-// Why 13 bits lose nothing: an AC coefficient of hiccup's orthonormal 8x8 DCT-II
-// (transform.py:67-84) of pixels - 128 is bounded by 128 * (sum |c_u(x)|) *
-// (sum |c_v(y)|) <= 128 * 4 * 4 = 2048 (every 1-D basis entry is at most 1/2 in
-// magnitude), and the quantizer divides by a table entry >= 1
-// (quantization.py:47-52), so |q| <= 2048 < 4096.  The pack kernel still checks
-// every value and raises *d_flag for one outside [-4096, 4095] (the caller then
-// sends the raw blocks).  The DC (a 16-bit zig-zag slot) is carried whole.
+// Why 13 bits lose nothing: hiccup's dct2 (transform.py:67-84) is scipy's
+// unnormalised DCT-II along both axes, y = 4 sum x cos cos over pixels - 128, so
+// |y| <= 4 * 128 * 8 * 8 = 32768, and both quantisation tables
+// (quantization.py:14-44) have every entry >= 10, so |q| <= 3277 < 4096 (the
+// largest reachable value is ~2141, luminance (0, 2)).  The pack kernel still
+// checks every value and raises *d_flag for one outside [-4096, 4095] (the caller
+// then sends the raw blocks).  The DC (a 16-bit zig-zag slot) is carried whole.
 //
 //  hic_wire_pack_i16:   nblk blocks (64 int16, ZIGZAG_I16) -> ceil(nblk / 64) tiles
 //  hic_wire_unpack_i16: the inverse (blocks past nblk in the last tile dropped)

@@ -139,7 +139,12 @@ class Encoder:
         ev = (dct_events.start, dct_events.stop) if dct_events is not None else (None, None)
         if self.fused:
             # colour + pyrDown + DCT/quantize/zig-zag of the three planes + RLE tile
-            # records in ONE launch (dct_events time it)
+            # records in ONE launch (dct_events time it).  The kernel addresses its
+            # input rows with 32-bit offsets: hand it the span it reads (< 2 GiB by
+            # can_fuse) when the caller passes more rows
+            a, b = self.input_span()
+            if rgb.shape[0] * self.W * 3 > 2**31 - 1 and in_row0 <= a and in_row0 + rgb.shape[0] >= b:
+                rgb, in_row0 = rgb[a - in_row0:b - in_row0], a
             _lib.call("hic_encode420_u8", device.ptr(rgb), in_row0, rgb.shape[0], self.H, self.W, r0, r1 - r0,
                       *[device.ptr(self.coef[k]) for k in CHANNELS], *[device.ptr(self.ws[k]) for k in CHANNELS],
                       self.max_len, s, *ev)

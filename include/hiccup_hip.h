@@ -377,8 +377,9 @@ int hic_huffman_decode(const uint8_t *d_bits, int64_t nbits, const int32_t *h_ch
  *      shard's quantized zig-zag blocks -- codec.jpeg_encode's input after
  *      dct_channel, codec.py:286-301 -- to the gathering rank, losslessly).  A block
  *      is 835 bits: the DC slot as 16 bits, the 63 AC slots as 13-bit two's
- *      complement (|q| <= 2048 for hiccup's orthonormal DCT and tables >= 1); a
- *      64-block tile is 1670 little-endian 32-bit words.
+ *      complement (|q| <= 32768 / 10: hiccup's unnormalised DCT, table entries
+ *      >= 10); a 64-block tile is 1670 little-endian 32-bit words at a stride of
+ *      1672 (6688 B, 16-byte aligned).
  *  hic_wire_bytes: the wire size of nblk blocks (whole tiles).
  *  hic_wire_pack_i16: blocks (nblk x 64 int16, 16-byte aligned) -> wire; *d_flag
  *    (device int, caller-zeroed) becomes 1 if an AC value lies outside 13 bits

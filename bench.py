@@ -225,10 +225,11 @@ def extra_4k_rgb_encode(steps=40, n_streams=2):
 
 def extra_uhd_rgb_encode(steps=40, n_streams=2):
     """3840 x 2160 (UHD: W % 512 != 0, the fused kernel's ragged last strip) full
-    encode, fused against the two-kernel chain on the same inputs."""
+    encode, fused against the two-kernel chain (the default for such widths) on the
+    same inputs."""
     out = {"workload": "3840x2160 RGB -> YCrCb 4:2:0 full encode, 1 GPU, %d streams (fused: ragged last strip, "
                        "tile records by a tile pass; chain: colour kernel + plane DCT)" % n_streams}
-    out["fused"] = extra_rgb_encode(2160, 3840, steps, n_streams)
+    out["fused"] = extra_rgb_encode(2160, 3840, steps, n_streams, fused=True)
     out["two_kernel_chain"] = extra_rgb_encode(2160, 3840, steps, n_streams, fused=False)
     return out
 

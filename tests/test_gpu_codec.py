@@ -279,9 +279,9 @@ def _oracle_encode(rgb):
 @pytest.mark.parametrize("H,W", [(64, 96), (4320, 7680), (250, 330), (512, 768), (512, 1024), (272, 1536),
                                  (2160, 3840), (1088, 1920), (32, 16)])
 def test_pipeline_encoder(H, W):
-    """The device encoder vs the C oracle; W and H multiples of 16 run the fused
-    kernel (hic_encode420_u8; W % 512 != 0: a ragged last strip), the others the
-    two-kernel chain."""
+    """The device encoder vs the C oracle, on its default path (fused when W % 512
+    == 0 and H % 16 == 0, else the two-kernel chain) and, for any W, H multiples of
+    16, on the fused kernel (W % 512 != 0: a ragged last strip)."""
     rng = np.random.default_rng(H)
     rgb = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
     if H in (250, 272):
@@ -289,17 +289,21 @@ def test_pipeline_encoder(H, W):
     if H == 512:  # few grey levels: exact quantiser ties on the fast DCT path
         rgb = (rng.integers(0, 4, (H, W, 1)) * 85).astype(np.uint8).repeat(3, 2)
     enc = pipeline.Encoder(H, W)
-    assert enc.fused == (W % 16 == 0 and H % 16 == 0)
-    enc.encode(device.to_device(rgb))
-    got = enc.result()
+    assert enc.fused == (W % 512 == 0 and H % 16 == 0)
     exp = _oracle_encode(rgb)
-    for k in pipeline.CHANNELS:
-        zz, dc, L, V = got[k]
-        ezz, edc, eL, eV = exp[k]
-        np.testing.assert_array_equal(zz.astype(np.int32), ezz, err_msg=k)
-        np.testing.assert_array_equal(dc, edc, err_msg=k)
-        np.testing.assert_array_equal(L.astype(np.int32), eL, err_msg=k)
-        np.testing.assert_array_equal(V.astype(np.int32), eV, err_msg=k)
+    variants = [enc] + ([pipeline.Encoder(H, W, fused=True)] if (W % 16 == 0 and H % 16 == 0 and not enc.fused)
+                        else [])
+    for e in variants:
+        e.encode(device.to_device(rgb))
+        got_e = e.result()
+        for k in pipeline.CHANNELS:
+            zz, dc, L, V = got_e[k]
+            ezz, edc, eL, eV = exp[k]
+            np.testing.assert_array_equal(zz.astype(np.int32), ezz, err_msg=(k, e.fused))
+            np.testing.assert_array_equal(dc, edc, err_msg=(k, e.fused))
+            np.testing.assert_array_equal(L.astype(np.int32), eL, err_msg=(k, e.fused))
+            np.testing.assert_array_equal(V.astype(np.int32), eV, err_msg=(k, e.fused))
+    got = enc.result()
     # decode back through the device chain: equals the oracle's inverse
     dec = pipeline.Decoder(H, W)
     dev = {k: (device.to_device(got[k][2]), device.to_device(got[k][3]), device.to_device(got[k][1]))

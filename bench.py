@@ -364,26 +364,34 @@ def extra_16k_roundtrip(steps=4):
     g = torch.Generator(device="cuda")
     g.manual_seed(5)
     xs = [torch.randint(0, 256, (n, n, 3), dtype=torch.uint8, device="cuda", generator=g) for _ in range(2)]
-    enc, dec = pipeline.Encoder(n, n), pipeline.Decoder(n, n)
+    enc, dec = pipeline.Encoder(n, n, index=True), pipeline.Decoder(n, n)
 
-    def trip(i):
+    def trip(i, indexed):
         enc.encode(xs[i % 2])
+        if indexed:  # encoder-side tile index, counts stay on the device: no host sync
+            return dec.decode(enc.sym_len, enc.sym_val, enc.counts, enc.dc, index=enc.index)
         counts = enc.counts.cpu().tolist()
         return dec.decode(enc.sym_len, enc.sym_val, counts, enc.dc)
 
-    trip(0)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(steps):
-        out = trip(1 + i)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / steps
+    res = {}
+    for indexed in (True, False):
+        trip(0, indexed)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            out = trip(1 + i, indexed)
+        torch.cuda.synchronize()
+        res[indexed] = (time.perf_counter() - t0) / steps
+        dec.check_status()
+    dt = res[True]
     x = xs[steps % 2]
     mse = float(((out.float() - x.float()) ** 2).mean())
     del xs, enc, dec
     torch.cuda.empty_cache()
-    return {"workload": "16384x16384 RGB encode + decode round trip, 1 GPU (BASELINE configs[4] at N=1)",
+    return {"workload": "16384x16384 RGB encode + decode round trip, 1 GPU (BASELINE configs[4] at N=1); decode "
+                        "from the encoder-side tile index (hic_rle_decode_i16_indexed)",
             "ms_per_roundtrip": round(dt * 1e3, 3), "mpix_s": round(n * n / dt / 1e6, 1),
+            "ms_per_roundtrip_unindexed_decode": round(res[False] * 1e3, 3),
             "psnr_db_vs_input": round(10 * np.log10(255.0 ** 2 / mse), 3), "timed_roundtrips": steps}
 
 

@@ -1459,6 +1459,118 @@ int rle_decode_blocks16(const uint8_t *sym_len, const int16_t *sym_val, int64_t 
   return check_launch("k_rld_status");
 }
 
+// ---------------------------------------------------------------------------
+// Encoder-side tile index and the indexed decode.  After the scan, the RLE
+// workspace holds for every record its stream offset and the last nonzero AC
+// position before it; the index keeps, per 64-block tile, {offset of the tile's
+// first symbol, last nonzero position before the tile (-1: none), DC of the block
+// before the tile}.  With it a decoder needs no symbol-tile pass, no scans and no
+// DC chain: one wave per coefficient tile walks exactly the symbols the encoder's
+// emit wrote for that tile (codec.decode_run_length, codec.py:102-113, restricted
+// to the tile's positions; utils.invert_differences, utils.py:66-73, from the
+// previous block's DC).
+__global__ __launch_bounds__(256) void k_rle_index16(const int64_t *__restrict__ offs, int rshift, int64_t ntiles,
+                                                     const int16_t *__restrict__ blocks, int64_t *__restrict__ index) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= ntiles) return;
+  const int64_t r = t << rshift;
+  index[3 * t] = offs[2 * r];
+  index[3 * t + 1] = offs[2 * r + 1];
+  index[3 * t + 2] = t > 0 ? (int64_t)blocks[(t * 64 - 1) * 64] : 0;
+}
+
+constexpr int kIS = 8;  // symbols per lane per step (512 per wave step)
+template <bool NT>
+__global__ __launch_bounds__(256) void k_rld_indexed16(const uint8_t *__restrict__ sym_len,
+                                                       const int16_t *__restrict__ sym_val,
+                                                       const int64_t *__restrict__ d_nsym,
+                                                       const int32_t *__restrict__ dc_diff, int64_t nblk,
+                                                       const int64_t *__restrict__ index, int16_t *__restrict__ blocks,
+                                                       int64_t *__restrict__ d_status) {
+  __shared__ uint4 s_tile[4][64 * 8];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t ntiles = (nblk + 63) / 64;
+  const int64_t t = (int64_t)blockIdx.x * 4 + wv;
+  if (t >= ntiles) return;  // wave-uniform
+  uint4 *tile = s_tile[wv];
+  int16_t *win = reinterpret_cast<int16_t *>(tile);
+  // the encoder's symbol count, read on the device (no host round trip); a failed
+  // encode's count (< 1) decodes nothing and reports status -1
+  const int64_t nsym_raw = *d_nsym, nsym = nsym_raw > 0 ? nsym_raw : 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) tile[64 * k + lane] = make_uint4(0, 0, 0, 0);
+  __builtin_amdgcn_wave_barrier();
+  const int64_t o0 = index[3 * t] < nsym ? index[3 * t] : nsym;
+  const int64_t o1 = t + 1 < ntiles ? (index[3 * (t + 1)] < nsym ? index[3 * (t + 1)] : nsym) : nsym;
+  const int64_t tb0 = t * 64 * 63;                    // the tile's first AC position
+  const int nvb = (int)(nblk - t * 64 < 64 ? nblk - t * 64 : 64);
+  const int span = nvb * 63;                           // its AC positions
+  // P: position of the current step's first run, relative to the tile
+  int64_t P = index[3 * t + 1] + 1 - tb0;
+  for (int64_t c = o0 & ~(int64_t)(kIS - 1); c < o1; c += 64 * kIS) {
+    const int64_t s0 = c + (int64_t)lane * kIS;
+    int len[kIS], val[kIS];
+    if (s0 >= o0 && s0 + kIS <= o1) {
+      const uint2 l = *reinterpret_cast<const uint2 *>(sym_len + s0);
+      const uint4 v = *reinterpret_cast<const uint4 *>(sym_val + s0);
+      const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < kIS; ++k) {
+        len[k] = (int)(((k < 4 ? l.x : l.y) >> (8 * (k & 3))) & 255);
+        val[k] = (int)(int16_t)(vw[k >> 1] >> (16 * (k & 1)));
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kIS; ++k) {
+        const bool in = s0 + k >= o0 && s0 + k < o1;
+        len[k] = in ? (int)sym_len[s0 + k] : -1;  // -1: not this tile's symbol
+        val[k] = in ? (int)sym_val[s0 + k] : 0;
+      }
+    }
+    int acc = 0;
+#pragma unroll
+    for (int k = 0; k < kIS; ++k) acc += len[k] + 1;
+    const int incl = wave_incl_sum_i32(acc);
+    int64_t q = P + (incl - acc);
+#pragma unroll
+    for (int k = 0; k < kIS; ++k) {
+      if (len[k] >= 0) {
+        q += len[k];
+        if (q >= 0 && q < span) {  // fillers of a run carried in land before the tile
+          const int qi = (int)q, b = qi / 63;
+          win[b * 64 + 1 + (qi - b * 63)] = (int16_t)val[k];
+        }
+        ++q;
+      }
+    }
+    P += wave_last_i32(incl);
+  }
+  // DC: the previous block's value plus this tile's differences
+  const int64_t b = t * 64 + lane;
+  const int d = lane < nvb ? dc_diff[b] : 0;
+  win[lane * 64] = (int16_t)(index[3 * t + 2] + wave_incl_sum_i32(d));
+  __builtin_amdgcn_wave_barrier();
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int ci = 64 * k + lane, bb = ci >> 3;
+    if (bb < nvb) {
+      const uint4 x = tile[ci];
+      u32x4 *o = reinterpret_cast<u32x4 *>(blocks + t * 64 * 64) + ci;
+      if (NT)
+        __builtin_nontemporal_store(u32x4{x.x, x.y, x.z, x.w}, o);
+      else
+        *o = u32x4{x.x, x.y, x.z, x.w};
+    }
+  }
+  if (t == ntiles - 1 && lane == 0) {
+    // codec.decode_run_length's length: an EOB zero-fills to the end
+    const int64_t total = tb0 + P, n_ac = nblk * 63;
+    const bool eob = nsym > 0 && sym_len[nsym - 1] == 0 && sym_val[nsym - 1] == 0;
+    *d_status = nsym_raw < 1 ? -1 : ((eob && total <= n_ac) ? n_ac : total);
+  }
+}
+
 }  // namespace
 }  // namespace hic
 
@@ -1546,6 +1658,37 @@ extern "C" int hic_rle_encode_i16_tiles_batch(int n, const hic_rle_job16 *jobs, 
                       static_cast<int64_t *>(a.workspace), 0, 0, 0, a.records_per_tile == 2 ? 1 : 0};
   }
   return encode_batch16(J, as_stream(stream));
+}
+
+extern "C" int hic_rle_tile_index_i16(const int16_t *blocks, int64_t nblk, int records_per_tile, const void *workspace,
+                                      int64_t *d_index, void *stream) {
+  if (!blocks || !workspace || !d_index) return arg_error("null pointer");
+  if (nblk <= 0) return arg_error("nblk");
+  if (records_per_tile != 1 && records_per_tile != 2) return arg_error("records_per_tile must be 1 or 2");
+  const int64_t ntiles = (nblk + kWT - 1) / kWT, nrec = (nblk * records_per_tile + kWT - 1) / kWT;
+  const int64_t *offs = static_cast<const int64_t *>(workspace) + 3 * nrec;
+  hipLaunchKernelGGL(k_rle_index16, dim3((unsigned)((ntiles + 255) / 256)), dim3(256), 0, as_stream(stream), offs,
+                     records_per_tile == 2 ? 1 : 0, ntiles, blocks, d_index);
+  return check_launch("k_rle_index16");
+}
+
+extern "C" int hic_rle_decode_i16_indexed(const uint8_t *sym_len, const int16_t *sym_val, const int64_t *d_nsym,
+                                          const int32_t *dc_diff, int64_t nblk, const int64_t *d_index,
+                                          int16_t *blocks, int64_t *d_status, void *stream) {
+  if (!sym_len || !sym_val || !d_nsym || !dc_diff || !d_index || !blocks || !d_status) return arg_error("null pointer");
+  if (nblk <= 0 || nblk * 63 >= ((int64_t)1 << 31)) return arg_error("nblk");
+  if ((reinterpret_cast<uintptr_t>(sym_len) | reinterpret_cast<uintptr_t>(sym_val) |
+       reinterpret_cast<uintptr_t>(blocks)) % 16)
+    return arg_error("symbol arrays and blocks must be 16-byte aligned");
+  const int64_t ntiles = (nblk + 63) / 64;
+  const dim3 grid((unsigned)((ntiles + 3) / 4)), block(256);
+  if (knob(HIC_KNOB_RLD_NT) == 1)
+    hipLaunchKernelGGL(k_rld_indexed16<true>, grid, block, 0, as_stream(stream), sym_len, sym_val, d_nsym, dc_diff, nblk,
+                       d_index, blocks, d_status);
+  else
+    hipLaunchKernelGGL(k_rld_indexed16<false>, grid, block, 0, as_stream(stream), sym_len, sym_val, d_nsym, dc_diff,
+                       nblk, d_index, blocks, d_status);
+  return check_launch("k_rld_indexed16");
 }
 
 extern "C" int hic_rle_shard_summary_records(const int16_t *blocks, int64_t nblk, int records_per_tile,

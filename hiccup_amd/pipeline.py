@@ -61,7 +61,7 @@ class Encoder:
     """rows=(r0, r1) makes this encoder one row-shard of an H x W image (r0 even;
     shards of one image split at multiples of 16 rows so chroma blocks align)."""
 
-    def __init__(self, H, W, max_len=15, rows=None, out=None, fused=None):
+    def __init__(self, H, W, max_len=15, rows=None, out=None, fused=None, index=False):
         """out: optional {channel: (coef (n, 64) int16, dc (n,) int32)} device views the
         encoder writes into (a gathering rank points them at its slice of the whole
         image's buffers, so its own shard needs no copy).
@@ -78,6 +78,7 @@ class Encoder:
         if r0 % 2 or not (0 <= r0 < r1 <= H):
             raise ValueError("bad row range %r" % ((r0, r1),))
         self.rows = (r0, r1)
+        self.want_index = bool(index)
         a, b = input_span(H, r0, r1)
         # (hic_encode420_u8 reads the input rows through 32-bit buffer offsets)
         can_fuse = (W % 16 == 0 and H % 16 == 0 and r0 % 16 == 0 and r1 % 16 == 0
@@ -122,6 +123,10 @@ class Encoder:
             self.sym_len[k] = device.empty((self.cap[k],), torch.uint8)
             self.sym_val[k] = device.empty((self.cap[k],), torch.int16)
             self.ws[k] = device.workspace(lib.hic_rle_workspace_bytes(n, 64))
+        # index=True: the encoder-side tile index a device decoder reads
+        # (Decoder.decode(..., index=enc.index)): 3 int64 per 64-block tile
+        self.index = ({k: device.empty((3 * -(-self.coef[k].shape[0] // 64),), torch.int64) for k in CHANNELS}
+                      if self.want_index else None)
 
     @property
     def pixels(self):
@@ -186,6 +191,10 @@ class Encoder:
                                     self.sym_len[k].data_ptr(), self.sym_val[k].data_ptr(), self.cap[k],
                                     self.counts[i:i + 1].data_ptr(), self.ws[k].data_ptr(), self.rpt[k])
         _lib.call("hic_rle_encode_i16_tiles_batch", 3, jobs, self.max_len, s)
+        if self.index is not None and stitch is None:
+            for k in CHANNELS:
+                _lib.call("hic_rle_tile_index_i16", device.ptr(self.coef[k]), self.coef[k].shape[0], self.rpt[k],
+                          device.ptr(self.ws[k]), device.ptr(self.index[k]), s)
 
     def encode(self, rgb, stream=None, dct_events=None):
         self.transform(rgb, stream, dct_events=dct_events)
@@ -251,19 +260,28 @@ class Decoder:
         self.rgb = device.empty((2 * (H // 2), 2 * (W // 2), 3), torch.uint8)
         self._ws = {}
 
-    def decode(self, sym_len, sym_val, counts, dc, stream=None):
-        """sym_len/sym_val/dc: {channel: device tensor}; counts: host ints per channel."""
+    def decode(self, sym_len, sym_val, counts, dc, stream=None, index=None):
+        """sym_len/sym_val/dc: {channel: device tensor}; counts: host ints per channel.
+        index: an Encoder(index=True)'s tile index ({channel: device tensor}); then
+        counts is the encoder's device count tensor (3,) and nothing crosses to the
+        host (hic_rle_decode_i16_indexed: no tile pass, scans or DC chain)."""
         s = device.stream_ptr(stream)
         lib = _lib.load()
         for i, k in enumerate(CHANNELS):
             h, w = self.shapes[k]
             n = self.blocks[k].shape[0]
-            nsym = int(counts[i])
-            need = lib.hic_rld_workspace_bytes(nsym, n)
-            if k not in self._ws or self._ws[k].numel() * 8 < need:
-                self._ws[k] = device.workspace(need)
-            _lib.call("hic_rle_decode_i16", device.ptr(sym_len[k]), device.ptr(sym_val[k]), nsym, device.ptr(dc[k]), n,
-                      64, device.ptr(self.blocks[k]), device.ptr(self.status[i:i + 1]), device.ptr(self._ws[k]), s)
+            if index is not None:
+                _lib.call("hic_rle_decode_i16_indexed", device.ptr(sym_len[k]), device.ptr(sym_val[k]),
+                          ctypes.c_void_p(counts.data_ptr() + 8 * i), device.ptr(dc[k]), n, device.ptr(index[k]),
+                          device.ptr(self.blocks[k]), device.ptr(self.status[i:i + 1]), s)
+            else:
+                nsym = int(counts[i])
+                need = lib.hic_rld_workspace_bytes(nsym, n)
+                if k not in self._ws or self._ws[k].numel() * 8 < need:
+                    self._ws[k] = device.workspace(need)
+                _lib.call("hic_rle_decode_i16", device.ptr(sym_len[k]), device.ptr(sym_val[k]), nsym,
+                          device.ptr(dc[k]), n, 64, device.ptr(self.blocks[k]), device.ptr(self.status[i:i + 1]),
+                          device.ptr(self._ws[k]), s)
             _lib.call("hic_dequant_idct_u8", device.ptr(self.blocks[k]), _lib.LAYOUT_ZIGZAG_I16, h, w, TABLES[k],
                       device.ptr(self.pix[k]), self.pix[k].stride(0), s)
         h, w = self.shapes["cr"]

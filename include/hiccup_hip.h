@@ -314,6 +314,23 @@ size_t hic_rld_workspace_bytes(int64_t nsym, int64_t nblk);
 int hic_rle_decode_i16(const uint8_t *sym_len, const int16_t *sym_val, int64_t nsym,
                        const int32_t *dc_diff, int64_t nblk, int block_len, int16_t *blocks,
                        int64_t *d_status, void *workspace, void *stream);
+/* Encoder-side tile index (no reference counterpart: it lets a device-to-device
+ * decoder skip the symbol-tile pass, the scans and the DC chain that find block
+ * boundaries in a bare stream).  hic_rle_tile_index_i16: after
+ * hic_rle_encode_i16_tiles[_batch] (its workspace holds the scan's offsets), per
+ * 64-block tile t: d_index[3t] = offset of the tile's first symbol, [3t + 1] = the
+ * stream's last nonzero AC position before the tile (-1: none), [3t + 2] = DC of
+ * block 64t - 1 (0 for t = 0).  records_per_tile as the encode job's.
+ * hic_rle_decode_i16_indexed: hic_rle_decode_i16's result (codec.py:102-113,
+ * 397-421 for one channel, 64-slot int16 blocks) from such an index: one wave per
+ * 64-block tile; *d_status as hic_rle_decode_i16's (-1 when *d_nsym < 1).
+ * Whole streams only (no stitch).  d_nsym: the symbol count on the device (the
+ * encoder's d_count, EOB included): no host round trip between encode and decode. */
+int hic_rle_tile_index_i16(const int16_t *blocks, int64_t nblk, int records_per_tile, const void *workspace,
+                           int64_t *d_index, void *stream);
+int hic_rle_decode_i16_indexed(const uint8_t *sym_len, const int16_t *sym_val, const int64_t *d_nsym,
+                               const int32_t *dc_diff, int64_t nblk, const int64_t *d_index, int16_t *blocks,
+                               int64_t *d_status, void *stream);
 /* One tile shard's slice of the channel stream (the sharded decode of
  * codec.jpeg_decode, codec.py:397-425): d_stitch is the shard's device record from
  * hic_rle_stitch {carry zeros, closes the stream, has previous DC, previous DC}.

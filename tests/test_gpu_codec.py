@@ -323,6 +323,29 @@ def test_pipeline_encoder(H, W):
     np.testing.assert_array_equal(rgb2, exp_rgb)
 
 
+@pytest.mark.parametrize("kind", ["random", "levels", "blocks", "flat"])
+@pytest.mark.parametrize("H,W", [(64, 96), (512, 1024), (272, 1536), (1088, 1920), (4320, 7680), (16, 16)])
+def test_indexed_decode(H, W, kind):
+    """Encoder(index=True) + Decoder.decode(index=...): one wave per 64-block
+    tile from the encoder-side index, counts read on the device -- the blocks and
+    RGB equal the plain decode's, the status equals nblk * 63, on fused (half-tile
+    chroma records) and two-kernel-chain encoders, with empty tiles and long
+    carried runs (flat)."""
+    rgb = _structured_rgb(kind, H, W, H * 7 + W)
+    enc = pipeline.Encoder(H, W, index=True)
+    enc.encode(device.to_device(rgb))
+    counts = enc.counts.cpu().tolist()
+    d1, d2 = pipeline.Decoder(H, W), pipeline.Decoder(H, W)
+    r1 = d1.decode(enc.sym_len, enc.sym_val, counts, enc.dc)
+    r2 = d2.decode(enc.sym_len, enc.sym_val, enc.counts, enc.dc, index=enc.index)
+    torch.cuda.synchronize()
+    for k in pipeline.CHANNELS:
+        assert torch.equal(d2.blocks[k], enc.coef[k]), k
+        assert torch.equal(d1.blocks[k], d2.blocks[k]), k
+    assert d2.status.cpu().tolist() == [enc.coef[k].shape[0] * 63 for k in pipeline.CHANNELS]
+    assert torch.equal(r1, r2)
+
+
 def _structured_rgb(kind, H, W, seed):
     rng = np.random.default_rng(seed)
     if kind == "random":
@@ -389,7 +412,7 @@ def test_16k_roundtrip_vs_oracle():
     H = W = 16384
     rng = np.random.default_rng(5)
     rgb = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
-    enc = pipeline.Encoder(H, W)
+    enc = pipeline.Encoder(H, W, index=True)
     enc.encode(device.to_device(rgb))
     counts = enc.counts.cpu().tolist()
     nblk = {k: enc.coef[k].shape[0] for k in pipeline.CHANNELS}
@@ -403,6 +426,14 @@ def test_16k_roundtrip_vs_oracle():
     for k in pipeline.CHANNELS:
         assert torch.equal(dec.blocks[k], enc.coef[k]), k
     rec = device.to_host(rec_dev)
+    # the indexed decode (encoder-side tile index, device counts): the same
+    dec2 = pipeline.Decoder(H, W)
+    rec2 = dec2.decode(enc.sym_len, enc.sym_val, enc.counts, enc.dc, index=enc.index)
+    assert dec2.status.cpu().tolist() == [nblk[k] * 63 for k in pipeline.CHANNELS]
+    for k in pipeline.CHANNELS:
+        assert torch.equal(dec2.blocks[k], enc.coef[k]), k
+    assert torch.equal(rec2, rec_dev)
+    del dec2, rec2
     del enc, dec, rec_dev
     torch.cuda.empty_cache()
     y, cr, cb = orcc.rgb_to_ycrcb(rgb)
@@ -475,6 +506,13 @@ def test_shards_stitch_to_single_stream(H, W, world, flat):
         d.check_status()
         a, b = d.out_rows
         np.testing.assert_array_equal(got, exp[a:b], err_msg="rank %d" % r)
+
+
+@pytest.mark.timeout(600)
+def test_shards_stitch_16k():
+    """BASELINE configs[4]'s size (16384 x 16384) over 8 shards: sharded encode
+    == the whole stream, every shard's decode == its rows of the whole decode."""
+    test_shards_stitch_to_single_stream(16384, 16384, 8, None)
 
 
 def test_two_stream_overlap_matches_single_stream():

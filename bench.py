@@ -440,6 +440,31 @@ def _extra_8k_jpeg_decode(steps, codec, device, hicimage, pipeline):
             "timed_decodes": steps}
 
 
+def measure_link(rank, world, group=None, nbytes=256 << 20, reps=5):
+    """The xGMI rate between rank 0 and rank 1, measured in this run: rank 0 sends
+    `nbytes` to rank 1 while rank 1 sends the same to rank 0 (one batch per
+    repetition, RCCL on the default stream), median of `reps` after one warmup.
+    Every rank joins the barriers; only ranks 0 and 1 move data.  Returns GB/s per
+    direction (None off ranks 0/1)."""
+    buf_s = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    buf_r = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    times = []
+    for i in range(reps + 1):
+        dist.barrier(group=group)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if rank in (0, 1):
+            peer = 1 - rank
+            ops = [dist.P2POp(dist.isend, buf_s, peer, group=group), dist.P2POp(dist.irecv, buf_r, peer, group=group)]
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        torch.cuda.synchronize()
+        if i:
+            times.append(time.perf_counter() - t0)
+    del buf_s, buf_r
+    return round(nbytes / float(np.median(times)) / 1e9, 1) if rank in (0, 1) else None
+
+
 def extra_16k_roundtrip_sharded(rank, world, backend, steps=4):
     """BASELINE configs[4] at N ranks: a 16384 x 16384 random RGB image tile-sharded
     by block rows.  Each rank encodes its shard (ShardEncoder: colour with halo, DCT,
@@ -817,6 +842,10 @@ def main():
                              "(no gather); not the headline value"}
     per_rank_rows = in_rows if world == 1 else encs[0].rows[1] - encs[0].rows[0]
     extra_sharded = None
+    link_gbs = None
+    if world > 1 and args.dist_backend == "nccl" and not args.same_device:
+        # the per-link rate the gather model uses, measured here (not assumed)
+        link_gbs = measure_link(rank, world)
     if world > 1 and not args.no_extras:
         # free the 8K run's buffers first (every rank holds ~1.2 GB of inputs)
         del encs, inputs, enc0
@@ -871,6 +900,7 @@ def main():
                 if gather else None,
                 "gather_us_per_image": None if gather_us is None else round(gather_us, 2),
                 "gather_link": gather_link,
+                "xgmi_link_gbs_measured": link_gbs,
                 "without_gather": no_gather,
                 "symbols_per_image_rank0": symbols,
                 "stream_ends_on": "the gathering rank (whole-image scan + emit)" if stream_gather else

@@ -35,6 +35,23 @@ def test_ctypes_signatures_match_header():
         nargs = 0 if args.strip() == "void" else len([a for a in args.split(",") if a.strip()])
         assert nargs == len(_lib.SIGNATURES[name][1]), name
     assert _lib.load().hic_abi_version() == 2
+    # argument kinds: every pointer parameter is bound as a pointer, every scalar
+    # with the header's width and signedness
+    kinds = {"int64_t": ctypes.c_int64, "int": ctypes.c_int, "int32_t": ctypes.c_int32, "size_t": ctypes.c_size_t,
+             "uint32_t": ctypes.c_uint32, "float": ctypes.c_float}
+    for name, args in decl.items():
+        if args.strip() == "void":
+            continue
+        for i, (a, t) in enumerate(zip(args.split(","), _lib.SIGNATURES[name][1])):
+            a = " ".join(a.split())
+            if "*" in a:
+                assert t in (ctypes.c_void_p, ctypes.c_char_p) or hasattr(t, "_type_") and t._type_ == "P" \
+                    or issubclass(t, ctypes._Pointer) or t.__name__.startswith("LP_") or \
+                    t.__name__.endswith("_Array"), (name, i, a, t)
+            else:
+                base = a.rsplit(" ", 1)[0].replace("const ", "")
+                assert base in kinds, (name, i, a)
+                assert ctypes.sizeof(t) == ctypes.sizeof(kinds[base]) and t not in (ctypes.c_void_p,), (name, i, a, t)
 
 
 def test_last_error_roundtrip():

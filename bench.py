@@ -79,9 +79,6 @@ def parse():
                     help="rehearsal on a 1-GPU box: every rank on cuda:0 (use with --dist-backend gloo)")
     ap.add_argument("--streams", type=int, default=2,
                     help="HIP streams the consecutive images alternate over (each image's chain stays on one)")
-    ap.add_argument("--cu-split", type=float, default=0.0, metavar="F",
-                    help="N=1 experiment: transform on a stream masked to a fraction F of the CUs, scan + emit on "
-                         "a stream over the rest (producer / consumer CU split); 0 = off")
     ap.add_argument("--unfused", action="store_true",
                     help="A/B: colour and DCT as two kernels (the planes round-trip HBM) instead of hic_encode420_u8")
     ap.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
@@ -644,16 +641,6 @@ def main():
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(args.streams - 1)]
     torch.cuda.synchronize()  # inputs / buffers were made on the current stream
 
-    cu_split = args.cu_split > 0 and world == 1
-    if cu_split:
-        # producer / consumer split of the CUs: image i's transform runs on stream A
-        # (a fraction of the CUs) while image i-1's scan + emit run on stream B (the
-        # rest); an encoder's buffers are reused only after its previous emit
-        s_a, s_b, cu_handles = device.cu_split_streams(args.cu_split)  # noqa: F841 (kept alive)
-        t_done = [torch.cuda.Event() for _ in encs]
-        e_done = [torch.cuda.Event() for _ in encs]
-        e_used = [False] * len(encs)
-
     exch_done = [None] * len(encs)  # event: the gather of the encoder's last image completed
     pending = []  # (encoder index, input, DCT events) of the group being collected
     n_groups = [0]
@@ -700,19 +687,6 @@ def main():
         if record and (i - args.warmup) % 4 == 0:
             ev = event_pool[len(timed_events)]
             timed_events.append(ev)
-        if cu_split:
-            k = i % len(encs)
-            if e_used[k]:
-                s_a.wait_event(e_done[k])
-            with torch.cuda.stream(s_a):
-                e.transform(x, dct_events=ev)
-                t_done[k].record(s_a)
-            s_b.wait_event(t_done[k])
-            with torch.cuda.stream(s_b):
-                e.entropy()
-                e_done[k].record(s_b)
-            e_used[k] = True
-            return
         if gather:
             pending.append((i % len(encs), x, ev))
             if len(pending) == world:
@@ -792,7 +766,7 @@ def main():
     dct_us = float(np.mean([ev.elapsed_ms() for ev in timed_events])) * 1e3
     roof_note = "timed region (every 4th step)"
     dct_us_overlapped = None
-    if len(streams) > 1 or gather or cu_split:
+    if len(streams) > 1 or gather:
         # with images overlapped on several streams (or a gather in the step) the DCT
         # shares the chip with other kernels, so its launch duration is no longer its
         # own: the roofline kernel is timed apart, on the same encoders and inputs,
@@ -890,7 +864,6 @@ def main():
                 "per_rank_rows": per_rank_rows,
                 "mode": "single" if world == 1 else args.mode,
                 "streams": args.streams,
-                "cu_split": args.cu_split if cu_split else None,
                 "gather": "image j of each group of %d to rank j, one grouped RCCL batch per group (%s)"
                           % (world, "torch.distributed P2P" if rgather is None else "C-ABI hic_gather_bytes")
                           if gather else None,

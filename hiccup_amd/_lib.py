@@ -46,10 +46,8 @@ SIGNATURES = {
     "hic_last_error": (_int, [ctypes.c_char_p, _sz]),
     "hic_device_count": (_int, [ctypes.POINTER(_int)]),
     "hic_stream_sync": (_int, [_vp]),
-    "hic_stream_create_cu_mask": (_int, [_vp, _int, _vp]),
     "hic_probe_copy": (_int, [_vp, _vp, _i64, _int, _vp, _vp, _vp]),
     "hic_probe_plane": (_int, [_vp, _i64, _i64, _vp, _int, _vp, _vp, _vp]),
-    "hic_stream_destroy": (_int, [_vp]),
     "hic_set_knob": (_int, [_int, _int]),
     "hic_get_knob": (_int, [_int, ctypes.POINTER(_int)]),
     "hic_dct_quant_u8": (_int, [_vp, _i64, _i64, _i64, _int, _int, _vp, _vp]),
@@ -168,8 +166,7 @@ def call(name, *args):
 
 # A/B knobs (include/hiccup_hip.h HIC_KNOB_*): every selectable path is bit-exact
 KNOBS = {"dct_path": 0, "dct_waves_per_cu": 1, "color_tiled": 2, "color_seg": 3, "color_nt": 4, "rle_nt": 5,
-         "rld_nt": 6, "rld_generic": 7, "dev": 8, "encode_waves": 9, "encode_nt": 10, "encode_dct": 11,
-         "encode_lds_pad": 12, "encode_xcd": 13}
+         "rld_nt": 6, "rld_generic": 7, "dev": 8, "encode_waves": 9, "encode_nt": 10, "encode_dct": 11}
 DCT_PATH_PK, DCT_PATH_F32, DCT_PATH_F64, DCT_PATH_F64_NOPF, DCT_PATH_EXACT = 4, 3, 1, 2, 0
 
 

@@ -7,7 +7,7 @@ namespace hic {
 static thread_local char g_last_error[512] = "";
 
 // hic_set_knob values (-1 = default; read by the launchers on every call)
-static int g_knobs[HIC_KNOB_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+static int g_knobs[HIC_KNOB_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 int knob(int k) {
   const int v = g_knobs[k];
   if (v >= 0) return v;
@@ -51,20 +51,6 @@ extern "C" int hic_stream_sync(void *stream) {
   return hic::hip_status(hipStreamSynchronize(hic::as_stream(stream)), "hipStreamSynchronize");
 }
 
-extern "C" int hic_stream_create_cu_mask(const uint32_t *h_mask, int nwords, void **h_stream) {
-  if (!h_mask || !h_stream || nwords <= 0) return hic::arg_error("null pointer / mask size");
-  hipStream_t s = nullptr;
-  const int rc = hic::hip_status(hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, h_mask),
-                                 "hipExtStreamCreateWithCUMask");
-  *h_stream = rc == HIC_OK ? (void *)s : nullptr;
-  return rc;
-}
-
-extern "C" int hic_stream_destroy(void *stream) {
-  if (!stream) return hic::arg_error("null stream");
-  return hic::hip_status(hipStreamDestroy((hipStream_t)stream), "hipStreamDestroy");
-}
-
 extern "C" int hic_event_create(void **h_event) {
   if (!h_event) return hic::arg_error("null pointer");
   hipEvent_t e = nullptr;
@@ -91,8 +77,6 @@ extern "C" int hic_set_knob(int k, int value) {
     return hic::arg_error("dct path %d (0 exact, 1 float64 AAN, 2 float64 AAN unpipelined, 3 float32, 4 packed float32)", value);
   if (k == HIC_KNOB_COLOR_SEG && value != -1 && value != 8 && value != 16) return hic::arg_error("colour segment");
   if (k == HIC_KNOB_ENCODE_WAVES && value != -1 && value != 2 && value != 3) return hic::arg_error("encode waves");
-  if (k == HIC_KNOB_ENCODE_XCD && value != -1 && value != 0 && value != 1) return hic::arg_error("encode xcd");
-  if (k == HIC_KNOB_ENCODE_LDS_PAD && value > 64) return hic::arg_error("encode LDS pad %d KiB (0..64)", value);
   if (value < -1) return hic::arg_error("knob value %d", value);
 #ifndef HIC_DEV
   if (k == HIC_KNOB_DEV && value > 0) return hic::arg_error("the dev knob needs a -DHIC_DEV build");

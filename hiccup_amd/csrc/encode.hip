@@ -54,7 +54,6 @@ struct Enc420 {
   int M;
   int nstrips, nunits;  // nunits: waves (HIC_ENC_VG unit rows each)
   int wlast;            // pixel columns of the last strip (16 .. 512)
-  int xcd;              // 1: workgroups remapped to a contiguous band of units per XCD
 };
 
 constexpr int kZZ = HIC_LAYOUT_ZIGZAG_I16;
@@ -527,17 +526,7 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
     __syncthreads();
   }
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // Workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8 share one,
-  // MI355X_MICROARCH.md "Workgroup dispatch"; for speed only, any placement is
-  // correct).  E.xcd: block b takes logical workgroup L so that each XCD's blocks
-  // are one contiguous run of units in raster order, i.e. a band of unit rows: the
-  // pyrDown halo rows a unit shares with the unit row above / below are then read
-  // by the same XCD at about the same time and served by its L2.
-  int b = blockIdx.x;
-  if (E.xcd) {
-    const int nwg = gridDim.x, per = nwg >> 3, rem = nwg & 7, x = b & 7, i = b >> 3;
-    b = x < rem ? x * (per + 1) + i : rem * (per + 1) + (x - rem) * per + i;
-  }
+  const int b = blockIdx.x;
   const int g = __builtin_amdgcn_readfirstlane(b * HIC_ENC_WPB + wv);
   if (g >= E.nunits) return;  // wave-uniform
   uint2 *st2 = s_stage + wv * 64 * kStageU2;
@@ -698,20 +687,16 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
   E.nstrips = (int)((W + 511) / 512);
   E.wlast = (int)(W - 512 * (int64_t)(E.nstrips - 1));
   E.nunits = E.nstrips * (int)((out_rows / 16 + HIC_ENC_VG - 1) / HIC_ENC_VG);  // waves
-  E.xcd = knob(HIC_KNOB_ENCODE_XCD) == 1;
   // one wave per unit (no persistent loop: units are the same size, and the
   // hardware's dispatch balances the tail better than a fixed split)
   const dim3 grid((unsigned)((E.nunits + HIC_ENC_WPB - 1) / HIC_ENC_WPB)), block(64 * HIC_ENC_WPB);
   hipStream_t s = as_stream(stream);
   hipEvent_t e0 = static_cast<hipEvent_t>(ev_start), e1 = static_cast<hipEvent_t>(ev_stop);
-  // knob encode_lds_pad: reserve extra LDS per workgroup (fewer encode workgroups
-  // per CU, room for a kernel of another stream beside them)
-  const size_t pad = (size_t)knob(HIC_KNOB_ENCODE_LDS_PAD) * 1024;
   auto launch = [&](auto kern) {
     if (e0 || e1)
-      hipExtLaunchKernelGGL(kern, grid, block, pad, s, e0, e1, 0, E);
+      hipExtLaunchKernelGGL(kern, grid, block, 0, s, e0, e1, 0, E);
     else
-      hipLaunchKernelGGL(kern, grid, block, pad, s, E);
+      hipLaunchKernelGGL(kern, grid, block, 0, s, E);
   };
   const bool w2 = knob(HIC_KNOB_ENCODE_WAVES) == 2, nt = knob(HIC_KNOB_ENCODE_NT) != 0;
   const int dm = knob(HIC_KNOB_ENCODE_DCT);

@@ -90,27 +90,3 @@ class KernelEvents:
         for e in (getattr(self, "start", None), getattr(self, "stop", None)):
             if e is not None and e.value:
                 self._lib.hic_event_destroy(e)
-
-
-def cu_split_streams(frac, n_cu=None):
-    """Two torch streams over complementary CU sets (hic_stream_create_cu_mask):
-    about `frac` of the CUs for the first, the rest for the second.  CU c goes to
-    the first set when (37 c mod n) < frac n, which spreads both sets over every XCD
-    whether the CU numbering is XCD-major or round-robin.  Returns (a, b, handles);
-    keep `handles` alive while the streams are in use."""
-    require_gpu()
-    lib = _lib.load()
-    n = n_cu or torch.cuda.get_device_properties(0).multi_processor_count
-    k = int(round(frac * n))
-    words = (n + 31) // 32
-    masks = [[0] * words, [0] * words]
-    for c in range(n):
-        side = 0 if (37 * c) % n < k else 1
-        masks[side][c // 32] |= 1 << (c % 32)
-    out = []
-    for m in masks:
-        arr = (ctypes.c_uint32 * words)(*m)
-        h = ctypes.c_void_p()
-        _lib.call("hic_stream_create_cu_mask", arr, words, ctypes.byref(h))
-        out.append(h)
-    return (torch.cuda.ExternalStream(out[0].value), torch.cuda.ExternalStream(out[1].value), out)

@@ -76,18 +76,11 @@ int hic_device_count(int *h_n);
 #define HIC_KNOB_ENCODE_WAVES 9     /* hic_encode420_u8: register budget for 2 (default) or 3 waves per SIMD */
 #define HIC_KNOB_ENCODE_NT 10       /* hic_encode420_u8: 1 = nontemporal coefficient stores (default 0: cached) */
 #define HIC_KNOB_ENCODE_DCT 11      /* hic_encode420_u8: 1 = scalar float32 AAN DCT, 2 = packed float32 AAN DCT (proven windows + in-place fallbacks; default 0: float64) */
-#define HIC_KNOB_ENCODE_LDS_PAD 12  /* hic_encode420_u8: KiB of extra LDS per workgroup (0..64; 40 leaves one encode workgroup per CU, the rest of the CU to a concurrent kernel) */
-#define HIC_KNOB_ENCODE_XCD 13     /* hic_encode420_u8: 1 = each XCD takes a contiguous band of unit rows (pyrDown halo rows re-read from its own L2), 0 = dispatch order */
-#define HIC_KNOB_COUNT 14
+#define HIC_KNOB_COUNT 12
 int hic_set_knob(int knob, int value);
 int hic_get_knob(int knob, int *h_value);
 /* Synchronises `stream`; returns HIC_ERR_HIP if an earlier async launch failed. */
 int hic_stream_sync(void *stream);
-/* A stream whose kernels run only on the CUs set in h_mask (nwords 32-bit words,
- * bit c = CU c; hipExtStreamCreateWithCUMask): the producer / consumer CU split
- * of bench.py --cu-split.  Destroy with hic_stream_destroy. */
-int hic_stream_create_cu_mask(const uint32_t *h_mask, int nwords, void **h_stream);
-int hic_stream_destroy(void *stream);
 
 /* ---- measurement probes (bench.py; no reference counterpart: SURVEY.md 8(d) asks
  *      for the box's device-copy bandwidth beside the roofline).  Memory-only, no

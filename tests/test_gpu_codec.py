@@ -368,7 +368,7 @@ def _structured_rgb(kind, H, W, seed):
 
 @pytest.mark.parametrize("variant", [{}, {"encode_dct": 1}, {"encode_waves": 3}, {"encode_dct": 1, "encode_waves": 3},
                                      {"encode_dct": 2}, {"encode_dct": 2, "encode_waves": 3}, {"encode_dct": 2, "encode_waves": 2},
-                                     {"encode_nt": 1}, {"encode_xcd": 0}, {"encode_xcd": 1}])
+                                     {"encode_nt": 1}])
 @pytest.mark.parametrize("kind", ["random", "levels", "colour_levels", "blocks", "flat"])
 @pytest.mark.parametrize("H,W", [(16, 512), (144, 2048), (1088, 1536)])
 def test_fused_encoder_matches_two_kernel_chain(kind, H, W, variant):

@@ -158,6 +158,56 @@ __device__ __forceinline__ double fma_scale_add(double y, double k_s, double c_v
   return d;
 }
 
+// Dequantize (q * T, exact in int32), the 2-D DCT-III in pocketfft's float64
+// operation order, /256 + 128, truncate, wrap, and store the 8x8 pixels of the
+// block at (y0, x0) of the H x W plane (FAST: whole block inside, 8-byte rows).
+template <int TABLE, bool FAST>
+__device__ __forceinline__ void idct_block_store(const int (&q)[64], int H, int W, int y0, int x0,
+                                                 uint8_t *__restrict__ out, int64_t ostride) {
+  // dequantize (q * T, exact in int32) and row pass
+  double a[8][8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    int c[8];
+#pragma unroll
+    for (int v = 0; v < 8; ++v) c[v] = q[u * 8 + v] * QT[TABLE][u * 8 + v];
+    idct8<int>(c, a[u]);
+  }
+  // column pass, /256 (exact) + 128, truncate toward zero, wrap mod 256.  The
+  // constants live in registers (2^-8 an SGPR pair, 128 a VGPR pair) for a
+  // three-address v_fma_f64: LLVM's v_fmac_f64 form overwrote its accumulator,
+  // so it re-materialised 128.0 (two v_mov_b32) before each of the 64 fmas
+  const double k2m8 = sreg_f64(0x1p-8), k128 = vreg_f64(128.0);
+  uint32_t px[16];  // row r: bytes v = 0..3 in px[2r], 4..7 in px[2r+1]
+#pragma unroll
+  for (int k = 0; k < 16; ++k) px[k] = 0;
+#pragma unroll
+  for (int v = 0; v < 8; ++v) {
+    double xc[8], yv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) xc[u] = a[u][v];
+    idct8<double>(xc, yv);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const double p = fma_scale_add(yv[r], k2m8, k128);  // == fl(y/256 + 128): y*2^-8 exact
+      const uint32_t b = (uint32_t)__double2int_rz(p) & 0xFFu;
+      px[2 * r + (v >> 2)] |= b << (8 * (v & 3));
+    }
+  }
+  if (FAST) {
+    uint8_t *o = out + (int64_t)y0 * ostride + x0;  // one 64-bit multiply; rows step by the uniform stride
+#pragma unroll
+    for (int r = 0; r < 8; ++r) *reinterpret_cast<uint2 *>(o + r * ostride) = make_uint2(px[2 * r], px[2 * r + 1]);
+  } else {
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int v = 0; v < 8; ++v)
+        if (y0 + r < H && x0 + v < W)
+          out[(int64_t)(y0 + r) * ostride + x0 + v] = (uint8_t)(px[2 * r + (v >> 2)] >> (8 * (v & 3)));
+  }
+}
+
 template <int TABLE, int LAYOUT, bool FAST>
 __global__ __launch_bounds__(256) void k_dequant_idct(const void *__restrict__ coef, int H, int W,
                                                       int nbx, int nblk, uint8_t *__restrict__ out,
@@ -218,48 +268,103 @@ __global__ __launch_bounds__(256) void k_dequant_idct(const void *__restrict__ c
     }
   }
 
-  // dequantize (q * T, exact in int32) and row pass
-  double a[8][8];
+  idct_block_store<TABLE, FAST>(q, H, W, y0, x0, out, ostride);
+}
+
+// Indexed decode fused with the inverse transform: one wave per 64-block tile
+// assembles its blocks in LDS from the symbols the encoder's tile index points at
+// (as k_rld_indexed16 in rle.hip), then every lane runs the dequantize + IDCT of
+// its block straight from LDS and stores pixels: the zig-zag blocks never reach
+// HBM (codec.jpeg_decode's RLE / DC half, codec.py:397-421, + inv_dct_channel,
+// transform.py:169-179, for one plane).
+constexpr int kRowI16 = 68;  // LDS block row: 64 slots + pad (136 B, conflict-free 8 B reads)
+constexpr int kDIS = 16;     // symbols per lane per step
+template <int TABLE, bool FAST>
+__global__ __launch_bounds__(256) void k_rld_idct_indexed(const uint8_t *__restrict__ sym_len,
+                                                          const int16_t *__restrict__ sym_val,
+                                                          const int64_t *__restrict__ d_nsym,
+                                                          const int32_t *__restrict__ dc_diff,
+                                                          const int64_t *__restrict__ index, int H, int W, int nbx,
+                                                          int64_t nblk, uint8_t *__restrict__ out, int64_t ostride,
+                                                          int64_t *__restrict__ d_status) {
+  __shared__ uint2 s_tile[4][64 * kRowI16 / 4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t ntiles = (nblk + 63) / 64;
+  const int64_t t = (int64_t)blockIdx.x * 4 + wv;
+  if (t >= ntiles) return;  // wave-uniform
+  uint2 *tile = s_tile[wv];
+  int16_t *win = reinterpret_cast<int16_t *>(tile);
+  const int64_t nsym_raw = *d_nsym, nsym = nsym_raw > 0 ? nsym_raw : 0;
+  for (int i = lane; i < 64 * kRowI16 / 4; i += 64) tile[i] = make_uint2(0, 0);
+  __builtin_amdgcn_wave_barrier();
+  const int64_t o0 = index[3 * t] < nsym ? index[3 * t] : nsym;
+  const int64_t o1 = t + 1 < ntiles ? (index[3 * (t + 1)] < nsym ? index[3 * (t + 1)] : nsym) : nsym;
+  const int64_t tb0 = t * 64 * 63;
+  const int nvb = (int)(nblk - t * 64 < 64 ? nblk - t * 64 : 64);
+  const int span = nvb * 63;
+  int P = (int)(index[3 * t + 1] + 1 - tb0);
+  for (int64_t c = o0 & ~(int64_t)(kDIS - 1); c < o1; c += 64 * kDIS) {
+    const int64_t s0 = c + (int64_t)lane * kDIS;
+    int len[kDIS], val[kDIS];
+    if (s0 >= o0 && s0 + kDIS <= o1) {
+      const uint4 l = *reinterpret_cast<const uint4 *>(sym_len + s0);
+      const uint4 v0 = *reinterpret_cast<const uint4 *>(sym_val + s0);
+      const uint4 v1 = *reinterpret_cast<const uint4 *>(sym_val + s0 + 8);
+      const uint32_t lw[4] = {l.x, l.y, l.z, l.w};
+      const uint32_t vw[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    int c[8];
+      for (int k = 0; k < kDIS; ++k) {
+        len[k] = (int)((lw[k >> 2] >> (8 * (k & 3))) & 255);
+        val[k] = (int)(int16_t)(vw[k >> 1] >> (16 * (k & 1)));
+      }
+    } else {
 #pragma unroll
-    for (int v = 0; v < 8; ++v) c[v] = q[u * 8 + v] * QT[TABLE][u * 8 + v];
-    idct8<int>(c, a[u]);
+      for (int k = 0; k < kDIS; ++k) {
+        const bool in = s0 + k >= o0 && s0 + k < o1;
+        len[k] = in ? (int)sym_len[s0 + k] : -1;
+        val[k] = in ? (int)sym_val[s0 + k] : 0;
+      }
+    }
+    int acc = 0;
+#pragma unroll
+    for (int k = 0; k < kDIS; ++k) acc += len[k] + 1;
+    const int incl = wave_incl_sum_i32(acc);
+    int q = P + (incl - acc);
+#pragma unroll
+    for (int k = 0; k < kDIS; ++k) {
+      q += len[k];
+      if (len[k] >= 0 && (unsigned)q < (unsigned)span) {
+        const int b = (q * 2081) >> 17;  // q / 63 on [0, 4032)
+        win[b * kRowI16 + 1 + (q - b * 63)] = (int16_t)val[k];
+      }
+      ++q;
+    }
+    P += wave_last_i32(incl);
   }
-  // column pass, /256 (exact) + 128, truncate toward zero, wrap mod 256.  The
-  // constants live in registers (2^-8 an SGPR pair, 128 a VGPR pair) for a
-  // three-address v_fma_f64: LLVM's v_fmac_f64 form overwrote its accumulator,
-  // so it re-materialised 128.0 (two v_mov_b32) before each of the 64 fmas
-  const double k2m8 = sreg_f64(0x1p-8), k128 = vreg_f64(128.0);
-  uint32_t px[16];  // row r: bytes v = 0..3 in px[2r], 4..7 in px[2r+1]
+  const int64_t blk = t * 64 + lane;
+  const int d = lane < nvb ? dc_diff[blk] : 0;
+  win[lane * kRowI16] = (int16_t)(index[3 * t + 2] + wave_incl_sum_i32(d));
+  __builtin_amdgcn_wave_barrier();
+  if (t == ntiles - 1 && lane == 0) {
+    const int64_t total = tb0 + (int64_t)P, n_ac = nblk * 63;
+    const bool eob = nsym > 0 && sym_len[nsym - 1] == 0 && sym_val[nsym - 1] == 0;
+    *d_status = nsym_raw < 1 ? -1 : ((eob && total <= n_ac) ? n_ac : total);
+  }
+  if (lane >= nvb) return;
+  int qv[64];  // raster [u][v]
+  {
+    const uint2 *row = tile + lane * (kRowI16 / 4);
 #pragma unroll
-  for (int k = 0; k < 16; ++k) px[k] = 0;
-#pragma unroll
-  for (int v = 0; v < 8; ++v) {
-    double xc[8], yv[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) xc[u] = a[u][v];
-    idct8<double>(xc, yv);
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const double p = fma_scale_add(yv[r], k2m8, k128);  // == fl(y/256 + 128): y*2^-8 exact
-      const uint32_t b = (uint32_t)__double2int_rz(p) & 0xFFu;
-      px[2 * r + (v >> 2)] |= b << (8 * (v & 3));
+    for (int k = 0; k < 16; ++k) {
+      const uint2 x = row[k];
+      qv[ZZ[4 * k]] = (int)(int16_t)(x.x & 0xFFFFu);
+      qv[ZZ[4 * k + 1]] = (int)(int16_t)(x.x >> 16);
+      qv[ZZ[4 * k + 2]] = (int)(int16_t)(x.y & 0xFFFFu);
+      qv[ZZ[4 * k + 3]] = (int)(int16_t)(x.y >> 16);
     }
   }
-  if (FAST) {
-    uint8_t *o = out + (int64_t)y0 * ostride + x0;  // one 64-bit multiply; rows step by the uniform stride
-#pragma unroll
-    for (int r = 0; r < 8; ++r) *reinterpret_cast<uint2 *>(o + r * ostride) = make_uint2(px[2 * r], px[2 * r + 1]);
-  } else {
-#pragma unroll
-    for (int r = 0; r < 8; ++r)
-#pragma unroll
-      for (int v = 0; v < 8; ++v)
-        if (y0 + r < H && x0 + v < W)
-          out[(int64_t)(y0 + r) * ostride + x0 + v] = (uint8_t)(px[2 * r + (v >> 2)] >> (8 * (v & 3)));
-  }
+  const int bi = (int)(blk / nbx), bj = (int)(blk - (int64_t)bi * nbx);
+  idct_block_store<TABLE, FAST>(qv, H, W, bi * 8, bj * 8, out, ostride);
 }
 
 // Production forward kernel for aligned planes: up to three planes per launch
@@ -1384,6 +1489,34 @@ extern "C" int hic_dequant_idct_u8(const void *coef, int layout, int64_t H, int6
   }
 #undef HIC_INV
   return arg_error("layout");
+}
+
+extern "C" int hic_rle_decode_idct_u8_indexed(const uint8_t *sym_len, const int16_t *sym_val, const int64_t *d_nsym,
+                                              const int32_t *dc_diff, const int64_t *d_index, int64_t H, int64_t W,
+                                              int table_id, uint8_t *out, int64_t out_stride, int64_t *d_status,
+                                              void *stream) {
+  if (!sym_len || !sym_val || !d_nsym || !dc_diff || !d_index || !out || !d_status) return arg_error("null pointer");
+  if (!dims_ok(H, W) || out_stride < W) return arg_error("plane shape / stride");
+  if (table_id != HIC_TABLE_LUMINANCE && table_id != HIC_TABLE_CHROMINANCE) return arg_error("table_id");
+  if ((reinterpret_cast<uintptr_t>(sym_len) | reinterpret_cast<uintptr_t>(sym_val)) % 16)
+    return arg_error("symbol arrays must be 16-byte aligned");
+  const int nbx = (int)((W + 7) / 8);
+  const int64_t nblk = (int64_t)nbx * ((H + 7) / 8);
+  if (nblk * 63 >= ((int64_t)1 << 31)) return arg_error("plane too large (AC stream >= 2^31)");
+  const bool fast = H % 8 == 0 && W % 8 == 0 && out_stride % 8 == 0 && aligned(out, 8);
+  const int64_t ntiles = (nblk + 63) / 64;
+  const dim3 grid((unsigned)((ntiles + 3) / 4)), block(256);
+  hipStream_t s = as_stream(stream);
+  const int h = (int)H, w = (int)W;
+#define HIC_RI(T, F)                                                                                              \
+  hipLaunchKernelGGL((k_rld_idct_indexed<T, F>), grid, block, 0, s, sym_len, sym_val, d_nsym, dc_diff, d_index, h, \
+                     w, nbx, nblk, out, out_stride, d_status)
+  if (table_id == 0 && fast) HIC_RI(0, true);
+  else if (table_id == 0) HIC_RI(0, false);
+  else if (fast) HIC_RI(1, true);
+  else HIC_RI(1, false);
+#undef HIC_RI
+  return check_launch("k_rld_idct_indexed");
 }
 
 extern "C" int hic_dct2_f64(const double *in, int64_t nblk, double *out, void *stream) {

@@ -1479,7 +1479,20 @@ __global__ __launch_bounds__(256) void k_rle_index16(const int64_t *__restrict__
   index[3 * t + 2] = t > 0 ? (int64_t)blocks[(t * 64 - 1) * 64] : 0;
 }
 
-constexpr int kIS = 8;  // symbols per lane per step (512 per wave step)
+constexpr int kIS = 16;  // symbols per lane per step (1024 per wave step)
+struct SymChunk {
+  uint4 l;     // 16 lengths
+  uint4 v[2];  // 16 values
+};
+__device__ __forceinline__ void load_chunk(const uint8_t *__restrict__ sym_len, const int16_t *__restrict__ sym_val,
+                                           int64_t s0, int64_t o0, int64_t o1, SymChunk &c, bool &whole) {
+  whole = s0 >= o0 && s0 + kIS <= o1;
+  if (whole) {
+    c.l = *reinterpret_cast<const uint4 *>(sym_len + s0);
+    c.v[0] = *reinterpret_cast<const uint4 *>(sym_val + s0);
+    c.v[1] = *reinterpret_cast<const uint4 *>(sym_val + s0 + 8);
+  }
+}
 template <bool NT>
 __global__ __launch_bounds__(256) void k_rld_indexed16(const uint8_t *__restrict__ sym_len,
                                                        const int16_t *__restrict__ sym_val,
@@ -1505,18 +1518,27 @@ __global__ __launch_bounds__(256) void k_rld_indexed16(const uint8_t *__restrict
   const int64_t tb0 = t * 64 * 63;                    // the tile's first AC position
   const int nvb = (int)(nblk - t * 64 < 64 ? nblk - t * 64 : 64);
   const int span = nvb * 63;                           // its AC positions
-  // P: position of the current step's first run, relative to the tile
-  int64_t P = index[3 * t + 1] + 1 - tb0;
-  for (int64_t c = o0 & ~(int64_t)(kIS - 1); c < o1; c += 64 * kIS) {
+  // P: position of the current step's first run, relative to the tile (a carried
+  // run can start far before it; every AC position of the stream fits int32)
+  int P = (int)(index[3 * t + 1] + 1 - tb0);
+  int64_t c = o0 & ~(int64_t)(kIS - 1);
+  SymChunk cur;
+  bool cur_whole;
+  if (c < o1) load_chunk(sym_len, sym_val, c + (int64_t)lane * kIS, o0, o1, cur, cur_whole);
+  for (; c < o1; c += 64 * kIS) {
+    // the next step's symbols load under this step's arithmetic
+    SymChunk nxt;
+    bool nxt_whole = false;
+    if (c + 64 * kIS < o1) load_chunk(sym_len, sym_val, c + 64 * kIS + (int64_t)lane * kIS, o0, o1, nxt, nxt_whole);
     const int64_t s0 = c + (int64_t)lane * kIS;
     int len[kIS], val[kIS];
-    if (s0 >= o0 && s0 + kIS <= o1) {
-      const uint2 l = *reinterpret_cast<const uint2 *>(sym_len + s0);
-      const uint4 v = *reinterpret_cast<const uint4 *>(sym_val + s0);
-      const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+    if (cur_whole) {
+      const uint32_t lw[4] = {cur.l.x, cur.l.y, cur.l.z, cur.l.w};
+      const uint32_t vw[8] = {cur.v[0].x, cur.v[0].y, cur.v[0].z, cur.v[0].w,
+                              cur.v[1].x, cur.v[1].y, cur.v[1].z, cur.v[1].w};
 #pragma unroll
       for (int k = 0; k < kIS; ++k) {
-        len[k] = (int)(((k < 4 ? l.x : l.y) >> (8 * (k & 3))) & 255);
+        len[k] = (int)((lw[k >> 2] >> (8 * (k & 3))) & 255);
         val[k] = (int)(int16_t)(vw[k >> 1] >> (16 * (k & 1)));
       }
     } else {
@@ -1531,19 +1553,21 @@ __global__ __launch_bounds__(256) void k_rld_indexed16(const uint8_t *__restrict
 #pragma unroll
     for (int k = 0; k < kIS; ++k) acc += len[k] + 1;
     const int incl = wave_incl_sum_i32(acc);
-    int64_t q = P + (incl - acc);
+    int q = P + (incl - acc);
 #pragma unroll
     for (int k = 0; k < kIS; ++k) {
-      if (len[k] >= 0) {
-        q += len[k];
-        if (q >= 0 && q < span) {  // fillers of a run carried in land before the tile
-          const int qi = (int)q, b = qi / 63;
-          win[b * 64 + 1 + (qi - b * 63)] = (int16_t)val[k];
-        }
-        ++q;
+      q += len[k];  // a masked symbol (len -1) leaves q unchanged after the ++ below
+      // fillers of a run carried in land before the tile; q / 63 = (q * 2081) >> 17
+      // on [0, 4032)
+      if (len[k] >= 0 && (unsigned)q < (unsigned)span) {
+        const int b = (q * 2081) >> 17;
+        win[b * 64 + 1 + (q - b * 63)] = (int16_t)val[k];
       }
+      ++q;
     }
     P += wave_last_i32(incl);
+    cur = nxt;
+    cur_whole = nxt_whole;
   }
   // DC: the previous block's value plus this tile's differences
   const int64_t b = t * 64 + lane;
@@ -1565,7 +1589,7 @@ __global__ __launch_bounds__(256) void k_rld_indexed16(const uint8_t *__restrict
   }
   if (t == ntiles - 1 && lane == 0) {
     // codec.decode_run_length's length: an EOB zero-fills to the end
-    const int64_t total = tb0 + P, n_ac = nblk * 63;
+    const int64_t total = tb0 + (int64_t)P, n_ac = nblk * 63;
     const bool eob = nsym > 0 && sym_len[nsym - 1] == 0 && sym_val[nsym - 1] == 0;
     *d_status = nsym_raw < 1 ? -1 : ((eob && total <= n_ac) ? n_ac : total);
   }

@@ -260,16 +260,25 @@ class Decoder:
         self.rgb = device.empty((2 * (H // 2), 2 * (W // 2), 3), torch.uint8)
         self._ws = {}
 
-    def decode(self, sym_len, sym_val, counts, dc, stream=None, index=None):
+    def decode(self, sym_len, sym_val, counts, dc, stream=None, index=None, keep_blocks=False):
         """sym_len/sym_val/dc: {channel: device tensor}; counts: host ints per channel.
         index: an Encoder(index=True)'s tile index ({channel: device tensor}); then
-        counts is the encoder's device count tensor (3,) and nothing crosses to the
-        host (hic_rle_decode_i16_indexed: no tile pass, scans or DC chain)."""
+        counts is the encoder's device count tensor (3,), nothing crosses to the
+        host, and each plane is decoded and inverse-transformed by ONE kernel
+        (hic_rle_decode_idct_u8_indexed: no tile pass, scans, DC chain or zig-zag
+        blocks in HBM); keep_blocks=True writes self.blocks too (the block-level
+        indexed decode, then the IDCT)."""
         s = device.stream_ptr(stream)
         lib = _lib.load()
         for i, k in enumerate(CHANNELS):
             h, w = self.shapes[k]
             n = self.blocks[k].shape[0]
+            if index is not None and not keep_blocks:
+                _lib.call("hic_rle_decode_idct_u8_indexed", device.ptr(sym_len[k]), device.ptr(sym_val[k]),
+                          ctypes.c_void_p(counts.data_ptr() + 8 * i), device.ptr(dc[k]), device.ptr(index[k]), h, w,
+                          TABLES[k], device.ptr(self.pix[k]), self.pix[k].stride(0),
+                          device.ptr(self.status[i:i + 1]), s)
+                continue
             if index is not None:
                 _lib.call("hic_rle_decode_i16_indexed", device.ptr(sym_len[k]), device.ptr(sym_val[k]),
                           ctypes.c_void_p(counts.data_ptr() + 8 * i), device.ptr(dc[k]), n, device.ptr(index[k]),

@@ -324,6 +324,15 @@ int hic_rle_tile_index_i16(const int16_t *blocks, int64_t nblk, int records_per_
 int hic_rle_decode_i16_indexed(const uint8_t *sym_len, const int16_t *sym_val, const int64_t *d_nsym,
                                const int32_t *dc_diff, int64_t nblk, const int64_t *d_index, int16_t *blocks,
                                int64_t *d_status, void *stream);
+/* hic_rle_decode_i16_indexed + hic_dequant_idct_u8 in ONE kernel: each wave
+ * assembles its 64-block tile in LDS and every lane inverts its block from there
+ * into the uint8 H x W plane `out` (row pitch out_stride): no zig-zag blocks in
+ * HBM.  The blocks are the plane's ((H+7)/8) x ((W+7)/8); table_id as
+ * hic_dequant_idct_u8; *d_status as hic_rle_decode_i16_indexed. */
+int hic_rle_decode_idct_u8_indexed(const uint8_t *sym_len, const int16_t *sym_val, const int64_t *d_nsym,
+                                   const int32_t *dc_diff, const int64_t *d_index, int64_t H, int64_t W,
+                                   int table_id, uint8_t *out, int64_t out_stride, int64_t *d_status,
+                                   void *stream);
 /* One tile shard's slice of the channel stream (the sharded decode of
  * codec.jpeg_decode, codec.py:397-425): d_stitch is the shard's device record from
  * hic_rle_stitch {carry zeros, closes the stream, has previous DC, previous DC}.

@@ -324,26 +324,37 @@ def test_pipeline_encoder(H, W):
 
 
 @pytest.mark.parametrize("kind", ["random", "levels", "blocks", "flat"])
-@pytest.mark.parametrize("H,W", [(64, 96), (512, 1024), (272, 1536), (1088, 1920), (4320, 7680), (16, 16)])
+@pytest.mark.parametrize("H,W", [(64, 96), (512, 1024), (272, 1536), (1088, 1920), (4320, 7680), (16, 16),
+                                 (250, 330), (37, 53)])
 def test_indexed_decode(H, W, kind):
     """Encoder(index=True) + Decoder.decode(index=...): one wave per 64-block
     tile from the encoder-side index, counts read on the device -- the blocks and
     RGB equal the plain decode's, the status equals nblk * 63, on fused (half-tile
     chroma records) and two-kernel-chain encoders, with empty tiles and long
     carried runs (flat)."""
+    if kind == "blocks" and (H % 8 or W % 8):
+        pytest.skip("the blocks image needs whole 8x8 blocks")
     rgb = _structured_rgb(kind, H, W, H * 7 + W)
     enc = pipeline.Encoder(H, W, index=True)
     enc.encode(device.to_device(rgb))
     counts = enc.counts.cpu().tolist()
-    d1, d2 = pipeline.Decoder(H, W), pipeline.Decoder(H, W)
+    d1, d2, d3 = pipeline.Decoder(H, W), pipeline.Decoder(H, W), pipeline.Decoder(H, W)
     r1 = d1.decode(enc.sym_len, enc.sym_val, counts, enc.dc)
-    r2 = d2.decode(enc.sym_len, enc.sym_val, enc.counts, enc.dc, index=enc.index)
+    r2 = d2.decode(enc.sym_len, enc.sym_val, enc.counts, enc.dc, index=enc.index, keep_blocks=True)
     torch.cuda.synchronize()
     for k in pipeline.CHANNELS:
         assert torch.equal(d2.blocks[k], enc.coef[k]), k
         assert torch.equal(d1.blocks[k], d2.blocks[k]), k
-    assert d2.status.cpu().tolist() == [enc.coef[k].shape[0] * 63 for k in pipeline.CHANNELS]
+    want = [enc.coef[k].shape[0] * 63 for k in pipeline.CHANNELS]
+    assert d2.status.cpu().tolist() == want
     assert torch.equal(r1, r2)
+    # the fused decode + IDCT (no blocks in HBM): the same planes and RGB
+    r3 = d3.decode(enc.sym_len, enc.sym_val, enc.counts, enc.dc, index=enc.index)
+    torch.cuda.synchronize()
+    for k in pipeline.CHANNELS:
+        assert torch.equal(d3.pix[k], d1.pix[k]), k
+    assert d3.status.cpu().tolist() == want
+    assert torch.equal(r1, r3)
 
 
 def _structured_rgb(kind, H, W, seed):
@@ -428,12 +439,15 @@ def test_16k_roundtrip_vs_oracle():
     rec = device.to_host(rec_dev)
     # the indexed decode (encoder-side tile index, device counts): the same
     dec2 = pipeline.Decoder(H, W)
-    rec2 = dec2.decode(enc.sym_len, enc.sym_val, enc.counts, enc.dc, index=enc.index)
+    rec2 = dec2.decode(enc.sym_len, enc.sym_val, enc.counts, enc.dc, index=enc.index, keep_blocks=True)
     assert dec2.status.cpu().tolist() == [nblk[k] * 63 for k in pipeline.CHANNELS]
     for k in pipeline.CHANNELS:
         assert torch.equal(dec2.blocks[k], enc.coef[k]), k
     assert torch.equal(rec2, rec_dev)
-    del dec2, rec2
+    rec3 = dec2.decode(enc.sym_len, enc.sym_val, enc.counts, enc.dc, index=enc.index)  # fused decode + IDCT
+    assert dec2.status.cpu().tolist() == [nblk[k] * 63 for k in pipeline.CHANNELS]
+    assert torch.equal(rec3, rec_dev)
+    del dec2, rec2, rec3
     del enc, dec, rec_dev
     torch.cuda.empty_cache()
     y, cr, cb = orcc.rgb_to_ycrcb(rgb)

@@ -392,7 +392,8 @@ def extra_16k_roundtrip(steps=4):
     del xs, enc, dec
     torch.cuda.empty_cache()
     return {"workload": "16384x16384 RGB encode + decode round trip, 1 GPU (BASELINE configs[4] at N=1); decode "
-                        "from the encoder-side tile index (hic_rle_decode_i16_indexed)",
+                        "from the encoder-side tile index, RLE decode + IDCT fused per plane "
+                        "(hic_rle_decode_idct_u8_indexed), no host sync between the halves",
             "ms_per_roundtrip": round(dt * 1e3, 3), "mpix_s": round(n * n / dt / 1e6, 1),
             "ms_per_roundtrip_unindexed_decode": round(res[False] * 1e3, 3),
             "psnr_db_vs_input": round(10 * np.log10(255.0 ** 2 / mse), 3), "timed_roundtrips": steps}

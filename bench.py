@@ -782,14 +782,14 @@ def main():
         # as in the timed region: back-to-back steps, the DCT timestamped on every
         # 4th (8 untimed steps first: the launches right after the overlapped region
         # run 5-15 % slow in the kernel trace, profiles/r01/bench_s2_kernel_trace_v9)
-        iso = [device.KernelEvents() for _ in range(4)]
+        iso = [device.KernelEvents() for _ in range(16)]
         for j in range(24):
-            ev = iso[(j - 8) // 4] if j >= 8 and j % 4 == 0 else None
+            ev = iso[j - 8] if j >= 8 else None
             encs[j % len(encs)].encode(inputs[j % nin], dct_events=ev)
         torch.cuda.synchronize()
-        dct_us = float(np.mean([ev.elapsed_ms() for ev in iso])) * 1e3
+        dct_us = float(np.median([ev.elapsed_ms() for ev in iso])) * 1e3
         timed_events = iso
-        roof_note = ("16 single-stream encodes (every 4th timestamped, after 8 untimed) right after the timed "
+        roof_note = ("median of 16 single-stream encodes (each timestamped, after 8 untimed) right after the timed "
                      "region; the timed region overlaps images on %d stream(s)%s"
                      % (len(streams), " and grouped gathers" if gather else ""))
     # algorithmic bytes of the timed launch: the two-kernel chain's DCT reads 1 B and

@@ -376,7 +376,7 @@ int hic_huffman_pack(const void *keys, int key_bytes, int64_t n, int32_t key_min
                      const uint64_t *d_code_bits, const uint8_t *d_code_len, uint8_t *out,
                      int64_t out_bytes, int64_t *d_nbits, void *workspace, void *stream);
 /* hic_huffman_decode: HuffmanTree.decode_data (huffman.py:149-178) of the nbits-bit
- *    MSB-first stream at d_bits (4-byte aligned; the payload bytes after
+ *    MSB-first stream at d_bits (4-byte aligned, ceil(nbits / 32) * 4 readable bytes; the payload bytes after
  *    iohelper's pad-length byte, iohelper.py:35-56) -- codec.jpeg_decode's nine
  *    huffman_data_decode calls (codec.py:372-388).  The tree is a host array:
  *    h_child[2n] / h_child[2n + 1] = node n's '1' (left) / '0' (right) child, >= 0

@@ -60,13 +60,13 @@ SIGNATURES = {
     "hic_key_range": (_int, [_vp, _int, _i64, _vp, _vp]),
     "hic_key_histogram": (_int, [_vp, _int, _i64, ctypes.c_int32, ctypes.c_int32, _vp, _vp, _vp]),
     "hic_huffman_pack_workspace_bytes": (_sz, [_i64]),
-    "hic_wire_bytes": (_sz, [_i64]),
+    "hic_wire_bytes": (_sz, [_i64, _int]),
     "hic_rle_decode_idct_u8_indexed": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _int, _vp, _i64, _vp, _vp]),
     "hic_rle_tile_index_i16": (_int, [_vp, _i64, _int, _vp, _vp, _vp]),
     "hic_rle_decode_i16_indexed": (_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp]),
     "hic_rle_tile_records_i16": (_int, [_vp, _i64, _int, _vp, _vp]),
-    "hic_wire_pack_i16": (_int, [_vp, _i64, _vp, _vp, _vp]),
-    "hic_wire_unpack_i16": (_int, [_vp, _i64, _vp, _vp]),
+    "hic_wire_pack_i16": (_int, [_vp, _i64, _int, _vp, _vp, _vp]),
+    "hic_wire_unpack_i16": (_int, [_vp, _i64, _int, _vp, _vp]),
     "hic_rle_records_rebase": (_int, [_vp, _i64, _i64, _vp, _vp]),
     "hic_huffman_decode_workspace_bytes": (_sz, [_i64, ctypes.c_int32, ctypes.c_int32]),
     "hic_huffman_decode": (_int, [_vp, _i64, _vp, ctypes.c_int32, _vp, ctypes.c_int32, _vp, _i64, _vp, _vp, _vp]),

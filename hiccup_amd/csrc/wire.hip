@@ -1,17 +1,14 @@
 // wire.hip -- the gather's lossless wire format for quantized zig-zag blocks
-// (DESIGN.md section 6): a block's DC as 16 bits and its 63 AC slots as 13-bit
-// two's complement, 835 bits per block, packed back to back, so a 64-block tile
-// is exactly 1670 32-bit words, stored at a stride of 1672 (6688 B against 8192 B
-// of int16 blocks; 16-byte aligned tiles).  Bit i of a tile is bit (i & 31) of its
-// word i >> 5 (LSB first).
-//
-// Why 13 bits lose nothing: hiccup's dct2 (transform.py:67-84) is scipy's
-// unnormalised DCT-II along both axes, y = 4 sum x cos cos over pixels - 128, so
-// |y| <= 4 * 128 * 8 * 8 = 32768, and both quantisation tables
-// (quantization.py:14-44) have every entry >= 10, so |q| <= 3277 < 4096 (the
-// largest reachable value is ~2141, luminance (0, 2)).  The pack kernel still
-// checks every value and raises *d_flag for one outside [-4096, 4095] (the caller
-// then sends the raw blocks).  The DC (a 16-bit zig-zag slot) is carried whole.
+// (DESIGN.md section 6): slot z of a block is stored in kWireW[table][z] bits of
+// two's complement, the per-slot widths proven sufficient by
+// tools/check/wire_widths.py (hiccup's unnormalised DCT of pixels - 128 is
+// bounded by 4 * 128 * S_u * S_v, divided by the table entry), so a luminance
+// block is 637 bits and a chrominance block 597 (against 1024 as int16).  Blocks
+// are packed back to back; a 64-block tile is 2 * bits-per-block 32-bit words
+// (whole words for any width), stored at a stride rounded up to 16 bytes.  Bit i
+// of a tile is bit (i & 31) of its word i >> 5 (LSB first).  The pack kernel
+// checks every value against its width and raises *d_flag on a violation (the
+// caller then sends the raw blocks).
 //
 //  hic_wire_pack_i16:   nblk blocks (64 int16, ZIGZAG_I16) -> ceil(nblk / 64) tiles
 //  hic_wire_unpack_i16: the inverse (blocks past nblk in the last tile dropped)
@@ -19,27 +16,34 @@
 //                       image's record array (positions + pos_shift), so the
 //                       gathering rank runs the scan + emit without a tile pass
 #include "hic_common.h"
+#include "wire_widths.h"
 
 namespace hic {
 namespace {
 
-constexpr int kBlkBits = 16 + 63 * 13;        // 835
-constexpr int kTileWords = 64 * kBlkBits / 32;  // 1670
-constexpr int kTileStride = 1672;              // words per tile on the wire (16-byte multiple)
-constexpr int kWPB = 4;                        // waves per workgroup
-static_assert(64 * kBlkBits % 32 == 0 && kTileWords <= kTileStride, "a tile is whole words");
+constexpr int kWPB = 4;  // waves per workgroup
+template <int TABLE>
+struct WireGeo {
+  static constexpr int kBits = kWireBits[TABLE];                    // per block
+  static constexpr int kWords = 2 * kBits;                          // per 64-block tile
+  static constexpr int kStride = (kWords + 3) / 4 * 4;              // words per tile on the wire
+};
+static_assert(WireGeo<0>::kStride <= 1280 && WireGeo<1>::kStride <= 1280, "LDS tile");
+constexpr int kTileLds = 1280;  // words of the LDS tile (>= every stride)
 
-// pack: lane j = block j of the wave's tile; its 835 bits are ORed into the LDS
-// tile at bit 835 j (the two words a lane shares with its neighbours need the OR)
+// pack: lane j = block j of the wave's tile; its bits are ORed into the LDS tile
+// at bit kBits * j (the two words a lane shares with its neighbours need the OR)
+template <int TABLE>
 __global__ __launch_bounds__(64 * kWPB) void k_wire_pack(const int16_t *__restrict__ blocks, int64_t nblk,
                                                          uint32_t *__restrict__ out, int *__restrict__ flag) {
-  __shared__ uint32_t s_tile[kWPB][kTileStride];
+  using G = WireGeo<TABLE>;
+  __shared__ uint32_t s_tile[kWPB][kTileLds];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t ntiles = (nblk + 63) / 64;
   const int64_t t = (int64_t)blockIdx.x * kWPB + wv;
   if (t >= ntiles) return;  // wave-uniform
   uint32_t *st = s_tile[wv];
-  for (int i = lane; i < kTileStride; i += 64) st[i] = 0;
+  for (int i = lane; i < G::kStride; i += 64) st[i] = 0;
   __builtin_amdgcn_wave_barrier();
   const int64_t b = t * 64 + lane;
   uint32_t w[32];
@@ -55,24 +59,16 @@ __global__ __launch_bounds__(64 * kWPB) void k_wire_pack(const int16_t *__restri
     for (int k = 0; k < 32; ++k) w[k] = 0;
   }
   // stream the fields into 32-bit words: acc holds `n` pending bits (LSB first)
-  const int bit0 = lane * kBlkBits;
+  const int bit0 = lane * G::kBits;
   int wi = bit0 >> 5, n = bit0 & 31;
   uint64_t acc = 0;
   bool bad = false;
 #pragma unroll
   for (int i = 0; i < 64; ++i) {
+    const int nb = kWireW[TABLE][i];
     const int v = (int)(int16_t)((w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
-    uint32_t f;
-    int nb;
-    if (i == 0) {
-      f = (uint32_t)v & 0xFFFFu;
-      nb = 16;
-    } else {
-      bad |= v < -4096 || v > 4095;
-      f = (uint32_t)v & 0x1FFFu;
-      nb = 13;
-    }
-    acc |= (uint64_t)f << n;
+    bad |= v < -(1 << (nb - 1)) || v >= (1 << (nb - 1));
+    acc |= (uint64_t)((uint32_t)v & ((1u << nb) - 1)) << n;
     n += nb;
     if (n >= 32) {
       atomicOr(&st[wi], (uint32_t)acc);  // first / last word: shared with a neighbour
@@ -84,31 +80,33 @@ __global__ __launch_bounds__(64 * kWPB) void k_wire_pack(const int16_t *__restri
   if (n > 0) atomicOr(&st[wi], (uint32_t)acc);
   if (bad) *flag = 1;
   __builtin_amdgcn_wave_barrier();
-  // copy out: 418 16-byte chunks (the last two words are zero padding)
-  uint4 *o = reinterpret_cast<uint4 *>(out + t * kTileStride);
-  for (int c = lane; c < kTileStride / 4; c += 64)
+  uint4 *o = reinterpret_cast<uint4 *>(out + t * G::kStride);
+  for (int c = lane; c < G::kStride / 4; c += 64)
     o[c] = make_uint4(st[4 * c], st[4 * c + 1], st[4 * c + 2], st[4 * c + 3]);
 }
 
 // unpack: the tile into LDS (coalesced), lane j extracts block j into its stage
 // row, the stage leaves as 1 KiB stores
 constexpr int kRowU4 = 9;  // 144 B stage rows (128 B + pad)
+template <int TABLE>
 __global__ __launch_bounds__(64 * kWPB) void k_wire_unpack(const uint32_t *__restrict__ wire, int64_t nblk,
                                                            int16_t *__restrict__ blocks) {
-  __shared__ uint32_t s_tile[kWPB][kTileStride];
+  using G = WireGeo<TABLE>;
+  __shared__ uint32_t s_tile[kWPB][kTileLds];
   __shared__ uint4 s_stage[kWPB][64 * kRowU4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t ntiles = (nblk + 63) / 64;
   const int64_t t = (int64_t)blockIdx.x * kWPB + wv;
   if (t >= ntiles) return;
   uint32_t *st = s_tile[wv];
-  const uint4 *src = reinterpret_cast<const uint4 *>(wire + t * kTileStride);
-  for (int c = lane; c < kTileStride / 4; c += 64) {
+  const uint4 *src = reinterpret_cast<const uint4 *>(wire + t * G::kStride);
+  for (int c = lane; c < G::kStride / 4; c += 64) {
     const uint4 v = src[c];
     st[4 * c] = v.x; st[4 * c + 1] = v.y; st[4 * c + 2] = v.z; st[4 * c + 3] = v.w;
   }
+  if (lane < 4) st[G::kStride + lane] = 0;  // a lane may read one word past its last field
   __builtin_amdgcn_wave_barrier();
-  const int bit0 = lane * kBlkBits;
+  const int bit0 = lane * G::kBits;
   int wi = bit0 >> 5, n = 0;
   uint64_t acc = 0;
   {
@@ -119,16 +117,13 @@ __global__ __launch_bounds__(64 * kWPB) void k_wire_unpack(const uint32_t *__res
   uint32_t w[32];
 #pragma unroll
   for (int i = 0; i < 64; ++i) {
-    const int nb = i == 0 ? 16 : 13;
+    const int nb = kWireW[TABLE][i];
     if (n < nb) {
       acc |= (uint64_t)st[wi++] << n;
       n += 32;
     }
-    int v;
-    if (i == 0)
-      v = (int)(int16_t)(acc & 0xFFFFu);
-    else
-      v = ((int)(acc & 0x1FFFu) ^ 0x1000) - 0x1000;  // sign-extend 13 bits
+    const int h = 1 << (nb - 1);
+    const int v = ((int)(acc & ((1u << nb) - 1)) ^ h) - h;  // sign-extend nb bits
     acc >>= nb;
     n -= nb;
     if (i & 1)
@@ -165,27 +160,42 @@ __global__ void k_records_rebase(const int64_t *__restrict__ src, int64_t nrec, 
 
 using namespace hic;
 
-extern "C" size_t hic_wire_bytes(int64_t nblk) { return nblk <= 0 ? 0 : (size_t)((nblk + 63) / 64) * kTileStride * 4; }
+extern "C" size_t hic_wire_bytes(int64_t nblk, int table_id) {
+  if (nblk <= 0 || (table_id != 0 && table_id != 1)) return 0;
+  const int stride = table_id == 0 ? WireGeo<0>::kStride : WireGeo<1>::kStride;
+  return (size_t)((nblk + 63) / 64) * stride * 4;
+}
 
-extern "C" int hic_wire_pack_i16(const int16_t *blocks, int64_t nblk, uint8_t *wire, int *d_flag, void *stream) {
+extern "C" int hic_wire_pack_i16(const int16_t *blocks, int64_t nblk, int table_id, uint8_t *wire, int *d_flag,
+                                 void *stream) {
   if (!blocks || !wire || !d_flag) return arg_error("null pointer");
   if (nblk <= 0) return arg_error("nblk");
+  if (table_id != HIC_TABLE_LUMINANCE && table_id != HIC_TABLE_CHROMINANCE) return arg_error("table_id");
   if ((reinterpret_cast<uintptr_t>(blocks) | reinterpret_cast<uintptr_t>(wire)) % 16)
     return arg_error("blocks and wire must be 16-byte aligned");
   const int64_t ntiles = (nblk + 63) / 64;
-  hipLaunchKernelGGL(k_wire_pack, dim3((unsigned)((ntiles + kWPB - 1) / kWPB)), dim3(64 * kWPB), 0, as_stream(stream),
-                     blocks, nblk, reinterpret_cast<uint32_t *>(wire), d_flag);
+  const dim3 grid((unsigned)((ntiles + kWPB - 1) / kWPB)), block(64 * kWPB);
+  uint32_t *w = reinterpret_cast<uint32_t *>(wire);
+  if (table_id == 0)
+    hipLaunchKernelGGL(k_wire_pack<0>, grid, block, 0, as_stream(stream), blocks, nblk, w, d_flag);
+  else
+    hipLaunchKernelGGL(k_wire_pack<1>, grid, block, 0, as_stream(stream), blocks, nblk, w, d_flag);
   return check_launch("k_wire_pack");
 }
 
-extern "C" int hic_wire_unpack_i16(const uint8_t *wire, int64_t nblk, int16_t *blocks, void *stream) {
+extern "C" int hic_wire_unpack_i16(const uint8_t *wire, int64_t nblk, int table_id, int16_t *blocks, void *stream) {
   if (!blocks || !wire) return arg_error("null pointer");
   if (nblk <= 0) return arg_error("nblk");
+  if (table_id != HIC_TABLE_LUMINANCE && table_id != HIC_TABLE_CHROMINANCE) return arg_error("table_id");
   if ((reinterpret_cast<uintptr_t>(blocks) | reinterpret_cast<uintptr_t>(wire)) % 16)
     return arg_error("blocks and wire must be 16-byte aligned");
   const int64_t ntiles = (nblk + 63) / 64;
-  hipLaunchKernelGGL(k_wire_unpack, dim3((unsigned)((ntiles + kWPB - 1) / kWPB)), dim3(64 * kWPB), 0,
-                     as_stream(stream), reinterpret_cast<const uint32_t *>(wire), nblk, blocks);
+  const dim3 grid((unsigned)((ntiles + kWPB - 1) / kWPB)), block(64 * kWPB);
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(wire);
+  if (table_id == 0)
+    hipLaunchKernelGGL(k_wire_unpack<0>, grid, block, 0, as_stream(stream), w, nblk, blocks);
+  else
+    hipLaunchKernelGGL(k_wire_unpack<1>, grid, block, 0, as_stream(stream), w, nblk, blocks);
   return check_launch("k_wire_unpack");
 }
 

@@ -101,6 +101,7 @@ def block_ranges(H, W, world):
 
 
 REC_BYTES = 24  # one RLE tile record: 3 int64
+TABLE_OF = {"lum": 0, "cr": 1, "cb": 1}  # the plane's quantisation table (the wire widths follow it)
 
 
 def wire_ranges(ranges, rpt, records):
@@ -115,7 +116,8 @@ def wire_ranges(ranges, rpt, records):
         for b0, b1 in ranges[k]:
             n = b1 - b0
             # (the records padded to 16 bytes: every segment starts 16-byte aligned)
-            size = lib.hic_wire_bytes(n) + (-(-(-(-n * rpt[k] // 64) * REC_BYTES) // 16) * 16 if records else 0)
+            size = lib.hic_wire_bytes(n, TABLE_OF[k]) + (-(-(-(-n * rpt[k] // 64) * REC_BYTES) // 16) * 16
+                                                            if records else 0)
             rr.append((o, o + size))
             o += size
         out[k] = rr
@@ -136,7 +138,8 @@ class ShardEncoder:
     (summaries, stitch, scan + emit) and gather_to collects the whole image's
     coefficient blocks and DC differences (gather_coefficients).
     gather_kind "stream": the ranks only transform; each ships its blocks in the
-    lossless 13-bit wire format (hic_wire_pack_i16) plus its rebased RLE tile
+    lossless wire format (hic_wire_pack_i16: per-slot widths proven for the
+    plane's table, 637 / 597 bits per block) plus its rebased RLE tile
     records to gather_to, which unpacks them and runs the scan + emit of the whole
     image -- codec.jpeg_encode's single stream (codec.py:55-99,286-301) ends on
     gather_to (self.whole.sym_len / sym_val / dc / counts), with no host sync and
@@ -205,8 +208,9 @@ class ShardEncoder:
             b0, b1 = self.ranges[k][self.rank]
             n = b1 - b0
             w = self.wire_send[k]
-            wb = lib.hic_wire_bytes(n)
-            _lib.call("hic_wire_pack_i16", device.ptr(self.enc.coef[k]), n, device.ptr(w), device.ptr(self.wire_flag), s)
+            wb = lib.hic_wire_bytes(n, TABLE_OF[k])
+            _lib.call("hic_wire_pack_i16", device.ptr(self.enc.coef[k]), n, TABLE_OF[k], device.ptr(w),
+                      device.ptr(self.wire_flag), s)
             if self.records:
                 nrec = -(-n * self.enc.rpt[k] // 64)
                 _lib.call("hic_rle_records_rebase", device.ptr(self.enc.ws[k]), nrec, b0 * 63,
@@ -243,9 +247,9 @@ class ShardEncoder:
                     continue
                 o0, _ = self.wranges[k][r]
                 seg = ctypes.c_void_p(self.wire_full[k].data_ptr() + o0)
-                _lib.call("hic_wire_unpack_i16", seg, n, device.ptr(whole.coef[k][b0:b1]), s)
+                _lib.call("hic_wire_unpack_i16", seg, n, TABLE_OF[k], device.ptr(whole.coef[k][b0:b1]), s)
                 if self.records:
-                    src = ctypes.c_void_p(self.wire_full[k].data_ptr() + o0 + lib.hic_wire_bytes(n))
+                    src = ctypes.c_void_p(self.wire_full[k].data_ptr() + o0 + lib.hic_wire_bytes(n, TABLE_OF[k]))
                     _lib.call("hic_rle_records_rebase", src, nrec, 0, dst_rec, s)
             if not self.records:
                 _lib.call("hic_rle_tile_records_i16", device.ptr(whole.coef[k]), whole.coef[k].shape[0],

@@ -394,24 +394,25 @@ int hic_huffman_decode(const uint8_t *d_bits, int64_t nbits, const int32_t *h_ch
 
 /* ---- the gather's wire format (no reference counterpart: the bytes that carry a
  *      shard's quantized zig-zag blocks -- codec.jpeg_encode's input after
- *      dct_channel, codec.py:286-301 -- to the gathering rank, losslessly).  A block
- *      is 835 bits: the DC slot as 16 bits, the 63 AC slots as 13-bit two's
- *      complement (|q| <= 32768 / 10: hiccup's unnormalised DCT, table entries
- *      >= 10); a 64-block tile is 1670 little-endian 32-bit words at a stride of
- *      1672 (6688 B, 16-byte aligned).
- *  hic_wire_bytes: the wire size of nblk blocks (whole tiles).
+ *      dct_channel, codec.py:286-301 -- to the gathering rank, losslessly).  Zig-zag
+ *      slot z of a block takes a fixed number of bits (two's complement) proven
+ *      sufficient for the plane's table by tools/check/wire_widths.py (hiccup's
+ *      unnormalised DCT bound 4 * 128 * S_u * S_v over the table entry): 637 bits
+ *      per luminance block, 597 per chrominance block; a 64-block tile is
+ *      2 * bits 32-bit little-endian words, stored at a stride rounded up to 16 B.
+ *  hic_wire_bytes: the wire size of nblk blocks of table table_id (whole tiles).
  *  hic_wire_pack_i16: blocks (nblk x 64 int16, 16-byte aligned) -> wire; *d_flag
- *    (device int, caller-zeroed) becomes 1 if an AC value lies outside 13 bits
- *    (then the wire is not lossless: send the raw blocks).
- *  hic_wire_unpack_i16: wire -> blocks (the inverse; nblk as packed).
+ *    (device int, caller-zeroed) becomes 1 if a value does not fit its slot's
+ *    width (then the wire is not lossless: send the raw blocks).
+ *  hic_wire_unpack_i16: wire -> blocks (the inverse; nblk and table as packed).
  *  hic_rle_records_rebase: nrec RLE tile records (3 int64: first / last nonzero
  *    stream position or -1, symbol count) copied to d_dst with pos_shift added to
  *    the positions: a shard's records placed in the whole image's record array
  *    (pos_shift = the shard's first block x 63; its records must start on a
  *    record boundary of the whole image). */
-size_t hic_wire_bytes(int64_t nblk);
-int hic_wire_pack_i16(const int16_t *blocks, int64_t nblk, uint8_t *wire, int *d_flag, void *stream);
-int hic_wire_unpack_i16(const uint8_t *wire, int64_t nblk, int16_t *blocks, void *stream);
+size_t hic_wire_bytes(int64_t nblk, int table_id);
+int hic_wire_pack_i16(const int16_t *blocks, int64_t nblk, int table_id, uint8_t *wire, int *d_flag, void *stream);
+int hic_wire_unpack_i16(const uint8_t *wire, int64_t nblk, int table_id, int16_t *blocks, void *stream);
 int hic_rle_records_rebase(const int64_t *d_src, int64_t nrec, int64_t pos_shift, int64_t *d_dst, void *stream);
 
 /* ---- Multi-GPU gather over RCCL (SURVEY.md section 8(b) hic_gather_*; the

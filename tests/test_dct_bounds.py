@@ -72,3 +72,26 @@ def test_bounds_are_sensitive():
     e1 = dct_bounds.E1()
     e64 = dct_bounds.E64()
     assert np.all(e1[:, 1:, :] > 1e3 * e64[:, 1:, :])
+
+
+def test_wire_widths_header_matches_proof():
+    """The gather's wire widths (hiccup_amd/csrc/wire_widths.h) are what
+    tools/check/wire_widths.py derives from the DCT bound, and every width holds
+    the largest quantised value its slot can take (checked against a brute-force
+    maximiser: the +-128 sign pattern of the slot's basis function)."""
+    import wire_widths
+    header = os.path.join(REPO, "hiccup_amd", "csrc", "wire_widths.h")
+    assert wire_widths.emit() == open(header).read(), \
+        "wire_widths.h differs from tools/check/wire_widths.py --emit: regenerate it"
+    for t, table in enumerate((wire_widths.LUM, wire_widths.CHROMA)):
+        w = wire_widths.widths(table)
+        for z in range(64):
+            u, v = divmod(wire_widths.ZZ[z], 8)
+            cu = np.cos(np.pi * u * (2 * np.arange(8) + 1) / 16)
+            cv = np.cos(np.pi * v * (2 * np.arange(8) + 1) / 16)
+            # the pixel block maximising |y|: +-128 by the sign of the basis
+            x = np.where(np.outer(cu, cv) >= 0, 127, -128)
+            y = 4 * float(np.sum(x * np.outer(cu, cv)))
+            q = abs(round(y / table[u][v]))
+            assert q < (1 << (w[z] - 1)), (t, z, q, w[z])
+        assert sum(w) == (637, 597)[t]

@@ -6,7 +6,7 @@ reassembles (a) the coefficient blocks + DC stream with sharding.gather_blocks -
 the same grouped batch_isend_irecv code the RCCL path runs; (a') a group of
 `world` images' gathers, image j to rank j, goes out as one batch
 (sharding.gather_blocks_group, the bench's exchange); (a'') the stream gather:
-blocks in the 13-bit wire format (tests/wire_host.py) to the receiving rank, which
+blocks in the wire format (tests/wire_host.py) to the receiving rank, which
 codes the whole stream -- and (b) the symbol
 streams with point-to-point sends.  Both must equal the single-stream encode.
 (c) Each rank then decodes its own slice (sharded decode: carried-zero skip, DC
@@ -79,7 +79,7 @@ def _wire_ranges_host(ranges):
     for k in pipeline.CHANNELS:
         o, rr = 0, []
         for b0, b1 in ranges[k]:
-            rr.append((o, o + wire_host.wire_bytes(b1 - b0)))
+            rr.append((o, o + wire_host.wire_bytes(b1 - b0, wire_host.TABLE_OF[k])))
             o = rr[-1][1]
         out[k] = rr
     return out
@@ -157,7 +157,8 @@ def _worker(rank, world, port, H, W, flat, results):
         assert wr == _wire_ranges_host(ranges)
         items = []
         for j in range(world):
-            mine_w = {k: (torch.from_numpy(wire_host.pack(mine[k] + j if j else mine[k]).copy()),)
+            mine_w = {k: (torch.from_numpy(wire_host.pack(mine[k] + j if j else mine[k],
+                                                          wire_host.TABLE_OF[k]).copy()),)
                       for k in pipeline.CHANNELS}
             full_w = ({k: (torch.zeros(wr[k][-1][1], dtype=torch.uint8),) for k in pipeline.CHANNELS}
                       if rank == j else None)
@@ -173,7 +174,8 @@ def _worker(rank, world, port, H, W, flat, results):
                     parts.append(mine[k] + rank if rank else mine[k])
                 else:
                     o0, o1 = wr[k][r]
-                    parts.append(wire_host.unpack(full_w[k][0][o0:o1].numpy(), b1 - b0).astype(np.int64))
+                    parts.append(wire_host.unpack(full_w[k][0][o0:o1].numpy(), b1 - b0,
+                                                  wire_host.TABLE_OF[k]).astype(np.int64))
             whole = np.concatenate(parts)
             want = zz[k] + rank if rank else zz[k]
             ok &= np.array_equal(whole, want)

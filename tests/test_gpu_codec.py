@@ -668,34 +668,36 @@ def test_huffman_decode_device_full_size():
     assert torch.equal(out[:n], keys)
 
 
+@pytest.mark.parametrize("table", [0, 1])
 @pytest.mark.parametrize("nblk", [1, 63, 64, 65, 777, 129600])
-def test_wire_pack_unpack(nblk):
+def test_wire_pack_unpack(nblk, table):
     """The gather's wire format: hic_wire_pack_i16 == the host restatement
-    (tests/wire_host.py, which the CPU gloo test of the stream gather uses),
-    unpack inverts it, the 13-bit range check raises the flag, and
-    hic_rle_records_rebase shifts record positions (-1 kept)."""
+    (tests/wire_host.py, which the CPU gloo test of the stream gather uses) for
+    every slot anywhere in its proven width, unpack inverts it, a value one past a
+    slot's width raises the flag, and hic_rle_records_rebase shifts record
+    positions (-1 kept).  A real 8K encode's blocks pack losslessly too."""
     import wire_host
-    rng = np.random.default_rng(nblk)
-    blocks = rng.integers(-4096, 4096, (nblk, 64)).astype(np.int16)
-    blocks[:, 0] = rng.integers(-32768, 32768, nblk)
-    blocks[rng.random((nblk, 64)) < 0.5] = 0
+    rng = np.random.default_rng(nblk + table)
+    blocks = wire_host.random_blocks(rng, nblk, table)
     lib = _lib.load()
-    nb = lib.hic_wire_bytes(nblk)
-    assert nb == wire_host.wire_bytes(nblk)
+    nb = lib.hic_wire_bytes(nblk, table)
+    assert nb == wire_host.wire_bytes(nblk, table)
     b = device.to_device(blocks)
     wire = device.empty((nb,), torch.uint8)
     flag = device.zeros((1,), torch.int32)
-    _lib.call("hic_wire_pack_i16", device.ptr(b), nblk, device.ptr(wire), device.ptr(flag), device.stream_ptr())
+    _lib.call("hic_wire_pack_i16", device.ptr(b), nblk, table, device.ptr(wire), device.ptr(flag),
+              device.stream_ptr())
     got = device.to_host(wire)
-    np.testing.assert_array_equal(got, wire_host.pack(blocks))
+    np.testing.assert_array_equal(got, wire_host.pack(blocks, table))
     assert int(flag.item()) == 0
     back = device.empty((nblk, 64), torch.int16)
-    _lib.call("hic_wire_unpack_i16", device.ptr(wire), nblk, device.ptr(back), device.stream_ptr())
+    _lib.call("hic_wire_unpack_i16", device.ptr(wire), nblk, table, device.ptr(back), device.stream_ptr())
     np.testing.assert_array_equal(device.to_host(back), blocks)
     bad = blocks.copy()
-    bad[nblk // 2, 7] = 4096
-    _lib.call("hic_wire_pack_i16", device.ptr(device.to_device(bad)), nblk, device.ptr(wire), device.ptr(flag),
-              device.stream_ptr())
+    j = int(rng.integers(0, 64))
+    bad[nblk // 2, j] = 1 << (wire_host.WIDTHS[table][j] - 1)
+    _lib.call("hic_wire_pack_i16", device.ptr(device.to_device(bad)), nblk, table, device.ptr(wire),
+              device.ptr(flag), device.stream_ptr())
     assert int(flag.item()) == 1
     rec = rng.integers(-1, 10 ** 6, (nblk, 3)).astype(np.int64)
     out = device.empty((nblk, 3), torch.int64)
@@ -704,6 +706,20 @@ def test_wire_pack_unpack(nblk):
     exp = rec.copy()
     exp[:, :2] = np.where(rec[:, :2] >= 0, rec[:, :2] + 1234567, rec[:, :2])
     np.testing.assert_array_equal(device.to_host(out), exp)
+    if nblk == 129600:  # the extreme-value images of the structured kinds, through a real encode
+        for kind in ("random", "colour_levels", "blocks"):
+            enc = pipeline.Encoder(4320 // 4, 7680 // 2)
+            enc.encode(device.to_device(_structured_rgb(kind, 4320 // 4, 7680 // 2, 3)))
+            k = "lum" if table == 0 else "cr"
+            coef = enc.coef[k]
+            w2 = device.empty((lib.hic_wire_bytes(coef.shape[0], table),), torch.uint8)
+            flag.zero_()
+            _lib.call("hic_wire_pack_i16", device.ptr(coef), coef.shape[0], table, device.ptr(w2),
+                      device.ptr(flag), device.stream_ptr())
+            back2 = device.empty(tuple(coef.shape), torch.int16)
+            _lib.call("hic_wire_unpack_i16", device.ptr(w2), coef.shape[0], table, device.ptr(back2),
+                      device.stream_ptr())
+            assert int(flag.item()) == 0 and torch.equal(back2, coef), kind
 
 
 def test_huffman_device_streams_batch_equals_single():

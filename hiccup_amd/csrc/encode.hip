@@ -150,82 +150,130 @@ __device__ __forceinline__ void enc_dct_f32(uint2 (&w)[8], int16_t *st) {
 
 // Packed float32 variant (knob "encode_dct" = 2): dct_block_pk (dct_core.h: two
 // transforms of the block per v_pk op, (4,4) ties decided in place), the proven
-// float32 windows.  The flagged coefficients (~0.03 per block on random data) are
-// resolved inline before the stage leaves: compacted into a per-wave LDS list
-// {owner lane, flag bit}, one item per lane, the owner's pixel rows fetched by
-// ds_bpermute (no LDS copy), resolve_coef (float64 dot product, pocketfft's own
-// operations for the rational classes), the result written into the owner's stage
-// row.  No call: an out-of-line resolve made every live register of this kernel
-// cross scratch.  A coefficient that stays ambiguous (or a list overflow) sends
-// the owner's block to the exact replica (out of line; never seen on natural data).
-constexpr int kEncQCap = 64;
+// float32 windows.  A flagged coefficient (~0.03 per block on random data) keeps
+// its provisional q (the estimate's rint) in the stage, which leaves for HBM as
+// usual, and is DEFERRED: the owner lane appends {block, plane, flag bit,
+// provisional q} and its block's 64 B of pixels to the WORKGROUP's LDS queue (one
+// LDS atomic per wave and compaction step).  When the workgroup's four units are
+// done, each wave resolves up to 64 queued items in ONE round, one per lane
+// (resolve_coef: float64 dot product, pocketfft's own operations for the rational
+// classes), patches the coefficient in HBM if it changed, and marks the unit's
+// record if q crossed zero (a flag moves q by at most one, so only then does the
+// tile record, built from the provisional stage, change); the marked records are
+// rebuilt from HBM afterwards.  One resolve round per four units, instead of one
+// per DCT pass (three per unit) as an in-place resolve needs.  A coefficient
+// resolve_coef cannot settle sends its block to the exact replica (whole block
+// patched); a queue overflow (tie-dense input only) does so in place, before the
+// store.
+#ifndef HIC_ENC_WPB
+#define HIC_ENC_WPB 4  // waves per workgroup (<= 4: the deferred queue's wave field)
+#endif
+static_assert(HIC_ENC_WPB <= 4, "enc_dct_pk's queue header holds a 2-bit wave index");
+constexpr int kEncQCap = 64 * HIC_ENC_WPB;
 
-__device__ __forceinline__ uint32_t enc_bperm(int src_lane, uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
-}
+struct EncQueue {
+  uint2 *qh;         // {block index in its plane, plane << 28 | Y row << 27 | wave << 16 ... see enc_enqueue}
+  uint4 *qp;         // 4 x 16 B: the block's 8 pixel rows
+  int *qn;           // items appended (may exceed kEncQCap: overflow)
+  uint32_t *dirty;   // bit 3 wave + r: record r (0, 1 Y block rows, 2 chroma) of that wave's unit
+};
 
+// header y: plane (2 bits) << 28 | rec (2 bits: 0/1 Y row, 2 chroma) << 24 | wave
+// (2 bits) << 22 | flag bit (6) << 16 | provisional q (16)
 template <int TABLE>
-__device__ __forceinline__ void enc_dct_pk(uint2 (&w)[8], int16_t *st, uint2 *st2, uint32_t *qlist, const double *cm,
-                                           const uint8_t *qt) {
+__device__ __forceinline__ void enc_dct_pk(uint2 (&w)[8], int16_t *st, const EncQueue &Q, bool valid, int plane,
+                                           int rec, int wv, int blk) {
   constexpr SlotOf<kZZ> kSlot{};
   uint32_t f0 = 0, f1 = 0;
   dct_block_pk<TABLE>(w, st, f0, f1);
   const int lane = threadIdx.x & 63;
-  uint64_t bits = ((uint64_t)f1 << 32) | f0;
+  uint64_t bits = valid ? ((uint64_t)f1 << 32) | f0 : 0;
 #if defined(HIC_DEV) && defined(HIC_ENC_DEV) && (HIC_ENC_DEV & 4)
   bits = 0;  // dev timing (results invalid): flags dropped, no resolve
 #endif
   if (!__builtin_amdgcn_ballot_w64(bits != 0)) return;
-  const bool mine = bits != 0;
-  int n = 0;
-  bool over = false;
-  for (;;) {  // compact: one flag per lane per pass
+  bool redo = false;
+  for (;;) {  // compact: one flag per lane per step
     const bool has = bits != 0;
     const uint64_t m = __builtin_amdgcn_ballot_w64(has);
     if (!m) break;
+    const int l0 = __builtin_ctzll(m);
+    int base = 0;
+    if (lane == l0) base = atomicAdd(Q.qn, __builtin_popcountll(m));
+    base = __builtin_amdgcn_readlane(base, l0);
     if (has) {
       const int b = __builtin_ctzll(bits);
       bits &= bits - 1;
-      const int pos = n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      if (pos < kEncQCap) qlist[pos] = (uint32_t)(lane << 8 | b);
-    }
-    n += __builtin_popcountll(m);
-  }
-  if (n > kEncQCap) {
-    over = true;
-    n = kEncQCap;
-  }
-  __builtin_amdgcn_wave_barrier();
-  // one round (n <= 64): lane j resolves item j
-  const uint32_t it = lane < n ? qlist[lane] : 0u;
-  const int owner = (int)(it >> 8);
-  uint2 wo[8];
+      const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (pos < kEncQCap) {
+        const uint32_t q0 = (uint16_t)st[kSlot.s[pk_flag_index(b)]];
+        Q.qh[pos] = make_uint2((uint32_t)blk, (uint32_t)plane << 28 | (uint32_t)rec << 24 | (uint32_t)wv << 22 |
+                                                  (uint32_t)b << 16 | q0);
 #pragma unroll
-  for (int r = 0; r < 8; ++r) wo[r] = make_uint2(enc_bperm(owner, w[r].x), enc_bperm(owner, w[r].y));
-  bool fail = false;
-  if (lane < n) {
-    const int i = pk_flag_index((int)(it & 63u));
-    int q = 0;
-    if (resolve_coef(wo, TABLE, i, q, cm, qt))  // cos / table lookups from LDS, not select chains
-      reinterpret_cast<int16_t *>(st2 + owner * kStageU2)[kSlot.s[i]] = (int16_t)q;
-    else
-      fail = true;
+        for (int r = 0; r < 4; ++r)
+          Q.qp[4 * pos + r] = make_uint4(w[2 * r].x, w[2 * r].y, w[2 * r + 1].x, w[2 * r + 1].y);
+      } else {
+        redo = true;
+      }
+    }
   }
-  // owners of an unresolved item (or of any item, after an overflow): exact replica
-  const uint64_t fm = __builtin_amdgcn_ballot_w64(fail);
-  bool redo = over && mine;
-  for (uint64_t mm = fm; mm; mm &= mm - 1) redo |= __builtin_amdgcn_readlane(owner, __builtin_ctzll(mm)) == lane;
-  __builtin_amdgcn_wave_barrier();
+  // queue full: this lane's block on the exact replica now (its items queued so far
+  // resolve to the same values later)
   if (__builtin_amdgcn_ballot_w64(redo))
     if (redo) enc_exact_block<TABLE>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], st);
 }
 
-// DM: the DCT variant (0 float64 AAN, 1 scalar float32, 2 packed float32)
+// The workgroup's deferred items: wave wv resolves items 64 wv .. 64 wv + 63, one per
+// lane (st: this lane's stage row, free once the units are done).  Called by every
+// wave of the workgroup after a barrier that follows all enqueues and all stores.
+__device__ __forceinline__ void enc_resolve_queue(const Enc420 &E, const EncQueue &Q, int wv, int lane, int16_t *st,
+                                                  const double *cm, const uint8_t *qt) {
+  constexpr SlotOf<kZZ> kSlot{};
+  int n = *Q.qn;
+  n = n < kEncQCap ? n : kEncQCap;
+  const int j = 64 * wv + lane;
+  if (j >= n) return;
+  const uint2 h = Q.qh[j];
+  uint2 w[8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint4 t = Q.qp[4 * j + k];
+    w[2 * k] = make_uint2(t.x, t.y);
+    w[2 * k + 1] = make_uint2(t.z, t.w);
+  }
+  const int plane = (int)(h.y >> 28), table = plane > 0 ? 1 : 0;
+  const int i = pk_flag_index((int)((h.y >> 16) & 63u));
+  const int q0 = (int)(int16_t)(h.y & 0xFFFFu);
+  int16_t *o = E.coef[plane] + (int64_t)h.x * 64;
+  bool mark = false;
+  int q = 0;
+  if (resolve_coef(w, table, i, q, cm, qt)) {
+    if (q != q0) {
+      o[kSlot.s[i]] = (int16_t)q;
+      mark = (q == 0) != (q0 == 0);
+    }
+  } else {
+    if (table == 0)
+      enc_exact_block<0>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], st);
+    else
+      enc_exact_block<1>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], st);
+    const uint2 *s2 = reinterpret_cast<const uint2 *>(st);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint2 lo = s2[2 * k], hi = s2[2 * k + 1];
+      reinterpret_cast<uint4 *>(o)[k] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+    }
+    mark = true;
+  }
+  if (mark) atomicOr(Q.dirty, 1u << (3 * ((h.y >> 22) & 3u) + ((h.y >> 24) & 3u)));
+}
+
+// DM: the DCT variant (0 float64 AAN, 1 scalar float32, 2 packed float32 + deferred resolve)
 template <int TABLE, int DM>
-__device__ __forceinline__ void enc_dct_any(uint2 (&w)[8], int16_t *st, uint2 *st2, uint32_t *qlist, const double *cm,
-                                            const uint8_t *qt) {
+__device__ __forceinline__ void enc_dct_any(uint2 (&w)[8], int16_t *st, const EncQueue &Q, bool valid, int plane,
+                                            int rec, int wv, int blk) {
   if (DM == 2)
-    enc_dct_pk<TABLE>(w, st, st2, qlist, cm, qt);
+    enc_dct_pk<TABLE>(w, st, Q, valid, plane, rec, wv, blk);
   else if (DM == 1)
     enc_dct_f32<TABLE>(w, st);
   else
@@ -487,9 +535,6 @@ struct EncColour {
   }
 };
 
-#ifndef HIC_ENC_WPB
-#define HIC_ENC_WPB 4  // waves per workgroup
-#endif
 #ifndef HIC_ENC_VG
 #define HIC_ENC_VG 1  // 16-row units per wave (2: two vertically adjacent units, 35 input rows
                       // for 32; measured 61-65 vs 60-63 us: no gain, scripts/gpu_r2ah.sh)
@@ -517,21 +562,32 @@ template <int TMF, bool NT, int DM>
 __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
   __shared__ uint2 s_stage[HIC_ENC_WPB * 64 * kStageU2];
   __shared__ uint32_t s_chroma_all[HIC_ENC_WPB][2 * 8 * 64];
-  __shared__ uint32_t s_qlist_all[HIC_ENC_WPB][DM == 2 ? kEncQCap : 1];
+  // the deferred queue of the packed variant (DM == 2): 72 B per item
+  __shared__ uint2 s_qh[DM == 2 ? kEncQCap : 1];
+  __shared__ uint4 s_qp[DM == 2 ? 4 * kEncQCap : 1];
+  __shared__ int s_qn;
+  __shared__ uint32_t s_dirty;
   __shared__ double s_cm[DM == 2 ? 64 : 1];    // the fallback's cos2 table and QT (per-lane lookups)
   __shared__ uint8_t s_qt[DM == 2 ? 128 : 1];
   if (DM == 2) {
     if (threadIdx.x < 64) s_cm[threadIdx.x] = cos2(kCm, threadIdx.x >> 3, threadIdx.x & 7);
     if (threadIdx.x < 128) s_qt[threadIdx.x] = (uint8_t)QT[threadIdx.x >> 6][threadIdx.x & 63];
+    if (threadIdx.x == 0) {
+      s_qn = 0;
+      s_dirty = 0;
+    }
     __syncthreads();
   }
+  const EncQueue Q{s_qh, s_qp, &s_qn, &s_dirty};
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = blockIdx.x;
   const int g = __builtin_amdgcn_readfirstlane(b * HIC_ENC_WPB + wv);
-  if (g >= E.nunits) return;  // wave-uniform
+  // wave-uniform; the packed variant's waves past the end still join the
+  // workgroup's barriers before the deferred resolve
+  if (DM != 2 && g >= E.nunits) return;
+  const bool live = g < E.nunits;
   uint2 *st2 = s_stage + wv * 64 * kStageU2;
   uint32_t *s_chroma = s_chroma_all[wv];
-  uint32_t *s_qlist = s_qlist_all[wv];
   int16_t *st = reinterpret_cast<int16_t *>(st2 + lane * kStageU2);
   // wave g: strip s, unit rows u0 .. u0 + HIC_ENC_VG - 1 (the last wave of a strip
   // may have one unit row only)
@@ -550,9 +606,9 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
     uint2 w[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) w[r] = yq[8 * br + r];
-    enc_dct_any<0, DM>(w, st, st2, s_qlist, s_cm, s_qt);
-    __builtin_amdgcn_wave_barrier();
     const int64_t b0 = (int64_t)(2 * u + br) * nbx + 64 * s;
+    enc_dct_any<0, DM>(w, st, Q, lane < nb, 0, br + 2 * (u - u0), wv, (int)b0 + lane);
+    __builtin_amdgcn_wave_barrier();
     int16_t *o = E.coef[0] + b0 * 64;
     enc_store<NT>(st2, lane, o, o + 32 * 64, nb < 32 ? nb : 32, nb > 32 ? nb - 32 : 0);
     if (TMF >= 0 && E.rec[0]) {
@@ -571,9 +627,9 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
     uint2 w[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = sc[i * 32];
-    enc_dct_any<1, DM>(w, st, st2, s_qlist, s_cm, s_qt);
-    __builtin_amdgcn_wave_barrier();
     const int64_t b0 = (int64_t)u * nbxc + 32 * s;
+    enc_dct_any<1, DM>(w, st, Q, (lane & 31) < (nb >> 1), 1 + (lane >> 5), 2, wv, (int)b0 + (lane & 31));
+    __builtin_amdgcn_wave_barrier();
     enc_store<NT>(st2, lane, E.coef[1] + b0 * 64, E.coef[2] + b0 * 64, nb >> 1, nb >> 1);
     if (TMF >= 0 && E.rec[1]) {
       uint32_t zw[32];
@@ -614,6 +670,8 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
   };
   using PC = std::integral_constant<short, HIC_ENC_PRIO_C>;
   using PD = std::integral_constant<short, HIC_ENC_PRIO_D>;
+  static_assert(DM != 2 || HIC_ENC_VG == 1, "the deferred queue marks one unit's records per wave");
+  if (live) {
   EncColour<HIC_ENC_VG == 2 ? 35 : 19> C;
   prio(PC{});
   C.init(E, y0, s, lane, nb);
@@ -638,7 +696,43 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
     c_blocks(u0 + 1);
     }
   }
+  }
 #endif
+  if constexpr (DM == 2) {
+    // the workgroup's deferred items: every wave's stores and enqueues are done
+    // (a patch must land after the provisional block store it corrects)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    enc_resolve_queue(E, Q, wv, lane, st, s_cm, s_qt);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // records whose zero pattern a resolved coefficient changed: rebuilt from HBM
+    const uint32_t d = (s_dirty >> (3 * wv)) & 7u;
+    if (TMF >= 0 && live && d) {
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      auto load_nt = [&](const int16_t *blk, uint32_t (&zw)[32]) {
+        const u32x4 *b4 = reinterpret_cast<const u32x4 *>(blk);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const u32x4 t = __builtin_nontemporal_load(b4 + k);
+          zw[4 * k] = t.x; zw[4 * k + 1] = t.y; zw[4 * k + 2] = t.z; zw[4 * k + 3] = t.w;
+        }
+      };
+      for (int br = 0; br < 2; ++br)
+        if ((d >> br) & 1u && E.rec[0]) {
+          const int64_t b0 = (int64_t)(2 * u0 + br) * nbx + 64 * s;
+          uint32_t zw[32];
+          load_nt(E.coef[0] + (b0 + lane) * 64, zw);
+          tile_record16<TMF>(zw, true, b0 + lane, E.M, E.rec[0] + (b0 >> 6) * 3);
+        }
+      if ((d >> 2) & 1u && E.rec[1]) {
+        const int64_t b0 = (int64_t)u0 * nbxc + 32 * s;
+        uint32_t zw[32];
+        load_nt(E.coef[1 + (lane >> 5)] + (b0 + (lane & 31)) * 64, zw);
+        tile_record16_half<TMF>(zw, b0, E.M, E.rec[1] + (b0 >> 5) * 3, E.rec[2] + (b0 >> 5) * 3);
+      }
+    }
+  }
 }
 
 }  // namespace

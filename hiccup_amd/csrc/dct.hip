@@ -1002,7 +1002,7 @@ __device__ __attribute__((noinline)) void pk_exact_block(const uint8_t *plane, i
 // wave's dirty-tile mask (bit k: set k's record must be rebuilt).
 __device__ __forceinline__ uint64_t pk_flush(const DctJobs &jobs, const uint2 *qh, const uint4 *qp, int n, int g0,
                                              int nwaves, uint2 *st2, const double *cm, const uint8_t *qt,
-                                             const int8_t *zz, int lane) {
+                                             const int8_t *zz, int lane, uint32_t *mark_to = nullptr) {
   bool mark = false;
   int kset = 0;
   if (lane < n) {
@@ -1038,6 +1038,10 @@ __device__ __forceinline__ uint64_t pk_flush(const DctJobs &jobs, const uint2 *q
       for (int k = 0; k < 8; ++k) reinterpret_cast<uint4 *>(o)[k] = stage16(st2, lane, k);
       mark = true;
     }
+  }
+  if (mark_to) {  // merged flush: the owner wave's set mask in LDS (per lane)
+    if (mark) atomicOr(mark_to + (kset >> 5), 1u << (kset & 31));
+    return 0;
   }
   uint64_t dirty = 0;
   for (uint64_t m = __builtin_amdgcn_ballot_w64(mark); m; m &= m - 1)
@@ -1088,9 +1092,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_PK_WPE)
   __shared__ double s_cm[64];
   __shared__ uint8_t s_qt[128];
   __shared__ int8_t s_zz[64];
+  __shared__ int s_qn[4];             // the waves' residual queue lengths (the merged final flush)
+  __shared__ uint32_t s_dirty[4 * 2];  // the waves' dirty-set masks, set by the merged flush
   if (threadIdx.x < 64) s_cm[threadIdx.x] = cos2(kCm, threadIdx.x >> 3, threadIdx.x & 7);
   if (threadIdx.x < 128) s_qt[threadIdx.x] = (uint8_t)QT[threadIdx.x >> 6][threadIdx.x & 63];
   if (threadIdx.x < 64) s_zz[threadIdx.x] = kZZInv[threadIdx.x];
+  if (threadIdx.x < 8) s_dirty[threadIdx.x] = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nwaves = gridDim.x * 4, g0 = blockIdx.x * 4 + wv;
@@ -1106,12 +1113,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_PK_WPE)
     k = (jobs.n > 2 && g >= jobs.j[2].set0) ? 2 : k;
     return __builtin_amdgcn_readfirstlane(k);
   };
-  if (g0 >= jobs.total_sets) return;  // wave-uniform
+  // (a wave without sets still joins the workgroup's barriers of the final flush)
   uint2 wn[8];
   if (dv & 8) {
 #pragma unroll
     for (int r = 0; r < 8; ++r) wn[r] = make_uint2(0x9E3779B1u * (lane + r), 0x85EBCA6Bu * (lane ^ r));
-  } else if (HIC_PK_PF) {
+  } else if (HIC_PK_PF && g0 < jobs.total_sets) {
     const DctJob &J0 = jobs.j[job_of(g0)];
     pk_load(J0, g0 - J0.set0, lane, wn);
   }
@@ -1191,8 +1198,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_PK_WPE)
       __builtin_amdgcn_wave_barrier();
     }
   }
-  if (qn > 0) dirty |= pk_flush(jobs, qh, qp, qn, g0, nwaves, st2, s_cm, s_qt, s_zz, lane);
-  if (TMF >= 0 && !(dv & 4)) {
+  // The residual items of the workgroup's waves, merged: one resolve round per 64
+  // items of the workgroup instead of one per wave (every wave ends with a partly
+  // full queue at the same time, in the launch's tail).  Wave v resolves the items
+  // 64 v .. 64 v + 63 of the concatenated queues; the set masks go to the owners.
+  if (lane == 0) s_qn[wv] = qn;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the provisional stores precede any patch
+  __syncthreads();
+  {
+    const int n0 = s_qn[0], n1 = s_qn[1], n2 = s_qn[2], n3 = s_qn[3];
+    const int j = 64 * wv + lane;
+    const int o = j < n0 ? 0 : (j < n0 + n1 ? 1 : (j < n0 + n1 + n2 ? 2 : 3));
+    const int jo = j - (o > 0 ? n0 : 0) - (o > 1 ? n1 : 0) - (o > 2 ? n2 : 0);
+    const int ntot = n0 + n1 + n2 + n3;
+    if (__builtin_amdgcn_ballot_w64(j < ntot)) {
+      // lane -> item jo of wave o's queue: pk_flush reads item `lane` of (qh, qp), so
+      // shift the bases per lane (n = lane + 1 keeps exactly this lane's item)
+      const uint2 *qho = s_qh + o * kPkQCap + jo - lane;
+      const uint4 *qpo = s_qp + (o * kPkQCap + jo - lane) * 4;
+      const uint64_t d = pk_flush(jobs, qho, qpo, j < ntot ? lane + 1 : 0, blockIdx.x * 4 + o, nwaves, st2, s_cm, s_qt,
+                                  s_zz, lane, s_dirty + 2 * o);
+      (void)d;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  dirty |= (uint64_t)s_dirty[2 * wv + 1] << 32 | s_dirty[2 * wv];
+  if (g0 < jobs.total_sets && TMF >= 0 && !(dv & 4)) {
     for (uint64_t d = dirty; d; d &= d - 1) pk_rebuild_record<TMF>(jobs, job_of, g0 + __builtin_ctzll(d) * nwaves, lane);
   }
 }

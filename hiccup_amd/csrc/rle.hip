@@ -620,8 +620,10 @@ struct RleJobs16 {
 };
 
 // Multi-workgroup scan for the batched hot path: each channel's tiles are cut
-// into partitions of kScanT tiles, one workgroup per partition (all resident at
-// once: a few dozen workgroups).  A partition reduces its tiles, publishes the
+// into partitions of kScan16T tiles, one workgroup per partition (all resident at
+// once: ~100 workgroups at 8K).  Partitions of 256 (4-wave workgroups): beside the
+// other stream's encoder (2 waves per SIMD of 234 VGPRs) a 1024-thread workgroup
+// waits for a whole CU's 16 wave slots to drain.  A partition reduces its tiles, publishes the
 // aggregate as three tagged 8-byte granules {value, epoch tag} (sc1 stores:
 // MI355X_MICROARCH.md, granule hand-off; no fences), polls the granules of every
 // earlier partition of its channel (sc1 loads) and folds them, then scans its
@@ -638,26 +640,31 @@ __device__ __forceinline__ bool get_granule(const uint64_t *g, uint32_t tag, int
   return (uint32_t)(x >> 32) == tag;
 }
 
-__global__ __launch_bounds__(kScanT) void k_rle_scan16b(RleJobs16 jobs, uint32_t epoch) {
-  __shared__ Agg s_wave[kScanT / 64 + 1];
+#ifndef HIC_SCAN16_T
+#define HIC_SCAN16_T 256
+#endif
+constexpr int kScan16T = HIC_SCAN16_T;
+static_assert(kScan16T % 64 == 0 && kScan16T <= 1024, "scan partition: whole waves");
+__global__ __launch_bounds__(kScan16T) void k_rle_scan16b(RleJobs16 jobs, uint32_t epoch) {
+  __shared__ Agg s_wave[kScan16T / 64 + 1];
   __shared__ Agg s_pre;
   __shared__ int s_fail;
   // workgroup -> (job, partition)
   int jb = 0;
   int64_t p = blockIdx.x;
-  while (jb + 1 < jobs.n && p >= (jobs.j[jb].nrec + kScanT - 1) / kScanT) {
-    p -= (jobs.j[jb].nrec + kScanT - 1) / kScanT;
+  while (jb + 1 < jobs.n && p >= (jobs.j[jb].nrec + kScan16T - 1) / kScan16T) {
+    p -= (jobs.j[jb].nrec + kScan16T - 1) / kScan16T;
     ++jb;
   }
   const RleJob16 &J = jobs.j[jb];
   const int M = jobs.M;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t nt = J.nrec, np = (nt + kScanT - 1) / kScanT;
+  const int64_t nt = J.nrec, np = (nt + kScan16T - 1) / kScan16T;
   const int64_t *tiles = J.ws;
   int64_t *offs = J.ws + 3 * nt;
   uint64_t *gran = reinterpret_cast<uint64_t *>(J.ws + 5 * nt);  // 3 per partition
   const uint32_t tag = (epoch << 2) | 1u;
-  const int64_t t = p * kScanT + threadIdx.x;
+  const int64_t t = p * kScan16T + threadIdx.x;
   const Agg rec = t < nt ? Agg{tiles[t * 3 + 0], tiles[t * 3 + 1], tiles[t * 3 + 2]} : Agg{-1, -1, 0};
   // workgroup inclusive scan of the partition's tile records
   Agg incl = rec;
@@ -670,7 +677,7 @@ __global__ __launch_bounds__(kScanT) void k_rle_scan16b(RleJobs16 jobs, uint32_t
   if (threadIdx.x == 0) s_fail = 0;
   __syncthreads();
   if (wave == 0) {
-    constexpr int NW = kScanT / 64;
+    constexpr int NW = kScan16T / 64;
     Agg it = lane < NW ? s_wave[lane] : Agg{-1, -1, 0};
 #pragma unroll
     for (int d = 1; d < NW; d <<= 1) {
@@ -721,7 +728,7 @@ __global__ __launch_bounds__(kScanT) void k_rle_scan16b(RleJobs16 jobs, uint32_t
     offs[t * 2 + 1] = excl.last >= 0 ? excl.last : p0;
   }
   if (p == np - 1 && threadIdx.x == 0) {  // the channel's last partition closes the stream
-    const Agg all = agg_combine(s_pre, s_wave[kScanT / 64], M);
+    const Agg all = agg_combine(s_pre, s_wave[kScan16T / 64], M);
     const int64_t last = all.last >= 0 ? all.last : p0;
     const int64_t n_ac = J.nblk * 63;
     const bool emit_eob = J.stitch ? J.stitch[1] != 0 : true;
@@ -754,7 +761,7 @@ __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
   const int M = jobs.M;
   if (blockIdx.x == 0 && threadIdx.x < jobs.n) {  // the scan's failure report (sticky)
     const RleJob16 &J = jobs.j[threadIdx.x];
-    const int64_t np = (J.nrec + kScanT - 1) / kScanT;
+    const int64_t np = (J.nrec + kScan16T - 1) / kScan16T;
     int64_t f;
     if (get_granule(reinterpret_cast<const uint64_t *>(J.ws + 5 * J.nrec) + 3 * np, (jobs.epoch << 2) | 1u, f))
       *J.d_count = HIC_COUNT_SCAN_TIMEOUT;
@@ -1343,9 +1350,9 @@ int encode_batch16(RleJobs16 &jobs, hipStream_t s) {
   static std::atomic<uint32_t> epoch{0};
   const uint32_t ep = (epoch.fetch_add(1) % ((1u << 30) - 1)) + 1;  // never 0 (zeroed workspace)
   int64_t nparts = 0;
-  for (int k = 0; k < jobs.n; ++k) nparts += (jobs.j[k].nrec + kScanT - 1) / kScanT;
+  for (int k = 0; k < jobs.n; ++k) nparts += (jobs.j[k].nrec + kScan16T - 1) / kScan16T;
   jobs.epoch = ep;
-  hipLaunchKernelGGL(k_rle_scan16b, dim3((unsigned)nparts), dim3(kScanT), 0, s, jobs, ep);
+  hipLaunchKernelGGL(k_rle_scan16b, dim3((unsigned)nparts), dim3(kScan16T), 0, s, jobs, ep);
   if (int e = check_launch("k_rle_scan16b")) return e;
   // persistent: 3 workgroups (12 waves) per CU fit the 51 KB LDS stage and the registers
 #ifndef HIC_EMIT_WPC
@@ -1613,7 +1620,7 @@ extern "C" size_t hic_rle_workspace_bytes(int64_t nblk, int block_len) {
   // >= its 64-block tiles and the generic 256-block tiles)
   const int64_t n = nblk > 0 ? nblk : 1, nt = (n + kWT / 2 - 1) / (kWT / 2);
   // tile records (3), offsets (2) per tile; 3 hand-off granules per scan partition
-  return (size_t)(5 * nt + 3 * ((nt + kScanT - 1) / kScanT) + 8) * sizeof(int64_t);
+  return (size_t)(5 * nt + 3 * ((nt + kScan16T - 1) / kScan16T) + 8) * sizeof(int64_t);
 }
 
 extern "C" int hic_rle_shard_summary_i16(const int16_t *blocks, int64_t nblk, int block_len, void *workspace,

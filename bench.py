@@ -15,8 +15,9 @@ bench.py --gpus N` starts the N ranks itself (torch.multiprocessing, before any
 GPU call in the parent); under torch.distributed.run it joins the given ranks.
   --mode strong (default): ONE 8K image split N ways by block rows; each rank
                  transforms its shard (colour with halo, DCT + quantize + zig-zag +
-                 RLE tile records) and ships its blocks in the lossless 13-bit wire
-                 format (hic_wire_pack_i16, 81.7 MB per 8K image with the records)
+                 RLE tile records) and ships its blocks in the lossless wire format
+                 (hic_wire_pack_i16: per-slot widths proven per table, 637 / 597 bits
+                 per block; 61.1 MB per 8K image with the records)
                  to the image's gathering rank, which unpacks them and runs the
                  scan + emit of the whole image: each timed image ends as ONE
                  encoded stream (codec.jpeg_encode's DC / RLE symbols) on one rank.
@@ -787,7 +788,7 @@ def main():
     mine = [e for e in encs if counts_of(e) is not None]
     symbols = [int(c) for c in counts_of(mine[0]).cpu().tolist()] if mine else None
     wire_flags = [int(e.wire_flag.item()) for e in encs if stream_gather]
-    assert not any(wire_flags), "a coefficient outside the 13-bit wire range"
+    assert not any(wire_flags), "a coefficient outside its wire width"
     # per image: each grouped batch's span / the images it carried
     gather_us = (float(sum(a.elapsed_time(b) for a, b, _ in gather_ev) / sum(n for _, _, n in gather_ev)) * 1e3
                  if gather_ev else None)
@@ -886,7 +887,7 @@ def main():
             wl += ("; %s: %s, block-row tile shards over %d ranks%s"
                    % ("BASELINE configs[3]" if (strong and args.workload == "8k") else "multi-GPU",
                       "one image split N ways" if strong else "one %d-row shard per rank" % H0, world,
-                      (", each image's blocks gathered to one rank in the 13-bit wire format with their RLE "
+                      (", each image's blocks gathered to one rank in the per-slot-width wire format with their RLE "
                        "tile records, where the whole image's DC / RLE stream is coded (image j of each group of "
                        "%d to rank j, the group's gathers in one grouped RCCL batch)" % world) if stream_gather else
                       (", each image's coefficient blocks + DC stream gathered to one rank (image j of each "

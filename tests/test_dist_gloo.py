@@ -146,7 +146,7 @@ def _worker(rank, world, port, H, W, flat, results):
             and np.array_equal(fj[k][1].numpy(), orc.dpcm(zz[k][:, 0].astype(np.int64)).astype(np.int32) - rank)
             for k in pipeline.CHANNELS)
         # (a'') the stream gather (gather_kind "stream", the bench's default): every
-        # rank ships its blocks in the 13-bit wire format (host restatement of
+        # rank ships its blocks in the wire format (host restatement of
         # hic_wire_pack_i16) into the byte ranges of sharding.wire_ranges, image j to
         # rank j in one batch (sharding.gather_blocks_group, the code the GPU path
         # runs); the receiver unpacks, codes the WHOLE stream and must get the

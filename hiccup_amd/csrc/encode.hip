@@ -426,11 +426,11 @@ __device__ __forceinline__ uint32_t wshl1(uint32_t v) {  // lane i <- lane i + 1
 #endif
 // NR input rows: 19 for one 16-row unit, 35 for two vertically adjacent units
 // (VG = 2: the second unit reuses the first's bottom halo rows).
-template <int NR>
+template <int NR, int LA = HIC_ENC_LA, bool PIN_Y = false>
 struct EncColour {
   // rows stream through a ring of kLA + 1 loads in flight (sched_barrier keeps the
   // compiler from hoisting all 19 rows' loads: 114 VGPRs)
-  static constexpr int kLA = HIC_ENC_LA;
+  static constexpr int kLA = LA;
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
   int lane, roff, voff, rlane;  // rlane: the strip's last lane (63 but in a ragged strip)
@@ -509,7 +509,12 @@ struct EncColour {
       ycc8(wd, K, Yh, c);
       // Y rows of the unit(s): input rows 2 .. NR - 2, slot (r - 2) mod 16 (a slot is
       // refilled only after the DCT of its block row has read it)
-      if (r >= 2 && r <= NR - 2) yq[(r - 2) & 15] = make_uint2(ypack4(Yh, 0), ypack4(Yh, 4));
+      if (r >= 2 && r <= NR - 2) {
+        yq[(r - 2) & 15] = make_uint2(ypack4(Yh, 0), ypack4(Yh, 4));
+        // PIN_Y: pack now (the compiler otherwise sinks the packing v_perms to the
+        // DCT and keeps the row's eight Yh dwords live, spilling them at 168 VGPRs)
+        if constexpr (PIN_Y) asm volatile("" : "+v"(yq[(r - 2) & 15].x), "+v"(yq[(r - 2) & 15].y));
+      }
       // neighbour pixels x0 - 2, x0 - 1 (left lane) and x0 + 8 (right lane)
       const uint32_t l2 = set_lane<0>(wshr1(c[6]), __builtin_amdgcn_readlane((int)hal_l2, r));
       const uint32_t l1 = set_lane<0>(wshr1(c[7]), __builtin_amdgcn_readlane((int)hal_l1, r));
@@ -539,7 +544,7 @@ struct EncColour {
 #define HIC_ENC_VG 1  // 16-row units per wave (2: two vertically adjacent units, 35 input rows
                       // for 32; measured 61-65 vs 60-63 us: no gain, scripts/gpu_r2ah.sh)
 #endif
-template <int TMF, bool NT, int DM>
+template <int TMF, bool NT, int DM, bool W3 = false>
 __device__ __forceinline__ void encode420_unit(const Enc420 &E);
 
 // Two register budgets (knob "encode_waves", A/B): 2 waves per SIMD (default: up
@@ -551,14 +556,14 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E);
 // DM: the DCT variant (knob "encode_dct": 0 float64 AAN, 1 scalar float32 enc_dct_f32, 2 packed float32 enc_dct_pk)
 template <int TMF, bool NT, int DM>
 __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_eu(3))) void k_encode420(Enc420 E) {
-  encode420_unit<TMF, NT, DM>(E);
+  encode420_unit<TMF, NT, DM, true>(E);
 }
 template <int TMF, bool NT, int DM>
 __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_eu(2))) void k_encode420_w2(Enc420 E) {
   encode420_unit<TMF, NT, DM>(E);
 }
 
-template <int TMF, bool NT, int DM>
+template <int TMF, bool NT, int DM, bool W3>
 __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
   __shared__ uint2 s_stage[HIC_ENC_WPB * 64 * kStageU2];
   __shared__ uint32_t s_chroma_all[HIC_ENC_WPB][2 * 8 * 64];
@@ -672,9 +677,20 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
   using PD = std::integral_constant<short, HIC_ENC_PRIO_D>;
   static_assert(DM != 2 || HIC_ENC_VG == 1, "the deferred queue marks one unit's records per wave");
   if (live) {
-  EncColour<HIC_ENC_VG == 2 ? 35 : 19> C;
+#ifndef HIC_ENC_LA3
+#define HIC_ENC_LA3 3  // the 3-wave variant's load lookahead (rows)
+#endif
+  EncColour<HIC_ENC_VG == 2 ? 35 : 19, W3 ? HIC_ENC_LA3 : HIC_ENC_LA, W3> C;
   prio(PC{});
   C.init(E, y0, s, lane, nb);
+  if constexpr (W3) {
+    // 3 waves per SIMD (<= 168 VGPRs): all 19 colour rows first, so no DCT runs
+    // while the row ring and the pyrDown window are live (the other waves of the
+    // SIMD hide the loads instead)
+    C.template rows<0, 19>(yq, s_chroma);
+    __builtin_amdgcn_sched_barrier(0);
+    y_blocks(u0, 0);
+  } else {
   C.template rows<0, 10>(yq, s_chroma);  // input rows 2 .. 9 = unit u0's Y block row 0
   __builtin_amdgcn_sched_barrier(0);
   prio(PD{});
@@ -682,6 +698,7 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
   prio(PC{});
   C.template rows<10, 19>(yq, s_chroma);
   __builtin_amdgcn_sched_barrier(0);
+  }
   prio(PD{});
   y_blocks(u0, 1);
   c_blocks(u0);  // before the second unit's chroma rows reuse the LDS area

@@ -547,9 +547,11 @@ struct EncColour {
 template <int TMF, bool NT, int DM, bool W3 = false>
 __device__ __forceinline__ void encode420_unit(const Enc420 &E);
 
-// Two register budgets (knob "encode_waves", A/B): 2 waves per SIMD (default: up
-// to 256 VGPRs, no spills; 63.7 us per 8K launch) or 3 (<= 168 VGPRs: the Y passes
-// spill ~80 dwords per unit; 76 us)
+// Two register budgets (knob "encode_waves"): 3 waves per SIMD (default since round
+// 3: <= 168 VGPRs, the 19 colour rows before the three DCT passes, packed Y rows
+// pinned; ~8 dwords of spill; launch equal to 2 waves, 8K bench 0.1017-0.1041 vs
+// 0.1043-0.1063 ms/step in 5 alternating pairs, profiles/r03/s2/enc_w3/) or 2 (up to
+// 256 VGPRs, the DCT of Y block row 0 between the colour rows 0..9 and 10..18)
 // NT: nontemporal coefficient stores (knob "encode_nt" = 1).  Default 0: plain
 // stores, so part of the coefficients is still in the Infinity Cache when the RLE
 // emit re-reads them (emit 59.7 -> 54.7 us; 8K encode +2-4 %, scripts/gpu_r2i.sh)
@@ -812,9 +814,10 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
   const bool w2 = knob(HIC_KNOB_ENCODE_WAVES) == 2, nt = knob(HIC_KNOB_ENCODE_NT) != 0;
   const int dm = knob(HIC_KNOB_ENCODE_DCT);
   // variants: {2, 3} waves per SIMD x {float64, float32, packed float32} DCT x
-  // {cached, nontemporal} stores (the last at 2 waves and float64 only) x {max_len 15, any}
+  // {cached, nontemporal} stores (nontemporal with float64 only) x {max_len 15, any}
 #define HIC_ENC_VARIANTS(M)                                                 \
   if (nt && w2 && dm == 0) launch(k_encode420_w2<M, true, 0>);              \
+  else if (nt && dm == 0) launch(k_encode420<M, true, 0>);                  \
   else if (w2 && dm == 2) launch(k_encode420_w2<M, false, 2>);              \
   else if (w2 && dm == 1) launch(k_encode420_w2<M, false, 1>);              \
   else if (w2) launch(k_encode420_w2<M, false, 0>);                         \

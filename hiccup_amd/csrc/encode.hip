@@ -389,6 +389,14 @@ __device__ __forceinline__ uint32_t ypack4(const uint32_t (&Yh)[8], int k0) {
   return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
 }
 
+// The lane index made afresh (v_mbcnt), opaque to CSE: the 3-wave kernel would
+// otherwise keep lane-derived values live from the colour stage into the DCT passes
+// and spill them
+__device__ __forceinline__ int fresh_lane() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
 __device__ __forceinline__ uint32_t opv(uint32_t k) {  // a constant held in a VGPR
   asm volatile("" : "+v"(k));
   return k;
@@ -617,10 +625,10 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
     enc_dct_any<0, DM>(w, st, Q, lane < nb, 0, br + 2 * (u - u0), wv, (int)b0 + lane);
     __builtin_amdgcn_wave_barrier();
     int16_t *o = E.coef[0] + b0 * 64;
-    enc_store<NT>(st2, lane, o, o + 32 * 64, nb < 32 ? nb : 32, nb > 32 ? nb - 32 : 0);
+    enc_store<NT>(st2, W3 ? fresh_lane() : lane, o, o + 32 * 64, nb < 32 ? nb : 32, nb > 32 ? nb - 32 : 0);
     if (TMF >= 0 && E.rec[0]) {
       uint32_t zw[32];
-      enc_stage_row(st2, lane, zw);
+      enc_stage_row(st2, W3 ? fresh_lane() : lane, zw);
       tile_record16<TMF>(zw, true, b0 + lane, E.M, E.rec[0] + (b0 >> 6) * 3);
     }
     __builtin_amdgcn_wave_barrier();
@@ -637,10 +645,10 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
     const int64_t b0 = (int64_t)u * nbxc + 32 * s;
     enc_dct_any<1, DM>(w, st, Q, (lane & 31) < (nb >> 1), 1 + (lane >> 5), 2, wv, (int)b0 + (lane & 31));
     __builtin_amdgcn_wave_barrier();
-    enc_store<NT>(st2, lane, E.coef[1] + b0 * 64, E.coef[2] + b0 * 64, nb >> 1, nb >> 1);
+    enc_store<NT>(st2, W3 ? fresh_lane() : lane, E.coef[1] + b0 * 64, E.coef[2] + b0 * 64, nb >> 1, nb >> 1);
     if (TMF >= 0 && E.rec[1]) {
       uint32_t zw[32];
-      enc_stage_row(st2, lane, zw);
+      enc_stage_row(st2, W3 ? fresh_lane() : lane, zw);
       tile_record16_half<TMF>(zw, b0, E.M, E.rec[1] + (b0 >> 5) * 3, E.rec[2] + (b0 >> 5) * 3);
     }
     __builtin_amdgcn_wave_barrier();

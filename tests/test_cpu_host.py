@@ -347,3 +347,18 @@ def test_huffman_flat_tree_matches_walk(golden_codec):
         _walk_flat(child.tolist(), leaves, "10")
     with pytest.raises(AttributeError):
         t.decode_data("10")
+
+
+def test_rle_workspace_covers_scan_partitions():
+    """hic_rle_workspace_bytes (rle.hip) holds, for any channel size and record
+    density (one record per 64-block tile, or per 32-block half tile as the fused
+    encoder's chroma writes them), the records (3 int64), the offsets (2 int64) and
+    the scan's hand-off granules: 3 per 256-record partition + the failure granule
+    (k_rle_scan16b, kScan16T = 256 in the product build)."""
+    lib = _lib.load()
+    for n in (1, 63, 64, 65, 4095, 32400, 129600, 518400, 4194304):
+        have = lib.hic_rle_workspace_bytes(n, 64)
+        for rpt in (1, 2):
+            nrec = -(-n * rpt // 64)
+            need = (5 * nrec + 3 * -(-nrec // 256) + 1) * 8
+            assert have >= need, (n, rpt, have, need)

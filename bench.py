@@ -78,8 +78,10 @@ def parse():
                     help="nccl (= RCCL) for the real multi-GPU run; gloo only to rehearse it")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank on cuda:0 (use with --dist-backend gloo)")
-    ap.add_argument("--streams", type=int, default=2,
-                    help="HIP streams the consecutive images alternate over (each image's chain stays on one)")
+    ap.add_argument("--streams", type=int, default=None,
+                    help="HIP streams the consecutive images alternate over (each image's chain stays on one); "
+                         "default 4 on one GPU (0.1020-0.1028 vs 0.1025-0.1037 ms/step for 2 in 3 alternating "
+                         "pairs, profiles/r03/s2/streams/), 2 with N > 1 ranks")
     ap.add_argument("--unfused", action="store_true",
                     help="A/B: colour and DCT as two kernels (the planes round-trip HBM) instead of hic_encode420_u8")
     ap.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
@@ -687,6 +689,8 @@ def main():
     # consecutive images alternate over the streams (4 rotating encoders: an
     # encoder's buffers are reused only by later work on its own stream when
     # len(streams) divides 4)
+    if args.streams is None:
+        args.streams = 4 if world == 1 else 2
     assert 4 % args.streams == 0, "--streams must be 1, 2 or 4"
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(args.streams - 1)]
     torch.cuda.synchronize()  # inputs / buffers were made on the current stream

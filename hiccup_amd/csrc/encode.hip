@@ -27,9 +27,10 @@
 //      (the strip's edge pixels converted once per unit, one row per lane, and
 //      written into lane 0 / 63 by v_writelane), the vertical taps over a 5-row
 //      window -> 8 chroma rows x 4 columns per lane and plane;
-//   2. DCT of Y block row 0 (between the colour rows 0..9 and 10..18) and row 1
-//      (lane = block): coefficients to the LDS stage at their zig-zag slot,
-//      copied out in 1 KiB stores, the tile record from the stage;
+//   2. DCT of Y block row 0 and row 1 (lane = block; after all 19 colour rows in
+//      the default 3-waves-per-SIMD kernel, between the colour rows 0..9 and
+//      10..18 in the 2-wave one): coefficients to the LDS stage at their zig-zag
+//      slot, copied out in 1 KiB stores, the tile record from the stage;
 //   3. chroma: the colour stage left the chroma rows in a 4 KiB LDS area per wave;
 //      chroma block m of Cr is read into lane m and of Cb into lane 32 + m (a
 //      block spans the columns of lanes 2m, 2m + 1), one DCT pass with the

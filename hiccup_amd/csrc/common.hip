@@ -16,7 +16,7 @@ int knob(int k) {
     case HIC_KNOB_COLOR_SEG: return 8;
     case HIC_KNOB_RLE_NT: return 1;
     case HIC_KNOB_ENCODE_WAVES: return 3;
-    case HIC_KNOB_ENCODE_NT: return 0;
+    case HIC_KNOB_ENCODE_NT: return 1;
     default: return k == HIC_KNOB_DCT_WAVES_PER_CU ? -1 : 0;
   }
 }

@@ -561,9 +561,12 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E);
 // pinned; ~8 dwords of spill; launch equal to 2 waves, 8K bench 0.1017-0.1041 vs
 // 0.1043-0.1063 ms/step in 5 alternating pairs, profiles/r03/s2/enc_w3/) or 2 (up to
 // 256 VGPRs, the DCT of Y block row 0 between the colour rows 0..9 and 10..18)
-// NT: nontemporal coefficient stores (knob "encode_nt" = 1).  Default 0: plain
-// stores, so part of the coefficients is still in the Infinity Cache when the RLE
-// emit re-reads them (emit 59.7 -> 54.7 us; 8K encode +2-4 %, scripts/gpu_r2i.sh)
+// NT: nontemporal coefficient stores (knob "encode_nt", default 1 since round 3).
+// With 2 waves and 2 images in flight plain stores were better (part of the
+// coefficients still in the Infinity Cache for the RLE emit: emit 59.7 -> 54.7 us,
+// 8K encode +2-4 %, scripts/gpu_r2i.sh); with 3 waves and 4 images in flight
+// nontemporal stores win (0.0999-0.1033 vs 0.1041-0.1051 ms/step, 3 alternating
+// pairs, profiles/r03/s2/nt/)
 // DM: the DCT variant (knob "encode_dct": 0 float64 AAN, 1 scalar float32 enc_dct_f32, 2 packed float32 enc_dct_pk)
 template <int TMF, bool NT, int DM>
 __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_eu(3))) void k_encode420(Enc420 E) {

@@ -377,9 +377,10 @@ def _structured_rgb(kind, H, W, seed):
     raise ValueError(kind)
 
 
-@pytest.mark.parametrize("variant", [{}, {"encode_dct": 1}, {"encode_waves": 3}, {"encode_dct": 1, "encode_waves": 3},
+# (defaults: 3 waves per SIMD, float64 DCT, nontemporal coefficient stores)
+@pytest.mark.parametrize("variant", [{}, {"encode_dct": 1}, {"encode_waves": 2}, {"encode_dct": 1, "encode_waves": 2},
                                      {"encode_dct": 2}, {"encode_dct": 2, "encode_waves": 3}, {"encode_dct": 2, "encode_waves": 2},
-                                     {"encode_nt": 1}])
+                                     {"encode_nt": 0}, {"encode_nt": 0, "encode_waves": 2}])
 @pytest.mark.parametrize("kind", ["random", "levels", "colour_levels", "blocks", "flat"])
 @pytest.mark.parametrize("H,W", [(16, 512), (144, 2048), (1088, 1536)])
 def test_fused_encoder_matches_two_kernel_chain(kind, H, W, variant):
@@ -401,7 +402,7 @@ def test_fused_encoder_matches_two_kernel_chain(kind, H, W, variant):
     np.testing.assert_array_equal(got.shard_summaries().cpu().numpy(), exp.shard_summaries().cpu().numpy())
 
 
-@pytest.mark.parametrize("variant", [{}, {"encode_dct": 2}, {"encode_waves": 3}, {"encode_nt": 1}])
+@pytest.mark.parametrize("variant", [{}, {"encode_dct": 2}, {"encode_waves": 2}, {"encode_nt": 0}])
 @pytest.mark.parametrize("kind", ["random", "levels", "blocks", "flat"])
 @pytest.mark.parametrize("H,W", [(2160, 3840), (1088, 1920), (32, 528), (48, 16), (16, 1040)])
 def test_fused_encoder_ragged_matches_chain(kind, H, W, variant):

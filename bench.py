@@ -292,6 +292,52 @@ def extra_8k_plane_dct(steps=24, luma_only=False, floor_us=None):
     return out
 
 
+def extra_8k_luma_batched(nplanes=8, steps=12):
+    """north_star's DCT+quantize pass measured the way the product runs planes back to
+    back: ONE hic_dct_quant_rle_u8_batch launch over `nplanes` 8K luminance planes of
+    consecutive images (each 4320 x 7680 uint8 -> quantized int16 zig-zag blocks + RLE
+    tile records), >= 1.2 GB rotating, timed by the launch's own events; the figure
+    is launch time / nplanes (the per-launch ramp and tail amortised over the batch).
+    Per-launch spread (min / median / max) is reported beside it."""
+    from hiccup_amd import _lib, device
+    h, w = H8K, W8K
+    px = h * w
+    per_set = nplanes * 3 * px
+    rot = max(2, int(np.ceil(ROT_BYTES / per_set)))
+    g = torch.Generator(device="cuda")
+    g.manual_seed(12)
+    nblk = px // 64
+    sets = []
+    for _ in range(rot):
+        planes = [torch.randint(0, 256, (h, w), dtype=torch.uint8, device="cuda", generator=g) for _ in range(nplanes)]
+        outs = [device.empty((nblk, 64), torch.int16) for _ in range(nplanes)]
+        wss = [device.workspace(_lib.load().hic_rle_workspace_bytes(nblk, 64)) for _ in range(nplanes)]
+        jobs = (_lib.DctPlaneJob * nplanes)()
+        for i in range(nplanes):
+            jobs[i] = _lib.DctPlaneJob(planes[i].data_ptr(), h, w, w, 0, outs[i].data_ptr(), wss[i].data_ptr())
+        sets.append((planes, outs, wss, jobs))
+    evs = [device.KernelEvents() for _ in range(steps)]
+    for i in range(3):
+        _lib.call("hic_dct_quant_rle_u8_batch", nplanes, sets[i % rot][3], 15, device.stream_ptr(), None, None)
+    for i, e in enumerate(evs):
+        _lib.call("hic_dct_quant_rle_u8_batch", nplanes, sets[(3 + i) % rot][3], 15, device.stream_ptr(), e.start,
+                  e.stop)
+    torch.cuda.synchronize()
+    ts = np.array([e.elapsed_ms() for e in evs]) * 1e3
+    us = float(np.median(ts)) / nplanes
+    gbs = 3 * px / (us * 1e-6) / 1e9
+    del sets
+    torch.cuda.empty_cache()
+    return {"workload": "%d x 8K luminance planes (4320 x 7680 uint8, consecutive images) per launch -> quantized "
+                        "int16 zig-zag blocks + RLE tile records: north_star's DCT+quantize pass back to back "
+                        "(SURVEY.md 8(d): >= 0.70 = <= 17.8 us per plane)" % nplanes,
+            "kernel": "k_dct_mfma<15>" if _lib.get_knob("dct_path") == _lib.DCT_PATH_MFMA else "k_dct_planes<-1,ZIGZAG_I16,15>",
+            "planes_per_launch": nplanes, "us_per_plane": round(us, 2),
+            "launch_us_min_med_max": [round(float(v), 2) for v in (ts.min(), np.median(ts), ts.max())],
+            "achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_plane": 3 * px,
+            "timed_launches": steps}
+
+
 def measure_floors(steps=20):
     """In-run memory floors (hic_probe_copy / hic_probe_plane, memory-only probes in
     the product library), each timed by the launches' own HIP events over >= 1.2 GB

@@ -25,6 +25,7 @@
 #include <stdlib.h>
 
 #include "dct_core.h"
+#include "dct_mfma_tables.h"
 #include "rle_core.h"
 
 namespace hic {
@@ -388,8 +389,9 @@ struct DctJob {
   int64_t *tiles;
   int W, nbx, nblk, nsets, set0, table;
 };
+constexpr int kMaxPlaneJobs = 16;  // planes per launch (hic_dct_quant_rle_u8_batch)
 struct DctJobs {
-  DctJob j[3];
+  DctJob j[kMaxPlaneJobs];
   int n, total_sets, M;
 };
 
@@ -597,642 +599,273 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DCT_WPE
 }
 
 // ---------------------------------------------------------------------------
-// Production forward kernel (aligned planes): the float32 fast path of
-// dct_core.h (dct_block_f32) with its two fallbacks.
-//  * tier 1: float32 AAN per block (one block per lane, 64 consecutive blocks =
-//    one set = one RLE tile per wave iteration), quantised with proven tie
-//    windows (dct_windows.h); a coefficient outside its window is final.
-//  * tier 2: every flagged coefficient (~0.03 per block on random data) is
-//    queued in LDS (block, plane, raster index) and resolved 64 at a time, one
-//    per lane, by resolve_coef (float64 dot product; pocketfft's own operations
-//    for (4,4) and the (2,2) class).  Deferred items patch the already stored
-//    coefficient in HBM.  A flagged coefficient whose candidates straddle zero
-//    ("zero-ambiguous") would change the set's RLE tile record, so such a set
-//    drains the queue before its store; items of the set being built then land
-//    in its LDS stage.
-//  * tier 3: a coefficient inside the float64 window that tier 2 cannot settle,
-//    or a set that overflows the queue, has its whole set recomputed after the
-//    main loop on the exact pocketfft replica (dct_block_2ph).
-// Coefficients go to an LDS stage at their output slot and leave in 1 KiB
-// contiguous (nontemporal) stores; the set's RLE tile record is computed from the
-// stage (TMF >= 0).  Persistent grid; each wave keeps <= 64 sets (redo mask).
-constexpr int kQCap = 32;  // queued items per wave (one resolve round)
-constexpr int kPSlots = 16;  // pixel slots per wave: 64 B copies of the flagged blocks' pixels
+// Integer-MFMA forward kernel (production path for aligned planes, dct_path 5).
+// The 2-D DCT-II + quantiser of a block is one linear map of its 64 centred
+// pixels, so a wave evaluates it for 16 blocks at a time as a [64 slots x 64
+// pixels] . [64 pixels x 16 blocks] contraction on the matrix cores
+// (v_mfma_i32_16x16x64_i8), in exact integer arithmetic:
+//  * x = p XOR 0x80 is the centred pixel p - 128 as an int8 (no conversion);
+//  * A[z][k] = round(2^32 C_uv,k / T_uv) (rows in zig-zag order, the table folded
+//    in; tools/check/dct_mfma.py, dct_mfma_tables.h) is split into four balanced
+//    base-256 digits, one MFMA each: S_d = sum_k a_d[z][k] x_k, exact in int32;
+//  * the digits combine with two truncating shifts fed back through the MFMA's
+//    accumulator input (D0 = S0 + c0, D1 = S1 + (D0 >> 8), D2 = S2 + (S3 << 8) +
+//    2^15, R = (D2 << 3) + (D1 >> 5)): R / 2^19 estimates y/T + 1/2 within the
+//    proven window, q = R >> 19;
+//  * R mod 2^19 < kMfmaL flags a coefficient whose rounding the estimate cannot
+//    decide (~3.5e-4 per block on random data).  The DC row is 2^30 for both
+//    tables: the exact pixel sum, rounded in integers (dc_quant).  Luminance (4,4)
+//    is y/T = K/34, flagged exactly at its ties (~3 % of blocks): the wave resolves
+//    them in place with pocketfft's own roundings (pf_y44 on the rows' signed sums,
+//    one v_dot4 per row half).  A set with any other flag is recomputed after the
+//    main loop on the float64 AAN path (dct_block_aan, with its own fallbacks).
+// Per 16 blocks: 16 MFMAs and ~6.5 VALU per coefficient (2 shifts, 2 shift-adds,
+// half a v_perm and half a v_pk_ashrrev_i16 to pack q, v_and + half a v_min3 for
+// the flag), against ~18 float64 operations per coefficient on the AAN path.
+// Output slot layout: lane (n = lane & 15, g = lane >> 4) of M-tile mt holds slots
+// 16 mt + 4 g .. + 3 of block n: one 8-byte LDS store into the stage, which leaves
+// in 1 KiB nontemporal stores (and feeds the RLE tile record) as in k_dct_planes.
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef int16_t s16x2 __attribute__((ext_vector_type(2)));
 
-__constant__ int8_t kZZInv[64] = {0,  2,  3,  9,  10, 20, 21, 35, 1,  4,  8,  11, 19, 22, 34, 36,
-                                  5,  7,  12, 18, 23, 33, 37, 48, 6,  13, 17, 24, 32, 38, 47, 49,
-                                  14, 16, 25, 31, 39, 46, 50, 57, 15, 26, 30, 40, 45, 51, 56, 58,
-                                  27, 29, 41, 44, 52, 55, 59, 62, 28, 42, 43, 53, 54, 60, 61, 63};
+constexpr int32_t mfma_digit(int32_t a, int d) {
+  for (int k = 0; k < d; ++k) {
+    const int32_t dk = ((a + 128) & 255) - 128;
+    a = (a - dk) / 256;  // exact
+  }
+  return d < 3 ? ((a + 128) & 255) - 128 : a;
+}
 
-// Wave-level pieces shared by the main loop and the cold paths.  `sj` is the
-// workgroup's LDS copy of the jobs (cold paths index it per lane).
-struct F32Wave {
-  const DctJob *sj;
-  uint2 *st2;  // this wave's stage: 64 rows of kStageU2 x 8 B
-  uint2 *qu;   // this wave's item queue: {block, plane << 16 | pixel slot << 8 | raster index}
-  uint4 *pix;  // this wave's pixel slots: 4 x 16 B per flagged block
-  const double *cm;      // LDS copies of the fallback's constants (cos2 table,
-  const uint8_t *qt;     // QT[2][64], kZZInv): per-lane lookups without memory latency
-  const int8_t *zz;
-  int lane, g0, nwaves, M;
+// A's digits in MFMA fragment order: w[t][mt][d][lane][c] = dword c of lane
+// `lane`'s A operand for M-tile mt (slots 16 mt ..), digit d.  Byte j of lane
+// (zl = lane & 15, g = lane >> 4) is digit d of A[t][16 mt + zl][16 g + j]: pixel
+// 16 g + j = row 2 g + j / 8, column j % 8 -- the same (g, j) the B operand's
+// pixel rows use.
+struct MfmaFrag {
+  uint32_t w[2][4][4][64][4];
+  constexpr MfmaFrag() : w() {
+    for (int t = 0; t < 2; ++t)
+      for (int mt = 0; mt < 4; ++mt)
+        for (int d = 0; d < 4; ++d)
+          for (int l = 0; l < 64; ++l)
+            for (int c = 0; c < 4; ++c) {
+              uint32_t v = 0;
+              for (int b = 0; b < 4; ++b) {
+                const int32_t a = kMfmaA[t][16 * mt + (l & 15)][16 * (l >> 4) + 4 * c + b];
+                v |= (uint32_t)(uint8_t)(int8_t)mfma_digit(a, d) << (8 * b);
+              }
+              w[t][mt][d][l][c] = v;
+            }
+  }
 };
+__device__ const MfmaFrag kMfmaFragDev{};
 
-__device__ __forceinline__ uint4 stage16(const uint2 *st2, int b, int k) {
-  const uint2 lo = st2[b * kStageU2 + 2 * k], hi = st2[b * kStageU2 + 2 * k + 1];
-  return make_uint4(lo.x, lo.y, hi.x, hi.y);
+__device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
+  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
 }
 
-// stage -> output layout (+ the set's RLE tile record)
-template <int LAYOUT, int TMF>
-__device__ __forceinline__ void f32_store(const F32Wave &V, const DctJob &J, int set) {
-  const int lane = V.lane;
+// pocketfft's half-scaled y'[4][4] from the rows' signed sums k_r (pf_y44 with the
+// integer prefix done): a luminance (4,4) tie is decided by these roundings
+__device__ __forceinline__ double pf_y44_k(const int (&k)[8]) {
+  double y[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) y[r] = (double)k[r] * TW3;
+  const double c1 = y[1] + y[2], c3 = y[3] + y[4], c5 = y[5] + y[6], H0 = y[0] + y[7];
+  const double h1 = c1 + c5, T2 = H0 + c3;
+  return (T2 - h1) * TW3;
+}
+
+// stage (this wave's 64 rows) -> ZIGZAG_I16 output (+ the set's RLE tile record)
+template <int TMF>
+__device__ __forceinline__ void mfma_store(const DctJob &J, int set, const uint2 *st2, int lane, int M) {
   __builtin_amdgcn_wave_barrier();
   const int blk = set * 64 + lane;
-  if (LAYOUT == HIC_LAYOUT_ZIGZAG_I16) {
-    uint4 *o = reinterpret_cast<uint4 *>(static_cast<int16_t *>(J.out) + (int64_t)set * 64 * 64);
-    auto sv = [&](int k) { return stage16(V.st2, 8 * k + (lane >> 3), lane & 7); };
-    if ((set + 1) * 64 <= J.nblk) {
-      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  auto st16 = [&](int b, int k) {
+    const uint2 lo = st2[b * kStageU2 + 2 * k], hi = st2[b * kStageU2 + 2 * k + 1];
+    return make_uint4(lo.x, lo.y, hi.x, hi.y);
+  };
+  uint4 *o = reinterpret_cast<uint4 *>(static_cast<int16_t *>(J.out) + (int64_t)set * 64 * 64);
+  auto sv = [&](int k) { return st16(8 * k + (lane >> 3), lane & 7); };
+  if ((set + 1) * 64 <= J.nblk) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint4 t = sv(k);
-        const u32x4 v = {t.x, t.y, t.z, t.w};
-        __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(o + 64 * k + lane));
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (set * 64 + 8 * k + (lane >> 3) < J.nblk) o[64 * k + lane] = sv(k);
+    for (int k = 0; k < 8; ++k) {
+      const uint4 t = sv(k);
+      const u32x4 v = {t.x, t.y, t.z, t.w};
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(o + 64 * k + lane));
     }
-    if (TMF >= 0) {
-      uint32_t zw[32];
+  } else {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint4 t = stage16(V.st2, lane, k);
-        zw[4 * k] = t.x; zw[4 * k + 1] = t.y; zw[4 * k + 2] = t.z; zw[4 * k + 3] = t.w;
-      }
-      tile_record16<TMF>(zw, blk < J.nblk, blk, V.M, J.tiles + (int64_t)set * 3);
+    for (int k = 0; k < 8; ++k)
+      if (set * 64 + 8 * k + (lane >> 3) < J.nblk) o[64 * k + lane] = sv(k);
+  }
+  if (TMF >= 0) {
+    uint32_t zw[32];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint4 t = st16(lane, k);
+      zw[4 * k] = t.x; zw[4 * k + 1] = t.y; zw[4 * k + 2] = t.z; zw[4 * k + 3] = t.w;
     }
-  } else if (blk < J.nblk) {
-    const int bi = blk / J.nbx, bj = blk - bi * J.nbx;
-    if (LAYOUT == HIC_LAYOUT_RASTER_I16) {
-      int16_t *o = static_cast<int16_t *>(J.out) + (int64_t)bi * 8 * J.W + bj * 8;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) *reinterpret_cast<uint4 *>(o + (int64_t)u * J.W) = stage16(V.st2, lane, u);
-    } else {
-      int32_t *o = static_cast<int32_t *>(J.out) + (int64_t)bi * 8 * J.W + bj * 8;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const uint4 t = stage16(V.st2, lane, u);
-        const uint32_t wd[4] = {t.x, t.y, t.z, t.w};
-        int q[8];
-#pragma unroll
-        for (int v = 0; v < 8; ++v) q[v] = (int)(int16_t)(wd[v >> 1] >> (16 * (v & 1)));
-        int4 *row = reinterpret_cast<int4 *>(o + (int64_t)u * J.W);
-        row[0] = make_int4(q[0], q[1], q[2], q[3]);
-        row[1] = make_int4(q[4], q[5], q[6], q[7]);
-      }
-    }
+    tile_record16<TMF>(zw, blk < J.nblk, blk, M, J.tiles + (int64_t)set * 3);
   }
   __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ void load_set(const DctJob &J, int set, int lane, uint2 (&w)[8]) {
-  const int blk = set * 64 + lane;
-  const int cblk = blk < J.nblk ? blk : J.nblk - 1;
-  const int bi = cblk / J.nbx, bj = cblk - bi * J.nbx;
-  const uint8_t *p = J.plane + (int64_t)bi * 8 * J.stride + bj * 8;
-#pragma unroll
-  for (int r = 0; r < 8; ++r) w[r] = *reinterpret_cast<const uint2 *>(p + r * J.stride);
-}
-
-// Tier 2 (cold): resolve the n <= kQCap queued items, one per lane,
-// reading each block's pixels from its LDS slot (no memory latency).  (cur_kj,
-// cur_set): the set whose stage is not stored yet (-1: none); its items land in
-// the stage, earlier sets' items patch HBM.  Returns the wave's tier-3 bits.
-template <int LAYOUT>
-__device__ __forceinline__ uint64_t f32_round(const F32Wave &V, int n, int cur_kj, int cur_set) {
-  const int lane = V.lane;
-  const bool act = lane < n;
-  const uint2 it = act ? V.qu[lane] : make_uint2(0u, 0u);
-  const int blk = (int)it.x, kj = (int)(it.y >> 16), slot = (int)((it.y >> 8) & 0xFFu), i = (int)(it.y & 63u);
-  bool t3 = false;
-  if (act) {
-    const DctJob &J = V.sj[kj];
-    uint2 w[8];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint4 t = V.pix[slot * 4 + k];
-      w[2 * k] = make_uint2(t.x, t.y);
-      w[2 * k + 1] = make_uint2(t.z, t.w);
-    }
-    int q = 0;
-    if (resolve_coef(w, J.table, i, q, V.cm, V.qt)) {
-      const int zs = LAYOUT == HIC_LAYOUT_ZIGZAG_I16 ? (int)V.zz[i] : i;
-      if (kj == cur_kj && (blk >> 6) == cur_set) {
-        reinterpret_cast<int16_t *>(V.st2 + (blk & 63) * kStageU2)[zs] = (int16_t)q;
-      } else {
-        // this wave stored the set earlier; a wave's stores to one address complete
-        // in program order, so the patch lands after it (no fence: a wait here
-        // would also stall on the next set's prefetch)
-        if (LAYOUT == HIC_LAYOUT_ZIGZAG_I16) {
-          static_cast<int16_t *>(J.out)[(int64_t)blk * 64 + zs] = (int16_t)q;
-        } else {
-          const int bi = blk / J.nbx, bj = blk - bi * J.nbx;
-          const int64_t at = (int64_t)(bi * 8 + (i >> 3)) * J.W + bj * 8 + (i & 7);
-          if (LAYOUT == HIC_LAYOUT_RASTER_I16)
-            static_cast<int16_t *>(J.out)[at] = (int16_t)q;
-          else
-            static_cast<int32_t *>(J.out)[at] = q;
-        }
-      }
-    } else {
-      t3 = true;
-    }
-  }
-  uint64_t redo = 0;
-  uint64_t m = __builtin_amdgcn_ballot_w64(t3);
-  while (m) {  // rare: the item's whole set goes to the exact replica
-    const int l = __builtin_ctzll(m);
-    m &= m - 1;
-    const int kl = __builtin_amdgcn_readlane(kj, l), bl = __builtin_amdgcn_readlane(blk, l);
-    const int g = V.sj[kl].set0 + (bl >> 6);
-    redo |= 1ull << ((g - V.g0) / V.nwaves);
-  }
-  __builtin_amdgcn_wave_barrier();
-  return redo;
-}
-
-// Tier 3 (cold, out of line): set `set` of job kj on the exact pocketfft replica.
-template <int LAYOUT, int TMF>
-__device__ __attribute__((noinline)) void f32_exact_set(const F32Wave &V, int kj, int set) {
-  const DctJob &J = V.sj[kj];
-  uint2 w[8];
-  load_set(J, set, V.lane, w);
-  int16_t *st = reinterpret_cast<int16_t *>(V.st2 + V.lane * kStageU2);
-  if (J.table == 0)
-    dct_block_2ph<0, LAYOUT>(w, st);
-  else
-    dct_block_2ph<1, LAYOUT>(w, st);
-  f32_store<LAYOUT, TMF>(V, J, set);
-}
-
-// Queue this set's flagged coefficients (cold, after the block pass):
-// bit i of (fhi:flo) = raster index i of this lane's block is flagged.  Each
-// flagged block's pixels go to an LDS slot; its items {block, plane << 16 | slot
-// << 8 | i} to the queue.  Returns qn | ns << 8, or -1 if the queue or the slots
-// would overflow (the set then goes to tier 3).
-template <int LAYOUT>
-__device__ __forceinline__ int f32_enqueue(const F32Wave &V, int qn, int ns, int blk, int kj, uint32_t flo,
-                                                     uint32_t fhi, uint2 w0, uint2 w1, uint2 w2, uint2 w3, uint2 w4,
-                                                     uint2 w5, uint2 w6, uint2 w7) {
-  const bool has = (flo | fhi) != 0;
-  const uint64_t hm = __builtin_amdgcn_ballot_w64(has);
-  const int nb = __builtin_popcountll(hm);
-  int cnt = __builtin_popcountll(((uint64_t)fhi << 32) | flo);
-  // total items this set (wave sum of cnt)
-  int tot = 0;
-  for (uint64_t m = hm; m; m &= m - 1) tot += __builtin_amdgcn_readlane(cnt, __builtin_ctzll(m));
-  if (qn + tot > kQCap || ns + nb > kPSlots) return -1;
-  const int slot = ns + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
-  if (has) {
-    uint4 *p = V.pix + slot * 4;
-    p[0] = make_uint4(w0.x, w0.y, w1.x, w1.y);
-    p[1] = make_uint4(w2.x, w2.y, w3.x, w3.y);
-    p[2] = make_uint4(w4.x, w4.y, w5.x, w5.y);
-    p[3] = make_uint4(w6.x, w6.y, w7.x, w7.y);
-  }
-  uint64_t bits = ((uint64_t)fhi << 32) | flo;
-  while (__builtin_amdgcn_ballot_w64(bits != 0)) {  // one item per lane per pass
-    const bool on = bits != 0;
-    const uint64_t m = __builtin_amdgcn_ballot_w64(on);
-    if (on) {
-      const int i = __builtin_ctzll(bits);
-      bits &= bits - 1;
-      const int pos = qn + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      V.qu[pos] = make_uint2((uint32_t)blk, (uint32_t)(kj << 16 | slot << 8 | i));
-    }
-    qn += __builtin_popcountll(m);
-  }
-  __builtin_amdgcn_wave_barrier();
-  return qn | (ns + nb) << 8;
-}
-
-template <int LAYOUT, int TMF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_dct_f32(DctJobs jobs, int dev) {
-#ifdef HIC_DEV
-  // dev timing bits (results invalid): 1 drop tier 2, 2 no pre-store drains, 4 no
-  // stores, 8 no pixel loads, 16 no DCT, 32 queue but never resolve
-  const int dv = dev;
-#else
-  constexpr int dv = 0;
-  (void)dev;
-#endif
+template <int TMF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_dct_mfma(DctJobs jobs) {
   __shared__ uint2 s_stage[4 * 64 * kStageU2];
-  __shared__ uint2 s_queue[4 * kQCap];
-  __shared__ uint4 s_pix[4 * kPSlots * 4];
-  __shared__ DctJob s_jobs[3];
-  __shared__ double s_cm[64];
-  __shared__ uint8_t s_qt[128];
-  __shared__ int8_t s_zz[64];
-  if (threadIdx.x < 3) s_jobs[threadIdx.x] = jobs.j[threadIdx.x < jobs.n ? threadIdx.x : 0];
-  if (threadIdx.x < 64) s_cm[threadIdx.x] = cos2(kCm, threadIdx.x >> 3, threadIdx.x & 7);
-  if (threadIdx.x < 128) s_qt[threadIdx.x] = (uint8_t)QT[threadIdx.x >> 6][threadIdx.x & 63];
-  if (threadIdx.x < 64) s_zz[threadIdx.x] = kZZInv[threadIdx.x];
-  __syncthreads();
+  __shared__ int2 s_k44[4 * 64 * 4];  // (4,4) tie path: the 8 signed row sums per block
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  F32Wave V;
-  V.sj = s_jobs;
-  V.st2 = s_stage + wv * 64 * kStageU2;
-  V.qu = s_queue + wv * kQCap;
-  V.pix = s_pix + wv * kPSlots * 4;
-  V.cm = s_cm;
-  V.qt = s_qt;
-  V.zz = s_zz;
-  V.lane = lane;
-  V.nwaves = gridDim.x * 4;
-  V.g0 = blockIdx.x * 4 + wv;
-  V.M = jobs.M;
-  const int g0 = V.g0, nwaves = V.nwaves;
-  int16_t *st = reinterpret_cast<int16_t *>(V.st2 + lane * kStageU2);
-  auto job_of = [&](int g) {
-    g = __builtin_amdgcn_readfirstlane(g);
+  const int nwaves = gridDim.x * 4;
+  const int g0 = blockIdx.x * 4 + wv;
+  uint2 *st2 = s_stage + wv * 64 * kStageU2;
+  int2 *k44 = s_k44 + wv * 64 * 4;
+  const int n = lane & 15, g = lane >> 4;
+  const int M = jobs.M;
+  auto job_of = [&](int gi) {
+    gi = __builtin_amdgcn_readfirstlane(gi);
     int k = 0;
-    while (k + 1 < jobs.n && g >= jobs.j[k + 1].set0) ++k;
+    while (k + 1 < jobs.n && gi >= jobs.j[k + 1].set0) ++k;
     return __builtin_amdgcn_readfirstlane(k);
   };
-
+  const i32x4 c0v = {kMfmaC0, kMfmaC0, kMfmaC0, kMfmaC0}, zero = {0, 0, 0, 0};
+  const uint32_t dcmask = g == 0 ? 0x7FFFFu : 0u;
   uint64_t redo = 0;
-  int qn = 0, ns = 0;  // queued items, used pixel slots (wave-uniform)
-  int k = 0;
+  int i = 0;
   if (g0 < jobs.total_sets) {
     int kj = job_of(g0);
     DctJob J = jobs.j[kj];
     int next0 = kj + 1 < jobs.n ? jobs.j[kj + 1].set0 : jobs.total_sets;
-    // software pipeline: the next set's pixels are loaded while this one computes
-    uint2 wn[8];
-    if (dv & 8) {
-#pragma unroll
-      for (int r = 0; r < 8; ++r) wn[r] = make_uint2(0x9E3779B1u * (lane + r), 0x85EBCA6Bu * (lane ^ r));
-    } else {
-      load_set(J, g0 - J.set0, lane, wn);
-    }
-    for (int g = g0; g < jobs.total_sets; g += nwaves, ++k) {
-      if (g >= next0) {
-        kj = job_of(g);
+    int table = -1;
+    i32x4 A[4][4];
+    for (int gs = g0; gs < jobs.total_sets; gs += nwaves, ++i) {
+      if (gs >= next0) {
+        kj = job_of(gs);
         J = jobs.j[kj];
         next0 = kj + 1 < jobs.n ? jobs.j[kj + 1].set0 : jobs.total_sets;
       }
-      const int set = g - J.set0;
-      uint2 w[8];
+      if (J.table != table) {  // wave-uniform: this plane's matrix digits
+        table = J.table;
+        const uint4 *f = reinterpret_cast<const uint4 *>(&kMfmaFragDev.w[table][0][0][0][0]);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) w[r] = wn[r];
-      const int gn = g + nwaves;
-      if (gn < jobs.total_sets && !(dv & 8)) {
-        const int kn = gn >= next0 ? job_of(gn) : kj;
-        load_set(jobs.j[kn], gn - jobs.j[kn].set0, lane, wn);
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            const uint4 v = f[(mt * 4 + d) * 64 + lane];
+            A[mt][d] = i32x4{(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+          }
       }
-      const int blk = set * 64 + lane;
-      bool zamb = false;
-      // per column: one uniform branch on the wave's flags of its 8 coefficients;
-      // flagged raster indices collect in a per-lane 64-bit mask (bit u*8+v)
-      uint32_t flo = 0, fhi = 0;
-      bool zl = false;  // this lane has a zero-ambiguous flag: candidates rint(e) and
-                        // rint(e) +- 1 (toward d) straddle zero
-      auto sink = [&](int v, const float (&rr)[8], const float (&d)[8], const bool (&f)[8]) {
-        const bool any = f[0] | f[1] | f[2] | f[3] | f[4] | f[5] | f[6] | f[7];
-        if (__builtin_amdgcn_ballot_w64(any)) {
-          const uint32_t lo = (uint32_t)f[0] | (uint32_t)f[1] << 8 | (uint32_t)f[2] << 16 | (uint32_t)f[3] << 24;
-          const uint32_t hi = (uint32_t)f[4] | (uint32_t)f[5] << 8 | (uint32_t)f[6] << 16 | (uint32_t)f[7] << 24;
-          flo |= lo << v;
-          fhi |= hi << v;
+      const int set = gs - J.set0;
+      // pixels: lane (n, g) of N-tile nt holds rows 2g, 2g + 1 of block 16 nt + n
+      i32x4 B[4];
 #pragma unroll
-          for (int u = 0; u < 8; ++u)
-            zl |= f[u] && (rr[u] == 0.f || (rr[u] == 1.f && d[u] < 0.f) || (rr[u] == -1.f && d[u] > 0.f));
+      for (int nt = 0; nt < 4; ++nt) {
+        const int blk = set * 64 + 16 * nt + n;
+        const int cblk = blk < J.nblk ? blk : J.nblk - 1;
+        const int bi = cblk / J.nbx, bj = cblk - bi * J.nbx;
+        const uint8_t *p = J.plane + (int64_t)(bi * 8 + 2 * g) * J.stride + bj * 8;
+        const uint2 r0 = *reinterpret_cast<const uint2 *>(p), r1 = *reinterpret_cast<const uint2 *>(p + J.stride);
+        B[nt] = i32x4{(int)(r0.x ^ 0x80808080u), (int)(r0.y ^ 0x80808080u), (int)(r1.x ^ 0x80808080u),
+                      (int)(r1.y ^ 0x80808080u)};
+      }
+      const uint32_t z44mask = (g == 1 && table == 0) ? 0x7FFFFu : 0u;
+      uint32_t fmin = 0xFFFFFFFFu;
+      uint64_t m44 = 0;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        uint2 *row = st2 + (16 * nt + n) * kStageU2 + g;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const i32x4 D0 = mfma_i8(A[mt][0], B[nt], c0v);
+          const i32x4 D3 = mfma_i8(A[mt][3], B[nt], zero);
+          const i32x4 D1 = mfma_i8(A[mt][1], B[nt], D0 >> 8);
+          const i32x4 D2 = mfma_i8(A[mt][2], B[nt], (D3 << 8) + 32768);
+          const i32x4 R = (D2 << 3) + (D1 >> 5);
+          uint32_t f0 = (uint32_t)R.x & 0x7FFFFu, f3 = (uint32_t)R.w & 0x7FFFFu;
+          if (mt == 0) f0 |= dcmask;
+          if (mt == 2) {
+            if (table == 0) {
+              const uint64_t b = __builtin_amdgcn_ballot_w64(g == 1 && f3 < kMfmaL);
+              m44 |= ((b >> 16) & 0xFFFFull) << (16 * nt);
+            }
+            f3 |= z44mask;
+          }
+          fmin = min(min(fmin, f0), (uint32_t)R.y & 0x7FFFFu);  // v_min3_u32
+          fmin = min(min(fmin, (uint32_t)R.z & 0x7FFFFu), f3);
+          // q = R >> 19 as int16 pairs: the high halves, then >> 3 per half
+          s16x2 q01 = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm((uint32_t)R.y, (uint32_t)R.x, 0x07060302u));
+          s16x2 q23 = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm((uint32_t)R.w, (uint32_t)R.z, 0x07060302u));
+          q01 = q01 >> (s16x2){3, 3};
+          q23 = q23 >> (s16x2){3, 3};
+          uint32_t w01 = __builtin_bit_cast(uint32_t, q01);
+          if (mt == 0) {
+            // DC: the exact pixel sum X = (R - 2^18) >> 17, rounded as numpy does
+            const int X = (R.x - (1 << 18)) >> 17;
+            const int qdc = table == 0 ? dc_quant<0>(X) : dc_quant<1>(X);
+            if (g == 0) w01 = (w01 & 0xFFFF0000u) | ((uint32_t)qdc & 0xFFFFu);
+          }
+          row[4 * mt] = make_uint2(w01, __builtin_bit_cast(uint32_t, q23));
         }
-      };
-      if (dv & 16) {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) reinterpret_cast<uint2 *>(st)[r] = w[r];
-      } else if (J.table == 0) {
-        dct_block_f32<0, LAYOUT>(w, st, sink);
-      } else {
-        dct_block_f32<1, LAYOUT>(w, st, sink);
       }
-      if (dv & 1) flo = fhi = 0;
-      const bool has = (flo | fhi) != 0;
-      if (__builtin_amdgcn_ballot_w64(has)) {
-        const int r = f32_enqueue<LAYOUT>(V, qn, ns, blk, kj, flo, fhi, w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7]);
-        if (r < 0) {  // overflow: this set's items are dropped and the whole set goes to tier 3
-          redo |= 1ull << k;
-        } else {
-          qn = __builtin_amdgcn_readfirstlane(r & 0xFF);
-          ns = __builtin_amdgcn_readfirstlane((r >> 8) & 0xFF);
-          zamb = __builtin_amdgcn_ballot_w64(zl) != 0 && !(dv & 2);
+      if (__builtin_amdgcn_ballot_w64(fmin < kMfmaL) != 0) {
+        redo |= 1ull << i;  // the whole set again on the float64 path, after the loop
+        continue;
+      }
+      if (m44 != 0) {
+        // luminance (4,4) ties: the rows' signed sums (+ - - + + - - +) of each block
+        // to its lane, pocketfft's own roundings on them, the exact q into the stage
+        constexpr int kS = 0x01FFFF01;  // int8 (+1, -1, -1, +1)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const int ka = __builtin_amdgcn_sdot4(B[nt].y, kS, __builtin_amdgcn_sdot4(B[nt].x, kS, 0, false), false);
+          const int kb = __builtin_amdgcn_sdot4(B[nt].w, kS, __builtin_amdgcn_sdot4(B[nt].z, kS, 0, false), false);
+          k44[(16 * nt + n) * 4 + g] = make_int2(ka, kb);
         }
+        __builtin_amdgcn_wave_barrier();
+        if ((m44 >> lane) & 1) {
+          int k[8];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int2 v = k44[lane * 4 + r];
+            k[2 * r] = v.x;
+            k[2 * r + 1] = v.y;
+          }
+          reinterpret_cast<int16_t *>(st2 + lane * kStageU2)[kMfmaZ44] = (int16_t)quant_fast<0>(pf_y44_k(k), 36);
+        }
+        __builtin_amdgcn_wave_barrier();
       }
-      // resolve the queue before this set's store when a zero-ambiguous item needs
-      // it for the RLE tile record, or early enough that the next set finds room
-      // (one code site: items of this set land in its stage, older ones patch HBM)
-      if (dv & 32) qn = ns = 0, zamb = false;
-      if (zamb || qn > kQCap - 12 || ns > kPSlots - 6) {
-        redo |= f32_round<LAYOUT>(V, qn, kj, set);
-        qn = ns = 0;
-      }
-      if (!(dv & 4)) f32_store<LAYOUT, TMF>(V, J, set);
+      mfma_store<TMF>(J, set, st2, lane, M);
     }
   }
-  if (qn > 0) redo |= f32_round<LAYOUT>(V, qn, -1, -1);
-  // tier 3: whole sets on the exact pocketfft replica
-  while (redo) {
-    const int kk = __builtin_ctzll(redo);
-    redo &= redo - 1;
-    const int g = g0 + kk * nwaves;
-    const int kj = job_of(g);
-    f32_exact_set<LAYOUT, TMF>(V, kj, g - jobs.j[kj].set0);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Production forward kernel for aligned planes: the packed float32 transform
-// (dct_core.h dct_block_pk), one 8x8 block per lane, one 64-block set (= one RLE
-// tile) per wave iteration, persistent grid at 4 waves per SIMD (<= 128 VGPRs,
-// ~9.6 KiB of LDS per wave) with the next set's pixels loading during the current
-// set's arithmetic.
-//  * Every float operation is one v_pk_*_f32 for two transforms of the block (row
-//    pairs, then column pairs).  Coefficients go to an LDS stage at their zig-zag
-//    slot, leave in 1 KiB nontemporal stores, and the tile record is computed from
-//    the stage.
-//  * Exactness: a coefficient whose float32 estimate lies inside its proven tie
-//    window is flagged (~0.06 per luminance block on random data, 0.02 chroma;
-//    (4,4) flags only at exact ties).  Its provisional q (the estimate's rint) is
-//    stored; the flag is DEFERRED into a per-wave LDS queue {set, lane, coefficient,
-//    provisional q} and resolved 64 at a time, one per lane, by resolve_coef
-//    (float64 dot product; pocketfft's own operations for (4,4) and the (2,2)
-//    class), which patches the coefficient in HBM (a wave's stores to one address
-//    complete in program order).  A flag changes q by at most one, so a tile record
-//    built from the provisional values is exact unless q crossed zero; such a tile
-//    (rare, zero-ambiguous ties) is marked and its record rebuilt from HBM after the
-//    patches.  A coefficient that resolve_coef cannot settle recomputes its block on
-//    the exact pocketfft replica (and marks the tile); a set whose flags overflow
-//    the queue runs its flagged blocks on the replica before its store.
-constexpr int kPkQCap = 48;    // deferred items per wave (each with its block's 64 B of pixels)
-constexpr int kPkQFlush = 36;  // flush after a set once this many are queued
-
-__device__ __forceinline__ void pk_load(const DctJob &J, int set, int lane, uint2 (&w)[8]) {
-  int blk = set * 64 + lane;
-  blk = blk < J.nblk ? blk : J.nblk - 1;  // clamp (the lane's results are discarded)
-  const int bi = blk / J.nbx, bj = blk - bi * J.nbx;
-  const uint8_t *p = J.plane + (int64_t)bi * 8 * J.stride + bj * 8;
-#pragma unroll
-  for (int r = 0; r < 8; ++r) w[r] = *reinterpret_cast<const uint2 *>(p + r * J.stride);
-}
-
-// Tier 3 (cold, out of line; by value: a reference would put the caller's job in
-// scratch memory): block blk on the exact pocketfft replica into stage row st.
-__device__ __attribute__((noinline)) void pk_exact_block(const uint8_t *plane, int64_t stride, int nbx, int table,
-                                                         int blk, int16_t *st) {
-  const int bi = blk / nbx, bj = blk - bi * nbx;
-  const uint8_t *p = plane + (int64_t)bi * 8 * stride + bj * 8;
-  uint2 w[8];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) w[r] = *reinterpret_cast<const uint2 *>(p + r * stride);
-  if (table == 0)
-    dct_block_2ph<0, HIC_LAYOUT_ZIGZAG_I16>(w, st);
-  else
-    dct_block_2ph<1, HIC_LAYOUT_ZIGZAG_I16>(w, st);
-}
-
-// Flush (cold): resolve the n <= 48 queued items, one per lane.  Item =
-// {wave set index k (g = g0 + k nwaves), lane << 26 | flag bit << 20 | provisional
-// q} + its block's 8 pixel rows (qp, 4 x 16 B), so no HBM reads.  Returns the
-// wave's dirty-tile mask (bit k: set k's record must be rebuilt).
-__device__ __forceinline__ uint64_t pk_flush(const DctJobs &jobs, const uint2 *qh, const uint4 *qp, int n, int g0,
-                                             int nwaves, uint2 *st2, const double *cm, const uint8_t *qt,
-                                             const int8_t *zz, int lane, uint32_t *mark_to = nullptr) {
-  bool mark = false;
-  int kset = 0;
-  if (lane < n) {
-    const uint2 it = qh[lane];
-    kset = (int)it.x;
-    const int g = g0 + kset * nwaves;
-    // items of one flush come from different sets, possibly different planes: the
-    // job is selected per lane (job_of is wave-uniform)
-    const int kj = (jobs.n > 2 && g >= jobs.j[2].set0) ? 2 : ((jobs.n > 1 && g >= jobs.j[1].set0) ? 1 : 0);
-    const DctJob J = kj == 2 ? jobs.j[2] : (kj == 1 ? jobs.j[1] : jobs.j[0]);
-    const int sl = (int)(it.y >> 26), i = pk_flag_index((int)((it.y >> 20) & 63u));
-    const int q0 = (int)(int16_t)(it.y & 0xFFFFu);
-    const int blk = (g - J.set0) * 64 + sl;
-    uint2 w[8];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint4 t = qp[4 * lane + k];
-      w[2 * k] = make_uint2(t.x, t.y);
-      w[2 * k + 1] = make_uint2(t.z, t.w);
-    }
-    int qv = 0;
-    int16_t *o = static_cast<int16_t *>(J.out) + (int64_t)blk * 64;
-    if (resolve_coef(w, J.table, i, qv, cm, qt)) {
-      if (qv != q0) {
-        o[zz[i]] = (int16_t)qv;
-        mark = (qv == 0) != (q0 == 0);  // q crossed zero: the tile's record changes
-      }
-    } else {
-      // only the replica decides: the whole block, through this lane's stage row
-      int16_t *st = reinterpret_cast<int16_t *>(st2 + lane * kStageU2);
-      pk_exact_block(J.plane, J.stride, J.nbx, J.table, blk, st);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) reinterpret_cast<uint4 *>(o)[k] = stage16(st2, lane, k);
-      mark = true;
-    }
-  }
-  if (mark_to) {  // merged flush: the owner wave's set mask in LDS (per lane)
-    if (mark) atomicOr(mark_to + (kset >> 5), 1u << (kset & 31));
-    return 0;
-  }
-  uint64_t dirty = 0;
-  for (uint64_t m = __builtin_amdgcn_ballot_w64(mark); m; m &= m - 1)
-    dirty |= 1ull << __builtin_amdgcn_readlane(kset, __builtin_ctzll(m));
-  return dirty;
-}
-
-// Rebuild the tile record of wave set k from HBM (cold: a flagged coefficient
-// crossed zero).  The patches above were stored by this wave: drain them, then
-// read the tile back past the L1 (nontemporal loads).
-template <int MF, typename JobOf>
-__device__ __forceinline__ void pk_rebuild_record(const DctJobs &jobs, JobOf job_of, int g, int lane) {
-  const DctJob &J = jobs.j[job_of(g)];
-  const int set = g - J.set0, blk = set * 64 + lane;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  uint32_t zw[32];
-  if (blk < J.nblk) {
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 *b4 = reinterpret_cast<const u32x4 *>(static_cast<const int16_t *>(J.out) + (int64_t)blk * 64);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const u32x4 t = __builtin_nontemporal_load(b4 + k);
-      zw[4 * k] = t.x; zw[4 * k + 1] = t.y; zw[4 * k + 2] = t.z; zw[4 * k + 3] = t.w;
-    }
-  }
-  tile_record16<MF>(zw, blk < J.nblk, blk, jobs.M, J.tiles + (int64_t)set * 3);
-}
-
-#ifndef HIC_PK_WPE
-#define HIC_PK_WPE 3  // register budget: waves per SIMD (<= 168 VGPRs; LDS: 3 workgroups of 4 waves per CU)
-#endif
-#ifndef HIC_PK_PF
-#define HIC_PK_PF 1  // 1: the next set's pixels load during this set's arithmetic (+16 VGPRs)
-#endif
-template <int TMF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_PK_WPE))) void k_dct_pk(DctJobs jobs, int dev) {
-#ifdef HIC_DEV
-  // dev timing bits (results invalid): 1 drop the flags (no exact resolution), 4 no
-  // stores / records, 8 no pixel loads (synthetic pixels), 16 no DCT
-  const int dv = dev;
-#else
-  constexpr int dv = 0;
-  (void)dev;
-#endif
-  __shared__ uint2 s_stage[4 * 64 * kStageU2];
-  __shared__ uint2 s_qh[4 * kPkQCap];
-  __shared__ uint4 s_qp[4 * kPkQCap * 4];
-  __shared__ double s_cm[64];
-  __shared__ uint8_t s_qt[128];
-  __shared__ int8_t s_zz[64];
-  __shared__ int s_qn[4];             // the waves' residual queue lengths (the merged final flush)
-  __shared__ uint32_t s_dirty[4 * 2];  // the waves' dirty-set masks, set by the merged flush
-  if (threadIdx.x < 64) s_cm[threadIdx.x] = cos2(kCm, threadIdx.x >> 3, threadIdx.x & 7);
-  if (threadIdx.x < 128) s_qt[threadIdx.x] = (uint8_t)QT[threadIdx.x >> 6][threadIdx.x & 63];
-  if (threadIdx.x < 64) s_zz[threadIdx.x] = kZZInv[threadIdx.x];
-  if (threadIdx.x < 8) s_dirty[threadIdx.x] = 0;
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nwaves = gridDim.x * 4, g0 = blockIdx.x * 4 + wv;
-  uint2 *st2 = s_stage + wv * 64 * kStageU2;
-  uint2 *qh = s_qh + wv * kPkQCap;
-  uint4 *qp = s_qp + wv * kPkQCap * 4;
+  // flagged sets: the float64 AAN path (its own exact fallbacks) on this wave's sets
   int16_t *st = reinterpret_cast<int16_t *>(st2 + lane * kStageU2);
-  // the job of wave-uniform set g: an SGPR index, so each field is one scalar load
-  // from the kernel arguments (recomputed per set: no job state carried in the loop)
-  auto job_of = [&](int g) -> int {
-    g = __builtin_amdgcn_readfirstlane(g);
-    int k = (jobs.n > 1 && g >= jobs.j[1].set0) ? 1 : 0;
-    k = (jobs.n > 2 && g >= jobs.j[2].set0) ? 2 : k;
-    return __builtin_amdgcn_readfirstlane(k);
-  };
-  // (a wave without sets still joins the workgroup's barriers of the final flush)
-  uint2 wn[8];
-  if (dv & 8) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r) wn[r] = make_uint2(0x9E3779B1u * (lane + r), 0x85EBCA6Bu * (lane ^ r));
-  } else if (HIC_PK_PF && g0 < jobs.total_sets) {
-    const DctJob &J0 = jobs.j[job_of(g0)];
-    pk_load(J0, g0 - J0.set0, lane, wn);
-  }
-  int qn = 0;          // queued items (wave-uniform)
-  uint64_t dirty = 0;  // sets whose record must be rebuilt
-  int k = 0;
-  for (int g = g0; g < jobs.total_sets; g += nwaves, ++k) {
-    const DctJob &J = jobs.j[job_of(g)];
-    const int set = g - J.set0, blk = set * 64 + lane;
+  while (redo) {
+    const int k = __builtin_ctzll(redo);
+    redo &= redo - 1;
+    const int gs = g0 + k * nwaves;
+    const DctJob &J = jobs.j[job_of(gs)];
+    const int set = gs - J.set0;
+    const int blk = set * 64 + lane;
+    const int cblk = blk < J.nblk ? blk : J.nblk - 1;
+    const int bi = cblk / J.nbx, bj = cblk - bi * J.nbx;
+    const uint8_t *p = J.plane + (int64_t)bi * 8 * J.stride + bj * 8;
     uint2 w[8];
-    if (HIC_PK_PF | (dv & 8)) {
 #pragma unroll
-      for (int r = 0; r < 8; ++r) w[r] = wn[r];
-    } else {
-      pk_load(J, set, lane, w);
+    for (int r = 0; r < 8; ++r) w[r] = *reinterpret_cast<const uint2 *>(p + r * J.stride);
+    bool t26 = false;
+    const bool f = dct_block_aan<-1, HIC_LAYOUT_ZIGZAG_I16>(w, st, &t26, nullptr, J.table);
+    if (f) {
+      dct_block_2ph<-1, HIC_LAYOUT_ZIGZAG_I16>(w, st, J.table);
+    } else if (t26) {
+      constexpr SlotOf<HIC_LAYOUT_ZIGZAG_I16> kSlot{};
+      int q[4];
+      dct_fix26<-1>(w, q, J.table);
+      st[kSlot.s[18]] = (int16_t)q[0];
+      st[kSlot.s[22]] = (int16_t)q[1];
+      st[kSlot.s[50]] = (int16_t)q[2];
+      st[kSlot.s[54]] = (int16_t)q[3];
     }
-    const int gn = g + nwaves;
-    if (HIC_PK_PF && gn < jobs.total_sets && !(dv & 8)) {
-      const DctJob &Jn = jobs.j[job_of(gn)];
-      pk_load(Jn, gn - Jn.set0, lane, wn);
-    }
-    uint32_t f0 = 0, f1 = 0;
-    if (dv & 16) {
-#pragma unroll
-      for (int r = 0; r < 8; ++r) reinterpret_cast<uint2 *>(st)[r] = w[r];
-    } else if (J.table == 0) {
-      dct_block_pk<0>(w, st, f0, f1);
-    } else {
-      dct_block_pk<1>(w, st, f0, f1);
-    }
-    const uint64_t flags = (blk < J.nblk && !(dv & 1)) ? ((uint64_t)f1 << 32 | f0) : 0;
-    if (__builtin_amdgcn_ballot_w64(flags != 0)) {
-      // queue the set's flags, one per lane per pass (stage reads: provisional q)
-      uint64_t bits = flags;
-      int n = qn;
-      bool over = false;
-      for (;;) {
-        const bool has = bits != 0;
-        const uint64_t m = __builtin_amdgcn_ballot_w64(has);
-        if (!m) break;
-        if (n + __builtin_popcountll(m) > kPkQCap) {
-          over = true;
-          break;
-        }
-        if (has) {
-          const int b = __builtin_ctzll(bits);
-          bits &= bits - 1;
-          const int pos = n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-          const uint32_t q0 = (uint16_t)st[s_zz[pk_flag_index(b)]];
-          qh[pos] = make_uint2((uint32_t)k, (uint32_t)lane << 26 | (uint32_t)b << 20 | q0);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) qp[4 * pos + r] = make_uint4(w[2 * r].x, w[2 * r].y, w[2 * r + 1].x, w[2 * r + 1].y);
-        }
-        n += __builtin_popcountll(m);
-      }
-      if (over) {
-        // the queue is full (only on tie-dense inputs): this set's flagged blocks go
-        // to the exact replica before the store, and its items queued so far are
-        // dropped (qn is not advanced)
-        if (flags != 0) pk_exact_block(J.plane, J.stride, J.nbx, J.table, blk, st);
-      } else {
-        qn = __builtin_amdgcn_readfirstlane(n);
-      }
-    }
-    // copy-out (1 KiB contiguous stores) + the tile record from the stage
-    if (!(dv & 4)) {
-      F32Wave V;
-      V.st2 = st2;
-      V.lane = lane;
-      V.M = jobs.M;
-      f32_store<HIC_LAYOUT_ZIGZAG_I16, TMF>(V, J, set);
-    }
-    __builtin_amdgcn_wave_barrier();
-    if (qn >= kPkQFlush) {
-      dirty |= pk_flush(jobs, qh, qp, qn, g0, nwaves, st2, s_cm, s_qt, s_zz, lane);
-      qn = 0;
-      __builtin_amdgcn_wave_barrier();
-    }
-  }
-  // The residual items of the workgroup's waves, merged: one resolve round per 64
-  // items of the workgroup instead of one per wave (every wave ends with a partly
-  // full queue at the same time, in the launch's tail).  Wave v resolves the items
-  // 64 v .. 64 v + 63 of the concatenated queues; the set masks go to the owners.
-  if (lane == 0) s_qn[wv] = qn;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the provisional stores precede any patch
-  __syncthreads();
-  {
-    const int n0 = s_qn[0], n1 = s_qn[1], n2 = s_qn[2], n3 = s_qn[3];
-    const int j = 64 * wv + lane;
-    const int o = j < n0 ? 0 : (j < n0 + n1 ? 1 : (j < n0 + n1 + n2 ? 2 : 3));
-    const int jo = j - (o > 0 ? n0 : 0) - (o > 1 ? n1 : 0) - (o > 2 ? n2 : 0);
-    const int ntot = n0 + n1 + n2 + n3;
-    if (__builtin_amdgcn_ballot_w64(j < ntot)) {
-      // lane -> item jo of wave o's queue: pk_flush reads item `lane` of (qh, qp), so
-      // shift the bases per lane (n = lane + 1 keeps exactly this lane's item)
-      const uint2 *qho = s_qh + o * kPkQCap + jo - lane;
-      const uint4 *qpo = s_qp + (o * kPkQCap + jo - lane) * 4;
-      const uint64_t d = pk_flush(jobs, qho, qpo, j < ntot ? lane + 1 : 0, blockIdx.x * 4 + o, nwaves, st2, s_cm, s_qt,
-                                  s_zz, lane, s_dirty + 2 * o);
-      (void)d;
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  dirty |= (uint64_t)s_dirty[2 * wv + 1] << 32 | s_dirty[2 * wv];
-  if (g0 < jobs.total_sets && TMF >= 0 && !(dv & 4)) {
-    for (uint64_t d = dirty; d; d &= d - 1) pk_rebuild_record<TMF>(jobs, job_of, g0 + __builtin_ctzll(d) * nwaves, lane);
+    mfma_store<TMF>(J, set, st2, lane, M);
   }
 }
 
@@ -1300,10 +933,10 @@ __global__ void k_dequantize_i32(const int32_t *__restrict__ in, int64_t n, int 
 inline bool aligned(const void *p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
 
 // Forward-path selection (A/B tests only; every path is bit-exact): knob
-// "dct_path" 1 = float64 AAN fast path with the next set's pixels prefetched
-// (default), 2 = the same without the prefetch, 3 = float32 AAN + float64
-// fallback (k_dct_f32), 0 = the exact pocketfft replica for every block; "dct_waves_per_cu" = persistent grid
-// size (0 = one wave per set).  Set through hic_set_knob (common.hip); the
+// "dct_path" 5 = integer-MFMA transform (k_dct_mfma, ZIGZAG_I16 output; the
+// raster layouts take path 1), 1 = float64 AAN fast path (k_dct_planes), 2 = the
+// same (the prefetch variant is compiled out), 0 = the exact pocketfft replica for
+// every block; "dct_waves_per_cu" = persistent grid size (0 = one wave per set).  Set through hic_set_knob (common.hip); the
 // library reads no environment variables.
 inline int dct_path() { return knob(HIC_KNOB_DCT_PATH); }
 inline int dct_waves_per_cu(int njobs) {
@@ -1311,48 +944,18 @@ inline int dct_waves_per_cu(int njobs) {
   // float64 path: one wave per set for a multi-plane launch (the hardware's dispatch
   // balances the planes' mixed tail: 8K Y + Cr + Cb 37.5 us vs 39.7 for 12
   // persistent waves per CU), 12 persistent waves per CU for one plane (4K luma
-  // 13.4 vs 13.8 us, 8K luma 27.4 vs 27.8; scripts/gpu_r2aj.sh); the float32 path
-  // keeps its persistent queue
-  return v >= 0 ? v : (dct_path() == 3 ? 16 : (njobs > 1 ? 0 : 12));
+  // 13.4 vs 13.8 us, 8K luma 27.4 vs 27.8; scripts/gpu_r2aj.sh); the MFMA path
+  // runs a persistent grid of 3 waves per SIMD
+  return v >= 0 ? v : (dct_path() == 5 ? 12 : (njobs > 1 ? 0 : 12));
 }
 
 inline bool fwd_fast(int H, int W, int64_t stride, const void *plane, const void *out) {
   return (H % 8 == 0) && (W % 8 == 0) && (stride % 8 == 0) && aligned(plane, 8) && aligned(out, 16);
 }
 
-// The packed kernel's planes: 16-byte aligned outputs (1 KiB stage copy-out).
-inline bool pk_ok(const DctJob &J) { return aligned(J.out, 16); }  // (jobs are fwd_fast planes)
-
-// Persistent launch of k_dct_pk over the jobs' 64-block sets.
-template <int TMF>
-int launch_pk(DctJobs &jobs, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-  int total = 0;
-  for (int k = 0; k < jobs.n; ++k) {
-    jobs.j[k].nsets = (jobs.j[k].nblk + 63) / 64;
-    jobs.j[k].set0 = total;
-    total += jobs.j[k].nsets;
-  }
-  jobs.total_sets = total;
-  const int v = knob(HIC_KNOB_DCT_WAVES_PER_CU);
-  int cap = (v > 0 ? v : 12) * cu_count();  // 3 waves per SIMD
-  if ((total + cap - 1) / cap > 64) cap = (total + 63) / 64;  // <= 64 sets per wave (the dirty mask)
-  const int waves = (v == 0 || total < cap) ? total : cap;
-  const dim3 grid((waves + 3) / 4), block(256);
-  if (e0 || e1)
-    hipExtLaunchKernelGGL((k_dct_pk<TMF>), grid, block, 0, s, e0, e1, 0, jobs, knob(HIC_KNOB_DEV));
-  else
-    hipLaunchKernelGGL((k_dct_pk<TMF>), grid, block, 0, s, jobs, knob(HIC_KNOB_DEV));
-  return check_launch("k_dct_pk");
-}
-
 // Persistent launch of k_dct_planes over the jobs' sets (all fast-path planes).
 template <int TABLE, int LAYOUT, int TMF>
 int launch_planes(DctJobs &jobs, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-  if (LAYOUT == HIC_LAYOUT_ZIGZAG_I16 && dct_path() == 4) {
-    bool ok = true;
-    for (int k = 0; k < jobs.n; ++k) ok = ok && pk_ok(jobs.j[k]);
-    if (ok) return launch_pk<TMF>(jobs, s, e0, e1);
-  }
   int total = 0;
   for (int k = 0; k < jobs.n; ++k) {
     jobs.j[k].set0 = total;
@@ -1363,13 +966,13 @@ int launch_planes(DctJobs &jobs, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   if (cap > 0 && (total + cap - 1) / cap > 64) cap = (total + 63) / 64;  // <= 64 sets per wave (redo mask)
   const int waves = (cap == 0 || total < cap) ? total : cap;
   const dim3 grid((waves + 3) / 4), block(256);
-  const int path = dct_path() == 4 ? 1 : dct_path();  // 4 on planes k_dct_pk cannot take: the float64 path
-  if (path == 3) {
+  const int path = dct_path();
+  if (path == 5 && LAYOUT == HIC_LAYOUT_ZIGZAG_I16) {
     if (e0 || e1)
-      hipExtLaunchKernelGGL((k_dct_f32<LAYOUT, TMF>), grid, block, 0, s, e0, e1, 0, jobs, knob(HIC_KNOB_DEV));
+      hipExtLaunchKernelGGL((k_dct_mfma<TMF>), grid, block, 0, s, e0, e1, 0, jobs);
     else
-      hipLaunchKernelGGL((k_dct_f32<LAYOUT, TMF>), grid, block, 0, s, jobs, knob(HIC_KNOB_DEV));
-    return check_launch("k_dct_f32");
+      hipLaunchKernelGGL((k_dct_mfma<TMF>), grid, block, 0, s, jobs);
+    return check_launch("k_dct_mfma");
   }
   if (e0 || e1)
     hipExtLaunchKernelGGL((k_dct_planes<TABLE, LAYOUT, TMF>), grid, block, 0, s, e0, e1, 0, jobs, path);
@@ -1460,7 +1063,7 @@ extern "C" int hic_dct_quant_rle_u8(const uint8_t *plane, int64_t H, int64_t W, 
 
 extern "C" int hic_dct_quant_rle_u8_batch(int n, const hic_dct_plane_job *jobs, int max_len, void *stream,
                                           void *ev_start, void *ev_stop) {
-  if (n < 1 || n > 3 || !jobs) return arg_error("1 <= n <= 3 planes");
+  if (n < 1 || n > kMaxPlaneJobs || !jobs) return arg_error("1 <= n <= %d planes", kMaxPlaneJobs);
   if (max_len < 1 || max_len > 256) return arg_error("max_len must be in [1, 256]");
   hipStream_t s = as_stream(stream);
   const hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;

@@ -57,11 +57,29 @@ def check_count(c, channel=""):
     raise MemoryError("symbol buffer too small for channel %s: %d symbols needed" % (channel, -c))
 
 
+def encoder_layout(H, W, rows=None, fused=None):
+    """(fused, rpt) of an Encoder of rows `rows` of an H x W image: whether it runs
+    the fused kernel (None = the measured default: W % 512 == 0 and fusable), and its
+    RLE tile records per 64-block tile per channel (the fused kernel's chroma: one
+    per 32-block half tile)."""
+    r0, r1 = rows if rows is not None else (0, H)
+    a, b = input_span(H, r0, r1)
+    # (hic_encode420_u8 reads the input rows through 32-bit buffer offsets)
+    can_fuse = (W % 16 == 0 and H % 16 == 0 and r0 % 16 == 0 and r1 % 16 == 0
+                and (b - a) * W * 3 <= 2**31 - 1)
+    if fused and not can_fuse:
+        raise ValueError("the fused encoder needs W, H and rows multiples of 16, "
+                         "and < 2 GiB of input rows")
+    f = (can_fuse and W % 512 == 0) if fused is None else bool(fused)
+    half = f and W % 512 == 0
+    return f, {"lum": 1, "cr": 2 if half else 1, "cb": 2 if half else 1}
+
+
 class Encoder:
     """rows=(r0, r1) makes this encoder one row-shard of an H x W image (r0 even;
     shards of one image split at multiples of 16 rows so chroma blocks align)."""
 
-    def __init__(self, H, W, max_len=15, rows=None, out=None, fused=None, index=False):
+    def __init__(self, H, W, max_len=15, rows=None, out=None, fused=None, index=False, landing_rpt=None):
         """out: optional {channel: (coef (n, 64) int16, dc (n,) int32)} device views the
         encoder writes into (a gathering rank points them at its slice of the whole
         image's buffers, so its own shard needs no copy).
@@ -69,7 +87,10 @@ class Encoder:
         reach HBM; W, H and the row range multiples of 16); None = the faster path
         as measured: fused when W % 512 == 0, else the two-kernel chain (a ragged
         last strip needs a tile pass for its RLE records: 3840x2160 measured 44.6 vs
-        40.5 us per image); False = the chain."""
+        40.5 us per image); False = the chain.
+        landing_rpt: a landing zone only (the gathering rank of a stream gather): no
+        transform, no plane buffers, and the RLE record layout of the shards that
+        fill it (their encoder_layout rpt), whatever this shape alone would pick."""
         if H < 2 or W < 2:
             raise ValueError("image must be at least 2 x 2")
         device.require_gpu()
@@ -79,30 +100,22 @@ class Encoder:
             raise ValueError("bad row range %r" % ((r0, r1),))
         self.rows = (r0, r1)
         self.want_index = bool(index)
-        a, b = input_span(H, r0, r1)
-        # (hic_encode420_u8 reads the input rows through 32-bit buffer offsets)
-        can_fuse = (W % 16 == 0 and H % 16 == 0 and r0 % 16 == 0 and r1 % 16 == 0
-                    and (b - a) * W * 3 <= 2**31 - 1)
-        if fused and not can_fuse:
-            raise ValueError("the fused encoder needs W, H and rows multiples of 16, "
-                             "and < 2 GiB of input rows")
-        self.fused = (can_fuse and W % 512 == 0) if fused is None else bool(fused)
+        self.landing = landing_rpt is not None
+        if self.landing:
+            self.fused, self.rpt = False, dict(landing_rpt)
+        else:
+            self.fused, self.rpt = encoder_layout(H, W, (r0, r1), fused)
         c0, c1 = r0 // 2, min(H // 2, r1 // 2)
         self.shapes = {"lum": (r1 - r0, W), "cr": (c1 - c0, W // 2), "cb": (c1 - c0, W // 2)}
         ys, cs = self.shapes["lum"], self.shapes["cr"]
         lib = _lib.load()
         # the planes exist only on the two-kernel path
         self.y = self.cr = self.cb = None
-        if not self.fused:
+        if not self.fused and not self.landing:
             self.y = device.empty(ys, torch.uint8)
             self.cr = device.empty(cs, torch.uint8)
             self.cb = device.empty(cs, torch.uint8)
         self.planes = {"lum": self.y, "cr": self.cr, "cb": self.cb}
-        # tile records per 64-block tile: the fused kernel writes chroma records per
-        # 32-block half tile
-        # (W % 512 == 0; a ragged last strip gets one record per 64-block tile)
-        half = self.fused and W % 512 == 0
-        self.rpt = {"lum": 1, "cr": 2 if half else 1, "cb": 2 if half else 1}
         self.coef, self.dc, self.sym_len, self.sym_val, self.ws = {}, {}, {}, {}, {}
         self.cap = {}
         self.counts = device.zeros((3,), torch.int64)
@@ -140,6 +153,8 @@ class Encoder:
         """Steps 1-2: colour + 4:2:0 + DCT/quantize/zig-zag of the three planes.
         rgb holds image rows [in_row0, in_row0 + rgb.shape[0]) (default: the
         whole image for an unsharded encoder, input_span() for a shard)."""
+        if self.landing:
+            raise RuntimeError("a landing-zone Encoder does not transform")
         s = device.stream_ptr(stream)
         if in_row0 is None:
             in_row0 = 0 if self.rows == (0, self.H) else self.input_span()[0]

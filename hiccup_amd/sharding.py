@@ -159,13 +159,21 @@ class ShardEncoder:
         self.ranges = block_ranges(H, W, self.world)
         self.gather_to = gather_to
         self.gather_kind = gather_kind
+        if fused is None:
+            # one decision for every rank (the record layout of the whole stream
+            # depends on it): fused only if every shard can run the fused kernel
+            fused = all(pipeline.encoder_layout(H, W, rr)[0] for rr in plan(H, self.world))
         self.whole = None
         out = None
         if gather_to is not None and self.rank == gather_to:
             if gather_kind == "stream":
                 # the whole image's entropy stage lives here: its buffers are the
-                # landing zone, this rank's encoder writes its slice in place
-                self.whole = pipeline.Encoder(H, W, max_len=max_len, fused=fused)
+                # landing zone, this rank's encoder writes its slice in place.  Its
+                # RLE records follow the SHARDS' layout (wire_ranges sizes and packs
+                # them with it): a whole image past 2 GiB of input cannot run the fused
+                # kernel, its shards can, and their chroma records are half tiles
+                self.whole = pipeline.Encoder(H, W, max_len=max_len,
+                                              landing_rpt=pipeline.encoder_layout(H, W, self.rows, fused)[1])
                 self.full_coef, self.full_dc = self.whole.coef, self.whole.dc
             else:
                 self.full_coef, self.full_dc = {}, {}
@@ -234,8 +242,10 @@ class ShardEncoder:
         s = device.stream_ptr(stream)
         lib = _lib.load()
         whole = self.whole
+        if whole.rpt != self.enc.rpt:
+            raise RuntimeError("landing zone record layout %r != the shards' %r" % (whole.rpt, self.enc.rpt))
         for k in CHANNELS:
-            rpt = whole.rpt[k]
+            rpt = self.enc.rpt[k]  # the layout wire_ranges sized the segments with
             for r in range(self.world):
                 b0, b1 = self.ranges[k][r]
                 n = b1 - b0

@@ -64,7 +64,7 @@ int hic_device_count(int *h_n);
  * Every selectable path is bit-exact: a knob never changes results, only which
  * kernel variant computes them.  The library reads no environment variables.
  * Values are process-wide; -1 restores the default. */
-#define HIC_KNOB_DCT_PATH 0         /* forward DCT: 1 float64 AAN (default), 4 packed-float32 AAN + deferred exact queue (aligned planes), 2 float64 AAN unpipelined, 3 scalar float32 AAN + float64 fallback, 0 exact replica */
+#define HIC_KNOB_DCT_PATH 0         /* forward DCT of aligned planes: 5 integer-MFMA transform (ZIGZAG_I16 output), 1 / 2 float64 AAN, 0 exact replica */
 #define HIC_KNOB_DCT_WAVES_PER_CU 1 /* forward DCT persistent grid (waves per CU; 0 = one wave per set) */
 #define HIC_KNOB_COLOR_TILED 2      /* 1: LDS-tiled colour kernels instead of the wave-walk ones */
 #define HIC_KNOB_COLOR_SEG 3        /* wave-walk colour: chroma rows per segment (8 default, 16) */
@@ -117,12 +117,11 @@ int hic_dct_quant_u8_timed(const uint8_t *plane, int64_t H, int64_t W, int64_t s
  * hic_rle_shard_summary_tiles).  Events as in hic_dct_quant_u8_timed (nullable). */
 int hic_dct_quant_rle_u8(const uint8_t *plane, int64_t H, int64_t W, int64_t stride, int table_id, int max_len,
                          int16_t *out, void *rle_workspace, void *stream, void *ev_start, void *ev_stop);
-/* hic_dct_quant_rle_u8 for up to 3 planes (the Y, Cr, Cb of one image): one
- * launch per quantisation table, each a persistent grid over all its planes'
- * 64-block sets.  Each job names its plane, table, ZIGZAG_I16 output and RLE
- * workspace.  Events (nullable) time the first launch (the luminance one when
- * the jobs are Y, Cr, Cb).  Ragged planes (H or W not a multiple of 8) take
- * separate launches. */
+/* hic_dct_quant_rle_u8 for up to 16 planes (the Y, Cr, Cb of one image, or the
+ * planes of consecutive images): ONE launch, a persistent grid over all their
+ * 64-block sets (each plane's table read at run time).  Each job names its plane,
+ * table, ZIGZAG_I16 output and RLE workspace.  Events (nullable) time that
+ * launch.  Ragged planes (H or W not a multiple of 8) take separate launches. */
 typedef struct {
   const uint8_t *plane;
   int64_t H, W, stride;

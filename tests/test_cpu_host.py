@@ -362,3 +362,29 @@ def test_rle_workspace_covers_scan_partitions():
             nrec = -(-n * rpt // 64)
             need = (5 * nrec + 3 * -(-nrec // 256) + 1) * 8
             assert have >= need, (n, rpt, have, need)
+
+
+def test_stream_gather_record_layout_past_2gib():
+    """a stream gather's landing zone takes the SHARDS' RLE record
+    layout.  At 32768^2 the whole image (3.2 GB of RGB) cannot run the fused kernel
+    while its 8 row shards can (their chroma records are 32-block half tiles); the
+    wire segments are sized with the shards' layout, and every rank makes the same
+    fused decision (all shards fusable), so the ranges agree across ranks."""
+    from hiccup_amd import pipeline
+    H = W = 32768
+    assert pipeline.encoder_layout(H, W)[0] is False
+    rows = sharding.plan(H, 8)
+    lay = [pipeline.encoder_layout(H, W, rr) for rr in rows]
+    assert all(f for f, _ in lay)
+    assert all(r == {"lum": 1, "cr": 2, "cb": 2} for _, r in lay)
+    ranges = sharding.block_ranges(H, W, 8)
+    wr = sharding.wire_ranges(ranges, lay[0][1], sharding.records_aligned(ranges, lay[0][1]))
+    lib = _lib.load()
+    for k in sharding.CHANNELS:
+        for (b0, b1), (o0, o1) in zip(ranges[k], wr[k]):
+            n = b1 - b0
+            nrec = -(-n * lay[0][1][k] // 64)
+            assert o1 - o0 == lib.hic_wire_bytes(n, sharding.TABLE_OF[k]) + -(-nrec * sharding.REC_BYTES // 16) * 16
+    # a ragged image whose last shard cannot fuse: one decision for all (the chain)
+    rows = sharding.plan(4328, 4)
+    assert not all(pipeline.encoder_layout(4328, 7680, rr)[0] for rr in rows)

@@ -51,6 +51,7 @@ H8K, W8K = 4320, 7680
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 XGMI_LINK_GBS = 153.0  # per xGMI link of an MI355X (7 per GPU), the figure given with this build
 ROT_BYTES = 1.2e9          # rotate >= 1.2 GB of inputs: defeats the 256 MiB Infinity Cache
+REGION_REPEATS = 7         # extra timed regions for the ms_per_step spread (p10 / p50 / p90)
 # the fused encoder's memory-only floor (19 RGB rows + 24 KiB of stores per unit, no
 # arithmetic) from the committed micro-benchmark log profiles/r02/micro_rgb_rows.log
 # (tools/micro/rgb_rows.hip) -- NOT measured in the bench run; the plane pass's floor
@@ -152,6 +153,14 @@ def cpu_baseline(budget_s):
                                                      "BASELINE.md); its RLE is quadratic (infeasible at 8K)"}
 
 
+def plane_kernel(tmf):
+    """The forward plane kernel the library runs for ZIGZAG_I16 planes (dct_path knob)."""
+    from hiccup_amd import _lib
+    if _lib.get_knob("dct_path") == _lib.DCT_PATH_MFMA:
+        return "k_dct_mfma<%d> (integer MFMA)" % tmf
+    return "k_dct_planes<-1,ZIGZAG_I16,%d> (float64 AAN)" % tmf
+
+
 def extra_4k_luma(steps=20, floor_us=None):
     """BASELINE configs[1]: 4096 x 4096 random luminance, DCT + quantize + zig-zag on
     one GPU (hic_dct_quant_u8_timed: the launch's own begin / end timestamps), with
@@ -179,7 +188,7 @@ def extra_4k_luma(steps=20, floor_us=None):
     us = float(np.mean([e.elapsed_ms() for e in evs])) * 1e3
     gbs = n * n * 3 / (us * 1e-6) / 1e9
     return {"workload": "4096x4096 uint8 luminance -> quantized int16 zig-zag blocks (BASELINE configs[1])",
-            "kernel": "k_dct_planes<0,ZIGZAG_I16,-1>", "avg_launch_us": round(us, 2),
+            "kernel": plane_kernel(-1), "avg_launch_us": round(us, 2),
             "mpix_s": round(n * n / us, 1), "achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
             "algorithmic_bytes": n * n * 3, "timed_launches": steps,
             "memory_floor_us_measured": floor_us,
@@ -281,7 +290,7 @@ def extra_8k_plane_dct(steps=24, luma_only=False, floor_us=None):
                         "(<= 17.8 us for 99.5 MB)" if luma_only else
                         "8K Y + Cr + Cb planes -> quantized int16 zig-zag blocks + RLE tile records (k_dct_planes, "
                         "the DCT+quantize pass without the colour stage)"),
-           "kernel": "k_dct_planes<-1,ZIGZAG_I16,15>", "median_launch_us": round(us, 2),
+           "kernel": plane_kernel(15), "median_launch_us": round(us, 2),
            "achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes": px * 3,
            "read_only_frac": round(px / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4), "timed_launches": steps}
     if luma_only and floor_us:
@@ -331,7 +340,7 @@ def extra_8k_luma_batched(nplanes=8, steps=12):
     return {"workload": "%d x 8K luminance planes (4320 x 7680 uint8, consecutive images) per launch -> quantized "
                         "int16 zig-zag blocks + RLE tile records: north_star's DCT+quantize pass back to back "
                         "(SURVEY.md 8(d): >= 0.70 = <= 17.8 us per plane)" % nplanes,
-            "kernel": "k_dct_mfma<15>" if _lib.get_knob("dct_path") == _lib.DCT_PATH_MFMA else "k_dct_planes<-1,ZIGZAG_I16,15>",
+            "kernel": plane_kernel(15),
             "planes_per_launch": nplanes, "us_per_plane": round(us, 2),
             "launch_us_min_med_max": [round(float(v), 2) for v in (ts.min(), np.median(ts), ts.max())],
             "achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_plane": 3 * px,
@@ -813,10 +822,34 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
+
+    def max_over_ranks(v):
+        if world == 1:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        return float(t.item())
+
+    elapsed = max_over_ranks(elapsed)
+    # spread: the same K-step region (same brackets) repeated; `value` stays the
+    # first region's.  The regions are ~2 ms of wall time each at 8K, so one region's
+    # ms_per_step moves with box clocks and queue timing: these samples say by how much
+    region_ms = [elapsed / args.steps * 1e3]
+    for rep in range(REGION_REPEATS):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        base = args.warmup + args.steps * (rep + 1)
+        for i in range(args.steps):
+            step(base + i)
+        if gather:
+            flush()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        region_ms.append(max_over_ranks(time.perf_counter() - t1) / args.steps * 1e3)
     # every step's symbol counts are valid (a failed step would report a negative count);
     # in stream-gather mode the streams live on the gathering ranks
     stream_gather = gather and args.gather_kind == "stream"
@@ -953,6 +986,10 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step_p10": round(float(np.percentile(region_ms, 10)), 4),
+            "ms_per_step_p50": round(float(np.percentile(region_ms, 50)), 4),
+            "ms_per_step_p90": round(float(np.percentile(region_ms, 90)), 4),
+            "ms_per_step_regions": [round(v, 4) for v in region_ms],
             "higher_is_better": True,
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
@@ -987,8 +1024,8 @@ def main():
                 "kernel": ("k_encode420<15> (RGB -> YCrCb + 4:2:0 pyrDown + AAN DCT + quantize + zig-zag + RLE "
                            "tile records of the rank's image/shard in one launch; algorithmic bytes = 3 B RGB read + "
                            "2 B int16 written per Y / Cr / Cb coefficient)" if fused else
-                           "k_dct_planes<-1,ZIGZAG_I16,15> (Y + Cr + Cb of the rank's image/shard in one launch: "
-                           "AAN DCT + quantize + zig-zag + RLE tile records, per-plane table; 1 B read + 2 B "
+                           plane_kernel(15) + " (Y + Cr + Cb of the rank's image/shard in one launch: "
+                           "DCT + quantize + zig-zag + RLE tile records, per-plane table; 1 B read + 2 B "
                            "written per plane pixel)"),
                 "timed_launches": len(timed_events),
                 "achieved": round(achieved, 1),
@@ -1011,6 +1048,9 @@ def main():
             out["memory_floors"] = floors
             out["roofline"]["device_copy_gbs"] = floors["device_copy_gbs"]
             out["roofline"]["frac_of_device_copy"] = round(achieved / floors["device_copy_gbs"], 4)
+            # the headline normalised by this box's own streaming copy rate (box-to-box
+            # HBM / clock spread divides out): Mpix/s per GB/s of measured device copy
+            out["value_per_copy_gbs"] = round(value / floors["device_copy_gbs"], 5)
         if not args.no_extras and world == 1:
             out["extra_configs"] = {"4k_rgb_encode": extra_4k_rgb_encode(),
                                     "3840x2160_rgb_encode": extra_uhd_rgb_encode(),
@@ -1019,6 +1059,7 @@ def main():
                                     "8k_plane_dct": extra_8k_plane_dct(),
                                     "8k_luma_dct": extra_8k_plane_dct(
                                         luma_only=True, floor_us=floors["luma_pattern"]["1x"]["median_launch_us"]),
+                                    "8k_luma_dct_back_to_back": extra_8k_luma_batched(),
                                     "8k_jpeg_decode": extra_8k_jpeg_decode(),
                                     "8k_encode_from_host": extra_8k_encode_from_host(),
                                     "16k_roundtrip": extra_16k_roundtrip()}

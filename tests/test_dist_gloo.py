@@ -152,13 +152,31 @@ def _worker(rank, world, port, H, W, flat, results):
         # runs); the receiver unpacks, codes the WHOLE stream and must get the
         # single-stream encode
         import wire_host
-        rpt = {k: 1 for k in pipeline.CHANNELS}
-        wr = sharding.wire_ranges(ranges, rpt, False)  # hic_wire_bytes: host code, no GPU
-        assert wr == _wire_ranges_host(ranges)
+        # W % 512 == 0: the fused kernel's record layout (chroma half tiles), every
+        # shard on a record boundary, so the segments carry the shards' RLE tile
+        # records rebased to whole-image positions behind their blocks (ShardEncoder
+        # .pack / .finish); other widths: blocks only (the receiver's tile pass)
+        rpt = pipeline.encoder_layout(H, W, (r0, r1))[1] if W % 512 == 0 else {k: 1 for k in pipeline.CHANNELS}
+        records = sharding.records_aligned(ranges, rpt)
+        assert records == (W % 512 == 0)
+        wr = sharding.wire_ranges(ranges, rpt, records)  # hic_wire_bytes: host code, no GPU
+        if not records:
+            assert wr == _wire_ranges_host(ranges)
+
+        def segment(k, blocks, b0):
+            w = wire_host.pack(blocks, wire_host.TABLE_OF[k])
+            if not records:
+                return w
+            per = 64 // rpt[k]
+            rec = wire_host.rebase(wire_host.tile_records(blocks, per), b0 * 63)  # shard-local, then rebased
+            seg = np.zeros(wr[k][rank][1] - wr[k][rank][0], np.uint8)
+            seg[:len(w)] = w
+            seg[len(w):len(w) + rec.nbytes] = rec.reshape(-1).view(np.uint8)
+            return seg
+
         items = []
         for j in range(world):
-            mine_w = {k: (torch.from_numpy(wire_host.pack(mine[k] + j if j else mine[k],
-                                                          wire_host.TABLE_OF[k]).copy()),)
+            mine_w = {k: (torch.from_numpy(segment(k, mine[k] + j if j else mine[k], ranges[k][rank][0]).copy()),)
                       for k in pipeline.CHANNELS}
             full_w = ({k: (torch.zeros(wr[k][-1][1], dtype=torch.uint8),) for k in pipeline.CHANNELS}
                       if rank == j else None)
@@ -179,6 +197,22 @@ def _worker(rank, world, port, H, W, flat, results):
             whole = np.concatenate(parts)
             want = zz[k] + rank if rank else zz[k]
             ok &= np.array_equal(whole, want)
+            if records:
+                # the placed records (ShardEncoder.finish: record b0 * rpt / 64 of the
+                # whole image's workspace) == the whole image's own tile records
+                per = 64 // rpt[k]
+                recs = np.zeros((-(-len(want) // per), 3), np.int64)
+                for r in range(world):
+                    b0, b1 = ranges[k][r]
+                    nrec = -(-(b1 - b0) * rpt[k] // 64)
+                    if r == rank:
+                        got = wire_host.rebase(wire_host.tile_records(parts[r], per), b0 * 63)
+                    else:
+                        o0, _ = wr[k][r]
+                        wb = wire_host.wire_bytes(b1 - b0, wire_host.TABLE_OF[k])
+                        got = full_w[k][0][o0 + wb:o0 + wb + nrec * 24].numpy().view(np.int64).reshape(nrec, 3)
+                    recs[b0 * rpt[k] // 64:b0 * rpt[k] // 64 + nrec] = got
+                ok &= np.array_equal(recs, wire_host.tile_records(want, per))
             L, V = orc.rle_encode(whole[:, 1:].reshape(-1), 15)
             eL, eV = orc.rle_encode(want[:, 1:].reshape(-1), 15)
             ok &= np.array_equal(L, eL) and np.array_equal(V, eV)
@@ -247,7 +281,10 @@ def _worker(rank, world, port, H, W, flat, results):
 
 
 @pytest.mark.parametrize("world,H,W,flat", [(2, 96, 80, None), (3, 130, 72, None), (4, 160, 48, None),
-                                            (3, 144, 64, (48, 96))])
+                                            (3, 144, 64, (48, 96)), (2, 64, 512, None),
+                                            # the 8K plan's geometry: 270 unit rows over 8 ranks (34 / 33 each),
+                                            # W % 512 == 0 (records rebased and gathered with the blocks)
+                                            (8, 4320, 512, None)])
 def test_sharded_exchange_gloo(world, H, W, flat):
     mgr = mp.Manager()
     results = mgr.dict()

@@ -67,3 +67,35 @@ def random_blocks(rng, n, table):
     b = (rng.random((n, 64)) * (hi - lo) + lo).astype(np.int64)
     b[rng.random((n, 64)) < 0.5] = 0
     return b.astype(np.int16)
+
+
+def tile_records(zz, per, M=15, base_blk=0):
+    """Host restatement of the RLE tile records (rle_core.h tile_record16 /
+    tile_record16_half): (n, 64) zig-zag blocks -> int64 [ceil(n / per), 3] with
+    `per` blocks per record (64: full tiles, 32: the fused kernel's chroma half
+    tiles); AC element j of block b sits at stream position (base_blk + b) * 63 + j.
+      [0] position of the record's first nonzero AC (-1: none)
+      [1] position of its last nonzero AC (-1: none)
+      [2] symbols of every nonzero but the first: 1 + run // M each, runs counted
+          across the record's blocks (codec.py:55-99 splits runs >= M)."""
+    zz = np.asarray(zz)
+    n = zz.shape[0]
+    nrec = -(-n // per)
+    out = np.zeros((nrec, 3), np.int64)
+    for r in range(nrec):
+        pos = np.flatnonzero(zz[r * per:(r + 1) * per, 1:].reshape(-1) != 0)
+        if len(pos) == 0:
+            out[r] = (-1, -1, 0)
+            continue
+        g0 = (base_blk + r * per) * 63
+        gaps = np.diff(pos) - 1
+        out[r] = (g0 + pos[0], g0 + pos[-1], len(gaps) + int((gaps // M).sum()))
+    return out
+
+
+def rebase(rec, shift):
+    """hic_rle_records_rebase: positions (>= 0) moved by `shift`, counts kept."""
+    out = rec.copy()
+    for c in (0, 1):
+        out[:, c] = np.where(rec[:, c] >= 0, rec[:, c] + shift, rec[:, c])
+    return out

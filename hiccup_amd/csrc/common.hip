@@ -76,7 +76,10 @@ extern "C" int hic_set_knob(int k, int value) {
   if (k == HIC_KNOB_DCT_PATH && value != -1 && !(value == 0 || value == 1 || value == 2 || value == 5))
     return hic::arg_error("dct path %d (0 exact, 1 / 2 float64 AAN, 5 integer MFMA)", value);
   if (k == HIC_KNOB_COLOR_SEG && value != -1 && value != 8 && value != 16) return hic::arg_error("colour segment");
-  if (k == HIC_KNOB_ENCODE_WAVES && value != -1 && value != 2 && value != 3) return hic::arg_error("encode waves");
+  // retired variants (measured slower, removed in round 4): only the shipped value
+  if (k == HIC_KNOB_ENCODE_WAVES && value != -1 && value != 3) return hic::arg_error("encode waves: 3 only (retired)");
+  if (k == HIC_KNOB_ENCODE_NT && value != -1 && value != 1) return hic::arg_error("encode_nt: 1 only (retired)");
+  if (k == HIC_KNOB_ENCODE_DCT && value != -1 && value != 0) return hic::arg_error("encode_dct: 0 only (retired)");
   if (value < -1) return hic::arg_error("knob value %d", value);
 #ifndef HIC_DEV
   if (k == HIC_KNOB_DEV && value > 0) return hic::arg_error("the dev knob needs a -DHIC_DEV build");

@@ -558,48 +558,6 @@ __host__ __device__ __forceinline__ void dct_fix26(const uint2 (&w)[8], int (&q)
 
 
 // ---------------------------------------------------------------------------
-// Float32 fast path (production, aligned planes).  The AAN factorisation runs in
-// float32 on the raw pixel bytes (v_cvt_f32_ubyteN; the -128 offset of
-// dct_channel only reaches the DC, which is computed apart as an exact integer),
-// so its float work issues at the 32-bit rate and needs half the registers of the
-// float64 path.  Exactness rests on proven bounds, not on measurement
-// (tools/check/dct_bounds.py): for every (u, v) and table the
-// float32 estimate e = Y * R of y / T is within E1[t][u][v] (2^-10 .. 2^-16) of
-// the exact value, and pocketfft's own float64 y within EP of it.  The quantiser
-// takes q = rint(e) and d = e - q; |d| <= kThr32 = 1/2 - W1 with W1 > E1 + EP/T
-// + test rounding proves q == rint(fl(y_pf / T)), the reference's value.  A
-// coefficient with |d| > kThr32 ("flagged", ~0.03 per block on random data) is
-// handed to `flag`, which resolves it with the float64 fallback below.
-constexpr float kM32 = 0x1.8p23f;  // fl(e + kM32) = kM32 + rint(e); low 16 bits of the bits = q
-
-__host__ __device__ __forceinline__ void aan8_f32(const float (&x)[8], float (&o)[8]) {
-  // float32 roundings of the AAN constants (the bounds take |K - c| <= 2^-24 |c|)
-  constexpr float a1 = (float)kA1, a2 = (float)kA2, a4 = (float)kA4, a5 = (float)kA5;
-  const float s0 = x[0] + x[7], s1 = x[1] + x[6], s2 = x[2] + x[5], s3 = x[3] + x[4];
-  const float t10 = s0 + s3, t13 = s0 - s3, t11 = s1 + s2, t12 = s1 - s2;
-  o[0] = t10 + t11;
-  o[4] = t10 - t11;
-  const float wv = t12 + t13;
-  o[2] = __builtin_fmaf(a1, wv, t13);
-  o[6] = __builtin_fmaf(-a1, wv, t13);
-  const float d7 = x[0] - x[7], d6 = x[1] - x[6], d5 = x[2] - x[5], d4 = x[3] - x[4];
-  const float u10 = d4 + d5, u11 = d5 + d6, u12 = d6 + d7;
-  const float z5 = (u10 - u12) * a5;
-  const float z2 = __builtin_fmaf(a2, u10, z5), z4 = __builtin_fmaf(a4, u12, z5);
-  const float z11 = __builtin_fmaf(a1, u11, d7), z13 = __builtin_fmaf(-a1, u11, d7);
-  o[5] = z13 + z2;
-  o[3] = z13 - z2;
-  o[1] = z11 + z4;
-  o[7] = z11 - z4;
-}
-
-__host__ __device__ __forceinline__ float byte_f32(uint32_t w, int k) {
-  return (float)((w >> (8 * k)) & 0xFFu);  // v_cvt_f32_ubyte<k>
-}
-
-// The bit pattern's low 16 bits of fl(e + kM32) (== rint(e) mod 2^16).
-__host__ __device__ __forceinline__ uint32_t f32_bits(float f) { return __builtin_bit_cast(uint32_t, f); }
-
 // round-half-even(4 X / T[0][0]) for the centred pixel sum X (|X| <= 8192), in
 // integers: the DC is exact, and its ties (X = 2 mod 4 for T = 16) are real.
 template <int TABLE>
@@ -608,253 +566,6 @@ __host__ __device__ __forceinline__ int dc_quant(int X) {
   const int a = 8 * X + T;                        // 2 (4X) + T
   const int q = (a >= 0 ? a : a - (2 * T - 1)) / (2 * T);  // floor(a / 2T)
   return (a == q * 2 * T && (q & 1)) ? q - 1 : q;  // exact tie: to even
-}
-
-// Even (0, 2, 4, 6) or odd (1, 3, 5, 7) outputs of the AAN 8-point DCT-II.
-template <int PH>
-__host__ __device__ __forceinline__ void aan4_f32(const float (&x)[8], float (&o)[4]) {
-  constexpr float a1 = (float)kA1, a2 = (float)kA2, a4 = (float)kA4, a5 = (float)kA5;
-  if (PH == 0) {
-    const float s0 = x[0] + x[7], s1 = x[1] + x[6], s2 = x[2] + x[5], s3 = x[3] + x[4];
-    const float t10 = s0 + s3, t13 = s0 - s3, t11 = s1 + s2, t12 = s1 - s2;
-    const float wv = t12 + t13;
-    o[0] = t10 + t11;
-    o[1] = __builtin_fmaf(a1, wv, t13);   // output 2
-    o[2] = t10 - t11;                     // output 4
-    o[3] = __builtin_fmaf(-a1, wv, t13);  // output 6
-  } else {
-    const float d7 = x[0] - x[7], d6 = x[1] - x[6], d5 = x[2] - x[5], d4 = x[3] - x[4];
-    const float u10 = d4 + d5, u11 = d5 + d6, u12 = d6 + d7;
-    const float z5 = (u10 - u12) * a5;
-    const float z2 = __builtin_fmaf(a2, u10, z5), z4 = __builtin_fmaf(a4, u12, z5);
-    const float z11 = __builtin_fmaf(a1, u11, d7), z13 = __builtin_fmaf(-a1, u11, d7);
-    o[0] = z11 + z4;  // output 1
-    o[1] = z13 - z2;  // output 3
-    o[2] = z13 + z2;  // output 5
-    o[3] = z11 - z4;  // output 7
-  }
-}
-
-// One 8x8 block (this lane's raw pixel rows) -> quantized int16 coefficients at
-// st[slot] in the order of LAYOUT.  Two phases (even row outputs -> even
-// columns, then odd -> odd), so only half the row outputs are live at once.
-// After each column v, flag(v, rr, d, f) gets its 8 coefficients (u = 0..7):
-// rr = rint(e) as float, d = e - rr, f = (|d| > kThr32[TABLE][8u + v]); f[0] is
-// false for the DC, which is exact.
-template <int TABLE, int LAYOUT, typename Flag>
-__host__ __device__ __forceinline__ void dct_block_f32(const uint2 (&w)[8], int16_t *st, Flag &&flag) {
-  constexpr SlotOf<LAYOUT> kSlot{};
-#pragma unroll
-  for (int ph = 0; ph < 2; ++ph) {
-    uint2 wp[8];  // this phase's copy of the rows, opaque: the compiler must not keep
-                  // 64 unpacked pixels live from the even phase into the odd one
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      wp[r] = w[r];
-#ifdef __HIP_DEVICE_COMPILE__
-      asm volatile("" : "+v"(wp[r].x), "+v"(wp[r].y));
-#endif
-    }
-    float a[8][4];  // this phase's row outputs [row][k]: column v = 2k + ph
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const float x[8] = {byte_f32(wp[r].x, 0), byte_f32(wp[r].x, 1), byte_f32(wp[r].x, 2), byte_f32(wp[r].x, 3),
-                          byte_f32(wp[r].y, 0), byte_f32(wp[r].y, 1), byte_f32(wp[r].y, 2), byte_f32(wp[r].y, 3)};
-      if (ph == 0)
-        aan4_f32<0>(x, a[r]);
-      else
-        aan4_f32<1>(x, a[r]);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int v = 2 * k + ph;
-      float c[8], Y[8];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) c[r] = a[r][k];
-      aan8_f32(c, Y);
-      float rr[8], d[8];
-      bool f[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int i = u * 8 + v;
-        if (i == 0) {
-          // DC: Y = the sum of the raw bytes (exact); y00 = 4 (Y - 64 * 128)
-          st[kSlot.s[0]] = (int16_t)dc_quant<TABLE>((int)Y[0] - 8192);
-          rr[0] = 0.f, d[0] = 0.f, f[0] = false;
-          continue;
-        }
-        const float R = kR32[TABLE][i];
-        const float t = __builtin_fmaf(Y[u], R, kM32);
-        const float nrr = kM32 - t;                    // -rint(e), exact
-        d[u] = __builtin_fmaf(Y[u], R, nrr);           // e - rint(e), |error| <= 2^-25
-        rr[u] = -nrr;
-        f[u] = __builtin_fabsf(d[u]) > kThr32[TABLE][i];
-        st[kSlot.s[i]] = (int16_t)(f32_bits(t) & 0xFFFFu);
-      }
-      flag(v, rr, d, f);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Packed float32 transform (production forward path for aligned planes).
-// Every float value is a <2 x float> holding two transforms of ONE block (see
-// dct_block_pk), so each AAN operation of dct_block_f32 above is one
-// v_pk_{add,mul,fma}_f32 for two of them.  The per-element operations and their
-// order are exactly dct_block_f32's (aan4_f32 / aan8_f32), so the proven bounds
-// (dct_bounds.py E1, dct_windows.h) hold unchanged:
-//  * rows: s_k = x_k + x_{7-k} and d_k = x_k - x_{7-k} of the raw pixel bytes are
-//    integers (exact as float32), formed on the integer unit before the convert;
-//  * columns: the AAN on the row outputs, then per coefficient e = Y R:
-//      t = fma(Y, R, 1.5 2^23)  -> low 16 bits of t's bits = rint(e) (the int16 q)
-//      d = fma(Y, R, 1.5 2^23 - t) = e - rint(e) (exact to 2^-25)
-//      g = fma(-d, d, c)        -> sign bit set iff d^2 > c, c <= kThr32^2: flagged
-//    the flag bits shift into one dword per phase (v_alignbit);
-//  * (0,0): the raw-byte sum is exact; dc_quant rounds 4 X / T in integers.
-//    (4,4): Y44 is an exact integer, so only an exact tie can be flagged there
-//    (luminance: 2.9 % of random blocks; chrominance never ties); such a tie is
-//    decided in place with pocketfft's own float64 operations on the rows' outputs 4.
-// Any other flagged coefficient's q is provisional; the caller resolves it exactly
-// (resolve_coef) and overwrites it.
-typedef float f2 __attribute__((ext_vector_type(2)));
-__host__ __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-__host__ __device__ __forceinline__ f2 splat2(float k) { return (f2){k, k}; }
-
-// AAN even half from s_k = x_k + x_{7-k}: outputs 0, 2, 4, 6 -> o[0..3] (aan4_f32<0>)
-__host__ __device__ __forceinline__ void aan_even_pk(f2 s0, f2 s1, f2 s2, f2 s3, f2 (&o)[4]) {
-  const f2 a1 = splat2((float)kA1);
-  const f2 t10 = s0 + s3, t13 = s0 - s3, t11 = s1 + s2, t12 = s1 - s2;
-  const f2 wv = t12 + t13;
-  o[0] = t10 + t11;
-  o[1] = pk_fma(a1, wv, t13);
-  o[2] = t10 - t11;
-  o[3] = pk_fma(-a1, wv, t13);
-}
-// AAN odd half from d7 = x0 - x7, d6 = x1 - x6, d5 = x2 - x5, d4 = x3 - x4:
-// outputs 1, 3, 5, 7 -> o[0..3] (aan4_f32<1>)
-__host__ __device__ __forceinline__ void aan_odd_pk(f2 d7, f2 d6, f2 d5, f2 d4, f2 (&o)[4]) {
-  const f2 a1 = splat2((float)kA1), a2 = splat2((float)kA2), a4 = splat2((float)kA4), a5 = splat2((float)kA5);
-  const f2 u10 = d4 + d5, u11 = d5 + d6, u12 = d6 + d7;
-  const f2 z5 = (u10 - u12) * a5;
-  const f2 z2 = pk_fma(a2, u10, z5), z4 = pk_fma(a4, u12, z5);
-  const f2 z11 = pk_fma(a1, u11, d7), z13 = pk_fma(-a1, u11, d7);
-  o[0] = z11 + z4;
-  o[1] = z13 - z2;
-  o[2] = z13 + z2;
-  o[3] = z11 - z4;
-}
-
-__host__ __device__ __forceinline__ uint32_t pk_byte(uint32_t w, int k) { return (w >> (8 * k)) & 0xFFu; }
-__host__ __device__ __forceinline__ f2 pk_i2f(int a, int b) { return (f2){(float)a, (float)b}; }
-
-// One 8x8 block (this lane's raw pixel rows) on the packed path: the two halves of
-// every <2 x float> are two rows (row pass: rows 2m, 2m + 1) or two columns
-// (column pass) of the SAME block, so one lane holds one block and each AAN
-// operation is one v_pk_*_f32 for two of its transforms.  Two phases keep half the
-// row outputs live: PH 0 the rows' even outputs (from s_k = x_k + x_{7-k}) feed the
-// column pairs (0, 2) and (4, 6); PH 1 the odd outputs (from d_k = x_k - x_{7-k})
-// the pairs (1, 3) and (5, 7).  A 2 x 2 transpose (v_pk_mov_b32) turns row pairs
-// into column pairs.  Quantised coefficients go to st (zig-zag slots, int16);
-// f0 / f1 collect the flag bits: the p-th coefficient quantised (p = 16 c + 2 u + h:
-// column kPkCol[c] + 2h, row u) is bit 31 - (p & 31) of f[p >> 5].
-constexpr int kPkCol[4] = {0, 4, 1, 5};
-
-template <int TABLE, int PH>
-__host__ __device__ __forceinline__ void dct_block_pk_phase(const uint2 (&w)[8], int16_t *st, uint32_t &f) {
-  constexpr SlotOf<HIC_LAYOUT_ZIGZAG_I16> kSlot{};
-  f2 R[4][4];  // R[m][k] = (row 2m's output 2k + PH, row 2m + 1's output 2k + PH)
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    uint2 a = w[2 * m], b = w[2 * m + 1];
-#ifdef __HIP_DEVICE_COMPILE__
-    // opaque per-phase copies: the byte extracts both phases read must not be kept
-    // live from the even phase into the odd one
-    asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(b.x), "+v"(b.y));
-#endif
-    if (PH == 0) {  // s_k = x_k + x_{7-k} of the raw bytes (exact integers)
-      const f2 s0 = pk_i2f((int)(pk_byte(a.x, 0) + pk_byte(a.y, 3)), (int)(pk_byte(b.x, 0) + pk_byte(b.y, 3)));
-      const f2 s1 = pk_i2f((int)(pk_byte(a.x, 1) + pk_byte(a.y, 2)), (int)(pk_byte(b.x, 1) + pk_byte(b.y, 2)));
-      const f2 s2 = pk_i2f((int)(pk_byte(a.x, 2) + pk_byte(a.y, 1)), (int)(pk_byte(b.x, 2) + pk_byte(b.y, 1)));
-      const f2 s3 = pk_i2f((int)(pk_byte(a.x, 3) + pk_byte(a.y, 0)), (int)(pk_byte(b.x, 3) + pk_byte(b.y, 0)));
-      aan_even_pk(s0, s1, s2, s3, R[m]);  // outputs 0, 2, 4, 6
-    } else {  // d_k = x_k - x_{7-k}
-      const f2 d7 = pk_i2f((int)pk_byte(a.x, 0) - (int)pk_byte(a.y, 3), (int)pk_byte(b.x, 0) - (int)pk_byte(b.y, 3));
-      const f2 d6 = pk_i2f((int)pk_byte(a.x, 1) - (int)pk_byte(a.y, 2), (int)pk_byte(b.x, 1) - (int)pk_byte(b.y, 2));
-      const f2 d5 = pk_i2f((int)pk_byte(a.x, 2) - (int)pk_byte(a.y, 1), (int)pk_byte(b.x, 2) - (int)pk_byte(b.y, 1));
-      const f2 d4 = pk_i2f((int)pk_byte(a.x, 3) - (int)pk_byte(a.y, 0), (int)pk_byte(b.x, 3) - (int)pk_byte(b.y, 0));
-      aan_odd_pk(d7, d6, d5, d4, R[m]);  // outputs 1, 3, 5, 7
-    }
-  }
-  const f2 kM = splat2(kM32);
-#pragma unroll
-  for (int jj = 0; jj < 2; ++jj) {
-    const int c = 2 * PH + jj, v0 = kPkCol[c];  // column pair (v0, v0 + 2): row outputs 2jj, 2jj + 1 of the phase
-    f2 X[8];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      X[2 * m] = (f2){R[m][2 * jj].x, R[m][2 * jj + 1].x};
-      X[2 * m + 1] = (f2){R[m][2 * jj].y, R[m][2 * jj + 1].y};
-    }
-    const f2 s0 = X[0] + X[7], s1 = X[1] + X[6], s2 = X[2] + X[5], s3 = X[3] + X[4];
-    const f2 d7 = X[0] - X[7], d6 = X[1] - X[6], d5 = X[2] - X[5], d4 = X[3] - X[4];
-    f2 ev[4], od[4];
-    aan_even_pk(s0, s1, s2, s3, ev);
-    aan_odd_pk(d7, d6, d5, d4, od);
-    const f2 Y[8] = {ev[0], od[0], ev[1], od[1], ev[2], od[2], ev[3], od[3]};
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i0 = u * 8 + v0, i1 = i0 + 2;
-      const f2 Rq = (f2){kR32[TABLE][i0], kR32[TABLE][i1]};
-      const f2 t = pk_fma(Y[u], Rq, kM);
-      const f2 d = pk_fma(Y[u], Rq, kM - t);
-      const f2 g = pk_fma(-d, d, (f2){kThr32Sq[TABLE][i0], kThr32Sq[TABLE][i1]});
-      if (i0 == 0) {
-        // DC: Y = the sum of the raw bytes (exact); y00 = 4 (Y - 64 * 128), never flagged
-        st[kSlot.s[0]] = (int16_t)dc_quant<TABLE>((int)Y[0].x - 8192);
-        f <<= 1;
-      } else if (i0 == 36 && TABLE == 0) {
-        // (4,4), luminance: Y44 is an exact integer, so a flag means an exact tie
-        // (Y44 = 17 mod 34), which pocketfft's own roundings decide: its row outputs
-        // 4 are the integers X[r].x (this column pair's first half), scaled by TW3
-        // in float64 and combined as pf_y44 does.  In place, no queue entry.
-        int q = (int)(f32_bits(t.x) & 0xFFFFu);
-        const bool tie = (f32_bits(g.x) >> 31) != 0;
-#ifdef __HIP_DEVICE_COMPILE__
-        if (__builtin_amdgcn_ballot_w64(tie))
-#endif
-        {
-          if (tie) {
-            double y[8];
-#pragma unroll
-            for (int r = 0; r < 8; ++r) y[r] = (double)X[r].x * TW3;
-            const double c1 = y[1] + y[2], c3 = y[3] + y[4], c5 = y[5] + y[6], H0 = y[0] + y[7];
-            const double h1 = c1 + c5, T2 = H0 + c3;
-            q = quant_fast<0>((T2 - h1) * TW3, 36);
-          }
-        }
-        st[kSlot.s[36]] = (int16_t)q;
-        f <<= 1;
-      } else {
-        st[kSlot.s[i0]] = (int16_t)(f32_bits(t.x) & 0xFFFFu);
-        f = (f << 1) | (f32_bits(g.x) >> 31);  // a funnel shift: one v_alignbit_b32
-      }
-      st[kSlot.s[i1]] = (int16_t)(f32_bits(t.y) & 0xFFFFu);
-      f = (f << 1) | (f32_bits(g.y) >> 31);
-    }
-  }
-}
-
-template <int TABLE>
-__host__ __device__ __forceinline__ void dct_block_pk(const uint2 (&w)[8], int16_t *st, uint32_t &f0, uint32_t &f1) {
-  dct_block_pk_phase<TABLE, 0>(w, st, f0);
-  dct_block_pk_phase<TABLE, 1>(w, st, f1);
-}
-
-// The raster index of flag bit b (0..63: bits 0..31 of f0, then of f1) of
-// dct_block_pk.
-__host__ __device__ __forceinline__ int pk_flag_index(int b) {
-  const int p = (b & 32) + 31 - (b & 31), c = p >> 4, u = (p >> 1) & 7, h = p & 1;
-  return u * 8 + kPkCol[c] + 2 * h;
 }
 
 // Fallback: y_uv (full scale, as scipy's 2-D DCT-II of the centred block) in

@@ -27,10 +27,9 @@
 //      (the strip's edge pixels converted once per unit, one row per lane, and
 //      written into lane 0 / 63 by v_writelane), the vertical taps over a 5-row
 //      window -> 8 chroma rows x 4 columns per lane and plane;
-//   2. DCT of Y block row 0 and row 1 (lane = block; after all 19 colour rows in
-//      the default 3-waves-per-SIMD kernel, between the colour rows 0..9 and
-//      10..18 in the 2-wave one): coefficients to the LDS stage at their zig-zag
-//      slot, copied out in 1 KiB stores, the tile record from the stage;
+//   2. DCT of Y block row 0 and row 1 (lane = block; after all 19 colour rows):
+//      coefficients to the LDS stage at their zig-zag slot, copied out in 1 KiB
+//      stores, the tile record from the stage;
 //   3. chroma: the colour stage left the chroma rows in a 4 KiB LDS area per wave;
 //      chroma block m of Cr is read into lane m and of Cb into lane 32 + m (a
 //      block spans the columns of lanes 2m, 2m + 1), one DCT pass with the
@@ -53,7 +52,7 @@ struct Enc420 {
   int16_t *coef[3];  // ZIGZAG_I16 blocks of the shard's Y, Cr, Cb planes
   int64_t *rec[3];   // tile records: Y per 64-block tile, Cr / Cb per 32-block half tile
   int M;
-  int nstrips, nunits;  // nunits: waves (HIC_ENC_VG unit rows each)
+  int nstrips, nunits;  // nunits: waves (one unit each)
   int wlast;            // pixel columns of the last strip (16 .. 512)
 };
 
@@ -98,188 +97,9 @@ __device__ __forceinline__ void enc_dct(uint2 (&w)[8], int16_t *st) {
   }
 }
 
-// Float32 AAN variant (knob "encode_dct" = 1): dct_block_f32 (dct_core.h) with the
-// proven float32 tie windows (dct_windows.h, tools/check/dct_bounds.py E1); a
-// flagged coefficient (~0.03 per block on random data) is resolved in place by
-// resolve_coef (float64 dot product, then pocketfft's own operations for the
-// rational classes), a coefficient that stays ambiguous sends the block to the
-// exact replica.  Out of line: the flagged lanes only.  Measured slower than the
-// float64 path (104-111 vs 65-72 us at 8K, profiles/r02/ab_fused_f32.log): the
-// out-of-line resolve costs more than the float32 arithmetic saves.
-template <int TABLE>
-__device__ __attribute__((noinline)) bool enc_resolve(uint2 w0, uint2 w1, uint2 w2, uint2 w3, uint2 w4, uint2 w5,
-                                                      uint2 w6, uint2 w7, uint32_t mlo, uint32_t mhi, int16_t *st) {
-  const uint2 w[8] = {w0, w1, w2, w3, w4, w5, w6, w7};
-  constexpr SlotOf<kZZ> kSlot{};
-  uint64_t m = ((uint64_t)mhi << 32) | mlo;
-  bool ok = true;
-  while (m) {
-    const int i = __builtin_ctzll(m);
-    m &= m - 1;
-    int q = 0;
-    if (resolve_coef(w, TABLE, i, q))
-      st[kSlot.s[i]] = (int16_t)q;
-    else
-      ok = false;
-  }
-  return ok;
-}
-
-template <int TABLE>
-__device__ __forceinline__ void enc_dct_f32(uint2 (&w)[8], int16_t *st) {
-  uint32_t mlo = 0, mhi = 0;
-  auto sink = [&](int v, const float (&rr)[8], const float (&d)[8], const bool (&f)[8]) {
-    (void)rr;
-    (void)d;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = u * 8 + v;
-      if (i < 32)
-        mlo |= (uint32_t)f[u] << i;
-      else
-        mhi |= (uint32_t)f[u] << (i - 32);
-    }
-  };
-  dct_block_f32<TABLE, kZZ>(w, st, sink);
-  const bool has = (mlo | mhi) != 0;
-  if (__builtin_amdgcn_ballot_w64(has)) {
-    bool ok = true;
-    if (has) ok = enc_resolve<TABLE>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], mlo, mhi, st);
-    if (__builtin_amdgcn_ballot_w64(!ok)) enc_exact_block<TABLE>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], st);
-  }
-}
-
-// Packed float32 variant (knob "encode_dct" = 2): dct_block_pk (dct_core.h: two
-// transforms of the block per v_pk op, (4,4) ties decided in place), the proven
-// float32 windows.  A flagged coefficient (~0.03 per block on random data) keeps
-// its provisional q (the estimate's rint) in the stage, which leaves for HBM as
-// usual, and is DEFERRED: the owner lane appends {block, plane, flag bit,
-// provisional q} and its block's 64 B of pixels to the WORKGROUP's LDS queue (one
-// LDS atomic per wave and compaction step).  When the workgroup's four units are
-// done, each wave resolves up to 64 queued items in ONE round, one per lane
-// (resolve_coef: float64 dot product, pocketfft's own operations for the rational
-// classes), patches the coefficient in HBM if it changed, and marks the unit's
-// record if q crossed zero (a flag moves q by at most one, so only then does the
-// tile record, built from the provisional stage, change); the marked records are
-// rebuilt from HBM afterwards.  One resolve round per four units, instead of one
-// per DCT pass (three per unit) as an in-place resolve needs.  A coefficient
-// resolve_coef cannot settle sends its block to the exact replica (whole block
-// patched); a queue overflow (tie-dense input only) does so in place, before the
-// store.
 #ifndef HIC_ENC_WPB
-#define HIC_ENC_WPB 4  // waves per workgroup (<= 4: the deferred queue's wave field)
+#define HIC_ENC_WPB 4  // waves per workgroup
 #endif
-static_assert(HIC_ENC_WPB <= 4, "enc_dct_pk's queue header holds a 2-bit wave index");
-constexpr int kEncQCap = 64 * HIC_ENC_WPB;
-
-struct EncQueue {
-  uint2 *qh;         // {block index in its plane, plane << 28 | Y row << 27 | wave << 16 ... see enc_enqueue}
-  uint4 *qp;         // 4 x 16 B: the block's 8 pixel rows
-  int *qn;           // items appended (may exceed kEncQCap: overflow)
-  uint32_t *dirty;   // bit 3 wave + r: record r (0, 1 Y block rows, 2 chroma) of that wave's unit
-};
-
-// header y: plane (2 bits) << 28 | rec (2 bits: 0/1 Y row, 2 chroma) << 24 | wave
-// (2 bits) << 22 | flag bit (6) << 16 | provisional q (16)
-template <int TABLE>
-__device__ __forceinline__ void enc_dct_pk(uint2 (&w)[8], int16_t *st, const EncQueue &Q, bool valid, int plane,
-                                           int rec, int wv, int blk) {
-  constexpr SlotOf<kZZ> kSlot{};
-  uint32_t f0 = 0, f1 = 0;
-  dct_block_pk<TABLE>(w, st, f0, f1);
-  const int lane = threadIdx.x & 63;
-  uint64_t bits = valid ? ((uint64_t)f1 << 32) | f0 : 0;
-#if defined(HIC_DEV) && defined(HIC_ENC_DEV) && (HIC_ENC_DEV & 4)
-  bits = 0;  // dev timing (results invalid): flags dropped, no resolve
-#endif
-  if (!__builtin_amdgcn_ballot_w64(bits != 0)) return;
-  bool redo = false;
-  for (;;) {  // compact: one flag per lane per step
-    const bool has = bits != 0;
-    const uint64_t m = __builtin_amdgcn_ballot_w64(has);
-    if (!m) break;
-    const int l0 = __builtin_ctzll(m);
-    int base = 0;
-    if (lane == l0) base = atomicAdd(Q.qn, __builtin_popcountll(m));
-    base = __builtin_amdgcn_readlane(base, l0);
-    if (has) {
-      const int b = __builtin_ctzll(bits);
-      bits &= bits - 1;
-      const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      if (pos < kEncQCap) {
-        const uint32_t q0 = (uint16_t)st[kSlot.s[pk_flag_index(b)]];
-        Q.qh[pos] = make_uint2((uint32_t)blk, (uint32_t)plane << 28 | (uint32_t)rec << 24 | (uint32_t)wv << 22 |
-                                                  (uint32_t)b << 16 | q0);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          Q.qp[4 * pos + r] = make_uint4(w[2 * r].x, w[2 * r].y, w[2 * r + 1].x, w[2 * r + 1].y);
-      } else {
-        redo = true;
-      }
-    }
-  }
-  // queue full: this lane's block on the exact replica now (its items queued so far
-  // resolve to the same values later)
-  if (__builtin_amdgcn_ballot_w64(redo))
-    if (redo) enc_exact_block<TABLE>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], st);
-}
-
-// The workgroup's deferred items: wave wv resolves items 64 wv .. 64 wv + 63, one per
-// lane (st: this lane's stage row, free once the units are done).  Called by every
-// wave of the workgroup after a barrier that follows all enqueues and all stores.
-__device__ __forceinline__ void enc_resolve_queue(const Enc420 &E, const EncQueue &Q, int wv, int lane, int16_t *st,
-                                                  const double *cm, const uint8_t *qt) {
-  constexpr SlotOf<kZZ> kSlot{};
-  int n = *Q.qn;
-  n = n < kEncQCap ? n : kEncQCap;
-  const int j = 64 * wv + lane;
-  if (j >= n) return;
-  const uint2 h = Q.qh[j];
-  uint2 w[8];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint4 t = Q.qp[4 * j + k];
-    w[2 * k] = make_uint2(t.x, t.y);
-    w[2 * k + 1] = make_uint2(t.z, t.w);
-  }
-  const int plane = (int)(h.y >> 28), table = plane > 0 ? 1 : 0;
-  const int i = pk_flag_index((int)((h.y >> 16) & 63u));
-  const int q0 = (int)(int16_t)(h.y & 0xFFFFu);
-  int16_t *o = E.coef[plane] + (int64_t)h.x * 64;
-  bool mark = false;
-  int q = 0;
-  if (resolve_coef(w, table, i, q, cm, qt)) {
-    if (q != q0) {
-      o[kSlot.s[i]] = (int16_t)q;
-      mark = (q == 0) != (q0 == 0);
-    }
-  } else {
-    if (table == 0)
-      enc_exact_block<0>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], st);
-    else
-      enc_exact_block<1>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], st);
-    const uint2 *s2 = reinterpret_cast<const uint2 *>(st);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const uint2 lo = s2[2 * k], hi = s2[2 * k + 1];
-      reinterpret_cast<uint4 *>(o)[k] = make_uint4(lo.x, lo.y, hi.x, hi.y);
-    }
-    mark = true;
-  }
-  if (mark) atomicOr(Q.dirty, 1u << (3 * ((h.y >> 22) & 3u) + ((h.y >> 24) & 3u)));
-}
-
-// DM: the DCT variant (0 float64 AAN, 1 scalar float32, 2 packed float32 + deferred resolve)
-template <int TABLE, int DM>
-__device__ __forceinline__ void enc_dct_any(uint2 (&w)[8], int16_t *st, const EncQueue &Q, bool valid, int plane,
-                                            int rec, int wv, int blk) {
-  if (DM == 2)
-    enc_dct_pk<TABLE>(w, st, Q, valid, plane, rec, wv, blk);
-  else if (DM == 1)
-    enc_dct_f32<TABLE>(w, st);
-  else
-    enc_dct<TABLE>(w, st);
-}
 
 // 16 B chunk k of stage row b
 __device__ __forceinline__ uint4 enc_st16(const uint2 *st2, int b, int k) {
@@ -288,10 +108,11 @@ __device__ __forceinline__ uint4 enc_st16(const uint2 *st2, int b, int k) {
 }
 
 // stage rows 0..31 -> o_lo (32 blocks), rows 32..63 -> o_hi: 1 KiB per store
-// instruction, nontemporal (the coefficients are not re-read by this kernel).
-// n_lo / n_hi (wave-uniform): blocks of o_lo / o_hi that exist (32 but in a
-// ragged strip)
-template <bool NT>
+// instruction, nontemporal (the coefficients are not re-read by this kernel; with 3
+// waves per SIMD and 4 images in flight nontemporal stores won against cached ones
+// in 3 of 3 alternating pairs, 0.0999-0.1033 vs 0.1041-0.1051 ms/step,
+// profiles/r03/s2/nt/).  n_lo / n_hi (wave-uniform): blocks of o_lo / o_hi that
+// exist (32 but in a ragged strip)
 __device__ __forceinline__ void enc_store(const uint2 *st2, int lane, int16_t *o_lo, int16_t *o_hi, int n_lo = 32,
                                           int n_hi = 32) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -302,10 +123,7 @@ __device__ __forceinline__ void enc_store(const uint2 *st2, int lane, int16_t *o
     const u32x4 v = {t.x, t.y, t.z, t.w};
     u32x4 *o = reinterpret_cast<u32x4 *>(k < 4 ? o_lo : o_hi) + 64 * (k & 3) + lane;
     if (!full && 8 * (k & 3) + (lane >> 3) >= (k < 4 ? n_lo : n_hi)) continue;
-    if (NT)
-      __builtin_nontemporal_store(v, o);
-    else
-      *o = v;
+    __builtin_nontemporal_store(v, o);
   }
 }
 
@@ -549,110 +367,66 @@ struct EncColour {
   }
 };
 
-#ifndef HIC_ENC_VG
-#define HIC_ENC_VG 1  // 16-row units per wave (2: two vertically adjacent units, 35 input rows
-                      // for 32; measured 61-65 vs 60-63 us: no gain, scripts/gpu_r2ah.sh)
-#endif
-template <int TMF, bool NT, int DM, bool W3 = false>
-__device__ __forceinline__ void encode420_unit(const Enc420 &E);
-
-// Two register budgets (knob "encode_waves"): 3 waves per SIMD (default since round
-// 3: <= 168 VGPRs, the 19 colour rows before the three DCT passes, packed Y rows
-// pinned; ~8 dwords of spill; launch equal to 2 waves, 8K bench 0.1017-0.1041 vs
-// 0.1043-0.1063 ms/step in 5 alternating pairs, profiles/r03/s2/enc_w3/) or 2 (up to
-// 256 VGPRs, the DCT of Y block row 0 between the colour rows 0..9 and 10..18)
-// NT: nontemporal coefficient stores (knob "encode_nt", default 1 since round 3).
-// With 2 waves and 2 images in flight plain stores were better (part of the
-// coefficients still in the Infinity Cache for the RLE emit: emit 59.7 -> 54.7 us,
-// 8K encode +2-4 %, scripts/gpu_r2i.sh); with 3 waves and 4 images in flight
-// nontemporal stores win (0.0999-0.1033 vs 0.1041-0.1051 ms/step, 3 alternating
-// pairs, profiles/r03/s2/nt/)
-// DM: the DCT variant (knob "encode_dct": 0 float64 AAN, 1 scalar float32 enc_dct_f32, 2 packed float32 enc_dct_pk)
-template <int TMF, bool NT, int DM>
+// One wave per unit, 3 waves per SIMD (<= 168 VGPRs): all 19 colour rows first, so
+// no DCT runs while the row ring and the pyrDown window are live (the other waves of
+// the SIMD hide the loads instead); each packed Y row is pinned where it is made;
+// the DCT passes take the lane index afresh.  Round 3 measured this against the
+// 2-wave budget (colour rows 0..9, Y block row 0, rows 10..18): 8K bench
+// 0.1017-0.1041 vs 0.1043-0.1063 ms/step in 5 alternating pairs
+// (profiles/r03/s2/enc_w3/); the 2-wave kernel, the float32 / packed-float32 DCT
+// variants and cached stores were measured slower and are gone (git history).
+template <int TMF>
 __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_eu(3))) void k_encode420(Enc420 E) {
-  encode420_unit<TMF, NT, DM, true>(E);
-}
-template <int TMF, bool NT, int DM>
-__global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_eu(2))) void k_encode420_w2(Enc420 E) {
-  encode420_unit<TMF, NT, DM>(E);
-}
-
-template <int TMF, bool NT, int DM, bool W3>
-__device__ __forceinline__ void encode420_unit(const Enc420 &E) {
   __shared__ uint2 s_stage[HIC_ENC_WPB * 64 * kStageU2];
   __shared__ uint32_t s_chroma_all[HIC_ENC_WPB][2 * 8 * 64];
-  // the deferred queue of the packed variant (DM == 2): 72 B per item
-  __shared__ uint2 s_qh[DM == 2 ? kEncQCap : 1];
-  __shared__ uint4 s_qp[DM == 2 ? 4 * kEncQCap : 1];
-  __shared__ int s_qn;
-  __shared__ uint32_t s_dirty;
-  __shared__ double s_cm[DM == 2 ? 64 : 1];    // the fallback's cos2 table and QT (per-lane lookups)
-  __shared__ uint8_t s_qt[DM == 2 ? 128 : 1];
-  if (DM == 2) {
-    if (threadIdx.x < 64) s_cm[threadIdx.x] = cos2(kCm, threadIdx.x >> 3, threadIdx.x & 7);
-    if (threadIdx.x < 128) s_qt[threadIdx.x] = (uint8_t)QT[threadIdx.x >> 6][threadIdx.x & 63];
-    if (threadIdx.x == 0) {
-      s_qn = 0;
-      s_dirty = 0;
-    }
-    __syncthreads();
-  }
-  const EncQueue Q{s_qh, s_qp, &s_qn, &s_dirty};
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int b = blockIdx.x;
-  const int g = __builtin_amdgcn_readfirstlane(b * HIC_ENC_WPB + wv);
-  // wave-uniform; the packed variant's waves past the end still join the
-  // workgroup's barriers before the deferred resolve
-  if (DM != 2 && g >= E.nunits) return;
-  const bool live = g < E.nunits;
+  const int g = __builtin_amdgcn_readfirstlane(blockIdx.x * HIC_ENC_WPB + wv);
+  if (g >= E.nunits) return;  // wave-uniform
   uint2 *st2 = s_stage + wv * 64 * kStageU2;
   uint32_t *s_chroma = s_chroma_all[wv];
   int16_t *st = reinterpret_cast<int16_t *>(st2 + lane * kStageU2);
-  // wave g: strip s, unit rows u0 .. u0 + HIC_ENC_VG - 1 (the last wave of a strip
-  // may have one unit row only)
-  const int p = __builtin_amdgcn_readfirstlane(g / E.nstrips), s = __builtin_amdgcn_readfirstlane(g - p * E.nstrips);
-  const int u0 = HIC_ENC_VG * p;
+  // wave g: strip s, unit row u0
+  const int u0 = __builtin_amdgcn_readfirstlane(g / E.nstrips), s = __builtin_amdgcn_readfirstlane(g - u0 * E.nstrips);
   const int y0 = E.out_row0 + 16 * u0;
   // Y blocks of this strip's block rows (64 but in a ragged last strip)
   const int nb = __builtin_amdgcn_readfirstlane(s == E.nstrips - 1 ? E.wlast >> 3 : 64);
-  const bool has2 = HIC_ENC_VG == 2 && 16 * (u0 + 1) < E.out_rows;
   const int nbx = E.W >> 3, nbxc = E.W >> 4;
 
   uint2 yq[16];
-  // Y block row br of unit u: blocks 64 s .. 64 s + 63 of block row 2u + br (one
-  // RLE tile), from yq slots 8 br .. 8 br + 7
-  auto y_blocks = [&](int u, int br) {
+  // Y block row br: blocks 64 s .. 64 s + 63 of block row 2 u0 + br (one RLE tile),
+  // from yq slots 8 br .. 8 br + 7
+  auto y_blocks = [&](int br) {
     uint2 w[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) w[r] = yq[8 * br + r];
-    const int64_t b0 = (int64_t)(2 * u + br) * nbx + 64 * s;
-    enc_dct_any<0, DM>(w, st, Q, lane < nb, 0, br + 2 * (u - u0), wv, (int)b0 + lane);
+    const int64_t b0 = (int64_t)(2 * u0 + br) * nbx + 64 * s;
+    enc_dct<0>(w, st);
     __builtin_amdgcn_wave_barrier();
     int16_t *o = E.coef[0] + b0 * 64;
-    enc_store<NT>(st2, W3 ? fresh_lane() : lane, o, o + 32 * 64, nb < 32 ? nb : 32, nb > 32 ? nb - 32 : 0);
+    enc_store(st2, fresh_lane(), o, o + 32 * 64, nb < 32 ? nb : 32, nb > 32 ? nb - 32 : 0);
     if (TMF >= 0 && E.rec[0]) {
       uint32_t zw[32];
-      enc_stage_row(st2, W3 ? fresh_lane() : lane, zw);
+      enc_stage_row(st2, fresh_lane(), zw);
       tile_record16<TMF>(zw, true, b0 + lane, E.M, E.rec[0] + (b0 >> 6) * 3);
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
-  // chroma of unit u: block m of Cr -> lane m, of Cb -> lane 32 + m (block m spans
-  // the chroma columns of lanes 2m and 2m + 1 of this strip), read from the LDS area
-  auto c_blocks = [&](int u) {
+  // chroma: block m of Cr -> lane m, of Cb -> lane 32 + m (block m spans the chroma
+  // columns of lanes 2m and 2m + 1 of this strip), read from the LDS area
+  auto c_blocks = [&]() {
     __builtin_amdgcn_wave_barrier();
     const uint2 *sc = reinterpret_cast<const uint2 *>(s_chroma + (lane >> 5) * 512) + (lane & 31);
     uint2 w[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = sc[i * 32];
-    const int64_t b0 = (int64_t)u * nbxc + 32 * s;
-    enc_dct_any<1, DM>(w, st, Q, (lane & 31) < (nb >> 1), 1 + (lane >> 5), 2, wv, (int)b0 + (lane & 31));
+    const int64_t b0 = (int64_t)u0 * nbxc + 32 * s;
+    enc_dct<1>(w, st);
     __builtin_amdgcn_wave_barrier();
-    enc_store<NT>(st2, W3 ? fresh_lane() : lane, E.coef[1] + b0 * 64, E.coef[2] + b0 * 64, nb >> 1, nb >> 1);
+    enc_store(st2, fresh_lane(), E.coef[1] + b0 * 64, E.coef[2] + b0 * 64, nb >> 1, nb >> 1);
     if (TMF >= 0 && E.rec[1]) {
       uint32_t zw[32];
-      enc_stage_row(st2, W3 ? fresh_lane() : lane, zw);
+      enc_stage_row(st2, fresh_lane(), zw);
       tile_record16_half<TMF>(zw, b0, E.M, E.rec[1] + (b0 >> 5) * 3, E.rec[2] + (b0 >> 5) * 3);
     }
     __builtin_amdgcn_wave_barrier();
@@ -660,110 +434,22 @@ __device__ __forceinline__ void encode420_unit(const Enc420 &E) {
   };
 #if defined(HIC_DEV) && defined(HIC_ENC_DEV) && (HIC_ENC_DEV & 2)
   // dev timing (results invalid): no colour stage, synthetic pixels
-  for (int k = 0; k < (has2 ? 2 : 1); ++k) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) yq[r] = make_uint2(0x9E3779B1u * (lane + r + g), 0x85EBCA6Bu * (lane ^ r ^ g));
+  for (int r = 0; r < 16; ++r) yq[r] = make_uint2(0x9E3779B1u * (lane + r + g), 0x85EBCA6Bu * (lane ^ r ^ g));
 #pragma unroll
-    for (int i = 0; i < 16; ++i) s_chroma[i * 64 + lane] = 0x01000193u * (lane + i + g);
-    y_blocks(u0 + k, 0);
-    y_blocks(u0 + k, 1);
-    c_blocks(u0 + k);
-  }
+  for (int i = 0; i < 16; ++i) s_chroma[i * 64 + lane] = 0x01000193u * (lane + i + g);
 #else
-  // Each unit's Y block row 0 is transformed between the colour rows that complete
-  // it and the rest, so the loads of the following rows are in flight under its
-  // DCT.  With two units per wave (HIC_ENC_VG = 2) the second unit reuses the
-  // first one's bottom halo rows: 35 converted input rows for 32 image rows,
-  // against 2 x 19.
-  // HIC_ENC_PRIO (dev A/B): wave priority of the colour phases (PC) and of the DCT
-  // phases (PD): the SIMD's arbiter favours the higher one, e.g. the wave that
-  // issues the next rows' loads over one deep in a DCT
-#ifndef HIC_ENC_PRIO_C
-#define HIC_ENC_PRIO_C 0
-#endif
-#ifndef HIC_ENC_PRIO_D
-#define HIC_ENC_PRIO_D 0
-#endif
-  auto prio = [](auto p) {
-    if constexpr (HIC_ENC_PRIO_C != HIC_ENC_PRIO_D) __builtin_amdgcn_s_setprio(decltype(p)::value);
-  };
-  using PC = std::integral_constant<short, HIC_ENC_PRIO_C>;
-  using PD = std::integral_constant<short, HIC_ENC_PRIO_D>;
-  static_assert(DM != 2 || HIC_ENC_VG == 1, "the deferred queue marks one unit's records per wave");
-  if (live) {
 #ifndef HIC_ENC_LA3
-#define HIC_ENC_LA3 3  // the 3-wave variant's load lookahead (rows)
+#define HIC_ENC_LA3 3  // load lookahead (rows)
 #endif
-  EncColour<HIC_ENC_VG == 2 ? 35 : 19, W3 ? HIC_ENC_LA3 : HIC_ENC_LA, W3> C;
-  prio(PC{});
+  EncColour<19, HIC_ENC_LA3, true> C;
   C.init(E, y0, s, lane, nb);
-  if constexpr (W3) {
-    // 3 waves per SIMD (<= 168 VGPRs): all 19 colour rows first, so no DCT runs
-    // while the row ring and the pyrDown window are live (the other waves of the
-    // SIMD hide the loads instead)
-    C.template rows<0, 19>(yq, s_chroma);
-    __builtin_amdgcn_sched_barrier(0);
-    y_blocks(u0, 0);
-  } else {
-  C.template rows<0, 10>(yq, s_chroma);  // input rows 2 .. 9 = unit u0's Y block row 0
+  C.template rows<0, 19>(yq, s_chroma);
   __builtin_amdgcn_sched_barrier(0);
-  prio(PD{});
-  y_blocks(u0, 0);
-  prio(PC{});
-  C.template rows<10, 19>(yq, s_chroma);
-  __builtin_amdgcn_sched_barrier(0);
-  }
-  prio(PD{});
-  y_blocks(u0, 1);
-  c_blocks(u0);  // before the second unit's chroma rows reuse the LDS area
-  if constexpr (HIC_ENC_VG == 2) {
-    if (has2) {
-    C.template rows<19, 26>(yq, s_chroma);  // input rows 18 .. 25 = unit u0 + 1's Y block row 0
-    __builtin_amdgcn_sched_barrier(0);
-    y_blocks(u0 + 1, 0);
-    C.template rows<26, 35>(yq, s_chroma);
-    __builtin_amdgcn_sched_barrier(0);
-    y_blocks(u0 + 1, 1);
-    c_blocks(u0 + 1);
-    }
-  }
-  }
 #endif
-  if constexpr (DM == 2) {
-    // the workgroup's deferred items: every wave's stores and enqueues are done
-    // (a patch must land after the provisional block store it corrects)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    enc_resolve_queue(E, Q, wv, lane, st, s_cm, s_qt);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    // records whose zero pattern a resolved coefficient changed: rebuilt from HBM
-    const uint32_t d = (s_dirty >> (3 * wv)) & 7u;
-    if (TMF >= 0 && live && d) {
-      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-      auto load_nt = [&](const int16_t *blk, uint32_t (&zw)[32]) {
-        const u32x4 *b4 = reinterpret_cast<const u32x4 *>(blk);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const u32x4 t = __builtin_nontemporal_load(b4 + k);
-          zw[4 * k] = t.x; zw[4 * k + 1] = t.y; zw[4 * k + 2] = t.z; zw[4 * k + 3] = t.w;
-        }
-      };
-      for (int br = 0; br < 2; ++br)
-        if ((d >> br) & 1u && E.rec[0]) {
-          const int64_t b0 = (int64_t)(2 * u0 + br) * nbx + 64 * s;
-          uint32_t zw[32];
-          load_nt(E.coef[0] + (b0 + lane) * 64, zw);
-          tile_record16<TMF>(zw, true, b0 + lane, E.M, E.rec[0] + (b0 >> 6) * 3);
-        }
-      if ((d >> 2) & 1u && E.rec[1]) {
-        const int64_t b0 = (int64_t)u0 * nbxc + 32 * s;
-        uint32_t zw[32];
-        load_nt(E.coef[1 + (lane >> 5)] + (b0 + (lane & 31)) * 64, zw);
-        tile_record16_half<TMF>(zw, b0, E.M, E.rec[1] + (b0 >> 5) * 3, E.rec[2] + (b0 >> 5) * 3);
-      }
-    }
-  }
+  y_blocks(0);
+  y_blocks(1);
+  c_blocks();
 }
 
 }  // namespace
@@ -811,7 +497,7 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
   E.M = max_len;
   E.nstrips = (int)((W + 511) / 512);
   E.wlast = (int)(W - 512 * (int64_t)(E.nstrips - 1));
-  E.nunits = E.nstrips * (int)((out_rows / 16 + HIC_ENC_VG - 1) / HIC_ENC_VG);  // waves
+  E.nunits = E.nstrips * (int)(out_rows / 16);  // waves
   // one wave per unit (no persistent loop: units are the same size, and the
   // hardware's dispatch balances the tail better than a fixed split)
   const dim3 grid((unsigned)((E.nunits + HIC_ENC_WPB - 1) / HIC_ENC_WPB)), block(64 * HIC_ENC_WPB);
@@ -823,25 +509,10 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
     else
       hipLaunchKernelGGL(kern, grid, block, 0, s, E);
   };
-  const bool w2 = knob(HIC_KNOB_ENCODE_WAVES) == 2, nt = knob(HIC_KNOB_ENCODE_NT) != 0;
-  const int dm = knob(HIC_KNOB_ENCODE_DCT);
-  // variants: {2, 3} waves per SIMD x {float64, float32, packed float32} DCT x
-  // {cached, nontemporal} stores (nontemporal with float64 only) x {max_len 15, any}
-#define HIC_ENC_VARIANTS(M)                                                 \
-  if (nt && w2 && dm == 0) launch(k_encode420_w2<M, true, 0>);              \
-  else if (nt && dm == 0) launch(k_encode420<M, true, 0>);                  \
-  else if (w2 && dm == 2) launch(k_encode420_w2<M, false, 2>);              \
-  else if (w2 && dm == 1) launch(k_encode420_w2<M, false, 1>);              \
-  else if (w2) launch(k_encode420_w2<M, false, 0>);                         \
-  else if (dm == 2) launch(k_encode420<M, false, 2>);                       \
-  else if (dm == 1) launch(k_encode420<M, false, 1>);                       \
-  else launch(k_encode420<M, false, 0>)
-  if (max_len == 15) {
-    HIC_ENC_VARIANTS(15);
-  } else {
-    HIC_ENC_VARIANTS(0);
-  }
-#undef HIC_ENC_VARIANTS
+  if (max_len == 15)
+    launch(k_encode420<15>);
+  else
+    launch(k_encode420<0>);
   if (int e = check_launch("k_encode420")) return e;
   if (recs && !aligned) {  // one record per 64-block tile, all three planes
     const int64_t ny = (out_rows / 8) * (W / 8), nc = (out_rows / 16) * (W / 16);

@@ -73,9 +73,9 @@ int hic_device_count(int *h_n);
 #define HIC_KNOB_RLD_NT 6           /* 1: nontemporal block stores in the RLE decode */
 #define HIC_KNOB_RLD_GENERIC 7      /* 1: the generic (any block size) RLE decode */
 #define HIC_KNOB_DEV 8              /* dev builds only (-DHIC_DEV): timing bits that skip work; refused otherwise */
-#define HIC_KNOB_ENCODE_WAVES 9     /* hic_encode420_u8: register budget for 3 (default) or 2 waves per SIMD */
-#define HIC_KNOB_ENCODE_NT 10       /* hic_encode420_u8: 1 = nontemporal coefficient stores (default), 0 = cached */
-#define HIC_KNOB_ENCODE_DCT 11      /* hic_encode420_u8: 1 = scalar float32 AAN DCT, 2 = packed float32 AAN DCT (proven windows + in-place fallbacks; default 0: float64) */
+#define HIC_KNOB_ENCODE_WAVES 9     /* retired (round 4): hic_encode420_u8 runs 3 waves per SIMD; only 3 is accepted */
+#define HIC_KNOB_ENCODE_NT 10       /* retired (round 4): nontemporal coefficient stores; only 1 is accepted */
+#define HIC_KNOB_ENCODE_DCT 11      /* retired (round 4): the float64 AAN DCT; only 0 is accepted */
 #define HIC_KNOB_COUNT 12
 int hic_set_knob(int knob, int value);
 int hic_get_knob(int knob, int *h_value);

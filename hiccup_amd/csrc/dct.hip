@@ -25,7 +25,7 @@
 #include <stdlib.h>
 
 #include "dct_core.h"
-#include "dct_mfma_tables.h"
+#include "dct_mfma.h"
 #include "rle_core.h"
 
 namespace hic {
@@ -625,56 +625,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DCT_WPE
 // Output slot layout: lane (n = lane & 15, g = lane >> 4) of M-tile mt holds slots
 // 16 mt + 4 g .. + 3 of block n: one 8-byte LDS store into the stage, which leaves
 // in 1 KiB nontemporal stores (and feeds the RLE tile record) as in k_dct_planes.
-typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
-typedef int16_t s16x2 __attribute__((ext_vector_type(2)));
-
-constexpr int32_t mfma_digit(int32_t a, int d) {
-  for (int k = 0; k < d; ++k) {
-    const int32_t dk = ((a + 128) & 255) - 128;
-    a = (a - dk) / 256;  // exact
-  }
-  return d < 3 ? ((a + 128) & 255) - 128 : a;
-}
-
-// A's digits in MFMA fragment order: w[t][mt][d][lane][c] = dword c of lane
-// `lane`'s A operand for M-tile mt (slots 16 mt ..), digit d.  Byte j of lane
-// (zl = lane & 15, g = lane >> 4) is digit d of A[t][16 mt + zl][16 g + j]: pixel
-// 16 g + j = row 2 g + j / 8, column j % 8 -- the same (g, j) the B operand's
-// pixel rows use.
-struct MfmaFrag {
-  uint32_t w[2][4][4][64][4];
-  constexpr MfmaFrag() : w() {
-    for (int t = 0; t < 2; ++t)
-      for (int mt = 0; mt < 4; ++mt)
-        for (int d = 0; d < 4; ++d)
-          for (int l = 0; l < 64; ++l)
-            for (int c = 0; c < 4; ++c) {
-              uint32_t v = 0;
-              for (int b = 0; b < 4; ++b) {
-                const int32_t a = kMfmaA[t][16 * mt + (l & 15)][16 * (l >> 4) + 4 * c + b];
-                v |= (uint32_t)(uint8_t)(int8_t)mfma_digit(a, d) << (8 * b);
-              }
-              w[t][mt][d][l][c] = v;
-            }
-  }
-};
-__device__ const MfmaFrag kMfmaFragDev{};
-
-__device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
-  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
-}
-
-// pocketfft's half-scaled y'[4][4] from the rows' signed sums k_r (pf_y44 with the
-// integer prefix done): a luminance (4,4) tie is decided by these roundings
-__device__ __forceinline__ double pf_y44_k(const int (&k)[8]) {
-  double y[8];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) y[r] = (double)k[r] * TW3;
-  const double c1 = y[1] + y[2], c3 = y[3] + y[4], c5 = y[5] + y[6], H0 = y[0] + y[7];
-  const double h1 = c1 + c5, T2 = H0 + c3;
-  return (T2 - h1) * TW3;
-}
-
 // stage (this wave's 64 rows) -> ZIGZAG_I16 output (+ the set's RLE tile record)
 template <int TMF>
 __device__ __forceinline__ void mfma_store(const DctJob &J, int set, const uint2 *st2, int lane, int M) {
@@ -728,8 +678,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     while (k + 1 < jobs.n && gi >= jobs.j[k + 1].set0) ++k;
     return __builtin_amdgcn_readfirstlane(k);
   };
-  const i32x4 c0v = {kMfmaC0, kMfmaC0, kMfmaC0, kMfmaC0}, zero = {0, 0, 0, 0};
-  const uint32_t dcmask = g == 0 ? 0x7FFFFu : 0u;
   uint64_t redo = 0;
   int i = 0;
   if (g0 < jobs.total_sets) {
@@ -746,14 +694,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
       }
       if (J.table != table) {  // wave-uniform: this plane's matrix digits
         table = J.table;
-        const uint4 *f = reinterpret_cast<const uint4 *>(&kMfmaFragDev.w[table][0][0][0][0]);
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-          for (int d = 0; d < 4; ++d) {
-            const uint4 v = f[(mt * 4 + d) * 64 + lane];
-            A[mt][d] = i32x4{(int)v.x, (int)v.y, (int)v.z, (int)v.w};
-          }
+        mfma_load_A(table, lane, A);
       }
       const int set = gs - J.set0;
       // pixels: lane (n, g) of N-tile nt holds rows 2g, 2g + 1 of block 16 nt + n
@@ -765,49 +706,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
         const int bi = cblk / J.nbx, bj = cblk - bi * J.nbx;
         const uint8_t *p = J.plane + (int64_t)(bi * 8 + 2 * g) * J.stride + bj * 8;
         const uint2 r0 = *reinterpret_cast<const uint2 *>(p), r1 = *reinterpret_cast<const uint2 *>(p + J.stride);
-        B[nt] = i32x4{(int)(r0.x ^ 0x80808080u), (int)(r0.y ^ 0x80808080u), (int)(r1.x ^ 0x80808080u),
-                      (int)(r1.y ^ 0x80808080u)};
+        B[nt] = mfma_pixels(r0, r1);
       }
-      const uint32_t z44mask = (g == 1 && table == 0) ? 0x7FFFFu : 0u;
-      uint32_t fmin = 0xFFFFFFFFu;
       uint64_t m44 = 0;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        uint2 *row = st2 + (16 * nt + n) * kStageU2 + g;
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          const i32x4 D0 = mfma_i8(A[mt][0], B[nt], c0v);
-          const i32x4 D3 = mfma_i8(A[mt][3], B[nt], zero);
-          const i32x4 D1 = mfma_i8(A[mt][1], B[nt], D0 >> 8);
-          const i32x4 D2 = mfma_i8(A[mt][2], B[nt], (D3 << 8) + 32768);
-          const i32x4 R = (D2 << 3) + (D1 >> 5);
-          uint32_t f0 = (uint32_t)R.x & 0x7FFFFu, f3 = (uint32_t)R.w & 0x7FFFFu;
-          if (mt == 0) f0 |= dcmask;
-          if (mt == 2) {
-            if (table == 0) {
-              const uint64_t b = __builtin_amdgcn_ballot_w64(g == 1 && f3 < kMfmaL);
-              m44 |= ((b >> 16) & 0xFFFFull) << (16 * nt);
-            }
-            f3 |= z44mask;
-          }
-          fmin = min(min(fmin, f0), (uint32_t)R.y & 0x7FFFFu);  // v_min3_u32
-          fmin = min(min(fmin, (uint32_t)R.z & 0x7FFFFu), f3);
-          // q = R >> 19 as int16 pairs: the high halves, then >> 3 per half
-          s16x2 q01 = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm((uint32_t)R.y, (uint32_t)R.x, 0x07060302u));
-          s16x2 q23 = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm((uint32_t)R.w, (uint32_t)R.z, 0x07060302u));
-          q01 = q01 >> (s16x2){3, 3};
-          q23 = q23 >> (s16x2){3, 3};
-          uint32_t w01 = __builtin_bit_cast(uint32_t, q01);
-          if (mt == 0) {
-            // DC: the exact pixel sum X = (R - 2^18) >> 17, rounded as numpy does
-            const int X = (R.x - (1 << 18)) >> 17;
-            const int qdc = table == 0 ? dc_quant<0>(X) : dc_quant<1>(X);
-            if (g == 0) w01 = (w01 & 0xFFFF0000u) | ((uint32_t)qdc & 0xFFFFu);
-          }
-          row[4 * mt] = make_uint2(w01, __builtin_bit_cast(uint32_t, q23));
-        }
-      }
-      if (__builtin_amdgcn_ballot_w64(fmin < kMfmaL) != 0) {
+      const bool flagged = mfma_pass(A, B, st2, lane, table, m44);
+      if (flagged) {
         redo |= 1ull << i;  // the whole set again on the float64 path, after the loop
         continue;
       }

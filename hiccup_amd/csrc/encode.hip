@@ -41,6 +41,7 @@
 // above / below); coefficient writes 3 B per pixel.
 #include "color_core.h"
 #include "dct_core.h"
+#include "dct_mfma.h"
 #include "rle_core.h"
 
 namespace hic {
@@ -375,9 +376,11 @@ struct EncColour {
 // 0.1017-0.1041 vs 0.1043-0.1063 ms/step in 5 alternating pairs
 // (profiles/r03/s2/enc_w3/); the 2-wave kernel, the float32 / packed-float32 DCT
 // variants and cached stores were measured slower and are gone (git history).
-template <int TMF>
+// MFMA: the integer-MFMA transform (dct_mfma.h) for the three passes instead of the
+// float64 AAN (knob "encode_dct" 1; bit-exact either way).
+template <int TMF, bool MFMA>
 __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_eu(3))) void k_encode420(Enc420 E) {
-  __shared__ uint2 s_stage[HIC_ENC_WPB * 64 * kStageU2];
+  __shared__ __attribute__((aligned(16))) uint2 s_stage[HIC_ENC_WPB * 64 * kStageU2];
   __shared__ uint32_t s_chroma_all[HIC_ENC_WPB][2 * 8 * 64];
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = __builtin_amdgcn_readfirstlane(blockIdx.x * HIC_ENC_WPB + wv);
@@ -393,14 +396,16 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
   const int nbx = E.W >> 3, nbxc = E.W >> 4;
 
   uint2 yq[16];
+  i32x4 A[4][4];  // MFMA matrix digits of the pass's table (loaded after the colour rows)
   // Y block row br: blocks 64 s .. 64 s + 63 of block row 2 u0 + br (one RLE tile),
-  // from yq slots 8 br .. 8 br + 7
-  auto y_blocks = [&](int br) {
-    uint2 w[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) w[r] = yq[8 * br + r];
+  // from yq slots 8 br .. 8 br + 7.  MFMA: the lane's block rows go through the stage
+  // area (64 B per block at an 80 B stride: conflict-free 16 B stores) to the
+  // fragment layout (lane n, g: rows 2g, 2g + 1 of block 16 nt + n); the transform
+  // then overwrites the stage with the coefficients.  A flagged pass (~3 % on random
+  // data) is redone on the float64 AAN path from the rows still in registers; the
+  // luminance (4,4) ties are decided in place (pf_y44 on the lane's own block).
+  auto y_out = [&](int br) {  // stage -> HBM + the tile record
     const int64_t b0 = (int64_t)(2 * u0 + br) * nbx + 64 * s;
-    enc_dct<0>(w, st);
     __builtin_amdgcn_wave_barrier();
     int16_t *o = E.coef[0] + b0 * 64;
     enc_store(st2, fresh_lane(), o, o + 32 * 64, nb < 32 ? nb : 32, nb > 32 ? nb - 32 : 0);
@@ -412,16 +417,41 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
-  // chroma: block m of Cr -> lane m, of Cb -> lane 32 + m (block m spans the chroma
-  // columns of lanes 2m and 2m + 1 of this strip), read from the LDS area
-  auto c_blocks = [&]() {
-    __builtin_amdgcn_wave_barrier();
-    const uint2 *sc = reinterpret_cast<const uint2 *>(s_chroma + (lane >> 5) * 512) + (lane & 31);
+  // returns true (MFMA, wave-uniform) if the pass is flagged: nothing stored, the
+  // caller redoes it on the float64 AAN path after the other passes (the rows stay
+  // in registers; the matrix digits are dead by then)
+  auto y_blocks = [&](int br) -> bool {
     uint2 w[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) w[i] = sc[i * 32];
+    for (int r = 0; r < 8; ++r) w[r] = yq[8 * br + r];
+    if (MFMA) {
+      uint4 *pix = reinterpret_cast<uint4 *>(st2);
+      const int l = fresh_lane();
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pix[l * 5 + k] = make_uint4(w[2 * k].x, w[2 * k].y, w[2 * k + 1].x, w[2 * k + 1].y);
+      __builtin_amdgcn_wave_barrier();
+      i32x4 B[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const uint4 v = pix[(16 * nt + (l & 15)) * 5 + (l >> 4)];
+        B[nt] = mfma_pixels(make_uint2(v.x, v.y), make_uint2(v.z, v.w));
+      }
+      __builtin_amdgcn_wave_barrier();
+      uint64_t m44 = 0;
+      if (mfma_pass(A, B, st2, l, 0, m44)) return true;
+      if (m44 != 0 && ((m44 >> l) & 1)) st[kMfmaZ44] = (int16_t)quant_fast<0>(pf_y44(w), 36);
+    } else {
+      enc_dct<0>(w, st);
+    }
+    y_out(br);
+    return false;
+  };
+  // chroma: block m of Cr -> stage row m, of Cb -> row 32 + m (block m spans the
+  // chroma columns of lanes 2m and 2m + 1 of this strip; its row i is the 8 bytes
+  // at uint2 i * 32 + m of the plane's LDS area); the AAN path takes them one block
+  // per lane (Cr block m in lane m, Cb in lane 32 + m)
+  auto c_out = [&]() {
     const int64_t b0 = (int64_t)u0 * nbxc + 32 * s;
-    enc_dct<1>(w, st);
     __builtin_amdgcn_wave_barrier();
     enc_store(st2, fresh_lane(), E.coef[1] + b0 * 64, E.coef[2] + b0 * 64, nb >> 1, nb >> 1);
     if (TMF >= 0 && E.rec[1]) {
@@ -431,6 +461,33 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_sched_barrier(0);
+  };
+  auto c_aan = [&]() {
+    __builtin_amdgcn_wave_barrier();
+    const uint2 *sc = reinterpret_cast<const uint2 *>(s_chroma + (lane >> 5) * 512) + (lane & 31);
+    uint2 w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = sc[i * 32];
+    enc_dct<1>(w, st);
+    c_out();
+  };
+  auto c_blocks = [&]() -> bool {
+    if (!MFMA) {
+      c_aan();
+      return false;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int l = fresh_lane();
+    i32x4 B[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const uint2 *sc = reinterpret_cast<const uint2 *>(s_chroma + (nt >> 1) * 512) + 16 * (nt & 1) + (l & 15);
+      B[nt] = mfma_pixels(sc[(2 * (l >> 4)) * 32], sc[(2 * (l >> 4) + 1) * 32]);
+    }
+    uint64_t m44 = 0;  // (chrominance (4,4) never ties)
+    if (mfma_pass(A, B, st2, l, 1, m44)) return true;
+    c_out();
+    return false;
   };
 #if defined(HIC_DEV) && defined(HIC_ENC_DEV) && (HIC_ENC_DEV & 2)
   // dev timing (results invalid): no colour stage, synthetic pixels
@@ -447,9 +504,24 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
   C.template rows<0, 19>(yq, s_chroma);
   __builtin_amdgcn_sched_barrier(0);
 #endif
-  y_blocks(0);
-  y_blocks(1);
-  c_blocks();
+  if (MFMA) mfma_load_A(0, lane, A);
+  const bool redo0 = y_blocks(0);
+  const bool redo1 = y_blocks(1);
+  if (MFMA) mfma_load_A(1, lane, A);
+  const bool redoc = c_blocks();
+  if (MFMA) {  // flagged passes, on the float64 AAN path (~3 % of passes on random data)
+    if (redo0 || redo1) {
+      uint2 w[8];
+      for (int br = 0; br < 2; ++br) {
+        if (!(br == 0 ? redo0 : redo1)) continue;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) w[r] = yq[8 * br + r];
+        enc_dct<0>(w, st);
+        y_out(br);
+      }
+    }
+    if (redoc) c_aan();
+  }
 }
 
 }  // namespace
@@ -509,10 +581,11 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
     else
       hipLaunchKernelGGL(kern, grid, block, 0, s, E);
   };
+  const bool mfma = knob(HIC_KNOB_ENCODE_DCT) == 1;
   if (max_len == 15)
-    launch(k_encode420<15>);
+    mfma ? launch(k_encode420<15, true>) : launch(k_encode420<15, false>);
   else
-    launch(k_encode420<0>);
+    mfma ? launch(k_encode420<0, true>) : launch(k_encode420<0, false>);
   if (int e = check_launch("k_encode420")) return e;
   if (recs && !aligned) {  // one record per 64-block tile, all three planes
     const int64_t ny = (out_rows / 8) * (W / 8), nc = (out_rows / 16) * (W / 16);

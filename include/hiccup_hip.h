@@ -75,7 +75,7 @@ int hic_device_count(int *h_n);
 #define HIC_KNOB_DEV 8              /* dev builds only (-DHIC_DEV): timing bits that skip work; refused otherwise */
 #define HIC_KNOB_ENCODE_WAVES 9     /* retired (round 4): hic_encode420_u8 runs 3 waves per SIMD; only 3 is accepted */
 #define HIC_KNOB_ENCODE_NT 10       /* retired (round 4): nontemporal coefficient stores; only 1 is accepted */
-#define HIC_KNOB_ENCODE_DCT 11      /* retired (round 4): the float64 AAN DCT; only 0 is accepted */
+#define HIC_KNOB_ENCODE_DCT 11      /* hic_encode420_u8 transform: 0 float64 AAN, 1 integer MFMA (dct_mfma.h) */
 #define HIC_KNOB_COUNT 12
 int hic_set_knob(int knob, int value);
 int hic_get_knob(int knob, int *h_value);

@@ -377,12 +377,12 @@ def _structured_rgb(kind, H, W, seed):
     raise ValueError(kind)
 
 
-# the chain's plane DCT on both shipped paths: the integer-MFMA kernel and the
-# float64 AAN one (the fused kernel runs the float64 AAN)
-@pytest.mark.parametrize("chain_path", [_lib.DCT_PATH_MFMA, _lib.DCT_PATH_F64])
+# both transforms of the fused kernel (knob encode_dct: 0 float64 AAN, 1 integer
+# MFMA) against the chain's plane DCT on both of its paths (integer MFMA, float64 AAN)
+@pytest.mark.parametrize("enc_dct,chain_path", [(0, _lib.DCT_PATH_MFMA), (1, _lib.DCT_PATH_F64), (1, _lib.DCT_PATH_MFMA)])
 @pytest.mark.parametrize("kind", ["random", "levels", "colour_levels", "blocks", "flat"])
 @pytest.mark.parametrize("H,W", [(16, 512), (144, 2048), (1088, 1536)])
-def test_fused_encoder_matches_two_kernel_chain(kind, H, W, chain_path):
+def test_fused_encoder_matches_two_kernel_chain(kind, H, W, enc_dct, chain_path):
     """hic_encode420_u8 (colour + pyrDown + DCT + tile records in one kernel, exact
     tie fallbacks in place) == the two-kernel chain (hic_rgb_to_ycrcb420 +
     hic_dct_quant_rle_u8_batch), symbols and DC streams included (the fused chroma
@@ -390,7 +390,8 @@ def test_fused_encoder_matches_two_kernel_chain(kind, H, W, chain_path):
     rgb = _structured_rgb(kind, H, W, H + W)
     x = device.to_device(rgb)
     got, exp = pipeline.Encoder(H, W, fused=True), pipeline.Encoder(H, W, fused=False)
-    got.encode(x)
+    with _lib.knobs(encode_dct=enc_dct):
+        got.encode(x)
     with _lib.knobs(dct_path=chain_path):
         exp.encode(x)
     a, b = got.result(), exp.result()
@@ -401,14 +402,15 @@ def test_fused_encoder_matches_two_kernel_chain(kind, H, W, chain_path):
     np.testing.assert_array_equal(got.shard_summaries().cpu().numpy(), exp.shard_summaries().cpu().numpy())
 
 
+@pytest.mark.parametrize("enc_dct", [0, 1])
 @pytest.mark.parametrize("kind", ["random", "levels", "blocks", "flat"])
 @pytest.mark.parametrize("H,W", [(2160, 3840), (1088, 1920), (32, 528), (48, 16), (16, 1040)])
-def test_fused_encoder_ragged_matches_chain(kind, H, W):
+def test_fused_encoder_ragged_matches_chain(kind, H, W, enc_dct):
     """Widths that are not a multiple of 512: the fused kernel's last strip is
     ragged (lanes past W store nothing, the right-border pixel goes to the strip's
     last lane) and its tile records come from a tile pass -- symbols, DC and shard
     summaries equal the two-kernel chain's."""
-    test_fused_encoder_matches_two_kernel_chain(kind, H, W, _lib.DCT_PATH_MFMA)
+    test_fused_encoder_matches_two_kernel_chain(kind, H, W, enc_dct, _lib.DCT_PATH_MFMA)
 
 
 @pytest.mark.timeout(900)

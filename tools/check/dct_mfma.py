@@ -16,14 +16,12 @@ the matrix cores (v_mfma_i32_16x16x64_i8):
     8 i + j) is an integer below 2^31 in magnitude, split into four balanced
     base-256 digits a_0..a_3 in [-128, 127] (A = sum 2^(8d) a_d);
   * S_d = sum_k a_d,k x_k is computed EXACTLY (int8 x int8 -> int32 MFMA, |S_d| <= 2^20);
-  * the digits are combined with two truncating shifts fed back through the MFMA's
-    accumulator input:
-        D0 = S_0 + c0            t0 = D0 >> 8
-        D1 = S_1 + t0            t1 = D1 >> 5
-        D2 = S_2 + (S_3 << 8) + 2^15
-        R  = (D2 << 3) + t1
+  * the four digit products are independent MFMAs (c0 and 2^15 ride in the
+    accumulator inputs of digits 0 and 2) combined with ONE truncating shift:
+        R = ((S_0 + c0 + (S_1 << 8)) >> 13) + ((S_2 + 2^15) << 3) + (S_3 << 11)
     so R = (S + c0) / 2^13 + 2^18 - eps with eps in [0, 1): R / 2^19 estimates
-    y/T + 1/2 in units of 2^-19 (S = sum_d 2^(8d) S_d = sum_k A_k x_k).
+    y/T + 1/2 in units of 2^-19 (S = sum_d 2^(8d) S_d = sum_k A_k x_k; the 2^16 S_2
+    and 2^24 S_3 terms are multiples of 2^13, so the floor only cuts S_0 + 2^8 S_1).
   * q = R >> 19 (floor), flagged when R mod 2^19 < L.
 Proof (windows() below): |S / 2^32 - y/T| <= EA (A's rounding, summed exactly
 over the 64 columns with |x| <= 128), |y/T - fl(y_pf/T)| <= EQ (pocketfft's
@@ -59,8 +57,7 @@ ZZ = [0, 8, 1, 2, 9, 16, 24, 17, 10, 3, 4, 11, 18, 25, 32, 40, 33, 26, 19, 12, 5
 Z44 = ZZ.index(36)
 SCALE = 32          # A = round(2^32 C / T)
 RBITS = 19          # R = 2^19 (y/T + 1/2) - eps
-SH0, SH1, SH3 = 8, 5, 8   # t0 = D0 >> 8, t1 = D1 >> 5, D2 = S2 + (S3 << 8) + HALF2
-HALF2 = 1 << 15     # 1/2 in D2's units (2^-16)
+HALF2 = 1 << 15     # 1/2 in S2's units (2^-16 of y/T)
 DC_A = 1 << 30      # the DC row: 4 / 16 * 2^32 -> the exact pixel sum at 2^30
 
 
@@ -173,12 +170,10 @@ def emulate(x, t, c0):
     L4 = np.array([[limbs(A[z][k]) for k in range(64)] for z in range(64)], dtype=np.int64)  # [z][k][d]
     x = x.astype(np.int64)
     S = [x @ L4[:, :, d].T for d in range(4)]  # [n, z]
-    D0 = S[0] + c0
-    t0 = D0 >> SH0
-    D1 = S[1] + t0
-    t1 = D1 >> SH1
-    D2 = S[2] + (S[3] << SH3) + HALF2
-    R = (D2 << 3) + t1
+    # every intermediate stays inside int32 (the kernel's arithmetic wraps nowhere)
+    lo = (S[1] << 8) + S[0] + c0
+    assert np.abs(lo).max() < 2 ** 31
+    R = (lo >> 13) + ((S[2] + HALF2) << 3) + (S[3] << 11)
     assert np.abs(R).max() < 2 ** 31
     q = R >> RBITS
     fr = R & ((1 << RBITS) - 1)

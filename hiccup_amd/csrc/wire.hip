@@ -7,8 +7,10 @@
 // are packed back to back; a 64-block tile is 2 * bits-per-block 32-bit words
 // (whole words for any width), stored at a stride rounded up to 16 bytes.  Bit i
 // of a tile is bit (i & 31) of its word i >> 5 (LSB first).  The pack kernel
-// checks every value against its width and raises *d_flag on a violation (the
-// caller then sends the raw blocks).
+// checks every value against its width and raises *d_flag on a violation; the
+// stream gather points d_flag at a trailer word of the sender's segment, so the
+// flag travels with the data and the receiver turns it into the stream's count
+// (HIC_COUNT_WIRE_OVERFLOW, sharding.ShardEncoder.finish).
 //
 //  hic_wire_pack_i16:   nblk blocks (64 int16, ZIGZAG_I16) -> ceil(nblk / 64) tiles
 //  hic_wire_unpack_i16: the inverse (blocks past nblk in the last tile dropped)

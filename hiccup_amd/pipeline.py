@@ -46,6 +46,7 @@ def input_span(H, r0, r1):
 # -(symbols needed) when the buffer is too small, HIC_COUNT_SCAN_TIMEOUT when a
 # cross-workgroup scan hand-off timed out (never expected; the stream is invalid)
 COUNT_SCAN_TIMEOUT = -(2 ** 63)
+COUNT_WIRE_OVERFLOW = -(2 ** 63) + 1  # a gathered segment's sender flagged an out-of-width value
 
 
 def check_count(c, channel=""):
@@ -54,6 +55,9 @@ def check_count(c, channel=""):
         return
     if c == COUNT_SCAN_TIMEOUT:
         raise _lib.HipError("RLE scan hand-off timed out (channel %s): the stream is invalid" % channel)
+    if c == COUNT_WIRE_OVERFLOW:
+        raise _lib.HipError("a gathered shard flagged a coefficient outside its wire width (channel %s): the "
+                            "stream is invalid" % channel)
     raise MemoryError("symbol buffer too small for channel %s: %d symbols needed" % (channel, -c))
 
 

@@ -101,6 +101,7 @@ def block_ranges(H, W, world):
 
 
 REC_BYTES = 24  # one RLE tile record: 3 int64
+TRAILER_BYTES = 16  # a stream-gather segment's trailer: the sender's int32 out-of-width flag, padded
 TABLE_OF = {"lum": 0, "cr": 1, "cb": 1}  # the plane's quantisation table (the wire widths follow it)
 
 
@@ -108,7 +109,8 @@ def wire_ranges(ranges, rpt, records):
     """{channel: [(o0, o1)]}: rank r's byte segment of the whole image's wire buffer
     -- its blocks in the wire format (hic_wire_bytes) followed, when `records`, by
     its RLE tile records already rebased to whole-image positions (REC_BYTES each,
-    rpt records per 64 blocks, padded to a multiple of 16 bytes)."""
+    rpt records per 64 blocks, padded to a multiple of 16 bytes), then a
+    TRAILER_BYTES trailer whose first int32 is the sender's out-of-width flag."""
     lib = _lib.load()
     out = {}
     for k in CHANNELS:
@@ -117,7 +119,7 @@ def wire_ranges(ranges, rpt, records):
             n = b1 - b0
             # (the records padded to 16 bytes: every segment starts 16-byte aligned)
             size = lib.hic_wire_bytes(n, TABLE_OF[k]) + (-(-(-(-n * rpt[k] // 64) * REC_BYTES) // 16) * 16
-                                                            if records else 0)
+                                                            if records else 0) + TRAILER_BYTES
             rr.append((o, o + size))
             o += size
         out[k] = rr
@@ -193,7 +195,6 @@ class ShardEncoder:
         if gather_kind == "stream":
             self.records = records_aligned(self.ranges, self.enc.rpt)
             self.wranges = wire_ranges(self.ranges, self.enc.rpt, self.records)
-            self.wire_flag = device.zeros((1,), torch.int32)
             if self.rank == gather_to:
                 self.wire_full = {k: device.empty((self.wranges[k][-1][1],), torch.uint8) for k in CHANNELS}
                 self.wire_send = None
@@ -201,6 +202,16 @@ class ShardEncoder:
                 self.wire_full = None
                 self.wire_send = {k: device.empty((self.wranges[k][self.rank][1] - self.wranges[k][self.rank][0],),
                                                   torch.uint8) for k in CHANNELS}
+
+    @property
+    def wire_flag(self):
+        """The out-of-width flag this rank's pack raised (the trailer of its segment;
+        0 on the gathering rank, whose blocks never travel)."""
+        if self.wire_send is None:
+            return device.zeros((1,), torch.int32)
+        return self.wire_send["lum"][-TRAILER_BYTES:].view(torch.int32)[:1] | \
+            self.wire_send["cr"][-TRAILER_BYTES:].view(torch.int32)[:1] | \
+            self.wire_send["cb"][-TRAILER_BYTES:].view(torch.int32)[:1]
 
     @property
     def wire_bytes(self):
@@ -217,8 +228,12 @@ class ShardEncoder:
             n = b1 - b0
             w = self.wire_send[k]
             wb = lib.hic_wire_bytes(n, TABLE_OF[k])
+            # the flag travels in the segment's trailer (cleared on the pack's stream)
+            flag = w[-TRAILER_BYTES:]
+            with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream()):
+                flag.zero_()
             _lib.call("hic_wire_pack_i16", device.ptr(self.enc.coef[k]), n, TABLE_OF[k], device.ptr(w),
-                      device.ptr(self.wire_flag), s)
+                      device.ptr(flag), s)
             if self.records:
                 nrec = -(-n * self.enc.rpt[k] // 64)
                 _lib.call("hic_rle_records_rebase", device.ptr(self.enc.ws[k]), nrec, b0 * 63,
@@ -265,6 +280,26 @@ class ShardEncoder:
                 _lib.call("hic_rle_tile_records_i16", device.ptr(whole.coef[k]), whole.coef[k].shape[0],
                           whole.max_len, device.ptr(whole.ws[k]), s)
         whole.entropy(stream)
+        # the senders' out-of-width flags (segment trailers) -> the stream's count
+        # (HIC_COUNT_WIRE_OVERFLOW): device ops on `stream`, no host sync
+        with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream()):
+            for c, k in enumerate(CHANNELS):
+                idx = self._trailer_index(k)
+                if idx is None:
+                    continue
+                bad = self.wire_full[k].view(torch.int32)[idx].ne(0).any()
+                whole.counts[c:c + 1] = torch.where(bad, torch.full_like(whole.counts[c:c + 1],
+                                                                         pipeline.COUNT_WIRE_OVERFLOW),
+                                                    whole.counts[c:c + 1])
+
+    def _trailer_index(self, k):
+        """int32 indices (device) of the other ranks' trailer flags in wire_full[k]."""
+        if not hasattr(self, "_trailers"):
+            self._trailers = {}
+        if k not in self._trailers:
+            offs = [(self.wranges[k][r][1] - TRAILER_BYTES) // 4 for r in range(self.world) if r != self.rank]
+            self._trailers[k] = torch.tensor(offs, dtype=torch.int64, device="cuda") if offs else None
+        return self._trailers[k]
 
     @property
     def pixels(self):

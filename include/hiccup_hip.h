@@ -36,6 +36,8 @@ extern "C" {
 #define HIC_ERR_HIP (-2)      /* HIP runtime failure (launch, memcpy) */
 #define HIC_ERR_CAPACITY (-3) /* caller's output buffer too small */
 #define HIC_COUNT_SCAN_TIMEOUT INT64_MIN /* *d_count of an RLE encode whose scan hand-off timed out */
+#define HIC_COUNT_WIRE_OVERFLOW (INT64_MIN + 1) /* a gathered stream whose wire segment carried a sender's
+                                                   out-of-width flag (hic_wire_pack_i16): the stream is invalid */
 
 /* model.QTables (model.py:25-27) -> quantization.table (quantization.py:14-37) */
 #define HIC_TABLE_LUMINANCE 0

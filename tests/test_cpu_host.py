@@ -384,7 +384,8 @@ def test_stream_gather_record_layout_past_2gib():
         for (b0, b1), (o0, o1) in zip(ranges[k], wr[k]):
             n = b1 - b0
             nrec = -(-n * lay[0][1][k] // 64)
-            assert o1 - o0 == lib.hic_wire_bytes(n, sharding.TABLE_OF[k]) + -(-nrec * sharding.REC_BYTES // 16) * 16
+            assert o1 - o0 == (lib.hic_wire_bytes(n, sharding.TABLE_OF[k]) + -(-nrec * sharding.REC_BYTES // 16) * 16
+                               + sharding.TRAILER_BYTES)
     # a ragged image whose last shard cannot fuse: one decision for all (the chain)
     rows = sharding.plan(4328, 4)
     assert not all(pipeline.encoder_layout(4328, 7680, rr)[0] for rr in rows)

@@ -79,7 +79,7 @@ def _wire_ranges_host(ranges):
     for k in pipeline.CHANNELS:
         o, rr = 0, []
         for b0, b1 in ranges[k]:
-            rr.append((o, o + wire_host.wire_bytes(b1 - b0, wire_host.TABLE_OF[k])))
+            rr.append((o, o + wire_host.wire_bytes(b1 - b0, wire_host.TABLE_OF[k]) + sharding.TRAILER_BYTES))
             o = rr[-1][1]
         out[k] = rr
     return out
@@ -164,14 +164,14 @@ def _worker(rank, world, port, H, W, flat, results):
             assert wr == _wire_ranges_host(ranges)
 
         def segment(k, blocks, b0):
+            # blocks, [rebased records], trailer (the sender's out-of-width flag: 0)
             w = wire_host.pack(blocks, wire_host.TABLE_OF[k])
-            if not records:
-                return w
-            per = 64 // rpt[k]
-            rec = wire_host.rebase(wire_host.tile_records(blocks, per), b0 * 63)  # shard-local, then rebased
             seg = np.zeros(wr[k][rank][1] - wr[k][rank][0], np.uint8)
             seg[:len(w)] = w
-            seg[len(w):len(w) + rec.nbytes] = rec.reshape(-1).view(np.uint8)
+            if records:
+                per = 64 // rpt[k]
+                rec = wire_host.rebase(wire_host.tile_records(blocks, per), b0 * 63)  # shard-local, then rebased
+                seg[len(w):len(w) + rec.nbytes] = rec.reshape(-1).view(np.uint8)
             return seg
 
         items = []
@@ -197,6 +197,9 @@ def _worker(rank, world, port, H, W, flat, results):
             whole = np.concatenate(parts)
             want = zz[k] + rank if rank else zz[k]
             ok &= np.array_equal(whole, want)
+            # every sender's trailer flag arrived clear
+            ok &= all(int(full_w[k][0][wr[k][r][1] - sharding.TRAILER_BYTES:].view(torch.int32)[0]) == 0
+                      for r in range(world) if r != rank)
             if records:
                 # the placed records (ShardEncoder.finish: record b0 * rpt / 64 of the
                 # whole image's workspace) == the whole image's own tile records

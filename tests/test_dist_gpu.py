@@ -121,6 +121,20 @@ def _rank(rank, world, port, H, W, flat_rows, out_path):
     gok &= all(wholes[j] is None for j in range(world) if j != rank)
     gok &= all(int(e.wire_flag.item()) == 0 for e in sss)
     gok &= sss[rank].records == sharding.records_aligned(sss[rank].ranges, sss[rank].enc.rpt)
+    # a coefficient outside its wire width on a sender (forced here): the flag rides
+    # in the segment's trailer and the receiver marks that channel's stream invalid
+    sss2 = [sharding.ShardEncoder(H, W, rank=rank, world=world, gather_to=j, gather_kind="stream")
+            for j in range(world)]
+    sharding.encode_group(sss2, [device.to_device(img[a:b]) for img in imgs], stream=s)
+    torch.cuda.synchronize()
+    for j in range(world):
+        if j != rank:
+            sss2[j].enc.coef["lum"][0, 5] = 32000  # > any luminance slot width
+    wholes2 = sharding.gather_streams_group(sss2, group=xgroup, stream=s)
+    torch.cuda.synchronize()
+    c2 = wholes2[rank].counts.cpu().tolist()
+    gok &= c2[0] == pipeline.COUNT_WIRE_OVERFLOW and c2[1] >= 0 and c2[2] >= 0
+    gok &= all(int(sss2[j].wire_flag.item()) == 1 for j in range(world) if j != rank)
     goks = [None] * world
     dist.all_gather_object(goks, bool(gok))
     if rank == 0 and not all(goks):

@@ -661,8 +661,10 @@ __device__ __forceinline__ void mfma_store(const DctJob &J, int set, const uint2
   __builtin_amdgcn_wave_barrier();
 }
 
-template <int TMF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_dct_mfma(DctJobs jobs) {
+// WPE: waves per SIMD the register budget allows (3: <= 168 VGPRs, 2: <= 256); PF:
+// the next set's pixels load while this set computes (16 more VGPRs)
+template <int TMF, int WPE, bool PF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_dct_mfma(DctJobs jobs) {
   __shared__ uint2 s_stage[4 * 64 * kStageU2];
   __shared__ int2 s_k44[4 * 64 * 4];  // (4,4) tie path: the 8 signed row sums per block
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -686,6 +688,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     int next0 = kj + 1 < jobs.n ? jobs.j[kj + 1].set0 : jobs.total_sets;
     int table = -1;
     i32x4 A[4][4];
+    uint2 px[8];  // this set's (PF: the next set's) pixel rows
     for (int gs = g0; gs < jobs.total_sets; gs += nwaves, ++i) {
       if (gs >= next0) {
         kj = job_of(gs);
@@ -698,15 +701,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
       }
       const int set = gs - J.set0;
       // pixels: lane (n, g) of N-tile nt holds rows 2g, 2g + 1 of block 16 nt + n
+      auto load_px = [&](const DctJob &Jx, int setx, uint2 (&r)[8]) {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const int blk = setx * 64 + 16 * nt + n;
+          const int cblk = blk < Jx.nblk ? blk : Jx.nblk - 1;
+          const int bi = cblk / Jx.nbx, bj = cblk - bi * Jx.nbx;
+          const uint8_t *p = Jx.plane + (int64_t)(bi * 8 + 2 * g) * Jx.stride + bj * 8;
+          r[2 * nt] = *reinterpret_cast<const uint2 *>(p);
+          r[2 * nt + 1] = *reinterpret_cast<const uint2 *>(p + Jx.stride);
+        }
+      };
+      if (!PF || gs == g0) load_px(J, set, px);
       i32x4 B[4];
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int blk = set * 64 + 16 * nt + n;
-        const int cblk = blk < J.nblk ? blk : J.nblk - 1;
-        const int bi = cblk / J.nbx, bj = cblk - bi * J.nbx;
-        const uint8_t *p = J.plane + (int64_t)(bi * 8 + 2 * g) * J.stride + bj * 8;
-        const uint2 r0 = *reinterpret_cast<const uint2 *>(p), r1 = *reinterpret_cast<const uint2 *>(p + J.stride);
-        B[nt] = mfma_pixels(r0, r1);
+      for (int nt = 0; nt < 4; ++nt) B[nt] = mfma_pixels(px[2 * nt], px[2 * nt + 1]);
+      if (PF && gs + nwaves < jobs.total_sets) {
+        const int gn = gs + nwaves;
+        const int kn = gn >= next0 ? job_of(gn) : kj;
+        load_px(jobs.j[kn], gn - jobs.j[kn].set0, px);
       }
       uint64_t m44 = 0;
       const bool flagged = mfma_pass(A, B, st2, lane, table, m44);
@@ -848,8 +861,8 @@ inline int dct_waves_per_cu(int njobs) {
   // balances the planes' mixed tail: 8K Y + Cr + Cb 37.5 us vs 39.7 for 12
   // persistent waves per CU), 12 persistent waves per CU for one plane (4K luma
   // 13.4 vs 13.8 us, 8K luma 27.4 vs 27.8; scripts/gpu_r2aj.sh); the MFMA path
-  // runs a persistent grid of 3 waves per SIMD
-  return v >= 0 ? v : (dct_path() == 5 ? 12 : (njobs > 1 ? 0 : 12));
+  // runs a persistent grid of its register budget's waves per SIMD
+  return v >= 0 ? v : (dct_path() == 5 ? ((knob(HIC_KNOB_DCT_MFMA) & 2) ? 8 : 12) : (njobs > 1 ? 0 : 12));
 }
 
 inline bool fwd_fast(int H, int W, int64_t stride, const void *plane, const void *out) {
@@ -871,10 +884,17 @@ int launch_planes(DctJobs &jobs, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   const dim3 grid((waves + 3) / 4), block(256);
   const int path = dct_path();
   if (path == 5 && LAYOUT == HIC_LAYOUT_ZIGZAG_I16) {
-    if (e0 || e1)
-      hipExtLaunchKernelGGL((k_dct_mfma<TMF>), grid, block, 0, s, e0, e1, 0, jobs);
-    else
-      hipLaunchKernelGGL((k_dct_mfma<TMF>), grid, block, 0, s, jobs);
+    const int var = knob(HIC_KNOB_DCT_MFMA);
+    auto go = [&](auto kern) {
+      if (e0 || e1)
+        hipExtLaunchKernelGGL(kern, grid, block, 0, s, e0, e1, 0, jobs);
+      else
+        hipLaunchKernelGGL(kern, grid, block, 0, s, jobs);
+    };
+    if (var == 0) go(k_dct_mfma<TMF, 3, false>);
+    else if (var == 1) go(k_dct_mfma<TMF, 3, true>);
+    else if (var == 2) go(k_dct_mfma<TMF, 2, false>);
+    else go(k_dct_mfma<TMF, 2, true>);
     return check_launch("k_dct_mfma");
   }
   if (e0 || e1)

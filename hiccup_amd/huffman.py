@@ -289,6 +289,24 @@ class HuffmanTree:
             self._flat = (np.asarray(child, dtype=np.int32), leaves)
         return self._flat
 
+    def min_code_length(self):
+        """Depth of the shallowest leaf (>= 1): the shortest code of the tree."""
+        if getattr(self, "_minlen", None) is None:
+            child, _ = self.flat()
+            depth, frontier = 1, [0]
+            found = None
+            while frontier and found is None:
+                nxt = []
+                for node in frontier:
+                    for c in child[2 * node:2 * node + 2]:
+                        if c <= -2:
+                            found = depth
+                        elif c >= 0:
+                            nxt.append(int(c))
+                frontier, depth = nxt, depth + 1
+            self._minlen = found or 1
+        return self._minlen
+
     def decode_device(self, bits_dev, nbits, out=None, stream=None):
         """decode_data of a packed MSB-first stream on the device (hic_huffman_decode):
         bits_dev a 4-byte-aligned uint8 tensor, nbits the stream length.  Returns
@@ -302,7 +320,9 @@ class HuffmanTree:
         lib = _lib.load()
         with device.on_stream(stream):
             if out is None:
-                out = device.empty((max(int(nbits), 1),), torch.int32)
+                # every decoded symbol consumes at least the shallowest leaf's depth in
+                # bits: the output needs nbits / that many slots, not one per bit
+                out = device.empty((max(int(nbits) // self.min_code_length(), 1),), torch.int32)
             ws = device.workspace(lib.hic_huffman_decode_workspace_bytes(int(nbits), len(child) // 2, len(leaves)))
             count = ctypes.c_int64(0)
             st = lib.hic_huffman_decode(device.ptr(bits_dev) if nbits else None, int(nbits),

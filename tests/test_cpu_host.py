@@ -339,6 +339,9 @@ def test_huffman_flat_tree_matches_walk(golden_codec):
                     child, leaves = tree.flat()
                     assert child.dtype == np.int32 and child.size % 2 == 0
                     assert _walk_flat(child.tolist(), leaves, bits) == keys.tolist()
+                    # the decode's output sizing: no key takes fewer bits than this
+                    assert tree.min_code_length() == min(len(c) for _, c in table)
+                    assert len(keys) <= max(len(bits) // tree.min_code_length(), 1)
     # a one-leaf encoding tree: its empty '0' side is a missing child
     t = huffman.HuffmanTree.construct_from_data([7, 7, 7])
     child, leaves = t.flat()

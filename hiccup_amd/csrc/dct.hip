@@ -393,6 +393,7 @@ constexpr int kMaxPlaneJobs = 16;  // planes per launch (hic_dct_quant_rle_u8_ba
 struct DctJobs {
   DctJob j[kMaxPlaneJobs];
   int n, total_sets, M;
+  int dev;  // HIC_DEV builds only: timing bits of k_dct_mfma (results invalid)
 };
 
 #ifndef HIC_DCT_WPE
@@ -662,11 +663,14 @@ __device__ __forceinline__ void mfma_store(const DctJob &J, int set, const uint2
 }
 
 // WPE: waves per SIMD the register budget allows (3: <= 168 VGPRs, 2: <= 256); PF:
-// the next set's pixels load while this set computes (16 more VGPRs)
-template <int TMF, int WPE, bool PF>
+// the next set's pixels load while this set computes (16 more VGPRs); DIRECT: the
+// stage-free pass (mfma_pass_direct: coefficients stored from registers, the tile
+// record from the lanes' nonzero masks)
+template <int TMF, int WPE, bool PF, bool DIRECT = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_dct_mfma(DctJobs jobs) {
   __shared__ uint2 s_stage[4 * 64 * kStageU2];
   __shared__ int2 s_k44[4 * 64 * 4];  // (4,4) tie path: the 8 signed row sums per block
+  __shared__ __attribute__((aligned(8))) uint16_t s_nzm[DIRECT ? 4 * 64 * 4 : 1];  // direct: nonzero masks
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nwaves = gridDim.x * 4;
   const int g0 = blockIdx.x * 4 + wv;
@@ -674,6 +678,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   int2 *k44 = s_k44 + wv * 64 * 4;
   const int n = lane & 15, g = lane >> 4;
   const int M = jobs.M;
+#ifdef HIC_DEV
+  // dev timing bits (results invalid): 1 no transform, 2 no stores / records, 4 no
+  // (4,4) tie path, 8 no pixel loads, 16 no records
+  const int dv = jobs.dev;
+#else
+  constexpr int dv = 0;
+#endif
   auto job_of = [&](int gi) {
     gi = __builtin_amdgcn_readfirstlane(gi);
     int k = 0;
@@ -697,7 +708,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       }
       if (J.table != table) {  // wave-uniform: this plane's matrix digits
         table = J.table;
-        mfma_load_A(table, lane, A);
+        mfma_load_A<DIRECT>(table, lane, A);
       }
       const int set = gs - J.set0;
       // pixels: lane (n, g) of N-tile nt holds rows 2g, 2g + 1 of block 16 nt + n
@@ -712,17 +723,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           r[2 * nt + 1] = *reinterpret_cast<const uint2 *>(p + Jx.stride);
         }
       };
-      if (!PF || gs == g0) load_px(J, set, px);
+      if (dv & 8) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) px[r] = make_uint2(0x9E3779B1u * (lane + r + gs), 0x85EBCA6Bu * (lane ^ r));
+      } else if (!PF || gs == g0) {
+        load_px(J, set, px);
+      }
       i32x4 B[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) B[nt] = mfma_pixels(px[2 * nt], px[2 * nt + 1]);
-      if (PF && gs + nwaves < jobs.total_sets) {
+      if (PF && !(dv & 8) && gs + nwaves < jobs.total_sets) {
         const int gn = gs + nwaves;
         const int kn = gn >= next0 ? job_of(gn) : kj;
         load_px(jobs.j[kn], gn - jobs.j[kn].set0, px);
       }
+      if constexpr (DIRECT) {
+        uint16_t *nzm = s_nzm + wv * 64 * 4;
+        const int nvalid = J.nblk - set * 64 < 64 ? J.nblk - set * 64 : 64;
+        if (mfma_pass_direct(A, B, static_cast<int16_t *>(J.out) + (int64_t)set * 64 * 64, lane, table, nvalid,
+                             k44, TMF >= 0 ? nzm : nullptr)) {
+          redo |= 1ull << i;  // the whole set again on the float64 path, after the loop
+          continue;
+        }
+        if (TMF >= 0) {
+          __builtin_amdgcn_wave_barrier();
+          const uint64_t m = *reinterpret_cast<const uint64_t *>(nzm + lane * 4);
+          int first = -1, last = -1, nsym = 0;
+          if (lane < nvalid) summarize_ac<TMF>(m >> 1, M, first, last, nsym);
+          tile_record_fs(first, last, nsym, (int64_t)set * 64 + lane, M, J.tiles + (int64_t)set * 3);
+          __builtin_amdgcn_wave_barrier();
+        }
+        continue;
+      }
       uint64_t m44 = 0;
-      const bool flagged = mfma_pass(A, B, st2, lane, table, m44);
+      const bool flagged = (dv & 1) ? false : mfma_pass(A, B, st2, lane, table, m44);
+      if (dv & 4) m44 = 0;
       if (flagged) {
         redo |= 1ull << i;  // the whole set again on the float64 path, after the loop
         continue;
@@ -750,7 +785,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
         __builtin_amdgcn_wave_barrier();
       }
-      mfma_store<TMF>(J, set, st2, lane, M);
+      if (!(dv & 2)) {
+        if (dv & 16)
+          mfma_store<-1>(J, set, st2, lane, M);
+        else
+          mfma_store<TMF>(J, set, st2, lane, M);
+      }
     }
   }
   // flagged sets: the float64 AAN path (its own exact fallbacks) on this wave's sets
@@ -885,6 +925,7 @@ int launch_planes(DctJobs &jobs, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   const int path = dct_path();
   if (path == 5 && LAYOUT == HIC_LAYOUT_ZIGZAG_I16) {
     const int var = knob(HIC_KNOB_DCT_MFMA);
+    jobs.dev = knob(HIC_KNOB_DEV);
     auto go = [&](auto kern) {
       if (e0 || e1)
         hipExtLaunchKernelGGL(kern, grid, block, 0, s, e0, e1, 0, jobs);
@@ -894,7 +935,11 @@ int launch_planes(DctJobs &jobs, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     if (var == 0) go(k_dct_mfma<TMF, 3, false>);
     else if (var == 1) go(k_dct_mfma<TMF, 3, true>);
     else if (var == 2) go(k_dct_mfma<TMF, 2, false>);
-    else go(k_dct_mfma<TMF, 2, true>);
+    else if (var == 3) go(k_dct_mfma<TMF, 2, true>);
+    else if (var == 4) go(k_dct_mfma<TMF, 3, false, true>);
+    else if (var == 5) go(k_dct_mfma<TMF, 3, true, true>);
+    else if (var == 6) go(k_dct_mfma<TMF, 2, false, true>);
+    else go(k_dct_mfma<TMF, 2, true, true>);
     return check_launch("k_dct_mfma");
   }
   if (e0 || e1)

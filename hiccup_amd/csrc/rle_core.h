@@ -127,12 +127,10 @@ __device__ __forceinline__ uint64_t nz_mask16(const uint32_t (&w)[32]) {
 }
 
 // first / last nonzero AC index (-1 if none) and the symbols of every nonzero
-// after the first (runs inside the block), from the block's nonzero mask.
+// after the first (runs inside the block), from the block's AC nonzero mask
+// (bit j = AC j, j = 0..62).
 template <int MF>
-__device__ __forceinline__ void summarize16(const uint32_t (&w)[32], int M, int &first, int &last, int &nsym,
-                                            uint64_t *ac_out = nullptr) {
-  const uint64_t ac = nz_mask16(w) >> 1;  // bit j = AC j (slot j + 1), j = 0..62
-  if (ac_out) *ac_out = ac;
+__device__ __forceinline__ void summarize_ac(uint64_t ac, int M, int &first, int &last, int &nsym) {
   if (ac == 0) {
     first = last = -1;
     nsym = 0;
@@ -165,6 +163,15 @@ __device__ __forceinline__ void summarize16(const uint32_t (&w)[32], int M, int 
   }
 }
 
+// the same from a zig-zag int16 block held as 32 packed dwords
+template <int MF>
+__device__ __forceinline__ void summarize16(const uint32_t (&w)[32], int M, int &first, int &last, int &nsym,
+                                            uint64_t *ac_out = nullptr) {
+  const uint64_t ac = nz_mask16(w) >> 1;  // bit j = AC j (slot j + 1), j = 0..62
+  if (ac_out) *ac_out = ac;
+  summarize_ac<MF>(ac, M, first, last, nsym);
+}
+
 // ---------------------------------------------------------------------------
 // Hot path geometry: int16 zig-zag blocks of 64 (the DCT kernels' ZIGZAG_I16
 // output), AC = slots 1..63, one block per lane, one TILE = the 64 blocks of one
@@ -186,12 +193,12 @@ __device__ __forceinline__ void load_block16(const int16_t *__restrict__ blocks,
 
 // Wave-level: the tile record of the 64 blocks held by this wave's lanes
 // (valid = this lane's block exists).  Every lane must call it.
-template <int MF>
-__device__ __forceinline__ void tile_record16(const uint32_t (&w)[32], bool valid, int64_t b, int M,
-                                              int64_t *__restrict__ rec) {
+// Wave-level: the tile record from each lane's block summary (first / last nonzero
+// AC, symbols after the first; first = last = -1, nsym = 0 for a missing block).
+// Every lane must call it.
+__device__ __forceinline__ void tile_record_fs(int first, int last, int nsym, int64_t b, int M,
+                                               int64_t *__restrict__ rec) {
   const int lane = threadIdx.x & 63;
-  int first = -1, last = -1, nsym = 0;
-  if (valid) summarize16<MF>(w, M, first, last, nsym);
   // positions relative to the tile's first AC element (lane * 63 + j) fit int32
   const int lastr = last >= 0 ? lane * 63 + last : -1;
   const int incl = wave_incl_max_i32(lastr);
@@ -207,6 +214,16 @@ __device__ __forceinline__ void tile_record16(const uint32_t (&w)[32], bool vali
     rec[1] = all_last >= 0 ? base + all_last : -1;
     rec[2] = total;
   }
+}
+
+// Wave-level: the tile record of the 64 blocks held by this wave's lanes
+// (valid = this lane's block exists).  Every lane must call it.
+template <int MF>
+__device__ __forceinline__ void tile_record16(const uint32_t (&w)[32], bool valid, int64_t b, int M,
+                                              int64_t *__restrict__ rec) {
+  int first = -1, last = -1, nsym = 0;
+  if (valid) summarize16<MF>(w, M, first, last, nsym);
+  tile_record_fs(first, last, nsym, b, M, rec);
 }
 
 // Copy n elements from LDS (element e at s[a + e]) to global g[o0 + e], where

@@ -158,8 +158,14 @@ __device__ __forceinline__ bool mfma_pass(const i32x4 (&A)[4][4], const i32x4 (&
 // nzm[block][g] for the set's tile record.  Returns true (wave-uniform) if any
 // other coefficient is flagged: the caller redoes the set (which stores again).
 // blk_ok: this lane's block exists (its stores are skipped otherwise).
+// BUF: the stores go through the buffer resource `orsrc` (the plane's output, its
+// size as the record count) at scalar offset `soff` (the set's first byte): always
+// issued -- out-of-range lanes are dropped by the hardware -- so a set issues a
+// fixed number of vector-memory instructions (the DMA kernel's vmcnt bookkeeping)
+template <bool BUF = false>
 __device__ __forceinline__ bool mfma_pass_direct(const i32x4 (&A)[4][4], const i32x4 (&B)[4], int16_t *out_set,
-                                                 int lane, int table, int nvalid, int2 *k44, uint16_t *nzm) {
+                                                 int lane, int table, int nvalid, int2 *k44, uint16_t *nzm,
+                                                 __amdgpu_buffer_rsrc_t orsrc, uint32_t soff) {
   const int n = lane & 15, g = lane >> 4;
   const i32x4 c0v = {kMfmaC0, kMfmaC0, kMfmaC0, kMfmaC0}, zero = {0, 0, 0, 0};
   const i32x4 halfv = {1 << 15, 1 << 15, 1 << 15, 1 << 15};
@@ -223,7 +229,12 @@ __device__ __forceinline__ bool mfma_pass_direct(const i32x4 (&A)[4][4], const i
       __builtin_amdgcn_wave_barrier();
     }
     // this lane's 16 slots: 32 contiguous bytes of block 16 nt + n
-    if (16 * nt + n < nvalid) {
+    if (BUF) {
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      const uint32_t vo = (uint32_t)(((16 * nt + n) * 64 + 16 * g) * 2);
+      __builtin_amdgcn_raw_buffer_store_b128((u32x4){wq[0], wq[1], wq[2], wq[3]}, orsrc, vo, soff, 2);
+      __builtin_amdgcn_raw_buffer_store_b128((u32x4){wq[4], wq[5], wq[6], wq[7]}, orsrc, vo + 16, soff, 2);
+    } else if (16 * nt + n < nvalid) {
       uint4 *o = reinterpret_cast<uint4 *>(out_set + (16 * nt + n) * 64 + 16 * g);
       typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
       __builtin_nontemporal_store((u32x4){wq[0], wq[1], wq[2], wq[3]}, reinterpret_cast<u32x4 *>(o));

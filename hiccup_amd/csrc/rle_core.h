@@ -193,6 +193,27 @@ __device__ __forceinline__ void load_block16(const int16_t *__restrict__ blocks,
 
 // Wave-level: the tile record of the 64 blocks held by this wave's lanes
 // (valid = this lane's block exists).  Every lane must call it.
+// Wave-level: the tile record's three values (wave-uniform) from each lane's block
+// summary.  Every lane must call it.
+__device__ __forceinline__ void tile_record_values(int first, int last, int nsym, int64_t b, int M, int64_t &r0,
+                                                   int64_t &r1, int64_t &r2) {
+  const int lane = threadIdx.x & 63;
+  const int lastr = last >= 0 ? lane * 63 + last : -1;
+  const int incl = wave_incl_max_i32(lastr);
+  const int prev = wave_shr1_i32(-1, incl);
+  int cnt = nsym;
+  if (first >= 0 && prev >= 0) cnt += syms_for_run(lane * 63 + first - prev - 1, M);
+  const int total = wave_last_i32(wave_incl_sum_i32(cnt));
+  const int all_last = wave_last_i32(incl);
+  const int64_t base = (b - lane) * 63;
+  const uint64_t fm = __builtin_amdgcn_ballot_w64(first >= 0 && prev < 0);
+  const int fl = fm ? __builtin_ctzll(fm) : 0;
+  const int ff = __builtin_amdgcn_readlane(lane * 63 + first, fl);
+  r0 = all_last < 0 ? -1 : base + ff;
+  r1 = all_last >= 0 ? base + all_last : -1;
+  r2 = total;
+}
+
 // Wave-level: the tile record from each lane's block summary (first / last nonzero
 // AC, symbols after the first; first = last = -1, nsym = 0 for a missing block).
 // Every lane must call it.

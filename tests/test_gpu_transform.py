@@ -306,7 +306,7 @@ def test_measurement_probes():
         _lib.call("hic_probe_copy", device.ptr(a), device.ptr(b), 17, 0, device.stream_ptr(), None, None)
 
 
-@pytest.mark.parametrize("var", range(8))
+@pytest.mark.parametrize("var", range(10))
 @pytest.mark.parametrize("kind", ["random", "levels4", "nearflat", "checker"])
 def test_mfma_plane_variants(kind, var):
     """Every k_dct_mfma variant (knob dct_mfma: bit 0 prefetch, bit 1 two waves per

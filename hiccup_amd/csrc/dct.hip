@@ -668,7 +668,7 @@ __device__ __forceinline__ void mfma_store(const DctJob &J, int set, const uint2
 // record from the lanes' nonzero masks)
 template <int TMF, int WPE, bool PF, bool DIRECT = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_dct_mfma(DctJobs jobs) {
-  __shared__ uint2 s_stage[4 * 64 * kStageU2];
+  __shared__ __attribute__((aligned(16))) uint2 s_stage[4 * 64 * kStageU2];
   __shared__ int2 s_k44[4 * 64 * 4];  // (4,4) tie path: the 8 signed row sums per block
   __shared__ __attribute__((aligned(8))) uint16_t s_nzm[DIRECT ? 4 * 64 * 4 : 1];  // direct: nonzero masks
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -712,16 +712,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       }
       const int set = gs - J.set0;
       // pixels: lane (n, g) of N-tile nt holds rows 2g, 2g + 1 of block 16 nt + n
+      // pixels: lane L loads the 8 rows of block L of the set (each load instruction
+      // one contiguous 512 B image-row segment, the pattern of the memory-floor
+      // probe); the rows then go through the stage (80 B per block: conflict-free
+      // 16 B stores) to the fragment layout: lane (n, g) of N-tile nt holds rows
+      // 2g, 2g + 1 of block 16 nt + n (bytes 16 g .. 16 g + 15 of the block's 64).
+      // Measured: loading the fragments straight from HBM (4 image rows per
+      // instruction) waited twice as long on memory (SQ_WAIT_ANY 20.8 M vs 10.6 M).
       auto load_px = [&](const DctJob &Jx, int setx, uint2 (&r)[8]) {
+        const int blk = setx * 64 + lane;
+        const int cblk = blk < Jx.nblk ? blk : Jx.nblk - 1;
+        const int bi = cblk / Jx.nbx, bj = cblk - bi * Jx.nbx;
+        const uint8_t *p = Jx.plane + (int64_t)bi * 8 * Jx.stride + bj * 8;
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-          const int blk = setx * 64 + 16 * nt + n;
-          const int cblk = blk < Jx.nblk ? blk : Jx.nblk - 1;
-          const int bi = cblk / Jx.nbx, bj = cblk - bi * Jx.nbx;
-          const uint8_t *p = Jx.plane + (int64_t)(bi * 8 + 2 * g) * Jx.stride + bj * 8;
-          r[2 * nt] = *reinterpret_cast<const uint2 *>(p);
-          r[2 * nt + 1] = *reinterpret_cast<const uint2 *>(p + Jx.stride);
-        }
+        for (int rr = 0; rr < 8; ++rr) r[rr] = *reinterpret_cast<const uint2 *>(p + rr * Jx.stride);
       };
       if (dv & 8) {
 #pragma unroll
@@ -730,8 +734,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         load_px(J, set, px);
       }
       i32x4 B[4];
+      {
+        uint4 *pix = reinterpret_cast<uint4 *>(st2);
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) B[nt] = mfma_pixels(px[2 * nt], px[2 * nt + 1]);
+        for (int k = 0; k < 4; ++k)
+          pix[lane * 5 + k] = make_uint4(px[2 * k].x, px[2 * k].y, px[2 * k + 1].x, px[2 * k + 1].y);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const uint4 v = pix[(16 * nt + n) * 5 + g];
+          B[nt] = mfma_pixels(make_uint2(v.x, v.y), make_uint2(v.z, v.w));
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
       if (PF && !(dv & 8) && gs + nwaves < jobs.total_sets) {
         const int gn = gs + nwaves;
         const int kn = gn >= next0 ? job_of(gn) : kj;

@@ -12,7 +12,7 @@ from hiccup_amd import _lib  # noqa: E402
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 2
-    arms = [(1, 0)] + [(5, v) for v in range(10)]
+    arms = [(1, 0)] + [(5, int(v)) for v in os.environ.get("ARMS", "0,1,2,3,4,5,6,7,8,9").split(",")]
     for r in range(reps):
         for path, var in arms:
             with _lib.knobs(dct_path=path, dct_mfma=var):

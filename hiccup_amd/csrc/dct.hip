@@ -393,7 +393,6 @@ constexpr int kMaxPlaneJobs = 16;  // planes per launch (hic_dct_quant_rle_u8_ba
 struct DctJobs {
   DctJob j[kMaxPlaneJobs];
   int n, total_sets, M;
-  int dev;  // HIC_DEV builds only: timing bits of k_dct_mfma (results invalid)
 };
 
 #ifndef HIC_DCT_WPE
@@ -662,15 +661,13 @@ __device__ __forceinline__ void mfma_store(const DctJob &J, int set, const uint2
   __builtin_amdgcn_wave_barrier();
 }
 
-// WPE: waves per SIMD the register budget allows (3: <= 168 VGPRs, 2: <= 256); PF:
-// the next set's pixels load while this set computes (16 more VGPRs); DIRECT: the
-// stage-free pass (mfma_pass_direct: coefficients stored from registers, the tile
-// record from the lanes' nonzero masks)
-template <int TMF, int WPE, bool PF, bool DIRECT = false>
+// WPE: waves per SIMD the register budget allows (3: <= 168 VGPRs, 2: <= 256, with
+// the next group's MFMAs issued before this group's epilogue); PF: the next set's
+// pixels load while this set computes (16 more VGPRs)
+template <int TMF, int WPE, bool PF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_dct_mfma(DctJobs jobs) {
   __shared__ __attribute__((aligned(16))) uint2 s_stage[4 * 64 * kStageU2];
   __shared__ int2 s_k44[4 * 64 * 4];  // (4,4) tie path: the 8 signed row sums per block
-  __shared__ __attribute__((aligned(8))) uint16_t s_nzm[DIRECT ? 4 * 64 * 4 : 1];  // direct: nonzero masks
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nwaves = gridDim.x * 4;
   const int g0 = blockIdx.x * 4 + wv;
@@ -678,13 +675,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   int2 *k44 = s_k44 + wv * 64 * 4;
   const int n = lane & 15, g = lane >> 4;
   const int M = jobs.M;
-#ifdef HIC_DEV
-  // dev timing bits (results invalid): 1 no transform, 2 no stores / records, 4 no
-  // (4,4) tie path, 8 no pixel loads, 16 no records
-  const int dv = jobs.dev;
-#else
-  constexpr int dv = 0;
-#endif
   auto job_of = [&](int gi) {
     gi = __builtin_amdgcn_readfirstlane(gi);
     int k = 0;
@@ -708,7 +698,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       }
       if (J.table != table) {  // wave-uniform: this plane's matrix digits
         table = J.table;
-        mfma_load_A<DIRECT>(table, lane, A);
+        mfma_load_A(table, lane, A);
       }
       const int set = gs - J.set0;
       // pixels: lane (n, g) of N-tile nt holds rows 2g, 2g + 1 of block 16 nt + n
@@ -727,12 +717,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
         for (int rr = 0; rr < 8; ++rr) r[rr] = *reinterpret_cast<const uint2 *>(p + rr * Jx.stride);
       };
-      if (dv & 8) {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) px[r] = make_uint2(0x9E3779B1u * (lane + r + gs), 0x85EBCA6Bu * (lane ^ r));
-      } else if (!PF || gs == g0) {
-        load_px(J, set, px);
-      }
+      if (!PF || gs == g0) load_px(J, set, px);
       i32x4 B[4];
       {
         uint4 *pix = reinterpret_cast<uint4 *>(st2);
@@ -747,32 +732,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
         __builtin_amdgcn_wave_barrier();
       }
-      if (PF && !(dv & 8) && gs + nwaves < jobs.total_sets) {
+      if (PF && gs + nwaves < jobs.total_sets) {
         const int gn = gs + nwaves;
         const int kn = gn >= next0 ? job_of(gn) : kj;
         load_px(jobs.j[kn], gn - jobs.j[kn].set0, px);
       }
-      if constexpr (DIRECT) {
-        uint16_t *nzm = s_nzm + wv * 64 * 4;
-        const int nvalid = J.nblk - set * 64 < 64 ? J.nblk - set * 64 : 64;
-        if (mfma_pass_direct(A, B, static_cast<int16_t *>(J.out) + (int64_t)set * 64 * 64, lane, table, nvalid,
-                             k44, TMF >= 0 ? nzm : nullptr, __builtin_amdgcn_make_buffer_rsrc(nullptr, 0, 0, 0), 0)) {
-          redo |= 1ull << i;  // the whole set again on the float64 path, after the loop
-          continue;
-        }
-        if (TMF >= 0) {
-          __builtin_amdgcn_wave_barrier();
-          const uint64_t m = *reinterpret_cast<const uint64_t *>(nzm + lane * 4);
-          int first = -1, last = -1, nsym = 0;
-          if (lane < nvalid) summarize_ac<TMF>(m >> 1, M, first, last, nsym);
-          tile_record_fs(first, last, nsym, (int64_t)set * 64 + lane, M, J.tiles + (int64_t)set * 3);
-          __builtin_amdgcn_wave_barrier();
-        }
-        continue;
-      }
       uint64_t m44 = 0;
-      const bool flagged = (dv & 1) ? false : mfma_pass(A, B, st2, lane, table, m44);
-      if (dv & 4) m44 = 0;
+      const bool flagged = mfma_pass<WPE == 2>(A, B, st2, lane, table, m44);
       if (flagged) {
         redo |= 1ull << i;  // the whole set again on the float64 path, after the loop
         continue;
@@ -800,12 +766,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
         __builtin_amdgcn_wave_barrier();
       }
-      if (!(dv & 2)) {
-        if (dv & 16)
-          mfma_store<-1>(J, set, st2, lane, M);
-        else
-          mfma_store<TMF>(J, set, st2, lane, M);
-      }
+      mfma_store<TMF>(J, set, st2, lane, M);
     }
   }
   // flagged sets: the float64 AAN path (its own exact fallbacks) on this wave's sets
@@ -837,156 +798,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       st[kSlot.s[54]] = (int16_t)q[3];
     }
     mfma_store<TMF>(J, set, st2, lane, M);
-  }
-}
-
-// The direct pass fed by LDS-DMA prefetch (knob dct_mfma bit 3): each set's 4 KiB of
-// pixels arrive by buffer_load ... lds (16 B per lane, two adjacent blocks' row: W/8
-// even), two sets ahead, into two LDS buffers per wave -- no VGPRs held for the
-// prefetch.  The DMA completes on vmcnt, which counts every vector-memory
-// instruction in issue order, so every set issues a FIXED number of them: 8
-// coefficient stores (buffer stores: out-of-range lanes dropped, never skipped) and
-// 3 record stores from lane 0 (kSetVm); the wait before a set's pixels are read
-// leaves the later sets' instructions outstanding (the next set's 4 DMA loads and
-// the previous set's stores).  The stage-free pass needs no LDS stage; the rare
-// flagged set is redone after the loop in the pixel buffers (128-B stage rows).
-constexpr int kSetVmData = 8, kSetVmRec = 3;
-template <int TMF, int WPE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_dct_mfma_dma(DctJobs jobs) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_px[4][2][1024];  // [wave][buffer][row r][block b] 8 B
-  __shared__ int2 s_k44[4 * 64 * 4];
-  __shared__ __attribute__((aligned(8))) uint16_t s_nzm[4 * 64 * 4];
-  constexpr int kVm = kSetVmData + (TMF >= 0 ? kSetVmRec : 0);
-  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nwaves = gridDim.x * 4;
-  const int g0 = blockIdx.x * 4 + wv;
-  int2 *k44 = s_k44 + wv * 64 * 4;
-  uint16_t *nzm = s_nzm + wv * 64 * 4;
-  const int n = lane & 15, g = lane >> 4;
-  const int M = jobs.M;
-  auto job_of = [&](int gi) {
-    gi = __builtin_amdgcn_readfirstlane(gi);
-    int k = 0;
-    while (k + 1 < jobs.n && gi >= jobs.j[k + 1].set0) ++k;
-    return __builtin_amdgcn_readfirstlane(k);
-  };
-  typedef __attribute__((address_space(3))) void lds_void;
-  // set gs's pixels -> buffer bf: instruction k moves rows 2k, 2k + 1 (lane L: row
-  // 2k + L / 32, blocks 2 (L % 32), 2 (L % 32) + 1, 16 contiguous bytes)
-  auto dma = [&](int gs, int bf) {
-    const DctJob &J = jobs.j[job_of(gs)];
-    const int set = gs - J.set0;
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t *>(J.plane), 0, (int)(J.stride * (J.nblk / J.nbx) * 8), 0x00020000);
-    int blk = set * 64 + 2 * (lane & 31);
-    if (blk >= J.nblk) blk = set * 64;  // a pair past the plane: any valid one (ignored)
-    const int bi = blk / J.nbx, bj = blk - bi * J.nbx;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t vo = (uint32_t)((bi * 8 + 2 * k + (lane >> 5)) * J.stride + bj * 8);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void *)(s_px[wv][bf] + 256 * k), 16, vo, 0, 0, 0);
-    }
-  };
-  uint64_t redo = 0;
-  int i = 0;
-  if (g0 < jobs.total_sets) {
-    int kj = job_of(g0);
-    DctJob J = jobs.j[kj];
-    int next0 = kj + 1 < jobs.n ? jobs.j[kj + 1].set0 : jobs.total_sets;
-    int table = -1;
-    i32x4 A[4][4];
-    dma(g0, 0);
-    if (g0 + nwaves < jobs.total_sets) dma(g0 + nwaves, 1);
-    for (int gs = g0; gs < jobs.total_sets; gs += nwaves, ++i) {
-      if (gs >= next0) {
-        kj = job_of(gs);
-        J = jobs.j[kj];
-        next0 = kj + 1 < jobs.n ? jobs.j[kj + 1].set0 : jobs.total_sets;
-      }
-      const bool has_next = gs + nwaves < jobs.total_sets;
-      // this set's DMA done: the instructions issued after it may stay outstanding
-      if (i == 0) {
-        if (has_next) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      } else if (has_next) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kVm + 4) : "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kVm) : "memory");
-      }
-      if (J.table != table) {  // wave-uniform (its loads are younger than every DMA waited for)
-        table = J.table;
-        mfma_load_A<true>(table, lane, A);
-      }
-      const int set = gs - J.set0;
-      const uint32_t *px = s_px[wv][i & 1];
-      i32x4 B[4];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int b = 16 * nt + n;
-        const uint2 r0 = *reinterpret_cast<const uint2 *>(px + (2 * g) * 128 + 2 * b);
-        const uint2 r1 = *reinterpret_cast<const uint2 *>(px + (2 * g + 1) * 128 + 2 * b);
-        B[nt] = mfma_pixels(r0, r1);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the buffer is free for the DMA two sets ahead
-      if (gs + 2 * nwaves < jobs.total_sets) dma(gs + 2 * nwaves, i & 1);
-      const int nvalid = J.nblk - set * 64 < 64 ? J.nblk - set * 64 : 64;
-      const __amdgpu_buffer_rsrc_t orsrc =
-          __builtin_amdgcn_make_buffer_rsrc(J.out, 0, (int)((int64_t)J.nblk * 128), 0x00020000);
-      const bool flagged = mfma_pass_direct<true>(A, B, nullptr, lane, table, nvalid, k44, TMF >= 0 ? nzm : nullptr,
-                                                  orsrc, (uint32_t)set * 8192u);
-      if (flagged) redo |= 1ull << i;  // redone after the loop (its stores and record rewritten)
-      if (TMF >= 0) {
-        __builtin_amdgcn_wave_barrier();
-        const uint64_t m = *reinterpret_cast<const uint64_t *>(nzm + lane * 4);
-        int first = -1, last = -1, nsym = 0;
-        if (lane < nvalid) summarize_ac<TMF>(m >> 1, M, first, last, nsym);
-        int64_t r0, r1, r2;
-        tile_record_values(first, last, nsym, (int64_t)set * 64 + lane, M, r0, r1, r2);
-        // three 8-byte stores from lane 0: issued on every set (vmcnt bookkeeping)
-        const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(J.tiles, 0, 0x7FFFFFFF, 0x00020000);
-        if (lane == 0) {
-          typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-          const uint32_t so = (uint32_t)set * 24u;
-          __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)r0, (uint32_t)(r0 >> 32)}, rr, 0, so, 0);
-          __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)r1, (uint32_t)(r1 >> 32)}, rr, 8, so, 0);
-          __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)r2, (uint32_t)(r2 >> 32)}, rr, 16, so, 0);
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  // flagged sets: the float64 AAN path on the wave's pixel buffers as its stage
-  // (64 rows of 128 B), then 1 KiB stores and the record
-  uint2 *st2 = reinterpret_cast<uint2 *>(s_px[wv][0]);
-  int16_t *st = reinterpret_cast<int16_t *>(st2 + lane * 16);
-  while (redo) {
-    const int k = __builtin_ctzll(redo);
-    redo &= redo - 1;
-    const int gs = g0 + k * nwaves;
-    const DctJob &J = jobs.j[job_of(gs)];
-    const int set = gs - J.set0;
-    const int blk = set * 64 + lane;
-    const int cblk = blk < J.nblk ? blk : J.nblk - 1;
-    const int bi = cblk / J.nbx, bj = cblk - bi * J.nbx;
-    const uint8_t *p = J.plane + (int64_t)bi * 8 * J.stride + bj * 8;
-    uint2 w[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) w[r] = *reinterpret_cast<const uint2 *>(p + r * J.stride);
-    bool t26 = false;
-    const bool f = dct_block_aan<-1, HIC_LAYOUT_ZIGZAG_I16>(w, st, &t26, nullptr, J.table);
-    if (f) {
-      dct_block_2ph<-1, HIC_LAYOUT_ZIGZAG_I16>(w, st, J.table);
-    } else if (t26) {
-      constexpr SlotOf<HIC_LAYOUT_ZIGZAG_I16> kSlot{};
-      int q[4];
-      dct_fix26<-1>(w, q, J.table);
-      st[kSlot.s[18]] = (int16_t)q[0];
-      st[kSlot.s[22]] = (int16_t)q[1];
-      st[kSlot.s[50]] = (int16_t)q[2];
-      st[kSlot.s[54]] = (int16_t)q[3];
-    }
-    mfma_store<TMF, 16>(J, set, st2, lane, M);
   }
 }
 
@@ -1089,15 +900,7 @@ int launch_planes(DctJobs &jobs, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   const dim3 grid((waves + 3) / 4), block(256);
   const int path = dct_path();
   if (path == 5 && LAYOUT == HIC_LAYOUT_ZIGZAG_I16) {
-    int var = knob(HIC_KNOB_DCT_MFMA);
-    if (var >= 8) {  // the DMA kernel: 16-byte pixel pairs (W / 8 even, 8-byte aligned rows)
-      bool ok = true;
-      for (int k = 0; k < jobs.n; ++k)
-        ok = ok && jobs.j[k].nbx % 2 == 0 && jobs.j[k].stride % 8 == 0 &&
-             (int64_t)jobs.j[k].stride * (jobs.j[k].nblk / jobs.j[k].nbx) * 8 < (1ll << 31);
-      if (!ok) var = 4;
-    }
-    jobs.dev = knob(HIC_KNOB_DEV);
+    const int var = knob(HIC_KNOB_DCT_MFMA);
     auto go = [&](auto kern) {
       if (e0 || e1)
         hipExtLaunchKernelGGL(kern, grid, block, 0, s, e0, e1, 0, jobs);
@@ -1107,13 +910,7 @@ int launch_planes(DctJobs &jobs, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     if (var == 0) go(k_dct_mfma<TMF, 3, false>);
     else if (var == 1) go(k_dct_mfma<TMF, 3, true>);
     else if (var == 2) go(k_dct_mfma<TMF, 2, false>);
-    else if (var == 3) go(k_dct_mfma<TMF, 2, true>);
-    else if (var == 4) go(k_dct_mfma<TMF, 3, false, true>);
-    else if (var == 5) go(k_dct_mfma<TMF, 3, true, true>);
-    else if (var == 6) go(k_dct_mfma<TMF, 2, false, true>);
-    else if (var == 7) go(k_dct_mfma<TMF, 2, true, true>);
-    else if (var == 8) go(k_dct_mfma_dma<TMF, 3>);
-    else go(k_dct_mfma_dma<TMF, 2>);
+    else go(k_dct_mfma<TMF, 2, true>);
     return check_launch("k_dct_mfma");
   }
   if (e0 || e1)

@@ -306,12 +306,12 @@ def test_measurement_probes():
         _lib.call("hic_probe_copy", device.ptr(a), device.ptr(b), 17, 0, device.stream_ptr(), None, None)
 
 
-@pytest.mark.parametrize("var", range(10))
+@pytest.mark.parametrize("var", range(4))
 @pytest.mark.parametrize("kind", ["random", "levels4", "nearflat", "checker"])
 def test_mfma_plane_variants(kind, var):
     """Every k_dct_mfma variant (knob dct_mfma: bit 0 prefetch, bit 1 two waves per
-    SIMD, bit 2 the stage-free direct stores) writes the oracle's coefficients and
-    RLE tile records (a partial last set included)."""
+    SIMD) writes the oracle's coefficients and RLE tile records (a partial last set
+    included)."""
     for H, W in ((8 * 33, 8 * 130), (8 * 160, 8 * 320)):
         with _lib.knobs(dct_mfma=var):
             test_plane_dct_rle_records(kind, _lib.DCT_PATH_MFMA, H, W)

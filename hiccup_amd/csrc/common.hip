@@ -1,6 +1,8 @@
 // common.hip -- error state and small runtime entry points of the C-ABI.
 #include <string.h>
 
+#include <atomic>
+
 #include "hic_common.h"
 
 namespace hic {
@@ -19,6 +21,11 @@ int knob(int k) {
     case HIC_KNOB_ENCODE_NT: return 1;
     default: return k == HIC_KNOB_DCT_WAVES_PER_CU ? -1 : 0;
   }
+}
+
+uint32_t next_epoch() {
+  static std::atomic<uint32_t> epoch{0};
+  return (epoch.fetch_add(1) % ((1u << 30) - 1)) + 1;  // never 0 (zeroed workspace)
 }
 
 void set_error(const char *fmt, ...) {

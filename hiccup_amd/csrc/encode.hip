@@ -42,6 +42,7 @@
 #include "color_core.h"
 #include "dct_core.h"
 #include "dct_mfma.h"
+#include "onepass.h"
 #include "rle_core.h"
 
 namespace hic {
@@ -55,6 +56,18 @@ struct Enc420 {
   int M;
   int nstrips, nunits;  // nunits: waves (one unit each)
   int wlast;            // pixel columns of the last strip (16 .. 512)
+  // one-pass encode (hic_encode420_rle_u8): per plane Y, Cr, Cb
+  int32_t *dc[3];
+  uint8_t *sym_len[3];
+  int16_t *sym_val[3];
+  int64_t cap[3];
+  int64_t *d_count[3];
+  uint64_t *gran[3];  // look-back granules, 8 per record (onepass.h)
+  int last_rec[3];    // the plane's last record (it closes the stream)
+  int64_t n_ac[3];    // the plane's AC stream length
+  uint32_t *ticket;   // unit tickets (reset by the wave that takes the last one)
+  uint64_t *fail;     // the launch's timeout word (tag (epoch << 2) | 3)
+  uint32_t epoch;
 };
 
 constexpr int kZZ = HIC_LAYOUT_ZIGZAG_I16;
@@ -368,6 +381,88 @@ struct EncColour {
   }
 };
 
+// One-pass: the record of the pass in the stage (rows = this lane's block; SEG:
+// lanes 0-31 Cr record `rec`, 32-63 Cb record `rec`, else the Y record `rec`):
+// publish its aggregate, look back, publish the inclusive prefix, DC differences,
+// symbols, and (the plane's last record) the stream's EOB and count.  b: this lane's
+// block in its plane.
+template <int TMF, bool SEG>
+__device__ __forceinline__ void op_pass(const Enc420 &E, const uint2 *st2, uint8_t *s_len, int16_t *s_val, int rec,
+                                        int64_t b) {
+  const int lane = fresh_lane(), sl = SEG ? lane & 31 : lane, seg0 = SEG ? lane & 32 : 0;
+  const int p = SEG ? 1 + (lane >> 5) : 0;
+  const int M = E.M;
+  uint32_t zw[32];
+  enc_stage_row(st2, lane, zw);
+  const int16_t *blk = reinterpret_cast<const int16_t *>(st2 + lane * kStageU2);
+  int first = -1, last = -1, nsym = 0;
+  uint64_t ac = 0;
+  summarize16<TMF>(zw, M, first, last, nsym, &ac);
+  // the record's aggregate (tile_record16_half's fields, as stream positions)
+  const int lastr = last >= 0 ? sl * 63 + last : -1;
+  const int incl = SEG ? seg32_incl_max_i32(lastr) : wave_incl_max_i32(lastr);
+  int prevr = wave_shr1_i32(-1, incl);
+  if (sl == 0) prevr = -1;
+  int c = nsym;
+  if (first >= 0 && prevr >= 0) c += syms_for_run(sl * 63 + first - prevr - 1, M);
+  const int ic = SEG ? seg32_incl_sum_i32(c) : wave_incl_sum_i32(c);
+  const int segL = seg0 + (SEG ? 31 : 63);
+  const int all_last = __shfl(incl, segL), tot = __shfl(ic, segL);
+  const uint64_t fm = __builtin_amdgcn_ballot_w64(first >= 0);
+  const uint64_t fmh = SEG ? (fm >> seg0) & 0xFFFFFFFFull : fm;
+  const int fl = fmh ? __builtin_ctzll(fmh) : 0;
+  const int ff = __shfl(sl * 63 + first, seg0 + fl);
+  const int base = (int)((b - sl) * 63);  // stream position of the record's first AC
+  const Agg32 A = all_last < 0 ? Agg32{-1, -1, 0} : Agg32{base + ff, base + all_last, tot};
+  const int dc = (int)(int16_t)(zw[0] & 0xFFFFu);
+  const int lastdc = __shfl(dc, segL);
+  uint64_t *g = E.gran[p];
+  const uint32_t tagA = (E.epoch << 2) | 1u, tagP = (E.epoch << 2) | 2u;
+  auto put4 = [&](const Agg32 &a, int off, uint32_t tag) {
+    if (sl < 4) op_put(g + 8 * (int64_t)rec + off + sl, sl == 0 ? a.first : sl == 1 ? a.last : sl == 2 ? a.cnt : lastdc,
+                       tag);
+  };
+  put4(A, 0, tagA);
+  Agg32 ex;
+  int pdc;
+  const bool ok = op_lookback<SEG>(g, rec, tagA, tagP, M, ex, pdc);
+  const Agg32 P = agg32(ex, A, M);
+  put4(P, 4, tagP);
+  // DC differences (codec.differential_coding): the record's first block takes the
+  // previous record's last DC (0 before the plane's first block)
+  int pd = __shfl_up(dc, 1, 64);
+  if (sl == 0) pd = pdc;
+  E.dc[p][b] = dc - pd;
+  // the record's first symbol and the last nonzero before it (no carry: p0 = -1)
+  const int64_t o_seg = ex.last >= 0 ? (int64_t)ex.cnt + syms_for_run(ex.first, M) : 0;
+  const int64_t prev_seg = ex.last >= 0 ? ex.last : -1;
+  if (SEG)
+    op_emit<TMF, true>(zw, blk, b * 63, M, o_seg, prev_seg, first, last, nsym, ac, s_len, s_val, E.sym_len[1],
+                       E.sym_val[1], E.cap[1], E.sym_len[2], E.sym_val[2], E.cap[2]);
+  else
+    op_emit<TMF, false>(zw, blk, b * 63, M, o_seg, prev_seg, first, last, nsym, ac, s_len, s_val, E.sym_len[0],
+                        E.sym_val[0], E.cap[0], E.sym_len[0], E.sym_val[0], E.cap[0]);
+  if (!ok && sl == 0) {
+    op_put(E.fail, 1, (E.epoch << 2) | 3u);
+    __hip_atomic_store(E.d_count[p], (int64_t)HIC_COUNT_SCAN_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (rec == E.last_rec[p] && sl == 0) {
+    // the stream's end (k_rle_scan16b's closing step): EOB unless the last AC is nonzero
+    int64_t total = P.last >= 0 ? (int64_t)P.cnt + syms_for_run(P.first, M) : 0;
+    if (!(E.n_ac[p] > 0 && P.last == E.n_ac[p] - 1)) {
+      if (total < E.cap[p]) {
+        E.sym_len[p][total] = 0;
+        E.sym_val[p][total] = 0;
+      }
+      ++total;
+    }
+    __hip_atomic_store(E.d_count[p], total <= E.cap[p] ? total : -total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // a timeout anywhere in the launch wins over the count
+    if ((uint32_t)(op_get(E.fail) >> 32) == ((E.epoch << 2) | 3u))
+      __hip_atomic_store(E.d_count[p], (int64_t)HIC_COUNT_SCAN_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // One wave per unit, 3 waves per SIMD (<= 168 VGPRs): all 19 colour rows first, so
 // no DCT runs while the row ring and the pyrDown window are live (the other waves of
 // the SIMD hide the loads instead); each packed Y row is pinned where it is made;
@@ -378,13 +473,29 @@ struct EncColour {
 // variants and cached stores were measured slower and are gone (git history).
 // MFMA: the integer-MFMA transform (dct_mfma.h) for the three passes instead of the
 // float64 AAN (knob "encode_dct" 1; bit-exact either way).
-template <int TMF, bool MFMA>
-__global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_eu(3))) void k_encode420(Enc420 E) {
+// OP (one-pass, hic_encode420_rle_u8; float64 AAN only): 2 waves per SIMD -- each
+// wave also holds a 2048-symbol emission stage (6 KiB of LDS) -- units by ticket
+// (dispatch order, the look-back's progress guarantee), each pass's record handed
+// off and emitted right after its coefficients are stored (op_pass).
+template <int TMF, bool MFMA, bool OP = false>
+__global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_eu(OP ? 2 : 3))) void k_encode420(
+    Enc420 E) {
+  static_assert(!(MFMA && OP), "the one-pass encode runs the float64 AAN transform");
   __shared__ __attribute__((aligned(16))) uint2 s_stage[HIC_ENC_WPB * 64 * kStageU2];
   __shared__ uint32_t s_chroma_all[HIC_ENC_WPB][2 * 8 * 64];
+  __shared__ __attribute__((aligned(16))) uint8_t s_oplen[OP ? HIC_ENC_WPB : 1][OP ? kOpSyms + 32 : 16];
+  __shared__ __attribute__((aligned(16))) int16_t s_opval[OP ? HIC_ENC_WPB : 1][OP ? kOpSyms + 32 : 8];
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g = __builtin_amdgcn_readfirstlane(blockIdx.x * HIC_ENC_WPB + wv);
+  int g = __builtin_amdgcn_readfirstlane(blockIdx.x * HIC_ENC_WPB + wv);
   if (g >= E.nunits) return;  // wave-uniform
+  if (OP) {
+    // tickets in the order waves start; the last one resets the counter for the next
+    // launch (every ticket is taken by then)
+    uint32_t t = 0;
+    if (lane == 0) t = __hip_atomic_fetch_add(E.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    g = (int)__builtin_amdgcn_readfirstlane(t);
+    if (g == E.nunits - 1 && lane == 0) __hip_atomic_store(E.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   uint2 *st2 = s_stage + wv * 64 * kStageU2;
   uint32_t *s_chroma = s_chroma_all[wv];
   int16_t *st = reinterpret_cast<int16_t *>(st2 + lane * kStageU2);
@@ -409,7 +520,10 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
     __builtin_amdgcn_wave_barrier();
     int16_t *o = E.coef[0] + b0 * 64;
     enc_store(st2, fresh_lane(), o, o + 32 * 64, nb < 32 ? nb : 32, nb > 32 ? nb - 32 : 0);
-    if (TMF >= 0 && E.rec[0]) {
+    if (OP) {
+      op_pass<TMF, false>(E, st2, s_oplen[OP ? wv : 0], s_opval[OP ? wv : 0], (2 * u0 + br) * E.nstrips + s,
+                          b0 + fresh_lane());
+    } else if (TMF >= 0 && E.rec[0]) {
       uint32_t zw[32];
       enc_stage_row(st2, fresh_lane(), zw);
       tile_record16<TMF>(zw, true, b0 + lane, E.M, E.rec[0] + (b0 >> 6) * 3);
@@ -454,7 +568,10 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
     const int64_t b0 = (int64_t)u0 * nbxc + 32 * s;
     __builtin_amdgcn_wave_barrier();
     enc_store(st2, fresh_lane(), E.coef[1] + b0 * 64, E.coef[2] + b0 * 64, nb >> 1, nb >> 1);
-    if (TMF >= 0 && E.rec[1]) {
+    if (OP) {
+      op_pass<TMF, true>(E, st2, s_oplen[OP ? wv : 0], s_opval[OP ? wv : 0], u0 * E.nstrips + s,
+                         b0 + (fresh_lane() & 31));
+    } else if (TMF >= 0 && E.rec[1]) {
       uint32_t zw[32];
       enc_stage_row(st2, fresh_lane(), zw);
       tile_record16_half<TMF>(zw, b0, E.M, E.rec[1] + (b0 >> 5) * 3, E.rec[2] + (b0 >> 5) * 3);
@@ -583,9 +700,9 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
   };
   const bool mfma = knob(HIC_KNOB_ENCODE_DCT) == 1;
   if (max_len == 15)
-    mfma ? launch(k_encode420<15, true>) : launch(k_encode420<15, false>);
+    mfma ? launch(k_encode420<15, true, false>) : launch(k_encode420<15, false, false>);
   else
-    mfma ? launch(k_encode420<0, true>) : launch(k_encode420<0, false>);
+    mfma ? launch(k_encode420<0, true, false>) : launch(k_encode420<0, false, false>);
   if (int e = check_launch("k_encode420")) return e;
   if (recs && !aligned) {  // one record per 64-block tile, all three planes
     const int64_t ny = (out_rows / 8) * (W / 8), nc = (out_rows / 16) * (W / 16);
@@ -594,4 +711,69 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
     if (int e = rle_tile16_launch(coef_cb, nc, max_len, static_cast<int64_t *>(ws_cb), s)) return e;
   }
   return HIC_OK;
+}
+
+extern "C" int hic_encode420_rle_u8(const uint8_t *rgb, int64_t H, int64_t W, const hic_rle_job16 *jobs, int max_len,
+                                    void *stream, void *ev_start, void *ev_stop) {
+  if (!rgb || !jobs) return arg_error("null pointer");
+  if (H < 16 || W < 512 || H % 16 || W % 512 || H >= (1 << 20) || W >= (1 << 20))
+    return arg_error("hic_encode420_rle_u8 needs W %% 512 == 0 and H %% 16 == 0");
+  if (reinterpret_cast<uintptr_t>(rgb) % 8) return arg_error("rgb must be 8-byte aligned");
+  if (H * W * 3 > INT32_MAX) return arg_error("hic_encode420_rle_u8: image exceeds 2 GiB (use the chain)");
+  if (max_len < 0 || max_len > 256) return arg_error("max_len");
+  const int64_t nblk[3] = {(H / 8) * (W / 8), (H / 16) * (W / 16), (H / 16) * (W / 16)};
+  if (nblk[0] > (int64_t)INT32_MAX / 63) return arg_error("nblk too large (AC stream >= 2^31)");
+  Enc420 E{};
+  E.rgb = rgb;
+  E.in_row0 = 0;
+  E.in_rows = (int)H;
+  E.H = (int)H;
+  E.W = (int)W;
+  E.out_row0 = 0;
+  E.out_rows = (int)H;
+  E.M = max_len;
+  E.nstrips = (int)(W / 512);
+  E.wlast = 512;
+  E.nunits = E.nstrips * (int)(H / 16);
+  for (int k = 0; k < 3; ++k) {
+    const hic_rle_job16 &J = jobs[k];
+    if (!J.blocks || !J.dc_diff || !J.sym_len || !J.sym_val || !J.d_count || !J.workspace)
+      return arg_error("job %d: null pointer", k);
+    if (J.nblk != nblk[k]) return arg_error("job %d: nblk %lld, expected %lld", k, (long long)J.nblk, (long long)nblk[k]);
+    if (J.d_stitch) return arg_error("job %d: the one-pass encode takes whole images (no stitch)", k);
+    if (reinterpret_cast<uintptr_t>(J.blocks) % 16 || reinterpret_cast<uintptr_t>(J.sym_len) % 16 ||
+        reinterpret_cast<uintptr_t>(J.sym_val) % 16)
+      return arg_error("job %d: blocks / symbol buffers must be 16-byte aligned", k);
+    if (J.sym_cap < 0) return arg_error("job %d: sym_cap", k);
+    E.coef[k] = const_cast<int16_t *>(J.blocks);
+    E.rec[k] = nullptr;
+    E.dc[k] = J.dc_diff;
+    E.sym_len[k] = J.sym_len;
+    E.sym_val[k] = J.sym_val;
+    E.cap[k] = J.sym_cap;
+    E.d_count[k] = J.d_count;
+    E.gran[k] = static_cast<uint64_t *>(J.workspace);
+    E.last_rec[k] = k == 0 ? (int)(2 * (H / 16) * E.nstrips - 1) : (int)((H / 16) * E.nstrips - 1);
+    E.n_ac[k] = nblk[k] * 63;
+  }
+  // the ticket counter and the timeout word: the last words of Y's workspace
+  // (hic_rle_workspace_bytes; past the granules and the chain scan's hand-off)
+  const int64_t words = (int64_t)(hic_rle_workspace_bytes(nblk[0], 64) / sizeof(int64_t));
+  E.ticket = reinterpret_cast<uint32_t *>(E.gran[0] + words - 1);
+  E.fail = E.gran[0] + words - 2;
+  E.epoch = next_epoch();
+  const dim3 grid((unsigned)((E.nunits + HIC_ENC_WPB - 1) / HIC_ENC_WPB)), block(64 * HIC_ENC_WPB);
+  hipStream_t s = as_stream(stream);
+  hipEvent_t e0 = static_cast<hipEvent_t>(ev_start), e1 = static_cast<hipEvent_t>(ev_stop);
+  auto launch = [&](auto kern) {
+    if (e0 || e1)
+      hipExtLaunchKernelGGL(kern, grid, block, 0, s, e0, e1, 0, E);
+    else
+      hipLaunchKernelGGL(kern, grid, block, 0, s, E);
+  };
+  if (max_len == 15)
+    launch(k_encode420<15, false, true>);
+  else
+    launch(k_encode420<0, false, true>);
+  return check_launch("k_encode420 (one-pass)");
 }

@@ -66,6 +66,11 @@ inline int cu_count() {
   return n;
 }
 
+// A launch's hand-off epoch in [1, 2^30 - 1], unique per call (until it wraps):
+// tags of the RLE scan's and the one-pass encode's granules, shared so that one
+// workspace used by both never sees a stale granule match.
+uint32_t next_epoch();
+
 // Cross-file launchers (rle.hip): the hot-path RLE tile pass on int16 zig-zag
 // blocks of 64, for callers whose transform did not fuse it.
 int rle_tile16_launch(const int16_t *blocks, int64_t nblk, int max_len, int64_t *tiles, hipStream_t s);

@@ -1347,8 +1347,7 @@ int encode_batch16(RleJobs16 &jobs, hipStream_t s) {
     t0 += jobs.j[k].ntiles;
   }
   jobs.total_tiles = t0;
-  static std::atomic<uint32_t> epoch{0};
-  const uint32_t ep = (epoch.fetch_add(1) % ((1u << 30) - 1)) + 1;  // never 0 (zeroed workspace)
+  const uint32_t ep = next_epoch();
   int64_t nparts = 0;
   for (int k = 0; k < jobs.n; ++k) nparts += (jobs.j[k].nrec + kScan16T - 1) / kScan16T;
   jobs.epoch = ep;
@@ -1619,8 +1618,11 @@ extern "C" size_t hic_rle_workspace_bytes(int64_t nblk, int block_len) {
   // sized for the hot path's 32-block half-tile records (hic_encode420_u8's chroma;
   // >= its 64-block tiles and the generic 256-block tiles)
   const int64_t n = nblk > 0 ? nblk : 1, nt = (n + kWT / 2 - 1) / (kWT / 2);
-  // tile records (3), offsets (2) per tile; 3 hand-off granules per scan partition
-  return (size_t)(5 * nt + 3 * ((nt + kScan16T - 1) / kScan16T) + 8) * sizeof(int64_t);
+  // tile records (3), offsets (2) per tile; 3 hand-off granules per scan partition;
+  // or (hic_encode420_rle_u8) 8 look-back granules per record, then its ticket
+  // counter and timeout word
+  const int64_t chain = 5 * nt + 3 * ((nt + kScan16T - 1) / kScan16T) + 8, onepass = 8 * nt + 8;
+  return (size_t)(chain > onepass ? chain : onepass) * sizeof(int64_t);
 }
 
 extern "C" int hic_rle_shard_summary_i16(const int16_t *blocks, int64_t nblk, int block_len, void *workspace,

@@ -61,6 +61,10 @@ def check_count(c, channel=""):
     raise MemoryError("symbol buffer too small for channel %s: %d symbols needed" % (channel, -c))
 
 
+# Encoder.encode runs the one-pass kernel where it applies (whole image, W % 512 == 0)
+ONEPASS_DEFAULT = True
+
+
 def encoder_layout(H, W, rows=None, fused=None):
     """(fused, rpt) of an Encoder of rows `rows` of an H x W image: whether it runs
     the fused kernel (None = the measured default: W % 512 == 0 and fusable), and its
@@ -83,7 +87,8 @@ class Encoder:
     """rows=(r0, r1) makes this encoder one row-shard of an H x W image (r0 even;
     shards of one image split at multiples of 16 rows so chroma blocks align)."""
 
-    def __init__(self, H, W, max_len=15, rows=None, out=None, fused=None, index=False, landing_rpt=None):
+    def __init__(self, H, W, max_len=15, rows=None, out=None, fused=None, index=False, landing_rpt=None,
+                 onepass=None):
         """out: optional {channel: (coef (n, 64) int16, dc (n,) int32)} device views the
         encoder writes into (a gathering rank points them at its slice of the whole
         image's buffers, so its own shard needs no copy).
@@ -94,7 +99,11 @@ class Encoder:
         40.5 us per image); False = the chain.
         landing_rpt: a landing zone only (the gathering rank of a stream gather): no
         transform, no plane buffers, and the RLE record layout of the shards that
-        fill it (their encoder_layout rpt), whatever this shape alone would pick."""
+        fill it (their encoder_layout rpt), whatever this shape alone would pick.
+        onepass: encode() as ONE kernel (hic_encode420_rle_u8: the fused transform
+        with the DC / RLE emission and a look-back for the stream offsets) -- whole
+        images with W % 512 == 0 and no tile index; None = ONEPASS_DEFAULT where it
+        applies, False = transform() + entropy()."""
         if H < 2 or W < 2:
             raise ValueError("image must be at least 2 x 2")
         device.require_gpu()
@@ -109,6 +118,11 @@ class Encoder:
             self.fused, self.rpt = False, dict(landing_rpt)
         else:
             self.fused, self.rpt = encoder_layout(H, W, (r0, r1), fused)
+        can_1p = (not self.landing and self.fused and (r0, r1) == (0, H) and W % 512 == 0 and not self.want_index
+                  and H * W * 3 <= 2**31 - 1)
+        if onepass and not can_1p:
+            raise ValueError("the one-pass encode needs a whole image with W % 512 == 0 (fused), no tile index")
+        self.onepass = can_1p and (ONEPASS_DEFAULT if onepass is None else bool(onepass))
         c0, c1 = r0 // 2, min(H // 2, r1 // 2)
         self.shapes = {"lum": (r1 - r0, W), "cr": (c1 - c0, W // 2), "cb": (c1 - c0, W // 2)}
         ys, cs = self.shapes["lum"], self.shapes["cr"]
@@ -203,21 +217,33 @@ class Encoder:
         emit launch for all three).  stitch: None or a (3, 4) int64 device tensor of
         per-channel {carry_zeros, emit_eob, has_prev_dc, prev_dc}."""
         s = device.stream_ptr(stream)
-        jobs = (_lib.RleJob16 * 3)()
-        for i, k in enumerate(CHANNELS):
-            jobs[i] = _lib.RleJob16(self.coef[k].data_ptr(), self.coef[k].shape[0],
-                                    stitch[i].data_ptr() if stitch is not None else None, self.dc[k].data_ptr(),
-                                    self.sym_len[k].data_ptr(), self.sym_val[k].data_ptr(), self.cap[k],
-                                    self.counts[i:i + 1].data_ptr(), self.ws[k].data_ptr(), self.rpt[k])
-        _lib.call("hic_rle_encode_i16_tiles_batch", 3, jobs, self.max_len, s)
+        _lib.call("hic_rle_encode_i16_tiles_batch", 3, self._rle_jobs(stitch), self.max_len, s)
         if self.index is not None and stitch is None:
             for k in CHANNELS:
                 _lib.call("hic_rle_tile_index_i16", device.ptr(self.coef[k]), self.coef[k].shape[0], self.rpt[k],
                           device.ptr(self.ws[k]), device.ptr(self.index[k]), s)
 
     def encode(self, rgb, stream=None, dct_events=None):
+        if self.onepass:
+            # transform + DC DPCM + AC RLE of the three channels in one launch
+            # (dct_events time it)
+            if tuple(rgb.shape) != (self.H, self.W, 3):
+                raise ValueError("the one-pass encode takes the whole H x W x 3 image")
+            ev = (dct_events.start, dct_events.stop) if dct_events is not None else (None, None)
+            _lib.call("hic_encode420_rle_u8", device.ptr(rgb), self.H, self.W, self._rle_jobs(None), self.max_len,
+                      device.stream_ptr(stream), *ev)
+            return
         self.transform(rgb, stream, dct_events=dct_events)
         self.entropy(stream)
+
+    def _rle_jobs(self, stitch):
+        jobs = (_lib.RleJob16 * 3)()
+        for i, k in enumerate(CHANNELS):
+            jobs[i] = _lib.RleJob16(self.coef[k].data_ptr(), self.coef[k].shape[0],
+                                    stitch[i].data_ptr() if stitch is not None else None, self.dc[k].data_ptr(),
+                                    self.sym_len[k].data_ptr(), self.sym_val[k].data_ptr(), self.cap[k],
+                                    self.counts[i:i + 1].data_ptr(), self.ws[k].data_ptr(), self.rpt[k])
+        return jobs
 
     def hic_image(self, stream=None):
         """codec.jpeg_encode of this encode, from the device streams: the nine Huffman

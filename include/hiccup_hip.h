@@ -276,6 +276,24 @@ typedef struct {
                                2: one per 32 blocks (hic_encode420_u8's chroma planes) */
 } hic_rle_job16;
 int hic_rle_encode_i16_tiles_batch(int n, const hic_rle_job16 *jobs, int max_len, void *stream);
+/* ---- one-pass encode (round 4): hic_encode420_u8 + hic_rle_encode_i16_tiles_batch
+ *      of the three channels in ONE kernel -- compression.jpeg_compression's
+ *      transform (compression.py:16-39) and codec.jpeg_encode's differential_coding
+ *      + run_length_coding of each channel (codec.py:47-99, 286-301).  Each unit's
+ *      records take their stream offsets by a decoupled look-back over the earlier
+ *      records' published aggregates; DC differences and AC symbols leave from the
+ *      unit's LDS stage (no coefficient re-read, no scan launch).  Output identical
+ *      to the two calls it replaces.
+ *  rgb: the whole H x W x 3 uint8 image (8-byte aligned, < 2 GiB); W % 512 == 0,
+ *  H % 16 == 0.  jobs[0..2] = Y, Cr, Cb: blocks = the ZIGZAG_I16 coefficient output
+ *  (nblk = (H/8)(W/8), (H/16)(W/16), (H/16)(W/16)), dc_diff, sym_len / sym_val /
+ *  sym_cap / d_count as hic_rle_encode_i16; d_stitch must be NULL (whole images);
+ *  records_per_tile is ignored; workspace: hic_rle_workspace_bytes(nblk, 64) bytes,
+ *  zero-filled before its first use (it carries tagged look-back granules and the
+ *  launch's unit tickets), reusable after, one launch at a time per workspace.
+ *  ev_start / ev_stop (optional): the launch's own begin / end timestamps. */
+int hic_encode420_rle_u8(const uint8_t *rgb, int64_t H, int64_t W, const hic_rle_job16 *jobs, int max_len,
+                         void *stream, void *ev_start, void *ev_stop);
 /* hic_rle_shard_summary_i16 from the tile records of hic_dct_quant_rle_u8. */
 int hic_rle_shard_summary_tiles(const int16_t *blocks, int64_t nblk, void *workspace, int64_t *d_summary,
                                 void *stream);

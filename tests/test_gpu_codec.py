@@ -389,7 +389,7 @@ def test_fused_encoder_matches_two_kernel_chain(kind, H, W, enc_dct, chain_path)
     records are 32-block half tiles)."""
     rgb = _structured_rgb(kind, H, W, H + W)
     x = device.to_device(rgb)
-    got, exp = pipeline.Encoder(H, W, fused=True), pipeline.Encoder(H, W, fused=False)
+    got, exp = pipeline.Encoder(H, W, fused=True, onepass=False), pipeline.Encoder(H, W, fused=False)
     with _lib.knobs(encode_dct=enc_dct):
         got.encode(x)
     with _lib.knobs(dct_path=chain_path):
@@ -411,6 +411,72 @@ def test_fused_encoder_ragged_matches_chain(kind, H, W, enc_dct):
     last lane) and its tile records come from a tile pass -- symbols, DC and shard
     summaries equal the two-kernel chain's."""
     test_fused_encoder_matches_two_kernel_chain(kind, H, W, enc_dct, _lib.DCT_PATH_MFMA)
+
+
+@pytest.mark.parametrize("max_len", [15, 0])
+@pytest.mark.parametrize("kind", ["random", "levels", "colour_levels", "blocks", "flat", "sparse", "zeros"])
+@pytest.mark.parametrize("H,W", [(16, 512), (32, 1024), (144, 2048), (1088, 1536), (400, 512)])
+def test_onepass_matches_chain(kind, H, W, max_len):
+    """hic_encode420_rle_u8 (transform + DC DPCM + AC RLE in one kernel, stream
+    offsets by look-back) == the fused transform + the scan / emit launches:
+    coefficients, DC differences, both symbol arrays and the counts, for dense
+    blocks, exact-tie images, constant blocks, long carried zero runs (flat, sparse:
+    a few nonzeros far apart; zeros: an all-black image, one EOB per plane) and
+    max_len 0 (no fillers).  Two images back to back on the same encoder (the ticket
+    counter resets, the look-back granules of the first launch never match)."""
+    rng = np.random.default_rng(H * 3 + W)
+    if kind == "sparse":
+        rgb = np.full((H, W, 3), 128, np.uint8)
+        for _ in range(5):
+            rgb[rng.integers(0, H), rng.integers(0, W)] = rng.integers(0, 256, 3)
+    elif kind == "zeros":
+        rgb = np.zeros((H, W, 3), np.uint8)
+    else:
+        rgb = _structured_rgb(kind, H, W, H + W)
+    rgb2 = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    got = pipeline.Encoder(H, W, max_len=max_len)
+    exp = pipeline.Encoder(H, W, max_len=max_len, fused=True, onepass=False)
+    assert got.onepass and not exp.onepass
+    for img in (rgb, rgb2, rgb):
+        x = device.to_device(img)
+        got.encode(x)
+        exp.encode(x)
+        a, b = got.result(), exp.result()
+        for k in pipeline.CHANNELS:
+            for j, what in enumerate(("coef", "dc", "sym_len", "sym_val")):
+                np.testing.assert_array_equal(a[k][j], b[k][j], err_msg="%s %s" % (k, what))
+        np.testing.assert_array_equal(got.counts.cpu().numpy(), exp.counts.cpu().numpy())
+
+
+def test_onepass_streams_and_small_cap():
+    """Four one-pass encoders on two streams at once (their look-backs and tickets
+    independent) equal the single-stream results; a symbol buffer one short reports
+    -(needed) and writes nothing past its end."""
+    H, W = 1088, 2048
+    rng = np.random.default_rng(5)
+    imgs = [device.to_device(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)) for _ in range(4)]
+    encs = [pipeline.Encoder(H, W) for _ in range(4)]
+    ss = [torch.cuda.Stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+    for i, e in enumerate(encs):
+        e.encode(imgs[i], stream=ss[i % 2])
+    torch.cuda.synchronize()
+    for i, e in enumerate(encs):
+        ref = pipeline.Encoder(H, W, fused=True, onepass=False)
+        ref.encode(imgs[i])
+        a, b = e.result(), ref.result()
+        for k in pipeline.CHANNELS:
+            for j in range(4):
+                np.testing.assert_array_equal(a[k][j], b[k][j], err_msg="%d %s %d" % (i, k, j))
+    # a symbol buffer one short of the luma count
+    e = encs[0]
+    need = int(e.counts[0].item())
+    e.cap["lum"] = need - 1
+    e.sym_len["lum"].fill_(0xAB)
+    e.encode(imgs[0])
+    torch.cuda.synchronize()
+    assert int(e.counts[0].item()) == -need
+    assert int(e.sym_len["lum"][need - 1].item()) == 0xAB
 
 
 @pytest.mark.timeout(900)

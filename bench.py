@@ -83,6 +83,9 @@ def parse():
                     help="HIP streams the consecutive images alternate over (each image's chain stays on one); "
                          "default 4 on one GPU (0.1020-0.1028 vs 0.1025-0.1037 ms/step for 2 in 3 alternating "
                          "pairs, profiles/r03/s2/streams/), 2 with N > 1 ranks")
+    ap.add_argument("--onepass", action="store_true",
+                    help="single GPU: the one-pass encode kernel (hic_encode420_rle_u8) instead of the fused "
+                         "transform + scan / emit launches (measured slower; DESIGN.md section 5)")
     ap.add_argument("--unfused", action="store_true",
                     help="A/B: colour and DCT as two kernels (the planes round-trip HBM) instead of hic_encode420_u8")
     ap.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
@@ -723,7 +726,8 @@ def main():
                                                fused=False if args.unfused else None)
     else:
         H = H0
-        make = lambda j: pipeline.Encoder(H0, W0, fused=False if args.unfused else None)  # noqa: E731
+        make = lambda j: pipeline.Encoder(H0, W0, fused=False if args.unfused else None,  # noqa: E731
+                                          onepass=True if args.onepass else None)
     encs = [make(j) for j in range(n_enc)]  # rotate outputs too (~1.2 GB per 4)
     span = encs[0].span if world > 1 else (0, H)
     in_rows = span[1] - span[0]

@@ -63,6 +63,7 @@ struct Enc420 {
   int64_t cap[3];
   int64_t *d_count[3];
   uint64_t *gran[3];  // look-back granules, 8 per record (onepass.h)
+  uint64_t *gwin[3];  // and 4 per window (unit row)
   int last_rec[3];    // the plane's last record (it closes the stream)
   int64_t n_ac[3];    // the plane's AC stream length
   uint32_t *ticket;   // unit tickets (reset by the wave that takes the last one)
@@ -381,67 +382,89 @@ struct EncColour {
   }
 };
 
-// One-pass: the record of the pass in the stage (rows = this lane's block; SEG:
-// lanes 0-31 Cr record `rec`, 32-63 Cb record `rec`, else the Y record `rec`):
-// publish its aggregate, look back, publish the inclusive prefix, DC differences,
-// symbols, and (the plane's last record) the stream's EOB and count.  b: this lane's
-// block in its plane.
+// One-pass: a pass's record (lane = block; SEG: lanes 0-31 Cr record `rec`, 32-63 Cb
+// record `rec`, else the Y record `rec`) in two steps.  op_publish summarises the
+// lane's block (zw: its zig-zag words) and publishes the record's aggregate;
+// op_finish looks back, publishes the inclusive prefix, writes the DC differences
+// and emits the symbols (blk: the block in the LDS stage, for lane-varying reads),
+// and the plane's last record closes its stream.  A unit publishes BOTH Y records
+// before it looks back: a Y tile's predecessors include the row above's second Y
+// tiles of later units, whose aggregates must not wait on their own look-backs (that
+// chains the look-backs row after row down the image).  b: this lane's block.
+struct OpRec {
+  int first, last, nsym, dc, lastdc;
+  uint64_t ac;
+  Agg32 A;
+};
 template <int TMF, bool SEG>
-__device__ __forceinline__ void op_pass(const Enc420 &E, const uint2 *st2, uint8_t *s_len, int16_t *s_val, int rec,
-                                        int64_t b) {
+__device__ __forceinline__ OpRec op_publish(const Enc420 &E, const uint32_t (&zw)[32], int rec, int64_t b) {
   const int lane = fresh_lane(), sl = SEG ? lane & 31 : lane, seg0 = SEG ? lane & 32 : 0;
   const int p = SEG ? 1 + (lane >> 5) : 0;
   const int M = E.M;
-  uint32_t zw[32];
-  enc_stage_row(st2, lane, zw);
-  const int16_t *blk = reinterpret_cast<const int16_t *>(st2 + lane * kStageU2);
-  int first = -1, last = -1, nsym = 0;
-  uint64_t ac = 0;
-  summarize16<TMF>(zw, M, first, last, nsym, &ac);
+  OpRec R;
+  R.first = -1;
+  R.last = -1;
+  R.nsym = 0;
+  R.ac = 0;
+  summarize16<TMF>(zw, M, R.first, R.last, R.nsym, &R.ac);
   // the record's aggregate (tile_record16_half's fields, as stream positions)
-  const int lastr = last >= 0 ? sl * 63 + last : -1;
+  const int lastr = R.last >= 0 ? sl * 63 + R.last : -1;
   const int incl = SEG ? seg32_incl_max_i32(lastr) : wave_incl_max_i32(lastr);
   int prevr = wave_shr1_i32(-1, incl);
   if (sl == 0) prevr = -1;
-  int c = nsym;
-  if (first >= 0 && prevr >= 0) c += syms_for_run(sl * 63 + first - prevr - 1, M);
+  int c = R.nsym;
+  if (R.first >= 0 && prevr >= 0) c += syms_for_run(sl * 63 + R.first - prevr - 1, M);
   const int ic = SEG ? seg32_incl_sum_i32(c) : wave_incl_sum_i32(c);
   const int segL = seg0 + (SEG ? 31 : 63);
   const int all_last = __shfl(incl, segL), tot = __shfl(ic, segL);
-  const uint64_t fm = __builtin_amdgcn_ballot_w64(first >= 0);
+  const uint64_t fm = __builtin_amdgcn_ballot_w64(R.first >= 0);
   const uint64_t fmh = SEG ? (fm >> seg0) & 0xFFFFFFFFull : fm;
   const int fl = fmh ? __builtin_ctzll(fmh) : 0;
-  const int ff = __shfl(sl * 63 + first, seg0 + fl);
+  const int ff = __shfl(sl * 63 + R.first, seg0 + fl);
   const int base = (int)((b - sl) * 63);  // stream position of the record's first AC
-  const Agg32 A = all_last < 0 ? Agg32{-1, -1, 0} : Agg32{base + ff, base + all_last, tot};
-  const int dc = (int)(int16_t)(zw[0] & 0xFFFFu);
-  const int lastdc = __shfl(dc, segL);
+  R.A = all_last < 0 ? Agg32{-1, -1, 0} : Agg32{base + ff, base + all_last, tot};
+  R.dc = (int)(int16_t)(zw[0] & 0xFFFFu);
+  R.lastdc = __shfl(R.dc, segL);
+  if (sl < 4)
+    op_put(E.gran[p] + 8 * (int64_t)rec + sl,
+           sl == 0 ? R.A.first : sl == 1 ? R.A.last : sl == 2 ? R.A.cnt : R.lastdc, (E.epoch << 2) | 1u);
+  return R;
+}
+
+template <int TMF, bool SEG>
+__device__ __forceinline__ void op_finish(const Enc420 &E, const OpRec &R, const uint32_t (&zw)[32],
+                                          const int16_t *blk, uint8_t *s_len, int16_t *s_val, int rec, int64_t b,
+                                          int u, int o) {
+  const int lane = fresh_lane(), sl = SEG ? lane & 31 : lane;
+  const int p = SEG ? 1 + (lane >> 5) : 0;
+  const int M = E.M;
   uint64_t *g = E.gran[p];
   const uint32_t tagA = (E.epoch << 2) | 1u, tagP = (E.epoch << 2) | 2u;
-  auto put4 = [&](const Agg32 &a, int off, uint32_t tag) {
-    if (sl < 4) op_put(g + 8 * (int64_t)rec + off + sl, sl == 0 ? a.first : sl == 1 ? a.last : sl == 2 ? a.cnt : lastdc,
-                       tag);
-  };
-  put4(A, 0, tagA);
-  Agg32 ex;
-  int pdc;
-  const bool ok = op_lookback<SEG>(g, rec, tagA, tagP, M, ex, pdc);
-  const Agg32 P = agg32(ex, A, M);
-  put4(P, 4, tagP);
+  Agg32 ex{-1, -1, 0};
+  int pdc = 0;
+#if defined(HIC_DEV) && defined(HIC_OP_NOWAIT)
+  const bool ok = true;  // dev timing (results invalid): no look-back
+#else
+  const bool ok = op_lookback<SEG>(g, E.gwin[p], u, o, E.nstrips, !SEG, tagA, tagP, (E.epoch << 2) | 3u, M, ex, pdc);
+#endif
+  const Agg32 P = agg32(ex, R.A, M);
+  if (sl < 4) op_put(g + 8 * (int64_t)rec + 4 + sl, sl == 0 ? P.first : sl == 1 ? P.last : sl == 2 ? P.cnt : R.lastdc, tagP);
   // DC differences (codec.differential_coding): the record's first block takes the
   // previous record's last DC (0 before the plane's first block)
-  int pd = __shfl_up(dc, 1, 64);
+  int pd = __shfl_up(R.dc, 1, 64);
   if (sl == 0) pd = pdc;
-  E.dc[p][b] = dc - pd;
+  E.dc[p][b] = R.dc - pd;
   // the record's first symbol and the last nonzero before it (no carry: p0 = -1)
   const int64_t o_seg = ex.last >= 0 ? (int64_t)ex.cnt + syms_for_run(ex.first, M) : 0;
   const int64_t prev_seg = ex.last >= 0 ? ex.last : -1;
+#if !(defined(HIC_DEV) && defined(HIC_OP_NOEMIT))  // dev timing (results invalid): no symbol emission
   if (SEG)
-    op_emit<TMF, true>(zw, blk, b * 63, M, o_seg, prev_seg, first, last, nsym, ac, s_len, s_val, E.sym_len[1],
-                       E.sym_val[1], E.cap[1], E.sym_len[2], E.sym_val[2], E.cap[2]);
+    op_emit<TMF, true>(zw, blk, b * 63, M, o_seg, prev_seg, R.first, R.last, R.nsym, R.ac, s_len, s_val,
+                       E.sym_len[1], E.sym_val[1], E.cap[1], E.sym_len[2], E.sym_val[2], E.cap[2]);
   else
-    op_emit<TMF, false>(zw, blk, b * 63, M, o_seg, prev_seg, first, last, nsym, ac, s_len, s_val, E.sym_len[0],
-                        E.sym_val[0], E.cap[0], E.sym_len[0], E.sym_val[0], E.cap[0]);
+    op_emit<TMF, false>(zw, blk, b * 63, M, o_seg, prev_seg, R.first, R.last, R.nsym, R.ac, s_len, s_val,
+                        E.sym_len[0], E.sym_val[0], E.cap[0], E.sym_len[0], E.sym_val[0], E.cap[0]);
+#endif
   if (!ok && sl == 0) {
     op_put(E.fail, 1, (E.epoch << 2) | 3u);
     __hip_atomic_store(E.d_count[p], (int64_t)HIC_COUNT_SCAN_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -461,6 +484,13 @@ __device__ __forceinline__ void op_pass(const Enc420 &E, const uint2 *st2, uint8
     if ((uint32_t)(op_get(E.fail) >> 32) == ((E.epoch << 2) | 3u))
       __hip_atomic_store(E.d_count[p], (int64_t)HIC_COUNT_SCAN_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+
+// the lane's stage row <- zw (a Y tile's words back into the stage for its emission)
+__device__ __forceinline__ void enc_row_to_stage(uint2 *st2, int lane, const uint32_t (&zw)[32]) {
+  uint2 *row = st2 + lane * kStageU2;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) row[k] = make_uint2(zw[2 * k], zw[2 * k + 1]);
 }
 
 // One wave per unit, 3 waves per SIMD (<= 168 VGPRs): all 19 colour rows first, so
@@ -507,6 +537,8 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
   const int nbx = E.W >> 3, nbxc = E.W >> 4;
 
   uint2 yq[16];
+  uint32_t zw1[32], zw2[32];  // OP: the two Y tiles' words until their emission
+  OpRec R1{}, R2{}, Rc{};
   i32x4 A[4][4];  // MFMA matrix digits of the pass's table (loaded after the colour rows)
   // Y block row br: blocks 64 s .. 64 s + 63 of block row 2 u0 + br (one RLE tile),
   // from yq slots 8 br .. 8 br + 7.  MFMA: the lane's block rows go through the stage
@@ -521,8 +553,10 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
     int16_t *o = E.coef[0] + b0 * 64;
     enc_store(st2, fresh_lane(), o, o + 32 * 64, nb < 32 ? nb : 32, nb > 32 ? nb - 32 : 0);
     if (OP) {
-      op_pass<TMF, false>(E, st2, s_oplen[OP ? wv : 0], s_opval[OP ? wv : 0], (2 * u0 + br) * E.nstrips + s,
-                          b0 + fresh_lane());
+      // the tile's words stay in registers (zw1 / zw2) until both Y records are out
+      uint32_t(&zw)[32] = br == 0 ? zw1 : zw2;
+      enc_stage_row(st2, fresh_lane(), zw);
+      (br == 0 ? R1 : R2) = op_publish<TMF, false>(E, zw, (2 * u0 + br) * E.nstrips + s, b0 + fresh_lane());
     } else if (TMF >= 0 && E.rec[0]) {
       uint32_t zw[32];
       enc_stage_row(st2, fresh_lane(), zw);
@@ -569,8 +603,12 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
     __builtin_amdgcn_wave_barrier();
     enc_store(st2, fresh_lane(), E.coef[1] + b0 * 64, E.coef[2] + b0 * 64, nb >> 1, nb >> 1);
     if (OP) {
-      op_pass<TMF, true>(E, st2, s_oplen[OP ? wv : 0], s_opval[OP ? wv : 0], u0 * E.nstrips + s,
-                         b0 + (fresh_lane() & 31));
+      // every record of the unit published before any look-back; the chroma
+      // coefficients stay in the stage for their emission
+      uint32_t zw[32];
+      const int l = fresh_lane();
+      enc_stage_row(st2, l, zw);
+      Rc = op_publish<TMF, true>(E, zw, u0 * E.nstrips + s, b0 + (l & 31));
     } else if (TMF >= 0 && E.rec[1]) {
       uint32_t zw[32];
       enc_stage_row(st2, fresh_lane(), zw);
@@ -626,6 +664,39 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
   const bool redo1 = y_blocks(1);
   if (MFMA) mfma_load_A(1, lane, A);
   const bool redoc = c_blocks();
+  if (OP) {  // the unit's three records published: look back and emit, chroma first
+    if (s == E.nstrips - 1) {  // the row's last unit: its windows' aggregates first
+      const uint32_t tagA = (E.epoch << 2) | 1u, tagW = (E.epoch << 2) | 3u;
+      const bool okw = op_publish_wa<false>(E.gran[0], E.gwin[0], u0, E.nstrips, true, tagA, tagW, E.M, R2.A, R2.lastdc) &
+                       op_publish_wa<true>(E.gran[1 + (fresh_lane() >> 5)], E.gwin[1 + (fresh_lane() >> 5)], u0,
+                                           E.nstrips, false, tagA, tagW, E.M, Rc.A, Rc.lastdc);
+      if (!okw && fresh_lane() == 0) {
+        op_put(E.fail, 1, (E.epoch << 2) | 3u);
+        for (int p = 0; p < 3; ++p)
+          __hip_atomic_store(E.d_count[p], (int64_t)HIC_COUNT_SCAN_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    const int l = fresh_lane();
+    const int16_t *blk = reinterpret_cast<const int16_t *>(st2 + l * kStageU2);
+    {
+      uint32_t zw[32];
+      enc_stage_row(st2, l, zw);
+      op_finish<TMF, true>(E, Rc, zw, blk, s_oplen[OP ? wv : 0], s_opval[OP ? wv : 0], u0 * E.nstrips + s,
+                           (int64_t)u0 * (nbx >> 1) + 32 * s + (l & 31), u0, s);
+    }
+    __builtin_amdgcn_wave_barrier();
+    enc_row_to_stage(st2, l, zw1);
+    __builtin_amdgcn_wave_barrier();
+    const int64_t by = (int64_t)(2 * u0) * nbx + 64 * s + l;
+    op_finish<TMF, false>(E, R1, zw1, blk, s_oplen[OP ? wv : 0], s_opval[OP ? wv : 0], (2 * u0) * E.nstrips + s, by,
+                          u0, s);
+    __builtin_amdgcn_wave_barrier();
+    enc_row_to_stage(st2, l, zw2);
+    __builtin_amdgcn_wave_barrier();
+    op_finish<TMF, false>(E, R2, zw2, blk, s_oplen[OP ? wv : 0], s_opval[OP ? wv : 0], (2 * u0 + 1) * E.nstrips + s,
+                          by + nbx, u0, E.nstrips + s);
+    __builtin_amdgcn_wave_barrier();
+  }
   if (MFMA) {  // flagged passes, on the float64 AAN path (~3 % of passes on random data)
     if (redo0 || redo1) {
       uint2 w[8];
@@ -716,11 +787,11 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
 extern "C" int hic_encode420_rle_u8(const uint8_t *rgb, int64_t H, int64_t W, const hic_rle_job16 *jobs, int max_len,
                                     void *stream, void *ev_start, void *ev_stop) {
   if (!rgb || !jobs) return arg_error("null pointer");
-  if (H < 16 || W < 512 || H % 16 || W % 512 || H >= (1 << 20) || W >= (1 << 20))
-    return arg_error("hic_encode420_rle_u8 needs W %% 512 == 0 and H %% 16 == 0");
+  if (H < 16 || W < 512 || H % 16 || W % 512 || H >= (1 << 20) || W > 16384)
+    return arg_error("hic_encode420_rle_u8 needs W %% 512 == 0, W <= 16384 and H %% 16 == 0");
   if (reinterpret_cast<uintptr_t>(rgb) % 8) return arg_error("rgb must be 8-byte aligned");
   if (H * W * 3 > INT32_MAX) return arg_error("hic_encode420_rle_u8: image exceeds 2 GiB (use the chain)");
-  if (max_len < 0 || max_len > 256) return arg_error("max_len");
+  if (max_len < 1 || max_len > 256) return arg_error("max_len must be in [1, 256] for uint8 symbol lengths");
   const int64_t nblk[3] = {(H / 8) * (W / 8), (H / 16) * (W / 16), (H / 16) * (W / 16)};
   if (nblk[0] > (int64_t)INT32_MAX / 63) return arg_error("nblk too large (AC stream >= 2^31)");
   Enc420 E{};
@@ -752,9 +823,10 @@ extern "C" int hic_encode420_rle_u8(const uint8_t *rgb, int64_t H, int64_t W, co
     E.sym_val[k] = J.sym_val;
     E.cap[k] = J.sym_cap;
     E.d_count[k] = J.d_count;
-    E.gran[k] = static_cast<uint64_t *>(J.workspace);
     E.last_rec[k] = k == 0 ? (int)(2 * (H / 16) * E.nstrips - 1) : (int)((H / 16) * E.nstrips - 1);
     E.n_ac[k] = nblk[k] * 63;
+    E.gran[k] = static_cast<uint64_t *>(J.workspace);
+    E.gwin[k] = E.gran[k] + 8 * (int64_t)(E.last_rec[k] + 1);  // past the record granules
   }
   // the ticket counter and the timeout word: the last words of Y's workspace
   // (hic_rle_workspace_bytes; past the granules and the chain scan's hand-off)

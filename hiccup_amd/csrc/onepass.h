@@ -49,83 +49,164 @@ __device__ __forceinline__ Agg32 agg32(const Agg32 &A, const Agg32 &B, int M) {
 
 constexpr int kOpSpin = 1 << 22;  // look-back polls before a launch reports a timeout
 
-// Exclusive aggregate of record `rec` of this lane's plane (granules g) and the DC
-// of record rec - 1's last block (0 for rec 0).  SEG: lanes 0-31 and 32-63 look
-// back in two planes at once (rec uniform per half).  Returns false on a timeout.
-template <bool SEG>
-__device__ __forceinline__ bool op_lookback(const uint64_t *g, int rec, uint32_t tagA, uint32_t tagP, int M,
-                                            Agg32 &excl, int &prevdc) {
-  constexpr int S = SEG ? 32 : 64;
-  const int lane = threadIdx.x & 63, sl = lane & (S - 1), hf = SEG ? lane >> 5 : 0;
-  Agg32 acc{-1, -1, 0};
-  int pdc = 0;
-  bool ok = true, first_win = true;
-  int q = rec - 1;  // newest record of this segment's window
-  bool done = q < 0;
-  while (__builtin_amdgcn_ballot_w64(!done) != 0) {
-    const int idx = q - sl;
-    Agg32 v{-1, -1, 0};
-    int dcv = 0, lp = S;
-    for (int spin = 0;; ++spin) {
-      // records before the stream (and finished segments) read as the empty prefix
-      int st = 2;
-      v = Agg32{-1, -1, 0};
-      dcv = 0;
-      if (!done && idx >= 0) {
-        const uint64_t *r = g + 8 * (int64_t)idx;
-        uint64_t w[8];
+// spin-wait helper: back off, a wave far ahead of the published prefixes polls less
+__device__ __forceinline__ void op_backoff(int spin) {
+  if (spin < 4)
+    __builtin_amdgcn_s_sleep(4);
+  else if (spin < 32)
+    __builtin_amdgcn_s_sleep(16);
+  else
+    __builtin_amdgcn_s_sleep(64);
+}
+
+// fold of lanes sl = 0 .. S-1 of a segment (lane sl holds the sl-th item counting
+// back from the newest; lanes past the wanted ones hold the empty aggregate): the
+// segment's items folded in stream order, in every lane of the segment
+template <int S>
+__device__ __forceinline__ Agg32 op_fold(Agg32 v, int sl, int M) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) w[k] = op_get(r + k);
-        auto tags = [&](int k0, uint32_t t) {
-          return ((uint32_t)(w[k0] >> 32) == t) & ((uint32_t)(w[k0 + 1] >> 32) == t) &
-                 ((uint32_t)(w[k0 + 2] >> 32) == t) & ((uint32_t)(w[k0 + 3] >> 32) == t);
-        };
-        if (tags(4, tagP)) {
-          st = 2;
-          v = Agg32{(int)(uint32_t)w[4], (int)(uint32_t)w[5], (int)(uint32_t)w[6]};
-          dcv = (int)(uint32_t)w[7];
-        } else if (tags(0, tagA)) {
-          st = 1;
-          v = Agg32{(int)(uint32_t)w[0], (int)(uint32_t)w[1], (int)(uint32_t)w[2]};
-          dcv = (int)(uint32_t)w[3];
-        } else {
-          st = 0;
-        }
-      }
-      const uint64_t pm = __builtin_amdgcn_ballot_w64(st == 2);
-      if (SEG) {
-        const uint32_t ph = (uint32_t)(pm >> (32 * hf));
-        lp = ph ? __builtin_ctz(ph) : 32;
-      } else {
-        lp = pm ? __builtin_ctzll(pm) : 64;
-      }
-      if (__builtin_amdgcn_ballot_w64(st == 0 && sl < lp) == 0) break;
-      if (spin >= kOpSpin) {
-        ok = false;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
+  for (int d = 1; d < S; d <<= 1) {
+    const Agg32 o{__shfl_down(v.first, d, S), __shfl_down(v.last, d, S), __shfl_down(v.cnt, d, S)};
+    if ((sl & (2 * d - 1)) == 0) v = agg32(o, v, M);
+  }
+  return Agg32{__shfl(v.first, 0, S), __shfl(v.last, 0, S), __shfl(v.cnt, 0, S)};
+}
+
+// granule group {value0..3} with tag t at r (4 words): all four tags must match
+__device__ __forceinline__ bool op_read4(const uint64_t *r, uint32_t t, Agg32 &v, int &dc) {
+  uint64_t w[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) w[k] = op_get(r + k);
+  const bool ok = ((uint32_t)(w[0] >> 32) == t) & ((uint32_t)(w[1] >> 32) == t) & ((uint32_t)(w[2] >> 32) == t) &
+                  ((uint32_t)(w[3] >> 32) == t);
+  if (ok) {
+    v = Agg32{(int)(uint32_t)w[0], (int)(uint32_t)w[1], (int)(uint32_t)w[2]};
+    dc = (int)(uint32_t)w[3];
+  }
+  return ok;
+}
+
+// nearest lane of this segment (32 lanes if SEG) with `has` (S if none)
+template <bool SEG>
+__device__ __forceinline__ int op_nearest(bool has) {
+  const uint64_t m = __builtin_amdgcn_ballot_w64(has);
+  if (SEG) {
+    const uint32_t h = (uint32_t)(m >> ((threadIdx.x & 63) & 32));
+    return h ? __builtin_ctz(h) : 32;
+  }
+  return m ? __builtin_ctzll(m) : 64;
+}
+
+// The look-back windows are the image's unit rows: window u holds the records of
+// unit row u in stream order -- Y: rows 2u and 2u + 1 of the plane's tiles (2 ns
+// records, offsets 0 .. ns - 1 and ns .. 2 ns - 1), Cr / Cb: ns half tiles.  All
+// records of a window belong to the ns units of one unit row, which start together;
+// the row's last unit publishes the window's aggregate WA as soon as its row-mates'
+// aggregates are out, BEFORE any look-back of its own (published from inside its
+// look-back, WA waited on that unit's earlier emissions and chained the rows: 3.1 ms
+// per 8K image).
+__device__ __forceinline__ int op_rec(int u, int o, int ns, bool luma) {
+  return luma ? (o < ns ? 2 * u * ns + o : (2 * u + 1) * ns + o - ns) : u * ns + o;
+}
+
+// WA of window u (this lane's plane), by the unit holding its last record (mine,
+// mydc: that record's aggregate and last DC): the window-mates' aggregates, folded.
+// Returns false on a timeout.
+template <bool SEG>
+__device__ __forceinline__ bool op_publish_wa(const uint64_t *g, uint64_t *gw, int u, int ns, bool luma,
+                                              uint32_t tagA, uint32_t tagW, int M, const Agg32 &mine, int mydc) {
+  constexpr int S = SEG ? 32 : 64;
+  const int lane = threadIdx.x & 63, sl = lane & (S - 1);
+  const int o = (luma ? 2 * ns : ns) - 1;  // the last record's offset
+  Agg32 va{-1, -1, 0};
+  int dca = 0;
+  bool ha = !(sl < o);
+  for (int spin = 0;; ++spin) {
+    if (!ha) ha = op_read4(g + 8 * (int64_t)op_rec(u, o - 1 - sl, ns, luma), tagA, va, dca);
+    if (__builtin_amdgcn_ballot_w64(!ha) == 0) break;
+    if (spin >= kOpSpin) return false;
+    op_backoff(spin);
+  }
+  const Agg32 wa = agg32(op_fold<S>(va, sl, M), mine, M);
+  if (sl < 4) op_put(gw + 4 * (int64_t)u + sl, sl == 0 ? wa.first : sl == 1 ? wa.last : sl == 2 ? wa.cnt : mydc, tagW);
+  return true;
+}
+
+// Exclusive aggregate of the record at offset o of window u (this lane's plane:
+// record granules g, window granules gw) and the DC of the record before it (0 at
+// the plane's start).  SEG: lanes 0-31 and 32-63 look back in two planes at once
+// (u, o uniform).
+//  1. the window's earlier records (one lane each, one poll when published): their
+//     nearest P ends the look-back;
+//  2. else the earlier windows (one lane each, 64 / 32 per poll): a window whose last
+//     record has P ends it, any other contributes its WA.
+// A launch's first waves reach their look-backs together, far from any P; a
+// record-by-record walk back cost them ~110 us per 8K image (profiles/r04/onepass).
+// Only lanes still missing their granules poll again.  Returns false on a timeout.
+template <bool SEG>
+__device__ __forceinline__ bool op_lookback(const uint64_t *g, uint64_t *gw, int u, int o, int ns, bool luma,
+                                            uint32_t tagA, uint32_t tagP, uint32_t tagW, int M, Agg32 &excl,
+                                            int &prevdc) {
+  constexpr int S = SEG ? 32 : 64;
+  const int lane = threadIdx.x & 63, sl = lane & (S - 1);
+  const int wn = luma ? 2 * ns : ns;  // records per window (<= S)
+  const Agg32 none{-1, -1, 0};
+  // ---- 1. the window's earlier records: lane sl holds offset o - 1 - sl
+  Agg32 va = none, vp = none;
+  int dca = 0, dcp = 0, lp = o;
+  bool ha = false, hp = false;
+  for (int spin = 0;; ++spin) {
+    if (sl < o && !ha) {  // a lane with the aggregate needs nothing more
+      const uint64_t *r = g + 8 * (int64_t)op_rec(u, o - 1 - sl, ns, luma);
+      if (!hp) hp = op_read4(r + 4, tagP, vp, dcp);
+      ha = op_read4(r, tagA, va, dca);
     }
-    if (!ok) break;
-    if (first_win) {  // record rec - 1 (this segment's lane 0)
-      pdc = __shfl(dcv, 0, S);
+    const int np = op_nearest<SEG>(hp && sl < o);
+    lp = np < o ? np : o;
+    // the aggregates up to the nearest P
+    if (__builtin_amdgcn_ballot_w64(!ha && sl < lp) == 0) break;
+    if (spin >= kOpSpin) return false;
+    op_backoff(spin);
+  }
+  int pdc = __shfl(ha ? dca : dcp, 0, S);  // the previous record's last DC (o > 0)
+  const Agg32 own = op_fold<S>(sl < lp ? va : (sl == lp && lp < o ? vp : none), sl, M);
+  if (lp < o) {
+    excl = own;
+    prevdc = pdc;
+    return true;
+  }
+  // ---- 2. earlier windows: lane sl holds window q - sl (its last record's P, or WA)
+  Agg32 acc = own;
+  int q = u - 1;
+  bool done = q < 0, first_win = true;
+  while (__builtin_amdgcn_ballot_w64(!done) != 0) {
+    const int iw = q - sl;
+    const bool live = !done && iw >= 0;
+    Agg32 v = none;
+    int dcv = 0, lq = S;
+    bool hw = false, hq = !live;  // hq: the window's P (windows before the stream: empty)
+    for (int spin = 0;; ++spin) {
+      if (live && !hq && !hw) {
+        hq = op_read4(g + 8 * (int64_t)op_rec(iw, wn - 1, ns, luma) + 4, tagP, v, dcv);
+        if (!hq) hw = op_read4(gw + 4 * (int64_t)iw, tagW, v, dcv);
+      }
+      lq = op_nearest<SEG>(hq);
+      if (__builtin_amdgcn_ballot_w64(!hq && !hw && sl < lq) == 0) break;
+      if (spin >= kOpSpin) return false;
+      op_backoff(spin);
+    }
+    if (first_win) {
+      if (o == 0) pdc = __shfl(dcv, 0, S);  // the previous window's last DC
       first_win = false;
     }
-    if (sl > lp) v = Agg32{-1, -1, 0};
-    // lane sl holds record q - sl: fold toward sl = 0, earlier records on the left
-#pragma unroll
-    for (int d = 1; d < S; d <<= 1) {
-      const Agg32 o{__shfl_down(v.first, d, S), __shfl_down(v.last, d, S), __shfl_down(v.cnt, d, S)};
-      if ((sl & (2 * d - 1)) == 0) v = agg32(o, v, M);
-    }
-    const Agg32 W{__shfl(v.first, 0, S), __shfl(v.last, 0, S), __shfl(v.cnt, 0, S)};
+    const Agg32 W = op_fold<S>(sl > lq ? none : v, sl, M);
     if (!done) acc = agg32(W, acc, M);
-    done = done || lp < S;
+    done = done || lq < S;
     q -= S;
   }
   excl = acc;
   prevdc = pdc;
-  return ok;
+  return true;
 }
 
 constexpr int kOpSyms = 2048;  // staged symbols per half pass (32 blocks hold <= 2016)

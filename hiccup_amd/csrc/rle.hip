@@ -1619,9 +1619,9 @@ extern "C" size_t hic_rle_workspace_bytes(int64_t nblk, int block_len) {
   // >= its 64-block tiles and the generic 256-block tiles)
   const int64_t n = nblk > 0 ? nblk : 1, nt = (n + kWT / 2 - 1) / (kWT / 2);
   // tile records (3), offsets (2) per tile; 3 hand-off granules per scan partition;
-  // or (hic_encode420_rle_u8) 8 look-back granules per record, then its ticket
-  // counter and timeout word
-  const int64_t chain = 5 * nt + 3 * ((nt + kScan16T - 1) / kScan16T) + 8, onepass = 8 * nt + 8;
+  // or (hic_encode420_rle_u8) 8 look-back granules per record and 4 per unit row
+  // (<= one per record), then its ticket counter and timeout word
+  const int64_t chain = 5 * nt + 3 * ((nt + kScan16T - 1) / kScan16T) + 8, onepass = 12 * nt + 16;
   return (size_t)(chain > onepass ? chain : onepass) * sizeof(int64_t);
 }
 

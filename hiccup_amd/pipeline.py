@@ -61,8 +61,10 @@ def check_count(c, channel=""):
     raise MemoryError("symbol buffer too small for channel %s: %d symbols needed" % (channel, -c))
 
 
-# Encoder.encode runs the one-pass kernel where it applies (whole image, W % 512 == 0)
-ONEPASS_DEFAULT = True
+# Encoder.encode's default where the one-pass kernel applies (whole image, W % 512
+# == 0): off -- exact, but 0.135 vs 0.100 ms per 8K image against the fused
+# transform + scan + emit launches on one MI355X (one-pass encode)
+ONEPASS_DEFAULT = False
 
 
 def encoder_layout(H, W, rows=None, fused=None):
@@ -102,8 +104,8 @@ class Encoder:
         fill it (their encoder_layout rpt), whatever this shape alone would pick.
         onepass: encode() as ONE kernel (hic_encode420_rle_u8: the fused transform
         with the DC / RLE emission and a look-back for the stream offsets) -- whole
-        images with W % 512 == 0 and no tile index; None = ONEPASS_DEFAULT where it
-        applies, False = transform() + entropy()."""
+        images with W % 512 == 0, W <= 16384 and no tile index; None = ONEPASS_DEFAULT where
+        it applies, False = transform() + entropy()."""
         if H < 2 or W < 2:
             raise ValueError("image must be at least 2 x 2")
         device.require_gpu()
@@ -118,8 +120,8 @@ class Encoder:
             self.fused, self.rpt = False, dict(landing_rpt)
         else:
             self.fused, self.rpt = encoder_layout(H, W, (r0, r1), fused)
-        can_1p = (not self.landing and self.fused and (r0, r1) == (0, H) and W % 512 == 0 and not self.want_index
-                  and H * W * 3 <= 2**31 - 1)
+        can_1p = (not self.landing and self.fused and (r0, r1) == (0, H) and W % 512 == 0 and W <= 16384
+                  and not self.want_index and H * W * 3 <= 2**31 - 1)
         if onepass and not can_1p:
             raise ValueError("the one-pass encode needs a whole image with W % 512 == 0 (fused), no tile index")
         self.onepass = can_1p and (ONEPASS_DEFAULT if onepass is None else bool(onepass))

@@ -413,7 +413,7 @@ def test_fused_encoder_ragged_matches_chain(kind, H, W, enc_dct):
     test_fused_encoder_matches_two_kernel_chain(kind, H, W, enc_dct, _lib.DCT_PATH_MFMA)
 
 
-@pytest.mark.parametrize("max_len", [15, 0])
+@pytest.mark.parametrize("max_len", [15, 4])
 @pytest.mark.parametrize("kind", ["random", "levels", "colour_levels", "blocks", "flat", "sparse", "zeros"])
 @pytest.mark.parametrize("H,W", [(16, 512), (32, 1024), (144, 2048), (1088, 1536), (400, 512)])
 def test_onepass_matches_chain(kind, H, W, max_len):
@@ -421,8 +421,8 @@ def test_onepass_matches_chain(kind, H, W, max_len):
     offsets by look-back) == the fused transform + the scan / emit launches:
     coefficients, DC differences, both symbol arrays and the counts, for dense
     blocks, exact-tie images, constant blocks, long carried zero runs (flat, sparse:
-    a few nonzeros far apart; zeros: an all-black image, one EOB per plane) and
-    max_len 0 (no fillers).  Two images back to back on the same encoder (the ticket
+    a few nonzeros far apart; zeros: an all-black image, one EOB per plane), with
+    max_len 15 (the M = 15 specialisation) and 4 (the generic one).  Two images back to back on the same encoder (the ticket
     counter resets, the look-back granules of the first launch never match)."""
     rng = np.random.default_rng(H * 3 + W)
     if kind == "sparse":
@@ -434,7 +434,7 @@ def test_onepass_matches_chain(kind, H, W, max_len):
     else:
         rgb = _structured_rgb(kind, H, W, H + W)
     rgb2 = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
-    got = pipeline.Encoder(H, W, max_len=max_len)
+    got = pipeline.Encoder(H, W, max_len=max_len, onepass=True)
     exp = pipeline.Encoder(H, W, max_len=max_len, fused=True, onepass=False)
     assert got.onepass and not exp.onepass
     for img in (rgb, rgb2, rgb):
@@ -455,7 +455,7 @@ def test_onepass_streams_and_small_cap():
     H, W = 1088, 2048
     rng = np.random.default_rng(5)
     imgs = [device.to_device(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)) for _ in range(4)]
-    encs = [pipeline.Encoder(H, W) for _ in range(4)]
+    encs = [pipeline.Encoder(H, W, onepass=True) for _ in range(4)]
     ss = [torch.cuda.Stream(), torch.cuda.Stream()]
     torch.cuda.synchronize()
     for i, e in enumerate(encs):
@@ -603,7 +603,7 @@ def test_two_stream_overlap_matches_single_stream():
     H, W = 1088, 1920
     rng = np.random.default_rng(11)
     imgs = [device.to_device(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)) for _ in range(3)]
-    encs = [pipeline.Encoder(H, W) for _ in range(4)]
+    encs = [pipeline.Encoder(H, W, onepass=True) for _ in range(4)]
     streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
     torch.cuda.synchronize()
     last = {}

@@ -858,6 +858,39 @@ def main():
     # in stream-gather mode the streams live on the gathering ranks
     stream_gather = gather and args.gather_kind == "stream"
 
+    # N > 1 stream gather: one more group of N copies of one full image (every rank
+    # makes the same image, encodes its row shard); each gathering rank's received
+    # whole-image streams must equal a single-GPU Encoder's of that image, bit for bit
+    verify = None
+    if stream_gather and world > 1:
+        gv = torch.Generator(device="cuda")
+        gv.manual_seed(99)
+        full = torch.randint(0, 256, (H, W0, 3), dtype=torch.uint8, device="cuda", generator=gv)
+        xs = full[span[0]:span[1]].contiguous()
+        torch.cuda.synchronize()
+        for j in range(world):
+            pending.append((j, xs, None))
+        flush()
+        torch.cuda.synchronize()
+        ref = pipeline.Encoder(H, W0)
+        ref.encode(full)
+        torch.cuda.synchronize()
+        got = encs[rank].whole
+        same = True
+        for ci, k in enumerate(pipeline.CHANNELS):
+            c = int(got.counts[ci].item())
+            same = same and c == int(ref.counts[ci].item()) and c > 0
+            same = same and torch.equal(got.sym_len[k][:c], ref.sym_len[k][:c])
+            same = same and torch.equal(got.sym_val[k][:c], ref.sym_val[k][:c])
+            same = same and torch.equal(got.dc[k], ref.dc[k]) and torch.equal(got.coef[k], ref.coef[k])
+        t = torch.tensor([1 if same else 0], dtype=torch.int64,
+                         device="cuda" if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        verify = {"received_stream_bit_exact_vs_single_gpu": bool(t.item()),
+                  "checked": "every rank's gathered image (coefficients, DC differences, both symbol arrays, "
+                             "counts) vs pipeline.Encoder on the whole image, one extra group after the timing"}
+        del full, xs, ref
+
     def counts_of(e):
         if world == 1:
             return e.counts
@@ -1017,6 +1050,7 @@ def main():
                 "xgmi_link_gbs_measured": link_gbs,
                 "without_gather": no_gather,
                 "symbols_per_image_rank0": symbols,
+                "gather_verify": verify,
                 "stream_ends_on": "the gathering rank (whole-image scan + emit)" if stream_gather else
                 ("every rank holds its slice" if world > 1 else "this GPU"),
                 "dist_backend": None if world == 1 else args.dist_backend + (" (same device)" if args.same_device

@@ -169,7 +169,7 @@ def call(name, *args):
 # A/B knobs (include/hiccup_hip.h HIC_KNOB_*): every selectable path is bit-exact
 KNOBS = {"dct_path": 0, "dct_waves_per_cu": 1, "color_tiled": 2, "color_seg": 3, "color_nt": 4, "rle_nt": 5,
          "rld_nt": 6, "rld_generic": 7, "dev": 8, "encode_waves": 9, "encode_nt": 10, "encode_dct": 11,
-         "dct_mfma": 12}
+         "dct_mfma": 12, "encode_order": 13}
 DCT_PATH_MFMA, DCT_PATH_F64, DCT_PATH_F64_NOPF, DCT_PATH_EXACT = 5, 1, 2, 0
 
 

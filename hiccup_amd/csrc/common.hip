@@ -9,7 +9,7 @@ namespace hic {
 static thread_local char g_last_error[512] = "";
 
 // hic_set_knob values (-1 = default; read by the launchers on every call)
-static int g_knobs[HIC_KNOB_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+static int g_knobs[HIC_KNOB_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 int knob(int k) {
   const int v = g_knobs[k];
   if (v >= 0) return v;
@@ -87,6 +87,7 @@ extern "C" int hic_set_knob(int k, int value) {
   if (k == HIC_KNOB_ENCODE_WAVES && value != -1 && value != 3) return hic::arg_error("encode waves: 3 only (retired)");
   if (k == HIC_KNOB_ENCODE_NT && value != -1 && value != 1) return hic::arg_error("encode_nt: 1 only (retired)");
   if (k == HIC_KNOB_DCT_MFMA && value != -1 && (value < 0 || value > 3)) return hic::arg_error("dct_mfma 0..3");
+  if (k == HIC_KNOB_ENCODE_ORDER && value != -1 && (value < 0 || value > 1)) return hic::arg_error("encode_order 0/1");
   if (k == HIC_KNOB_ENCODE_DCT && value != -1 && value != 0 && value != 1)
     return hic::arg_error("encode_dct: 0 float64 AAN, 1 integer MFMA");
   if (value < -1) return hic::arg_error("knob value %d", value);

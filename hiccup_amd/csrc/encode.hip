@@ -55,6 +55,7 @@ struct Enc420 {
   int64_t *rec[3];   // tile records: Y per 64-block tile, Cr / Cb per 32-block half tile
   int M;
   int nstrips, nunits;  // nunits: waves (one unit each)
+  int vstack;           // 1: a workgroup's waves take 4 vertically stacked units of one strip
   int wlast;            // pixel columns of the last strip (16 .. 512)
   // one-pass encode (hic_encode420_rle_u8): per plane Y, Cr, Cb
   int32_t *dc[3];
@@ -517,7 +518,7 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
   __shared__ __attribute__((aligned(16))) int16_t s_opval[OP ? HIC_ENC_WPB : 1][OP ? kOpSyms + 32 : 8];
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int g = __builtin_amdgcn_readfirstlane(blockIdx.x * HIC_ENC_WPB + wv);
-  if (g >= E.nunits) return;  // wave-uniform
+  if ((OP || !E.vstack) && g >= E.nunits) return;  // wave-uniform
   if (OP) {
     // tickets in the order waves start; the last one resets the counter for the next
     // launch (every ticket is taken by then)
@@ -529,8 +530,19 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
   uint2 *st2 = s_stage + wv * 64 * kStageU2;
   uint32_t *s_chroma = s_chroma_all[wv];
   int16_t *st = reinterpret_cast<int16_t *>(st2 + lane * kStageU2);
-  // wave g: strip s, unit row u0
-  const int u0 = __builtin_amdgcn_readfirstlane(g / E.nstrips), s = __builtin_amdgcn_readfirstlane(g - u0 * E.nstrips);
+  // wave g: strip s, unit row u0 (vstack: workgroup b = strip b % nstrips, unit rows
+  // 4 (b / nstrips) .. + 3 -- the halo rows a unit shares with the one below are
+  // fetched once into the CU's caches)
+  int u0, s;
+  if (!OP && E.vstack) {
+    const int b = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+    s = __builtin_amdgcn_readfirstlane(b % E.nstrips);
+    u0 = __builtin_amdgcn_readfirstlane((b / E.nstrips) * HIC_ENC_WPB + wv);
+    if (u0 * 16 >= E.out_rows) return;  // wave-uniform
+  } else {
+    u0 = __builtin_amdgcn_readfirstlane(g / E.nstrips);
+    s = __builtin_amdgcn_readfirstlane(g - u0 * E.nstrips);
+  }
   const int y0 = E.out_row0 + 16 * u0;
   // Y blocks of this strip's block rows (64 but in a ragged last strip)
   const int nb = __builtin_amdgcn_readfirstlane(s == E.nstrips - 1 ? E.wlast >> 3 : 64);
@@ -760,7 +772,11 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
   E.nunits = E.nstrips * (int)(out_rows / 16);  // waves
   // one wave per unit (no persistent loop: units are the same size, and the
   // hardware's dispatch balances the tail better than a fixed split)
-  const dim3 grid((unsigned)((E.nunits + HIC_ENC_WPB - 1) / HIC_ENC_WPB)), block(64 * HIC_ENC_WPB);
+  E.vstack = knob(HIC_KNOB_ENCODE_ORDER) == 1;
+  const int nu = (int)(out_rows / 16);
+  const dim3 grid((unsigned)(E.vstack ? E.nstrips * ((nu + HIC_ENC_WPB - 1) / HIC_ENC_WPB)
+                                      : (E.nunits + HIC_ENC_WPB - 1) / HIC_ENC_WPB)),
+      block(64 * HIC_ENC_WPB);
   hipStream_t s = as_stream(stream);
   hipEvent_t e0 = static_cast<hipEvent_t>(ev_start), e1 = static_cast<hipEvent_t>(ev_stop);
   auto launch = [&](auto kern) {

@@ -413,6 +413,17 @@ def test_fused_encoder_ragged_matches_chain(kind, H, W, enc_dct):
     test_fused_encoder_matches_two_kernel_chain(kind, H, W, enc_dct, _lib.DCT_PATH_MFMA)
 
 
+@pytest.mark.parametrize("order", [0, 1])
+@pytest.mark.parametrize("kind", ["random", "levels", "flat"])
+@pytest.mark.parametrize("H,W", [(16, 512), (48, 1024), (80, 2048), (272, 1536), (144, 1040), (2160, 3840)])
+def test_fused_encoder_unit_order(kind, H, W, order):
+    """knob encode_order (0: a workgroup = 4 strips side by side, 1: 4 vertically
+    stacked units of one strip, unit-row counts not a multiple of 4 and ragged last
+    strips included) == the two-kernel chain."""
+    with _lib.knobs(encode_order=order):
+        test_fused_encoder_matches_two_kernel_chain(kind, H, W, 0, _lib.DCT_PATH_F64)
+
+
 @pytest.mark.parametrize("max_len", [15, 4])
 @pytest.mark.parametrize("kind", ["random", "levels", "colour_levels", "blocks", "flat", "sparse", "zeros"])
 @pytest.mark.parametrize("H,W", [(16, 512), (32, 1024), (144, 2048), (1088, 1536), (400, 512)])

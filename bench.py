@@ -241,14 +241,14 @@ def extra_4k_rgb_encode(steps=40, n_streams=2):
     return out
 
 
-def extra_uhd_rgb_encode(steps=40, n_streams=2):
-    """3840 x 2160 (UHD: W % 512 != 0, the fused kernel's ragged last strip) full
-    encode, fused against the two-kernel chain (the default for such widths) on the
-    same inputs."""
-    out = {"workload": "3840x2160 RGB -> YCrCb 4:2:0 full encode, 1 GPU, %d streams (fused: ragged last strip, "
-                       "tile records by a tile pass; chain: colour kernel + plane DCT)" % n_streams}
-    out["fused"] = extra_rgb_encode(2160, 3840, steps, n_streams, fused=True)
-    out["two_kernel_chain"] = extra_rgb_encode(2160, 3840, steps, n_streams, fused=False)
+def extra_ragged_rgb_encode(H, W, steps=40, n_streams=2):
+    """H x W with W % 512 != 0 (the fused kernel's ragged last strip) full encode:
+    the default (fused, one RLE record per strip segment, the scan / emit walking row
+    segments) against the two-kernel chain on the same inputs."""
+    out = {"workload": "%dx%d RGB -> YCrCb 4:2:0 full encode, 1 GPU, %d streams (fused: ragged last strip, one RLE "
+                       "record per strip segment; chain: colour kernel + plane DCT)" % (W, H, n_streams)}
+    out["fused"] = extra_rgb_encode(H, W, steps, n_streams, fused=True)
+    out["two_kernel_chain"] = extra_rgb_encode(H, W, steps, n_streams, fused=False)
     return out
 
 
@@ -1091,7 +1091,9 @@ def main():
             out["value_per_copy_gbs"] = round(value / floors["device_copy_gbs"], 5)
         if not args.no_extras and world == 1:
             out["extra_configs"] = {"4k_rgb_encode": extra_4k_rgb_encode(),
-                                    "3840x2160_rgb_encode": extra_uhd_rgb_encode(),
+                                    "3840x2160_rgb_encode": extra_ragged_rgb_encode(2160, 3840),
+                                    # 1080 rows are not a multiple of 16 (the fused kernel's unit): 1088
+                                    "1920x1088_rgb_encode": extra_ragged_rgb_encode(1088, 1920),
                                     "4k_luma_dct": extra_4k_luma(
                                         floor_us=floors["luma_pattern"]["4k_luma"]["median_launch_us"]),
                                     "8k_plane_dct": extra_8k_plane_dct(),

@@ -76,6 +76,9 @@ SIGNATURES = {
                                 _vp, _vp]),
     "hic_rle_encode_i16_tiles_batch": (_int, [_int, _vp, _int, _vp]),
     "hic_encode420_rle_u8": (_int, [_vp, _i64, _i64, _vp, _int, _vp, _vp, _vp]),
+    "hic_encode420_seg_u8": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _int,
+                                    _vp, _vp, _vp]),
+    "hic_rle_encode_i16_rows_batch": (_int, [_int, _vp, _vp, _int, _vp]),
     "hic_event_create": (_int, [_vp]),
     "hic_event_destroy": (_int, [_vp]),
     "hic_event_elapsed_ms": (_int, [_vp, _vp, _vp]),

@@ -572,7 +572,9 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
     } else if (TMF >= 0 && E.rec[0]) {
       uint32_t zw[32];
       enc_stage_row(st2, fresh_lane(), zw);
-      tile_record16<TMF>(zw, true, b0 + lane, E.M, E.rec[0] + (b0 >> 6) * 3);
+      // one record per strip segment of the block row (64 blocks, or the ragged last
+      // strip's nb): record (2 u0 + br) * nstrips + s (= b0 / 64 when W % 512 == 0)
+      tile_record16<TMF>(zw, lane < nb, b0 + lane, E.M, E.rec[0] + ((2 * u0 + br) * E.nstrips + s) * 3);
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -624,7 +626,8 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
     } else if (TMF >= 0 && E.rec[1]) {
       uint32_t zw[32];
       enc_stage_row(st2, fresh_lane(), zw);
-      tile_record16_half<TMF>(zw, b0, E.M, E.rec[1] + (b0 >> 5) * 3, E.rec[2] + (b0 >> 5) * 3);
+      const int64_t rc = (int64_t)u0 * E.nstrips + s;  // = b0 / 32 when W % 512 == 0
+      tile_record16_half<TMF>(zw, b0, E.M, E.rec[1] + rc * 3, E.rec[2] + rc * 3, nb >> 1);
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -679,9 +682,10 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
   if (OP) {  // the unit's three records published: look back and emit, chroma first
     if (s == E.nstrips - 1) {  // the row's last unit: its windows' aggregates first
       const uint32_t tagA = (E.epoch << 2) | 1u, tagW = (E.epoch << 2) | 3u;
-      const bool okw = op_publish_wa<false>(E.gran[0], E.gwin[0], u0, E.nstrips, true, tagA, tagW, E.M, R2.A, R2.lastdc) &
-                       op_publish_wa<true>(E.gran[1 + (fresh_lane() >> 5)], E.gwin[1 + (fresh_lane() >> 5)], u0,
+      const bool oky = op_publish_wa<false>(E.gran[0], E.gwin[0], u0, E.nstrips, true, tagA, tagW, E.M, R2.A, R2.lastdc);
+      const bool okc = op_publish_wa<true>(E.gran[1 + (fresh_lane() >> 5)], E.gwin[1 + (fresh_lane() >> 5)], u0,
                                            E.nstrips, false, tagA, tagW, E.M, Rc.A, Rc.lastdc);
+      const bool okw = oky && okc;
       if (!okw && fresh_lane() == 0) {
         op_put(E.fail, 1, (E.epoch << 2) | 3u);
         for (int p = 0; p < 3; ++p)
@@ -729,10 +733,10 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
 
 using namespace hic;
 
-extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, int64_t H, int64_t W,
-                                int64_t out_row0, int64_t out_rows, int16_t *coef_y, int16_t *coef_cr,
-                                int16_t *coef_cb, void *ws_y, void *ws_cr, void *ws_cb, int max_len, void *stream,
-                                void *ev_start, void *ev_stop) {
+static int encode420(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, int64_t H, int64_t W,
+                     int64_t out_row0, int64_t out_rows, int16_t *coef_y, int16_t *coef_cr, int16_t *coef_cb,
+                     void *ws_y, void *ws_cr, void *ws_cb, int max_len, void *stream, void *ev_start, void *ev_stop,
+                     bool seg) {
   if (!rgb_rows || !coef_y || !coef_cr || !coef_cb) return arg_error("null pointer");
   if (H < 16 || W < 16 || H >= (1 << 20) || W >= (1 << 20)) return arg_error("image shape");
   if (W % 16 || H % 16) return arg_error("hic_encode420_u8 needs W %% 16 == 0 and H %% 16 == 0");
@@ -761,8 +765,9 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
   E.coef[0] = coef_y;
   E.coef[1] = coef_cr;
   E.coef[2] = coef_cb;
-  // ragged last strip: the records come from a tile pass after the launch
-  const bool aligned = W % 512 == 0;
+  // ragged last strip: the records come from a tile pass after the launch, or (seg)
+  // one per strip segment from the kernel itself
+  const bool aligned = W % 512 == 0 || seg;
   E.rec[0] = aligned ? static_cast<int64_t *>(ws_y) : nullptr;
   E.rec[1] = aligned ? static_cast<int64_t *>(ws_cr) : nullptr;
   E.rec[2] = aligned ? static_cast<int64_t *>(ws_cb) : nullptr;
@@ -791,13 +796,29 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
   else
     mfma ? launch(k_encode420<0, true, false>) : launch(k_encode420<0, false, false>);
   if (int e = check_launch("k_encode420")) return e;
-  if (recs && !aligned) {  // one record per 64-block tile, all three planes
+  if (recs && !aligned) {  // one record per 64-block tile, all three planes (not seg)
     const int64_t ny = (out_rows / 8) * (W / 8), nc = (out_rows / 16) * (W / 16);
     if (int e = rle_tile16_launch(coef_y, ny, max_len, static_cast<int64_t *>(ws_y), s)) return e;
     if (int e = rle_tile16_launch(coef_cr, nc, max_len, static_cast<int64_t *>(ws_cr), s)) return e;
     if (int e = rle_tile16_launch(coef_cb, nc, max_len, static_cast<int64_t *>(ws_cb), s)) return e;
   }
   return HIC_OK;
+}
+
+extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, int64_t H, int64_t W,
+                                int64_t out_row0, int64_t out_rows, int16_t *coef_y, int16_t *coef_cr,
+                                int16_t *coef_cb, void *ws_y, void *ws_cr, void *ws_cb, int max_len, void *stream,
+                                void *ev_start, void *ev_stop) {
+  return encode420(rgb_rows, in_row0, in_rows, H, W, out_row0, out_rows, coef_y, coef_cr, coef_cb, ws_y, ws_cr, ws_cb,
+                   max_len, stream, ev_start, ev_stop, false);
+}
+
+extern "C" int hic_encode420_seg_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, int64_t H, int64_t W,
+                                    int64_t out_row0, int64_t out_rows, int16_t *coef_y, int16_t *coef_cr,
+                                    int16_t *coef_cb, void *ws_y, void *ws_cr, void *ws_cb, int max_len, void *stream,
+                                    void *ev_start, void *ev_stop) {
+  return encode420(rgb_rows, in_row0, in_rows, H, W, out_row0, out_rows, coef_y, coef_cr, coef_cb, ws_y, ws_cr, ws_cb,
+                   max_len, stream, ev_start, ev_stop, true);
 }
 
 extern "C" int hic_encode420_rle_u8(const uint8_t *rgb, int64_t H, int64_t W, const hic_rle_job16 *jobs, int max_len,

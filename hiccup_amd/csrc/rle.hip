@@ -610,6 +610,10 @@ struct RleJob16 {
   int64_t tile0;   // first global tile index of this job
   int64_t nrec;    // records: one per 64-block tile, or one per 32-block half tile (rshift 1)
   int rshift;      // log2(records per 64-block tile)
+  // row segments (hic_rle_encode_i16_rows_batch): rows of rowb blocks, each cut into
+  // tiles of 64 blocks from the row's start, the last one shorter; 0 = plain tiles
+  int64_t rowb;
+  int64_t tpr, rpr;  // tiles and records per row
 };
 struct RleJobs16 {
   RleJob16 j[kMaxJobs];
@@ -778,25 +782,39 @@ __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
     while (k + 1 < jobs.n && gt >= jobs.j[k + 1].tile0) ++k;
     return k;
   };
+  // tile t's first block, its block count and its first record
+  auto geo = [&](const RleJob16 &J, int64_t t, int64_t &b0, int64_t &bend, int64_t &r0) {
+    if (J.rowb > 0) {
+      const int64_t row = t / J.tpr, j = t - row * J.tpr;
+      b0 = row * J.rowb + j * kWT;
+      bend = row * J.rowb + (j * kWT + kWT < J.rowb ? j * kWT + kWT : J.rowb);
+      r0 = row * J.rpr + (j << J.rshift);
+    } else {
+      b0 = t * kWT;
+      bend = b0 + kWT < J.nblk ? b0 + kWT : J.nblk;
+      r0 = t << J.rshift;
+    }
+  };
   auto fetch = [&](int64_t gt, Next &n) {
     const RleJob16 &J = jobs.j[job_of(gt)];
     const int64_t t = gt - J.tile0;
-    const int64_t b = t * kWT + lane;
+    int64_t b0, bend, r0;
+    geo(J, t, b0, bend, r0);
+    const int64_t b = b0 + lane;
 #if HIC_EMIT_COAL
     // coalesced: 16-B chunk c = 64 k + lane of the tile (block c / 8, part c % 8)
     // into w[4k .. 4k + 3]; transposed to one block per lane through LDS (to_lanes)
     {
-      const int64_t b0 = t * kWT;
       const uint4 *q = reinterpret_cast<const uint4 *>(J.blocks + b0 * 64);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const bool ok = b0 + 8 * k + (lane >> 3) < J.nblk;
+        const bool ok = b0 + 8 * k + (lane >> 3) < bend;
         const uint4 v = ok ? q[64 * k + lane] : make_uint4(0, 0, 0, 0);
         n.w[4 * k] = v.x; n.w[4 * k + 1] = v.y; n.w[4 * k + 2] = v.z; n.w[4 * k + 3] = v.w;
       }
     }
 #else
-    if (b < J.nblk) {
+    if (b < bend) {
       load_block16(J.blocks, b, n.w);
     } else {
 #pragma unroll
@@ -805,8 +823,8 @@ __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
 #endif
     // the tile's first record (a 64-block tile may carry two 32-block records)
     const int64_t *offs = J.ws + 3 * J.nrec;
-    n.off = offs[(t << J.rshift) * 2 + 0];
-    n.prev = offs[(t << J.rshift) * 2 + 1];
+    n.off = offs[r0 * 2 + 0];
+    n.prev = offs[r0 * 2 + 1];
     n.pdc = (lane == 0 && b > 0 && b <= J.nblk) ? (int)J.blocks[(b - 1) * 64] : 0;
   };
   Next cur;
@@ -816,7 +834,10 @@ __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
     Next nxt;
     if (gn < jobs.total_tiles) fetch(gn, nxt);
     const RleJob16 &J = jobs.j[job_of(g)];
-    const int64_t b = (g - J.tile0) * kWT + lane;
+    int64_t b0, bend, r0;
+    geo(J, g - J.tile0, b0, bend, r0);
+    const int64_t b = b0 + lane;
+    const bool valid = b < bend;
 #if HIC_EMIT_COAL
     {
       // transpose through the wave's symbol-value stage (free until this tile's
@@ -842,13 +863,13 @@ __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
     const int dc = (int)(int16_t)(cur.w[0] & 0xFFFFu);
     int pdc = __shfl_up(dc, 1, 64);
     if (lane == 0) pdc = cur.pdc;
-    if (b < J.nblk) {
+    if (valid) {
       if (b > 0)
         J.dc_diff[b] = dc - pdc;
       else
         J.dc_diff[b] = (J.stitch && J.stitch[2]) ? dc - (int)J.stitch[3] : dc;
     }
-    emit_tile16<MF, NT>(cur.w, J.blocks + (b < J.nblk ? b : 0) * 64, b < J.nblk, b, J.nblk, M, cur.off, cur.prev,
+    emit_tile16<MF, NT>(cur.w, J.blocks + (valid ? b : 0) * 64, valid, b, J.nblk, M, cur.off, cur.prev,
                     s_len_all[wv], s_val_all[wv], J.sym_len, J.sym_val, J.cap);
     if (gn >= jobs.total_tiles) break;
     g = gn;
@@ -1341,8 +1362,16 @@ int encode_batch16(RleJobs16 &jobs, hipStream_t s) {
   for (int k = 0; k < jobs.n; ++k) {
     // stream positions and counts travel as int32 through the scan's hand-off
     if (jobs.j[k].nblk > (int64_t)INT32_MAX / 63) return arg_error("nblk too large (AC stream >= 2^31)");
-    jobs.j[k].ntiles = ntiles16(jobs.j[k].nblk);
-    jobs.j[k].nrec = (jobs.j[k].nblk * (1 << jobs.j[k].rshift) + kWT - 1) / kWT;
+    if (jobs.j[k].rowb > 0) {  // row segments
+      const int64_t rows = jobs.j[k].nblk / jobs.j[k].rowb, seg = kWT >> jobs.j[k].rshift;
+      jobs.j[k].tpr = (jobs.j[k].rowb + kWT - 1) / kWT;
+      jobs.j[k].rpr = (jobs.j[k].rowb + seg - 1) / seg;
+      jobs.j[k].ntiles = rows * jobs.j[k].tpr;
+      jobs.j[k].nrec = rows * jobs.j[k].rpr;
+    } else {
+      jobs.j[k].ntiles = ntiles16(jobs.j[k].nblk);
+      jobs.j[k].nrec = (jobs.j[k].nblk * (1 << jobs.j[k].rshift) + kWT - 1) / kWT;
+    }
     jobs.j[k].tile0 = t0;
     t0 += jobs.j[k].ntiles;
   }
@@ -1689,6 +1718,29 @@ extern "C" int hic_rle_encode_i16_tiles_batch(int n, const hic_rle_job16 *jobs, 
       return arg_error("job %d: records_per_tile must be 1 or 2", k);
     J.j[k] = RleJob16{a.blocks, a.nblk, a.d_stitch, a.dc_diff, a.sym_len, a.sym_val, a.sym_cap, a.d_count,
                       static_cast<int64_t *>(a.workspace), 0, 0, 0, a.records_per_tile == 2 ? 1 : 0};
+  }
+  return encode_batch16(J, as_stream(stream));
+}
+
+extern "C" int hic_rle_encode_i16_rows_batch(int n, const hic_rle_job16 *jobs, const int64_t *h_row_blocks,
+                                             int max_len, void *stream) {
+  if (n < 1 || n > kMaxJobs || !jobs || !h_row_blocks) return arg_error("1 <= n <= %d jobs", kMaxJobs);
+  if (max_len < 1 || max_len > 256) return arg_error("max_len must be in [1, 256] for uint8 symbol lengths");
+  RleJobs16 J{};
+  J.n = n;
+  J.M = max_len;
+  for (int k = 0; k < n; ++k) {
+    const hic_rle_job16 &a = jobs[k];
+    if (!a.blocks || !a.dc_diff || !a.sym_len || !a.sym_val || !a.d_count || !a.workspace)
+      return arg_error("job %d: null pointer", k);
+    if (a.nblk <= 0) return arg_error("job %d: nblk", k);
+    if (reinterpret_cast<uintptr_t>(a.blocks) & 15) return arg_error("job %d: blocks must be 16-byte aligned", k);
+    if (a.records_per_tile != 0 && a.records_per_tile != 1 && a.records_per_tile != 2)
+      return arg_error("job %d: records_per_tile must be 1 or 2", k);
+    const int64_t rb = h_row_blocks[k];
+    if (rb < 1 || a.nblk % rb) return arg_error("job %d: row_blocks must divide nblk", k);
+    J.j[k] = RleJob16{a.blocks, a.nblk, a.d_stitch, a.dc_diff, a.sym_len, a.sym_val, a.sym_cap, a.d_count,
+                      static_cast<int64_t *>(a.workspace), 0, 0, 0, a.records_per_tile == 2 ? 1 : 0, rb};
   }
   return encode_batch16(J, as_stream(stream));
 }

@@ -305,13 +305,15 @@ __device__ __forceinline__ int seg32_incl_max_i32(int v) {
 // Two half-tile records at once: lanes 0-31 hold blocks b0 .. b0 + 31 of one stream
 // (record -> rec_lo), lanes 32-63 the same block indices of another stream (->
 // rec_hi); each record covers 32 blocks (a 64-block tile's two halves combine as
-// the scan's agg_combine does).  Same fields as tile_record16.
+// the scan's agg_combine does), or the first nvalid of them (a ragged row segment).
+// Same fields as tile_record16.
 template <int MF>
 __device__ __forceinline__ void tile_record16_half(const uint32_t (&w)[32], int64_t b0, int M,
-                                                   int64_t *__restrict__ rec_lo, int64_t *__restrict__ rec_hi) {
+                                                   int64_t *__restrict__ rec_lo, int64_t *__restrict__ rec_hi,
+                                                   int nvalid = 32) {
   const int lane = threadIdx.x & 63, sl = lane & 31;
   int first = -1, last = -1, nsym = 0;
-  summarize16<MF>(w, M, first, last, nsym);
+  if (sl < nvalid) summarize16<MF>(w, M, first, last, nsym);  // nvalid: blocks of each half that exist
   const int lastr = last >= 0 ? sl * 63 + last : -1;
   const int incl = seg32_incl_max_i32(lastr);
   int prev = wave_shr1_i32(-1, incl);

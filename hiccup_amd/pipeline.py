@@ -67,11 +67,13 @@ def check_count(c, channel=""):
 ONEPASS_DEFAULT = False
 
 
-def encoder_layout(H, W, rows=None, fused=None):
-    """(fused, rpt) of an Encoder of rows `rows` of an H x W image: whether it runs
-    the fused kernel (None = the measured default: W % 512 == 0 and fusable), and its
-    RLE tile records per 64-block tile per channel (the fused kernel's chroma: one
-    per 32-block half tile)."""
+def encoder_layout(H, W, rows=None, fused=None, index=False):
+    """(fused, rpt) of an Encoder of rows `rows` of an H x W image (None: the whole
+    image, its own encoder): whether it runs the fused kernel (None = the measured
+    default: fusable, and for row shards or an encoder with a tile index W % 512 ==
+    0 too), and its RLE records per 64-block tile per channel (the fused kernel's
+    chroma: one per 32-block half tile; a whole image's ragged last strip: one per
+    strip segment, see Encoder.seg)."""
     r0, r1 = rows if rows is not None else (0, H)
     a, b = input_span(H, r0, r1)
     # (hic_encode420_u8 reads the input rows through 32-bit buffer offsets)
@@ -80,8 +82,9 @@ def encoder_layout(H, W, rows=None, fused=None):
     if fused and not can_fuse:
         raise ValueError("the fused encoder needs W, H and rows multiples of 16, "
                          "and < 2 GiB of input rows")
-    f = (can_fuse and W % 512 == 0) if fused is None else bool(fused)
-    half = f and W % 512 == 0
+    seg = rows is None and not index  # a whole image's own encoder: records per strip segment
+    f = (can_fuse and (W % 512 == 0 or seg)) if fused is None else bool(fused)
+    half = f and (W % 512 == 0 or seg)
     return f, {"lum": 1, "cr": 2 if half else 1, "cb": 2 if half else 1}
 
 
@@ -119,12 +122,16 @@ class Encoder:
         if self.landing:
             self.fused, self.rpt = False, dict(landing_rpt)
         else:
-            self.fused, self.rpt = encoder_layout(H, W, (r0, r1), fused)
+            self.fused, self.rpt = encoder_layout(H, W, rows, fused, index)
         can_1p = (not self.landing and self.fused and (r0, r1) == (0, H) and W % 512 == 0 and W <= 16384
                   and not self.want_index and H * W * 3 <= 2**31 - 1)
         if onepass and not can_1p:
             raise ValueError("the one-pass encode needs a whole image with W % 512 == 0 (fused), no tile index")
         self.onepass = can_1p and (ONEPASS_DEFAULT if onepass is None else bool(onepass))
+        # a whole image's ragged last strip (W % 512 != 0): the fused kernel writes one
+        # RLE record per strip segment (hic_encode420_seg_u8) and the scan / emit walk
+        # row segments (hic_rle_encode_i16_rows_batch): no tile pass
+        self.seg = not self.landing and self.fused and rows is None and W % 512 != 0 and not self.want_index
         c0, c1 = r0 // 2, min(H // 2, r1 // 2)
         self.shapes = {"lum": (r1 - r0, W), "cr": (c1 - c0, W // 2), "cb": (c1 - c0, W // 2)}
         ys, cs = self.shapes["lum"], self.shapes["cr"]
@@ -188,7 +195,8 @@ class Encoder:
             a, b = self.input_span()
             if rgb.shape[0] * self.W * 3 > 2**31 - 1 and in_row0 <= a and in_row0 + rgb.shape[0] >= b:
                 rgb, in_row0 = rgb[a - in_row0:b - in_row0], a
-            _lib.call("hic_encode420_u8", device.ptr(rgb), in_row0, rgb.shape[0], self.H, self.W, r0, r1 - r0,
+            _lib.call("hic_encode420_seg_u8" if self.seg else "hic_encode420_u8", device.ptr(rgb), in_row0,
+                      rgb.shape[0], self.H, self.W, r0, r1 - r0,
                       *[device.ptr(self.coef[k]) for k in CHANNELS], *[device.ptr(self.ws[k]) for k in CHANNELS],
                       self.max_len, s, *ev)
             return
@@ -207,6 +215,9 @@ class Encoder:
 
     def shard_summaries(self, stream=None):
         """Per-channel {trailing zeros, has nonzero, first DC, last DC} (sharded encode)."""
+        if self.seg:
+            raise ValueError("shard summaries read 64-block tile records (a row shard's); this whole-image "
+                             "encoder keeps one per strip segment")
         s = device.stream_ptr(stream)
         for i, k in enumerate(CHANNELS):
             n = self.coef[k].shape[0]
@@ -219,7 +230,11 @@ class Encoder:
         emit launch for all three).  stitch: None or a (3, 4) int64 device tensor of
         per-channel {carry_zeros, emit_eob, has_prev_dc, prev_dc}."""
         s = device.stream_ptr(stream)
-        _lib.call("hic_rle_encode_i16_tiles_batch", 3, self._rle_jobs(stitch), self.max_len, s)
+        if self.seg:
+            rowb = (ctypes.c_int64 * 3)(self.W // 8, self.W // 16, self.W // 16)
+            _lib.call("hic_rle_encode_i16_rows_batch", 3, self._rle_jobs(stitch), rowb, self.max_len, s)
+        else:
+            _lib.call("hic_rle_encode_i16_tiles_batch", 3, self._rle_jobs(stitch), self.max_len, s)
         if self.index is not None and stitch is None:
             for k in CHANNELS:
                 _lib.call("hic_rle_tile_index_i16", device.ptr(self.coef[k]), self.coef[k].shape[0], self.rpt[k],

@@ -156,6 +156,16 @@ int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, 
                      int64_t out_row0, int64_t out_rows, int16_t *coef_y, int16_t *coef_cr, int16_t *coef_cb,
                      void *ws_y, void *ws_cr, void *ws_cb, int max_len, void *stream, void *ev_start,
                      void *ev_stop);
+/* hic_encode420_u8 with one RLE record per strip segment for any W % 16 == 0 (round
+ * 4): each block row is cut into 512-pixel strips (64 Y / 32 chroma blocks per
+ * record), the last strip's record covering what remains -- no tile pass after the
+ * launch.  Identical to hic_encode420_u8 when W % 512 == 0.  Consume the records with
+ * hic_rle_encode_i16_rows_batch (row_blocks W/8 for Y, W/16 for Cr / Cb,
+ * records_per_tile 1 / 2). */
+int hic_encode420_seg_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, int64_t H, int64_t W,
+                         int64_t out_row0, int64_t out_rows, int16_t *coef_y, int16_t *coef_cr, int16_t *coef_cb,
+                         void *ws_y, void *ws_cr, void *ws_cb, int max_len, void *stream, void *ev_start,
+                         void *ev_stop);
 /* Timing events (hipEvent_t handles) for the *_timed entry points. */
 int hic_event_create(void **h_event);
 int hic_event_destroy(void *event);
@@ -277,6 +287,13 @@ typedef struct {
                                2: one per 32 blocks (hic_encode420_u8's chroma planes) */
 } hic_rle_job16;
 int hic_rle_encode_i16_tiles_batch(int n, const hic_rle_job16 *jobs, int max_len, void *stream);
+/* The same over records per row segment (round 4; hic_encode420_seg_u8's records):
+ * job k's blocks are rows of h_row_blocks[k] blocks (dividing nblk), each row cut into
+ * tiles of 64 blocks from its start (the last one shorter) with records_per_tile
+ * records per full tile (1: per tile; 2: per 32 blocks, the last one shorter).  With
+ * h_row_blocks[k] % 64 == 0 identical to hic_rle_encode_i16_tiles_batch. */
+int hic_rle_encode_i16_rows_batch(int n, const hic_rle_job16 *jobs, const int64_t *h_row_blocks, int max_len,
+                                  void *stream);
 /* ---- one-pass encode (round 4): hic_encode420_u8 + hic_rle_encode_i16_tiles_batch
  *      of the three channels in ONE kernel -- compression.jpeg_compression's
  *      transform (compression.py:16-39) and codec.jpeg_encode's differential_coding

@@ -289,10 +289,14 @@ def test_pipeline_encoder(H, W):
     if H == 512:  # few grey levels: exact quantiser ties on the fast DCT path
         rgb = (rng.integers(0, 4, (H, W, 1)) * 85).astype(np.uint8).repeat(3, 2)
     enc = pipeline.Encoder(H, W)
-    assert enc.fused == (W % 512 == 0 and H % 16 == 0)
+    assert enc.fused == (W % 16 == 0 and H % 16 == 0)
+    assert enc.seg == (enc.fused and W % 512 != 0)
     exp = _oracle_encode(rgb)
-    variants = [enc] + ([pipeline.Encoder(H, W, fused=True)] if (W % 16 == 0 and H % 16 == 0 and not enc.fused)
-                        else [])
+    # the fused kernel with a tile pass for a ragged last strip (an encoder with a tile
+    # index) and the two-kernel chain beside the default
+    variants = [enc]
+    if enc.seg:
+        variants += [pipeline.Encoder(H, W, fused=True, index=True), pipeline.Encoder(H, W, fused=False)]
     for e in variants:
         e.encode(device.to_device(rgb))
         got_e = e.result()
@@ -398,8 +402,10 @@ def test_fused_encoder_matches_two_kernel_chain(kind, H, W, enc_dct, chain_path)
     for k in pipeline.CHANNELS:
         for j, what in enumerate(("coef", "dc", "sym_len", "sym_val")):
             np.testing.assert_array_equal(a[k][j], b[k][j], err_msg="%s %s" % (k, what))
-    # the shard summaries read the half-tile records
-    np.testing.assert_array_equal(got.shard_summaries().cpu().numpy(), exp.shard_summaries().cpu().numpy())
+    # the shard summaries read the half-tile records (a whole ragged image keeps one
+    # record per strip segment instead: no shard summaries)
+    if not got.seg:
+        np.testing.assert_array_equal(got.shard_summaries().cpu().numpy(), exp.shard_summaries().cpu().numpy())
 
 
 @pytest.mark.parametrize("enc_dct", [0, 1])
@@ -408,9 +414,22 @@ def test_fused_encoder_matches_two_kernel_chain(kind, H, W, enc_dct, chain_path)
 def test_fused_encoder_ragged_matches_chain(kind, H, W, enc_dct):
     """Widths that are not a multiple of 512: the fused kernel's last strip is
     ragged (lanes past W store nothing, the right-border pixel goes to the strip's
-    last lane) and its tile records come from a tile pass -- symbols, DC and shard
-    summaries equal the two-kernel chain's."""
+    last lane); the whole image's encoder writes one RLE record per strip segment
+    (hic_encode420_seg_u8) and the scan / emit walk row segments -- symbols and DC
+    equal the two-kernel chain's; with a tile index the records come from a tile
+    pass after the launch (hic_encode420_u8), equal too."""
     test_fused_encoder_matches_two_kernel_chain(kind, H, W, enc_dct, _lib.DCT_PATH_MFMA)
+    rgb = _structured_rgb(kind, H, W, H + W)
+    x = device.to_device(rgb)
+    got, exp = pipeline.Encoder(H, W, fused=True, index=True), pipeline.Encoder(H, W, fused=False)
+    assert not got.seg
+    with _lib.knobs(encode_dct=enc_dct):
+        got.encode(x)
+    exp.encode(x)
+    a, b = got.result(), exp.result()
+    for k in pipeline.CHANNELS:
+        for j, what in enumerate(("coef", "dc", "sym_len", "sym_val")):
+            np.testing.assert_array_equal(a[k][j], b[k][j], err_msg="%s %s" % (k, what))
 
 
 @pytest.mark.parametrize("order", [0, 1])

@@ -6,10 +6,12 @@
 // a leaf's value and restarts at the root; trailing bits that do not finish a code
 // are dropped, and a step into a missing child (a one-leaf encoding tree's empty
 // right side) raises.  The stream has no markers, so it is cut into fixed
-// subsequences of kSub bits, one per thread, decoded speculatively from their
-// nominal first bit; Huffman codes resynchronise within a few codewords, so after
-// the exit bit of subsequence i is handed to i+1 and only changed subsequences
-// re-decode (a handful of rounds), every subsequence starts on a codeword boundary.
+// subsequences of g.sub bits (kSub = 1024; with equal-length codes of L bits the
+// multiple of L at or above it, so every subsequence starts on a codeword), one
+// per thread, decoded speculatively from their nominal first bit; Huffman codes
+// resynchronise within a few codewords, so after the exit bit of subsequence i is
+// handed to i+1 and only changed subsequences re-decode (a handful of rounds,
+// checked kRoundsPerSync at a time), every subsequence starts on a codeword boundary.
 // A prefix sum over the per-subsequence symbol counts then places each one's
 // output and a second decode writes the symbols.
 //
@@ -27,9 +29,10 @@ namespace hic {
 namespace {
 
 constexpr int kLutBits = 12, kLut = 1 << kLutBits;
-constexpr int kSub = 1024;      // bits per subsequence (one thread each)
+constexpr int kSub = 1024;      // bits per subsequence (one thread each), at least
 constexpr int kDT = 256;        // threads per workgroup
 constexpr int kMaxRounds = 24;  // resynchronisation rounds before the serial chain
+constexpr int kRoundsPerSync = 4;  // rounds launched between two host reads of their flags
 constexpr int64_t kEnd = INT64_MAX;  // exit of a subsequence that reached the stream end
 
 enum : uint32_t { kLeaf = 0, kNode = 1, kMissing = 2 };
@@ -101,7 +104,7 @@ __device__ __forceinline__ int next_symbol(BitReader &br, int64_t &p, int64_t nb
 
 struct DecGeo {
   const uint32_t *words;
-  int64_t nwords, nbits, nsub;
+  int64_t nwords, nbits, nsub, sub;  // sub: bits per subsequence
   const uint32_t *lut;  // global copy (the kernels stage it in LDS)
   const int32_t *child;
 };
@@ -141,8 +144,8 @@ __global__ __launch_bounds__(kDT) void k_hd_count(DecGeo g, int64_t *__restrict_
   if (i >= g.nsub) return;
   int64_t e;
   int32_t c;
-  count_sub(g, s_lut, i * kSub, (i + 1) * kSub, e, c);
-  start[i] = i * kSub;
+  count_sub(g, s_lut, i * g.sub, (i + 1) * g.sub, e, c);
+  start[i] = i * g.sub;
   exit[i] = e;
   cnt[i] = c;
 }
@@ -162,7 +165,7 @@ __global__ __launch_bounds__(kDT) void k_hd_sync(DecGeo g, int64_t *__restrict__
   }
   int64_t e;
   int32_t c;
-  count_sub(g, s_lut, s, (i + 1) * kSub, e, c);
+  count_sub(g, s_lut, s, (i + 1) * g.sub, e, c);
   start[i] = s;
   exit_out[i] = e;
   cnt[i] = c;
@@ -178,7 +181,7 @@ __global__ void k_hd_chain(DecGeo g, int64_t *__restrict__ start, int64_t *__res
     if (s == start[i]) continue;
     int64_t e;
     int32_t c;
-    count_sub(g, g.lut, s, (i + 1) * kSub, e, c);
+    count_sub(g, g.lut, s, (i + 1) * g.sub, e, c);
     start[i] = s;
     exit[i] = e;
     cnt[i] = c;
@@ -244,7 +247,7 @@ __global__ __launch_bounds__(kDT) void k_hd_emit(DecGeo g, const int64_t *__rest
   int64_t tot;
   const int64_t o = boff[blockIdx.x] + blk_excl(i < g.nsub ? cnt[i] : 0, s_w, tot);
   if (i >= g.nsub) return;
-  const int64_t s = start[i], end = (i + 1) * kSub;
+  const int64_t s = start[i], end = (i + 1) * g.sub;
   if (s >= end) return;
   BitReader br;
   br.init(g.words, g.nwords, s);
@@ -286,7 +289,7 @@ DecWs carve(void *ws, int64_t nsub, int32_t nnodes, int32_t nleaves) {
   w.bsum = reinterpret_cast<int64_t *>(take((size_t)(nblk + 1) * 8));
   w.total = reinterpret_cast<int64_t *>(take(16));  // {symbols, first error bit}: one read back
   w.err = reinterpret_cast<unsigned long long *>(w.total + 1);
-  w.changed = reinterpret_cast<int32_t *>(take(4));
+  w.changed = reinterpret_cast<int32_t *>(take(4 * kRoundsPerSync));
   return w;
 }
 
@@ -301,7 +304,7 @@ extern "C" size_t hic_huffman_decode_workspace_bytes(int64_t nbits, int32_t nnod
   const int64_t nblk = ceil_div(nsub, kDT);
   const int64_t r = 256;
   return (size_t)(round_up(kLut * 4, r) + round_up(2LL * nnodes * 4, r) + round_up((nleaves > 0 ? nleaves : 1) * 4LL, r) +
-                  3 * round_up(nsub * 8, r) + round_up(nsub * 4, r) + round_up((nblk + 1) * 8, r) + 2 * r);
+                  3 * round_up(nsub * 8, r) + round_up(nsub * 4, r) + round_up((nblk + 1) * 8, r) + 3 * r);
 }
 
 extern "C" int hic_huffman_decode(const uint8_t *d_bits, int64_t nbits, const int32_t *h_child, int32_t nnodes,
@@ -343,7 +346,32 @@ extern "C" int hic_huffman_decode(const uint8_t *d_bits, int64_t nbits, const in
     lut[v] = e;
   }
   const hipStream_t s = as_stream(stream);
-  const int64_t nsub = ceil_div(nbits, kSub) > 0 ? ceil_div(nbits, kSub) : 1;
+  // equal-length codes (every leaf at one depth L, e.g. a near-uniform table): a
+  // subsequence of a multiple of L bits starts on a codeword, so round 0 is already
+  // synchronised (with 1024 bits and L not dividing it the rounds may never converge)
+  int64_t sub = kSub;
+  {
+    std::vector<int32_t> depth((size_t)nnodes, -1);
+    depth[0] = 0;
+    int leaf_depth = -1;
+    bool equal = true;
+    std::vector<int32_t> queue{0};
+    for (size_t qi = 0; qi < queue.size() && equal; ++qi) {
+      const int32_t n = queue[qi];
+      for (int b = 0; b < 2; ++b) {
+        const int32_t c = h_child[2 * n + b];
+        if (c >= 0) {
+          depth[c] = depth[n] + 1;
+          queue.push_back(c);
+        } else if (c <= -2) {
+          if (leaf_depth < 0) leaf_depth = depth[n] + 1;
+          equal = equal && leaf_depth == depth[n] + 1;
+        }
+      }
+    }
+    if (equal && leaf_depth > 0) sub = (int64_t)leaf_depth * ceil_div(kSub, leaf_depth);
+  }
+  const int64_t nsub = ceil_div(nbits, sub) > 0 ? ceil_div(nbits, sub) : 1;
   DecWs w = carve(workspace, nsub, nnodes, nleaves);
   *h_count = 0;
   if (nbits == 0) return HIC_OK;
@@ -359,24 +387,29 @@ extern "C" int hic_huffman_decode(const uint8_t *d_bits, int64_t nbits, const in
   // the host tables are locals / the caller's: wait for the uploads before anything can return
   if (int e = hip_status(hipStreamSynchronize(s), "hipStreamSynchronize")) return e;
   if (int e = hip_status(hipMemsetAsync(w.err, 0xFF, 8, s), "hipMemsetAsync")) return e;
-  DecGeo g{reinterpret_cast<const uint32_t *>(d_bits), ceil_div(nbits, 32), nbits, nsub, w.lut, w.child};
+  DecGeo g{reinterpret_cast<const uint32_t *>(d_bits), ceil_div(nbits, 32), nbits, nsub, sub, w.lut, w.child};
   const dim3 grid((unsigned)ceil_div(nsub, kDT)), block(kDT);
   hipLaunchKernelGGL(k_hd_count, grid, block, 0, s, g, w.start, w.exit_a, w.cnt);
   if (int e = check_launch("k_hd_count")) return e;
   int64_t *ein = w.exit_a, *eout = w.exit_b;
   bool synced = nsub == 1;
-  for (int round = 0; !synced && round < kMaxRounds; ++round) {
-    if (int e = hip_status(hipMemsetAsync(w.changed, 0, 4, s), "hipMemsetAsync")) return e;
-    hipLaunchKernelGGL(k_hd_sync, grid, block, 0, s, g, w.start, ein, eout, w.cnt, w.changed);
-    if (int e = check_launch("k_hd_sync")) return e;
-    int32_t changed = 0;
-    if (int e = hip_status(hipMemcpyAsync(&changed, w.changed, 4, hipMemcpyDeviceToHost, s), "hipMemcpyAsync"))
+  // rounds in batches of kRoundsPerSync, one host read of their change flags per
+  // batch: a round without a change means every later one has none either
+  for (int round = 0; !synced && round < kMaxRounds; round += kRoundsPerSync) {
+    if (int e = hip_status(hipMemsetAsync(w.changed, 0, 4 * kRoundsPerSync, s), "hipMemsetAsync")) return e;
+    for (int k = 0; k < kRoundsPerSync; ++k) {
+      hipLaunchKernelGGL(k_hd_sync, grid, block, 0, s, g, w.start, ein, eout, w.cnt, w.changed + k);
+      if (int e = check_launch("k_hd_sync")) return e;
+      int64_t *t = ein;
+      ein = eout;
+      eout = t;
+    }
+    int32_t changed[kRoundsPerSync] = {};
+    if (int e = hip_status(hipMemcpyAsync(changed, w.changed, 4 * kRoundsPerSync, hipMemcpyDeviceToHost, s),
+                           "hipMemcpyAsync"))
       return e;
     if (int e = hip_status(hipStreamSynchronize(s), "hipStreamSynchronize")) return e;
-    int64_t *t = ein;
-    ein = eout;
-    eout = t;
-    synced = changed == 0;
+    for (int k = 0; k < kRoundsPerSync; ++k) synced = synced || changed[k] == 0;
   }
   if (!synced) {
     hipLaunchKernelGGL(k_hd_chain, dim3(1), dim3(1), 0, s, g, w.start, ein, w.cnt);

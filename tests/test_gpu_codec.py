@@ -765,6 +765,38 @@ def test_huffman_decode_device_full_size():
     assert torch.equal(out[:n], keys)
 
 
+@pytest.mark.parametrize("nkeys", [8, 5, 16])
+def test_huffman_decode_device_equal_length_codes(nkeys):
+    """a near-uniform table gives every key the same code length L
+    (3 bits for 8 keys, 4 for 16); with 1024-bit subsequences and L not dividing
+    1024 the speculative starts never resynchronise and the decode fell to the serial
+    one-thread chain.  Subsequences are now a multiple of L bits: 30 M coded bits
+    decode to the keys, and in well under a second (5 keys: unequal lengths, the
+    usual resynchronisation)."""
+    import time
+    from hiccup_amd import huffman
+    rng = np.random.default_rng(nkeys)
+    n = 10_000_000
+    keys = device.to_device(rng.integers(0, nkeys, n).astype(np.int32))
+    ds = huffman.DeviceStream(keys)
+    packed, nbits = ds.packed()
+    dec = huffman.HuffmanTree.construct_from_coding(ds.tree.encode_table())
+    if nkeys in (8, 16):
+        assert dec.min_code_length() == {8: 3, 16: 4}[nkeys]
+    buf = np.zeros(-(-nbits // 32) * 4, np.uint8)
+    buf[:packed.size] = packed
+    bits = device.to_device(buf)
+    dec.decode_device(bits, nbits)  # warm-up (LUT build, workspace)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out, cnt, ints = dec.decode_device(bits, nbits)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    assert ints and cnt == n
+    assert torch.equal(out[:n], keys)
+    assert dt < 0.5, "%.3f s for %d bits" % (dt, nbits)
+
+
 @pytest.mark.parametrize("table", [0, 1])
 @pytest.mark.parametrize("nblk", [1, 63, 64, 65, 777, 129600])
 def test_wire_pack_unpack(nblk, table):

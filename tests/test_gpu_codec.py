@@ -633,7 +633,7 @@ def test_two_stream_overlap_matches_single_stream():
     H, W = 1088, 1920
     rng = np.random.default_rng(11)
     imgs = [device.to_device(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)) for _ in range(3)]
-    encs = [pipeline.Encoder(H, W, onepass=True) for _ in range(4)]
+    encs = [pipeline.Encoder(H, W) for _ in range(4)]
     streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
     torch.cuda.synchronize()
     last = {}

@@ -760,7 +760,11 @@ __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
   // per wave: kWSyms symbols + 16-byte alignment slack + the dummy slot
   __shared__ __attribute__((aligned(16))) uint8_t s_len_all[4][kWSyms + 32];
   __shared__ __attribute__((aligned(16))) int16_t s_val_all[4][kWSyms + 32];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // wv (and the tile / job indices derived from it) wave-uniform in SGPRs: the jobs'
+  // fields are then scalar loads from the kernel arguments, not per-lane loads of a
+  // dynamically indexed argument copy, each followed by a vmcnt(0) that also drained
+  // the next tile's prefetch and this tile's symbol stores
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   const int M = jobs.M;
   if (blockIdx.x == 0 && threadIdx.x < jobs.n) {  // the scan's failure report (sticky)
@@ -780,12 +784,12 @@ __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
   auto job_of = [&](int64_t gt) {
     int k = 0;
     while (k + 1 < jobs.n && gt >= jobs.j[k + 1].tile0) ++k;
-    return k;
+    return __builtin_amdgcn_readfirstlane(k);
   };
   // tile t's first block, its block count and its first record
   auto geo = [&](const RleJob16 &J, int64_t t, int64_t &b0, int64_t &bend, int64_t &r0) {
     if (J.rowb > 0) {
-      const int64_t row = t / J.tpr, j = t - row * J.tpr;
+      const int64_t row = (int)t / (int)J.tpr, j = t - row * J.tpr;  // tile counts < 2^31
       b0 = row * J.rowb + j * kWT;
       bend = row * J.rowb + (j * kWT + kWT < J.rowb ? j * kWT + kWT : J.rowb);
       r0 = row * J.rpr + (j << J.rshift);

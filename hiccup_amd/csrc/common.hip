@@ -87,7 +87,7 @@ extern "C" int hic_set_knob(int k, int value) {
   if (k == HIC_KNOB_ENCODE_WAVES && value != -1 && value != 3) return hic::arg_error("encode waves: 3 only (retired)");
   if (k == HIC_KNOB_ENCODE_NT && value != -1 && value != 1) return hic::arg_error("encode_nt: 1 only (retired)");
   if (k == HIC_KNOB_DCT_MFMA && value != -1 && (value < 0 || value > 3)) return hic::arg_error("dct_mfma 0..3");
-  if (k == HIC_KNOB_ENCODE_ORDER && value != -1 && (value < 0 || value > 1)) return hic::arg_error("encode_order 0/1");
+  if (k == HIC_KNOB_ENCODE_ORDER && value != -1 && (value < 0 || value > 7)) return hic::arg_error("encode_order 0..7");
   if (k == HIC_KNOB_ENCODE_DCT && value != -1 && value != 0 && value != 1)
     return hic::arg_error("encode_dct: 0 float64 AAN, 1 integer MFMA");
   if (value < -1) return hic::arg_error("knob value %d", value);

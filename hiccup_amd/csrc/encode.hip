@@ -37,8 +37,11 @@
 //      half-tile records (hic_rle_job16.records_per_tile = 2).
 // Exact-tie fallbacks (dct_block_2ph, dct_fix26) run in place on the pixels still
 // in registers: a unit never revisits HBM.
-// RGB traffic: 19/16 of the image (the vertical halo rows are re-read by the unit
-// above / below); coefficient writes 3 B per pixel.
+// RGB traffic: 19/16 of the image fetched by the waves (the vertical halo rows are
+// re-read by the unit above / below), of which the default unit order (knob
+// encode_order 6: XCD-major workgroups, odd unit rows bottom-up) has the L2 serve
+// most re-reads: 109.6 MB from HBM per 8K launch against the image's 99.5 MB;
+// coefficient writes 3 B per pixel.
 #include "color_core.h"
 #include "dct_core.h"
 #include "dct_mfma.h"
@@ -56,6 +59,8 @@ struct Enc420 {
   int M;
   int nstrips, nunits;  // nunits: waves (one unit each)
   int vstack;           // 1: a workgroup's waves take 4 vertically stacked units of one strip
+  int xcd;              // 1: workgroups remapped XCD-major (xcd_block)
+  int alt;              // 1: odd unit rows run their colour rows bottom-up
   int wlast;            // pixel columns of the last strip (16 .. 512)
   // one-pass encode (hic_encode420_rle_u8): per plane Y, Cr, Cb
   int32_t *dc[3];
@@ -73,6 +78,15 @@ struct Enc420 {
 };
 
 constexpr int kZZ = HIC_LAYOUT_ZIGZAG_I16;
+
+// Workgroup b of n, as dispatched round-robin over the 8 XCDs (b % 8), -> the logical
+// block that puts consecutive logical blocks on one XCD (its own L2): XCD x takes
+// blocks x * q + min(x, r) .. (q = n / 8, r = n % 8), so the pixel rows and strip-edge
+// lines neighbouring units share are fetched once into that L2.
+__device__ __forceinline__ int xcd_block(int b, int n) {
+  const int q = n >> 3, r = n & 7, x = b & 7, i = b >> 3;
+  return x * q + (x < r ? x : r) + i;
+}
 
 // Exact fallbacks, out of line (cold; by-value pixel rows keep them in VGPRs).
 template <int TABLE>
@@ -271,6 +285,7 @@ __device__ __forceinline__ uint32_t wshl1(uint32_t v) {  // lane i <- lane i + 1
 // (VG = 2: the second unit reuses the first's bottom halo rows).
 template <int NR, int LA = HIC_ENC_LA, bool PIN_Y = false>
 struct EncColour {
+  static_assert(NR % 2 == 1, "the bottom-up chroma rows assume an odd row count");
   // rows stream through a ring of kLA + 1 loads in flight (sched_barrier keeps the
   // compiler from hoisting all 19 rows' loads: 114 VGPRs)
   static constexpr int kLA = LA;
@@ -288,13 +303,14 @@ struct EncColour {
 #ifndef HIC_ENC_LOAD_AUX
 #define HIC_ENC_LOAD_AUX 0
 #endif
-  __device__ __forceinline__ void load_row(int r) {
+  // input row r into ring slot t % (kLA + 1) (t: the row's turn)
+  __device__ __forceinline__ void load_row_at(int r, int t) {
     const int so = __builtin_amdgcn_readlane(roff, r);
-    ring_a[r % (kLA + 1)] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, so, HIC_ENC_LOAD_AUX);
-    ring_b[r % (kLA + 1)] = __builtin_amdgcn_raw_buffer_load_b64(rsrc, voff + 16, so, HIC_ENC_LOAD_AUX);
+    ring_a[t % (kLA + 1)] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, so, HIC_ENC_LOAD_AUX);
+    ring_b[t % (kLA + 1)] = __builtin_amdgcn_raw_buffer_load_b64(rsrc, voff + 16, so, HIC_ENC_LOAD_AUX);
   }
 
-  __device__ __forceinline__ void init(const Enc420 &E, int y0, int s, int lane_, int nb) {
+  __device__ __forceinline__ void init(const Enc420 &E, int y0, int s, int lane_, int nb, bool rev = false) {
     lane = lane_;
     rlane = __builtin_amdgcn_readfirstlane(nb - 1);
     const int W = E.W, H = E.H, pitch = 3 * W;
@@ -335,39 +351,54 @@ struct EncColour {
     k4 = opq(0x00040004u);
     k6 = opq(0x00060006u);
     k128 = opq(0x00800080u);
+    // rev: the rows run bottom-up (rows_rev)
 #pragma unroll
-    for (int r = 0; r < kLA; ++r) load_row(r);
+    for (int t = 0; t < kLA; ++t) load_row_at(rev ? NR - 1 - t : t, t);
   }
 
-  // input rows R0 .. R1 - 1
-  template <int R0, int R1>
-  __device__ __forceinline__ void rows(uint2 (&yq)[16], uint32_t *s_chroma) {
+  // all NR input rows, top-down, or bottom-up (rev, wave-uniform; init(.., rev)): a
+  // unit row's bottom halo rows are then fetched while the unit row below, running
+  // the other way, fetches them as its top rows (not ~20 us apart, after the L2 has
+  // turned over).  One code path: row t of the pass is input row r = t or NR - 1 - t,
+  // and as the pyrDown filter is symmetric only the Y slot and the chroma row a turn
+  // fills depend on the direction.
+  __device__ __forceinline__ void rows(uint2 (&yq)[16], uint32_t *s_chroma, bool rev) {
 #pragma unroll
-    for (int r = R0; r < R1; ++r) {
-      if (r + kLA < NR) load_row(r + kLA);
-      const u32x4 qa = ring_a[r % (kLA + 1)];
-      const u32x2 qb = ring_b[r % (kLA + 1)];
+    for (int t = 0; t < NR; ++t) {
+      const int r = rev ? NR - 1 - t : t;  // wave-uniform
+      if (t + kLA < NR) load_row_at(rev ? NR - 1 - (t + kLA) : t + kLA, t + kLA);
+      const u32x4 qa = ring_a[t % (kLA + 1)];
+      const u32x2 qb = ring_b[t % (kLA + 1)];
       const uint32_t wd[6] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y};
       uint32_t Yh[8], c[8];
       ycc8(wd, K, Yh, c);
-      // Y rows of the unit(s): input rows 2 .. NR - 2, slot (r - 2) mod 16 (a slot is
-      // refilled only after the DCT of its block row has read it)
-      if (r >= 2 && r <= NR - 2) {
-        yq[(r - 2) & 15] = make_uint2(ypack4(Yh, 0), ypack4(Yh, 4));
+      // Y rows of the unit: input rows 2 .. NR - 2, slot r - 2 (top-down: turns
+      // 2 .. NR - 2, slot t - 2; bottom-up: turns 1 .. NR - 3, slot NR - 3 - t)
+      const uint2 yv = make_uint2(ypack4(Yh, 0), ypack4(Yh, 4));
+      if (t >= 2 && t <= NR - 2) {
+        uint2 &q = yq[(t - 2) & 15];
+        q = rev ? q : yv;
         // PIN_Y: pack now (the compiler otherwise sinks the packing v_perms to the
         // DCT and keeps the row's eight Yh dwords live, spilling them at 168 VGPRs)
-        if constexpr (PIN_Y) asm volatile("" : "+v"(yq[(r - 2) & 15].x), "+v"(yq[(r - 2) & 15].y));
+        if constexpr (PIN_Y) asm volatile("" : "+v"(q.x), "+v"(q.y));
+      }
+      if (t >= 1 && t <= NR - 3) {
+        uint2 &q = yq[(NR - 3 - t) & 15];
+        q = rev ? yv : q;
+        if constexpr (PIN_Y) asm volatile("" : "+v"(q.x), "+v"(q.y));
       }
       // neighbour pixels x0 - 2, x0 - 1 (left lane) and x0 + 8 (right lane)
       const uint32_t l2 = set_lane<0>(wshr1(c[6]), __builtin_amdgcn_readlane((int)hal_l2, r));
       const uint32_t l1 = set_lane<0>(wshr1(c[7]), __builtin_amdgcn_readlane((int)hal_l1, r));
       const uint32_t r0 = set_lane_s(wshl1(c[0]), __builtin_amdgcn_readlane((int)hal_r, r), lane, rlane);
-      h[r][0] = pk_taps5(l2, l1, c[0], c[1], c[2], k4, k6);
-      h[r][1] = pk_taps5(c[0], c[1], c[2], c[3], c[4], k4, k6);
-      h[r][2] = pk_taps5(c[2], c[3], c[4], c[5], c[6], k4, k6);
-      h[r][3] = pk_taps5(c[4], c[5], c[6], c[7], r0, k4, k6);
-      if (r >= 4 && r % 2 == 0) {  // chroma row i = r / 2 - 2 has all five input rows
-        const int a = r - 4, i = r / 2 - 2;
+      h[t][0] = pk_taps5(l2, l1, c[0], c[1], c[2], k4, k6);
+      h[t][1] = pk_taps5(c[0], c[1], c[2], c[3], c[4], k4, k6);
+      h[t][2] = pk_taps5(c[2], c[3], c[4], c[5], c[6], k4, k6);
+      h[t][3] = pk_taps5(c[4], c[5], c[6], c[7], r0, k4, k6);
+      // chroma row i has all five input rows 2 i .. 2 i + 4: the turns t - 4 .. t
+      // (t even; i = t / 2 - 2, or bottom-up (NR - 1 - t) / 2)
+      if (t >= 4 && t % 2 == 0) {
+        const int a = t - 4, i = rev ? (NR - 1 - t) / 2 : t / 2 - 2;  // NR odd
         uint32_t v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j)  // sum + 128 < 2^16: (sum + 128) >> 8 is the high byte
@@ -518,7 +549,7 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
   __shared__ __attribute__((aligned(16))) int16_t s_opval[OP ? HIC_ENC_WPB : 1][OP ? kOpSyms + 32 : 8];
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int g = __builtin_amdgcn_readfirstlane(blockIdx.x * HIC_ENC_WPB + wv);
-  if ((OP || !E.vstack) && g >= E.nunits) return;  // wave-uniform
+  if (OP && g >= E.nunits) return;  // wave-uniform
   if (OP) {
     // tickets in the order waves start; the last one resets the counter for the next
     // launch (every ticket is taken by then)
@@ -529,17 +560,22 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
   }
   uint2 *st2 = s_stage + wv * 64 * kStageU2;
   uint32_t *s_chroma = s_chroma_all[wv];
+  const int bx = __builtin_amdgcn_readfirstlane(E.xcd ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x);
   int16_t *st = reinterpret_cast<int16_t *>(st2 + lane * kStageU2);
   // wave g: strip s, unit row u0 (vstack: workgroup b = strip b % nstrips, unit rows
   // 4 (b / nstrips) .. + 3 -- the halo rows a unit shares with the one below are
   // fetched once into the CU's caches)
   int u0, s;
   if (!OP && E.vstack) {
-    const int b = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+    const int b = bx;
     s = __builtin_amdgcn_readfirstlane(b % E.nstrips);
     u0 = __builtin_amdgcn_readfirstlane((b / E.nstrips) * HIC_ENC_WPB + wv);
     if (u0 * 16 >= E.out_rows) return;  // wave-uniform
   } else {
+    if (!OP) {
+      g = __builtin_amdgcn_readfirstlane(bx * HIC_ENC_WPB + wv);
+      if (g >= E.nunits) return;  // wave-uniform
+    }
     u0 = __builtin_amdgcn_readfirstlane(g / E.nstrips);
     s = __builtin_amdgcn_readfirstlane(g - u0 * E.nstrips);
   }
@@ -670,8 +706,9 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
 #define HIC_ENC_LA3 3  // load lookahead (rows)
 #endif
   EncColour<19, HIC_ENC_LA3, true> C;
-  C.init(E, y0, s, lane, nb);
-  C.template rows<0, 19>(yq, s_chroma);
+  const bool rev = E.alt && (u0 & 1);  // wave-uniform
+  C.init(E, y0, s, lane, nb, rev);
+  C.rows(yq, s_chroma, rev);
   __builtin_amdgcn_sched_barrier(0);
 #endif
   if (MFMA) mfma_load_A(0, lane, A);
@@ -777,7 +814,13 @@ static int encode420(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, 
   E.nunits = E.nstrips * (int)(out_rows / 16);  // waves
   // one wave per unit (no persistent loop: units are the same size, and the
   // hardware's dispatch balances the tail better than a fixed split)
-  E.vstack = knob(HIC_KNOB_ENCODE_ORDER) == 1;
+  // default 6: row-major, XCD-major workgroups, odd unit rows bottom-up (FETCH_SIZE
+  // 109.6 vs 131.7 MB per 8K launch, kernel 58.0 vs 58.9 us, bench 0.0996 vs 0.1004
+  // ms/step median of 10 alternating pairs: profiles/r04/enc_order_xcd)
+  const int order = knob(HIC_KNOB_ENCODE_ORDER) < 0 ? 6 : knob(HIC_KNOB_ENCODE_ORDER);
+  E.vstack = order & 1;
+  E.xcd = (order >> 1) & 1;
+  E.alt = (order >> 2) & 1;
   const int nu = (int)(out_rows / 16);
   const dim3 grid((unsigned)(E.vstack ? E.nstrips * ((nu + HIC_ENC_WPB - 1) / HIC_ENC_WPB)
                                       : (E.nunits + HIC_ENC_WPB - 1) / HIC_ENC_WPB)),

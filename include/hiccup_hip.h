@@ -79,7 +79,7 @@ int hic_device_count(int *h_n);
 #define HIC_KNOB_ENCODE_NT 10       /* retired (round 4): nontemporal coefficient stores; only 1 is accepted */
 #define HIC_KNOB_ENCODE_DCT 11      /* hic_encode420_u8 transform: 0 float64 AAN, 1 integer MFMA (dct_mfma.h) */
 #define HIC_KNOB_DCT_MFMA 12        /* k_dct_mfma variant (0..3): bit 0 = next set's pixels prefetched, bit 1 = 2 waves per SIMD (else 3) */
-#define HIC_KNOB_ENCODE_ORDER 13     /* hic_encode420_u8 unit order: 0 row-major (a workgroup = 4 strips side by side), 1 = 4 units stacked vertically (their pyrDown halo rows shared in the CU's caches) */
+#define HIC_KNOB_ENCODE_ORDER 13     /* hic_encode420_u8 unit order: 0 row-major (a workgroup = 4 strips side by side), 1 = 4 units stacked vertically (their pyrDown halo rows shared in the CU's caches); + 2: workgroups remapped XCD-major (neighbouring units on one XCD's L2); + 4: odd unit rows run their colour rows bottom-up (the halo rows two unit rows share fetched at the same time); default 6 */
 #define HIC_KNOB_COUNT 14
 int hic_set_knob(int knob, int value);
 int hic_get_knob(int knob, int *h_value);

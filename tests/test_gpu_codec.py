@@ -432,13 +432,15 @@ def test_fused_encoder_ragged_matches_chain(kind, H, W, enc_dct):
             np.testing.assert_array_equal(a[k][j], b[k][j], err_msg="%s %s" % (k, what))
 
 
-@pytest.mark.parametrize("order", [0, 1])
+@pytest.mark.parametrize("order", [0, 1, 2, 3, 4, 6, 7])
 @pytest.mark.parametrize("kind", ["random", "levels", "flat"])
 @pytest.mark.parametrize("H,W", [(16, 512), (48, 1024), (80, 2048), (272, 1536), (144, 1040), (2160, 3840)])
 def test_fused_encoder_unit_order(kind, H, W, order):
     """knob encode_order (0: a workgroup = 4 strips side by side, 1: 4 vertically
     stacked units of one strip, unit-row counts not a multiple of 4 and ragged last
-    strips included) == the two-kernel chain."""
+    strips included; 2 / 3: the same with workgroups remapped XCD-major; + 4: odd
+    unit rows run their colour rows bottom-up) == the
+    two-kernel chain."""
     with _lib.knobs(encode_order=order):
         test_fused_encoder_matches_two_kernel_chain(kind, H, W, 0, _lib.DCT_PATH_F64)
 

@@ -450,13 +450,42 @@ def extra_16k_roundtrip(steps=4):
     dt = res[True]
     x = xs[steps % 2]
     mse = float(((out.float() - x.float()) ** 2).mean())
-    del xs, enc, dec
+    del out
+    # the same trips pipelined: consecutive trips alternate over two streams, each
+    # with its own encoder / decoder, so one trip's decode overlaps the next one's
+    # encode (per-trip time = throughput; ms_per_roundtrip above is the latency)
+    enc2, dec2 = pipeline.Encoder(n, n, index=True), pipeline.Decoder(n, n)
+    pairs = [(enc, dec), (enc2, dec2)]
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+
+    def trip2(i):
+        e, d = pairs[i % 2]
+        with torch.cuda.stream(streams[i % 2]):
+            e.encode(xs[i % 2], streams[i % 2])
+            return d.decode(e.sym_len, e.sym_val, e.counts, e.dc, stream=streams[i % 2], index=e.index)
+
+    trip2(0)
+    trip2(1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(2 * steps):
+        trip2(i)
+    torch.cuda.synchronize()
+    dt2 = (time.perf_counter() - t0) / (2 * steps)
+    dec.check_status()
+    dec2.check_status()
+    out_a = dec2.rgb.clone()  # trip 2 * steps + 1: xs[1], against a one-stream trip of it
+    ref = trip(1, True)
+    torch.cuda.synchronize()
+    same = bool(torch.equal(ref, out_a))
+    del xs, enc, dec, enc2, dec2, pairs, ref, out_a
     torch.cuda.empty_cache()
     return {"workload": "16384x16384 RGB encode + decode round trip, 1 GPU (BASELINE configs[4] at N=1); decode "
                         "from the encoder-side tile index, RLE decode + IDCT fused per plane "
                         "(hic_rle_decode_idct_u8_indexed), no host sync between the halves",
             "ms_per_roundtrip": round(dt * 1e3, 3), "mpix_s": round(n * n / dt / 1e6, 1),
             "ms_per_roundtrip_unindexed_decode": round(res[False] * 1e3, 3),
+            "ms_per_roundtrip_2streams": round(dt2 * 1e3, 3), "two_stream_output_equal": same,
             "psnr_db_vs_input": round(10 * np.log10(255.0 ** 2 / mse), 3), "timed_roundtrips": steps}
 
 

@@ -280,8 +280,11 @@ __global__ __launch_bounds__(256) void k_dequant_idct(const void *__restrict__ c
 // transform.py:169-179, for one plane).
 constexpr int kRowI16 = 68;  // LDS block row: 64 slots + pad (136 B, conflict-free 8 B reads)
 constexpr int kDIS = 16;     // symbols per lane per step
+#ifndef HIC_DEC_WPE
+#define HIC_DEC_WPE 4
+#endif
 template <int TABLE, bool FAST>
-__global__ __launch_bounds__(256) void k_rld_idct_indexed(const uint8_t *__restrict__ sym_len,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DEC_WPE))) void k_rld_idct_indexed(const uint8_t *__restrict__ sym_len,
                                                           const int16_t *__restrict__ sym_val,
                                                           const int64_t *__restrict__ d_nsym,
                                                           const int32_t *__restrict__ dc_diff,

@@ -191,8 +191,6 @@ __device__ __forceinline__ void load_block16(const int16_t *__restrict__ blocks,
   }
 }
 
-// Wave-level: the tile record of the 64 blocks held by this wave's lanes
-// (valid = this lane's block exists).  Every lane must call it.
 // Wave-level: the tile record's three values (wave-uniform) from each lane's block
 // summary.  Every lane must call it.
 __device__ __forceinline__ void tile_record_values(int first, int last, int nsym, int64_t b, int M, int64_t &r0,

@@ -18,9 +18,10 @@ def main():
             a = bench.extra_8k_plane_dct()
             b = bench.extra_8k_plane_dct(luma_only=True)
             c = bench.extra_4k_luma()
-        print("%-28s %-24s planes %7.2f us (%.3f)  luma %7.2f us (%.3f)  4k %7.2f us (%.3f)" % (
-            lib, label, a["median_launch_us"], a["frac"], b["median_launch_us"], b["frac"], c["avg_launch_us"],
-            c["frac"]), flush=True)
+            d = bench.extra_8k_luma_batched()
+        print("%-28s %-24s planes %7.2f us (%.3f)  luma %7.2f us (%.3f)  4k %7.2f us (%.3f)  luma x8 %7.2f us/plane "
+              "(%.3f)" % (lib, label, a["median_launch_us"], a["frac"], b["median_launch_us"], b["frac"],
+                          c["avg_launch_us"], c["frac"], d["us_per_plane"], d["frac"]), flush=True)
 
 
 if __name__ == "__main__":

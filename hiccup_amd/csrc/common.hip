@@ -19,6 +19,7 @@ int knob(int k) {
     case HIC_KNOB_RLE_NT: return 1;
     case HIC_KNOB_ENCODE_WAVES: return 3;
     case HIC_KNOB_ENCODE_NT: return 1;
+    case HIC_KNOB_ENCODE_ORDER: return 6;  // XCD-major workgroups, odd unit rows bottom-up
     default: return k == HIC_KNOB_DCT_WAVES_PER_CU ? -1 : 0;
   }
 }

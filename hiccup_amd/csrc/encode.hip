@@ -817,7 +817,7 @@ static int encode420(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, 
   // default 6: row-major, XCD-major workgroups, odd unit rows bottom-up (FETCH_SIZE
   // 109.6 vs 131.7 MB per 8K launch, kernel 58.0 vs 58.9 us, bench 0.0996 vs 0.1004
   // ms/step median of 10 alternating pairs: profiles/r04/enc_order_xcd)
-  const int order = knob(HIC_KNOB_ENCODE_ORDER) < 0 ? 6 : knob(HIC_KNOB_ENCODE_ORDER);
+  const int order = knob(HIC_KNOB_ENCODE_ORDER);
   E.vstack = order & 1;
   E.xcd = (order >> 1) & 1;
   E.alt = (order >> 2) & 1;

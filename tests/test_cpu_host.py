@@ -63,6 +63,19 @@ def test_last_error_roundtrip():
         _lib.check(rc, "x")
 
 
+def test_knob_defaults_and_ranges():
+    """The launch defaults the measurements chose (hic_get_knob reports the effective
+    value; no GPU call): encode_order 6 = XCD-major workgroups + odd unit rows
+    bottom-up (profiles/r04/enc_order_xcd); out-of-range values are refused."""
+    assert _lib.get_knob("encode_order") == 6
+    assert _lib.get_knob("dct_path") == 1
+    with _lib.knobs(encode_order=3):
+        assert _lib.get_knob("encode_order") == 3
+    assert _lib.get_knob("encode_order") == 6
+    with pytest.raises(ValueError):
+        _lib.set_knob("encode_order", 8)
+
+
 def _names(d, prefix):
     return sorted(k[len(prefix):] for k in d if k.startswith(prefix))
 

@@ -52,11 +52,6 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 XGMI_LINK_GBS = 153.0  # per xGMI link of an MI355X (7 per GPU), the figure given with this build
 ROT_BYTES = 1.2e9          # rotate >= 1.2 GB of inputs: defeats the 256 MiB Infinity Cache
 REGION_REPEATS = 7         # extra timed regions for the ms_per_step spread (p10 / p50 / p90)
-# the fused encoder's memory-only floor (19 RGB rows + 24 KiB of stores per unit, no
-# arithmetic) from the committed micro-benchmark log profiles/r02/micro_rgb_rows.log
-# (tools/micro/rgb_rows.hip) -- NOT measured in the bench run; the plane pass's floor
-# and the device-copy rate are (measure_floors)
-FUSED_FLOOR_US_MICRO = 43.0
 
 
 def parse():
@@ -413,6 +408,27 @@ def measure_floors(steps=20):
         del planes, outs
         torch.cuda.empty_cache()
     out["luma_pattern"] = pat
+    # the fused encoder's own byte pattern (hic_probe_encode420: the same grid, unit
+    # order and 19 row loads per unit, stage and 1 KiB stores, no arithmetic) on the
+    # 8K RGB image: k_encode420's in-run memory floor
+    h, w = H8K, W8K
+    px = h * w
+    rot = max(2, int(np.ceil(ROT_BYTES / (6 * px))))
+    g = torch.Generator(device="cuda")
+    g.manual_seed(10)
+    imgs = [torch.randint(0, 256, (h, w, 3), dtype=torch.uint8, device="cuda", generator=g) for _ in range(rot)]
+    co = [(device.empty((px // 64, 64), torch.int16), device.empty((px // 256, 64), torch.int16),
+           device.empty((px // 256, 64), torch.int16)) for _ in range(rot)]
+    rec_y = device.empty(((h // 8) * (w // 512) * 3,), torch.int64)
+    rec_c = device.empty(((h // 16) * (w // 512) * 3,), torch.int64)
+    us = timed(lambda i, e0, e1: _lib.call("hic_probe_encode420", device.ptr(imgs[i % rot]), h, w,
+                                           *[device.ptr(t) for t in co[i % rot]], device.ptr(rec_y),
+                                           device.ptr(rec_c), device.stream_ptr(), e0, e1))
+    out["encode420_pattern"] = {"image_hw": [h, w], "bytes_per_launch": 6 * px, "median_launch_us": round(us, 2),
+                                "gbs": round(6 * px / (us * 1e-6) / 1e9, 1),
+                                "frac_of_8tbs": round(6 * px / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+    del imgs, co, rec_y, rec_c
+    torch.cuda.empty_cache()
     return out
 
 
@@ -1105,9 +1121,6 @@ def main():
                 "avg_launch_us": round(dct_us, 2),
                 "timed_over": roof_note,
                 "avg_launch_us_overlapped": None if dct_us_overlapped is None else round(dct_us_overlapped, 2),
-                "memory_floor_us_micro": FUSED_FLOOR_US_MICRO if (fused and args.workload == "8k" and world == 1)
-                else None,
-                "memory_floor_source": "profiles/r02/micro_rgb_rows.log (committed micro log, not this run)",
             },
         }
         if world == 1:
@@ -1115,6 +1128,12 @@ def main():
             out["memory_floors"] = floors
             out["roofline"]["device_copy_gbs"] = floors["device_copy_gbs"]
             out["roofline"]["frac_of_device_copy"] = round(achieved / floors["device_copy_gbs"], 4)
+            if fused and args.workload == "8k":
+                # the kernel's own byte pattern without its arithmetic, measured in this run
+                fl = floors["encode420_pattern"]["median_launch_us"]
+                out["roofline"]["memory_floor_us"] = fl
+                out["roofline"]["frac_of_memory_floor"] = round(fl / dct_us, 4)
+                out["roofline"]["memory_floor_source"] = "memory_floors.encode420_pattern (hic_probe_encode420, this run)"
             # the headline normalised by this box's own streaming copy rate (box-to-box
             # HBM / clock spread divides out): Mpix/s per GB/s of measured device copy
             out["value_per_copy_gbs"] = round(value / floors["device_copy_gbs"], 5)

@@ -48,6 +48,7 @@ SIGNATURES = {
     "hic_stream_sync": (_int, [_vp]),
     "hic_probe_copy": (_int, [_vp, _vp, _i64, _int, _vp, _vp, _vp]),
     "hic_probe_plane": (_int, [_vp, _i64, _i64, _vp, _int, _vp, _vp, _vp]),
+    "hic_probe_encode420": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "hic_set_knob": (_int, [_int, _int]),
     "hic_get_knob": (_int, [_int, ctypes.POINTER(_int)]),
     "hic_dct_quant_u8": (_int, [_vp, _i64, _i64, _i64, _int, _int, _vp, _vp]),

@@ -412,6 +412,21 @@ struct EncColour {
       __builtin_amdgcn_sched_barrier(0);
     }
   }
+
+  // hic_probe_encode420: the same NR row loads in the same order, no arithmetic --
+  // each row's words (and the edge pixels) folded into the Y slots so the probe's
+  // stores carry what its loads fetched
+  __device__ __forceinline__ void fold_rows(uint2 (&yq)[16], bool rev) {
+#pragma unroll
+    for (int t = 0; t < NR; ++t) {
+      if (t + kLA < NR) load_row_at(rev ? NR - 1 - (t + kLA) : t + kLA, t + kLA);
+      const u32x4 qa = ring_a[t % (kLA + 1)];
+      const u32x2 qb = ring_b[t % (kLA + 1)];
+      yq[t & 15].x ^= qa.x ^ qa.z ^ qb.x;
+      yq[t & 15].y ^= qa.y ^ qa.w ^ qb.y;
+    }
+    yq[0].x ^= hal_l2 ^ hal_l1 ^ hal_r;
+  }
 };
 
 // One-pass: a pass's record (lane = block; SEG: lanes 0-31 Cr record `rec`, 32-63 Cb
@@ -765,6 +780,55 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
   }
 }
 
+// Memory-only probe of k_encode420's byte pattern (bench.py's in-run floor for the
+// fused kernel): the same grid, unit order and 19 row loads per unit, the LDS stage
+// and the three passes' 1 KiB nontemporal stores plus their records, no colour
+// conversion, pyrDown, DCT or RLE summary.
+__global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_eu(3))) void k_probe_encode420(
+    Enc420 E) {
+  __shared__ __attribute__((aligned(16))) uint2 s_stage[HIC_ENC_WPB * 64 * kStageU2];
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int bx = __builtin_amdgcn_readfirstlane(E.xcd ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x);
+  const int g = __builtin_amdgcn_readfirstlane(bx * HIC_ENC_WPB + wv);
+  if (g >= E.nunits) return;  // wave-uniform
+  const int u0 = __builtin_amdgcn_readfirstlane(g / E.nstrips), s = __builtin_amdgcn_readfirstlane(g - u0 * E.nstrips);
+  const int y0 = E.out_row0 + 16 * u0, nbx = E.W >> 3, nbxc = E.W >> 4;
+  uint2 *st2 = s_stage + wv * 64 * kStageU2;
+  uint2 yq[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) yq[r] = make_uint2(0, 0);
+  EncColour<19, HIC_ENC_LA3, true> C;
+  const bool rev = E.alt && (u0 & 1);
+  C.init(E, y0, s, lane, 64, rev);
+  C.fold_rows(yq, rev);
+  for (int p = 0; p < 3; ++p) {  // Y block rows 0 and 1, then Cr | Cb
+    uint2 *row = st2 + lane * kStageU2;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) row[k] = make_uint2(yq[k].x ^ p, yq[k].y);
+    __builtin_amdgcn_wave_barrier();
+    int16_t *lo, *hi;
+    int64_t *rec;
+    if (p < 2) {
+      const int64_t b0 = (int64_t)(2 * u0 + p) * nbx + 64 * s;
+      lo = E.coef[0] + b0 * 64;
+      hi = lo + 32 * 64;
+      rec = E.rec[0] + (b0 >> 6) * 3;
+    } else {
+      const int64_t b0 = (int64_t)u0 * nbxc + 32 * s;
+      lo = E.coef[1] + b0 * 64;
+      hi = E.coef[2] + b0 * 64;
+      rec = E.rec[1] + (b0 >> 5) * 3;
+    }
+    enc_store(st2, lane, lo, hi);
+    if (lane == 0) {
+      rec[0] = yq[p].x;
+      rec[1] = yq[p].y;
+      rec[2] = p;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 }  // namespace
 }  // namespace hic
 
@@ -928,4 +992,44 @@ extern "C" int hic_encode420_rle_u8(const uint8_t *rgb, int64_t H, int64_t W, co
   else
     launch(k_encode420<0, false, true>);
   return check_launch("k_encode420 (one-pass)");
+}
+
+extern "C" int hic_probe_encode420(const uint8_t *rgb, int64_t H, int64_t W, int16_t *coef_y, int16_t *coef_cr,
+                                   int16_t *coef_cb, int64_t *rec_y, int64_t *rec_c, void *stream, void *ev_start,
+                                   void *ev_stop) {
+  if (!rgb || !coef_y || !coef_cr || !coef_cb || !rec_y || !rec_c) return arg_error("null pointer");
+  if (H < 16 || W < 512 || H % 16 || W % 512 || H >= (1 << 20) || W >= (1 << 20))
+    return arg_error("hic_probe_encode420 needs W %% 512 == 0 and H %% 16 == 0");
+  if (H * W * 3 > INT32_MAX) return arg_error("image exceeds 2 GiB");
+  if (reinterpret_cast<uintptr_t>(rgb) % 8 ||
+      (reinterpret_cast<uintptr_t>(coef_y) | reinterpret_cast<uintptr_t>(coef_cr) |
+       reinterpret_cast<uintptr_t>(coef_cb)) % 16)
+    return arg_error("alignment");
+  Enc420 E{};
+  E.rgb = rgb;
+  E.in_row0 = 0;
+  E.in_rows = (int)H;
+  E.H = (int)H;
+  E.W = (int)W;
+  E.out_row0 = 0;
+  E.out_rows = (int)H;
+  E.coef[0] = coef_y;
+  E.coef[1] = coef_cr;
+  E.coef[2] = coef_cb;
+  E.rec[0] = rec_y;
+  E.rec[1] = rec_c;
+  E.nstrips = (int)(W / 512);
+  E.wlast = 512;
+  E.nunits = E.nstrips * (int)(H / 16);
+  const int order = knob(HIC_KNOB_ENCODE_ORDER);
+  E.xcd = (order >> 1) & 1;
+  E.alt = (order >> 2) & 1;
+  const dim3 grid((unsigned)((E.nunits + HIC_ENC_WPB - 1) / HIC_ENC_WPB)), block(64 * HIC_ENC_WPB);
+  const hipStream_t s = as_stream(stream);
+  const hipEvent_t e0 = static_cast<hipEvent_t>(ev_start), e1 = static_cast<hipEvent_t>(ev_stop);
+  if (e0 || e1)
+    hipExtLaunchKernelGGL(k_probe_encode420, grid, block, 0, s, e0, e1, 0, E);
+  else
+    hipLaunchKernelGGL(k_probe_encode420, grid, block, 0, s, E);
+  return check_launch("k_probe_encode420");
 }

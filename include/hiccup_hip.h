@@ -96,11 +96,19 @@ int hic_stream_sync(void *stream);
  *    H x W plane (pitch W, multiples of 8) read as 8x8 blocks (one per lane), 128 B
  *    per block written to out (nblk x 64 int16) through the LDS stage and 1 KiB
  *    nontemporal stores of k_dct_pk, persistent grid: the pass's memory floor.
- *  waves_per_cu: persistent grid size (0 = default: 16 for the copy, 12 for the plane). */
+ *  waves_per_cu: persistent grid size (0 = default: 16 for the copy, 12 for the plane).
+ *  hic_probe_encode420: hic_encode420_u8's byte pattern without its arithmetic, on a
+ *    whole H x W RGB image (W % 512 == 0, H % 16 == 0): the same grid, unit order
+ *    (knob encode_order) and 19 row loads per 16-row unit, the LDS stage and 1 KiB
+ *    nontemporal stores of the Y / Cr / Cb blocks (coef_*: the encoder's outputs'
+ *    sizes) and one 24 B record per tile (rec_y: H/8 * W/512 records, rec_c: H/16 *
+ *    W/512): the fused kernel's memory floor. */
 int hic_probe_copy(const void *src, void *dst, int64_t bytes, int waves_per_cu, void *stream, void *ev_start,
                    void *ev_stop);
 int hic_probe_plane(const uint8_t *plane, int64_t H, int64_t W, int16_t *out, int waves_per_cu, void *stream,
                     void *ev_start, void *ev_stop);
+int hic_probe_encode420(const uint8_t *rgb, int64_t H, int64_t W, int16_t *coef_y, int16_t *coef_cr, int16_t *coef_cb,
+                        int64_t *rec_y, int64_t *rec_c, void *stream, void *ev_start, void *ev_stop);
 
 /* ---- forward transform: replaces transform.dct_channel (transform.py:182-193) =
  *      offset -128 (:186), split_matrix/pad (:33-42), dct2 (:67-84, scipy pocketfft

@@ -304,6 +304,31 @@ def test_measurement_probes():
     np.testing.assert_array_equal(got[:, 64:], swapped)
     with pytest.raises(ValueError):
         _lib.call("hic_probe_copy", device.ptr(a), device.ptr(b), 17, 0, device.stream_ptr(), None, None)
+    # hic_probe_encode420 (the fused encoder's byte pattern): every unit writes all
+    # its coefficient slots and its three records (record word 2 = the pass: 0 / 1
+    # for the unit's two Y block rows, 2 for its chroma), in every unit order
+    H, W = 80, 1024
+    rgb = device.to_device(np.random.default_rng(7).integers(0, 256, (H, W, 3), dtype=np.uint8))
+    for order in (0, 6):
+        co = [device.zeros(((H // 8) * (W // 8), 64), torch.int16)] + \
+             [device.zeros(((H // 16) * (W // 16), 64), torch.int16) for _ in range(2)]
+        for t in co:
+            t.fill_(0x5A5A)
+        ry = device.zeros(((H // 8) * (W // 512) * 3,), torch.int64)
+        rc = device.zeros(((H // 16) * (W // 512) * 3,), torch.int64)
+        ry.fill_(-7)
+        rc.fill_(-7)
+        with _lib.knobs(encode_order=order):
+            _lib.call("hic_probe_encode420", device.ptr(rgb), H, W, *[device.ptr(t) for t in co], device.ptr(ry),
+                      device.ptr(rc), device.stream_ptr(), None, None)
+        for t in co:
+            assert int((device.to_host(t) == 0x5A5A).sum()) < 16, order  # (a folded word may equal it by chance)
+        np.testing.assert_array_equal(device.to_host(ry).reshape(-1, 3)[:, 2],
+                                      np.repeat(np.arange(H // 8) % 2, W // 512), err_msg=str(order))
+        assert (device.to_host(rc).reshape(-1, 3)[:, 2] == 2).all(), order
+    with pytest.raises(ValueError):
+        _lib.call("hic_probe_encode420", device.ptr(rgb), H, 1000, *[device.ptr(t) for t in co], device.ptr(ry),
+                  device.ptr(rc), device.stream_ptr(), None, None)
 
 
 @pytest.mark.parametrize("var", range(4))

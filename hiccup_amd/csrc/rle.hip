@@ -713,11 +713,17 @@ __global__ __launch_bounds__(kScan16T) void k_rle_scan16b(RleJobs16 jobs, uint32
         }
         if (!ok) s_fail = 1;
       }
-      // ordered fold of this window (64 partitions at most per window; usually one)
-      for (int k = 0; k < 64 && q0 + k < p; ++k) {
-        const Agg ak{__shfl(a.first, k, 64), __shfl(a.last, k, 64), __shfl(a.cnt, k, 64)};
-        pre = agg_combine(pre, ak, M);
+      // the window's ordered total by a wave scan (agg_combine is associative):
+      // log2(64) steps instead of one serial combine per earlier partition (the
+      // 16K image has 512 partitions per channel, and its last ones folded them all)
+      Agg wi = a;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const Agg o = agg_shfl_up(wi, d);
+        if (lane >= d) wi = agg_combine(o, wi, M);
       }
+      const int lastl = (int)(p - q0 < 64 ? p - q0 - 1 : 63);
+      pre = agg_combine(pre, Agg{__shfl(wi.first, lastl, 64), __shfl(wi.last, lastl, 64), __shfl(wi.cnt, lastl, 64)}, M);
     }
     if (lane == 0) s_pre = pre;
   }

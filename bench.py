@@ -1030,6 +1030,10 @@ def main():
                      "note": "same sharded encode and steps with the stream left distributed on the ranks "
                              "(no gather); not the headline value"}
     per_rank_rows = in_rows if world == 1 else encs[0].rows[1] - encs[0].rows[0]
+    # read off the encoders now: the N > 1 extras below free them first
+    gather_bytes = ((encs[0].wire_bytes if stream_gather else
+                     sum(encs[0].ranges[k][-1][1] * (64 * 2 + 4) for k in pipeline.CHANNELS))
+                    if gather else None)
     extra_sharded = None
     link_gbs = None
     if world > 1 and args.dist_backend == "nccl" and not args.same_device:
@@ -1087,9 +1091,7 @@ def main():
                           % (world, "torch.distributed P2P" if rgather is None else "C-ABI hic_gather_bytes")
                           if gather else None,
                 "gather_kind": args.gather_kind if gather else None,
-                "gather_bytes_per_image": (encs[0].wire_bytes if stream_gather else
-                                           sum(encs[0].ranges[k][-1][1] * (64 * 2 + 4) for k in pipeline.CHANNELS))
-                if gather else None,
+                "gather_bytes_per_image": gather_bytes,
                 "gather_us_per_image": None if gather_us is None else round(gather_us, 2),
                 "gather_link": gather_link,
                 "xgmi_link_gbs_measured": link_gbs,

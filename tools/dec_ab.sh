@@ -2,7 +2,7 @@
 # dev: decode A/B, libraries alternating (new = the tree's, old = hiccup_amd/lib/libhiccup_hip_devold.so)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-out=gpurun_out/r4/dec_ab
+out=gpurun_out/r4/dec_ab_${1:-x}
 mkdir -p $out
 for r in 1 2; do
   for v in new old; do

@@ -592,29 +592,33 @@ def _extra_8k_jpeg_decode(steps, codec, device, hicimage, pipeline):
             "timed_decodes": steps}
 
 
-def measure_link(rank, world, group=None, nbytes=256 << 20, reps=5):
-    """The xGMI rate between rank 0 and rank 1, measured in this run: rank 0 sends
-    `nbytes` to rank 1 while rank 1 sends the same to rank 0 (one batch per
-    repetition, RCCL on the default stream), median of `reps` after one warmup.
-    Every rank joins the barriers; only ranks 0 and 1 move data.  Returns GB/s per
-    direction (None off ranks 0/1)."""
-    buf_s = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    buf_r = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+def measure_link(rank, world, group=None, nbytes=256 << 20, reps=5, device="cuda"):
+    """The xGMI rate of one link, measured in this run: every rank sends `nbytes` to
+    rank + 1 and receives as much from rank - 1 (a ring: each rank's traffic crosses
+    one link per direction, and every rank of the group takes part in each P2P batch,
+    as RCCL's batched P2P expects), one batch per repetition on the default stream,
+    the slowest rank's time, median of `reps` after one warmup.  Returns GB/s per
+    link and direction."""
+    buf_s = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    buf_r = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    nxt, prv = (rank + 1) % world, (rank - 1) % world
     times = []
     for i in range(reps + 1):
         dist.barrier(group=group)
-        torch.cuda.synchronize()
+        if device == "cuda":
+            torch.cuda.synchronize()
         t0 = time.perf_counter()
-        if rank in (0, 1):
-            peer = 1 - rank
-            ops = [dist.P2POp(dist.isend, buf_s, peer, group=group), dist.P2POp(dist.irecv, buf_r, peer, group=group)]
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
-        torch.cuda.synchronize()
+        ops = [dist.P2POp(dist.isend, buf_s, nxt, group=group), dist.P2POp(dist.irecv, buf_r, prv, group=group)]
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+        if device == "cuda":
+            torch.cuda.synchronize()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
         if i:
-            times.append(time.perf_counter() - t0)
+            times.append(float(t.item()))
     del buf_s, buf_r
-    return round(nbytes / float(np.median(times)) / 1e9, 1) if rank in (0, 1) else None
+    return round(nbytes / float(np.median(times)) / 1e9, 1)
 
 
 def extra_16k_roundtrip_sharded(rank, world, backend, steps=4):

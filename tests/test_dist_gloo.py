@@ -298,3 +298,26 @@ def test_sharded_exchange_gloo(world, H, W, flat):
     exp.update({"group_%d" % r: True for r in range(world)})
     exp.update({"stream_%d" % r: True for r in range(world)})
     assert dict(results) == exp
+
+
+def _link_worker(rank, world, port, results):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    try:
+        results[rank] = bench.measure_link(rank, world, nbytes=1 << 16, reps=2, device="cpu")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_measure_link_ring_gloo(world):
+    """bench.measure_link (the N > 1 line's in-run link rate): a ring in which every
+    rank takes part in each P2P batch, so it completes at any world size (gloo on
+    CPU here; RCCL on the node) and every rank reports the same slowest-rank rate."""
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_link_worker, args=(world, _free_port(), results), nprocs=world, join=True)
+    got = dict(results)
+    assert sorted(got) == list(range(world))
+    assert len(set(got.values())) == 1 and list(got.values())[0] > 0

@@ -514,16 +514,25 @@ def test_onepass_streams_and_small_cap():
 @pytest.mark.timeout(900)
 def test_16k_roundtrip_vs_oracle():
     """BASELINE configs[4] on one GPU: a 16384 x 16384 random RGB image (the
-    config's seed) through the device encoder and decoder.  The symbol stream is
-    checked through size-independent properties (counts, DC integration, EOB) and
-    the reconstruction bit-exactly against the CPU restatement of the reference's
-    chain (cvtColor -> pyrDown -> dct_channel -> inv_dct_channel -> pyrUp ->
-    cvtColor, compression.py:16-56); PSNR vs the input is the same number."""
+    config's seed) through the device encoder and decoder.  The encoder's
+    coefficients, DC differences and both symbol arrays equal the CPU restatement's
+    (the C oracle's colour, DCT, zig-zag, DPCM and RLE of the whole image; round 4,
+    before only properties of the stream were checked at this size), the stream's
+    properties hold (counts, DC integration, EOB), and the reconstruction is
+    bit-exact against the restatement of the reference's chain (cvtColor ->
+    pyrDown -> dct_channel -> inv_dct_channel -> pyrUp -> cvtColor,
+    compression.py:16-56); PSNR vs the input is the same number."""
     H = W = 16384
     rng = np.random.default_rng(5)
     rgb = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
     enc = pipeline.Encoder(H, W, index=True)
     enc.encode(device.to_device(rgb))
+    got = enc.result()
+    exp = _oracle_encode(rgb)
+    for k in pipeline.CHANNELS:
+        for j, what in enumerate(("coef", "dc", "sym_len", "sym_val")):
+            np.testing.assert_array_equal(np.asarray(got[k][j]).astype(np.int32), exp[k][j], err_msg=(k, what))
+    del got, exp
     counts = enc.counts.cpu().tolist()
     nblk = {k: enc.coef[k].shape[0] for k in pipeline.CHANNELS}
     for k, c in zip(pipeline.CHANNELS, counts):

@@ -287,7 +287,7 @@ def _decode_channel(dc, lens, vals, n, shape, bs):
         assert int(status.cpu()[0]) == nblk * sub
     raster = device.zeros((H, W), torch.int32)
     _lib.call("hic_izigzag_blocks_i32", device.ptr(blocks), H, W, bs, device.ptr(raster), device.stream_ptr())
-    return device.to_host(raster).astype(np.float64)
+    return device.to_host_f64(raster)
 
 
 # ------------------------------------------------------------------ out of scope

@@ -69,6 +69,38 @@ def to_host(t):
     return t.cpu().numpy()
 
 
+_staging = None  # pinned host staging for to_host_f64 (grown on demand, reused)
+_cast_pool = None
+_staging_lock = None
+
+
+def to_host_f64(t):
+    """A device int32 tensor as a new float64 numpy array (the reference's planes are
+    float64): one DMA into a reused pinned buffer, then the cast split over host
+    threads.  A pageable copy runs at ~4 GB/s here and the single-threaded cast after
+    it doubled the time (8K luma: 48 ms, tools/prof_d2h.py)."""
+    global _staging, _cast_pool, _staging_lock
+    import threading
+    from concurrent.futures import ThreadPoolExecutor
+    assert t.dtype == torch.int32 and t.is_cuda
+    n = t.numel()
+    sync()
+    if _staging_lock is None:
+        _staging_lock = threading.Lock()
+    out = np.empty(n, np.float64)
+    with _staging_lock:  # one staging buffer: callers on several threads take turns
+        if _staging is None or _staging.numel() < n:
+            _staging = torch.empty(max(n, 1), dtype=torch.int32, pin_memory=True)
+        _staging[:n].copy_(t.reshape(-1))
+        src = _staging[:n].numpy()
+        if _cast_pool is None:
+            _cast_pool = ThreadPoolExecutor(8)
+        k = 8 if n >= (1 << 20) else 1
+        bounds = [(i * n // k, (i + 1) * n // k) for i in range(k)]
+        list(_cast_pool.map(lambda ab: np.copyto(out[ab[0]:ab[1]], src[ab[0]:ab[1]]), bounds))
+    return out.reshape(tuple(t.shape))
+
+
 class KernelEvents:
     """A pair of HIP events that a *_timed entry point fills with one kernel's
     own begin / end timestamps (hipExtLaunchKernelGGL)."""

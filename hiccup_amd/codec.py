@@ -218,7 +218,20 @@ def jpeg_decode(hic_image):
     coded streams are decoded on the GPU (hic_huffman_decode, in the reference's
     order: DC, AC values, AC lengths, codec.py:372-388) and stay there for the RLE
     decode, DC integration and izigzag (hic_rle_decode_i32, hic_izigzag_blocks_i32);
-    only the nine trees (from the tables) are built on the host."""
+    only the nine trees (from the tables) are built on the host.  Python's cyclic
+    collector is paused for the call: the trees' many small nodes set off full
+    collections that cost 15-60 ms at 8K (tools/prof_jdec.py)."""
+    import gc
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        return _jpeg_decode(hic_image)
+    finally:
+        if was:
+            gc.enable()
+
+
+def _jpeg_decode(hic_image):
     utils.debug_msg("JPEG decode")
     assert hic_image.hic_type == model.Compression.JPEG
     p = hic_image.payloads

@@ -64,6 +64,12 @@ def _i32(a, what):
     return a.astype(np.int32)
 
 
+def _i32_device(a, what):
+    """_i32's checks and result as an int32 device tensor (large float planes are
+    checked and cast on the GPU: device.to_device_i32)."""
+    return device.to_device_i32(a, "%s must be integer-valued" % what, "%s out of int32 range" % what)
+
+
 def differential_coding(blocks):
     """codec.py:47-52: [dc0, dc1 - dc0, ...] over the blocks' [0][0] entries."""
     return utils.differences([b[0][0] for b in blocks])
@@ -153,11 +159,11 @@ def encode_channel_device(raster_dev, H, W, bs, stream=None):
 def encode_channel(plane, bs=None):
     """(dc_diffs, ac_lengths, ac_values) numpy arrays for one coefficient plane."""
     bs = settings.JPEG_BLOCK_SIZE if bs is None else bs
-    p = _i32(plane, "coefficient plane")
+    p = _i32_device(plane, "coefficient plane")
     if p.ndim != 2:
         raise ValueError("expected a 2-D coefficient plane")
     H, W = p.shape
-    dc, Ls, Vs, cnt = encode_channel_device(device.to_device(p), H, W, bs)
+    dc, Ls, Vs, cnt = encode_channel_device(p, H, W, bs)
     count = int(device.to_host(cnt)[0])
     return dc.cpu().numpy(), Ls[:count].cpu().numpy(), Vs[:count].cpu().numpy()
 
@@ -195,10 +201,10 @@ def jpeg_encode(compressed):
         # the reference's DC keys are elements of the plane (utils.differences over
         # block[0][0]): numpy scalars of its dtype
         dc_type[k] = np.asarray(v).dtype.type
-        p = _i32(v, "coefficient plane")
+        p = _i32_device(v, "coefficient plane")
         if p.ndim != 2:
             raise ValueError("expected a 2-D coefficient plane")
-        dc, Ls, Vs, cnt = encode_channel_device(device.to_device(p), p.shape[0], p.shape[1], bs)
+        dc, Ls, Vs, cnt = encode_channel_device(p, p.shape[0], p.shape[1], bs)
         count = int(device.to_host(cnt)[0])
         # trees per channel: DC differences, AC values, AC lengths (codec.py:304-313)
         keys[k] = ((dc, dc.numel()), (Vs, count), (Ls, count))

@@ -44,24 +44,23 @@ def jpeg_compression(rgb_image):
         "cr": transform.dct_channel_device(cr, 1),
         "cb": transform.dct_channel_device(cb, 1),
     }
-    device.sync()
-    return model.CompressedImage.from_dict(dict((k, v.cpu().numpy()) for k, v in planes.items()))
+    return model.CompressedImage.from_dict(dict((k, device.to_host(v)) for k, v in planes.items()))
 
 
 def jpeg_decompression(d):
     """compression.py:42-56: CompressedImage -> (2h) x (2w) x 3 uint8 RGB."""
     _check_block()
-    lum = transform._as_i32_plane(d.luminance_component)
-    cr = transform._as_i32_plane(d.red_chrominance_component)
-    cb = transform._as_i32_plane(d.blue_chrominance_component)
+    lum = transform._as_i32_plane_device(d.luminance_component)
+    cr = transform._as_i32_plane_device(d.red_chrominance_component)
+    cb = transform._as_i32_plane_device(d.blue_chrominance_component)
     assert cr.shape == cb.shape  # transform.force_merge
     H, W = lum.shape
     h, w = cr.shape
     if 2 * h > H or 2 * w > W:
         raise ValueError("luminance plane smaller than the up-sampled chroma planes")
-    y = transform.inv_dct_channel_device(device.to_device(lum), H, W, 0)
-    crp = transform.inv_dct_channel_device(device.to_device(cr), h, w, 1)
-    cbp = transform.inv_dct_channel_device(device.to_device(cb), h, w, 1)
+    y = transform.inv_dct_channel_device(lum, H, W, 0)
+    crp = transform.inv_dct_channel_device(cr, h, w, 1)
+    cbp = transform.inv_dct_channel_device(cb, h, w, 1)
     rgb = device.empty((2 * h, 2 * w, 3), torch.uint8)
     _lib.call("hic_ycrcb420_to_rgb", device.ptr(y), y.stride(0), device.ptr(crp), device.ptr(cbp), h, w,
               device.ptr(rgb), device.stream_ptr())

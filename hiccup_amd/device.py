@@ -40,8 +40,18 @@ def ptr(t):
 
 
 def to_device(a):
+    """A host array as a new device tensor.  Large arrays (>= 4 MiB) go through a
+    reused pinned buffer (threaded host copy, then one DMA): a pageable copy runs at
+    ~4 GB/s on the MI355X boxes (tools/prof_d2h.py)."""
     require_gpu()
-    return torch.from_numpy(np.ascontiguousarray(a)).to("cuda")
+    a = np.ascontiguousarray(a)
+    if a.nbytes < _PIN_MIN or a.dtype.hasobject:
+        return torch.from_numpy(a).to("cuda")
+    with _lock():
+        st = _stage(a.nbytes)
+        dst = st[:a.nbytes].numpy().view(a.dtype).reshape(a.shape)
+        _par_copy(dst, a)
+        return st[:a.nbytes].view(torch.from_numpy(a[:0].reshape(-1)).dtype).view(tuple(a.shape)).to("cuda")
 
 
 def empty(shape, dtype):
@@ -65,40 +75,98 @@ def sync(stream=None):
 
 
 def to_host(t):
+    """A device tensor as a new numpy array (through the pinned buffer when large)."""
     sync()
-    return t.cpu().numpy()
-
-
-_staging = None  # pinned host staging for to_host_f64 (grown on demand, reused)
-_cast_pool = None
-_staging_lock = None
+    nbytes = t.numel() * t.element_size()
+    if nbytes < _PIN_MIN or not t.is_cuda:
+        return t.cpu().numpy()
+    t = t.contiguous()
+    out = np.empty(tuple(t.shape), torch.empty(0, dtype=t.dtype).numpy().dtype)
+    with _lock():
+        st = _stage(nbytes)
+        st[:nbytes].view(t.dtype).copy_(t.reshape(-1))
+        _par_copy(out.reshape(-1), st[:nbytes].numpy().view(out.dtype))
+    return out
 
 
 def to_host_f64(t):
     """A device int32 tensor as a new float64 numpy array (the reference's planes are
-    float64): one DMA into a reused pinned buffer, then the cast split over host
-    threads.  A pageable copy runs at ~4 GB/s here and the single-threaded cast after
-    it doubled the time (8K luma: 48 ms, tools/prof_d2h.py)."""
-    global _staging, _cast_pool, _staging_lock
-    import threading
-    from concurrent.futures import ThreadPoolExecutor
+    float64): one DMA into the pinned buffer, then the cast split over host threads.
+    A pageable copy runs at ~4 GB/s here and the single-threaded cast after it
+    doubled the time (8K luma: 48 vs 17 ms, tools/prof_d2h.py)."""
     assert t.dtype == torch.int32 and t.is_cuda
-    n = t.numel()
     sync()
-    if _staging_lock is None:
-        _staging_lock = threading.Lock()
+    t = t.contiguous()
+    n = t.numel()
     out = np.empty(n, np.float64)
-    with _staging_lock:  # one staging buffer: callers on several threads take turns
-        if _staging is None or _staging.numel() < n:
-            _staging = torch.empty(max(n, 1), dtype=torch.int32, pin_memory=True)
-        _staging[:n].copy_(t.reshape(-1))
-        src = _staging[:n].numpy()
-        if _cast_pool is None:
-            _cast_pool = ThreadPoolExecutor(8)
-        k = 8 if n >= (1 << 20) else 1
-        bounds = [(i * n // k, (i + 1) * n // k) for i in range(k)]
-        list(_cast_pool.map(lambda ab: np.copyto(out[ab[0]:ab[1]], src[ab[0]:ab[1]]), bounds))
+    with _lock():
+        st = _stage(4 * n)
+        st[:4 * n].view(torch.int32).copy_(t.reshape(-1))
+        _par_copy(out, st[:4 * n].numpy().view(np.int32))
     return out.reshape(tuple(t.shape))
+
+
+def to_device_i32(a, nonint_msg, range_msg):
+    """A host array of integer values as a new int32 device tensor, refusing
+    non-integer (ValueError(nonint_msg)) or out-of-int32 (ValueError(range_msg))
+    values as the host checks did.  Large float arrays (the reference's float64
+    planes) are checked and cast on the GPU after one pinned copy: np.mod, min / max
+    and two casts of an 8K float64 plane took ~0.2 s on the host."""
+    a = np.asarray(a)
+    if a.dtype == np.int32:  # already in range
+        return to_device(a)
+    if a.dtype.kind != "f" or a.nbytes < _PIN_MIN:
+        if a.size and a.dtype.kind not in "iub" and not np.all(np.mod(a, 1) == 0):
+            raise ValueError(nonint_msg)
+        b = a.astype(np.int64)
+        if b.size and (b.min() < -(1 << 31) or b.max() >= (1 << 31)):
+            raise ValueError(range_msg)
+        return to_device(b.astype(np.int32))
+    t = to_device(a)
+    if not bool((torch.remainder(t, 1) == 0).all()):
+        raise ValueError(nonint_msg)
+    if bool(((t < -(1 << 31)) | (t >= (1 << 31))).any()):
+        raise ValueError(range_msg)
+    return t.to(torch.int32)
+
+
+# one pinned host staging buffer (grown on demand, reused; callers on several
+# threads take turns) and a small thread pool for the host side of the copies
+_PIN_MIN = 4 << 20
+_staging = None
+_staging_lock = None
+_pool = None
+
+
+def _lock():
+    global _staging_lock
+    if _staging_lock is None:
+        import threading
+        _staging_lock = threading.Lock()
+    return _staging_lock
+
+
+def _stage(nbytes):
+    """The pinned uint8 buffer, at least nbytes long (call with _lock() held)."""
+    global _staging
+    if _staging is None or _staging.numel() < nbytes:
+        _staging = None
+        _staging = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, pin_memory=True)
+    return _staging
+
+
+def _par_copy(dst, src):
+    """dst[...] = src (same shape; a cast if the dtypes differ) in 8 row ranges on
+    host threads (numpy releases the GIL while it copies)."""
+    global _pool
+    if _pool is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _pool = ThreadPoolExecutor(8)
+    d, s_ = dst.reshape(-1), src.reshape(-1)
+    n = d.size
+    k = 8 if n >= (1 << 20) else 1
+    bounds = [(i * n // k, (i + 1) * n // k) for i in range(k)]
+    list(_pool.map(lambda ab: np.copyto(d[ab[0]:ab[1]], s_[ab[0]:ab[1]], casting="unsafe"), bounds))
 
 
 class KernelEvents:

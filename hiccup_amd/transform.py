@@ -126,6 +126,16 @@ def _as_i32_plane(channel):
     return ch.astype(np.int32)
 
 
+def _as_i32_plane_device(channel):
+    """_as_i32_plane's checks and result, as an int32 device tensor (large float
+    planes are checked and cast on the GPU, device.to_device_i32)."""
+    ch = np.asarray(channel)
+    if ch.ndim != 2:
+        raise ValueError("expected a 2-D channel, got shape %s" % (ch.shape,))
+    return device.to_device_i32(ch, "inv_dct_channel expects integer-valued coefficients",
+                                "coefficients out of int32 range")
+
+
 def dct_channel_device(plane_dev, table_id, layout=_lib.LAYOUT_RASTER_I32, out=None, stream=None):
     """Device-resident forward transform: uint8 (H, W) CUDA tensor -> coefficients."""
     H, W = plane_dev.shape
@@ -161,9 +171,9 @@ def dct_channel(channel, quantization_table, block_size=8):
 def inv_dct_channel(channel, quantization_table, block_size=8):
     """transform.py:169-179: coefficients H x W -> uint8 H x W pixels."""
     _check_block_size(block_size)
-    coef = _as_i32_plane(channel)
+    coef = _as_i32_plane_device(channel)
     H, W = coef.shape
-    out = inv_dct_channel_device(device.to_device(coef), H, W, model.table_id(quantization_table))
+    out = inv_dct_channel_device(coef, H, W, model.table_id(quantization_table))
     return device.to_host(out)
 
 

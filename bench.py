@@ -592,6 +592,39 @@ def _extra_8k_jpeg_decode(steps, codec, device, hicimage, pipeline):
             "timed_decodes": steps}
 
 
+def extra_8k_reference_api(steps=3):
+    """The drop-in surface at 8K from host arrays, as a user of the reference calls
+    it: compression.jpeg_compression (RGB -> quantized planes), codec.jpeg_encode
+    (-> HicImage), codec.jpeg_decode (HicImage -> planes) and
+    compression.jpeg_decompression (-> RGB); wall time per call, median of `steps`
+    after one untimed call, host copies included (PCIe-inclusive, never the headline)."""
+    from hiccup_amd import codec, compression, settings
+    debug, settings.DEBUG = settings.DEBUG, False
+    try:
+        rgb = np.random.default_rng(1).integers(0, 256, (H8K, W8K, 3), dtype=np.uint8)
+
+        def med(f):
+            ts, r = [], None
+            for _ in range(steps + 1):
+                t = time.perf_counter()
+                r = f()
+                ts.append(time.perf_counter() - t)
+            return r, round(float(np.median(ts[1:])) * 1e3, 1)
+
+        ci, t_comp = med(lambda: compression.jpeg_compression(rgb))
+        hic, t_enc = med(lambda: codec.jpeg_encode(ci))
+        ci2, t_dec = med(lambda: codec.jpeg_decode(hic))
+        rec, t_decomp = med(lambda: compression.jpeg_decompression(ci2))
+        same = all(np.array_equal(a, b) for a, b in zip(ci.as_dict.values(), ci2.as_dict.values()))
+        return {"workload": "8K RGB through the reference API from host arrays (jpeg_compression, jpeg_encode, "
+                            "jpeg_decode, jpeg_decompression), host copies included",
+                "ms_jpeg_compression": t_comp, "ms_jpeg_encode": t_enc, "ms_jpeg_decode": t_dec,
+                "ms_jpeg_decompression": t_decomp, "planes_equal_after_entropy_round_trip": same,
+                "rgb_out_shape": list(rec.shape), "timed_calls": steps}
+    finally:
+        settings.DEBUG = debug
+
+
 def measure_link(rank, world, group=None, nbytes=256 << 20, reps=5, device="cuda"):
     """The xGMI rate of one link, measured in this run: every rank sends `nbytes` to
     rank + 1 and receives as much from rank - 1 (a ring: each rank's traffic crosses
@@ -1156,7 +1189,8 @@ def main():
                                     "8k_luma_dct_back_to_back": extra_8k_luma_batched(),
                                     "8k_jpeg_decode": extra_8k_jpeg_decode(),
                                     "8k_encode_from_host": extra_8k_encode_from_host(),
-                                    "16k_roundtrip": extra_16k_roundtrip()}
+                                    "16k_roundtrip": extra_16k_roundtrip(),
+                                    "8k_reference_api": extra_8k_reference_api()}
         if extra_sharded is not None:
             out["extra_configs"] = {"16k_roundtrip": extra_sharded}
         if not args.no_cpu_baseline and world == 1:

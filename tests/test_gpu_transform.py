@@ -340,3 +340,38 @@ def test_mfma_plane_variants(kind, var):
     for H, W in ((8 * 33, 8 * 130), (8 * 160, 8 * 320)):
         with _lib.knobs(dct_mfma=var):
             test_plane_dct_rle_records(kind, _lib.DCT_PATH_MFMA, H, W)
+
+
+@pytest.mark.parametrize("dtype", [np.uint8, np.int16, np.int32, np.float32, np.float64, np.bool_])
+def test_pinned_host_copies(dtype):
+    """device.to_device / to_host above the pinned-staging threshold (4 MiB) return
+    new arrays equal to the input for every dtype the API moves, in both directions,
+    back to back (the staging buffer is reused and grown), and to_host_f64 /
+    to_device_i32 keep the host checks' results and errors."""
+    rng = np.random.default_rng(11)
+    for shape in [(1500, 1000, 3), (2049, 1031)]:
+        a = (rng.integers(0, 2, shape) if dtype == np.bool_ else rng.integers(-100, 100, shape)).astype(dtype)
+        t = device.to_device(a)
+        assert t.shape == a.shape and t.is_cuda
+        b = device.to_host(t)
+        assert b.dtype == a.dtype and b.shape == a.shape
+        np.testing.assert_array_equal(b, a)
+        t.add_(1) if dtype != np.bool_ else t.logical_not_()
+        np.testing.assert_array_equal(b, a)  # a copy, not a view of the staging buffer
+    p = rng.integers(-5000, 5000, (2048, 1024)).astype(np.int32)
+    f = device.to_host_f64(device.to_device(p))
+    assert f.dtype == np.float64
+    np.testing.assert_array_equal(f, p)
+    g = device.to_device_i32(p.astype(np.float64), "bad", "range")
+    assert g.dtype == torch.int32
+    np.testing.assert_array_equal(device.to_host(g), p)
+    q = p.astype(np.float64)
+    q[7, 9] = 0.5
+    with pytest.raises(ValueError, match="bad"):
+        device.to_device_i32(q, "bad", "range")
+    q[7, 9] = 2.0 ** 31
+    with pytest.raises(ValueError, match="range"):
+        device.to_device_i32(q, "bad", "range")
+    q[7, 9] = np.nan
+    with pytest.raises(ValueError, match="bad"):
+        device.to_device_i32(q, "bad", "range")

@@ -78,9 +78,6 @@ def parse():
                     help="HIP streams the consecutive images alternate over (each image's chain stays on one); "
                          "default 4 on one GPU (0.1020-0.1028 vs 0.1025-0.1037 ms/step for 2 in 3 alternating "
                          "pairs, profiles/r03/s2/streams/), 2 with N > 1 ranks")
-    ap.add_argument("--onepass", action="store_true",
-                    help="single GPU: the one-pass encode kernel (hic_encode420_rle_u8) instead of the fused "
-                         "transform + scan / emit launches (measured slower; DESIGN.md section 5)")
     ap.add_argument("--unfused", action="store_true",
                     help="A/B: colour and DCT as two kernels (the planes round-trip HBM) instead of hic_encode420_u8")
     ap.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
@@ -154,15 +151,25 @@ def cpu_baseline(budget_s):
 def plane_kernel(tmf):
     """The forward plane kernel the library runs for ZIGZAG_I16 planes (dct_path knob)."""
     from hiccup_amd import _lib
-    if _lib.get_knob("dct_path") == _lib.DCT_PATH_MFMA:
-        return "k_dct_mfma<%d> (integer MFMA)" % tmf
+    if _lib.get_knob("dct_path") == _lib.DCT_PATH_PK:
+        return "k_dct_pk<%d> (packed float32 AAN, cooperative float64 redo of flagged blocks)" % tmf
     return "k_dct_planes<-1,ZIGZAG_I16,%d> (float64 AAN)" % tmf
 
 
-def extra_4k_luma(steps=20, floor_us=None):
+def spread(ts_us):
+    """min / median / max / p10 / p90 of per-launch times (us)."""
+    ts = np.asarray(ts_us, dtype=np.float64)
+    return {"min": round(float(ts.min()), 2), "p10": round(float(np.percentile(ts, 10)), 2),
+            "median": round(float(np.median(ts)), 2), "p90": round(float(np.percentile(ts, 90)), 2),
+            "max": round(float(ts.max()), 2), "n": int(ts.size)}
+
+
+def extra_4k_luma(steps=24, warmup=8, floor_us=None):
     """BASELINE configs[1]: 4096 x 4096 random luminance, DCT + quantize + zig-zag on
     one GPU (hic_dct_quant_u8_timed: the launch's own begin / end timestamps), with
-    >= 1.2 GB of rotating planes so every launch reads HBM, not the Infinity Cache."""
+    >= 1.2 GB of rotating planes so every launch reads HBM, not the Infinity Cache.
+    The median over `steps` launches after `warmup` untimed ones (round 4 reported a
+    mean of 20 after 3, which one slow launch moved by 47 %), with the spread."""
     from hiccup_amd import _lib, device
     n = 4096
     rot = int(np.ceil(ROT_BYTES / (n * n * 3)))
@@ -177,18 +184,21 @@ def extra_4k_luma(steps=20, floor_us=None):
         _lib.call("hic_dct_quant_u8_timed", device.ptr(p), n, n, n, _lib.TABLE_LUMINANCE, _lib.LAYOUT_ZIGZAG_I16,
                   device.ptr(o), None, ev.start if ev else None, ev.stop if ev else None)
 
-    for i in range(3):
+    for i in range(warmup):
         launch(i)
     torch.cuda.synchronize()
     for i in range(steps):
-        launch(3 + i, evs[i])
+        launch(warmup + i, evs[i])
     torch.cuda.synchronize()
-    us = float(np.mean([e.elapsed_ms() for e in evs])) * 1e3
+    ts = [e.elapsed_ms() * 1e3 for e in evs]
+    us = float(np.median(ts))
     gbs = n * n * 3 / (us * 1e-6) / 1e9
+    del planes, outs
+    torch.cuda.empty_cache()
     return {"workload": "4096x4096 uint8 luminance -> quantized int16 zig-zag blocks (BASELINE configs[1])",
-            "kernel": plane_kernel(-1), "avg_launch_us": round(us, 2),
+            "kernel": plane_kernel(-1), "median_launch_us": round(us, 2), "launch_us": spread(ts),
             "mpix_s": round(n * n / us, 1), "achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
-            "algorithmic_bytes": n * n * 3, "timed_launches": steps,
+            "algorithmic_bytes": n * n * 3, "timed_launches": steps, "warmup_launches": warmup,
             "memory_floor_us_measured": floor_us,
             "frac_of_measured_floor": round(floor_us / us, 4) if floor_us else None}
 
@@ -299,50 +309,86 @@ def extra_8k_plane_dct(steps=24, luma_only=False, floor_us=None):
     return out
 
 
-def extra_8k_luma_batched(nplanes=8, steps=12):
-    """north_star's DCT+quantize pass measured the way the product runs planes back to
-    back: ONE hic_dct_quant_rle_u8_batch launch over `nplanes` 8K luminance planes of
-    consecutive images (each 4320 x 7680 uint8 -> quantized int16 zig-zag blocks + RLE
-    tile records), >= 1.2 GB rotating, timed by the launch's own events; the figure
-    is launch time / nplanes (the per-launch ramp and tail amortised over the batch).
-    Per-launch spread (min / median / max) is reported beside it."""
+def _luma_sets(nplanes, records, seed=12):
+    """Rotating sets (>= 1.2 GB in all) of `nplanes` 8K luminance planes with their
+    outputs and a hic_dct_plane_job array each (records: RLE workspaces, else NULL =
+    the records-free pass)."""
     from hiccup_amd import _lib, device
     h, w = H8K, W8K
     px = h * w
-    per_set = nplanes * 3 * px
-    rot = max(2, int(np.ceil(ROT_BYTES / per_set)))
+    rot = max(2, int(np.ceil(ROT_BYTES / (nplanes * 3 * px))))
     g = torch.Generator(device="cuda")
-    g.manual_seed(12)
+    g.manual_seed(seed)
     nblk = px // 64
     sets = []
     for _ in range(rot):
         planes = [torch.randint(0, 256, (h, w), dtype=torch.uint8, device="cuda", generator=g) for _ in range(nplanes)]
         outs = [device.empty((nblk, 64), torch.int16) for _ in range(nplanes)]
-        wss = [device.workspace(_lib.load().hic_rle_workspace_bytes(nblk, 64)) for _ in range(nplanes)]
+        wss = [device.workspace(_lib.load().hic_rle_workspace_bytes(nblk, 64)) if records else None
+               for _ in range(nplanes)]
         jobs = (_lib.DctPlaneJob * nplanes)()
         for i in range(nplanes):
-            jobs[i] = _lib.DctPlaneJob(planes[i].data_ptr(), h, w, w, 0, outs[i].data_ptr(), wss[i].data_ptr())
+            jobs[i] = _lib.DctPlaneJob(planes[i].data_ptr(), h, w, w, 0, outs[i].data_ptr(),
+                                       wss[i].data_ptr() if records else None)
         sets.append((planes, outs, wss, jobs))
+    return sets
+
+
+def _time_batches(sets, nplanes, steps, warmup):
+    from hiccup_amd import _lib, device
+    rot = len(sets)
     evs = [device.KernelEvents() for _ in range(steps)]
-    for i in range(3):
+    for i in range(warmup):
         _lib.call("hic_dct_quant_rle_u8_batch", nplanes, sets[i % rot][3], 15, device.stream_ptr(), None, None)
     for i, e in enumerate(evs):
-        _lib.call("hic_dct_quant_rle_u8_batch", nplanes, sets[(3 + i) % rot][3], 15, device.stream_ptr(), e.start,
-                  e.stop)
+        _lib.call("hic_dct_quant_rle_u8_batch", nplanes, sets[(warmup + i) % rot][3], 15, device.stream_ptr(),
+                  e.start, e.stop)
     torch.cuda.synchronize()
-    ts = np.array([e.elapsed_ms() for e in evs]) * 1e3
-    us = float(np.median(ts)) / nplanes
-    gbs = 3 * px / (us * 1e-6) / 1e9
+    return [e.elapsed_ms() * 1e3 for e in evs]
+
+
+def extra_8k_luma_batched(nplanes=16, steps=16, warmup=8, floor_us_per_plane=None):
+    """north_star's DCT+quantize pass measured the way the product runs planes back to
+    back: ONE hic_dct_quant_rle_u8_batch launch over `nplanes` 8K luminance planes of
+    consecutive images (each 4320 x 7680 uint8 -> quantized int16 zig-zag blocks),
+    >= 1.2 GB rotating, timed by the launch's own events; the figure is the median
+    launch time / nplanes (the per-launch ramp and tail amortised over the batch).
+    Two variants: records-free (DCT + quantize + zig-zag: north_star's pass and
+    what transform.dct_channel / configs[1] run; the headline of this entry) and with
+    the RLE tile records fused into the epilogue (what the two-kernel chain runs);
+    plus the records-free pass as one launch per plane."""
+    h, w = H8K, W8K
+    px = h * w
+    out = {"workload": "%d x 8K luminance planes (4320 x 7680 uint8, consecutive images) per launch -> quantized "
+                       "int16 zig-zag blocks: north_star's DCT+quantize pass back to back (SURVEY.md 8(d): >= 0.70 "
+                       "= <= 17.8 us per plane)" % nplanes,
+           "kernel": plane_kernel(-1), "planes_per_launch": nplanes, "algorithmic_bytes_per_plane": 3 * px}
+    for records in (False, True):
+        sets = _luma_sets(nplanes, records)
+        ts = _time_batches(sets, nplanes, steps, warmup)
+        del sets
+        torch.cuda.empty_cache()
+        us = float(np.median(ts)) / nplanes
+        gbs = 3 * px / (us * 1e-6) / 1e9
+        v = {"us_per_plane": round(us, 2), "launch_us": spread(ts), "achieved_gbs": round(gbs, 1),
+             "frac": round(gbs / HBM_PEAK_GBS, 4), "timed_launches": steps, "warmup_launches": warmup}
+        if records:
+            v["kernel"] = plane_kernel(15)
+            out["with_rle_records"] = v
+        else:
+            out.update(v)
+            if floor_us_per_plane:
+                out["memory_floor_us_per_plane"] = floor_us_per_plane
+                out["frac_of_measured_floor"] = round(floor_us_per_plane / us, 4)
+    sets = _luma_sets(1, False, seed=13)
+    ts = _time_batches(sets, 1, 24, 8)
     del sets
     torch.cuda.empty_cache()
-    return {"workload": "%d x 8K luminance planes (4320 x 7680 uint8, consecutive images) per launch -> quantized "
-                        "int16 zig-zag blocks + RLE tile records: north_star's DCT+quantize pass back to back "
-                        "(SURVEY.md 8(d): >= 0.70 = <= 17.8 us per plane)" % nplanes,
-            "kernel": plane_kernel(15),
-            "planes_per_launch": nplanes, "us_per_plane": round(us, 2),
-            "launch_us_min_med_max": [round(float(v), 2) for v in (ts.min(), np.median(ts), ts.max())],
-            "achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_plane": 3 * px,
-            "timed_launches": steps}
+    us = float(np.median(ts))
+    gbs = 3 * px / (us * 1e-6) / 1e9
+    out["single_launch"] = {"median_launch_us": round(us, 2), "launch_us": spread(ts), "achieved_gbs": round(gbs, 1),
+                            "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    return out
 
 
 def measure_floors(steps=20):
@@ -808,8 +854,7 @@ def main():
                                                fused=False if args.unfused else None)
     else:
         H = H0
-        make = lambda j: pipeline.Encoder(H0, W0, fused=False if args.unfused else None,  # noqa: E731
-                                          onepass=True if args.onepass else None)
+        make = lambda j: pipeline.Encoder(H0, W0, fused=False if args.unfused else None)  # noqa: E731
     encs = [make(j) for j in range(n_enc)]  # rotate outputs too (~1.2 GB per 4)
     span = encs[0].span if world > 1 else (0, H)
     in_rows = span[1] - span[0]
@@ -917,9 +962,9 @@ def main():
         return float(t.item())
 
     elapsed = max_over_ranks(elapsed)
-    # spread: the same K-step region (same brackets) repeated; `value` stays the
-    # first region's.  The regions are ~2 ms of wall time each at 8K, so one region's
-    # ms_per_step moves with box clocks and queue timing: these samples say by how much
+    # the same K-step region (same brackets) repeated: `value` is the median region
+    # (a ~2 ms region moves with box clocks and queue timing), the first
+    # region is reported beside it
     region_ms = [elapsed / args.steps * 1e3]
     for rep in range(REGION_REPEATS):
         if world > 1:
@@ -1084,7 +1129,11 @@ def main():
 
     if rank == 0:
         total_px = px_per_step_rank * world * args.steps
-        value = total_px / elapsed / 1e6
+        # value: the median of the 8 timed regions (each K steps between barriers and
+        # synchronisations); the first region's rate beside it
+        med_ms = float(np.median(region_ms))
+        value = total_px / (med_ms * args.steps * 1e-3) / 1e6
+        value_first = total_px / elapsed / 1e6
         pmc = load_pmc_traffic(fused)
         cfg_idx = 2 if world == 1 else 3
         wl = ("%dx%d RGB -> YCrCb 4:2:0 full encode: colour+pyrDown, 8x8 DCT+quantize+zig-zag (3 planes), "
@@ -1108,7 +1157,10 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(med_ms, 4),
+            "value_first_region": round(value_first, 2),
+            "ms_per_step_first_region": round(elapsed / args.steps * 1e3, 4),
+            "value_is": "median over the %d timed regions of K steps" % len(region_ms),
             "ms_per_step_p10": round(float(np.percentile(region_ms, 10)), 4),
             "ms_per_step_p50": round(float(np.percentile(region_ms, 50)), 4),
             "ms_per_step_p90": round(float(np.percentile(region_ms, 90)), 4),
@@ -1186,7 +1238,9 @@ def main():
                                     "8k_plane_dct": extra_8k_plane_dct(),
                                     "8k_luma_dct": extra_8k_plane_dct(
                                         luma_only=True, floor_us=floors["luma_pattern"]["1x"]["median_launch_us"]),
-                                    "8k_luma_dct_back_to_back": extra_8k_luma_batched(),
+                                    "8k_luma_dct_back_to_back": extra_8k_luma_batched(
+                                        floor_us_per_plane=round(floors["luma_pattern"]["4x"]["median_launch_us"] / 4,
+                                                                 2)),
                                     "8k_jpeg_decode": extra_8k_jpeg_decode(),
                                     "8k_encode_from_host": extra_8k_encode_from_host(),
                                     "16k_roundtrip": extra_16k_roundtrip(),

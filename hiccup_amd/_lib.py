@@ -32,7 +32,8 @@ _sz = ctypes.c_size_t
 class RleJob16(ctypes.Structure):
     """hic_rle_job16 (include/hiccup_hip.h)."""
     _fields_ = [("blocks", _vp), ("nblk", _i64), ("d_stitch", _vp), ("dc_diff", _vp), ("sym_len", _vp),
-                ("sym_val", _vp), ("sym_cap", _i64), ("d_count", _vp), ("workspace", _vp), ("records_per_tile", _i64)]
+                ("sym_val", _vp), ("sym_cap", _i64), ("d_count", _vp), ("workspace", _vp), ("records_per_tile", _i64),
+                ("workspace_bytes", _i64)]
 
 
 class DctPlaneJob(ctypes.Structure):
@@ -76,9 +77,8 @@ SIGNATURES = {
     "hic_encode420_u8": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _int, _vp,
                                 _vp, _vp]),
     "hic_rle_encode_i16_tiles_batch": (_int, [_int, _vp, _int, _vp]),
-    "hic_encode420_rle_u8": (_int, [_vp, _i64, _i64, _vp, _int, _vp, _vp, _vp]),
-    "hic_encode420_seg_u8": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _int,
-                                    _vp, _vp, _vp]),
+    "hic_encode420_seg_u8": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64,
+                                    _i64, _int, _vp, _vp, _vp]),
     "hic_rle_encode_i16_rows_batch": (_int, [_int, _vp, _vp, _int, _vp]),
     "hic_event_create": (_int, [_vp]),
     "hic_event_destroy": (_int, [_vp]),
@@ -98,6 +98,7 @@ SIGNATURES = {
     "hic_zigzag_blocks_i32": (_int, [_vp, _i64, _i64, _int, _vp, _vp]),
     "hic_izigzag_blocks_i32": (_int, [_vp, _i64, _i64, _int, _vp, _vp]),
     "hic_rle_workspace_bytes": (_sz, [_i64, _int]),
+    "hic_rle_rows_workspace_bytes": (_sz, [_i64, _i64, _int]),
     "hic_rle_shard_summary_i16": (_int, [_vp, _i64, _int, _vp, _vp, _vp]),
     "hic_rle_shard_summary_i32": (_int, [_vp, _i64, _int, _vp, _vp, _vp]),
     "hic_rle_encode_i16": (_int, [_vp, _i64, _int, _int, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
@@ -172,9 +173,8 @@ def call(name, *args):
 
 # A/B knobs (include/hiccup_hip.h HIC_KNOB_*): every selectable path is bit-exact
 KNOBS = {"dct_path": 0, "dct_waves_per_cu": 1, "color_tiled": 2, "color_seg": 3, "color_nt": 4, "rle_nt": 5,
-         "rld_nt": 6, "rld_generic": 7, "dev": 8, "encode_waves": 9, "encode_nt": 10, "encode_dct": 11,
-         "dct_mfma": 12, "encode_order": 13}
-DCT_PATH_MFMA, DCT_PATH_F64, DCT_PATH_F64_NOPF, DCT_PATH_EXACT = 5, 1, 2, 0
+         "rld_nt": 6, "rld_generic": 7, "dev": 8, "encode_order": 13}
+DCT_PATH_PK, DCT_PATH_F64, DCT_PATH_F64_NOPF, DCT_PATH_EXACT = 3, 1, 2, 0
 
 
 def set_knob(name, value):

@@ -17,8 +17,6 @@ int knob(int k) {
     case HIC_KNOB_DCT_PATH: return 1;
     case HIC_KNOB_COLOR_SEG: return 8;
     case HIC_KNOB_RLE_NT: return 1;
-    case HIC_KNOB_ENCODE_WAVES: return 3;
-    case HIC_KNOB_ENCODE_NT: return 1;
     case HIC_KNOB_ENCODE_ORDER: return 6;  // XCD-major workgroups, odd unit rows bottom-up
     default: return k == HIC_KNOB_DCT_WAVES_PER_CU ? -1 : 0;
   }
@@ -81,16 +79,13 @@ extern "C" int hic_event_elapsed_ms(void *start, void *stop, float *h_ms) {
 
 extern "C" int hic_set_knob(int k, int value) {
   if (k < 0 || k >= HIC_KNOB_COUNT) return hic::arg_error("knob %d", k);
-  if (k == HIC_KNOB_DCT_PATH && value != -1 && !(value == 0 || value == 1 || value == 2 || value == 5))
-    return hic::arg_error("dct path %d (0 exact, 1 / 2 float64 AAN, 5 integer MFMA)", value);
+  if (k == HIC_KNOB_DCT_PATH && value != -1 && !(value == 0 || value == 1 || value == 2 || value == 3))
+    return hic::arg_error("dct path %d (0 exact, 1 / 2 float64 AAN, 3 packed float32)", value);
   if (k == HIC_KNOB_COLOR_SEG && value != -1 && value != 8 && value != 16) return hic::arg_error("colour segment");
-  // retired variants (measured slower, removed in round 4): only the shipped value
-  if (k == HIC_KNOB_ENCODE_WAVES && value != -1 && value != 3) return hic::arg_error("encode waves: 3 only (retired)");
-  if (k == HIC_KNOB_ENCODE_NT && value != -1 && value != 1) return hic::arg_error("encode_nt: 1 only (retired)");
-  if (k == HIC_KNOB_DCT_MFMA && value != -1 && (value < 0 || value > 3)) return hic::arg_error("dct_mfma 0..3");
-  if (k == HIC_KNOB_ENCODE_ORDER && value != -1 && (value < 0 || value > 7)) return hic::arg_error("encode_order 0..7");
-  if (k == HIC_KNOB_ENCODE_DCT && value != -1 && value != 0 && value != 1)
-    return hic::arg_error("encode_dct: 0 float64 AAN, 1 integer MFMA");
+  // retired knobs (measured slower, removed in rounds 4-5)
+  if (k >= 9 && k <= 12) return hic::arg_error("knob %d is retired", k);
+  if (k == HIC_KNOB_ENCODE_ORDER && value != -1 && (value < 0 || value > 7 || (value & 1)))
+    return hic::arg_error("encode_order 0, 2, 4 or 6");
   if (value < -1) return hic::arg_error("knob value %d", value);
 #ifndef HIC_DEV
   if (k == HIC_KNOB_DEV && value > 0) return hic::arg_error("the dev knob needs a -DHIC_DEV build");

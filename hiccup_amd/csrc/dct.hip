@@ -25,7 +25,6 @@
 #include <stdlib.h>
 
 #include "dct_core.h"
-#include "dct_mfma.h"
 #include "rle_core.h"
 
 namespace hic {
@@ -602,209 +601,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DCT_WPE
 }
 
 // ---------------------------------------------------------------------------
-// Integer-MFMA forward kernel (production path for aligned planes, dct_path 5).
-// The 2-D DCT-II + quantiser of a block is one linear map of its 64 centred
-// pixels, so a wave evaluates it for 16 blocks at a time as a [64 slots x 64
-// pixels] . [64 pixels x 16 blocks] contraction on the matrix cores
-// (v_mfma_i32_16x16x64_i8), in exact integer arithmetic:
-//  * x = p XOR 0x80 is the centred pixel p - 128 as an int8 (no conversion);
-//  * A[z][k] = round(2^32 C_uv,k / T_uv) (rows in zig-zag order, the table folded
-//    in; tools/check/dct_mfma.py, dct_mfma_tables.h) is split into four balanced
-//    base-256 digits, one MFMA each: S_d = sum_k a_d[z][k] x_k, exact in int32;
-//  * the digits combine with two truncating shifts fed back through the MFMA's
-//    accumulator input (D0 = S0 + c0, D1 = S1 + (D0 >> 8), D2 = S2 + (S3 << 8) +
-//    2^15, R = (D2 << 3) + (D1 >> 5)): R / 2^19 estimates y/T + 1/2 within the
-//    proven window, q = R >> 19;
-//  * R mod 2^19 < kMfmaL flags a coefficient whose rounding the estimate cannot
-//    decide (~3.5e-4 per block on random data).  The DC row is 2^30 for both
-//    tables: the exact pixel sum, rounded in integers (dc_quant).  Luminance (4,4)
-//    is y/T = K/34, flagged exactly at its ties (~3 % of blocks): the wave resolves
-//    them in place with pocketfft's own roundings (pf_y44 on the rows' signed sums,
-//    one v_dot4 per row half).  A set with any other flag is recomputed after the
-//    main loop on the float64 AAN path (dct_block_aan, with its own fallbacks).
-// Per 16 blocks: 16 MFMAs and ~6.5 VALU per coefficient (2 shifts, 2 shift-adds,
-// half a v_perm and half a v_pk_ashrrev_i16 to pack q, v_and + half a v_min3 for
-// the flag), against ~18 float64 operations per coefficient on the AAN path.
-// Output slot layout: lane (n = lane & 15, g = lane >> 4) of M-tile mt holds slots
-// 16 mt + 4 g .. + 3 of block n: one 8-byte LDS store into the stage, which leaves
-// in 1 KiB nontemporal stores (and feeds the RLE tile record) as in k_dct_planes.
-// stage (this wave's 64 rows) -> ZIGZAG_I16 output (+ the set's RLE tile record)
-template <int TMF, int PITCH = kStageU2>
-__device__ __forceinline__ void mfma_store(const DctJob &J, int set, const uint2 *st2, int lane, int M) {
-  __builtin_amdgcn_wave_barrier();
-  const int blk = set * 64 + lane;
-  auto st16 = [&](int b, int k) {
-    const uint2 lo = st2[b * PITCH + 2 * k], hi = st2[b * PITCH + 2 * k + 1];
-    return make_uint4(lo.x, lo.y, hi.x, hi.y);
-  };
-  uint4 *o = reinterpret_cast<uint4 *>(static_cast<int16_t *>(J.out) + (int64_t)set * 64 * 64);
-  auto sv = [&](int k) { return st16(8 * k + (lane >> 3), lane & 7); };
-  if ((set + 1) * 64 <= J.nblk) {
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const uint4 t = sv(k);
-      const u32x4 v = {t.x, t.y, t.z, t.w};
-      __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(o + 64 * k + lane));
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (set * 64 + 8 * k + (lane >> 3) < J.nblk) o[64 * k + lane] = sv(k);
-  }
-  if (TMF >= 0) {
-    uint32_t zw[32];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const uint4 t = st16(lane, k);
-      zw[4 * k] = t.x; zw[4 * k + 1] = t.y; zw[4 * k + 2] = t.z; zw[4 * k + 3] = t.w;
-    }
-    tile_record16<TMF>(zw, blk < J.nblk, blk, M, J.tiles + (int64_t)set * 3);
-  }
-  __builtin_amdgcn_wave_barrier();
-}
-
-// WPE: waves per SIMD the register budget allows (3: <= 168 VGPRs, 2: <= 256, with
-// the next group's MFMAs issued before this group's epilogue); PF: the next set's
-// pixels load while this set computes (16 more VGPRs)
-template <int TMF, int WPE, bool PF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_dct_mfma(DctJobs jobs) {
-  __shared__ __attribute__((aligned(16))) uint2 s_stage[4 * 64 * kStageU2];
-  __shared__ int2 s_k44[4 * 64 * 4];  // (4,4) tie path: the 8 signed row sums per block
-  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nwaves = gridDim.x * 4;
-  const int g0 = blockIdx.x * 4 + wv;
-  uint2 *st2 = s_stage + wv * 64 * kStageU2;
-  int2 *k44 = s_k44 + wv * 64 * 4;
-  const int n = lane & 15, g = lane >> 4;
-  const int M = jobs.M;
-  auto job_of = [&](int gi) {
-    gi = __builtin_amdgcn_readfirstlane(gi);
-    int k = 0;
-    while (k + 1 < jobs.n && gi >= jobs.j[k + 1].set0) ++k;
-    return __builtin_amdgcn_readfirstlane(k);
-  };
-  uint64_t redo = 0;
-  int i = 0;
-  if (g0 < jobs.total_sets) {
-    int kj = job_of(g0);
-    DctJob J = jobs.j[kj];
-    int next0 = kj + 1 < jobs.n ? jobs.j[kj + 1].set0 : jobs.total_sets;
-    int table = -1;
-    i32x4 A[4][4];
-    uint2 px[8];  // this set's (PF: the next set's) pixel rows
-    for (int gs = g0; gs < jobs.total_sets; gs += nwaves, ++i) {
-      if (gs >= next0) {
-        kj = job_of(gs);
-        J = jobs.j[kj];
-        next0 = kj + 1 < jobs.n ? jobs.j[kj + 1].set0 : jobs.total_sets;
-      }
-      if (J.table != table) {  // wave-uniform: this plane's matrix digits
-        table = J.table;
-        mfma_load_A(table, lane, A);
-      }
-      const int set = gs - J.set0;
-      // pixels: lane (n, g) of N-tile nt holds rows 2g, 2g + 1 of block 16 nt + n
-      // pixels: lane L loads the 8 rows of block L of the set (each load instruction
-      // one contiguous 512 B image-row segment, the pattern of the memory-floor
-      // probe); the rows then go through the stage (80 B per block: conflict-free
-      // 16 B stores) to the fragment layout: lane (n, g) of N-tile nt holds rows
-      // 2g, 2g + 1 of block 16 nt + n (bytes 16 g .. 16 g + 15 of the block's 64).
-      // Measured: loading the fragments straight from HBM (4 image rows per
-      // instruction) waited twice as long on memory (SQ_WAIT_ANY 20.8 M vs 10.6 M).
-      auto load_px = [&](const DctJob &Jx, int setx, uint2 (&r)[8]) {
-        const int blk = setx * 64 + lane;
-        const int cblk = blk < Jx.nblk ? blk : Jx.nblk - 1;
-        const int bi = cblk / Jx.nbx, bj = cblk - bi * Jx.nbx;
-        const uint8_t *p = Jx.plane + (int64_t)bi * 8 * Jx.stride + bj * 8;
-#pragma unroll
-        for (int rr = 0; rr < 8; ++rr) r[rr] = *reinterpret_cast<const uint2 *>(p + rr * Jx.stride);
-      };
-      if (!PF || gs == g0) load_px(J, set, px);
-      i32x4 B[4];
-      {
-        uint4 *pix = reinterpret_cast<uint4 *>(st2);
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          pix[lane * 5 + k] = make_uint4(px[2 * k].x, px[2 * k].y, px[2 * k + 1].x, px[2 * k + 1].y);
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-          const uint4 v = pix[(16 * nt + n) * 5 + g];
-          B[nt] = mfma_pixels(make_uint2(v.x, v.y), make_uint2(v.z, v.w));
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
-      if (PF && gs + nwaves < jobs.total_sets) {
-        const int gn = gs + nwaves;
-        const int kn = gn >= next0 ? job_of(gn) : kj;
-        load_px(jobs.j[kn], gn - jobs.j[kn].set0, px);
-      }
-      uint64_t m44 = 0;
-      const bool flagged = mfma_pass<WPE == 2>(A, B, st2, lane, table, m44);
-      if (flagged) {
-        redo |= 1ull << i;  // the whole set again on the float64 path, after the loop
-        continue;
-      }
-      if (m44 != 0) {
-        // luminance (4,4) ties: the rows' signed sums (+ - - + + - - +) of each block
-        // to its lane, pocketfft's own roundings on them, the exact q into the stage
-        constexpr int kS = 0x01FFFF01;  // int8 (+1, -1, -1, +1)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-          const int ka = __builtin_amdgcn_sdot4(B[nt].y, kS, __builtin_amdgcn_sdot4(B[nt].x, kS, 0, false), false);
-          const int kb = __builtin_amdgcn_sdot4(B[nt].w, kS, __builtin_amdgcn_sdot4(B[nt].z, kS, 0, false), false);
-          k44[(16 * nt + n) * 4 + g] = make_int2(ka, kb);
-        }
-        __builtin_amdgcn_wave_barrier();
-        if ((m44 >> lane) & 1) {
-          int k[8];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int2 v = k44[lane * 4 + r];
-            k[2 * r] = v.x;
-            k[2 * r + 1] = v.y;
-          }
-          reinterpret_cast<int16_t *>(st2 + lane * kStageU2)[kMfmaZ44] = (int16_t)quant_fast<0>(pf_y44_k(k), 36);
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
-      mfma_store<TMF>(J, set, st2, lane, M);
-    }
-  }
-  // flagged sets: the float64 AAN path (its own exact fallbacks) on this wave's sets
-  int16_t *st = reinterpret_cast<int16_t *>(st2 + lane * kStageU2);
-  while (redo) {
-    const int k = __builtin_ctzll(redo);
-    redo &= redo - 1;
-    const int gs = g0 + k * nwaves;
-    const DctJob &J = jobs.j[job_of(gs)];
-    const int set = gs - J.set0;
-    const int blk = set * 64 + lane;
-    const int cblk = blk < J.nblk ? blk : J.nblk - 1;
-    const int bi = cblk / J.nbx, bj = cblk - bi * J.nbx;
-    const uint8_t *p = J.plane + (int64_t)bi * 8 * J.stride + bj * 8;
-    uint2 w[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) w[r] = *reinterpret_cast<const uint2 *>(p + r * J.stride);
-    bool t26 = false;
-    const bool f = dct_block_aan<-1, HIC_LAYOUT_ZIGZAG_I16>(w, st, &t26, nullptr, J.table);
-    if (f) {
-      dct_block_2ph<-1, HIC_LAYOUT_ZIGZAG_I16>(w, st, J.table);
-    } else if (t26) {
-      constexpr SlotOf<HIC_LAYOUT_ZIGZAG_I16> kSlot{};
-      int q[4];
-      dct_fix26<-1>(w, q, J.table);
-      st[kSlot.s[18]] = (int16_t)q[0];
-      st[kSlot.s[22]] = (int16_t)q[1];
-      st[kSlot.s[50]] = (int16_t)q[2];
-      st[kSlot.s[54]] = (int16_t)q[3];
-    }
-    mfma_store<TMF>(J, set, st2, lane, M);
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Block-level helpers (transform.dct2 / idct2, quantization.jpeg_quantize /
 // invert_jpeg_quantize on arbitrary float64 / int blocks): one block per lane.
 __global__ __launch_bounds__(256) void k_dct2_f64(const double *__restrict__ in, int64_t nblk, double *__restrict__ out) {
@@ -868,20 +664,18 @@ __global__ void k_dequantize_i32(const int32_t *__restrict__ in, int64_t n, int 
 inline bool aligned(const void *p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
 
 // Forward-path selection (A/B tests only; every path is bit-exact): knob
-// "dct_path" 5 = integer-MFMA transform (k_dct_mfma, ZIGZAG_I16 output; the
-// raster layouts take path 1), 1 = float64 AAN fast path (k_dct_planes), 2 = the
-// same (the prefetch variant is compiled out), 0 = the exact pocketfft replica for
-// every block; "dct_waves_per_cu" = persistent grid size (0 = one wave per set).  Set through hic_set_knob (common.hip); the
-// library reads no environment variables.
+// "dct_path" 1 = float64 AAN fast path (k_dct_planes), 2 = the same (the prefetch
+// variant is compiled out), 0 = the exact pocketfft replica for every block;
+// "dct_waves_per_cu" = persistent grid size (0 = one wave per set).  Set through
+// hic_set_knob (common.hip); the library reads no environment variables.
 inline int dct_path() { return knob(HIC_KNOB_DCT_PATH); }
 inline int dct_waves_per_cu(int njobs) {
   const int v = knob(HIC_KNOB_DCT_WAVES_PER_CU);
   // float64 path: one wave per set for a multi-plane launch (the hardware's dispatch
   // balances the planes' mixed tail: 8K Y + Cr + Cb 37.5 us vs 39.7 for 12
   // persistent waves per CU), 12 persistent waves per CU for one plane (4K luma
-  // 13.4 vs 13.8 us, 8K luma 27.4 vs 27.8; scripts/gpu_r2aj.sh); the MFMA path
-  // runs a persistent grid of its register budget's waves per SIMD
-  return v >= 0 ? v : (dct_path() == 5 ? ((knob(HIC_KNOB_DCT_MFMA) & 2) ? 8 : 12) : (njobs > 1 ? 0 : 12));
+  // 13.4 vs 13.8 us, 8K luma 27.4 vs 27.8; scripts/gpu_r2aj.sh)
+  return v >= 0 ? v : (njobs > 1 ? 0 : 12);
 }
 
 inline bool fwd_fast(int H, int W, int64_t stride, const void *plane, const void *out) {
@@ -901,21 +695,7 @@ int launch_planes(DctJobs &jobs, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   if (cap > 0 && (total + cap - 1) / cap > 64) cap = (total + 63) / 64;  // <= 64 sets per wave (redo mask)
   const int waves = (cap == 0 || total < cap) ? total : cap;
   const dim3 grid((waves + 3) / 4), block(256);
-  const int path = dct_path();
-  if (path == 5 && LAYOUT == HIC_LAYOUT_ZIGZAG_I16) {
-    const int var = knob(HIC_KNOB_DCT_MFMA);
-    auto go = [&](auto kern) {
-      if (e0 || e1)
-        hipExtLaunchKernelGGL(kern, grid, block, 0, s, e0, e1, 0, jobs);
-      else
-        hipLaunchKernelGGL(kern, grid, block, 0, s, jobs);
-    };
-    if (var == 0) go(k_dct_mfma<TMF, 3, false>);
-    else if (var == 1) go(k_dct_mfma<TMF, 3, true>);
-    else if (var == 2) go(k_dct_mfma<TMF, 2, false>);
-    else go(k_dct_mfma<TMF, 2, true>);
-    return check_launch("k_dct_mfma");
-  }
+  const int path = dct_path() == 3 ? 1 : dct_path();
   if (e0 || e1)
     hipExtLaunchKernelGGL((k_dct_planes<TABLE, LAYOUT, TMF>), grid, block, 0, s, e0, e1, 0, jobs, path);
   else
@@ -1013,9 +793,13 @@ extern "C" int hic_dct_quant_rle_u8_batch(int n, const hic_dct_plane_job *jobs, 
   // table at run time)
   const bool merge = true;
   DctJobs fastj[2] = {};
+  // rle_workspace: every job's or none (NULL: the records-free pass, DCT + quantize +
+  // zig-zag only)
+  const bool recs = jobs[0].rle_workspace != nullptr;
   for (int k = 0; k < n; ++k) {
     const hic_dct_plane_job &a = jobs[k];
-    if (!a.plane || !a.out || !a.rle_workspace) return arg_error("plane %d: null pointer", k);
+    if (!a.plane || !a.out) return arg_error("plane %d: null pointer", k);
+    if ((a.rle_workspace != nullptr) != recs) return arg_error("plane %d: rle_workspace for every plane or none", k);
     if (!dims_ok(a.H, a.W) || a.stride < a.W) return arg_error("plane %d: shape / stride", k);
     if (a.table_id != HIC_TABLE_LUMINANCE && a.table_id != HIC_TABLE_CHROMINANCE) return arg_error("plane %d: table_id", k);
     const int h = (int)a.H, w = (int)a.W;
@@ -1029,7 +813,8 @@ extern "C" int hic_dct_quant_rle_u8_batch(int n, const hic_dct_plane_job *jobs, 
     const int e = a.table_id == 0 ? launch_fwd<0, HIC_LAYOUT_ZIGZAG_I16>(a.plane, h, w, a.stride, a.out, s, e0, e1)
                                   : launch_fwd<1, HIC_LAYOUT_ZIGZAG_I16>(a.plane, h, w, a.stride, a.out, s, e0, e1);
     if (e) return e;
-    if (int e2 = rle_tile16_launch(a.out, (int64_t)((h + 7) / 8) * ((w + 7) / 8), max_len, tiles, s)) return e2;
+    if (recs)
+      if (int e2 = rle_tile16_launch(a.out, (int64_t)((h + 7) / 8) * ((w + 7) / 8), max_len, tiles, s)) return e2;
   }
   // the events (if any) time the first launch
   bool timed = false;
@@ -1040,7 +825,9 @@ extern "C" int hic_dct_quant_rle_u8_batch(int n, const hic_dct_plane_job *jobs, 
     const hipEvent_t a0 = timed ? nullptr : e0, a1 = timed ? nullptr : e1;
     timed = true;
     int e;
-    if (merge)
+    if (!recs)
+      e = launch_planes<-1, HIC_LAYOUT_ZIGZAG_I16, -1>(J, s, a0, a1);
+    else if (merge)
       e = max_len == 15 ? launch_planes<-1, HIC_LAYOUT_ZIGZAG_I16, 15>(J, s, a0, a1)
                         : launch_planes<-1, HIC_LAYOUT_ZIGZAG_I16, 0>(J, s, a0, a1);
     else if (t == 0)

@@ -44,8 +44,6 @@
 // coefficient writes 3 B per pixel.
 #include "color_core.h"
 #include "dct_core.h"
-#include "dct_mfma.h"
-#include "onepass.h"
 #include "rle_core.h"
 
 namespace hic {
@@ -58,23 +56,9 @@ struct Enc420 {
   int64_t *rec[3];   // tile records: Y per 64-block tile, Cr / Cb per 32-block half tile
   int M;
   int nstrips, nunits;  // nunits: waves (one unit each)
-  int vstack;           // 1: a workgroup's waves take 4 vertically stacked units of one strip
   int xcd;              // 1: workgroups remapped XCD-major (xcd_block)
   int alt;              // 1: odd unit rows run their colour rows bottom-up
   int wlast;            // pixel columns of the last strip (16 .. 512)
-  // one-pass encode (hic_encode420_rle_u8): per plane Y, Cr, Cb
-  int32_t *dc[3];
-  uint8_t *sym_len[3];
-  int16_t *sym_val[3];
-  int64_t cap[3];
-  int64_t *d_count[3];
-  uint64_t *gran[3];  // look-back granules, 8 per record (onepass.h)
-  uint64_t *gwin[3];  // and 4 per window (unit row)
-  int last_rec[3];    // the plane's last record (it closes the stream)
-  int64_t n_ac[3];    // the plane's AC stream length
-  uint32_t *ticket;   // unit tickets (reset by the wave that takes the last one)
-  uint64_t *fail;     // the launch's timeout word (tag (epoch << 2) | 3)
-  uint32_t epoch;
 };
 
 constexpr int kZZ = HIC_LAYOUT_ZIGZAG_I16;
@@ -429,198 +413,47 @@ struct EncColour {
   }
 };
 
-// One-pass: a pass's record (lane = block; SEG: lanes 0-31 Cr record `rec`, 32-63 Cb
-// record `rec`, else the Y record `rec`) in two steps.  op_publish summarises the
-// lane's block (zw: its zig-zag words) and publishes the record's aggregate;
-// op_finish looks back, publishes the inclusive prefix, writes the DC differences
-// and emits the symbols (blk: the block in the LDS stage, for lane-varying reads),
-// and the plane's last record closes its stream.  A unit publishes BOTH Y records
-// before it looks back: a Y tile's predecessors include the row above's second Y
-// tiles of later units, whose aggregates must not wait on their own look-backs (that
-// chains the look-backs row after row down the image).  b: this lane's block.
-struct OpRec {
-  int first, last, nsym, dc, lastdc;
-  uint64_t ac;
-  Agg32 A;
-};
-template <int TMF, bool SEG>
-__device__ __forceinline__ OpRec op_publish(const Enc420 &E, const uint32_t (&zw)[32], int rec, int64_t b) {
-  const int lane = fresh_lane(), sl = SEG ? lane & 31 : lane, seg0 = SEG ? lane & 32 : 0;
-  const int p = SEG ? 1 + (lane >> 5) : 0;
-  const int M = E.M;
-  OpRec R;
-  R.first = -1;
-  R.last = -1;
-  R.nsym = 0;
-  R.ac = 0;
-  summarize16<TMF>(zw, M, R.first, R.last, R.nsym, &R.ac);
-  // the record's aggregate (tile_record16_half's fields, as stream positions)
-  const int lastr = R.last >= 0 ? sl * 63 + R.last : -1;
-  const int incl = SEG ? seg32_incl_max_i32(lastr) : wave_incl_max_i32(lastr);
-  int prevr = wave_shr1_i32(-1, incl);
-  if (sl == 0) prevr = -1;
-  int c = R.nsym;
-  if (R.first >= 0 && prevr >= 0) c += syms_for_run(sl * 63 + R.first - prevr - 1, M);
-  const int ic = SEG ? seg32_incl_sum_i32(c) : wave_incl_sum_i32(c);
-  const int segL = seg0 + (SEG ? 31 : 63);
-  const int all_last = __shfl(incl, segL), tot = __shfl(ic, segL);
-  const uint64_t fm = __builtin_amdgcn_ballot_w64(R.first >= 0);
-  const uint64_t fmh = SEG ? (fm >> seg0) & 0xFFFFFFFFull : fm;
-  const int fl = fmh ? __builtin_ctzll(fmh) : 0;
-  const int ff = __shfl(sl * 63 + R.first, seg0 + fl);
-  const int base = (int)((b - sl) * 63);  // stream position of the record's first AC
-  R.A = all_last < 0 ? Agg32{-1, -1, 0} : Agg32{base + ff, base + all_last, tot};
-  R.dc = (int)(int16_t)(zw[0] & 0xFFFFu);
-  R.lastdc = __shfl(R.dc, segL);
-  if (sl < 4)
-    op_put(E.gran[p] + 8 * (int64_t)rec + sl,
-           sl == 0 ? R.A.first : sl == 1 ? R.A.last : sl == 2 ? R.A.cnt : R.lastdc, (E.epoch << 2) | 1u);
-  return R;
-}
-
-template <int TMF, bool SEG>
-__device__ __forceinline__ void op_finish(const Enc420 &E, const OpRec &R, const uint32_t (&zw)[32],
-                                          const int16_t *blk, uint8_t *s_len, int16_t *s_val, int rec, int64_t b,
-                                          int u, int o) {
-  const int lane = fresh_lane(), sl = SEG ? lane & 31 : lane;
-  const int p = SEG ? 1 + (lane >> 5) : 0;
-  const int M = E.M;
-  uint64_t *g = E.gran[p];
-  const uint32_t tagA = (E.epoch << 2) | 1u, tagP = (E.epoch << 2) | 2u;
-  Agg32 ex{-1, -1, 0};
-  int pdc = 0;
-#if defined(HIC_DEV) && defined(HIC_OP_NOWAIT)
-  const bool ok = true;  // dev timing (results invalid): no look-back
-#else
-  const bool ok = op_lookback<SEG>(g, E.gwin[p], u, o, E.nstrips, !SEG, tagA, tagP, (E.epoch << 2) | 3u, M, ex, pdc);
-#endif
-  const Agg32 P = agg32(ex, R.A, M);
-  if (sl < 4) op_put(g + 8 * (int64_t)rec + 4 + sl, sl == 0 ? P.first : sl == 1 ? P.last : sl == 2 ? P.cnt : R.lastdc, tagP);
-  // DC differences (codec.differential_coding): the record's first block takes the
-  // previous record's last DC (0 before the plane's first block)
-  int pd = __shfl_up(R.dc, 1, 64);
-  if (sl == 0) pd = pdc;
-  E.dc[p][b] = R.dc - pd;
-  // the record's first symbol and the last nonzero before it (no carry: p0 = -1)
-  const int64_t o_seg = ex.last >= 0 ? (int64_t)ex.cnt + syms_for_run(ex.first, M) : 0;
-  const int64_t prev_seg = ex.last >= 0 ? ex.last : -1;
-#if !(defined(HIC_DEV) && defined(HIC_OP_NOEMIT))  // dev timing (results invalid): no symbol emission
-  if (SEG)
-    op_emit<TMF, true>(zw, blk, b * 63, M, o_seg, prev_seg, R.first, R.last, R.nsym, R.ac, s_len, s_val,
-                       E.sym_len[1], E.sym_val[1], E.cap[1], E.sym_len[2], E.sym_val[2], E.cap[2]);
-  else
-    op_emit<TMF, false>(zw, blk, b * 63, M, o_seg, prev_seg, R.first, R.last, R.nsym, R.ac, s_len, s_val,
-                        E.sym_len[0], E.sym_val[0], E.cap[0], E.sym_len[0], E.sym_val[0], E.cap[0]);
-#endif
-  if (!ok && sl == 0) {
-    op_put(E.fail, 1, (E.epoch << 2) | 3u);
-    __hip_atomic_store(E.d_count[p], (int64_t)HIC_COUNT_SCAN_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (rec == E.last_rec[p] && sl == 0) {
-    // the stream's end (k_rle_scan16b's closing step): EOB unless the last AC is nonzero
-    int64_t total = P.last >= 0 ? (int64_t)P.cnt + syms_for_run(P.first, M) : 0;
-    if (!(E.n_ac[p] > 0 && P.last == E.n_ac[p] - 1)) {
-      if (total < E.cap[p]) {
-        E.sym_len[p][total] = 0;
-        E.sym_val[p][total] = 0;
-      }
-      ++total;
-    }
-    __hip_atomic_store(E.d_count[p], total <= E.cap[p] ? total : -total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // a timeout anywhere in the launch wins over the count
-    if ((uint32_t)(op_get(E.fail) >> 32) == ((E.epoch << 2) | 3u))
-      __hip_atomic_store(E.d_count[p], (int64_t)HIC_COUNT_SCAN_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// the lane's stage row <- zw (a Y tile's words back into the stage for its emission)
-__device__ __forceinline__ void enc_row_to_stage(uint2 *st2, int lane, const uint32_t (&zw)[32]) {
-  uint2 *row = st2 + lane * kStageU2;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) row[k] = make_uint2(zw[2 * k], zw[2 * k + 1]);
-}
-
 // One wave per unit, 3 waves per SIMD (<= 168 VGPRs): all 19 colour rows first, so
 // no DCT runs while the row ring and the pyrDown window are live (the other waves of
 // the SIMD hide the loads instead); each packed Y row is pinned where it is made;
 // the DCT passes take the lane index afresh.  Round 3 measured this against the
 // 2-wave budget (colour rows 0..9, Y block row 0, rows 10..18): 8K bench
 // 0.1017-0.1041 vs 0.1043-0.1063 ms/step in 5 alternating pairs
-// (profiles/r03/s2/enc_w3/); the 2-wave kernel, the float32 / packed-float32 DCT
-// variants and cached stores were measured slower and are gone (git history).
-// MFMA: the integer-MFMA transform (dct_mfma.h) for the three passes instead of the
-// float64 AAN (knob "encode_dct" 1; bit-exact either way).
-// OP (one-pass, hic_encode420_rle_u8; float64 AAN only): 2 waves per SIMD -- each
-// wave also holds a 2048-symbol emission stage (6 KiB of LDS) -- units by ticket
-// (dispatch order, the look-back's progress guarantee), each pass's record handed
-// off and emitted right after its coefficients are stored (op_pass).
-template <int TMF, bool MFMA, bool OP = false>
-__global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_eu(OP ? 2 : 3))) void k_encode420(
-    Enc420 E) {
-  static_assert(!(MFMA && OP), "the one-pass encode runs the float64 AAN transform");
+// (profiles/r03/s2/enc_w3/).  Measured slower and removed (git history): the 2-wave
+// kernel, the float32 / packed-float32 / integer-MFMA transforms, cached stores, the
+// one-pass (look-back + emission) variant and vertically stacked units.
+template <int TMF>
+__global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_eu(3))) void k_encode420(Enc420 E) {
   __shared__ __attribute__((aligned(16))) uint2 s_stage[HIC_ENC_WPB * 64 * kStageU2];
   __shared__ uint32_t s_chroma_all[HIC_ENC_WPB][2 * 8 * 64];
-  __shared__ __attribute__((aligned(16))) uint8_t s_oplen[OP ? HIC_ENC_WPB : 1][OP ? kOpSyms + 32 : 16];
-  __shared__ __attribute__((aligned(16))) int16_t s_opval[OP ? HIC_ENC_WPB : 1][OP ? kOpSyms + 32 : 8];
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int g = __builtin_amdgcn_readfirstlane(blockIdx.x * HIC_ENC_WPB + wv);
-  if (OP && g >= E.nunits) return;  // wave-uniform
-  if (OP) {
-    // tickets in the order waves start; the last one resets the counter for the next
-    // launch (every ticket is taken by then)
-    uint32_t t = 0;
-    if (lane == 0) t = __hip_atomic_fetch_add(E.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    g = (int)__builtin_amdgcn_readfirstlane(t);
-    if (g == E.nunits - 1 && lane == 0) __hip_atomic_store(E.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
   uint2 *st2 = s_stage + wv * 64 * kStageU2;
   uint32_t *s_chroma = s_chroma_all[wv];
   const int bx = __builtin_amdgcn_readfirstlane(E.xcd ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x);
   int16_t *st = reinterpret_cast<int16_t *>(st2 + lane * kStageU2);
-  // wave g: strip s, unit row u0 (vstack: workgroup b = strip b % nstrips, unit rows
-  // 4 (b / nstrips) .. + 3 -- the halo rows a unit shares with the one below are
-  // fetched once into the CU's caches)
-  int u0, s;
-  if (!OP && E.vstack) {
-    const int b = bx;
-    s = __builtin_amdgcn_readfirstlane(b % E.nstrips);
-    u0 = __builtin_amdgcn_readfirstlane((b / E.nstrips) * HIC_ENC_WPB + wv);
-    if (u0 * 16 >= E.out_rows) return;  // wave-uniform
-  } else {
-    if (!OP) {
-      g = __builtin_amdgcn_readfirstlane(bx * HIC_ENC_WPB + wv);
-      if (g >= E.nunits) return;  // wave-uniform
-    }
-    u0 = __builtin_amdgcn_readfirstlane(g / E.nstrips);
-    s = __builtin_amdgcn_readfirstlane(g - u0 * E.nstrips);
-  }
+  // wave g: strip s of unit row u0
+  const int g = __builtin_amdgcn_readfirstlane(bx * HIC_ENC_WPB + wv);
+  if (g >= E.nunits) return;  // wave-uniform
+  const int u0 = __builtin_amdgcn_readfirstlane(g / E.nstrips);
+  const int s = __builtin_amdgcn_readfirstlane(g - u0 * E.nstrips);
   const int y0 = E.out_row0 + 16 * u0;
   // Y blocks of this strip's block rows (64 but in a ragged last strip)
   const int nb = __builtin_amdgcn_readfirstlane(s == E.nstrips - 1 ? E.wlast >> 3 : 64);
   const int nbx = E.W >> 3, nbxc = E.W >> 4;
 
   uint2 yq[16];
-  uint32_t zw1[32], zw2[32];  // OP: the two Y tiles' words until their emission
-  OpRec R1{}, R2{}, Rc{};
-  i32x4 A[4][4];  // MFMA matrix digits of the pass's table (loaded after the colour rows)
   // Y block row br: blocks 64 s .. 64 s + 63 of block row 2 u0 + br (one RLE tile),
-  // from yq slots 8 br .. 8 br + 7.  MFMA: the lane's block rows go through the stage
-  // area (64 B per block at an 80 B stride: conflict-free 16 B stores) to the
-  // fragment layout (lane n, g: rows 2g, 2g + 1 of block 16 nt + n); the transform
-  // then overwrites the stage with the coefficients.  A flagged pass (~3 % on random
-  // data) is redone on the float64 AAN path from the rows still in registers; the
-  // luminance (4,4) ties are decided in place (pf_y44 on the lane's own block).
-  auto y_out = [&](int br) {  // stage -> HBM + the tile record
+  // from yq slots 8 br .. 8 br + 7
+  auto y_blocks = [&](int br) {
+    uint2 w[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) w[r] = yq[8 * br + r];
+    enc_dct<0>(w, st);
     const int64_t b0 = (int64_t)(2 * u0 + br) * nbx + 64 * s;
     __builtin_amdgcn_wave_barrier();
     int16_t *o = E.coef[0] + b0 * 64;
     enc_store(st2, fresh_lane(), o, o + 32 * 64, nb < 32 ? nb : 32, nb > 32 ? nb - 32 : 0);
-    if (OP) {
-      // the tile's words stay in registers (zw1 / zw2) until both Y records are out
-      uint32_t(&zw)[32] = br == 0 ? zw1 : zw2;
-      enc_stage_row(st2, fresh_lane(), zw);
-      (br == 0 ? R1 : R2) = op_publish<TMF, false>(E, zw, (2 * u0 + br) * E.nstrips + s, b0 + fresh_lane());
-    } else if (TMF >= 0 && E.rec[0]) {
+    if (TMF >= 0 && E.rec[0]) {
       uint32_t zw[32];
       enc_stage_row(st2, fresh_lane(), zw);
       // one record per strip segment of the block row (64 blocks, or the ragged last
@@ -630,51 +463,21 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
-  // returns true (MFMA, wave-uniform) if the pass is flagged: nothing stored, the
-  // caller redoes it on the float64 AAN path after the other passes (the rows stay
-  // in registers; the matrix digits are dead by then)
-  auto y_blocks = [&](int br) -> bool {
-    uint2 w[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) w[r] = yq[8 * br + r];
-    if (MFMA) {
-      uint4 *pix = reinterpret_cast<uint4 *>(st2);
-      const int l = fresh_lane();
-#pragma unroll
-      for (int k = 0; k < 4; ++k) pix[l * 5 + k] = make_uint4(w[2 * k].x, w[2 * k].y, w[2 * k + 1].x, w[2 * k + 1].y);
-      __builtin_amdgcn_wave_barrier();
-      i32x4 B[4];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const uint4 v = pix[(16 * nt + (l & 15)) * 5 + (l >> 4)];
-        B[nt] = mfma_pixels(make_uint2(v.x, v.y), make_uint2(v.z, v.w));
-      }
-      __builtin_amdgcn_wave_barrier();
-      uint64_t m44 = 0;
-      if (mfma_pass(A, B, st2, l, 0, m44)) return true;
-      if (m44 != 0 && ((m44 >> l) & 1)) st[kMfmaZ44] = (int16_t)quant_fast<0>(pf_y44(w), 36);
-    } else {
-      enc_dct<0>(w, st);
-    }
-    y_out(br);
-    return false;
-  };
   // chroma: block m of Cr -> stage row m, of Cb -> row 32 + m (block m spans the
   // chroma columns of lanes 2m and 2m + 1 of this strip; its row i is the 8 bytes
-  // at uint2 i * 32 + m of the plane's LDS area); the AAN path takes them one block
-  // per lane (Cr block m in lane m, Cb in lane 32 + m)
-  auto c_out = [&]() {
+  // at uint2 i * 32 + m of the plane's LDS area), one block per lane (Cr block m in
+  // lane m, Cb in lane 32 + m)
+  auto c_blocks = [&]() {
+    __builtin_amdgcn_wave_barrier();
+    const uint2 *sc = reinterpret_cast<const uint2 *>(s_chroma + (lane >> 5) * 512) + (lane & 31);
+    uint2 w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = sc[i * 32];
+    enc_dct<1>(w, st);
     const int64_t b0 = (int64_t)u0 * nbxc + 32 * s;
     __builtin_amdgcn_wave_barrier();
     enc_store(st2, fresh_lane(), E.coef[1] + b0 * 64, E.coef[2] + b0 * 64, nb >> 1, nb >> 1);
-    if (OP) {
-      // every record of the unit published before any look-back; the chroma
-      // coefficients stay in the stage for their emission
-      uint32_t zw[32];
-      const int l = fresh_lane();
-      enc_stage_row(st2, l, zw);
-      Rc = op_publish<TMF, true>(E, zw, u0 * E.nstrips + s, b0 + (l & 31));
-    } else if (TMF >= 0 && E.rec[1]) {
+    if (TMF >= 0 && E.rec[1]) {
       uint32_t zw[32];
       enc_stage_row(st2, fresh_lane(), zw);
       const int64_t rc = (int64_t)u0 * E.nstrips + s;  // = b0 / 32 when W % 512 == 0
@@ -682,33 +485,6 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_sched_barrier(0);
-  };
-  auto c_aan = [&]() {
-    __builtin_amdgcn_wave_barrier();
-    const uint2 *sc = reinterpret_cast<const uint2 *>(s_chroma + (lane >> 5) * 512) + (lane & 31);
-    uint2 w[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) w[i] = sc[i * 32];
-    enc_dct<1>(w, st);
-    c_out();
-  };
-  auto c_blocks = [&]() -> bool {
-    if (!MFMA) {
-      c_aan();
-      return false;
-    }
-    __builtin_amdgcn_wave_barrier();
-    const int l = fresh_lane();
-    i32x4 B[4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const uint2 *sc = reinterpret_cast<const uint2 *>(s_chroma + (nt >> 1) * 512) + 16 * (nt & 1) + (l & 15);
-      B[nt] = mfma_pixels(sc[(2 * (l >> 4)) * 32], sc[(2 * (l >> 4) + 1) * 32]);
-    }
-    uint64_t m44 = 0;  // (chrominance (4,4) never ties)
-    if (mfma_pass(A, B, st2, l, 1, m44)) return true;
-    c_out();
-    return false;
   };
 #if defined(HIC_DEV) && defined(HIC_ENC_DEV) && (HIC_ENC_DEV & 2)
   // dev timing (results invalid): no colour stage, synthetic pixels
@@ -726,58 +502,9 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
   C.rows(yq, s_chroma, rev);
   __builtin_amdgcn_sched_barrier(0);
 #endif
-  if (MFMA) mfma_load_A(0, lane, A);
-  const bool redo0 = y_blocks(0);
-  const bool redo1 = y_blocks(1);
-  if (MFMA) mfma_load_A(1, lane, A);
-  const bool redoc = c_blocks();
-  if (OP) {  // the unit's three records published: look back and emit, chroma first
-    if (s == E.nstrips - 1) {  // the row's last unit: its windows' aggregates first
-      const uint32_t tagA = (E.epoch << 2) | 1u, tagW = (E.epoch << 2) | 3u;
-      const bool oky = op_publish_wa<false>(E.gran[0], E.gwin[0], u0, E.nstrips, true, tagA, tagW, E.M, R2.A, R2.lastdc);
-      const bool okc = op_publish_wa<true>(E.gran[1 + (fresh_lane() >> 5)], E.gwin[1 + (fresh_lane() >> 5)], u0,
-                                           E.nstrips, false, tagA, tagW, E.M, Rc.A, Rc.lastdc);
-      const bool okw = oky && okc;
-      if (!okw && fresh_lane() == 0) {
-        op_put(E.fail, 1, (E.epoch << 2) | 3u);
-        for (int p = 0; p < 3; ++p)
-          __hip_atomic_store(E.d_count[p], (int64_t)HIC_COUNT_SCAN_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    const int l = fresh_lane();
-    const int16_t *blk = reinterpret_cast<const int16_t *>(st2 + l * kStageU2);
-    {
-      uint32_t zw[32];
-      enc_stage_row(st2, l, zw);
-      op_finish<TMF, true>(E, Rc, zw, blk, s_oplen[OP ? wv : 0], s_opval[OP ? wv : 0], u0 * E.nstrips + s,
-                           (int64_t)u0 * (nbx >> 1) + 32 * s + (l & 31), u0, s);
-    }
-    __builtin_amdgcn_wave_barrier();
-    enc_row_to_stage(st2, l, zw1);
-    __builtin_amdgcn_wave_barrier();
-    const int64_t by = (int64_t)(2 * u0) * nbx + 64 * s + l;
-    op_finish<TMF, false>(E, R1, zw1, blk, s_oplen[OP ? wv : 0], s_opval[OP ? wv : 0], (2 * u0) * E.nstrips + s, by,
-                          u0, s);
-    __builtin_amdgcn_wave_barrier();
-    enc_row_to_stage(st2, l, zw2);
-    __builtin_amdgcn_wave_barrier();
-    op_finish<TMF, false>(E, R2, zw2, blk, s_oplen[OP ? wv : 0], s_opval[OP ? wv : 0], (2 * u0 + 1) * E.nstrips + s,
-                          by + nbx, u0, E.nstrips + s);
-    __builtin_amdgcn_wave_barrier();
-  }
-  if (MFMA) {  // flagged passes, on the float64 AAN path (~3 % of passes on random data)
-    if (redo0 || redo1) {
-      uint2 w[8];
-      for (int br = 0; br < 2; ++br) {
-        if (!(br == 0 ? redo0 : redo1)) continue;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) w[r] = yq[8 * br + r];
-        enc_dct<0>(w, st);
-        y_out(br);
-      }
-    }
-    if (redoc) c_aan();
-  }
+  y_blocks(0);
+  y_blocks(1);
+  c_blocks();
 }
 
 // Memory-only probe of k_encode420's byte pattern (bench.py's in-run floor for the
@@ -837,7 +564,7 @@ using namespace hic;
 static int encode420(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, int64_t H, int64_t W,
                      int64_t out_row0, int64_t out_rows, int16_t *coef_y, int16_t *coef_cr, int16_t *coef_cb,
                      void *ws_y, void *ws_cr, void *ws_cb, int max_len, void *stream, void *ev_start, void *ev_stop,
-                     bool seg) {
+                     bool seg, int64_t wsb_y = 0, int64_t wsb_c = 0) {
   if (!rgb_rows || !coef_y || !coef_cr || !coef_cb) return arg_error("null pointer");
   if (H < 16 || W < 16 || H >= (1 << 20) || W >= (1 << 20)) return arg_error("image shape");
   if (W % 16 || H % 16) return arg_error("hic_encode420_u8 needs W %% 16 == 0 and H %% 16 == 0");
@@ -855,6 +582,16 @@ static int encode420(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, 
   const bool recs = ws_y && ws_cr && ws_cb;
   if ((ws_y || ws_cr || ws_cb) && !recs) return arg_error("workspaces: all three or none");
   if (recs && (max_len < 0 || max_len > 256)) return arg_error("max_len");
+  if (seg && recs) {
+    // records per strip segment: a narrow image has more of them than 64-block tiles
+    // (hic_rle_rows_workspace_bytes)
+    const int64_t ny = (out_rows / 8) * (W / 8), nc = (out_rows / 16) * (W / 16);
+    const int64_t need_y = (int64_t)hic_rle_rows_workspace_bytes(ny, W / 8, 1);
+    const int64_t need_c = (int64_t)hic_rle_rows_workspace_bytes(nc, W / 16, 2);
+    if (wsb_y < need_y || wsb_c < need_c)
+      return arg_error("hic_encode420_seg_u8: workspaces of %lld / %lld bytes, %lld / %lld needed", (long long)wsb_y,
+                       (long long)wsb_c, (long long)need_y, (long long)need_c);
+  }
   Enc420 E{};
   E.rgb = rgb_rows;
   E.in_row0 = (int)in_row0;
@@ -878,17 +615,13 @@ static int encode420(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, 
   E.nunits = E.nstrips * (int)(out_rows / 16);  // waves
   // one wave per unit (no persistent loop: units are the same size, and the
   // hardware's dispatch balances the tail better than a fixed split)
-  // default 6: row-major, XCD-major workgroups, odd unit rows bottom-up (FETCH_SIZE
-  // 109.6 vs 131.7 MB per 8K launch, kernel 58.0 vs 58.9 us, bench 0.0996 vs 0.1004
-  // ms/step median of 10 alternating pairs: profiles/r04/enc_order_xcd)
+  // default 6: XCD-major workgroups, odd unit rows bottom-up (FETCH_SIZE 109.6 vs
+  // 131.7 MB per 8K launch, kernel 58.0 vs 58.9 us, bench 0.0996 vs 0.1004 ms/step
+  // median of 10 alternating pairs: profiles/r04/enc_order_xcd)
   const int order = knob(HIC_KNOB_ENCODE_ORDER);
-  E.vstack = order & 1;
   E.xcd = (order >> 1) & 1;
   E.alt = (order >> 2) & 1;
-  const int nu = (int)(out_rows / 16);
-  const dim3 grid((unsigned)(E.vstack ? E.nstrips * ((nu + HIC_ENC_WPB - 1) / HIC_ENC_WPB)
-                                      : (E.nunits + HIC_ENC_WPB - 1) / HIC_ENC_WPB)),
-      block(64 * HIC_ENC_WPB);
+  const dim3 grid((unsigned)((E.nunits + HIC_ENC_WPB - 1) / HIC_ENC_WPB)), block(64 * HIC_ENC_WPB);
   hipStream_t s = as_stream(stream);
   hipEvent_t e0 = static_cast<hipEvent_t>(ev_start), e1 = static_cast<hipEvent_t>(ev_stop);
   auto launch = [&](auto kern) {
@@ -897,11 +630,10 @@ static int encode420(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, 
     else
       hipLaunchKernelGGL(kern, grid, block, 0, s, E);
   };
-  const bool mfma = knob(HIC_KNOB_ENCODE_DCT) == 1;
   if (max_len == 15)
-    mfma ? launch(k_encode420<15, true, false>) : launch(k_encode420<15, false, false>);
+    launch(k_encode420<15>);
   else
-    mfma ? launch(k_encode420<0, true, false>) : launch(k_encode420<0, false, false>);
+    launch(k_encode420<0>);
   if (int e = check_launch("k_encode420")) return e;
   if (recs && !aligned) {  // one record per 64-block tile, all three planes (not seg)
     const int64_t ny = (out_rows / 8) * (W / 8), nc = (out_rows / 16) * (W / 16);
@@ -922,76 +654,10 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
 
 extern "C" int hic_encode420_seg_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, int64_t H, int64_t W,
                                     int64_t out_row0, int64_t out_rows, int16_t *coef_y, int16_t *coef_cr,
-                                    int16_t *coef_cb, void *ws_y, void *ws_cr, void *ws_cb, int max_len, void *stream,
-                                    void *ev_start, void *ev_stop) {
+                                    int16_t *coef_cb, void *ws_y, void *ws_cr, void *ws_cb, int64_t ws_bytes_y,
+                                    int64_t ws_bytes_c, int max_len, void *stream, void *ev_start, void *ev_stop) {
   return encode420(rgb_rows, in_row0, in_rows, H, W, out_row0, out_rows, coef_y, coef_cr, coef_cb, ws_y, ws_cr, ws_cb,
-                   max_len, stream, ev_start, ev_stop, true);
-}
-
-extern "C" int hic_encode420_rle_u8(const uint8_t *rgb, int64_t H, int64_t W, const hic_rle_job16 *jobs, int max_len,
-                                    void *stream, void *ev_start, void *ev_stop) {
-  if (!rgb || !jobs) return arg_error("null pointer");
-  if (H < 16 || W < 512 || H % 16 || W % 512 || H >= (1 << 20) || W > 16384)
-    return arg_error("hic_encode420_rle_u8 needs W %% 512 == 0, W <= 16384 and H %% 16 == 0");
-  if (reinterpret_cast<uintptr_t>(rgb) % 8) return arg_error("rgb must be 8-byte aligned");
-  if (H * W * 3 > INT32_MAX) return arg_error("hic_encode420_rle_u8: image exceeds 2 GiB (use the chain)");
-  if (max_len < 1 || max_len > 256) return arg_error("max_len must be in [1, 256] for uint8 symbol lengths");
-  const int64_t nblk[3] = {(H / 8) * (W / 8), (H / 16) * (W / 16), (H / 16) * (W / 16)};
-  if (nblk[0] > (int64_t)INT32_MAX / 63) return arg_error("nblk too large (AC stream >= 2^31)");
-  Enc420 E{};
-  E.rgb = rgb;
-  E.in_row0 = 0;
-  E.in_rows = (int)H;
-  E.H = (int)H;
-  E.W = (int)W;
-  E.out_row0 = 0;
-  E.out_rows = (int)H;
-  E.M = max_len;
-  E.nstrips = (int)(W / 512);
-  E.wlast = 512;
-  E.nunits = E.nstrips * (int)(H / 16);
-  for (int k = 0; k < 3; ++k) {
-    const hic_rle_job16 &J = jobs[k];
-    if (!J.blocks || !J.dc_diff || !J.sym_len || !J.sym_val || !J.d_count || !J.workspace)
-      return arg_error("job %d: null pointer", k);
-    if (J.nblk != nblk[k]) return arg_error("job %d: nblk %lld, expected %lld", k, (long long)J.nblk, (long long)nblk[k]);
-    if (J.d_stitch) return arg_error("job %d: the one-pass encode takes whole images (no stitch)", k);
-    if (reinterpret_cast<uintptr_t>(J.blocks) % 16 || reinterpret_cast<uintptr_t>(J.sym_len) % 16 ||
-        reinterpret_cast<uintptr_t>(J.sym_val) % 16)
-      return arg_error("job %d: blocks / symbol buffers must be 16-byte aligned", k);
-    if (J.sym_cap < 0) return arg_error("job %d: sym_cap", k);
-    E.coef[k] = const_cast<int16_t *>(J.blocks);
-    E.rec[k] = nullptr;
-    E.dc[k] = J.dc_diff;
-    E.sym_len[k] = J.sym_len;
-    E.sym_val[k] = J.sym_val;
-    E.cap[k] = J.sym_cap;
-    E.d_count[k] = J.d_count;
-    E.last_rec[k] = k == 0 ? (int)(2 * (H / 16) * E.nstrips - 1) : (int)((H / 16) * E.nstrips - 1);
-    E.n_ac[k] = nblk[k] * 63;
-    E.gran[k] = static_cast<uint64_t *>(J.workspace);
-    E.gwin[k] = E.gran[k] + 8 * (int64_t)(E.last_rec[k] + 1);  // past the record granules
-  }
-  // the ticket counter and the timeout word: the last words of Y's workspace
-  // (hic_rle_workspace_bytes; past the granules and the chain scan's hand-off)
-  const int64_t words = (int64_t)(hic_rle_workspace_bytes(nblk[0], 64) / sizeof(int64_t));
-  E.ticket = reinterpret_cast<uint32_t *>(E.gran[0] + words - 1);
-  E.fail = E.gran[0] + words - 2;
-  E.epoch = next_epoch();
-  const dim3 grid((unsigned)((E.nunits + HIC_ENC_WPB - 1) / HIC_ENC_WPB)), block(64 * HIC_ENC_WPB);
-  hipStream_t s = as_stream(stream);
-  hipEvent_t e0 = static_cast<hipEvent_t>(ev_start), e1 = static_cast<hipEvent_t>(ev_stop);
-  auto launch = [&](auto kern) {
-    if (e0 || e1)
-      hipExtLaunchKernelGGL(kern, grid, block, 0, s, e0, e1, 0, E);
-    else
-      hipLaunchKernelGGL(kern, grid, block, 0, s, E);
-  };
-  if (max_len == 15)
-    launch(k_encode420<15, false, true>);
-  else
-    launch(k_encode420<0, false, true>);
-  return check_launch("k_encode420 (one-pass)");
+                   max_len, stream, ev_start, ev_stop, true, ws_bytes_y, ws_bytes_c);
 }
 
 extern "C" int hic_probe_encode420(const uint8_t *rgb, int64_t H, int64_t W, int16_t *coef_y, int16_t *coef_cr,

@@ -614,6 +614,7 @@ struct RleJob16 {
   // tiles of 64 blocks from the row's start, the last one shorter; 0 = plain tiles
   int64_t rowb;
   int64_t tpr, rpr;  // tiles and records per row
+  int64_t wsb;       // workspace bytes (0: not checked; a rows job must give it)
 };
 struct RleJobs16 {
   RleJob16 j[kMaxJobs];
@@ -649,6 +650,12 @@ __device__ __forceinline__ bool get_granule(const uint64_t *g, uint32_t tag, int
 #endif
 constexpr int kScan16T = HIC_SCAN16_T;
 static_assert(kScan16T % 64 == 0 && kScan16T <= 1024, "scan partition: whole waves");
+// workspace words of a job with nrec records: the records (3) and their offsets (2),
+// 3 hand-off granules per scan partition and the failure granule, + slack
+inline int64_t rle_ws_words(int64_t nrec) {
+  const int64_t n = nrec > 0 ? nrec : 1;
+  return 5 * n + 3 * ((n + kScan16T - 1) / kScan16T) + 8;
+}
 __global__ __launch_bounds__(kScan16T) void k_rle_scan16b(RleJobs16 jobs, uint32_t epoch) {
   __shared__ Agg s_wave[kScan16T / 64 + 1];
   __shared__ Agg s_pre;
@@ -1384,6 +1391,11 @@ int encode_batch16(RleJobs16 &jobs, hipStream_t s) {
     }
     jobs.j[k].tile0 = t0;
     t0 += jobs.j[k].ntiles;
+    // the scan reads 5 words per record and the partitions' hand-off granules
+    const int64_t need = rle_ws_words(jobs.j[k].nrec) * (int64_t)sizeof(int64_t);
+    if (jobs.j[k].rowb > 0 && jobs.j[k].wsb <= 0) return arg_error("job %d: row segments need workspace_bytes", k);
+    if (jobs.j[k].wsb > 0 && jobs.j[k].wsb < need)
+      return arg_error("job %d: workspace of %lld bytes, %lld needed", k, (long long)jobs.j[k].wsb, (long long)need);
   }
   jobs.total_tiles = t0;
   const uint32_t ep = next_epoch();
@@ -1656,12 +1668,18 @@ extern "C" size_t hic_rle_workspace_bytes(int64_t nblk, int block_len) {
   (void)block_len;
   // sized for the hot path's 32-block half-tile records (hic_encode420_u8's chroma;
   // >= its 64-block tiles and the generic 256-block tiles)
-  const int64_t n = nblk > 0 ? nblk : 1, nt = (n + kWT / 2 - 1) / (kWT / 2);
-  // tile records (3), offsets (2) per tile; 3 hand-off granules per scan partition;
-  // or (hic_encode420_rle_u8) 8 look-back granules per record and 4 per unit row
-  // (<= one per record), then its ticket counter and timeout word
-  const int64_t chain = 5 * nt + 3 * ((nt + kScan16T - 1) / kScan16T) + 8, onepass = 12 * nt + 16;
-  return (size_t)(chain > onepass ? chain : onepass) * sizeof(int64_t);
+  const int64_t n = nblk > 0 ? nblk : 1;
+  return (size_t)rle_ws_words((n + kWT / 2 - 1) / (kWT / 2)) * sizeof(int64_t);
+}
+
+extern "C" size_t hic_rle_rows_workspace_bytes(int64_t nblk, int64_t row_blocks, int records_per_tile) {
+  // records per row segment (hic_encode420_seg_u8 / hic_rle_encode_i16_rows_batch):
+  // rows x ceil(row_blocks / segment) records, segment 64 / records_per_tile blocks
+  const int64_t n = nblk > 0 ? nblk : 1, rb = row_blocks > 0 ? row_blocks : 1;
+  const int64_t seg = records_per_tile == 2 ? kWT / 2 : kWT;
+  const int64_t nrec = ((n + rb - 1) / rb) * ((rb + seg - 1) / seg);
+  const size_t rows = (size_t)rle_ws_words(nrec) * sizeof(int64_t), tiles = hic_rle_workspace_bytes(nblk, 64);
+  return rows > tiles ? rows : tiles;
 }
 
 extern "C" int hic_rle_shard_summary_i16(const int16_t *blocks, int64_t nblk, int block_len, void *workspace,
@@ -1727,7 +1745,8 @@ extern "C" int hic_rle_encode_i16_tiles_batch(int n, const hic_rle_job16 *jobs, 
     if (a.records_per_tile != 0 && a.records_per_tile != 1 && a.records_per_tile != 2)
       return arg_error("job %d: records_per_tile must be 1 or 2", k);
     J.j[k] = RleJob16{a.blocks, a.nblk, a.d_stitch, a.dc_diff, a.sym_len, a.sym_val, a.sym_cap, a.d_count,
-                      static_cast<int64_t *>(a.workspace), 0, 0, 0, a.records_per_tile == 2 ? 1 : 0};
+                      static_cast<int64_t *>(a.workspace), 0, 0, 0, a.records_per_tile == 2 ? 1 : 0, 0, 0, 0,
+                      a.workspace_bytes};
   }
   return encode_batch16(J, as_stream(stream));
 }
@@ -1750,7 +1769,8 @@ extern "C" int hic_rle_encode_i16_rows_batch(int n, const hic_rle_job16 *jobs, c
     const int64_t rb = h_row_blocks[k];
     if (rb < 1 || a.nblk % rb) return arg_error("job %d: row_blocks must divide nblk", k);
     J.j[k] = RleJob16{a.blocks, a.nblk, a.d_stitch, a.dc_diff, a.sym_len, a.sym_val, a.sym_cap, a.d_count,
-                      static_cast<int64_t *>(a.workspace), 0, 0, 0, a.records_per_tile == 2 ? 1 : 0, rb};
+                      static_cast<int64_t *>(a.workspace), 0, 0, 0, a.records_per_tile == 2 ? 1 : 0, rb, 0, 0,
+                      a.workspace_bytes};
   }
   return encode_batch16(J, as_stream(stream));
 }

@@ -61,12 +61,6 @@ def check_count(c, channel=""):
     raise MemoryError("symbol buffer too small for channel %s: %d symbols needed" % (channel, -c))
 
 
-# Encoder.encode's default where the one-pass kernel applies (whole image, W % 512
-# == 0): off -- exact, but 0.135 vs 0.100 ms per 8K image against the fused
-# transform + scan + emit launches on one MI355X (one-pass encode)
-ONEPASS_DEFAULT = False
-
-
 def encoder_layout(H, W, rows=None, fused=None, index=False):
     """(fused, rpt) of an Encoder of rows `rows` of an H x W image (None: the whole
     image, its own encoder): whether it runs the fused kernel (None = the measured
@@ -92,23 +86,19 @@ class Encoder:
     """rows=(r0, r1) makes this encoder one row-shard of an H x W image (r0 even;
     shards of one image split at multiples of 16 rows so chroma blocks align)."""
 
-    def __init__(self, H, W, max_len=15, rows=None, out=None, fused=None, index=False, landing_rpt=None,
-                 onepass=None):
+    def __init__(self, H, W, max_len=15, rows=None, out=None, fused=None, index=False, landing_rpt=None):
         """out: optional {channel: (coef (n, 64) int16, dc (n,) int32)} device views the
         encoder writes into (a gathering rank points them at its slice of the whole
         image's buffers, so its own shard needs no copy).
         fused: colour + 4:2:0 + DCT in one kernel (hic_encode420_u8, the planes never
         reach HBM; W, H and the row range multiples of 16); None = the faster path
-        as measured: fused when W % 512 == 0, else the two-kernel chain (a ragged
-        last strip needs a tile pass for its RLE records: 3840x2160 measured 44.6 vs
-        40.5 us per image); False = the chain.
+        as measured (encoder_layout): fused for a whole image with W % 16 == 0 (a
+        ragged last strip gets one RLE record per strip segment: 3840x2160 38.1-40.1
+        vs 40.5-41.4 us per image for the chain), and for a row
+        shard or an encoder with a tile index when W % 512 == 0; False = the chain.
         landing_rpt: a landing zone only (the gathering rank of a stream gather): no
         transform, no plane buffers, and the RLE record layout of the shards that
-        fill it (their encoder_layout rpt), whatever this shape alone would pick.
-        onepass: encode() as ONE kernel (hic_encode420_rle_u8: the fused transform
-        with the DC / RLE emission and a look-back for the stream offsets) -- whole
-        images with W % 512 == 0, W <= 16384 and no tile index; None = ONEPASS_DEFAULT where
-        it applies, False = transform() + entropy()."""
+        fill it (their encoder_layout rpt), whatever this shape alone would pick."""
         if H < 2 or W < 2:
             raise ValueError("image must be at least 2 x 2")
         device.require_gpu()
@@ -123,11 +113,6 @@ class Encoder:
             self.fused, self.rpt = False, dict(landing_rpt)
         else:
             self.fused, self.rpt = encoder_layout(H, W, rows, fused, index)
-        can_1p = (not self.landing and self.fused and (r0, r1) == (0, H) and W % 512 == 0 and W <= 16384
-                  and not self.want_index and H * W * 3 <= 2**31 - 1)
-        if onepass and not can_1p:
-            raise ValueError("the one-pass encode needs a whole image with W % 512 == 0 (fused), no tile index")
-        self.onepass = can_1p and (ONEPASS_DEFAULT if onepass is None else bool(onepass))
         # a whole image's ragged last strip (W % 512 != 0): the fused kernel writes one
         # RLE record per strip segment (hic_encode420_seg_u8) and the scan / emit walk
         # row segments (hic_rle_encode_i16_rows_batch): no tile pass
@@ -143,7 +128,7 @@ class Encoder:
             self.cr = device.empty(cs, torch.uint8)
             self.cb = device.empty(cs, torch.uint8)
         self.planes = {"lum": self.y, "cr": self.cr, "cb": self.cb}
-        self.coef, self.dc, self.sym_len, self.sym_val, self.ws = {}, {}, {}, {}, {}
+        self.coef, self.dc, self.sym_len, self.sym_val, self.ws, self.ws_bytes = {}, {}, {}, {}, {}, {}
         self.cap = {}
         self.counts = device.zeros((3,), torch.int64)
         self.summaries = device.zeros((3, 4), torch.int64)
@@ -162,7 +147,12 @@ class Encoder:
             self.cap[k] = n * 63 + 1 + (lead * 63 // max_len if max_len > 0 else 1)
             self.sym_len[k] = device.empty((self.cap[k],), torch.uint8)
             self.sym_val[k] = device.empty((self.cap[k],), torch.int16)
-            self.ws[k] = device.workspace(lib.hic_rle_workspace_bytes(n, 64))
+            # a whole image's row-segment records outnumber its 64-block tiles when the
+            # image is narrow (W <= ~350): size by the records
+            rowb = -(-self.shapes[k][1] // 8)
+            self.ws_bytes[k] = (lib.hic_rle_rows_workspace_bytes(n, rowb, self.rpt[k]) if self.seg
+                                else lib.hic_rle_workspace_bytes(n, 64))
+            self.ws[k] = device.workspace(self.ws_bytes[k])
         # index=True: the encoder-side tile index a device decoder reads
         # (Decoder.decode(..., index=enc.index)): 3 int64 per 64-block tile
         self.index = ({k: device.empty((3 * -(-self.coef[k].shape[0] // 64),), torch.int64) for k in CHANNELS}
@@ -195,10 +185,15 @@ class Encoder:
             a, b = self.input_span()
             if rgb.shape[0] * self.W * 3 > 2**31 - 1 and in_row0 <= a and in_row0 + rgb.shape[0] >= b:
                 rgb, in_row0 = rgb[a - in_row0:b - in_row0], a
-            _lib.call("hic_encode420_seg_u8" if self.seg else "hic_encode420_u8", device.ptr(rgb), in_row0,
-                      rgb.shape[0], self.H, self.W, r0, r1 - r0,
-                      *[device.ptr(self.coef[k]) for k in CHANNELS], *[device.ptr(self.ws[k]) for k in CHANNELS],
-                      self.max_len, s, *ev)
+            coefs = [device.ptr(self.coef[k]) for k in CHANNELS]
+            wss = [device.ptr(self.ws[k]) for k in CHANNELS]
+            if self.seg:
+                _lib.call("hic_encode420_seg_u8", device.ptr(rgb), in_row0, rgb.shape[0], self.H, self.W, r0, r1 - r0,
+                          *coefs, *wss, self.ws_bytes["lum"], min(self.ws_bytes["cr"], self.ws_bytes["cb"]),
+                          self.max_len, s, *ev)
+            else:
+                _lib.call("hic_encode420_u8", device.ptr(rgb), in_row0, rgb.shape[0], self.H, self.W, r0, r1 - r0,
+                          *coefs, *wss, self.max_len, s, *ev)
             return
         _lib.call("hic_rgb_to_ycrcb420_rows", device.ptr(rgb), in_row0, rgb.shape[0], self.H, self.W, r0, r1 - r0,
                   device.ptr(self.y), device.ptr(self.cr), device.ptr(self.cb), s)
@@ -241,15 +236,6 @@ class Encoder:
                           device.ptr(self.ws[k]), device.ptr(self.index[k]), s)
 
     def encode(self, rgb, stream=None, dct_events=None):
-        if self.onepass:
-            # transform + DC DPCM + AC RLE of the three channels in one launch
-            # (dct_events time it)
-            if tuple(rgb.shape) != (self.H, self.W, 3):
-                raise ValueError("the one-pass encode takes the whole H x W x 3 image")
-            ev = (dct_events.start, dct_events.stop) if dct_events is not None else (None, None)
-            _lib.call("hic_encode420_rle_u8", device.ptr(rgb), self.H, self.W, self._rle_jobs(None), self.max_len,
-                      device.stream_ptr(stream), *ev)
-            return
         self.transform(rgb, stream, dct_events=dct_events)
         self.entropy(stream)
 
@@ -259,7 +245,8 @@ class Encoder:
             jobs[i] = _lib.RleJob16(self.coef[k].data_ptr(), self.coef[k].shape[0],
                                     stitch[i].data_ptr() if stitch is not None else None, self.dc[k].data_ptr(),
                                     self.sym_len[k].data_ptr(), self.sym_val[k].data_ptr(), self.cap[k],
-                                    self.counts[i:i + 1].data_ptr(), self.ws[k].data_ptr(), self.rpt[k])
+                                    self.counts[i:i + 1].data_ptr(), self.ws[k].data_ptr(), self.rpt[k],
+                                    self.ws_bytes[k])
         return jobs
 
     def hic_image(self, stream=None):

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define HIC_ABI_VERSION 2
+#define HIC_ABI_VERSION 3
 
 #define HIC_OK 0
 #define HIC_ERR_ARG (-1)      /* bad shape / pointer / enum: the reference asserts or raises */
@@ -66,7 +66,7 @@ int hic_device_count(int *h_n);
  * Every selectable path is bit-exact: a knob never changes results, only which
  * kernel variant computes them.  The library reads no environment variables.
  * Values are process-wide; -1 restores the default. */
-#define HIC_KNOB_DCT_PATH 0         /* forward DCT of aligned planes: 5 integer-MFMA transform (ZIGZAG_I16 output), 1 / 2 float64 AAN, 0 exact replica */
+#define HIC_KNOB_DCT_PATH 0         /* forward DCT of aligned planes: 3 packed-float32 AAN (ZIGZAG_I16 output; the default), 1 / 2 float64 AAN, 0 exact replica */
 #define HIC_KNOB_DCT_WAVES_PER_CU 1 /* forward DCT persistent grid (waves per CU; 0 = one wave per set) */
 #define HIC_KNOB_COLOR_TILED 2      /* 1: LDS-tiled colour kernels instead of the wave-walk ones */
 #define HIC_KNOB_COLOR_SEG 3        /* wave-walk colour: chroma rows per segment (8 default, 16) */
@@ -75,11 +75,9 @@ int hic_device_count(int *h_n);
 #define HIC_KNOB_RLD_NT 6           /* 1: nontemporal block stores in the RLE decode */
 #define HIC_KNOB_RLD_GENERIC 7      /* 1: the generic (any block size) RLE decode */
 #define HIC_KNOB_DEV 8              /* dev builds only (-DHIC_DEV): timing bits that skip work; refused otherwise */
-#define HIC_KNOB_ENCODE_WAVES 9     /* retired (round 4): hic_encode420_u8 runs 3 waves per SIMD; only 3 is accepted */
-#define HIC_KNOB_ENCODE_NT 10       /* retired (round 4): nontemporal coefficient stores; only 1 is accepted */
-#define HIC_KNOB_ENCODE_DCT 11      /* hic_encode420_u8 transform: 0 float64 AAN, 1 integer MFMA (dct_mfma.h) */
-#define HIC_KNOB_DCT_MFMA 12        /* k_dct_mfma variant (0..3): bit 0 = next set's pixels prefetched, bit 1 = 2 waves per SIMD (else 3) */
-#define HIC_KNOB_ENCODE_ORDER 13     /* hic_encode420_u8 unit order: 0 row-major (a workgroup = 4 strips side by side), 1 = 4 units stacked vertically (their pyrDown halo rows shared in the CU's caches); + 2: workgroups remapped XCD-major (neighbouring units on one XCD's L2); + 4: odd unit rows run their colour rows bottom-up (the halo rows two unit rows share fetched at the same time); default 6 */
+/* knobs 9-12 were retired in rounds 4-5 (encode waves / nontemporal stores / integer-MFMA
+ * transforms: measured slower, removed); hic_set_knob refuses them */
+#define HIC_KNOB_ENCODE_ORDER 13     /* hic_encode420_u8 unit order: 0 row-major; + 2: workgroups remapped XCD-major (neighbouring units on one XCD's L2); + 4: odd unit rows run their colour rows bottom-up (the halo rows two unit rows share fetched at the same time); default 6; odd values refused */
 #define HIC_KNOB_COUNT 14
 int hic_set_knob(int knob, int value);
 int hic_get_knob(int knob, int *h_value);
@@ -132,8 +130,10 @@ int hic_dct_quant_rle_u8(const uint8_t *plane, int64_t H, int64_t W, int64_t str
 /* hic_dct_quant_rle_u8 for up to 16 planes (the Y, Cr, Cb of one image, or the
  * planes of consecutive images): ONE launch, a persistent grid over all their
  * 64-block sets (each plane's table read at run time).  Each job names its plane,
- * table, ZIGZAG_I16 output and RLE workspace.  Events (nullable) time that
- * launch.  Ragged planes (H or W not a multiple of 8) take separate launches. */
+ * table, ZIGZAG_I16 output and RLE workspace; rle_workspace NULL for every job
+ * (round 5) = the records-free pass (DCT + quantize + zig-zag only, no tile
+ * records).  Events (nullable) time that launch.  Ragged planes (H or W not a
+ * multiple of 8) take separate launches. */
 typedef struct {
   const uint8_t *plane;
   int64_t H, W, stride;
@@ -169,11 +169,14 @@ int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, 
  * record), the last strip's record covering what remains -- no tile pass after the
  * launch.  Identical to hic_encode420_u8 when W % 512 == 0.  Consume the records with
  * hic_rle_encode_i16_rows_batch (row_blocks W/8 for Y, W/16 for Cr / Cb,
- * records_per_tile 1 / 2). */
+ * records_per_tile 1 / 2).  ws_bytes_y / ws_bytes_c: the sizes of ws_y and of each of
+ * ws_cr / ws_cb; at least hic_rle_rows_workspace_bytes(nblk, row_blocks,
+ * records_per_tile) of the plane (a narrow image has more records than 64-block
+ * tiles), else HIC_ERR_ARG and nothing is launched (round 5). */
 int hic_encode420_seg_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, int64_t H, int64_t W,
                          int64_t out_row0, int64_t out_rows, int16_t *coef_y, int16_t *coef_cr, int16_t *coef_cb,
-                         void *ws_y, void *ws_cr, void *ws_cb, int max_len, void *stream, void *ev_start,
-                         void *ev_stop);
+                         void *ws_y, void *ws_cr, void *ws_cb, int64_t ws_bytes_y, int64_t ws_bytes_c, int max_len,
+                         void *stream, void *ev_start, void *ev_stop);
 /* Timing events (hipEvent_t handles) for the *_timed entry points. */
 int hic_event_create(void **h_event);
 int hic_event_destroy(void *event);
@@ -293,6 +296,8 @@ typedef struct {
   void *workspace;
   int64_t records_per_tile; /* 0 or 1: one tile record per 64 blocks (hic_dct_quant_rle_u8);
                                2: one per 32 blocks (hic_encode420_u8's chroma planes) */
+  int64_t workspace_bytes;  /* size of `workspace` (round 5): checked against the job's
+                               records when > 0; required by hic_rle_encode_i16_rows_batch */
 } hic_rle_job16;
 int hic_rle_encode_i16_tiles_batch(int n, const hic_rle_job16 *jobs, int max_len, void *stream);
 /* The same over records per row segment (round 4; hic_encode420_seg_u8's records):
@@ -302,24 +307,10 @@ int hic_rle_encode_i16_tiles_batch(int n, const hic_rle_job16 *jobs, int max_len
  * h_row_blocks[k] % 64 == 0 identical to hic_rle_encode_i16_tiles_batch. */
 int hic_rle_encode_i16_rows_batch(int n, const hic_rle_job16 *jobs, const int64_t *h_row_blocks, int max_len,
                                   void *stream);
-/* ---- one-pass encode (round 4): hic_encode420_u8 + hic_rle_encode_i16_tiles_batch
- *      of the three channels in ONE kernel -- compression.jpeg_compression's
- *      transform (compression.py:16-39) and codec.jpeg_encode's differential_coding
- *      + run_length_coding of each channel (codec.py:47-99, 286-301).  Each unit's
- *      records take their stream offsets by a decoupled look-back over the earlier
- *      records' published aggregates; DC differences and AC symbols leave from the
- *      unit's LDS stage (no coefficient re-read, no scan launch).  Output identical
- *      to the two calls it replaces.
- *  rgb: the whole H x W x 3 uint8 image (8-byte aligned, < 2 GiB); W % 512 == 0,
- *  H % 16 == 0.  jobs[0..2] = Y, Cr, Cb: blocks = the ZIGZAG_I16 coefficient output
- *  (nblk = (H/8)(W/8), (H/16)(W/16), (H/16)(W/16)), dc_diff, sym_len / sym_val /
- *  sym_cap / d_count as hic_rle_encode_i16; d_stitch must be NULL (whole images);
- *  records_per_tile is ignored; workspace: hic_rle_workspace_bytes(nblk, 64) bytes,
- *  zero-filled before its first use (it carries tagged look-back granules and the
- *  launch's unit tickets), reusable after, one launch at a time per workspace.
- *  ev_start / ev_stop (optional): the launch's own begin / end timestamps. */
-int hic_encode420_rle_u8(const uint8_t *rgb, int64_t H, int64_t W, const hic_rle_job16 *jobs, int max_len,
-                         void *stream, void *ev_start, void *ev_stop);
+/* Workspace bytes of a row-segment job (hic_encode420_seg_u8 /
+ * hic_rle_encode_i16_rows_batch): nblk blocks in rows of row_blocks, records_per_tile
+ * as the job's; never less than hic_rle_workspace_bytes(nblk, 64). */
+size_t hic_rle_rows_workspace_bytes(int64_t nblk, int64_t row_blocks, int records_per_tile);
 /* hic_rle_shard_summary_i16 from the tile records of hic_dct_quant_rle_u8. */
 int hic_rle_shard_summary_tiles(const int16_t *blocks, int64_t nblk, void *workspace, int64_t *d_summary,
                                 void *stream);

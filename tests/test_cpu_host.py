@@ -34,7 +34,7 @@ def test_ctypes_signatures_match_header():
     for name, args in decl.items():
         nargs = 0 if args.strip() == "void" else len([a for a in args.split(",") if a.strip()])
         assert nargs == len(_lib.SIGNATURES[name][1]), name
-    assert _lib.load().hic_abi_version() == 2
+    assert _lib.load().hic_abi_version() == 3
     # argument kinds: every pointer parameter is bound as a pointer, every scalar
     # with the header's width and signedness
     kinds = {"int64_t": ctypes.c_int64, "int": ctypes.c_int, "int32_t": ctypes.c_int32, "size_t": ctypes.c_size_t,
@@ -69,11 +69,14 @@ def test_knob_defaults_and_ranges():
     bottom-up (profiles/r04/enc_order_xcd); out-of-range values are refused."""
     assert _lib.get_knob("encode_order") == 6
     assert _lib.get_knob("dct_path") == 1
-    with _lib.knobs(encode_order=3):
-        assert _lib.get_knob("encode_order") == 3
+    with _lib.knobs(encode_order=2):
+        assert _lib.get_knob("encode_order") == 2
     assert _lib.get_knob("encode_order") == 6
-    with pytest.raises(ValueError):
-        _lib.set_knob("encode_order", 8)
+    for bad in (8, 3, 1):  # odd: the stacked-unit order was removed in round 5
+        with pytest.raises(ValueError):
+            _lib.set_knob("encode_order", bad)
+    for retired in (9, 10, 11, 12):  # retired knobs are refused outright
+        assert _lib.load().hic_set_knob(retired, 0) == _lib.HIC_ERR_ARG
 
 
 def _names(d, prefix):
@@ -378,6 +381,29 @@ def test_rle_workspace_covers_scan_partitions():
             nrec = -(-n * rpt // 64)
             need = (5 * nrec + 3 * -(-nrec // 256) + 1) * 8
             assert have >= need, (n, rpt, have, need)
+
+
+@pytest.mark.parametrize("H,W", [(1024, 16), (2048, 16), (1024, 48), (48, 16), (16, 1040), (1088, 1920),
+                                 (2160, 3840), (4320, 7680)])
+def test_rle_rows_workspace_covers_segment_records(H, W):
+    """a whole image's fused encoder with a ragged last strip
+    (hic_encode420_seg_u8) writes one record per strip segment of every block row:
+    rows x ceil(W / 512) of them, far more than the 64-block tiles of a narrow, tall
+    image.  hic_rle_rows_workspace_bytes covers those records, their offsets and the
+    scan's granules, and the Encoder sizes its workspaces with it (and the library
+    refuses a smaller one, tested on the GPU)."""
+    from hiccup_amd import pipeline
+    lib = _lib.load()
+    fused, rpt = pipeline.encoder_layout(H, W)
+    for k, (h, w, rowb) in {"lum": (H, W, W // 8), "cr": (H // 2, W // 2, W // 16)}.items():
+        n = (h // 8) * (w // 8)
+        nrec = (n // rowb) * -(-rowb // (64 // rpt[k]))
+        need = (5 * nrec + 3 * -(-nrec // 256) + 1) * 8
+        have = lib.hic_rle_rows_workspace_bytes(n, rowb, rpt[k])
+        assert have >= need and have >= lib.hic_rle_workspace_bytes(n, 64), (k, have, need)
+    if W <= 48 and H >= 1024:  # the case the advisor found: the tile-sized workspace is too small
+        n = (H // 8) * (W // 8)
+        assert lib.hic_rle_workspace_bytes(n, 64) < lib.hic_rle_rows_workspace_bytes(n, W // 8, 1)
 
 
 def test_stream_gather_record_layout_past_2gib():

@@ -381,21 +381,20 @@ def _structured_rgb(kind, H, W, seed):
     raise ValueError(kind)
 
 
-# both transforms of the fused kernel (knob encode_dct: 0 float64 AAN, 1 integer
-# MFMA) against the chain's plane DCT on both of its paths (integer MFMA, float64 AAN)
-@pytest.mark.parametrize("enc_dct,chain_path", [(0, _lib.DCT_PATH_MFMA), (1, _lib.DCT_PATH_F64), (1, _lib.DCT_PATH_MFMA)])
+# the fused kernel against the chain's plane DCT on both of its shipped paths (packed
+# float32 with the cooperative float64 redo, float64 AAN)
+@pytest.mark.parametrize("chain_path", [_lib.DCT_PATH_PK, _lib.DCT_PATH_F64])
 @pytest.mark.parametrize("kind", ["random", "levels", "colour_levels", "blocks", "flat"])
 @pytest.mark.parametrize("H,W", [(16, 512), (144, 2048), (1088, 1536)])
-def test_fused_encoder_matches_two_kernel_chain(kind, H, W, enc_dct, chain_path):
+def test_fused_encoder_matches_two_kernel_chain(kind, H, W, chain_path):
     """hic_encode420_u8 (colour + pyrDown + DCT + tile records in one kernel, exact
     tie fallbacks in place) == the two-kernel chain (hic_rgb_to_ycrcb420 +
     hic_dct_quant_rle_u8_batch), symbols and DC streams included (the fused chroma
     records are 32-block half tiles)."""
     rgb = _structured_rgb(kind, H, W, H + W)
     x = device.to_device(rgb)
-    got, exp = pipeline.Encoder(H, W, fused=True, onepass=False), pipeline.Encoder(H, W, fused=False)
-    with _lib.knobs(encode_dct=enc_dct):
-        got.encode(x)
+    got, exp = pipeline.Encoder(H, W, fused=True), pipeline.Encoder(H, W, fused=False)
+    got.encode(x)
     with _lib.knobs(dct_path=chain_path):
         exp.encode(x)
     a, b = got.result(), exp.result()
@@ -408,23 +407,24 @@ def test_fused_encoder_matches_two_kernel_chain(kind, H, W, enc_dct, chain_path)
         np.testing.assert_array_equal(got.shard_summaries().cpu().numpy(), exp.shard_summaries().cpu().numpy())
 
 
-@pytest.mark.parametrize("enc_dct", [0, 1])
 @pytest.mark.parametrize("kind", ["random", "levels", "blocks", "flat"])
-@pytest.mark.parametrize("H,W", [(2160, 3840), (1088, 1920), (32, 528), (48, 16), (16, 1040)])
-def test_fused_encoder_ragged_matches_chain(kind, H, W, enc_dct):
+@pytest.mark.parametrize("H,W", [(2160, 3840), (1088, 1920), (32, 528), (48, 16), (16, 1040), (2048, 16),
+                                 (1024, 48)])
+def test_fused_encoder_ragged_matches_chain(kind, H, W):
     """Widths that are not a multiple of 512: the fused kernel's last strip is
     ragged (lanes past W store nothing, the right-border pixel goes to the strip's
     last lane); the whole image's encoder writes one RLE record per strip segment
     (hic_encode420_seg_u8) and the scan / emit walk row segments -- symbols and DC
     equal the two-kernel chain's; with a tile index the records come from a tile
-    pass after the launch (hic_encode420_u8), equal too."""
-    test_fused_encoder_matches_two_kernel_chain(kind, H, W, enc_dct, _lib.DCT_PATH_MFMA)
+    pass after the launch (hic_encode420_u8), equal too.  2048x16 and 1024x48 are
+    the narrow, tall shapes whose segment records outnumber their 64-block tiles
+    (ADVICE r4)."""
+    test_fused_encoder_matches_two_kernel_chain(kind, H, W, _lib.DCT_PATH_PK)
     rgb = _structured_rgb(kind, H, W, H + W)
     x = device.to_device(rgb)
     got, exp = pipeline.Encoder(H, W, fused=True, index=True), pipeline.Encoder(H, W, fused=False)
     assert not got.seg
-    with _lib.knobs(encode_dct=enc_dct):
-        got.encode(x)
+    got.encode(x)
     exp.encode(x)
     a, b = got.result(), exp.result()
     for k in pipeline.CHANNELS:
@@ -432,83 +432,54 @@ def test_fused_encoder_ragged_matches_chain(kind, H, W, enc_dct):
             np.testing.assert_array_equal(a[k][j], b[k][j], err_msg="%s %s" % (k, what))
 
 
-@pytest.mark.parametrize("order", [0, 1, 2, 3, 4, 6, 7])
+@pytest.mark.parametrize("order", [0, 2, 4, 6])
 @pytest.mark.parametrize("kind", ["random", "levels", "flat"])
 @pytest.mark.parametrize("H,W", [(16, 512), (48, 1024), (80, 2048), (272, 1536), (144, 1040), (2160, 3840)])
 def test_fused_encoder_unit_order(kind, H, W, order):
-    """knob encode_order (0: a workgroup = 4 strips side by side, 1: 4 vertically
-    stacked units of one strip, unit-row counts not a multiple of 4 and ragged last
-    strips included; 2 / 3: the same with workgroups remapped XCD-major; + 4: odd
-    unit rows run their colour rows bottom-up) == the
-    two-kernel chain."""
+    """knob encode_order (0: a workgroup = 4 strips side by side; + 2: workgroups
+    remapped XCD-major; + 4: odd unit rows run their colour rows bottom-up; ragged
+    last strips included) == the two-kernel chain."""
     with _lib.knobs(encode_order=order):
-        test_fused_encoder_matches_two_kernel_chain(kind, H, W, 0, _lib.DCT_PATH_F64)
+        test_fused_encoder_matches_two_kernel_chain(kind, H, W, _lib.DCT_PATH_F64)
 
 
-@pytest.mark.parametrize("max_len", [15, 4])
-@pytest.mark.parametrize("kind", ["random", "levels", "colour_levels", "blocks", "flat", "sparse", "zeros"])
-@pytest.mark.parametrize("H,W", [(16, 512), (32, 1024), (144, 2048), (1088, 1536), (400, 512)])
-def test_onepass_matches_chain(kind, H, W, max_len):
-    """hic_encode420_rle_u8 (transform + DC DPCM + AC RLE in one kernel, stream
-    offsets by look-back) == the fused transform + the scan / emit launches:
-    coefficients, DC differences, both symbol arrays and the counts, for dense
-    blocks, exact-tie images, constant blocks, long carried zero runs (flat, sparse:
-    a few nonzeros far apart; zeros: an all-black image, one EOB per plane), with
-    max_len 15 (the M = 15 specialisation) and 4 (the generic one).  Two images back to back on the same encoder (the ticket
-    counter resets, the look-back granules of the first launch never match)."""
-    rng = np.random.default_rng(H * 3 + W)
-    if kind == "sparse":
-        rgb = np.full((H, W, 3), 128, np.uint8)
-        for _ in range(5):
-            rgb[rng.integers(0, H), rng.integers(0, W)] = rng.integers(0, 256, 3)
-    elif kind == "zeros":
-        rgb = np.zeros((H, W, 3), np.uint8)
-    else:
-        rgb = _structured_rgb(kind, H, W, H + W)
-    rgb2 = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
-    got = pipeline.Encoder(H, W, max_len=max_len, onepass=True)
-    exp = pipeline.Encoder(H, W, max_len=max_len, fused=True, onepass=False)
-    assert got.onepass and not exp.onepass
-    for img in (rgb, rgb2, rgb):
-        x = device.to_device(img)
-        got.encode(x)
-        exp.encode(x)
-        a, b = got.result(), exp.result()
-        for k in pipeline.CHANNELS:
-            for j, what in enumerate(("coef", "dc", "sym_len", "sym_val")):
-                np.testing.assert_array_equal(a[k][j], b[k][j], err_msg="%s %s" % (k, what))
-        np.testing.assert_array_equal(got.counts.cpu().numpy(), exp.counts.cpu().numpy())
-
-
-def test_onepass_streams_and_small_cap():
-    """Four one-pass encoders on two streams at once (their look-backs and tickets
-    independent) equal the single-stream results; a symbol buffer one short reports
-    -(needed) and writes nothing past its end."""
-    H, W = 1088, 2048
-    rng = np.random.default_rng(5)
-    imgs = [device.to_device(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)) for _ in range(4)]
-    encs = [pipeline.Encoder(H, W, onepass=True) for _ in range(4)]
-    ss = [torch.cuda.Stream(), torch.cuda.Stream()]
-    torch.cuda.synchronize()
-    for i, e in enumerate(encs):
-        e.encode(imgs[i], stream=ss[i % 2])
-    torch.cuda.synchronize()
-    for i, e in enumerate(encs):
-        ref = pipeline.Encoder(H, W, fused=True, onepass=False)
-        ref.encode(imgs[i])
-        a, b = e.result(), ref.result()
-        for k in pipeline.CHANNELS:
-            for j in range(4):
-                np.testing.assert_array_equal(a[k][j], b[k][j], err_msg="%d %s %d" % (i, k, j))
-    # a symbol buffer one short of the luma count
-    e = encs[0]
-    need = int(e.counts[0].item())
-    e.cap["lum"] = need - 1
-    e.sym_len["lum"].fill_(0xAB)
-    e.encode(imgs[0])
-    torch.cuda.synchronize()
-    assert int(e.counts[0].item()) == -need
-    assert int(e.sym_len["lum"][need - 1].item()) == 0xAB
+@pytest.mark.parametrize("H,W", [(2048, 16), (1024, 48), (4096, 32)])
+def test_seg_workspace_canary_and_refusal(H, W):
+    """the row-segment records of a narrow, tall image need more
+    workspace than its 64-block tiles.  Every workspace is followed by a canary that
+    must survive the fused encode and the scan / emit (nothing is written past the
+    size hic_rle_rows_workspace_bytes gives), and a workspace one record short is
+    refused by both the fused kernel's launcher and the rows batch (HIC_ERR_ARG,
+    nothing launched)."""
+    lib = _lib.load()
+    rgb = device.to_device(np.random.default_rng(W).integers(0, 256, (H, W, 3), dtype=np.uint8))
+    enc = pipeline.Encoder(H, W)
+    assert enc.seg
+    canary = 0x5A5A5A5A5A5A5A5A - (1 << 64)
+    for k in pipeline.CHANNELS:
+        n = enc.ws[k].numel()
+        buf = device.zeros((n + 64,), torch.int64)
+        buf[n:] = canary
+        enc.ws[k] = buf
+    enc.encode(rgb)
+    ref = pipeline.Encoder(H, W, fused=False)
+    ref.encode(rgb)
+    a, b = enc.result(), ref.result()
+    for k in pipeline.CHANNELS:
+        n = enc.ws[k].numel() - 64
+        assert (enc.ws[k][n:] == canary).all().item(), k
+        for j in range(4):
+            np.testing.assert_array_equal(a[k][j], b[k][j], err_msg=k)
+    # one record (3 words) short: refused
+    r0 = enc.ws_bytes["lum"]
+    enc.ws_bytes["lum"] = r0 - 24
+    with pytest.raises(ValueError, match="workspace"):
+        enc.transform(rgb)
+    with pytest.raises(ValueError, match="workspace"):
+        enc.entropy()
+    enc.ws_bytes["lum"] = r0
+    tiles = lib.hic_rle_workspace_bytes(enc.coef["lum"].shape[0], 64)
+    assert tiles < r0  # the tile-sized workspace the advisor found too small
 
 
 @pytest.mark.timeout(900)

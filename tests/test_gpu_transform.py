@@ -98,11 +98,11 @@ def test_layouts_roundtrip(layout, shape):
         np.testing.assert_array_equal(device.to_host(rec), orcc.inv_dct_channel(exp, tab))
 
 
-@pytest.mark.parametrize("path", [-1, _lib.DCT_PATH_MFMA, _lib.DCT_PATH_F64])
+@pytest.mark.parametrize("path", [-1, _lib.DCT_PATH_PK, _lib.DCT_PATH_F64])
 @pytest.mark.parametrize("H,W", [(4096, 4096), (4320, 7680)])
 def test_full_size_bit_exact(H, W, path):
     """BASELINE configs 2/3 plane sizes, bit-exact against the C oracle (multi-threaded),
-    on the default forward path, the integer-MFMA one and the float64 AAN one."""
+    on the default forward path, the packed-float32 one and the float64 AAN one."""
     with _lib.knobs(dct_path=path):
         _full_size_bit_exact(H, W)
 
@@ -130,7 +130,7 @@ def test_tie_blocks_many():
         np.testing.assert_array_equal(transform.dct_channel(plane, QT[tab]), orcc.dct_channel(plane, tab, threads=8))
 
 
-@pytest.mark.parametrize("path", [_lib.DCT_PATH_MFMA, _lib.DCT_PATH_F64, _lib.DCT_PATH_EXACT])
+@pytest.mark.parametrize("path", [_lib.DCT_PATH_PK, _lib.DCT_PATH_F64, _lib.DCT_PATH_EXACT])
 @pytest.mark.parametrize("kind", ["levels4", "nearflat", "stripes", "checker", "blur"])
 def test_fast_path_structured_ties(kind, path):
     with _lib.knobs(dct_path=path):
@@ -195,11 +195,11 @@ def test_bad_args():
         _lib.call("hic_dct_quant_u8", device.ptr(dev), 8, 8, 8, 0, 9, device.ptr(out), device.stream_ptr())
 
 
-@pytest.mark.parametrize("path", [_lib.DCT_PATH_MFMA, _lib.DCT_PATH_F64])
-@pytest.mark.parametrize("kind", ["random", "levels4", "nearflat", "blur"])
+@pytest.mark.parametrize("path", [_lib.DCT_PATH_PK, _lib.DCT_PATH_F64])
+@pytest.mark.parametrize("kind", ["random", "levels4", "nearflat", "blur", "checker"])
 @pytest.mark.parametrize("H,W", [(8, 16), (8 * 61, 16 * 7), (8 * 33, 8 * 130), (8 * 160, 8 * 320)])
 def test_plane_dct_rle_records(kind, path, H, W):
-    """The plane DCT's fused RLE tile records (k_dct_mfma / k_dct_planes, partial
+    """The plane DCT's fused RLE tile records (k_dct_pk / k_dct_planes, partial
     last sets included) drive the channel RLE: symbols and DC
     differences of hic_dct_quant_rle_u8 + hic_rle_encode_i16_tiles_batch equal the
     C oracle's run_length_coding / differential_coding (codec.py:47-99)."""
@@ -230,14 +230,14 @@ def test_plane_dct_rle_records(kind, path, H, W):
         np.testing.assert_array_equal(device.to_host(dc), orcc.dpcm(exp[:, 0].copy()), err_msg=(kind, tab))
 
 
-@pytest.mark.parametrize("path", [_lib.DCT_PATH_MFMA, _lib.DCT_PATH_F64])
+@pytest.mark.parametrize("path", [_lib.DCT_PATH_PK, _lib.DCT_PATH_F64])
 @pytest.mark.parametrize("waves_per_cu", [-1, 1])
 @pytest.mark.parametrize("kind", ["random", "levels4"])
 def test_plane_batch_three_planes(kind, waves_per_cu, path):
     """hic_dct_quant_rle_u8_batch over BASELINE configs[2]'s three planes (8K Y +
     two 4K chroma) in one launch: with few persistent waves each wave walks sets of
-    different planes (and tables, so the MFMA kernel reloads its matrix digits) and
-    keeps several flagged sets for its float64 pass after the loop.  Coefficients,
+    different planes and tables, and (float64 path) keeps several flagged sets for
+    its pass after the loop.  Coefficients,
     DC differences and symbols vs the C oracle."""
     _plane_batch([(4320, 7680, 0), (2160, 3840, 1), (2160, 3840, 1)], kind, waves_per_cu, path)
 
@@ -245,10 +245,10 @@ def test_plane_batch_three_planes(kind, waves_per_cu, path):
 @pytest.mark.parametrize("kind", ["random", "nearflat"])
 def test_plane_batch_sixteen_planes(kind):
     """The batched launch at its maximum: 16 planes of mixed tables and sizes (incl.
-    a partial last set) in ONE launch of the MFMA kernel, as the back-to-back
+    a partial last set) in ONE launch of the default kernel, as the back-to-back
     measurement runs it."""
     shapes = [(8 * 40 + 8 * (i % 3), 8 * 64 + 24 * i, i % 2) for i in range(16)]
-    _plane_batch(shapes, kind, -1, _lib.DCT_PATH_MFMA)
+    _plane_batch(shapes, kind, -1, -1)
 
 
 def _plane_batch(shapes, kind, waves_per_cu, path):
@@ -329,17 +329,6 @@ def test_measurement_probes():
     with pytest.raises(ValueError):
         _lib.call("hic_probe_encode420", device.ptr(rgb), H, 1000, *[device.ptr(t) for t in co], device.ptr(ry),
                   device.ptr(rc), device.stream_ptr(), None, None)
-
-
-@pytest.mark.parametrize("var", range(4))
-@pytest.mark.parametrize("kind", ["random", "levels4", "nearflat", "checker"])
-def test_mfma_plane_variants(kind, var):
-    """Every k_dct_mfma variant (knob dct_mfma: bit 0 prefetch, bit 1 two waves per
-    SIMD) writes the oracle's coefficients and RLE tile records (a partial last set
-    included)."""
-    for H, W in ((8 * 33, 8 * 130), (8 * 160, 8 * 320)):
-        with _lib.knobs(dct_mfma=var):
-            test_plane_dct_rle_records(kind, _lib.DCT_PATH_MFMA, H, W)
 
 
 @pytest.mark.parametrize("dtype", [np.uint8, np.int16, np.int32, np.float32, np.float64, np.bool_])

@@ -9,7 +9,7 @@ namespace hic {
 static thread_local char g_last_error[512] = "";
 
 // hic_set_knob values (-1 = default; read by the launchers on every call)
-static int g_knobs[HIC_KNOB_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+static int g_knobs[HIC_KNOB_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 int knob(int k) {
   const int v = g_knobs[k];
   if (v >= 0) return v;
@@ -82,6 +82,8 @@ extern "C" int hic_set_knob(int k, int value) {
   if (k == HIC_KNOB_DCT_PATH && value != -1 && !(value == 0 || value == 1 || value == 2 || value == 3))
     return hic::arg_error("dct path %d (0 exact, 1 / 2 float64 AAN, 3 packed float32)", value);
   if (k == HIC_KNOB_COLOR_SEG && value != -1 && value != 8 && value != 16) return hic::arg_error("colour segment");
+  if ((k == HIC_KNOB_DCT_PK_PF || k == HIC_KNOB_ENCODE_PK) && value != -1 && value != 0 && value != 1)
+    return hic::arg_error("knob %d: 0 or 1", k);
   // retired knobs (measured slower, removed in rounds 4-5)
   if (k >= 9 && k <= 12) return hic::arg_error("knob %d is retired", k);
   if (k == HIC_KNOB_ENCODE_ORDER && value != -1 && (value < 0 || value > 7 || (value & 1)))

@@ -25,6 +25,7 @@
 #include <stdlib.h>
 
 #include "dct_core.h"
+#include "dct_pk.h"
 #include "rle_core.h"
 
 namespace hic {
@@ -601,6 +602,167 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DCT_WPE
 }
 
 // ---------------------------------------------------------------------------
+// Packed-float32 forward kernel for aligned planes (dct_path 3, the default since
+// round 5; dct_pk.h).  The float64 AAN kernel above issues ~1000 VALU instructions
+// per 64-block set at 3 waves per SIMD: its VALU time alone is about the 8K luma
+// pass's memory floor, so the two do not overlap into that floor.  This kernel
+// runs the AAN transform on <2 x float> pairs (half the instructions of float64
+// for the same work), checks every coefficient against its proven float32 window,
+// and recomputes the few flagged blocks (~2 per set on random data) in float64 with
+// the whole wave at once (pk_coop_redo) instead of one block per lane; 4 waves per
+// SIMD (<= 128 VGPRs; the 136-byte LDS stage rows of 4-wave workgroups allow no
+// more).  PF: the next set's pixel rows load while this set computes.
+#ifndef HIC_PK_WPE
+#define HIC_PK_WPE 4
+#endif
+template <int TMF, bool PF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_PK_WPE))) void k_dct_pk(DctJobs jobs) {
+  __shared__ __attribute__((aligned(16))) uint2 s_stage[4 * 64 * kStageU2];
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nwaves = gridDim.x * 4;
+  const int g0 = blockIdx.x * 4 + wv;
+  uint2 *st2 = s_stage + wv * 64 * kStageU2;
+  int16_t *st = reinterpret_cast<int16_t *>(st2 + lane * kStageU2);
+  const int M = jobs.M;
+  // this lane's (u, v) = (lane >> 3, lane & 7) slot in a stage row: the cooperative redo
+  const int slot_off = 2 * kPkSlot.s[lane];
+  auto st16 = [&](int b, int k) {
+    const uint2 lo = st2[b * kStageU2 + 2 * k], hi = st2[b * kStageU2 + 2 * k + 1];
+    return make_uint4(lo.x, lo.y, hi.x, hi.y);
+  };
+  auto job_of = [&](int g) {
+    g = __builtin_amdgcn_readfirstlane(g);
+    int k = 0;
+    while (k + 1 < jobs.n && g >= jobs.j[k + 1].set0) ++k;
+    return __builtin_amdgcn_readfirstlane(k);
+  };
+  // the set's block coordinates: the set's first block by scalar division, each lane
+  // past it by at most one row wrap when a block row holds >= 64 blocks (a per-lane
+  // division otherwise)
+  auto load = [&](const DctJob &J, int set, uint2 (&w)[8]) {
+    const int b0 = __builtin_amdgcn_readfirstlane(set * 64);
+    const int bi0 = __builtin_amdgcn_readfirstlane(b0 / J.nbx);
+    const int bj0 = __builtin_amdgcn_readfirstlane(b0 - bi0 * J.nbx);
+    const int blk = b0 + lane;
+    int bi, bj;
+    if (J.nbx >= 64) {
+      bj = bj0 + lane;
+      bi = bi0;
+      if (bj >= J.nbx) {
+        bj -= J.nbx;
+        ++bi;
+      }
+      if (blk >= J.nblk) {  // past the plane (a partial last set): its last block
+        bi = (J.nblk - 1) / J.nbx;
+        bj = J.nblk - 1 - bi * J.nbx;
+      }
+    } else {
+      const int cblk = blk < J.nblk ? blk : J.nblk - 1;
+      bi = cblk / J.nbx;
+      bj = cblk - bi * J.nbx;
+    }
+    const uint8_t *p = J.plane + (int64_t)bi * 8 * J.stride + bj * 8;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) w[r] = *reinterpret_cast<const uint2 *>(p + r * J.stride);
+  };
+  // stage -> ZIGZAG_I16 output in 1 KiB nontemporal stores (+ the RLE tile record)
+  auto store = [&](const DctJob &J, int set) {
+    __builtin_amdgcn_wave_barrier();
+    const int blk = set * 64 + lane;
+    uint4 *o = reinterpret_cast<uint4 *>(static_cast<int16_t *>(J.out) + (int64_t)set * 64 * 64);
+    auto sv = [&](int k) { return st16(8 * k + (lane >> 3), lane & 7); };
+    if ((set + 1) * 64 <= J.nblk) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint4 t = sv(k);
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 v = {t.x, t.y, t.z, t.w};
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(o + 64 * k + lane));
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (set * 64 + 8 * k + (lane >> 3) < J.nblk) o[64 * k + lane] = sv(k);
+    }
+    if (TMF >= 0) {
+      uint32_t zw[32];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint4 t = st16(lane, k);
+        zw[4 * k] = t.x; zw[4 * k + 1] = t.y; zw[4 * k + 2] = t.z; zw[4 * k + 3] = t.w;
+      }
+      tile_record16<TMF>(zw, blk < J.nblk, blk, M, J.tiles + (int64_t)set * 3);
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
+
+  uint64_t redo = 0;  // bit i: this wave's i-th set holds a coefficient only the exact replica decides
+  int i = 0;
+  if (g0 < jobs.total_sets) {
+    int kj = job_of(g0);
+    DctJob J = jobs.j[kj];
+    int next0 = kj + 1 < jobs.n ? jobs.j[kj + 1].set0 : jobs.total_sets;
+    uint2 wn[8];
+    if (PF) load(J, g0 - J.set0, wn);
+    for (int g = g0; g < jobs.total_sets; g += nwaves, ++i) {
+      if (g >= next0) {
+        kj = job_of(g);
+        J = jobs.j[kj];
+        next0 = kj + 1 < jobs.n ? jobs.j[kj + 1].set0 : jobs.total_sets;
+      }
+      const int set = g - J.set0;
+      const int tb = J.table;  // wave-uniform: the quantiser constants are scalar loads
+      uint2 w[8];
+      if (PF) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) w[r] = wn[r];
+        const int gn = g + nwaves;
+        if (gn < jobs.total_sets) {
+          const int kn = gn >= next0 ? job_of(gn) : kj;
+          load(jobs.j[kn], gn - jobs.j[kn].set0, wn);
+        }
+      } else {
+        load(J, set, w);
+      }
+      const uint32_t fl = pk_block<-1>(w, st, tb);
+      // flagged blocks: the whole wave recomputes each in float64, patching its stage row
+#if defined(HIC_DEV) && defined(HIC_PK_DEV) && (HIC_PK_DEV & 1)
+      uint64_t fb = 0;  // dev timing (results invalid): no cooperative redo
+      (void)fl;
+#else
+      uint64_t fb = __builtin_amdgcn_ballot_w64((int)fl < 0 && set * 64 + lane < J.nblk);
+#endif
+      bool hard = false;
+      while (fb) {
+        const int L = __builtin_ctzll(fb);
+        fb &= fb - 1;
+        const int blk = set * 64 + L;
+        const int bi = blk / J.nbx, bj = blk - bi * J.nbx;
+        __builtin_amdgcn_wave_barrier();
+        if (!pk_coop_redo(J.plane + (int64_t)bi * 8 * J.stride + bj * 8, J.stride, tb,
+                          reinterpret_cast<int16_t *>(st2 + L * kStageU2), slot_off, lane))
+          hard = true;
+      }
+      if (hard) redo |= 1ull << i;
+      store(J, set);
+    }
+  }
+  // sets with a coefficient inside the float64 window too (an exact (2,2)-class tie):
+  // the whole set again on the exact pocketfft replica
+  while (redo) {
+    const int k = __builtin_ctzll(redo);
+    redo &= redo - 1;
+    const int g = g0 + k * nwaves;
+    const DctJob &J = jobs.j[job_of(g)];
+    const int set = g - J.set0;
+    uint2 w[8];
+    load(J, set, w);
+    dct_block_2ph<-1, HIC_LAYOUT_ZIGZAG_I16>(w, st, J.table);
+    store(J, set);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Block-level helpers (transform.dct2 / idct2, quantization.jpeg_quantize /
 // invert_jpeg_quantize on arbitrary float64 / int blocks): one block per lane.
 __global__ __launch_bounds__(256) void k_dct2_f64(const double *__restrict__ in, int64_t nblk, double *__restrict__ out) {
@@ -664,18 +826,24 @@ __global__ void k_dequantize_i32(const int32_t *__restrict__ in, int64_t n, int 
 inline bool aligned(const void *p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
 
 // Forward-path selection (A/B tests only; every path is bit-exact): knob
-// "dct_path" 1 = float64 AAN fast path (k_dct_planes), 2 = the same (the prefetch
-// variant is compiled out), 0 = the exact pocketfft replica for every block;
-// "dct_waves_per_cu" = persistent grid size (0 = one wave per set).  Set through
-// hic_set_knob (common.hip); the library reads no environment variables.
+// "dct_path" 3 = packed-float32 AAN with the cooperative float64 redo (k_dct_pk,
+// ZIGZAG_I16 output; the default; raster layouts take path 1), 1 = float64 AAN fast
+// path (k_dct_planes), 2 = the same (its prefetch variant is compiled out), 0 = the
+// exact pocketfft replica for every block; "dct_waves_per_cu" = persistent grid size
+// (0 = one wave per set); "dct_pk_pf" 1 = k_dct_pk loads the next set's pixels
+// while this one computes.  Set through hic_set_knob (common.hip); the library
+// reads no environment variables.
 inline int dct_path() { return knob(HIC_KNOB_DCT_PATH); }
 inline int dct_waves_per_cu(int njobs) {
   const int v = knob(HIC_KNOB_DCT_WAVES_PER_CU);
+  if (v >= 0) return v;
+  // packed path: a persistent grid of its 4 waves per SIMD
+  if (dct_path() == 3) return 16;
   // float64 path: one wave per set for a multi-plane launch (the hardware's dispatch
   // balances the planes' mixed tail: 8K Y + Cr + Cb 37.5 us vs 39.7 for 12
   // persistent waves per CU), 12 persistent waves per CU for one plane (4K luma
   // 13.4 vs 13.8 us, 8K luma 27.4 vs 27.8; scripts/gpu_r2aj.sh)
-  return v >= 0 ? v : (njobs > 1 ? 0 : 12);
+  return njobs > 1 ? 0 : 12;
 }
 
 inline bool fwd_fast(int H, int W, int64_t stride, const void *plane, const void *out) {
@@ -695,11 +863,22 @@ int launch_planes(DctJobs &jobs, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   if (cap > 0 && (total + cap - 1) / cap > 64) cap = (total + 63) / 64;  // <= 64 sets per wave (redo mask)
   const int waves = (cap == 0 || total < cap) ? total : cap;
   const dim3 grid((waves + 3) / 4), block(256);
-  const int path = dct_path() == 3 ? 1 : dct_path();
+  const int path = dct_path();
+  if (path == 3 && LAYOUT == HIC_LAYOUT_ZIGZAG_I16) {
+    auto go = [&](auto kern) {
+      if (e0 || e1)
+        hipExtLaunchKernelGGL(kern, grid, block, 0, s, e0, e1, 0, jobs);
+      else
+        hipLaunchKernelGGL(kern, grid, block, 0, s, jobs);
+    };
+    if (knob(HIC_KNOB_DCT_PK_PF) == 1) go(k_dct_pk<TMF, true>);
+    else go(k_dct_pk<TMF, false>);
+    return check_launch("k_dct_pk");
+  }
   if (e0 || e1)
-    hipExtLaunchKernelGGL((k_dct_planes<TABLE, LAYOUT, TMF>), grid, block, 0, s, e0, e1, 0, jobs, path);
+    hipExtLaunchKernelGGL((k_dct_planes<TABLE, LAYOUT, TMF>), grid, block, 0, s, e0, e1, 0, jobs, path == 3 ? 1 : path);
   else
-    hipLaunchKernelGGL((k_dct_planes<TABLE, LAYOUT, TMF>), grid, block, 0, s, jobs, path);
+    hipLaunchKernelGGL((k_dct_planes<TABLE, LAYOUT, TMF>), grid, block, 0, s, jobs, path == 3 ? 1 : path);
   return check_launch("k_dct_planes");
 }
 

@@ -78,7 +78,9 @@ int hic_device_count(int *h_n);
 /* knobs 9-12 were retired in rounds 4-5 (encode waves / nontemporal stores / integer-MFMA
  * transforms: measured slower, removed); hic_set_knob refuses them */
 #define HIC_KNOB_ENCODE_ORDER 13     /* hic_encode420_u8 unit order: 0 row-major; + 2: workgroups remapped XCD-major (neighbouring units on one XCD's L2); + 4: odd unit rows run their colour rows bottom-up (the halo rows two unit rows share fetched at the same time); default 6; odd values refused */
-#define HIC_KNOB_COUNT 14
+#define HIC_KNOB_DCT_PK_PF 14        /* 1: the packed-float32 plane kernel loads the next set's pixel rows while a set computes */
+#define HIC_KNOB_ENCODE_PK 15        /* 1: hic_encode420_u8's three DCT passes on the packed-float32 transform (dct_pk.h) */
+#define HIC_KNOB_COUNT 16
 int hic_set_knob(int knob, int value);
 int hic_get_knob(int knob, int *h_value);
 /* Synchronises `stream`; returns HIC_ERR_HIP if an earlier async launch failed. */

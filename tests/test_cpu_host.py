@@ -68,7 +68,7 @@ def test_knob_defaults_and_ranges():
     value; no GPU call): encode_order 6 = XCD-major workgroups + odd unit rows
     bottom-up (profiles/r04/enc_order_xcd); out-of-range values are refused."""
     assert _lib.get_knob("encode_order") == 6
-    assert _lib.get_knob("dct_path") == 1
+    assert _lib.get_knob("dct_path") == _lib.DCT_PATH_F64 == 1
     with _lib.knobs(encode_order=2):
         assert _lib.get_knob("encode_order") == 2
     assert _lib.get_knob("encode_order") == 6

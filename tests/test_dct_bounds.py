@@ -55,6 +55,30 @@ def test_float32_windows_cover_their_bounds():
     assert W2.max() < 2.0 ** -k
 
 
+def test_float32_constants_within_the_proof_model():
+    """E1 (dct_bounds.py) models every float32 constant of the packed path as within
+    2^-24 |c| of its real value: the four AAN factors (dct_pk.h rounds dct_core.h's
+    float64 kA1 / kA2 / kA4 / kA5 to float32) and the quantiser constants kR32 =
+    float32(S_u S_v / T).  Checked against 50-digit values."""
+    import re
+    import mpmath as mp
+    mp.mp.dps = 50
+    core = open(os.path.join(REPO, "hiccup_amd", "csrc", "dct_core.h")).read()
+    hexv = dict(re.findall(r"constexpr double (kA[1245]) = (0x[0-9a-fp.+-]+);", core))
+    c8, c38 = mp.cos(mp.pi / 8), mp.cos(3 * mp.pi / 8)
+    exact = {"kA1": mp.cos(mp.pi / 4), "kA2": c8 - c38, "kA4": c8 + c38, "kA5": c38}
+    assert set(hexv) == set(exact)
+    for name, h in hexv.items():
+        k32 = float(np.float32(float.fromhex(h)))
+        assert abs(mp.mpf(k32) - exact[name]) <= mp.mpf(2) ** -24 * abs(exact[name]), name
+    r32 = _header_floats("kR32")
+    S = [mp.mpf(2)] + [1 / mp.cos(k * mp.pi / 16) for k in range(1, 8)]
+    for t in range(2):
+        for i in range(64):
+            R = S[i // 8] * S[i % 8] / dct_bounds.QT[t][i]
+            assert abs(mp.mpf(float(r32[t, i])) - R) <= mp.mpf(2) ** -24 * R, (t, i)
+
+
 def test_float64_fast_path_margin():
     """The float64 AAN path (k_encode420, dct_path 1): estimate + pocketfft + roundings
     < 2.5 * 2^-32, the qfast flag margin."""

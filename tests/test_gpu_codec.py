@@ -383,18 +383,21 @@ def _structured_rgb(kind, H, W, seed):
 
 # the fused kernel against the chain's plane DCT on both of its shipped paths (packed
 # float32 with the cooperative float64 redo, float64 AAN)
+@pytest.mark.parametrize("enc_pk", [0, 1])
 @pytest.mark.parametrize("chain_path", [_lib.DCT_PATH_PK, _lib.DCT_PATH_F64])
 @pytest.mark.parametrize("kind", ["random", "levels", "colour_levels", "blocks", "flat"])
 @pytest.mark.parametrize("H,W", [(16, 512), (144, 2048), (1088, 1536)])
-def test_fused_encoder_matches_two_kernel_chain(kind, H, W, chain_path):
+def test_fused_encoder_matches_two_kernel_chain(kind, H, W, chain_path, enc_pk):
     """hic_encode420_u8 (colour + pyrDown + DCT + tile records in one kernel, exact
-    tie fallbacks in place) == the two-kernel chain (hic_rgb_to_ycrcb420 +
-    hic_dct_quant_rle_u8_batch), symbols and DC streams included (the fused chroma
-    records are 32-block half tiles)."""
+    tie fallbacks in place; its DCT passes on the float64 or, knob encode_pk, the
+    packed-float32 transform) == the two-kernel chain (hic_rgb_to_ycrcb420 +
+    hic_dct_quant_rle_u8_batch on either plane kernel), symbols and DC streams
+    included (the fused chroma records are 32-block half tiles)."""
     rgb = _structured_rgb(kind, H, W, H + W)
     x = device.to_device(rgb)
     got, exp = pipeline.Encoder(H, W, fused=True), pipeline.Encoder(H, W, fused=False)
-    got.encode(x)
+    with _lib.knobs(encode_pk=enc_pk):
+        got.encode(x)
     with _lib.knobs(dct_path=chain_path):
         exp.encode(x)
     a, b = got.result(), exp.result()
@@ -419,7 +422,8 @@ def test_fused_encoder_ragged_matches_chain(kind, H, W):
     pass after the launch (hic_encode420_u8), equal too.  2048x16 and 1024x48 are
     the narrow, tall shapes whose segment records outnumber their 64-block tiles
     (ADVICE r4)."""
-    test_fused_encoder_matches_two_kernel_chain(kind, H, W, _lib.DCT_PATH_PK)
+    for enc_pk in (0, 1):
+        test_fused_encoder_matches_two_kernel_chain(kind, H, W, _lib.DCT_PATH_PK, enc_pk)
     rgb = _structured_rgb(kind, H, W, H + W)
     x = device.to_device(rgb)
     got, exp = pipeline.Encoder(H, W, fused=True, index=True), pipeline.Encoder(H, W, fused=False)
@@ -440,7 +444,7 @@ def test_fused_encoder_unit_order(kind, H, W, order):
     remapped XCD-major; + 4: odd unit rows run their colour rows bottom-up; ragged
     last strips included) == the two-kernel chain."""
     with _lib.knobs(encode_order=order):
-        test_fused_encoder_matches_two_kernel_chain(kind, H, W, _lib.DCT_PATH_F64)
+        test_fused_encoder_matches_two_kernel_chain(kind, H, W, _lib.DCT_PATH_F64, -1)
 
 
 @pytest.mark.parametrize("H,W", [(2048, 16), (1024, 48), (4096, 32)])
@@ -455,7 +459,7 @@ def test_seg_workspace_canary_and_refusal(H, W):
     rgb = device.to_device(np.random.default_rng(W).integers(0, 256, (H, W, 3), dtype=np.uint8))
     enc = pipeline.Encoder(H, W)
     assert enc.seg
-    canary = 0x5A5A5A5A5A5A5A5A - (1 << 64)
+    canary = 0x5A5A5A5A5A5A5A5A
     for k in pipeline.CHANNELS:
         n = enc.ws[k].numel()
         buf = device.zeros((n + 64,), torch.int64)

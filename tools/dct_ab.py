@@ -1,6 +1,6 @@
-"""dev: time k_dct_planes on the 8K planes and the 8K luma plane (bench.py's
-extras) under knob settings.  usage:
-  HICCUP_HIP_LIB=... python tools/dct_ab.py "label:knob=v,..." ..."""
+"""dev: time the forward plane kernels (bench.py's extras) under knob settings,
+alternating the specs `rounds` times.  usage:
+  python tools/dct_ab.py [-r ROUNDS] "label:knob=v,..." ..."""
 import os
 import sys
 
@@ -9,19 +9,32 @@ import bench  # noqa: E402
 from hiccup_amd import _lib  # noqa: E402
 
 
+def one(label, kw):
+    with _lib.knobs(**kw):
+        a = bench.extra_8k_plane_dct()
+        b = bench.extra_8k_plane_dct(luma_only=True)
+        c = bench.extra_4k_luma()
+        d = bench.extra_8k_luma_batched()
+    print("%-24s planes %6.2f us (%.3f)  luma %6.2f (%.3f)  4k %6.2f (%.3f)  luma x16 free %6.2f us/plane (%.3f) "
+          "rec %6.2f (%.3f)  single free %6.2f (%.3f)"
+          % (label, a["median_launch_us"], a["frac"], b["median_launch_us"], b["frac"], c["median_launch_us"],
+             c["frac"], d["us_per_plane"], d["frac"], d["with_rle_records"]["us_per_plane"],
+             d["with_rle_records"]["frac"], d["single_launch"]["median_launch_us"], d["single_launch"]["frac"]),
+          flush=True)
+
+
 def main():
-    lib = os.path.basename(os.environ.get("HICCUP_HIP_LIB", "default"))
-    for spec in sys.argv[1:] or ["default:"]:
+    args = sys.argv[1:]
+    rounds = 1
+    if args[:1] == ["-r"]:
+        rounds, args = int(args[1]), args[2:]
+    specs = []
+    for spec in args or ["default:"]:
         label, _, kv = spec.partition(":")
-        kw = {k: int(v) for k, v in (p.split("=") for p in kv.split(",") if p)}
-        with _lib.knobs(**kw):
-            a = bench.extra_8k_plane_dct()
-            b = bench.extra_8k_plane_dct(luma_only=True)
-            c = bench.extra_4k_luma()
-            d = bench.extra_8k_luma_batched()
-        print("%-28s %-24s planes %7.2f us (%.3f)  luma %7.2f us (%.3f)  4k %7.2f us (%.3f)  luma x8 %7.2f us/plane "
-              "(%.3f)" % (lib, label, a["median_launch_us"], a["frac"], b["median_launch_us"], b["frac"],
-                          c["avg_launch_us"], c["frac"], d["us_per_plane"], d["frac"]), flush=True)
+        specs.append((label, {k: int(v) for k, v in (p.split("=") for p in kv.split(",") if p)}))
+    for _ in range(rounds):
+        for label, kw in specs:
+            one(label, kw)
 
 
 if __name__ == "__main__":

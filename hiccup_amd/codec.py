@@ -14,7 +14,10 @@ Host ("next" row): the Huffman stage and payload assembly
 Deliberate deviation: jpeg_decode does not print the luminance AC list to
 stdout (the reference's debugging print at codec.py:406-408).
 """
+import contextlib
 import ctypes
+import gc
+import threading
 
 import numpy as np
 import torch
@@ -225,16 +228,35 @@ def jpeg_decode(hic_image):
     order: DC, AC values, AC lengths, codec.py:372-388) and stay there for the RLE
     decode, DC integration and izigzag (hic_rle_decode_i32, hic_izigzag_blocks_i32);
     only the nine trees (from the tables) are built on the host.  Python's cyclic
-    collector is paused for the call: the trees' many small nodes set off full
-    collections that cost 15-60 ms at 8K (tools/prof_jdec.py)."""
-    import gc
-    was = gc.isenabled()
-    gc.disable()
-    try:
+    collector (a process-wide switch) is paused while any jpeg_decode call runs: the
+    trees' many small nodes set off full collections that cost 15-60 ms at 8K
+    (tools/prof_jdec.py).  Concurrent calls share one pause (_gc_paused counts
+    them), so a call ending never re-enables it under another still running, and
+    the collector's state from before the first call is restored after the last."""
+    with _gc_paused():
         return _jpeg_decode(hic_image)
+
+
+_gc_lock = threading.Lock()
+_gc_users = 0
+_gc_was = True
+
+
+@contextlib.contextmanager
+def _gc_paused():
+    global _gc_users, _gc_was
+    with _gc_lock:
+        if _gc_users == 0:
+            _gc_was = gc.isenabled()
+            gc.disable()
+        _gc_users += 1
+    try:
+        yield
     finally:
-        if was:
-            gc.enable()
+        with _gc_lock:
+            _gc_users -= 1
+            if _gc_users == 0 and _gc_was:
+                gc.enable()
 
 
 def _jpeg_decode(hic_image):

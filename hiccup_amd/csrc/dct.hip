@@ -618,12 +618,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DCT_WPE
 template <int TMF, bool PF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_PK_WPE))) void k_dct_pk(DctJobs jobs) {
   __shared__ __attribute__((aligned(16))) uint2 s_stage[4 * 64 * kStageU2];
+  __shared__ uint2 s_px_all[4][16];  // per wave: two flagged blocks' pixel rows (the redo)
+  __shared__ __attribute__((aligned(16))) double s_tab_d[sizeof(PkRedoTab) / sizeof(double)];
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nwaves = gridDim.x * 4;
   const int g0 = blockIdx.x * 4 + wv;
   uint2 *st2 = s_stage + wv * 64 * kStageU2;
+  uint2 *s_px = s_px_all[wv];
   int16_t *st = reinterpret_cast<int16_t *>(st2 + lane * kStageU2);
   const int M = jobs.M;
+  // the redo's constants in LDS (its latency, not a global load's)
+  const PkRedoTab &s_tab = *reinterpret_cast<const PkRedoTab *>(s_tab_d);
+  {
+    const double *src = &kPkRedo.c[0][0];
+    for (int k = threadIdx.x; k < (int)(sizeof(PkRedoTab) / sizeof(double)); k += blockDim.x) s_tab_d[k] = src[k];
+    __syncthreads();
+  }
   // this lane's (u, v) = (lane >> 3, lane & 7) slot in a stage row: the cooperative redo
   const int slot_off = 2 * kPkSlot.s[lane];
   auto st16 = [&](int b, int k) {
@@ -724,7 +734,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_PK_WPE)
       } else {
         load(J, set, w);
       }
+#if defined(HIC_DEV) && defined(HIC_PK_DEV) && (HIC_PK_DEV & 8)
+      const uint32_t fl = pk_block<0>(w, st);  // dev timing (results invalid): the luminance table only
+#else
       const uint32_t fl = pk_block<-1>(w, st, tb);
+#endif
       // flagged blocks: the whole wave recomputes each in float64, patching its stage row
 #if defined(HIC_DEV) && defined(HIC_PK_DEV) && (HIC_PK_DEV & 1)
       uint64_t fb = 0;  // dev timing (results invalid): no cooperative redo
@@ -732,18 +746,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_PK_WPE)
 #else
       uint64_t fb = __builtin_amdgcn_ballot_w64((int)fl < 0 && set * 64 + lane < J.nblk);
 #endif
-      bool hard = false;
-      while (fb) {
-        const int L = __builtin_ctzll(fb);
-        fb &= fb - 1;
-        const int blk = set * 64 + L;
-        const int bi = blk / J.nbx, bj = blk - bi * J.nbx;
-        __builtin_amdgcn_wave_barrier();
-        if (!pk_coop_redo(J.plane + (int64_t)bi * 8 * J.stride + bj * 8, J.stride, tb,
-                          reinterpret_cast<int16_t *>(st2 + L * kStageU2), slot_off, lane))
-          hard = true;
-      }
-      if (hard) redo |= 1ull << i;
+#if defined(HIC_DEV) && defined(HIC_PK_DEV) && (HIC_PK_DEV & 16)
+      asm volatile("" ::"s"(fb));  // dev timing (results invalid): flags computed, no redo
+      fb = 0;
+#endif
+      // (the flagged blocks' pixel rows, still in their lanes' registers, reach every
+      // lane through LDS)
+      if (fb && !pk_redo_flagged(fb, w, s_px, st2, kStageU2, tb, slot_off, lane, s_tab)) redo |= 1ull << i;
       store(J, set);
     }
   }

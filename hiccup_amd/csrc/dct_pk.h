@@ -119,10 +119,11 @@ __device__ const SlotOf<HIC_LAYOUT_ZIGZAG_I16> kPkSlot{};
 // Returns false (wave-uniform) if some coefficient lies inside the E2 window: only
 // the exact pocketfft replica decides it (the caller redoes the set after its loop).
 // pk_coop_redo_px: the same with pixel row m = lane >> 3 of the block given (px).
-__device__ __forceinline__ bool pk_coop_redo_px(uint2 px, int table, int16_t *stage_row, int slot_off, int lane) {
+__device__ __forceinline__ bool pk_coop_redo_px(uint2 px, int table, int16_t *stage_row, int slot_off, int lane,
+                                                const PkRedoTab &tab = kPkRedo) {
   const int m = lane >> 3, v = lane & 7;
   auto b = [&](int n) -> int { return (int)(((n < 4 ? px.x : px.y) >> (8 * (n & 3))) & 0xFFu); };
-  const double *cv = kPkRedo.c[v];
+  const double *cv = tab.c[v];
   // a_n = x_n + (-1)^v x_{7-n} of the centred pixels (an exact integer)
   const bool vo = (v & 1) != 0;
   double r = (double)(vo ? b(0) - b(7) : b(0) + b(7) - 256) * cv[0];
@@ -139,14 +140,14 @@ __device__ __forceinline__ bool pk_coop_redo_px(uint2 px, int table, int16_t *st
     rm[k] = __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
   }
   const int u = m;
-  const double *cu = kPkRedo.c[u];
+  const double *cu = tab.c[u];
   const double su = (u & 1) ? -1.0 : 1.0;  // b_m = r_m +- r_{7-m}: one rounding (fma by +-1)
   double y = __builtin_fma(su, rm[7], rm[0]) * cu[0];
 #pragma unroll
   for (int k = 1; k < 4; ++k) y = __builtin_fma(__builtin_fma(su, rm[7 - k], rm[k]), cu[k], y);
   // quant_f64_window with the table's 1/T
   const unsigned long long t =
-      __builtin_bit_cast(unsigned long long, __builtin_fma(y, kPkRedo.rt[table][lane], 0x1.8p20 + 0.5 + 0x1p-30));
+      __builtin_bit_cast(unsigned long long, __builtin_fma(y, tab.rt[table][lane], 0x1.8p20 + 0.5 + 0x1p-30));
   const int q = (int)((uint32_t)(t >> 32) - kQHi);
   const bool keep = lane == 0 || (lane == 36 && table == 0);  // exact in the fast path
   const bool ok = keep || (uint32_t)t > 9u;
@@ -157,6 +158,101 @@ __device__ __forceinline__ bool pk_coop_redo(const uint8_t *row, int64_t stride,
                                              int slot_off, int lane) {
   const uint2 px = *reinterpret_cast<const uint2 *>(row + (int64_t)(lane >> 3) * stride);
   return pk_coop_redo_px(px, table, stage_row, slot_off, lane);
+}
+
+// K flagged blocks at once (pk_coop_redo_px's operations for each, interleaved): the
+// redo of one block is a chain of LDS and cross-lane latencies (pixel rows in, the
+// row sums across lanes), so K independent chains share that wait.  px[j]: pixel row
+// m = lane >> 3 of block j; stage_row[j]: its stage row.
+template <int K>
+__device__ __forceinline__ bool pk_coop_redo_k(const uint2 (&px)[K], int table, int16_t *const (&stage_row)[K],
+                                               int slot_off, int lane, const PkRedoTab &tab) {
+  const int m = lane >> 3, v = lane & 7;
+  const bool vo = (v & 1) != 0;
+  double cv[4], cu[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    cv[n] = tab.c[v][n];
+    cu[n] = tab.c[m][n];
+  }
+  const double rt = tab.rt[table][lane];
+  double r[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    auto b = [&](int n) -> int { return (int)(((n < 4 ? px[j].x : px[j].y) >> (8 * (n & 3))) & 0xFFu); };
+    r[j] = (double)(vo ? b(0) - b(7) : b(0) + b(7) - 256) * cv[0];
+#pragma unroll
+    for (int n = 1; n < 4; ++n)
+      r[j] = __builtin_fma((double)(vo ? b(n) - b(7 - n) : b(n) + b(7 - n) - 256), cv[n], r[j]);
+  }
+  double rm[K][8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int src = (8 * k + v) * 4;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const uint64_t rb = __builtin_bit_cast(uint64_t, r[j]);
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)rb);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(rb >> 32));
+      rm[j][k] = __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+    }
+  }
+  const double su = (m & 1) ? -1.0 : 1.0;
+  const bool keep = lane == 0 || (lane == 36 && table == 0);
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    double y = __builtin_fma(su, rm[j][7], rm[j][0]) * cu[0];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) y = __builtin_fma(__builtin_fma(su, rm[j][7 - k], rm[j][k]), cu[k], y);
+    const unsigned long long t =
+        __builtin_bit_cast(unsigned long long, __builtin_fma(y, rt, 0x1.8p20 + 0.5 + 0x1p-30));
+    const int q = (int)((uint32_t)(t >> 32) - kQHi);
+    ok = ok && (keep || (uint32_t)t > 9u);
+    if (!keep) *reinterpret_cast<int16_t *>(reinterpret_cast<uint8_t *>(stage_row[j]) + slot_off) = (int16_t)q;
+  }
+  return __builtin_amdgcn_ballot_w64(!ok) == 0;
+}
+
+// Every flagged block of a wave's 64 (fb: bit L = lane L's block; w: this lane's
+// pixel rows) redone by pk_coop_redo_k two at a time; s_px: the wave's 128-byte LDS
+// area for the pixel rows in flight; st2: the wave's stage.  Returns false if some
+// block needs the exact replica.
+__device__ __forceinline__ bool pk_redo_flagged(uint64_t fb, const uint2 (&w)[8], uint2 *s_px, uint2 *st2,
+                                                int stage_u2, int table, int slot_off, int lane,
+                                                const PkRedoTab &tab) {
+  bool ok = true;
+  while (fb) {
+    const int L0 = __builtin_ctzll(fb);
+    fb &= fb - 1;
+    __builtin_amdgcn_wave_barrier();
+    if (fb) {
+      const int L1 = __builtin_ctzll(fb);
+      fb &= fb - 1;
+      if (lane == L0 || lane == L1) {
+        uint2 *d = s_px + (lane == L0 ? 0 : 8);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) d[r] = w[r];
+      }
+      __builtin_amdgcn_wave_barrier();
+      const uint2 px[2] = {s_px[lane >> 3], s_px[8 + (lane >> 3)]};
+      __builtin_amdgcn_wave_barrier();
+      int16_t *const rows[2] = {reinterpret_cast<int16_t *>(st2 + L0 * stage_u2),
+                                reinterpret_cast<int16_t *>(st2 + L1 * stage_u2)};
+      ok = pk_coop_redo_k<2>(px, table, rows, slot_off, lane, tab) && ok;
+    } else {
+      if (lane == L0) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) s_px[r] = w[r];
+      }
+      __builtin_amdgcn_wave_barrier();
+      const uint2 px[1] = {s_px[lane >> 3]};
+      __builtin_amdgcn_wave_barrier();
+      int16_t *const rows[1] = {reinterpret_cast<int16_t *>(st2 + L0 * stage_u2)};
+      ok = pk_coop_redo_k<1>(px, table, rows, slot_off, lane, tab) && ok;
+    }
+  }
+  return ok;
 }
 
 // Quantise column pair (v0, v0 + 2) (Y[u]: the pair's column outputs u) into the

@@ -112,14 +112,16 @@ __device__ __forceinline__ void enc_dct(uint2 (&w)[8], int16_t *st) {
   }
 }
 
-// The packed-float32 transform (dct_pk.h; knob encode_pk 1): pk_block, then each
-// flagged block recomputed by the whole wave in float64 (its pixel rows broadcast
-// through the wave's 64-byte s_px area), and a pass with a coefficient inside the
-// float64 window too (an exact (2,2)-class tie) redone on the exact replica.
+// The packed-float32 transform (dct_pk.h; knob encode_pk 1): pk_block, then the
+// flagged blocks recomputed by the whole wave in float64 two at a time (their pixel
+// rows broadcast through the wave's 128-byte s_px area), and a pass with a
+// coefficient inside the float64 window too (an exact (2,2)-class tie) redone on the
+// exact replica.
 // valid: this lane's block exists (a ragged strip's lanes past W compute on
 // whatever their loads returned and store nothing).
 template <int TABLE>
-__device__ __forceinline__ void enc_dct_pk(uint2 (&w)[8], int16_t *st, uint2 *st2, uint2 *s_px, bool valid) {
+__device__ __forceinline__ void enc_dct_pk(uint2 (&w)[8], int16_t *st, uint2 *st2, uint2 *s_px, bool valid,
+                                           const PkRedoTab &tab, const uint8_t *s_slot) {
   const int lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
   const uint32_t fl = pk_block<TABLE>(w, st);
 #if defined(HIC_DEV) && defined(HIC_PK_DEV) && (HIC_PK_DEV & 1)
@@ -129,24 +131,12 @@ __device__ __forceinline__ void enc_dct_pk(uint2 (&w)[8], int16_t *st, uint2 *st
 #else
   uint64_t fb = __builtin_amdgcn_ballot_w64((int)fl < 0 && valid);
 #endif
-  if (fb) {
-    const int slot_off = 2 * kPkSlot.s[lane];
-    bool hard = false;
-    while (fb) {
-      const int L = __builtin_ctzll(fb);
-      fb &= fb - 1;
-      __builtin_amdgcn_wave_barrier();
-      if (lane == L) {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) s_px[r] = w[r];
-      }
-      __builtin_amdgcn_wave_barrier();
-      const uint2 px = s_px[lane >> 3];
-      __builtin_amdgcn_wave_barrier();
-      if (!pk_coop_redo_px(px, TABLE, reinterpret_cast<int16_t *>(st2 + L * kStageU2), slot_off, lane)) hard = true;
-    }
-    if (hard) enc_exact_block<TABLE>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], st);
-  }
+#if defined(HIC_DEV) && defined(HIC_PK_DEV) && (HIC_PK_DEV & 16)
+  asm volatile("" ::"s"(fb));  // dev timing (results invalid): flags computed, no redo
+  fb = 0;
+#endif
+  if (fb && !pk_redo_flagged(fb, w, s_px, st2, kStageU2, TABLE, 2 * s_slot[lane], lane, tab))
+    enc_exact_block<TABLE>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], st);
 }
 
 #ifndef HIC_ENC_WPB
@@ -464,7 +454,18 @@ template <int TMF, bool PK>
 __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_eu(3))) void k_encode420(Enc420 E) {
   __shared__ __attribute__((aligned(16))) uint2 s_stage[HIC_ENC_WPB * 64 * kStageU2];
   __shared__ uint32_t s_chroma_all[HIC_ENC_WPB][2 * 8 * 64];
-  __shared__ uint2 s_px_all[PK ? HIC_ENC_WPB : 1][8];  // PK: a flagged block's pixel rows
+  __shared__ uint2 s_px_all[PK ? HIC_ENC_WPB : 1][16];  // PK: two flagged blocks' pixel rows
+  // PK: the cooperative redo's constants and (u, v) slots in LDS (its latency, not a
+  // global load's)
+  __shared__ __attribute__((aligned(16))) double s_tab_d[PK ? sizeof(PkRedoTab) / sizeof(double) : 1];
+  __shared__ uint8_t s_slot[PK ? 64 : 1];
+  if (PK) {
+    const double *src = &kPkRedo.c[0][0];
+    for (int k = threadIdx.x; k < (int)(sizeof(PkRedoTab) / sizeof(double)); k += blockDim.x) s_tab_d[k] = src[k];
+    if (threadIdx.x < 64) s_slot[threadIdx.x] = (uint8_t)kPkSlot.s[threadIdx.x];
+    __syncthreads();
+  }
+  const PkRedoTab &s_tab = *reinterpret_cast<const PkRedoTab *>(s_tab_d);
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint2 *st2 = s_stage + wv * 64 * kStageU2;
   uint32_t *s_chroma = s_chroma_all[wv];
@@ -488,7 +489,7 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
 #pragma unroll
     for (int r = 0; r < 8; ++r) w[r] = yq[8 * br + r];
     if (PK)
-      enc_dct_pk<0>(w, st, st2, s_px_all[PK ? wv : 0], lane < nb);
+      enc_dct_pk<0>(w, st, st2, s_px_all[PK ? wv : 0], lane < nb, s_tab, s_slot);
     else
       enc_dct<0>(w, st);
     const int64_t b0 = (int64_t)(2 * u0 + br) * nbx + 64 * s;
@@ -516,7 +517,7 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = sc[i * 32];
     if (PK)
-      enc_dct_pk<1>(w, st, st2, s_px_all[PK ? wv : 0], (lane & 31) < (nb >> 1));
+      enc_dct_pk<1>(w, st, st2, s_px_all[PK ? wv : 0], (lane & 31) < (nb >> 1), s_tab, s_slot);
     else
       enc_dct<1>(w, st);
     const int64_t b0 = (int64_t)u0 * nbxc + 32 * s;

@@ -3,6 +3,7 @@ the compute is entirely in libhiccup_hip.so.  No CPU fallback: without a HIP
 device every entry point raises ``HipUnavailable``."""
 import contextlib
 import ctypes
+import threading
 
 import numpy as np
 import torch
@@ -40,18 +41,22 @@ def ptr(t):
 
 
 def to_device(a):
-    """A host array as a new device tensor.  Large arrays (>= 4 MiB) go through a
-    reused pinned buffer (threaded host copy, then one DMA): a pageable copy runs at
-    ~4 GB/s on the MI355X boxes (tools/prof_d2h.py)."""
+    """A host array as a new device tensor.  Large arrays (>= 4 MiB) go through the
+    pinned staging buffer in chunks of at most _PIN_MAX bytes (threaded host copy,
+    then one DMA each): a pageable copy runs at ~4 GB/s on the MI355X boxes
+    (tools/prof_d2h.py)."""
     require_gpu()
     a = np.ascontiguousarray(a)
     if a.nbytes < _PIN_MIN or a.dtype.hasobject:
         return torch.from_numpy(a).to("cuda")
-    with _lock():
-        st = _stage(a.nbytes)
-        dst = st[:a.nbytes].numpy().view(a.dtype).reshape(a.shape)
-        _par_copy(dst, a)
-        return st[:a.nbytes].view(torch.from_numpy(a[:0].reshape(-1)).dtype).view(tuple(a.shape)).to("cuda")
+    out = torch.empty(tuple(a.shape), dtype=torch.from_numpy(a[:0].reshape(-1)).dtype, device="cuda")
+    ob, ab = out.reshape(-1).view(torch.uint8), a.reshape(-1).view(np.uint8)
+    with _staging_lock:
+        for o, n in _chunks(a.nbytes):
+            st = _stage(n)
+            _par_copy(st.numpy(), ab[o:o + n])
+            ob[o:o + n].copy_(st)  # synchronous: the buffer is reused by the next chunk
+    return out
 
 
 def empty(shape, dtype):
@@ -82,16 +87,18 @@ def to_host(t):
         return t.cpu().numpy()
     t = t.contiguous()
     out = np.empty(tuple(t.shape), torch.empty(0, dtype=t.dtype).numpy().dtype)
-    with _lock():
-        st = _stage(nbytes)
-        st[:nbytes].view(t.dtype).copy_(t.reshape(-1))
-        _par_copy(out.reshape(-1), st[:nbytes].numpy().view(out.dtype))
+    tb, ob = t.reshape(-1).view(torch.uint8), out.reshape(-1).view(np.uint8)
+    with _staging_lock:
+        for o, n in _chunks(nbytes):
+            st = _stage(n)
+            st.copy_(tb[o:o + n])
+            _par_copy(ob[o:o + n], st.numpy())
     return out
 
 
 def to_host_f64(t):
     """A device int32 tensor as a new float64 numpy array (the reference's planes are
-    float64): one DMA into the pinned buffer, then the cast split over host threads.
+    float64): DMA into the pinned buffer, then the cast split over host threads.
     A pageable copy runs at ~4 GB/s here and the single-threaded cast after it
     doubled the time (8K luma: 48 vs 17 ms, tools/prof_d2h.py)."""
     assert t.dtype == torch.int32 and t.is_cuda
@@ -99,10 +106,12 @@ def to_host_f64(t):
     t = t.contiguous()
     n = t.numel()
     out = np.empty(n, np.float64)
-    with _lock():
-        st = _stage(4 * n)
-        st[:4 * n].view(torch.int32).copy_(t.reshape(-1))
-        _par_copy(out, st[:4 * n].numpy().view(np.int32))
+    ti = t.reshape(-1)
+    with _staging_lock:
+        for o, nb in _chunks(4 * n):
+            st = _stage(nb)
+            st.view(torch.int32).copy_(ti[o // 4:(o + nb) // 4])
+            _par_copy(out[o // 4:(o + nb) // 4], st.numpy().view(np.int32))
     return out.reshape(tuple(t.shape))
 
 
@@ -130,29 +139,31 @@ def to_device_i32(a, nonint_msg, range_msg):
     return t.to(torch.int32)
 
 
-# one pinned host staging buffer (grown on demand, reused; callers on several
-# threads take turns) and a small thread pool for the host side of the copies
+# one pinned host staging buffer (grown on demand up to _PIN_MAX bytes, reused;
+# callers on several threads take turns under _staging_lock; larger copies go in
+# _PIN_MAX chunks, so the buffer never holds more than that) and a small thread
+# pool for the host side of the copies
 _PIN_MIN = 4 << 20
+_PIN_MAX = 256 << 20
 _staging = None
-_staging_lock = None
+_staging_lock = threading.Lock()
 _pool = None
 
 
-def _lock():
-    global _staging_lock
-    if _staging_lock is None:
-        import threading
-        _staging_lock = threading.Lock()
-    return _staging_lock
+def _chunks(nbytes):
+    """(offset, length) pieces of a copy of nbytes, each <= _PIN_MAX (a multiple of 8)."""
+    return [(o, min(_PIN_MAX, nbytes - o)) for o in range(0, nbytes, _PIN_MAX)]
 
 
 def _stage(nbytes):
-    """The pinned uint8 buffer, at least nbytes long (call with _lock() held)."""
+    """The first nbytes (<= _PIN_MAX) of the pinned uint8 buffer (call with
+    _staging_lock held)."""
     global _staging
+    assert nbytes <= _PIN_MAX
     if _staging is None or _staging.numel() < nbytes:
         _staging = None
-        _staging = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, pin_memory=True)
-    return _staging
+        _staging = torch.empty(min(_PIN_MAX, max(2 * int(nbytes), _PIN_MIN)), dtype=torch.uint8, pin_memory=True)
+    return _staging[:nbytes]
 
 
 def _par_copy(dst, src):

@@ -431,3 +431,48 @@ def test_stream_gather_record_layout_past_2gib():
     # a ragged image whose last shard cannot fuse: one decision for all (the chain)
     rows = sharding.plan(4328, 4)
     assert not all(pipeline.encoder_layout(4328, 7680, rr)[0] for rr in rows)
+
+
+def test_jpeg_decode_gc_pause_is_shared():
+    """jpeg_decode pauses the process-wide cyclic collector; calls
+    that overlap (nested or on other threads) share one pause, the collector stays
+    off until the last ends, and its state from before the first returns."""
+    import gc
+    import threading
+    from hiccup_amd import codec
+    assert gc.isenabled()
+    inside, release = threading.Event(), threading.Event()
+
+    def other():
+        with codec._gc_paused():
+            inside.set()
+            release.wait(10)
+
+    t = threading.Thread(target=other)
+    t.start()
+    assert inside.wait(10)
+    with codec._gc_paused():
+        assert not gc.isenabled()
+    assert not gc.isenabled()  # the other call still runs
+    release.set()
+    t.join(10)
+    assert gc.isenabled()
+    gc.disable()
+    try:
+        with codec._gc_paused():
+            pass
+        assert not gc.isenabled()  # a collector the caller had off stays off
+    finally:
+        gc.enable()
+
+
+def test_pinned_staging_chunks():
+    """the pinned staging buffer is capped; larger copies go in
+    _PIN_MAX pieces that tile the copy exactly (int32 / float64 aligned)."""
+    from hiccup_amd import device
+    assert device._staging_lock is not None
+    for n in [device._PIN_MIN, device._PIN_MAX - 8, device._PIN_MAX, device._PIN_MAX + 4, 5 * device._PIN_MAX + 12]:
+        ch = device._chunks(n)
+        assert ch[0][0] == 0 and sum(c for _, c in ch) == n
+        assert all(o1 == o0 + c0 for (o0, c0), (o1, _) in zip(ch, ch[1:]))
+        assert all(c <= device._PIN_MAX and o % 8 == 0 for o, c in ch)

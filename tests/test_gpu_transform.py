@@ -364,3 +364,20 @@ def test_pinned_host_copies(dtype):
     q[7, 9] = np.nan
     with pytest.raises(ValueError, match="bad"):
         device.to_device_i32(q, "bad", "range")
+
+
+@pytest.mark.parametrize("dtype", [np.uint8, np.int32, np.float64, np.bool_])
+def test_pinned_host_copies_chunked(dtype, monkeypatch):
+    """Copies larger than the staging cap go in _PIN_MAX pieces (the cap lowered to
+    4 MiB + 8 here so that a ~13 MB copy takes four, the last one short)."""
+    monkeypatch.setattr(device, "_PIN_MAX", (4 << 20) + 8)
+    monkeypatch.setattr(device, "_staging", None)
+    rng = np.random.default_rng(12)
+    a = (rng.integers(0, 2, (1601, 2051)) if dtype == np.bool_ else rng.integers(-100, 100, (1601, 2051))).astype(dtype)
+    if a.nbytes < 3 * device._PIN_MAX:
+        a = np.concatenate([a] * (1 + 3 * device._PIN_MAX // a.nbytes))
+    t = device.to_device(a)
+    np.testing.assert_array_equal(device.to_host(t), a)
+    assert device._staging.numel() <= device._PIN_MAX
+    if dtype == np.int32:
+        np.testing.assert_array_equal(device.to_host_f64(t), a.astype(np.float64))

@@ -79,7 +79,7 @@ extern "C" int hic_event_elapsed_ms(void *start, void *stop, float *h_ms) {
 
 extern "C" int hic_set_knob(int k, int value) {
   if (k < 0 || k >= HIC_KNOB_COUNT) return hic::arg_error("knob %d", k);
-  if (k == HIC_KNOB_DCT_PATH && value != -1 && !(value == 0 || value == 1 || value == 2 || value == 3))
+  if (k == HIC_KNOB_DCT_PATH && value != -1 && !(value >= 0 && value <= 4))
     return hic::arg_error("dct path %d (0 exact, 1 / 2 float64 AAN, 3 packed float32)", value);
   if (k == HIC_KNOB_COLOR_SEG && value != -1 && value != 8 && value != 16) return hic::arg_error("colour segment");
   if ((k == HIC_KNOB_DCT_PK_PF || k == HIC_KNOB_ENCODE_PK) && value != -1 && value != 0 && value != 1)

@@ -19,7 +19,7 @@
 // sum, rounded in integers (dc_quant); luminance (4,4) is y/T = K/34, flagged only
 // at its exact ties, which pocketfft's own roundings decide in place (pf_y44 on the
 // rows' integer outputs 4).  Any other flag (~0.035 per luminance block on random
-// data, dct_bounds.py) sends the lane's block through pk_coop_redo: the whole wave
+// data, dct_bounds.py) sends the lane's block through pk_coop_redo_k: the whole wave
 // recomputes that one block in float64 (dct_coef_f64's separable, symmetry-folded
 // dot products, error window E2 <= 2^-31, lane = coefficient) and patches its
 // stage row before the set leaves.  A coefficient inside E2's window too (an exact
@@ -83,7 +83,7 @@ __device__ __forceinline__ void pk_cols(const f2 (&X)[8], f2 (&Y)[8]) {
   pk_odd(X[0] - X[7], X[1] - X[6], X[2] - X[5], X[3] - X[4], Y[1], Y[3], Y[5], Y[7]);
 }
 
-// The per-lane constants of the cooperative float64 redo (pk_coop_redo): the
+// The per-lane constants of the cooperative float64 redo (pk_coop_redo_k): the
 // separable fallback's factors C_k(n) = 2 cos(pi k (2n + 1) / 16) (dct_coef_f64's
 // cos2(kCm, k, n), k = 0..7, n = 0..3) and 1 / T per table, correctly rounded
 struct PkRedoTab {
@@ -106,69 +106,29 @@ __device__ const PkRedoTab kPkRedo{};
 // zig-zag slot of raster index i (lane i of the cooperative redo: its (u, v) slot)
 __device__ const SlotOf<HIC_LAYOUT_ZIGZAG_I16> kPkSlot{};
 
-// Block `L` of the wave's set (wave-uniform), whose fast-path coefficients include a
-// flagged one, recomputed by the whole wave in float64 and written over its stage
-// row: lane (m, v) = (lane >> 3, lane & 7) forms dct_coef_f64's row sum r_mv from
-// pixel row m of the block (reloaded: `row` points at row 0 of block L, rows
-// `stride` bytes apart), the rows' sums cross lanes by ds_bpermute, and lane (u, v)
-// = (lane >> 3, lane & 7) folds them into y_uv with the same operations, in the
-// same order, as dct_coef_f64 (the E2 bound of dct_bounds.py) and quantises y / T
-// with the E2 window (quant_f64_window).  The DC (exact in the fast path) and, for
-// luminance, (4,4) (decided in place) are not rewritten.  stage: the byte address of
-// block L's stage row; slot_off: this lane's (u, v) byte offset in a stage row.
-// Returns false (wave-uniform) if some coefficient lies inside the E2 window: only
-// the exact pocketfft replica decides it (the caller redoes the set after its loop).
-// pk_coop_redo_px: the same with pixel row m = lane >> 3 of the block given (px).
-__device__ __forceinline__ bool pk_coop_redo_px(uint2 px, int table, int16_t *stage_row, int slot_off, int lane,
-                                                const PkRedoTab &tab = kPkRedo) {
-  const int m = lane >> 3, v = lane & 7;
-  auto b = [&](int n) -> int { return (int)(((n < 4 ? px.x : px.y) >> (8 * (n & 3))) & 0xFFu); };
-  const double *cv = tab.c[v];
-  // a_n = x_n + (-1)^v x_{7-n} of the centred pixels (an exact integer)
-  const bool vo = (v & 1) != 0;
-  double r = (double)(vo ? b(0) - b(7) : b(0) + b(7) - 256) * cv[0];
-#pragma unroll
-  for (int n = 1; n < 4; ++n) r = __builtin_fma((double)(vo ? b(n) - b(7 - n) : b(n) + b(7 - n) - 256), cv[n], r);
-  // lane (u, v) gathers r_mv of lanes (m, v), m = 0..7
-  const uint64_t rb = __builtin_bit_cast(uint64_t, r);
-  double rm[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int src = (8 * k + v) * 4;
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)rb);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(rb >> 32));
-    rm[k] = __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
-  }
-  const int u = m;
-  const double *cu = tab.c[u];
-  const double su = (u & 1) ? -1.0 : 1.0;  // b_m = r_m +- r_{7-m}: one rounding (fma by +-1)
-  double y = __builtin_fma(su, rm[7], rm[0]) * cu[0];
-#pragma unroll
-  for (int k = 1; k < 4; ++k) y = __builtin_fma(__builtin_fma(su, rm[7 - k], rm[k]), cu[k], y);
-  // quant_f64_window with the table's 1/T
-  const unsigned long long t =
-      __builtin_bit_cast(unsigned long long, __builtin_fma(y, tab.rt[table][lane], 0x1.8p20 + 0.5 + 0x1p-30));
-  const int q = (int)((uint32_t)(t >> 32) - kQHi);
-  const bool keep = lane == 0 || (lane == 36 && table == 0);  // exact in the fast path
-  const bool ok = keep || (uint32_t)t > 9u;
-  if (!keep) *reinterpret_cast<int16_t *>(reinterpret_cast<uint8_t *>(stage_row) + slot_off) = (int16_t)q;
-  return __builtin_amdgcn_ballot_w64(!ok) == 0;
-}
-__device__ __forceinline__ bool pk_coop_redo(const uint8_t *row, int64_t stride, int table, int16_t *stage_row,
-                                             int slot_off, int lane) {
-  const uint2 px = *reinterpret_cast<const uint2 *>(row + (int64_t)(lane >> 3) * stride);
-  return pk_coop_redo_px(px, table, stage_row, slot_off, lane);
-}
-
-// K flagged blocks at once (pk_coop_redo_px's operations for each, interleaved): the
-// redo of one block is a chain of LDS and cross-lane latencies (pixel rows in, the
-// row sums across lanes), so K independent chains share that wait.  px[j]: pixel row
-// m = lane >> 3 of block j; stage_row[j]: its stage row.
+// K flagged blocks of the wave's set, each recomputed by the whole wave in float64
+// and written over its stage row: lane (m, v) = (lane >> 3, lane & 7) forms
+// dct_coef_f64's row sum r_mv from pixel row m of block j (px[j]), the rows' sums
+// cross lanes by ds_bpermute, and lane (u, v) = (lane >> 3, lane & 7) folds them
+// into y_uv with the same operations, in the same order, as dct_coef_f64 (the E2
+// bound of dct_bounds.py) and quantises y / T with the E2 window
+// (quant_f64_window).  The DC (exact in the fast path) and, for luminance, (4,4)
+// (decided in place) are not rewritten.  stage_row[j]: block j's stage row;
+// slot_off: this lane's (u, v) byte offset in a stage row.  The redo of one block is
+// a chain of LDS and cross-lane latencies (pixel rows in, the row sums across
+// lanes); K independent chains share that wait.  Returns false (wave-uniform) if
+// some coefficient lies inside the E2 window: only the exact pocketfft replica
+// decides it (the caller redoes the set or block).
 template <int K>
 __device__ __forceinline__ bool pk_coop_redo_k(const uint2 (&px)[K], int table, int16_t *const (&stage_row)[K],
                                                int slot_off, int lane, const PkRedoTab &tab) {
   const int m = lane >> 3, v = lane & 7;
-  const bool vo = (v & 1) != 0;
+  // branch-free: odd v takes a_n = x_n - x_{7-n}, even v a_n = x_n + x_{7-n} - 256 (a
+  // bit select between the two, each one byte-select add); the DC and (luminance)
+  // (4,4) lanes write their value into the stage row's pad instead of their slot
+  const uint32_t vm = (v & 1) ? ~0u : 0u;
+  const bool keep = lane == 0 || (lane == 36 && table == 0);
+  const int woff = keep ? 2 * 64 : slot_off;
   double cv[4], cu[4];
 #pragma unroll
   for (int n = 0; n < 4; ++n) {
@@ -179,11 +139,13 @@ __device__ __forceinline__ bool pk_coop_redo_k(const uint2 (&px)[K], int table, 
   double r[K];
 #pragma unroll
   for (int j = 0; j < K; ++j) {
-    auto b = [&](int n) -> int { return (int)(((n < 4 ? px[j].x : px[j].y) >> (8 * (n & 3))) & 0xFFu); };
-    r[j] = (double)(vo ? b(0) - b(7) : b(0) + b(7) - 256) * cv[0];
 #pragma unroll
-    for (int n = 1; n < 4; ++n)
-      r[j] = __builtin_fma((double)(vo ? b(n) - b(7 - n) : b(n) + b(7 - n) - 256), cv[n], r[j]);
+    for (int n = 0; n < 4; ++n) {
+      const uint32_t xn = (px[j].x >> (8 * n)) & 0xFFu, yn = (px[j].y >> (8 * (3 - n))) & 0xFFu;
+      const uint32_t sum = xn + yn - 256u, dif = xn - yn;
+      const int a = (int)((vm & dif) | (~vm & sum));
+      r[j] = n == 0 ? (double)a * cv[0] : __builtin_fma((double)a, cv[n], r[j]);
+    }
   }
   double rm[K][8];
 #pragma unroll
@@ -198,8 +160,7 @@ __device__ __forceinline__ bool pk_coop_redo_k(const uint2 (&px)[K], int table, 
     }
   }
   const double su = (m & 1) ? -1.0 : 1.0;
-  const bool keep = lane == 0 || (lane == 36 && table == 0);
-  bool ok = true;
+  uint32_t bad = 0;
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     double y = __builtin_fma(su, rm[j][7], rm[j][0]) * cu[0];
@@ -208,19 +169,34 @@ __device__ __forceinline__ bool pk_coop_redo_k(const uint2 (&px)[K], int table, 
     const unsigned long long t =
         __builtin_bit_cast(unsigned long long, __builtin_fma(y, rt, 0x1.8p20 + 0.5 + 0x1p-30));
     const int q = (int)((uint32_t)(t >> 32) - kQHi);
-    ok = ok && (keep || (uint32_t)t > 9u);
-    if (!keep) *reinterpret_cast<int16_t *>(reinterpret_cast<uint8_t *>(stage_row[j]) + slot_off) = (int16_t)q;
+    bad |= (uint32_t)t <= 9u;
+    *reinterpret_cast<int16_t *>(reinterpret_cast<uint8_t *>(stage_row[j]) + woff) = (int16_t)q;
   }
-  return __builtin_amdgcn_ballot_w64(!ok) == 0;
+  return __builtin_amdgcn_ballot_w64(bad != 0 && !keep) == 0;
 }
 
 // Every flagged block of a wave's 64 (fb: bit L = lane L's block; w: this lane's
 // pixel rows) redone by pk_coop_redo_k two at a time; s_px: the wave's 128-byte LDS
-// area for the pixel rows in flight; st2: the wave's stage.  Returns false if some
-// block needs the exact replica.
+// area for the pixel rows in flight; st2: the wave's stage.  s_tab_d: the
+// workgroup's LDS copy of kPkRedo, filled here by this wave on its first call
+// (tab_ready: wave-uniform; waves write identical values, so no barrier; s_slot,
+// when given, gets kPkSlot's 64 slots the same way).  Returns false if some block
+// needs the exact replica.
+__device__ __forceinline__ void pk_tab_fill(double *s_tab_d, uint8_t *s_slot, int lane, bool &tab_ready) {
+  if (tab_ready) return;
+  const double *src = &kPkRedo.c[0][0];
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(PkRedoTab) / sizeof(double)); k += 64)
+    if (k + lane < (int)(sizeof(PkRedoTab) / sizeof(double))) s_tab_d[k + lane] = src[k + lane];
+  if (s_slot) s_slot[lane] = (uint8_t)kPkSlot.s[lane];
+  __builtin_amdgcn_wave_barrier();
+  tab_ready = true;
+}
 __device__ __forceinline__ bool pk_redo_flagged(uint64_t fb, const uint2 (&w)[8], uint2 *s_px, uint2 *st2,
-                                                int stage_u2, int table, int slot_off, int lane,
-                                                const PkRedoTab &tab) {
+                                                int stage_u2, int table, int slot_off, int lane, double *s_tab_d,
+                                                bool &tab_ready) {
+  pk_tab_fill(s_tab_d, nullptr, lane, tab_ready);
+  const PkRedoTab &tab = *reinterpret_cast<const PkRedoTab *>(s_tab_d);
   bool ok = true;
   while (fb) {
     const int L0 = __builtin_ctzll(fb);
@@ -294,7 +270,7 @@ __device__ __forceinline__ void pk_quant_pair(const f2 (&Y)[8], int v0, int16_t 
 // One 8x8 block per lane on the packed path (w: its eight 8-byte pixel rows): the 64
 // quantised coefficients into st (the lane's stage row, zig-zag slots), luminance
 // (4,4) ties decided in place; returns the lane's flag word (sign bit set: some
-// coefficient needs the float64 redo, pk_coop_redo).  TABLE -1: the wave-uniform
+// coefficient needs the float64 redo, pk_coop_redo_k).  TABLE -1: the wave-uniform
 // table `trt`, the quantiser constants as literals behind a scalar branch per
 // column pair (runtime-indexed constants were 128 scalar loads per set, spilled to
 // VGPR lanes; a branch around the whole block spilled its row outputs).

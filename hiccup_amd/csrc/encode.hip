@@ -121,7 +121,7 @@ __device__ __forceinline__ void enc_dct(uint2 (&w)[8], int16_t *st) {
 // whatever their loads returned and store nothing).
 template <int TABLE>
 __device__ __forceinline__ void enc_dct_pk(uint2 (&w)[8], int16_t *st, uint2 *st2, uint2 *s_px, bool valid,
-                                           const PkRedoTab &tab, const uint8_t *s_slot) {
+                                           double *s_tab_d, uint8_t *s_slot, bool &tab_ready) {
   const int lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
   const uint32_t fl = pk_block<TABLE>(w, st);
 #if defined(HIC_DEV) && defined(HIC_PK_DEV) && (HIC_PK_DEV & 1)
@@ -135,8 +135,14 @@ __device__ __forceinline__ void enc_dct_pk(uint2 (&w)[8], int16_t *st, uint2 *st
   asm volatile("" ::"s"(fb));  // dev timing (results invalid): flags computed, no redo
   fb = 0;
 #endif
-  if (fb && !pk_redo_flagged(fb, w, s_px, st2, kStageU2, TABLE, 2 * s_slot[lane], lane, tab))
-    enc_exact_block<TABLE>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], st);
+#if defined(HIC_DEV) && defined(HIC_PK_DEV) && (HIC_PK_DEV & 32)
+  asm volatile("s_mov_b64 %0, 0" : "+s"(fb));  // dev timing (results invalid): the redo compiled, not run
+#endif
+  if (fb) {
+    pk_tab_fill(s_tab_d, s_slot, lane, tab_ready);
+    if (!pk_redo_flagged(fb, w, s_px, st2, kStageU2, TABLE, 2 * s_slot[lane], lane, s_tab_d, tab_ready))
+      enc_exact_block<TABLE>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], st);
+  }
 }
 
 #ifndef HIC_ENC_WPB
@@ -456,16 +462,10 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
   __shared__ uint32_t s_chroma_all[HIC_ENC_WPB][2 * 8 * 64];
   __shared__ uint2 s_px_all[PK ? HIC_ENC_WPB : 1][16];  // PK: two flagged blocks' pixel rows
   // PK: the cooperative redo's constants and (u, v) slots in LDS (its latency, not a
-  // global load's)
+  // global load's), copied there by the first wave of the workgroup that needs them
   __shared__ __attribute__((aligned(16))) double s_tab_d[PK ? sizeof(PkRedoTab) / sizeof(double) : 1];
   __shared__ uint8_t s_slot[PK ? 64 : 1];
-  if (PK) {
-    const double *src = &kPkRedo.c[0][0];
-    for (int k = threadIdx.x; k < (int)(sizeof(PkRedoTab) / sizeof(double)); k += blockDim.x) s_tab_d[k] = src[k];
-    if (threadIdx.x < 64) s_slot[threadIdx.x] = (uint8_t)kPkSlot.s[threadIdx.x];
-    __syncthreads();
-  }
-  const PkRedoTab &s_tab = *reinterpret_cast<const PkRedoTab *>(s_tab_d);
+  bool tab_ready = false;  // PK: filled by the wave's first redo (pk_tab_fill, no barrier)
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint2 *st2 = s_stage + wv * 64 * kStageU2;
   uint32_t *s_chroma = s_chroma_all[wv];
@@ -489,7 +489,7 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
 #pragma unroll
     for (int r = 0; r < 8; ++r) w[r] = yq[8 * br + r];
     if (PK)
-      enc_dct_pk<0>(w, st, st2, s_px_all[PK ? wv : 0], lane < nb, s_tab, s_slot);
+      enc_dct_pk<0>(w, st, st2, s_px_all[PK ? wv : 0], lane < nb, s_tab_d, s_slot, tab_ready);
     else
       enc_dct<0>(w, st);
     const int64_t b0 = (int64_t)(2 * u0 + br) * nbx + 64 * s;
@@ -517,7 +517,7 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = sc[i * 32];
     if (PK)
-      enc_dct_pk<1>(w, st, st2, s_px_all[PK ? wv : 0], (lane & 31) < (nb >> 1), s_tab, s_slot);
+      enc_dct_pk<1>(w, st, st2, s_px_all[PK ? wv : 0], (lane & 31) < (nb >> 1), s_tab_d, s_slot, tab_ready);
     else
       enc_dct<1>(w, st);
     const int64_t b0 = (int64_t)u0 * nbxc + 32 * s;

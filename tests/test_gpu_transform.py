@@ -98,11 +98,12 @@ def test_layouts_roundtrip(layout, shape):
         np.testing.assert_array_equal(device.to_host(rec), orcc.inv_dct_channel(exp, tab))
 
 
-@pytest.mark.parametrize("path", [-1, _lib.DCT_PATH_PK, _lib.DCT_PATH_F64])
+@pytest.mark.parametrize("path", [-1, _lib.DCT_PATH_2L, _lib.DCT_PATH_PK, _lib.DCT_PATH_F64])
 @pytest.mark.parametrize("H,W", [(4096, 4096), (4320, 7680)])
 def test_full_size_bit_exact(H, W, path):
     """BASELINE configs 2/3 plane sizes, bit-exact against the C oracle (multi-threaded),
-    on the default forward path, the packed-float32 one and the float64 AAN one."""
+    on the default forward path, the two-lanes-per-block float64 one, the
+    packed-float32 one and the one-lane float64 AAN one."""
     with _lib.knobs(dct_path=path):
         _full_size_bit_exact(H, W)
 
@@ -130,7 +131,7 @@ def test_tie_blocks_many():
         np.testing.assert_array_equal(transform.dct_channel(plane, QT[tab]), orcc.dct_channel(plane, tab, threads=8))
 
 
-@pytest.mark.parametrize("path", [_lib.DCT_PATH_PK, _lib.DCT_PATH_F64, _lib.DCT_PATH_EXACT])
+@pytest.mark.parametrize("path", [_lib.DCT_PATH_2L, _lib.DCT_PATH_PK, _lib.DCT_PATH_F64, _lib.DCT_PATH_EXACT])
 @pytest.mark.parametrize("kind", ["levels4", "nearflat", "stripes", "checker", "blur"])
 def test_fast_path_structured_ties(kind, path):
     with _lib.knobs(dct_path=path):
@@ -249,6 +250,32 @@ def test_plane_batch_sixteen_planes(kind):
     measurement runs it."""
     shapes = [(8 * 40 + 8 * (i % 3), 8 * 64 + 24 * i, i % 2) for i in range(16)]
     _plane_batch(shapes, kind, -1, -1)
+
+
+@pytest.mark.parametrize("path", [_lib.DCT_PATH_2L, _lib.DCT_PATH_PK, _lib.DCT_PATH_F64])
+@pytest.mark.parametrize("waves_per_cu", [-1, 1])
+@pytest.mark.parametrize("kind", ["random", "levels4", "nearflat", "blur"])
+def test_plane_batch_records_free(kind, waves_per_cu, path):
+    """The records-free batched pass (no RLE workspaces: north_star's DCT + quantize
+    + zig-zag, what the back-to-back measurement runs): 8K Y + two 4K chroma planes,
+    then 16 small planes of mixed tables whose block rows hold < 32, 32..63 and >= 64
+    blocks (the two-lane kernel's per-lane division and its one-wrap path) with
+    partial last sets; with one persistent wave per CU each wave walks many half sets
+    of different planes and keeps its tie sets for after the loop."""
+    shapes = [(4320, 7680, 0), (2160, 3840, 1), (2160, 3840, 1)]
+    small = [(8 * (5 + 3 * i), 8 * (7 + 9 * i), i % 2) for i in range(16)]
+    for sh in (shapes, small):
+        planes, outs, jobs = [], [], (_lib.DctPlaneJob * len(sh))()
+        for i, (h, w, t) in enumerate(sh):
+            p = _structured_plane(kind, h, w)
+            planes.append((p, device.to_device(p)))
+            outs.append(device.empty(((h // 8) * (w // 8), 64), torch.int16))
+            jobs[i] = _lib.DctPlaneJob(planes[i][1].data_ptr(), h, w, w, t, outs[i].data_ptr(), None)
+        with _lib.knobs(dct_waves_per_cu=waves_per_cu, dct_path=path):
+            _lib.call("hic_dct_quant_rle_u8_batch", len(sh), jobs, 15, device.stream_ptr(), None, None)
+        for i, (h, w, t) in enumerate(sh):
+            exp = orcc.zigzag_blocks(orcc.dct_channel(planes[i][0], t, threads=16), 8)
+            np.testing.assert_array_equal(device.to_host(outs[i]).astype(np.int32), exp, err_msg=(kind, i, h, w))
 
 
 def _plane_batch(shapes, kind, waves_per_cu, path):

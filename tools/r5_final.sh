@@ -10,6 +10,7 @@ tag=${1:-a}
 cd "$GRAFT_REPO_ROOT"
 out=gpurun_out/r5/final_$tag
 mkdir -p $out
+if [ "${2:-}" != "profonly" ]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
   > $out/gputest.log 2>&1 || { tail -30 $out/gputest.log; exit 1; }
 tail -3 $out/gputest.log
@@ -17,13 +18,15 @@ timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $out/s
 grep -v amdgpu.ids $out/smoke.log
 timeout -k 10 500 python -u bench.py > $out/bench_default.json 2>&1 || { tail -20 $out/bench_default.json; exit 1; }
 grep '^{' $out/bench_default.json | tail -1 | cut -c1-400
+fi
 [ "${2:-}" = "noprof" ] && exit 0
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/trace_default -o run --output-format csv -- \
+[ "${2:-}" = "profonly" ] || timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/trace_default -o run --output-format csv -- \
   python3 bench.py --no-cpu-baseline > $out/trace_default.json.log 2>&1 || { tail -5 $out/trace_default.json.log; exit 1; }
-python3 tools/trace_launches.py $out/trace_default/run_kernel_trace.csv k_dct > $out/trace_default_dct_launches.txt
-head -c 3000 $out/trace_default_dct_launches.txt
+[ "${2:-}" = "profonly" ] || { python3 tools/trace_launches.py $out/trace_default/run_kernel_trace.csv k_dct \
+  > $out/trace_default_dct_launches.txt; head -c 3000 $out/trace_default_dct_launches.txt; }
+[ "${2:-}" = "trace" ] && exit 0
 timeout -k 10 900 bash tools/prof_r2.sh r5_$tag > $out/prof_r2.log 2>&1 || { tail -5 $out/prof_r2.log; exit 1; }
 python3 tools/prof_r2_summary.py gpurun_out/prof_r5_$tag $out/prof_summary.json && echo profiled
-timeout -k 10 600 bash tools/r5_sq.sh $tag "1 3" > $out/sq.log 2>&1 || { tail -5 $out/sq.log; exit 1; }
+timeout -k 10 600 bash tools/r5_sq.sh $tag "1 3 4" > $out/sq.log 2>&1 || { tail -5 $out/sq.log; exit 1; }
 cat $out/sq.log

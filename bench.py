@@ -151,11 +151,6 @@ def cpu_baseline(budget_s):
 def plane_kernel(tmf):
     """The forward plane kernel the library runs for ZIGZAG_I16 planes (dct_path knob)."""
     from hiccup_amd import _lib
-    path = _lib.get_knob("dct_path")
-    if path == _lib.DCT_PATH_PK:
-        return "k_dct_pk<%d> (packed float32 AAN, cooperative float64 redo of flagged blocks)" % tmf
-    if path == _lib.DCT_PATH_2L and tmf < 0:
-        return "k_dct_2l<-1> (float64 AAN, two lanes per block)"
     return "k_dct_planes<-1,ZIGZAG_I16,%d> (float64 AAN)" % tmf
 
 

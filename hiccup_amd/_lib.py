@@ -173,9 +173,8 @@ def call(name, *args):
 
 # A/B knobs (include/hiccup_hip.h HIC_KNOB_*): every selectable path is bit-exact
 KNOBS = {"dct_path": 0, "dct_waves_per_cu": 1, "color_tiled": 2, "color_seg": 3, "color_nt": 4, "rle_nt": 5,
-         "rld_nt": 6, "rld_generic": 7, "dev": 8, "encode_order": 13, "dct_pk_pf": 14,
-         "encode_pk": 15}
-DCT_PATH_2L, DCT_PATH_PK, DCT_PATH_F64, DCT_PATH_F64_NOPF, DCT_PATH_EXACT = 4, 3, 1, 2, 0
+         "rld_nt": 6, "rld_generic": 7, "dev": 8, "encode_order": 13}
+DCT_PATH_F64, DCT_PATH_F64_NOPF, DCT_PATH_EXACT = 1, 2, 0
 
 
 def set_knob(name, value):

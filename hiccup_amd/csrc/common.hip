@@ -79,13 +79,12 @@ extern "C" int hic_event_elapsed_ms(void *start, void *stop, float *h_ms) {
 
 extern "C" int hic_set_knob(int k, int value) {
   if (k < 0 || k >= HIC_KNOB_COUNT) return hic::arg_error("knob %d", k);
-  if (k == HIC_KNOB_DCT_PATH && value != -1 && !(value >= 0 && value <= 4))
-    return hic::arg_error("dct path %d (0 exact, 1 / 2 float64 AAN, 3 packed float32)", value);
+  if (k == HIC_KNOB_DCT_PATH && value != -1 && !(value >= 0 && value <= 2))
+    return hic::arg_error("dct path %d (0 exact, 1 / 2 float64 AAN)", value);
   if (k == HIC_KNOB_COLOR_SEG && value != -1 && value != 8 && value != 16) return hic::arg_error("colour segment");
-  if ((k == HIC_KNOB_DCT_PK_PF || k == HIC_KNOB_ENCODE_PK) && value != -1 && value != 0 && value != 1)
-    return hic::arg_error("knob %d: 0 or 1", k);
-  // retired knobs (measured slower, removed in rounds 4-5)
-  if (k >= 9 && k <= 12) return hic::arg_error("knob %d is retired", k);
+  // retired knobs (measured slower, removed in rounds 4-5: 9-12 encode waves / nontemporal
+  // stores / integer-MFMA transforms, 14-15 the packed-float32 transforms)
+  if ((k >= 9 && k <= 12) || k == 14 || k == 15) return hic::arg_error("knob %d is retired", k);
   if (k == HIC_KNOB_ENCODE_ORDER && value != -1 && (value < 0 || value > 7 || (value & 1)))
     return hic::arg_error("encode_order 0, 2, 4 or 6");
   if (value < -1) return hic::arg_error("knob value %d", value);

@@ -25,8 +25,6 @@
 #include <stdlib.h>
 
 #include "dct_core.h"
-#include "dct_pk.h"
-#include "dct_2l.h"
 #include "rle_core.h"
 
 namespace hic {
@@ -603,339 +601,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DCT_WPE
 }
 
 // ---------------------------------------------------------------------------
-// Packed-float32 forward kernel for aligned planes (dct_path 3, the default since
-// round 5; dct_pk.h).  The float64 AAN kernel above issues ~1000 VALU instructions
-// per 64-block set at 3 waves per SIMD: its VALU time alone is about the 8K luma
-// pass's memory floor, so the two do not overlap into that floor.  This kernel
-// runs the AAN transform on <2 x float> pairs (half the instructions of float64
-// for the same work), checks every coefficient against its proven float32 window,
-// and recomputes the few flagged blocks (~2 per set on random data) in float64 with
-// the whole wave at once (pk_coop_redo_k) instead of one block per lane; 4 waves per
-// SIMD (<= 128 VGPRs; the 136-byte LDS stage rows of 4-wave workgroups allow no
-// more).  PF: the next set's pixel rows load while this set computes.
-#ifndef HIC_PK_WPE
-#define HIC_PK_WPE 4
-#endif
-template <int TMF, bool PF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_PK_WPE))) void k_dct_pk(DctJobs jobs) {
-  __shared__ __attribute__((aligned(16))) uint2 s_stage[4 * 64 * kStageU2];
-  __shared__ uint2 s_px_all[4][16];  // per wave: two flagged blocks' pixel rows (the redo)
-  __shared__ __attribute__((aligned(16))) double s_tab_d[sizeof(PkRedoTab) / sizeof(double)];
-  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nwaves = gridDim.x * 4;
-  const int g0 = blockIdx.x * 4 + wv;
-  uint2 *st2 = s_stage + wv * 64 * kStageU2;
-  uint2 *s_px = s_px_all[wv];
-  int16_t *st = reinterpret_cast<int16_t *>(st2 + lane * kStageU2);
-  const int M = jobs.M;
-  // the redo's constants: copied to LDS by the first wave of the workgroup that needs
-  // them (pk_redo_flagged; every wave that does writes the same values, no barrier)
-  bool tab_ready = false;
-  // this lane's (u, v) = (lane >> 3, lane & 7) slot in a stage row: the cooperative redo
-  const int slot_off = 2 * kPkSlot.s[lane];
-  auto st16 = [&](int b, int k) {
-    const uint2 lo = st2[b * kStageU2 + 2 * k], hi = st2[b * kStageU2 + 2 * k + 1];
-    return make_uint4(lo.x, lo.y, hi.x, hi.y);
-  };
-  auto job_of = [&](int g) {
-    g = __builtin_amdgcn_readfirstlane(g);
-    int k = 0;
-    while (k + 1 < jobs.n && g >= jobs.j[k + 1].set0) ++k;
-    return __builtin_amdgcn_readfirstlane(k);
-  };
-  // the set's block coordinates: the set's first block by scalar division, each lane
-  // past it by at most one row wrap when a block row holds >= 64 blocks (a per-lane
-  // division otherwise)
-  auto load = [&](const DctJob &J, int set, uint2 (&w)[8]) {
-    const int b0 = __builtin_amdgcn_readfirstlane(set * 64);
-    const int bi0 = __builtin_amdgcn_readfirstlane(b0 / J.nbx);
-    const int bj0 = __builtin_amdgcn_readfirstlane(b0 - bi0 * J.nbx);
-    const int blk = b0 + lane;
-    int bi, bj;
-    if (J.nbx >= 64) {
-      bj = bj0 + lane;
-      bi = bi0;
-      if (bj >= J.nbx) {
-        bj -= J.nbx;
-        ++bi;
-      }
-      if (blk >= J.nblk) {  // past the plane (a partial last set): its last block
-        bi = (J.nblk - 1) / J.nbx;
-        bj = J.nblk - 1 - bi * J.nbx;
-      }
-    } else {
-      const int cblk = blk < J.nblk ? blk : J.nblk - 1;
-      bi = cblk / J.nbx;
-      bj = cblk - bi * J.nbx;
-    }
-    const uint8_t *p = J.plane + (int64_t)bi * 8 * J.stride + bj * 8;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) w[r] = *reinterpret_cast<const uint2 *>(p + r * J.stride);
-  };
-  // stage -> ZIGZAG_I16 output in 1 KiB nontemporal stores (+ the RLE tile record)
-  auto store = [&](const DctJob &J, int set) {
-    __builtin_amdgcn_wave_barrier();
-    const int blk = set * 64 + lane;
-    uint4 *o = reinterpret_cast<uint4 *>(static_cast<int16_t *>(J.out) + (int64_t)set * 64 * 64);
-    auto sv = [&](int k) { return st16(8 * k + (lane >> 3), lane & 7); };
-    if ((set + 1) * 64 <= J.nblk) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint4 t = sv(k);
-        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 v = {t.x, t.y, t.z, t.w};
-        __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(o + 64 * k + lane));
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (set * 64 + 8 * k + (lane >> 3) < J.nblk) o[64 * k + lane] = sv(k);
-    }
-    if (TMF >= 0) {
-      uint32_t zw[32];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint4 t = st16(lane, k);
-        zw[4 * k] = t.x; zw[4 * k + 1] = t.y; zw[4 * k + 2] = t.z; zw[4 * k + 3] = t.w;
-      }
-      tile_record16<TMF>(zw, blk < J.nblk, blk, M, J.tiles + (int64_t)set * 3);
-    }
-    __builtin_amdgcn_wave_barrier();
-  };
-
-  uint64_t redo = 0;  // bit i: this wave's i-th set holds a coefficient only the exact replica decides
-  int i = 0;
-  if (g0 < jobs.total_sets) {
-    int kj = job_of(g0);
-    DctJob J = jobs.j[kj];
-    int next0 = kj + 1 < jobs.n ? jobs.j[kj + 1].set0 : jobs.total_sets;
-    uint2 wn[8];
-    if (PF) load(J, g0 - J.set0, wn);
-    for (int g = g0; g < jobs.total_sets; g += nwaves, ++i) {
-      if (g >= next0) {
-        kj = job_of(g);
-        J = jobs.j[kj];
-        next0 = kj + 1 < jobs.n ? jobs.j[kj + 1].set0 : jobs.total_sets;
-      }
-      const int set = g - J.set0;
-      const int tb = J.table;  // wave-uniform: the quantiser constants are scalar loads
-      uint2 w[8];
-      if (PF) {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) w[r] = wn[r];
-        const int gn = g + nwaves;
-        if (gn < jobs.total_sets) {
-          const int kn = gn >= next0 ? job_of(gn) : kj;
-          load(jobs.j[kn], gn - jobs.j[kn].set0, wn);
-        }
-      } else {
-        load(J, set, w);
-      }
-#if defined(HIC_DEV) && defined(HIC_PK_DEV) && (HIC_PK_DEV & 8)
-      const uint32_t fl = pk_block<0>(w, st);  // dev timing (results invalid): the luminance table only
-#else
-      const uint32_t fl = pk_block<-1>(w, st, tb);
-#endif
-      // flagged blocks: the whole wave recomputes each in float64, patching its stage row
-#if defined(HIC_DEV) && defined(HIC_PK_DEV) && (HIC_PK_DEV & 1)
-      uint64_t fb = 0;  // dev timing (results invalid): no cooperative redo
-      (void)fl;
-#else
-      uint64_t fb = __builtin_amdgcn_ballot_w64((int)fl < 0 && set * 64 + lane < J.nblk);
-#endif
-#if defined(HIC_DEV) && defined(HIC_PK_DEV) && (HIC_PK_DEV & 16)
-      asm volatile("" ::"s"(fb));  // dev timing (results invalid): flags computed, no redo
-      fb = 0;
-#endif
-#if defined(HIC_DEV) && defined(HIC_PK_DEV) && (HIC_PK_DEV & 32)
-      asm volatile("s_mov_b64 %0, 0" : "+s"(fb));  // dev timing (results invalid): the redo compiled, not run
-#endif
-      // (the flagged blocks' pixel rows, still in their lanes' registers, reach every
-      // lane through LDS)
-      if (fb && !pk_redo_flagged(fb, w, s_px, st2, kStageU2, tb, slot_off, lane, s_tab_d, tab_ready))
-        redo |= 1ull << i;
-      store(J, set);
-    }
-  }
-  // sets with a coefficient inside the float64 window too (an exact (2,2)-class tie):
-  // the whole set again on the exact pocketfft replica
-  while (redo) {
-    const int k = __builtin_ctzll(redo);
-    redo &= redo - 1;
-    const int g = g0 + k * nwaves;
-    const DctJob &J = jobs.j[job_of(g)];
-    const int set = g - J.set0;
-    uint2 w[8];
-    load(J, set, w);
-    dct_block_2ph<-1, HIC_LAYOUT_ZIGZAG_I16>(w, st, J.table);
-    store(J, set);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Float64 AAN forward kernel with two lanes per block (dct_path 4, dct_2l.h): the
-// records-free ZIGZAG_I16 pass (north_star's DCT + quantize + zig-zag).  A wave
-// iteration is a half set (32 blocks, 4 KiB of output): lane l holds block
-// l & 31's rows / columns 4h .. 4h + 3 (h = l >> 5), so the wave's state is half
-// a block per lane (<= 96 VGPRs) and its stage 32 rows (4.3 KiB): 5 waves per SIMD
-// instead of k_dct_planes' 3.  The stage rows are raster order; each 16-byte output
-// chunk gathers its 8 zig-zag coefficients (ds_read_u16 at per-lane addresses fixed
-// for the kernel, the store index k an immediate offset).  Ties are dct_block_aan's:
-// a half set with a (2,2)-class tie rewrites those four coefficients after the loop
-// (dct_fix26), one with any other tie runs the exact replica (one lane per block).
-#ifndef HIC_2L_WPE
-#define HIC_2L_WPE 5
-#endif
-template <int TMF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_2L_WPE))) void k_dct_2l(DctJobs jobs) {
-  static_assert(TMF < 0, "k_dct_2l: records-free pass only");
-  constexpr int kRowB = kStageU2 * 8;  // stage row bytes (136)
-  __shared__ __attribute__((aligned(16))) uint8_t s_stage[4 * 32 * kRowB];
-  __shared__ double s_kra[2 * 64];
-  __shared__ __attribute__((aligned(16))) uint16_t s_ga[64 * 8];
-  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int h = lane >> 5, b = lane & 31;
-  const int nwaves = gridDim.x * 4;
-  const int g0 = blockIdx.x * 4 + wv;
-  const int total = 2 * jobs.total_sets;  // half sets
-  uint8_t *sw = s_stage + wv * 32 * kRowB;
-  uint8_t *strow = sw + b * kRowB + 8 * h;
-  // the store's gather: lane l copies chunk c = l & 7 (zig-zag positions 8c .. 8c + 7)
-  // of block 8k + (l >> 3); s_ga[l][t]: the byte offset of position 8c + t in the
-  // wave's stage (row l >> 3), read as one 16-byte word per store
-  for (int k = threadIdx.x; k < 128; k += blockDim.x) s_kra[k] = kRA[k >> 6][k & 63];
-  for (int k = threadIdx.x; k < 64 * 8; k += blockDim.x)
-    s_ga[k] = (uint16_t)((k >> 6) * kRowB + kZzOff.o[8 * ((k >> 3) & 7) + (k & 7)]);
-  __syncthreads();
-  auto job_of = [&](int g) {
-    g = __builtin_amdgcn_readfirstlane(g);
-    int k = 0;
-    while (k + 1 < jobs.n && g >= jobs.j[k + 1].set0) ++k;
-    return __builtin_amdgcn_readfirstlane(k);
-  };
-  // block (hb0 + b)'s pixel rows 4h .. 4h + 3 (past the plane: its last block)
-  auto load = [&](const DctJob &J, int hb0, uint2 (&w)[4]) {
-    const int b0 = __builtin_amdgcn_readfirstlane(hb0);
-    const int bi0 = __builtin_amdgcn_readfirstlane(b0 / J.nbx);
-    const int bj0 = __builtin_amdgcn_readfirstlane(b0 - bi0 * J.nbx);
-    const int blk = b0 + b;
-    int bi, bj;
-    if (J.nbx >= 32) {
-      bj = bj0 + b;
-      bi = bi0;
-      if (bj >= J.nbx) {
-        bj -= J.nbx;
-        ++bi;
-      }
-      if (blk >= J.nblk) {
-        bi = (J.nblk - 1) / J.nbx;
-        bj = J.nblk - 1 - bi * J.nbx;
-      }
-    } else {
-      const int cblk = blk < J.nblk ? blk : J.nblk - 1;
-      bi = cblk / J.nbx;
-      bj = cblk - bi * J.nbx;
-    }
-    const uint8_t *p = J.plane + ((int64_t)bi * 8 + 4 * h) * J.stride + bj * 8;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) w[r] = *reinterpret_cast<const uint2 *>(p + r * J.stride);
-  };
-  // raster stage -> ZIGZAG_I16 output: 4 stores of 1 KiB (nontemporal for a whole half set)
-  auto store = [&](const DctJob &J, int hb0) {
-    __builtin_amdgcn_wave_barrier();
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    u32x4 *o = reinterpret_cast<u32x4 *>(static_cast<int16_t *>(J.out) + (int64_t)hb0 * 64);
-    const bool full = hb0 + 32 <= J.nblk;
-    const uint4 gw = reinterpret_cast<const uint4 *>(s_ga)[lane];
-    const uint32_t gv[4] = {gw.x, gw.y, gw.z, gw.w};
-    int ga[8];
-#pragma unroll
-    for (int t = 0; t < 8; ++t) ga[t] = (int)((gv[t >> 1] >> (16 * (t & 1))) & 0xFFFFu);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      uint32_t v[8];
-#pragma unroll
-      for (int t = 0; t < 8; ++t) v[t] = *reinterpret_cast<const uint16_t *>(sw + ga[t] + 8 * kRowB * k);
-      const u32x4 d = {v[0] | v[1] << 16, v[2] | v[3] << 16, v[4] | v[5] << 16, v[6] | v[7] << 16};
-      if (full)
-        __builtin_nontemporal_store(d, o + 64 * k + lane);
-      else if (hb0 + 8 * k + (lane >> 3) < J.nblk)
-        o[64 * k + lane] = d;
-    }
-    __builtin_amdgcn_wave_barrier();
-  };
-
-  uint64_t redo = 0, fix = 0;  // bit i: this wave's i-th half set (the launcher keeps <= 64)
-  int i = 0;
-  if (g0 < total) {
-    int kj = job_of(g0 >> 1);
-    DctJob J = jobs.j[kj];
-    int next0 = kj + 1 < jobs.n ? jobs.j[kj + 1].set0 : jobs.total_sets;
-    for (int g = g0; g < total; g += nwaves, ++i) {
-      const int gs = g >> 1;
-      if (gs >= next0) {
-        kj = job_of(gs);
-        J = jobs.j[kj];
-        next0 = kj + 1 < jobs.n ? jobs.j[kj + 1].set0 : jobs.total_sets;
-      }
-      const int hb0 = (gs - J.set0) * 64 + (g & 1) * 32;
-      uint2 w[4];
-      load(J, hb0, w);
-      uint32_t tie = 0xFFFFFFFFu, tie26 = 0xFFFFFFFFu;
-      dct_half_2l<-1>(w, strow, s_kra + J.table * 64 + 4 * h, h, tie, tie26, J.table);
-      if (__builtin_amdgcn_ballot_w64(tie <= kTieMax) != 0) redo |= 1ull << i;
-      if (__builtin_amdgcn_ballot_w64(tie26 <= kTieMax) != 0) fix |= 1ull << i;
-      store(J, hb0);
-    }
-  }
-  fix &= ~redo;
-  // after the loop, one lane per block (lanes 0..31, all eight pixel rows)
-  auto rows8 = [&](const DctJob &J, int blk, uint2 (&w)[8]) {
-    const int cblk = blk < J.nblk ? blk : J.nblk - 1;
-    const int bi = cblk / J.nbx, bj = cblk - bi * J.nbx;
-    const uint8_t *p = J.plane + (int64_t)bi * 8 * J.stride + bj * 8;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) w[r] = *reinterpret_cast<const uint2 *>(p + r * J.stride);
-  };
-  // (2,2)-class exact ties: those four coefficients of the half set's blocks, in place
-  while (fix) {
-    const int k = __builtin_ctzll(fix);
-    fix &= fix - 1;
-    const int g = g0 + k * nwaves;
-    const DctJob &J = jobs.j[job_of(g >> 1)];
-    const int blk = ((g >> 1) - J.set0) * 64 + (g & 1) * 32 + lane;
-    if (lane < 32) {
-      uint2 w[8];
-      rows8(J, blk, w);
-      int q[4];
-      dct_fix26<-1>(w, q, J.table);
-      if (blk < J.nblk) {
-        constexpr SlotOf<HIC_LAYOUT_ZIGZAG_I16> kSlot{};
-        constexpr int idx[4] = {18, 22, 50, 54};
-        int16_t *o = static_cast<int16_t *>(J.out) + (int64_t)blk * 64;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[kSlot.s[idx[j]]] = (int16_t)q[j];
-      }
-    }
-  }
-  // any other tie (rare): the half set again on the exact pocketfft replica
-  while (redo) {
-    const int k = __builtin_ctzll(redo);
-    redo &= redo - 1;
-    const int g = g0 + k * nwaves;
-    const DctJob &J = jobs.j[job_of(g >> 1)];
-    const int hb0 = ((g >> 1) - J.set0) * 64 + (g & 1) * 32;
-    __builtin_amdgcn_wave_barrier();
-    if (lane < 32) {
-      uint2 w[8];
-      rows8(J, hb0 + lane, w);
-      dct_block_2ph<-1, HIC_LAYOUT_RASTER_I16>(w, reinterpret_cast<int16_t *>(sw + lane * kRowB), J.table);
-    }
-    store(J, hb0);
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Block-level helpers (transform.dct2 / idct2, quantization.jpeg_quantize /
 // invert_jpeg_quantize on arbitrary float64 / int blocks): one block per lane.
 __global__ __launch_bounds__(256) void k_dct2_f64(const double *__restrict__ in, int64_t nblk, double *__restrict__ out) {
@@ -999,21 +664,16 @@ __global__ void k_dequantize_i32(const int32_t *__restrict__ in, int64_t n, int 
 inline bool aligned(const void *p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
 
 // Forward-path selection (A/B tests only; every path is bit-exact): knob
-// "dct_path" 3 = packed-float32 AAN with the cooperative float64 redo (k_dct_pk,
-// ZIGZAG_I16 output; the default; raster layouts take path 1), 1 = float64 AAN fast
-// path (k_dct_planes), 2 = the same (its prefetch variant is compiled out), 0 = the
-// exact pocketfft replica for every block; "dct_waves_per_cu" = persistent grid size
-// (0 = one wave per set); "dct_pk_pf" 1 = k_dct_pk loads the next set's pixels
-// while this one computes.  Set through hic_set_knob (common.hip); the library
-// reads no environment variables.
+// "dct_path" 1 = float64 AAN fast path (k_dct_planes, the default), 2 = the same
+// (its prefetch variant is compiled out), 0 = the exact pocketfft replica for every
+// block; "dct_waves_per_cu" = persistent grid size (0 = one wave per set).  Round 5
+// measured and removed the packed-float32 (path 3) and two-lanes-per-block (path 4)
+// kernels (commit ae5c500 holds them).  Set through
+// hic_set_knob (common.hip); the library reads no environment variables.
 inline int dct_path() { return knob(HIC_KNOB_DCT_PATH); }
 inline int dct_waves_per_cu(int njobs) {
   const int v = knob(HIC_KNOB_DCT_WAVES_PER_CU);
   if (v >= 0) return v;
-  // packed path: a persistent grid of its 4 waves per SIMD
-  if (dct_path() == 3) return 16;
-  // two lanes per block: a persistent grid of its 5 waves per SIMD
-  if (dct_path() == 4) return 20;
   // float64 path: one wave per set for a multi-plane launch (the hardware's dispatch
   // balances the planes' mixed tail: 8K Y + Cr + Cb 37.5 us vs 39.7 for 12
   // persistent waves per CU), 12 persistent waves per CU for one plane (4K luma
@@ -1039,34 +699,10 @@ int launch_planes(DctJobs &jobs, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   const int waves = (cap == 0 || total < cap) ? total : cap;
   const dim3 grid((waves + 3) / 4), block(256);
   const int path = dct_path();
-  if (path == 4 && LAYOUT == HIC_LAYOUT_ZIGZAG_I16 && TMF < 0) {
-    // half sets: <= 64 per wave (the fix / redo masks)
-    int cap2 = dct_waves_per_cu(jobs.n) * cu_count();
-    const int halves = 2 * total;
-    if (cap2 > 0 && (halves + cap2 - 1) / cap2 > 64) cap2 = (halves + 63) / 64;
-    const int waves2 = (cap2 == 0 || halves < cap2) ? halves : cap2;
-    const dim3 grid2((waves2 + 3) / 4);
-    if (e0 || e1)
-      hipExtLaunchKernelGGL(k_dct_2l<-1>, grid2, block, 0, s, e0, e1, 0, jobs);
-    else
-      hipLaunchKernelGGL(k_dct_2l<-1>, grid2, block, 0, s, jobs);
-    return check_launch("k_dct_2l");
-  }
-  if (path == 3 && LAYOUT == HIC_LAYOUT_ZIGZAG_I16) {
-    auto go = [&](auto kern) {
-      if (e0 || e1)
-        hipExtLaunchKernelGGL(kern, grid, block, 0, s, e0, e1, 0, jobs);
-      else
-        hipLaunchKernelGGL(kern, grid, block, 0, s, jobs);
-    };
-    if (knob(HIC_KNOB_DCT_PK_PF) == 1) go(k_dct_pk<TMF, true>);
-    else go(k_dct_pk<TMF, false>);
-    return check_launch("k_dct_pk");
-  }
   if (e0 || e1)
-    hipExtLaunchKernelGGL((k_dct_planes<TABLE, LAYOUT, TMF>), grid, block, 0, s, e0, e1, 0, jobs, path >= 3 ? 1 : path);
+    hipExtLaunchKernelGGL((k_dct_planes<TABLE, LAYOUT, TMF>), grid, block, 0, s, e0, e1, 0, jobs, path);
   else
-    hipLaunchKernelGGL((k_dct_planes<TABLE, LAYOUT, TMF>), grid, block, 0, s, jobs, path >= 3 ? 1 : path);
+    hipLaunchKernelGGL((k_dct_planes<TABLE, LAYOUT, TMF>), grid, block, 0, s, jobs, path);
   return check_launch("k_dct_planes");
 }
 

@@ -3,7 +3,6 @@
 // (encode.hip).  See dct.hip for the design notes and reference citations.
 #pragma once
 #include "hic_common.h"
-#include "dct_windows.h"
 
 namespace hic {
 namespace {
@@ -566,114 +565,6 @@ __host__ __device__ __forceinline__ int dc_quant(int X) {
   const int a = 8 * X + T;                        // 2 (4X) + T
   const int q = (a >= 0 ? a : a - (2 * T - 1)) / (2 * T);  // floor(a / 2T)
   return (a == q * 2 * T && (q & 1)) ? q - 1 : q;  // exact tie: to even
-}
-
-// Fallback: y_uv (full scale, as scipy's 2-D DCT-II of the centred block) in
-// float64, bounded by E2 (dct_bounds.py).  Separable and folded by symmetry
-// (C_k(7 - n) = (-1)^k C_k(n), C_k(n) = 2 cos(pi k (2n + 1) / 16)):
-//   r_m = sum_{n<4} C_v(n) a_mn,  a_mn = x_mn + (-1)^v x_m,7-n (centred; an exact
-//         integer), as one multiply and three fmas;
-//   y   = sum_{m<4} C_u(m) b_m,   b_m = r_m + (-1)^u r_7-m (one rounded add),
-// 40 float64 operations instead of 72.  u, v may differ per lane.  cm[m] = 2 cos(pi
-// m / 16), m = 0..8, correctly rounded; the factors follow by symmetry (period 32,
-// cos(pi - a) = -cos(a)).  The caller passes cm from wherever is cheapest to read
-// per lane (LDS in the kernels).
-constexpr double kCm[9] = {2.0,
-                           0x1.f6297cff75cb0p+0,
-                           0x1.d906bcf328d46p+0,
-                           0x1.a9b66290ea1a3p+0,
-                           0x1.6a09e667f3bcdp+0,
-                           0x1.1c73b39ae68c8p+0,
-                           0x1.87de2a6aea963p-1,
-                           0x1.8f8b83c69a60bp-2,
-                           0.0};
-__host__ __device__ __forceinline__ double cos2(const double *cm, int k, int n) {
-  int m = (k * (2 * n + 1)) & 31;
-  if (m > 16) m = 32 - m;
-  const bool neg = m > 8;
-  const double c = cm[neg ? 16 - m : m];
-  return neg ? -c : c;
-}
-
-// ctab: nullptr -> computed from kCm; else the full table ctab[8k + n] = cos2(kCm, k, n)
-__host__ __device__ __forceinline__ double dct_coef_f64(const uint2 (&w)[8], int u, int v,
-                                                       const double *ctab = nullptr) {
-  double cv[4], cu[4];
-#pragma unroll
-  for (int n = 0; n < 4; ++n) {
-    cv[n] = ctab ? ctab[8 * v + n] : cos2(kCm, v, n);
-    cu[n] = ctab ? ctab[8 * u + n] : cos2(kCm, u, n);
-  }
-  const int sv = (v & 1) ? -1 : 1, ov = (v & 1) ? 0 : 256;  // a = x_n + sv x_{7-n} - ov (raw bytes)
-  double r[8];
-#pragma unroll
-  for (int m = 0; m < 8; ++m) {
-    auto px = [&](int n) -> int { return (int)(((n < 4 ? w[m].x : w[m].y) >> (8 * (n & 3))) & 0xFFu); };
-    double acc = (double)(px(0) + sv * px(7) - ov) * cv[0];
-#pragma unroll
-    for (int n = 1; n < 4; ++n) acc = __builtin_fma((double)(px(n) + sv * px(7 - n) - ov), cv[n], acc);
-    r[m] = acc;
-  }
-  const bool uo = (u & 1) != 0;
-  double y = (uo ? r[0] - r[7] : r[0] + r[7]) * cu[0];
-#pragma unroll
-  for (int m = 1; m < 4; ++m) y = __builtin_fma(uo ? r[m] - r[7 - m] : r[m] + r[7 - m], cu[m], y);
-  return y;
-}
-
-// Quantise the fallback's y for raster index i of `table`: returns false (q unset)
-// when y / T is within 2^-kW2Log2 of a half-integer (the fallback's window; then
-// only the exact pocketfft replica decides).  p = y * (1/T) + 1/2 + 2^-30 is
-// rounded to a multiple of 2^-32 (|p| < 2^19 -> the fma's result lies in
-// [2^20, 2^21)); its low word is frac(p) in units of 2^-32.
-__host__ __device__ __forceinline__ bool quant_f64_window(double y, int T, int &q) {
-  static_assert(kW2Log2 == 30, "window constant below assumes 2^-30");
-  const double rT = 1.0 / (double)T;  // correctly rounded (IEEE division)
-  const unsigned long long t =
-      __builtin_bit_cast(unsigned long long, __builtin_fma(y, rT, 0x1.8p20 + 0.5 + 0x1p-30));
-  const uint32_t lo = (uint32_t)t;
-  q = (int)((uint32_t)(t >> 32) - kQHi);
-  // frac(y/T + 1/2 + 2^-30) < 2^-29 (+ 1 unit of the rounding): within 2^-30 of a tie
-  return lo > 9u;
-}
-
-
-// pocketfft's half-scaled y'[4][4] (row outputs 4 = an integer times TW3, then the
-// column pass's output-4 sequence): y44 is rational (2 x a pixel sum), so a tie
-// of the luminance table (T = 68: the sum = 17 mod 34) is decided by pocketfft's
-// roundings, which this reproduces.
-__host__ __device__ __forceinline__ double pf_y44(const uint2 (&w)[8]) {
-  double y[8];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    auto px = [&](int n) -> int { return (int)(((n < 4 ? w[r].x : w[r].y) >> (8 * (n & 3))) & 0xFFu); };
-    y[r] = (double)((px(0) + px(7) + px(3) + px(4)) - (px(1) + px(2) + px(5) + px(6))) * TW3;
-  }
-  const double c1 = y[1] + y[2], c3 = y[3] + y[4], c5 = y[5] + y[6], H0 = y[0] + y[7];
-  const double h1 = c1 + c5, T2 = H0 + c3;
-  return (T2 - h1) * TW3;
-}
-
-// Resolve AC coefficient i (raster) of this block exactly (table may differ per
-// lane).  The float64 estimate decides outside its window; inside it, the
-// coefficients whose y can be rational -- (4,4) and the (2,2) class, the only
-// ones that tie on non-adversarial data -- are recomputed with pocketfft's own
-// operation sequence.  Returns false if only the whole-block replica can decide.
-__host__ __device__ __forceinline__ bool resolve_coef(const uint2 (&w)[8], int table, int i, int &q,
-                                                     const double *ctab = nullptr, const uint8_t *qt = nullptr) {
-  const int T = qt ? (int)qt[table * 64 + i] : QT[table][i];
-  if (quant_f64_window(dct_coef_f64(w, i >> 3, i & 7, ctab), T, q)) return true;
-  if (i == 36) {
-    q = quant_fast<-1>(pf_y44(w), 36, table);
-    return true;
-  }
-  if (i == 18 || i == 22 || i == 50 || i == 54) {
-    int f[4];
-    dct_fix26<-1>(w, f, table);
-    q = i == 18 ? f[0] : i == 22 ? f[1] : i == 50 ? f[2] : f[3];
-    return true;
-  }
-  return false;
 }
 
 }  // namespace

@@ -44,7 +44,6 @@
 // coefficient writes 3 B per pixel.
 #include "color_core.h"
 #include "dct_core.h"
-#include "dct_pk.h"
 #include "rle_core.h"
 
 namespace hic {
@@ -109,39 +108,6 @@ __device__ __forceinline__ void enc_dct(uint2 (&w)[8], int16_t *st) {
     enc_exact_block<TABLE>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], st);
   } else if (__builtin_amdgcn_ballot_w64(t26)) {
     enc_fix26_block<TABLE>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], st);
-  }
-}
-
-// The packed-float32 transform (dct_pk.h; knob encode_pk 1): pk_block, then the
-// flagged blocks recomputed by the whole wave in float64 two at a time (their pixel
-// rows broadcast through the wave's 128-byte s_px area), and a pass with a
-// coefficient inside the float64 window too (an exact (2,2)-class tie) redone on the
-// exact replica.
-// valid: this lane's block exists (a ragged strip's lanes past W compute on
-// whatever their loads returned and store nothing).
-template <int TABLE>
-__device__ __forceinline__ void enc_dct_pk(uint2 (&w)[8], int16_t *st, uint2 *st2, uint2 *s_px, bool valid,
-                                           double *s_tab_d, uint8_t *s_slot, bool &tab_ready) {
-  const int lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-  const uint32_t fl = pk_block<TABLE>(w, st);
-#if defined(HIC_DEV) && defined(HIC_PK_DEV) && (HIC_PK_DEV & 1)
-  uint64_t fb = 0;  // dev timing (results invalid): no cooperative redo
-  (void)fl;
-  (void)valid;
-#else
-  uint64_t fb = __builtin_amdgcn_ballot_w64((int)fl < 0 && valid);
-#endif
-#if defined(HIC_DEV) && defined(HIC_PK_DEV) && (HIC_PK_DEV & 16)
-  asm volatile("" ::"s"(fb));  // dev timing (results invalid): flags computed, no redo
-  fb = 0;
-#endif
-#if defined(HIC_DEV) && defined(HIC_PK_DEV) && (HIC_PK_DEV & 32)
-  asm volatile("s_mov_b64 %0, 0" : "+s"(fb));  // dev timing (results invalid): the redo compiled, not run
-#endif
-  if (fb) {
-    pk_tab_fill(s_tab_d, s_slot, lane, tab_ready);
-    if (!pk_redo_flagged(fb, w, s_px, st2, kStageU2, TABLE, 2 * s_slot[lane], lane, s_tab_d, tab_ready))
-      enc_exact_block<TABLE>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], st);
   }
 }
 
@@ -454,18 +420,14 @@ struct EncColour {
 // 2-wave budget (colour rows 0..9, Y block row 0, rows 10..18): 8K bench
 // 0.1017-0.1041 vs 0.1043-0.1063 ms/step in 5 alternating pairs
 // (profiles/r03/s2/enc_w3/).  Measured slower and removed (git history): the 2-wave
-// kernel, the float32 / packed-float32 / integer-MFMA transforms, cached stores, the
-// one-pass (look-back + emission) variant and vertically stacked units.
-template <int TMF, bool PK>
+// kernel, the float32 / packed-float32 / integer-MFMA transforms (the packed one
+// again in round 5, with proven windows and a cooperative float64 redo: 70.5-74.9
+// vs 55.6-57.7 us, commit ae5c500), cached stores, the one-pass (look-back +
+// emission) variant and vertically stacked units.
+template <int TMF>
 __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_eu(3))) void k_encode420(Enc420 E) {
   __shared__ __attribute__((aligned(16))) uint2 s_stage[HIC_ENC_WPB * 64 * kStageU2];
   __shared__ uint32_t s_chroma_all[HIC_ENC_WPB][2 * 8 * 64];
-  __shared__ uint2 s_px_all[PK ? HIC_ENC_WPB : 1][16];  // PK: two flagged blocks' pixel rows
-  // PK: the cooperative redo's constants and (u, v) slots in LDS (its latency, not a
-  // global load's), copied there by the first wave of the workgroup that needs them
-  __shared__ __attribute__((aligned(16))) double s_tab_d[PK ? sizeof(PkRedoTab) / sizeof(double) : 1];
-  __shared__ uint8_t s_slot[PK ? 64 : 1];
-  bool tab_ready = false;  // PK: filled by the wave's first redo (pk_tab_fill, no barrier)
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint2 *st2 = s_stage + wv * 64 * kStageU2;
   uint32_t *s_chroma = s_chroma_all[wv];
@@ -488,10 +450,7 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
     uint2 w[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) w[r] = yq[8 * br + r];
-    if (PK)
-      enc_dct_pk<0>(w, st, st2, s_px_all[PK ? wv : 0], lane < nb, s_tab_d, s_slot, tab_ready);
-    else
-      enc_dct<0>(w, st);
+    enc_dct<0>(w, st);
     const int64_t b0 = (int64_t)(2 * u0 + br) * nbx + 64 * s;
     __builtin_amdgcn_wave_barrier();
     int16_t *o = E.coef[0] + b0 * 64;
@@ -516,10 +475,7 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
     uint2 w[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = sc[i * 32];
-    if (PK)
-      enc_dct_pk<1>(w, st, st2, s_px_all[PK ? wv : 0], (lane & 31) < (nb >> 1), s_tab_d, s_slot, tab_ready);
-    else
-      enc_dct<1>(w, st);
+    enc_dct<1>(w, st);
     const int64_t b0 = (int64_t)u0 * nbxc + 32 * s;
     __builtin_amdgcn_wave_barrier();
     enc_store(st2, fresh_lane(), E.coef[1] + b0 * 64, E.coef[2] + b0 * 64, nb >> 1, nb >> 1);
@@ -676,11 +632,10 @@ static int encode420(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, 
     else
       hipLaunchKernelGGL(kern, grid, block, 0, s, E);
   };
-  const bool pk = knob(HIC_KNOB_ENCODE_PK) == 1;
   if (max_len == 15)
-    pk ? launch(k_encode420<15, true>) : launch(k_encode420<15, false>);
+    launch(k_encode420<15>);
   else
-    pk ? launch(k_encode420<0, true>) : launch(k_encode420<0, false>);
+    launch(k_encode420<0>);
   if (int e = check_launch("k_encode420")) return e;
   if (recs && !aligned) {  // one record per 64-block tile, all three planes (not seg)
     const int64_t ny = (out_rows / 8) * (W / 8), nc = (out_rows / 16) * (W / 16);

@@ -8,7 +8,7 @@
 //  hic_probe_plane: the forward plane pass's own byte pattern without the DCT --
 //                   lane = one 8x8 block (8 row loads of 8 B), the 64 blocks of a
 //                   wave's set staged in LDS and written as 1 KiB nontemporal
-//                   stores in block order (k_dct_pk's copy-out), the next set's
+//                   stores in block order (k_dct_planes' copy-out), the next set's
 //                   rows loading during the current set's stage and store: 1 B
 //                   read and 2 B written per pixel, the luma DCT pass's traffic.
 #include "hic_common.h"
@@ -120,7 +120,7 @@ extern "C" int hic_probe_plane(const uint8_t *plane, int64_t H, int64_t W, int16
   if ((H / 8) * (W / 8) >= (1LL << 31) / 64) return arg_error("plane too large");
   if (reinterpret_cast<uintptr_t>(plane) % 8 || reinterpret_cast<uintptr_t>(out) % 16) return arg_error("alignment");
   const int nbx = (int)(W / 8), nblk = (int)((H / 8) * nbx), nsets = (nblk + 63) / 64;
-  const int cap = (waves_per_cu ? waves_per_cu : 12) * cu_count();  // default: k_dct_pk's grid
+  const int cap = (waves_per_cu ? waves_per_cu : 12) * cu_count();  // default: k_dct_planes' one-plane grid
   const int waves = nsets < cap ? nsets : cap;
   const dim3 grid((unsigned)((waves + 3) / 4)), block(256);
   const hipStream_t s = as_stream(stream);

@@ -66,7 +66,7 @@ int hic_device_count(int *h_n);
  * Every selectable path is bit-exact: a knob never changes results, only which
  * kernel variant computes them.  The library reads no environment variables.
  * Values are process-wide; -1 restores the default. */
-#define HIC_KNOB_DCT_PATH 0         /* forward DCT of aligned planes: 3 packed-float32 AAN (ZIGZAG_I16 output; the default), 1 / 2 float64 AAN, 0 exact replica */
+#define HIC_KNOB_DCT_PATH 0         /* forward DCT of aligned planes: 1 / 2 float64 AAN (the default), 0 exact replica; 3 / 4 (packed float32, two lanes per block: removed in round 5) are refused */
 #define HIC_KNOB_DCT_WAVES_PER_CU 1 /* forward DCT persistent grid (waves per CU; 0 = one wave per set) */
 #define HIC_KNOB_COLOR_TILED 2      /* 1: LDS-tiled colour kernels instead of the wave-walk ones */
 #define HIC_KNOB_COLOR_SEG 3        /* wave-walk colour: chroma rows per segment (8 default, 16) */
@@ -78,8 +78,7 @@ int hic_device_count(int *h_n);
 /* knobs 9-12 were retired in rounds 4-5 (encode waves / nontemporal stores / integer-MFMA
  * transforms: measured slower, removed); hic_set_knob refuses them */
 #define HIC_KNOB_ENCODE_ORDER 13     /* hic_encode420_u8 unit order: 0 row-major; + 2: workgroups remapped XCD-major (neighbouring units on one XCD's L2); + 4: odd unit rows run their colour rows bottom-up (the halo rows two unit rows share fetched at the same time); default 6; odd values refused */
-#define HIC_KNOB_DCT_PK_PF 14        /* 1: the packed-float32 plane kernel loads the next set's pixel rows while a set computes */
-#define HIC_KNOB_ENCODE_PK 15        /* 1: hic_encode420_u8's three DCT passes on the packed-float32 transform (dct_pk.h) */
+/* 14, 15: retired in round 5 with the packed-float32 transforms (refused) */
 #define HIC_KNOB_COUNT 16
 int hic_set_knob(int knob, int value);
 int hic_get_knob(int knob, int *h_value);
@@ -95,7 +94,7 @@ int hic_stream_sync(void *stream);
  *  hic_probe_plane: the forward plane pass's byte pattern without the DCT: a uint8
  *    H x W plane (pitch W, multiples of 8) read as 8x8 blocks (one per lane), 128 B
  *    per block written to out (nblk x 64 int16) through the LDS stage and 1 KiB
- *    nontemporal stores of k_dct_pk, persistent grid: the pass's memory floor.
+ *    nontemporal stores of k_dct_planes, persistent grid: the pass's memory floor.
  *  waves_per_cu: persistent grid size (0 = default: 16 for the copy, 12 for the plane).
  *  hic_probe_encode420: hic_encode420_u8's byte pattern without its arithmetic, on a
  *    whole H x W RGB image (W % 512 == 0, H % 16 == 0): the same grid, unit order

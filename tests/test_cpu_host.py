@@ -75,12 +75,11 @@ def test_knob_defaults_and_ranges():
     for bad in (8, 3, 1):  # odd: the stacked-unit order was removed in round 5
         with pytest.raises(ValueError):
             _lib.set_knob("encode_order", bad)
-    with _lib.knobs(dct_path=_lib.DCT_PATH_2L):
-        assert _lib.get_knob("dct_path") == 4
-    for bad in (5, -2):
-        with pytest.raises(ValueError):
-            _lib.set_knob("dct_path", bad)
-    for retired in (9, 10, 11, 12):  # retired knobs are refused outright
+    with _lib.knobs(dct_path=_lib.DCT_PATH_EXACT):
+        assert _lib.get_knob("dct_path") == 0
+    for bad in (3, 4, 5, -2):  # 3 / 4: the packed and two-lane kernels, removed in round 5
+        assert _lib.load().hic_set_knob(0, bad) == _lib.HIC_ERR_ARG
+    for retired in (9, 10, 11, 12, 14, 15):  # retired knobs are refused outright
         assert _lib.load().hic_set_knob(retired, 0) == _lib.HIC_ERR_ARG
 
 

@@ -1,10 +1,12 @@
 """The exactness proof of the fast forward DCT paths, pinned (CPU).
 
 tools/check/dct_bounds.py derives rigorous forward-error bounds for every fast
-path and generates hiccup_amd/csrc/dct_windows.h, the tie
-windows the kernels compile in.  These tests re-run the derivation and fail when
-the committed header and the proof drift apart (a one-ulp edit of any constant),
-or when a path's bound no longer sits inside its margin.
+path: E64 for the float64 AAN path the product runs, and E1 /
+E2 for the packed-float32 path measured in round 5 and removed (commit ae5c500
+compiled its windows from tools/check/dct_windows.h, kept as the proof's output).
+These tests re-run the derivation and fail when the committed header and the proof
+drift apart (a one-ulp edit of any constant), or when a path's bound no longer sits
+inside its margin.
 """
 import math
 import os
@@ -16,7 +18,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tools", "check"))
 import dct_bounds  # noqa: E402
 
-HEADER = os.path.join(REPO, "hiccup_amd", "csrc", "dct_windows.h")
+HEADER = os.path.join(REPO, "tools", "check", "dct_windows.h")
 
 
 def test_windows_header_matches_proof(tmp_path):
@@ -57,7 +59,7 @@ def test_float32_windows_cover_their_bounds():
 
 def test_float32_constants_within_the_proof_model():
     """E1 (dct_bounds.py) models every float32 constant of the packed path as within
-    2^-24 |c| of its real value: the four AAN factors (dct_pk.h rounds dct_core.h's
+    2^-24 |c| of its real value: the four AAN factors (the packed kernel rounded dct_core.h's
     float64 kA1 / kA2 / kA4 / kA5 to float32) and the quantiser constants kR32 =
     float32(S_u S_v / T).  Checked against 50-digit values."""
     import re

@@ -381,25 +381,18 @@ def _structured_rgb(kind, H, W, seed):
     raise ValueError(kind)
 
 
-# the fused kernel against the chain's plane DCT on both of its shipped paths (packed
-# float32 with the cooperative float64 redo, float64 AAN)
-@pytest.mark.parametrize("enc_pk", [0, 1])
-@pytest.mark.parametrize("chain_path", [_lib.DCT_PATH_PK, _lib.DCT_PATH_F64])
 @pytest.mark.parametrize("kind", ["random", "levels", "colour_levels", "blocks", "flat"])
 @pytest.mark.parametrize("H,W", [(16, 512), (144, 2048), (1088, 1536)])
-def test_fused_encoder_matches_two_kernel_chain(kind, H, W, chain_path, enc_pk):
+def test_fused_encoder_matches_two_kernel_chain(kind, H, W):
     """hic_encode420_u8 (colour + pyrDown + DCT + tile records in one kernel, exact
-    tie fallbacks in place; its DCT passes on the float64 or, knob encode_pk, the
-    packed-float32 transform) == the two-kernel chain (hic_rgb_to_ycrcb420 +
-    hic_dct_quant_rle_u8_batch on either plane kernel), symbols and DC streams
-    included (the fused chroma records are 32-block half tiles)."""
+    tie fallbacks in place) == the two-kernel chain (hic_rgb_to_ycrcb420 +
+    hic_dct_quant_rle_u8_batch), symbols and DC streams included (the fused chroma
+    records are 32-block half tiles)."""
     rgb = _structured_rgb(kind, H, W, H + W)
     x = device.to_device(rgb)
     got, exp = pipeline.Encoder(H, W, fused=True), pipeline.Encoder(H, W, fused=False)
-    with _lib.knobs(encode_pk=enc_pk):
-        got.encode(x)
-    with _lib.knobs(dct_path=chain_path):
-        exp.encode(x)
+    got.encode(x)
+    exp.encode(x)
     a, b = got.result(), exp.result()
     for k in pipeline.CHANNELS:
         for j, what in enumerate(("coef", "dc", "sym_len", "sym_val")):
@@ -422,8 +415,7 @@ def test_fused_encoder_ragged_matches_chain(kind, H, W):
     pass after the launch (hic_encode420_u8), equal too.  2048x16 and 1024x48 are
     the narrow, tall shapes whose segment records outnumber their 64-block tiles
     (ADVICE r4)."""
-    for enc_pk in (0, 1):
-        test_fused_encoder_matches_two_kernel_chain(kind, H, W, _lib.DCT_PATH_PK, enc_pk)
+    test_fused_encoder_matches_two_kernel_chain(kind, H, W)
     rgb = _structured_rgb(kind, H, W, H + W)
     x = device.to_device(rgb)
     got, exp = pipeline.Encoder(H, W, fused=True, index=True), pipeline.Encoder(H, W, fused=False)

@@ -98,12 +98,11 @@ def test_layouts_roundtrip(layout, shape):
         np.testing.assert_array_equal(device.to_host(rec), orcc.inv_dct_channel(exp, tab))
 
 
-@pytest.mark.parametrize("path", [-1, _lib.DCT_PATH_2L, _lib.DCT_PATH_PK, _lib.DCT_PATH_F64])
+@pytest.mark.parametrize("path", [-1, _lib.DCT_PATH_EXACT])
 @pytest.mark.parametrize("H,W", [(4096, 4096), (4320, 7680)])
 def test_full_size_bit_exact(H, W, path):
     """BASELINE configs 2/3 plane sizes, bit-exact against the C oracle (multi-threaded),
-    on the default forward path, the two-lanes-per-block float64 one, the
-    packed-float32 one and the one-lane float64 AAN one."""
+    on the default forward path (float64 AAN) and the exact pocketfft replica."""
     with _lib.knobs(dct_path=path):
         _full_size_bit_exact(H, W)
 
@@ -131,7 +130,7 @@ def test_tie_blocks_many():
         np.testing.assert_array_equal(transform.dct_channel(plane, QT[tab]), orcc.dct_channel(plane, tab, threads=8))
 
 
-@pytest.mark.parametrize("path", [_lib.DCT_PATH_2L, _lib.DCT_PATH_PK, _lib.DCT_PATH_F64, _lib.DCT_PATH_EXACT])
+@pytest.mark.parametrize("path", [_lib.DCT_PATH_F64, _lib.DCT_PATH_EXACT])
 @pytest.mark.parametrize("kind", ["levels4", "nearflat", "stripes", "checker", "blur"])
 def test_fast_path_structured_ties(kind, path):
     with _lib.knobs(dct_path=path):
@@ -196,11 +195,11 @@ def test_bad_args():
         _lib.call("hic_dct_quant_u8", device.ptr(dev), 8, 8, 8, 0, 9, device.ptr(out), device.stream_ptr())
 
 
-@pytest.mark.parametrize("path", [_lib.DCT_PATH_PK, _lib.DCT_PATH_F64])
+@pytest.mark.parametrize("path", [_lib.DCT_PATH_F64, _lib.DCT_PATH_EXACT])
 @pytest.mark.parametrize("kind", ["random", "levels4", "nearflat", "blur", "checker"])
 @pytest.mark.parametrize("H,W", [(8, 16), (8 * 61, 16 * 7), (8 * 33, 8 * 130), (8 * 160, 8 * 320)])
 def test_plane_dct_rle_records(kind, path, H, W):
-    """The plane DCT's fused RLE tile records (k_dct_pk / k_dct_planes, partial
+    """The plane DCT's fused RLE tile records (k_dct_planes, partial
     last sets included) drive the channel RLE: symbols and DC
     differences of hic_dct_quant_rle_u8 + hic_rle_encode_i16_tiles_batch equal the
     C oracle's run_length_coding / differential_coding (codec.py:47-99)."""
@@ -231,7 +230,7 @@ def test_plane_dct_rle_records(kind, path, H, W):
         np.testing.assert_array_equal(device.to_host(dc), orcc.dpcm(exp[:, 0].copy()), err_msg=(kind, tab))
 
 
-@pytest.mark.parametrize("path", [_lib.DCT_PATH_PK, _lib.DCT_PATH_F64])
+@pytest.mark.parametrize("path", [_lib.DCT_PATH_F64, _lib.DCT_PATH_EXACT])
 @pytest.mark.parametrize("waves_per_cu", [-1, 1])
 @pytest.mark.parametrize("kind", ["random", "levels4"])
 def test_plane_batch_three_planes(kind, waves_per_cu, path):
@@ -252,16 +251,15 @@ def test_plane_batch_sixteen_planes(kind):
     _plane_batch(shapes, kind, -1, -1)
 
 
-@pytest.mark.parametrize("path", [_lib.DCT_PATH_2L, _lib.DCT_PATH_PK, _lib.DCT_PATH_F64])
+@pytest.mark.parametrize("path", [_lib.DCT_PATH_F64, _lib.DCT_PATH_EXACT])
 @pytest.mark.parametrize("waves_per_cu", [-1, 1])
 @pytest.mark.parametrize("kind", ["random", "levels4", "nearflat", "blur"])
 def test_plane_batch_records_free(kind, waves_per_cu, path):
     """The records-free batched pass (no RLE workspaces: north_star's DCT + quantize
     + zig-zag, what the back-to-back measurement runs): 8K Y + two 4K chroma planes,
     then 16 small planes of mixed tables whose block rows hold < 32, 32..63 and >= 64
-    blocks (the two-lane kernel's per-lane division and its one-wrap path) with
-    partial last sets; with one persistent wave per CU each wave walks many half sets
-    of different planes and keeps its tie sets for after the loop."""
+    blocks with partial last sets; with one persistent wave per CU each wave walks
+    many sets of different planes and keeps its tie sets for after the loop."""
     shapes = [(4320, 7680, 0), (2160, 3840, 1), (2160, 3840, 1)]
     small = [(8 * (5 + 3 * i), 8 * (7 + 9 * i), i % 2) for i in range(16)]
     for sh in (shapes, small):

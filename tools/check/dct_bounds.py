@@ -1,6 +1,7 @@
 """Rigorous forward-error bounds for the DCT paths of the forward kernel (DESIGN.md
-§5 "Why the fast path is exact").  Not product code: it prints/emits the tie
-windows compiled into hiccup_amd/csrc/dct_windows.h.
+§5 "Why the fast path is exact").  Not product code: it prints the bounds and
+emits tools/check/dct_windows.h, the float32 windows the round-5 packed kernel
+compiled in (removed from the product; commit ae5c500).
 
 Every intermediate is a linear functional L of the 64 pixels of a block (float64
 coefficients; we only need magnitudes).  For each node we carry a bound E on

@@ -28,5 +28,5 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 [ "${2:-}" = "trace" ] && exit 0
 timeout -k 10 900 bash tools/prof_r2.sh r5_$tag > $out/prof_r2.log 2>&1 || { tail -5 $out/prof_r2.log; exit 1; }
 python3 tools/prof_r2_summary.py gpurun_out/prof_r5_$tag $out/prof_summary.json && echo profiled
-timeout -k 10 600 bash tools/r5_sq.sh $tag "1 3 4" > $out/sq.log 2>&1 || { tail -5 $out/sq.log; exit 1; }
+timeout -k 10 600 bash tools/r5_sq.sh $tag "1" > $out/sq.log 2>&1 || { tail -5 $out/sq.log; exit 1; }
 cat $out/sq.log

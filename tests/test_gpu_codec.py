@@ -436,7 +436,7 @@ def test_fused_encoder_unit_order(kind, H, W, order):
     remapped XCD-major; + 4: odd unit rows run their colour rows bottom-up; ragged
     last strips included) == the two-kernel chain."""
     with _lib.knobs(encode_order=order):
-        test_fused_encoder_matches_two_kernel_chain(kind, H, W, _lib.DCT_PATH_F64, -1)
+        test_fused_encoder_matches_two_kernel_chain(kind, H, W)
 
 
 @pytest.mark.parametrize("H,W", [(2048, 16), (1024, 48), (4096, 32)])

@@ -827,18 +827,26 @@ extern "C" int hic_dct_quant_rle_u8_batch(int n, const hic_dct_plane_job *jobs, 
     J.M = max_len;
     const hipEvent_t a0 = timed ? nullptr : e0, a1 = timed ? nullptr : e1;
     timed = true;
+    // one table for every job (a batch of luminance planes, say): the kernel compiled
+    // for it, whose quantiser constants are literals instead of scalar loads per set
+    int uni = J.j[0].table;
+    for (int k = 1; k < J.n; ++k)
+      if (J.j[k].table != uni) uni = -1;
+    if (!merge) uni = t;
     int e;
     if (!recs)
-      e = launch_planes<-1, HIC_LAYOUT_ZIGZAG_I16, -1>(J, s, a0, a1);
-    else if (merge)
-      e = max_len == 15 ? launch_planes<-1, HIC_LAYOUT_ZIGZAG_I16, 15>(J, s, a0, a1)
-                        : launch_planes<-1, HIC_LAYOUT_ZIGZAG_I16, 0>(J, s, a0, a1);
-    else if (t == 0)
+      e = uni == 0   ? launch_planes<0, HIC_LAYOUT_ZIGZAG_I16, -1>(J, s, a0, a1)
+          : uni == 1 ? launch_planes<1, HIC_LAYOUT_ZIGZAG_I16, -1>(J, s, a0, a1)
+                     : launch_planes<-1, HIC_LAYOUT_ZIGZAG_I16, -1>(J, s, a0, a1);
+    else if (uni == 0)
       e = max_len == 15 ? launch_planes<0, HIC_LAYOUT_ZIGZAG_I16, 15>(J, s, a0, a1)
                         : launch_planes<0, HIC_LAYOUT_ZIGZAG_I16, 0>(J, s, a0, a1);
-    else
+    else if (uni == 1)
       e = max_len == 15 ? launch_planes<1, HIC_LAYOUT_ZIGZAG_I16, 15>(J, s, a0, a1)
                         : launch_planes<1, HIC_LAYOUT_ZIGZAG_I16, 0>(J, s, a0, a1);
+    else
+      e = max_len == 15 ? launch_planes<-1, HIC_LAYOUT_ZIGZAG_I16, 15>(J, s, a0, a1)
+                        : launch_planes<-1, HIC_LAYOUT_ZIGZAG_I16, 0>(J, s, a0, a1);
     if (e) return e;
   }
   return HIC_OK;

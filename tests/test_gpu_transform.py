@@ -242,6 +242,15 @@ def test_plane_batch_three_planes(kind, waves_per_cu, path):
     _plane_batch([(4320, 7680, 0), (2160, 3840, 1), (2160, 3840, 1)], kind, waves_per_cu, path)
 
 
+@pytest.mark.parametrize("table", [0, 1])
+@pytest.mark.parametrize("kind", ["random", "levels4"])
+def test_plane_batch_one_table_records(kind, table):
+    """A batch whose planes share one table runs the kernel compiled for that table
+    (literal quantiser constants), RLE tile records included: coefficients, DC
+    differences and symbols vs the C oracle."""
+    _plane_batch([(8 * 45, 8 * 96, table), (8 * 30 + 8, 8 * 64 + 24, table), (8 * 52, 8 * 70, table)], kind, -1, -1)
+
+
 @pytest.mark.parametrize("kind", ["random", "nearflat"])
 def test_plane_batch_sixteen_planes(kind):
     """The batched launch at its maximum: 16 planes of mixed tables and sizes (incl.
@@ -262,7 +271,10 @@ def test_plane_batch_records_free(kind, waves_per_cu, path):
     many sets of different planes and keeps its tie sets for after the loop."""
     shapes = [(4320, 7680, 0), (2160, 3840, 1), (2160, 3840, 1)]
     small = [(8 * (5 + 3 * i), 8 * (7 + 9 * i), i % 2) for i in range(16)]
-    for sh in (shapes, small):
+    # one table for every plane: the launch takes the kernel compiled for that table
+    luma = [(8 * (40 + i), 8 * (64 + 5 * i), 0) for i in range(4)]
+    chroma = [(8 * (33 + 2 * i), 8 * (70 + 3 * i), 1) for i in range(3)]
+    for sh in (shapes, small, luma, chroma):
         planes, outs, jobs = [], [], (_lib.DctPlaneJob * len(sh))()
         for i, (h, w, t) in enumerate(sh):
             p = _structured_plane(kind, h, w)

@@ -151,7 +151,8 @@ def cpu_baseline(budget_s):
 def plane_kernel(tmf):
     """The forward plane kernel the library runs for ZIGZAG_I16 planes (dct_path knob)."""
     from hiccup_amd import _lib
-    return "k_dct_planes<-1,ZIGZAG_I16,%d> (float64 AAN)" % tmf
+    return ("k_dct_planes<T,ZIGZAG_I16,%d> (float64 AAN; T = the planes' table when they share one, -1 = per "
+            "plane at run time)" % tmf)
 
 
 def spread(ts_us):

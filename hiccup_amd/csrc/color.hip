@@ -126,37 +126,6 @@ __global__ __launch_bounds__(256) void k_rgb_ycrcb420(const uint8_t *__restrict_
 // itself (x = -2, -1 -> 2, 1; x = W -> W - 2).
 constexpr int kStripQ = 64;
 
-typedef unsigned short u16x2c __attribute__((ext_vector_type(2)));
-typedef short s16x2c __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b) {
-  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2c, a) + __builtin_bit_cast(u16x2c, b));
-}
-__device__ __forceinline__ uint32_t pk_mad_u16(uint32_t a, uint32_t k, uint32_t c) {  // a * k + c per half
-  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2c, a) * __builtin_bit_cast(u16x2c, k) +
-                                          __builtin_bit_cast(u16x2c, c));
-}
-__device__ __forceinline__ uint32_t pk_sra6(uint32_t a) {
-  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2c, a) >> (short)6);
-}
-// acc + lo(crcb) * lo(k) + hi(crcb) * hi(k), signed 16-bit halves; the
-// three-operand form (k in an SGPR), so no copy of acc per channel
-__device__ __forceinline__ int ycc_dot(uint32_t crcb, uint32_t k, int acc) {
-  int d;
-  asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(crcb), "s"(k), "v"(acc));
-  return d;
-}
-__device__ __forceinline__ uint32_t sreg(uint32_t k) {  // opaque wave-uniform constant
-  asm volatile("" : "+s"(k));
-  return k;
-}
-// low 16 bits: sat8(a >> 14) | sat8(b >> 14) << 8 (gfx950 v_ashr_pk_u8_i32)
-__device__ __forceinline__ uint32_t sat_pk2(int a, int b) {
-  uint32_t d;
-  asm("v_ashr_pk_u8_i32 %0, %1, %2, 14" : "=v"(d) : "v"(a), "v"(b));
-  return d;
-}
-
-
 // [1 4 6 4 1] over five packed taps (k4 = 4 | 4 << 16, k6 = 6 | 6 << 16, registers:
 // a literal 4 is strength-reduced to a shift and an add)
 __device__ __forceinline__ uint32_t pk_taps5(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e, uint32_t k4,

@@ -49,5 +49,37 @@ __device__ __forceinline__ uint32_t pack4(uint32_t b0, uint32_t b1, uint32_t b2,
   return b0 | b1 << 8 | b2 << 16 | b3 << 24;
 }
 
+// Packed 16-bit pairs (cr | cb << 16) and the YCrCb -> RGB dot products of the
+// decode colour kernels (color.hip k_ycrcb420_rgb_walk, dct.hip k_rld_idct_rgb_indexed).
+typedef unsigned short u16x2c __attribute__((ext_vector_type(2)));
+typedef short s16x2c __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2c, a) + __builtin_bit_cast(u16x2c, b));
+}
+__device__ __forceinline__ uint32_t pk_mad_u16(uint32_t a, uint32_t k, uint32_t c) {  // a * k + c per half
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2c, a) * __builtin_bit_cast(u16x2c, k) +
+                                          __builtin_bit_cast(u16x2c, c));
+}
+__device__ __forceinline__ uint32_t pk_sra6(uint32_t a) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2c, a) >> (short)6);
+}
+// acc + lo(crcb) * lo(k) + hi(crcb) * hi(k), signed 16-bit halves; the
+// three-operand form (k in an SGPR), so no copy of acc per channel
+__device__ __forceinline__ int ycc_dot(uint32_t crcb, uint32_t k, int acc) {
+  int d;
+  asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(crcb), "s"(k), "v"(acc));
+  return d;
+}
+__device__ __forceinline__ uint32_t sreg(uint32_t k) {  // opaque wave-uniform constant
+  asm volatile("" : "+s"(k));
+  return k;
+}
+// low 16 bits: sat8(a >> 14) | sat8(b >> 14) << 8 (gfx950 v_ashr_pk_u8_i32)
+__device__ __forceinline__ uint32_t sat_pk2(int a, int b) {
+  uint32_t d;
+  asm("v_ashr_pk_u8_i32 %0, %1, %2, 14" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+
 }  // namespace
 }  // namespace hic

@@ -24,6 +24,7 @@
 //    numpy does.  The guard is > 10^3 x the reciprocal's error bound.
 #include <stdlib.h>
 
+#include "color_core.h"
 #include "dct_core.h"
 #include "rle_core.h"
 
@@ -161,9 +162,8 @@ __device__ __forceinline__ double fma_scale_add(double y, double k_s, double c_v
 // Dequantize (q * T, exact in int32), the 2-D DCT-III in pocketfft's float64
 // operation order, /256 + 128, truncate, wrap, and store the 8x8 pixels of the
 // block at (y0, x0) of the H x W plane (FAST: whole block inside, 8-byte rows).
-template <int TABLE, bool FAST>
-__device__ __forceinline__ void idct_block_store(const int (&q)[64], int H, int W, int y0, int x0,
-                                                 uint8_t *__restrict__ out, int64_t ostride) {
+template <int TABLE>
+__device__ __forceinline__ void idct_block_px(const int (&q)[64], uint32_t (&px)[16]) {
   // dequantize (q * T, exact in int32) and row pass
   double a[8][8];
 #pragma unroll
@@ -178,7 +178,7 @@ __device__ __forceinline__ void idct_block_store(const int (&q)[64], int H, int 
   // three-address v_fma_f64: LLVM's v_fmac_f64 form overwrote its accumulator,
   // so it re-materialised 128.0 (two v_mov_b32) before each of the 64 fmas
   const double k2m8 = sreg_f64(0x1p-8), k128 = vreg_f64(128.0);
-  uint32_t px[16];  // row r: bytes v = 0..3 in px[2r], 4..7 in px[2r+1]
+  // row r: bytes v = 0..3 in px[2r], 4..7 in px[2r+1]
 #pragma unroll
   for (int k = 0; k < 16; ++k) px[k] = 0;
 #pragma unroll
@@ -194,6 +194,12 @@ __device__ __forceinline__ void idct_block_store(const int (&q)[64], int H, int 
       px[2 * r + (v >> 2)] |= b << (8 * (v & 3));
     }
   }
+}
+template <int TABLE, bool FAST>
+__device__ __forceinline__ void idct_block_store(const int (&q)[64], int H, int W, int y0, int x0,
+                                                 uint8_t *__restrict__ out, int64_t ostride) {
+  uint32_t px[16];
+  idct_block_px<TABLE>(q, px);
   if (FAST) {
     uint8_t *o = out + (int64_t)y0 * ostride + x0;  // one 64-bit multiply; rows step by the uniform stride
 #pragma unroll
@@ -278,18 +284,137 @@ __global__ __launch_bounds__(256) void k_dequant_idct(const void *__restrict__ c
 // HBM (codec.jpeg_decode's RLE / DC half, codec.py:397-421, + inv_dct_channel,
 // transform.py:169-179, for one plane).
 constexpr int kRowI16 = 68;  // LDS block row: 64 slots + pad (136 B, conflict-free 8 B reads)
-constexpr int kDIS = 16;     // symbols per lane per step
 #ifndef HIC_DEC_WPE
 #define HIC_DEC_WPE 4
 #endif
-template <int TABLE, bool FAST>
+// The RGB of one 8x8 luma block (pixels px as idct_block_px leaves them) at block
+// (bi, bj) of an H x W image, H and W multiples of 8: pyrUp(Cr), pyrUp(Cb) of the
+// H/2 x W/2 chroma planes at its 64 pixels, then cvtColor(YCrCb2RGB)
+// (compression.jpeg_decompression, compression.py:48-56).  The arithmetic is
+// color.hip k_ycrcb420_rgb_walk's (cr | cb << 16 pairs biased by -1020 through both
+// pyrUp passes, one v_dot2_i32_i16 per channel), so the bytes equal that kernel's
+// on the same planes.  The chroma columns 4bj-1 / 4bj+4 next to the block's four come
+// from the neighbouring lanes' blocks (DPP) or, at the wave's ends, from one extra
+// dword load per row; reflect-101 at the top / left border, replicate at the
+// bottom / right, as pyr_up_at.  Every lane of the wave must take part (the DPP
+// reads); `live` gates the stores.
+__device__ __forceinline__ void colour_block(const uint32_t (&px)[16], int bi, int bj, int nbx, int nby, int lane,
+                                             bool live, const uint8_t *__restrict__ cr, const uint8_t *__restrict__ cb,
+                                             uint8_t *__restrict__ rgb, int64_t rgb_stride) {
+  const int w = 4 * nbx, h = 4 * nby;
+  // The packed pixels are opaque: otherwise the compiler forwards each truncated
+  // pixel past its packing to the byte extracts below, and 64 live values instead
+  // of 16 spill the IDCT.  bi, bj pass through the last of them, so no address
+  // below is computed (and held) across the IDCT.
+  uint32_t y[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    y[k] = px[k];
+    asm volatile("" : "+v"(y[k]));
+  }
+  asm volatile("" : "+v"(bi), "+v"(bj) : "v"(y[15]));
+  // chroma rows 4bi-1 .. 4bi+4: its own four columns, and the wave-end lanes' outer
+  // neighbour column (lane 0: the dword left of its own, lane 63: the one right)
+  const int ce = lane == 0 ? (bj > 0 ? 4 * bj - 4 : 4 * bj) : (bj < nbx - 1 ? 4 * bj + 4 : 4 * bj);
+  uint32_t dcr[6], dcb[6], ecr[6], ecb[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    int s = 4 * bi - 1 + r;
+    s = s < 0 ? 1 : (s >= h ? h - 1 : s);
+    const int64_t ro = (int64_t)s * w;
+    dcr[r] = *reinterpret_cast<const uint32_t *>(cr + ro + 4 * bj);
+    dcb[r] = *reinterpret_cast<const uint32_t *>(cb + ro + 4 * bj);
+    ecr[r] = *reinterpret_cast<const uint32_t *>(cr + ro + ce);
+    ecb[r] = *reinterpret_cast<const uint32_t *>(cb + ro + ce);
+  }
+  // KB: -1020 per half; K4 opaque (a splat 4 is strength-reduced to a shift + add)
+  const uint32_t K4 = sreg(0x00040004u), K6 = 0x00060006u, KB = 0xFC04FC04u;
+  const uint32_t kr = sreg((uint32_t)(uint16_t)kCR2R), kg = sreg((uint32_t)(uint16_t)kCR2G | (uint32_t)kCB2G << 16),
+                 kb = sreg((uint32_t)kCB2B << 16);
+  auto join = [](uint32_t lo, uint32_t hi) { return __builtin_amdgcn_perm(hi, lo, 0x05040100u); };
+  // horizontal pass of chroma row r: output columns 8bj .. 8bj+7 (x8 scale, biased)
+  auto horiz = [&](int r, uint32_t (&hv)[8]) {
+    uint32_t q[6];  // chroma columns 4bj-1 .. 4bj+4, packed cr | cb << 16
+#pragma unroll
+    for (int j = 0; j < 4; ++j) q[j + 1] = __builtin_amdgcn_perm(dcb[r], dcr[r], 0x0C040C00u + 0x00010001u * j);
+    uint32_t l = shr1(q[4]), rr = shl1(q[1]);
+    l = lane == 0 ? __builtin_amdgcn_perm(ecb[r], ecr[r], 0x0C070C03u) : l;
+    rr = lane == 63 ? __builtin_amdgcn_perm(ecb[r], ecr[r], 0x0C040C00u) : rr;
+    q[0] = bj == 0 ? q[2] : l;         // reflect-101: column -1 -> 1
+    q[5] = bj == nbx - 1 ? q[4] : rr;  // replicate: column w -> w - 1
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      hv[2 * c] = pk_mad_u16(q[c + 1], K6, pk_add_u16(q[c], pk_add_u16(q[c + 2], KB)));
+      hv[2 * c + 1] = pk_mad_u16(pk_add_u16(q[c + 1], q[c + 2]), K4, KB);
+    }
+  };
+  // output row 8bi + r8 from its vertical taps' packed sums v[8]
+  auto emit = [&](int r8, const uint32_t (&v)[8]) {
+    uint32_t o[6];
+    int pend = 0;  // channel bytes waiting for their pair partner
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+      const uint32_t crcb = pk_sra6(v[x]);  // (cr - 128, cb - 128)
+      const int acc = (int)(((y[2 * r8 + (x >> 2)] >> (8 * (x & 3))) & 255u) << 14 | 8192u);
+      const int c3[3] = {ycc_dot(crcb, kr, acc), ycc_dot(crcb, kg, acc), ycc_dot(crcb, kb, acc)};
+      // bytes 3x .. 3x+2 of the row's 24: pairs (2m, 2m+1) -> one v_ashr_pk_u8_i32
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        const int byte = 3 * x + ch;
+        if (byte & 1) {
+          const uint32_t pr = sat_pk2(pend, c3[ch]);  // bytes byte-1, byte
+          if ((byte >> 1) & 1) o[byte >> 2] = join(o[byte >> 2], pr);
+          else o[byte >> 2] = pr;
+        } else {
+          pend = c3[ch];
+        }
+      }
+    }
+    if (live) {
+      uint2 *d = reinterpret_cast<uint2 *>(rgb + (int64_t)(8 * bi + r8) * rgb_stride + 24 * bj);
+      d[0] = make_uint2(o[0], o[1]);
+      d[1] = make_uint2(o[2], o[3]);
+      d[2] = make_uint2(o[4], o[5]);
+    }
+  };
+  // a three-row window down chroma rows 4bi-1 .. 4bi+4: rows k, k+1, k+2 of it give
+  // output rows 8bi + 2k ([1 6 1]) and 8bi + 2k + 1 ([4 4])
+  uint32_t ha[8], hb[8], hc[8];
+  horiz(0, ha);
+  horiz(1, hb);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    horiz(k + 2, hc);
+    uint32_t v[8];
+#pragma unroll
+    for (int x = 0; x < 8; ++x) v[x] = pk_mad_u16(hb[x], K6, pk_add_u16(ha[x], hc[x]));
+    emit(2 * k, v);
+#pragma unroll
+    for (int x = 0; x < 8; ++x) v[x] = pk_mad_u16(pk_add_u16(hb[x], hc[x]), K4, 0);
+    emit(2 * k + 1, v);
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+      ha[x] = hb[x];
+      hb[x] = hc[x];
+    }
+  }
+}
+
+// RGB (luma plane only, TABLE 0, FAST): the pixels go through colour_block into
+// the RGB image instead of to a Y plane -- the Y plane never reaches HBM
+// (jpeg_decompression's decode of the luma channel + pyrUp + cvtColor, with the
+// chroma planes decoded before).
+template <int TABLE, bool FAST, bool RGB = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DEC_WPE))) void k_rld_idct_indexed(const uint8_t *__restrict__ sym_len,
                                                           const int16_t *__restrict__ sym_val,
                                                           const int64_t *__restrict__ d_nsym,
                                                           const int32_t *__restrict__ dc_diff,
                                                           const int64_t *__restrict__ index, int H, int W, int nbx,
                                                           int64_t nblk, uint8_t *__restrict__ out, int64_t ostride,
-                                                          int64_t *__restrict__ d_status) {
+                                                          int64_t *__restrict__ d_status,
+                                                          const uint8_t *__restrict__ cr = nullptr,
+                                                          const uint8_t *__restrict__ cb = nullptr) {
+  static_assert(!RGB || (TABLE == 0 && FAST), "the RGB form decodes whole-block luma planes");
   __shared__ uint2 s_tile[4][64 * kRowI16 / 4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t ntiles = (nblk + 63) / 64;
@@ -305,45 +430,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DEC_WPE
   const int64_t tb0 = t * 64 * 63;
   const int nvb = (int)(nblk - t * 64 < 64 ? nblk - t * 64 : 64);
   const int span = nvb * 63;
-  int P = (int)(index[3 * t + 1] + 1 - tb0);
-  for (int64_t c = o0 & ~(int64_t)(kDIS - 1); c < o1; c += 64 * kDIS) {
-    const int64_t s0 = c + (int64_t)lane * kDIS;
-    int len[kDIS], val[kDIS];
-    if (s0 >= o0 && s0 + kDIS <= o1) {
-      const uint4 l = *reinterpret_cast<const uint4 *>(sym_len + s0);
-      const uint4 v0 = *reinterpret_cast<const uint4 *>(sym_val + s0);
-      const uint4 v1 = *reinterpret_cast<const uint4 *>(sym_val + s0 + 8);
-      const uint32_t lw[4] = {l.x, l.y, l.z, l.w};
-      const uint32_t vw[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-      for (int k = 0; k < kDIS; ++k) {
-        len[k] = (int)((lw[k >> 2] >> (8 * (k & 3))) & 255);
-        val[k] = (int)(int16_t)(vw[k >> 1] >> (16 * (k & 1)));
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < kDIS; ++k) {
-        const bool in = s0 + k >= o0 && s0 + k < o1;
-        len[k] = in ? (int)sym_len[s0 + k] : -1;
-        val[k] = in ? (int)sym_val[s0 + k] : 0;
-      }
-    }
-    int acc = 0;
-#pragma unroll
-    for (int k = 0; k < kDIS; ++k) acc += len[k] + 1;
-    const int incl = wave_incl_sum_i32(acc);
-    int q = P + (incl - acc);
-#pragma unroll
-    for (int k = 0; k < kDIS; ++k) {
-      q += len[k];
-      if (len[k] >= 0 && (unsigned)q < (unsigned)span) {
-        const int b = (q * 2081) >> 17;  // q / 63 on [0, 4032)
-        win[b * kRowI16 + 1 + (q - b * 63)] = (int16_t)val[k];
-      }
-      ++q;
-    }
-    P += wave_last_i32(incl);
-  }
+  // the symbols of the tile into its LDS rows (trash: the lane's row's first pad slot)
+  const int P = gather_tile<kRowI16, HIC_DEC_G, HIC_DEC_PF>(sym_len, sym_val, o0, o1, nsym, (int)(index[3 * t + 1] + 1 - tb0),
+                                                span, win, lane * kRowI16 + 64, lane);
   const int64_t blk = t * 64 + lane;
   const int d = lane < nvb ? dc_diff[blk] : 0;
   win[lane * kRowI16] = (int16_t)(index[3 * t + 2] + wave_incl_sum_i32(d));
@@ -353,10 +442,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DEC_WPE
     const bool eob = nsym > 0 && sym_len[nsym - 1] == 0 && sym_val[nsym - 1] == 0;
     *d_status = nsym_raw < 1 ? -1 : ((eob && total <= n_ac) ? n_ac : total);
   }
-  if (lane >= nvb) return;
+  if (!RGB && lane >= nvb) return;
   int qv[64];  // raster [u][v]
   {
-    const uint2 *row = tile + lane * (kRowI16 / 4);
+    const uint2 *row = tile + (lane < nvb ? lane : nvb - 1) * (kRowI16 / 4);
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const uint2 x = row[k];
@@ -366,8 +455,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DEC_WPE
       qv[ZZ[4 * k + 3]] = (int)(int16_t)(x.y >> 16);
     }
   }
-  const int bi = (int)(blk / nbx), bj = (int)(blk - (int64_t)bi * nbx);
-  idct_block_store<TABLE, FAST>(qv, H, W, bi * 8, bj * 8, out, ostride);
+  const int64_t blk_c = lane < nvb ? blk : t * 64 + nvb - 1;  // RGB: the dead lanes redo the last block
+  const int bi = (int)(blk_c / nbx), bj = (int)(blk_c - (int64_t)bi * nbx);
+  if (RGB) {
+    uint32_t px[16];
+    idct_block_px<TABLE>(qv, px);
+    colour_block(px, bi, bj, nbx, H / 8, lane, lane < nvb, cr, cb, out, ostride);
+  } else {
+    idct_block_store<TABLE, FAST>(qv, H, W, bi * 8, bj * 8, out, ostride);
+  }
 }
 
 // Production forward kernel for aligned planes: up to three planes per launch
@@ -899,6 +995,27 @@ extern "C" int hic_rle_decode_idct_u8_indexed(const uint8_t *sym_len, const int1
   else HIC_RI(1, false);
 #undef HIC_RI
   return check_launch("k_rld_idct_indexed");
+}
+
+extern "C" int hic_rle_decode_idct_rgb_indexed(const uint8_t *sym_len, const int16_t *sym_val, const int64_t *d_nsym,
+                                               const int32_t *dc_diff, const int64_t *d_index, int64_t H, int64_t W,
+                                               const uint8_t *cr, const uint8_t *cb, uint8_t *rgb, int64_t rgb_stride,
+                                               int64_t *d_status, void *stream) {
+  if (!sym_len || !sym_val || !d_nsym || !dc_diff || !d_index || !cr || !cb || !rgb || !d_status)
+    return arg_error("null pointer");
+  if (!dims_ok(H, W) || H % 8 || W % 8) return arg_error("plane shape (H, W multiples of 8)");
+  if (rgb_stride < 3 * W || rgb_stride % 8 || !aligned(rgb, 8)) return arg_error("rgb stride / alignment (8 B)");
+  if (!aligned(cr, 4) || !aligned(cb, 4)) return arg_error("chroma planes must be 4-byte aligned");
+  if ((reinterpret_cast<uintptr_t>(sym_len) | reinterpret_cast<uintptr_t>(sym_val)) % 16)
+    return arg_error("symbol arrays must be 16-byte aligned");
+  const int nbx = (int)(W / 8);
+  const int64_t nblk = (int64_t)nbx * (H / 8);
+  if (nblk * 63 >= ((int64_t)1 << 31)) return arg_error("plane too large (AC stream >= 2^31)");
+  const int64_t ntiles = (nblk + 63) / 64;
+  hipLaunchKernelGGL((k_rld_idct_indexed<0, true, true>), dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0,
+                     as_stream(stream), sym_len, sym_val, d_nsym, dc_diff, d_index, (int)H, (int)W, nbx, nblk, rgb,
+                     rgb_stride, d_status, cr, cb);
+  return check_launch("k_rld_idct_indexed<rgb>");
 }
 
 extern "C" int hic_dct2_f64(const double *in, int64_t nblk, double *out, void *stream) {

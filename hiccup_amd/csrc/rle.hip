@@ -1536,20 +1536,6 @@ __global__ __launch_bounds__(256) void k_rle_index16(const int64_t *__restrict__
   index[3 * t + 2] = t > 0 ? (int64_t)blocks[(t * 64 - 1) * 64] : 0;
 }
 
-constexpr int kIS = 16;  // symbols per lane per step (1024 per wave step)
-struct SymChunk {
-  uint4 l;     // 16 lengths
-  uint4 v[2];  // 16 values
-};
-__device__ __forceinline__ void load_chunk(const uint8_t *__restrict__ sym_len, const int16_t *__restrict__ sym_val,
-                                           int64_t s0, int64_t o0, int64_t o1, SymChunk &c, bool &whole) {
-  whole = s0 >= o0 && s0 + kIS <= o1;
-  if (whole) {
-    c.l = *reinterpret_cast<const uint4 *>(sym_len + s0);
-    c.v[0] = *reinterpret_cast<const uint4 *>(sym_val + s0);
-    c.v[1] = *reinterpret_cast<const uint4 *>(sym_val + s0 + 8);
-  }
-}
 template <bool NT>
 __global__ __launch_bounds__(256) void k_rld_indexed16(const uint8_t *__restrict__ sym_len,
                                                        const int16_t *__restrict__ sym_val,
@@ -1557,7 +1543,7 @@ __global__ __launch_bounds__(256) void k_rld_indexed16(const uint8_t *__restrict
                                                        const int32_t *__restrict__ dc_diff, int64_t nblk,
                                                        const int64_t *__restrict__ index, int16_t *__restrict__ blocks,
                                                        int64_t *__restrict__ d_status) {
-  __shared__ uint4 s_tile[4][64 * 8];
+  __shared__ uint4 s_tile[4][64 * 8 + 8];  // 64 blocks + 64 trash slots
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t ntiles = (nblk + 63) / 64;
   const int64_t t = (int64_t)blockIdx.x * 4 + wv;
@@ -1575,57 +1561,11 @@ __global__ __launch_bounds__(256) void k_rld_indexed16(const uint8_t *__restrict
   const int64_t tb0 = t * 64 * 63;                    // the tile's first AC position
   const int nvb = (int)(nblk - t * 64 < 64 ? nblk - t * 64 : 64);
   const int span = nvb * 63;                           // its AC positions
-  // P: position of the current step's first run, relative to the tile (a carried
-  // run can start far before it; every AC position of the stream fits int32)
-  int P = (int)(index[3 * t + 1] + 1 - tb0);
-  int64_t c = o0 & ~(int64_t)(kIS - 1);
-  SymChunk cur;
-  bool cur_whole;
-  if (c < o1) load_chunk(sym_len, sym_val, c + (int64_t)lane * kIS, o0, o1, cur, cur_whole);
-  for (; c < o1; c += 64 * kIS) {
-    // the next step's symbols load under this step's arithmetic
-    SymChunk nxt;
-    bool nxt_whole = false;
-    if (c + 64 * kIS < o1) load_chunk(sym_len, sym_val, c + 64 * kIS + (int64_t)lane * kIS, o0, o1, nxt, nxt_whole);
-    const int64_t s0 = c + (int64_t)lane * kIS;
-    int len[kIS], val[kIS];
-    if (cur_whole) {
-      const uint32_t lw[4] = {cur.l.x, cur.l.y, cur.l.z, cur.l.w};
-      const uint32_t vw[8] = {cur.v[0].x, cur.v[0].y, cur.v[0].z, cur.v[0].w,
-                              cur.v[1].x, cur.v[1].y, cur.v[1].z, cur.v[1].w};
-#pragma unroll
-      for (int k = 0; k < kIS; ++k) {
-        len[k] = (int)((lw[k >> 2] >> (8 * (k & 3))) & 255);
-        val[k] = (int)(int16_t)(vw[k >> 1] >> (16 * (k & 1)));
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < kIS; ++k) {
-        const bool in = s0 + k >= o0 && s0 + k < o1;
-        len[k] = in ? (int)sym_len[s0 + k] : -1;  // -1: not this tile's symbol
-        val[k] = in ? (int)sym_val[s0 + k] : 0;
-      }
-    }
-    int acc = 0;
-#pragma unroll
-    for (int k = 0; k < kIS; ++k) acc += len[k] + 1;
-    const int incl = wave_incl_sum_i32(acc);
-    int q = P + (incl - acc);
-#pragma unroll
-    for (int k = 0; k < kIS; ++k) {
-      q += len[k];  // a masked symbol (len -1) leaves q unchanged after the ++ below
-      // fillers of a run carried in land before the tile; q / 63 = (q * 2081) >> 17
-      // on [0, 4032)
-      if (len[k] >= 0 && (unsigned)q < (unsigned)span) {
-        const int b = (q * 2081) >> 17;
-        win[b * 64 + 1 + (q - b * 63)] = (int16_t)val[k];
-      }
-      ++q;
-    }
-    P += wave_last_i32(incl);
-    cur = nxt;
-    cur_whole = nxt_whole;
-  }
+  // P: the position after the previous tile's last symbol, relative to the tile (a
+  // carried run can start far before it; every AC position of the stream fits int32).
+  // Trash slots (never read): the 64 after the tile.
+  const int P = gather_tile<64, HIC_DEC_G, HIC_DEC_PF>(sym_len, sym_val, o0, o1, nsym, (int)(index[3 * t + 1] + 1 - tb0), span,
+                                           win, 64 * 64 + lane, lane);
   // DC: the previous block's value plus this tile's differences
   const int64_t b = t * 64 + lane;
   const int d = lane < nvb ? dc_diff[b] : 0;

@@ -361,5 +361,125 @@ __device__ __forceinline__ void copy_out_wave16(const T *s, int a, T *__restrict
     if (e < cap) g[e] = s[(int)(e - sb)];
 }
 
+// ---- indexed tile gather -----------------------------------------------------
+// One wave expands the symbols [o0, o1) of one 64-block tile into its zeroed LDS
+// tile: AC position j of block b goes to win[b * ROW + 1 + j] (slot 0 is the DC,
+// slots 64 .. ROW-1 padding).  codec.decode_run_length's expansion (codec.py:102-113)
+// for the blocks of one tile, from the encoder-side index (k_rld_indexed16,
+// k_rld_idct_indexed).  P: the position after the previous tile's last symbol,
+// relative to this tile (<= 0: a run carried in starts before it); returns P after
+// this tile's last symbol.
+//
+// A wave step takes 64 G symbols, G consecutive ones per lane, loaded as whole
+// vectors.  The symbols of the step's first and last group that belong to other
+// tiles are not masked one by one: the lane holding o0 starts its positions
+// Σ(len+1) of its leading foreign symbols early, so they land before the tile
+// (negative positions), and every lane stops at `lim`, the position after its last
+// own symbol, so the trailing foreign ones land after it.  Each symbol is then
+// q += len + 1, one compare, q / 63 = (q * 2081) >> 17 on [0, 4032), and one
+// ds_write_b16 to its slot or to the lane's trash slot (never read) -- no branch.
+#ifndef HIC_DEC_G
+#define HIC_DEC_G 16  // the decoders' G
+#endif
+#ifndef HIC_DEC_PF
+#define HIC_DEC_PF 2  // and D (2 = one step ahead; 1-6 measured equal)
+#endif
+template <int G>
+struct SymGroup {
+  uint32_t l[G / 4];  // G lengths (bytes)
+  uint32_t v[G / 2];  // G values (int16 pairs)
+};
+template <int G>
+__device__ __forceinline__ void load_group(const uint8_t *__restrict__ sym_len, const int16_t *__restrict__ sym_val,
+                                           int64_t s0, int64_t nsym, SymGroup<G> &x) {
+  typedef uint32_t vl_t __attribute__((ext_vector_type(G / 4)));
+  typedef uint32_t vv_t __attribute__((ext_vector_type(G / 2)));
+  if (s0 + G <= nsym) {  // s0 is a multiple of G: aligned vector loads
+    const vl_t l = *reinterpret_cast<const vl_t *>(sym_len + s0);
+    const vv_t v = *reinterpret_cast<const vv_t *>(sym_val + s0);
+#pragma unroll
+    for (int j = 0; j < G / 4; ++j) x.l[j] = l[j];
+#pragma unroll
+    for (int j = 0; j < G / 2; ++j) x.v[j] = v[j];
+  } else {  // the stream's last group: nothing past nsym is read
+#pragma unroll
+    for (int j = 0; j < G / 4; ++j) x.l[j] = 0;
+#pragma unroll
+    for (int j = 0; j < G / 2; ++j) x.v[j] = 0;
+#pragma unroll
+    for (int k = 0; k < G; ++k)
+      if (s0 + k < nsym) {
+        x.l[k >> 2] |= (uint32_t)sym_len[s0 + k] << (8 * (k & 3));
+        x.v[k >> 1] |= (uint32_t)(uint16_t)sym_val[s0 + k] << (16 * (k & 1));
+      }
+  }
+}
+// n + the sum of the first n lengths (0 <= n <= G)
+template <int G>
+__device__ __forceinline__ int len_prefix(const SymGroup<G> &x, int n) {
+  int a = n;
+#pragma unroll
+  for (int j = 0; j < G / 4; ++j) {
+    const int m = n - 4 * j;
+    const uint32_t mask = m >= 4 ? 0xFFFFFFFFu : (m <= 0 ? 0u : (1u << (8 * m)) - 1u);
+    a = (int)__builtin_amdgcn_udot4(x.l[j] & mask, 0x01010101u, (uint32_t)a, false);
+  }
+  return a;
+}
+template <int ROW, int G, int D>
+__device__ __forceinline__ int gather_tile(const uint8_t *__restrict__ sym_len, const int16_t *__restrict__ sym_val,
+                                           int64_t o0, int64_t o1, int64_t nsym, int P, int span, int16_t *win,
+                                           int trash, int lane) {
+  static_assert(G == 4 || G == 8 || G == 16, "group size");
+  constexpr int S = 64 * G;  // symbols per wave step
+  const int64_t c0 = o0 & ~(int64_t)(G - 1);
+  // loads run D - 1 steps ahead of their use (a 64-block tile of dense blocks is ~4
+  // steps at G = 16).  D = 1 .. 6 measured the same (profiles/r05/decode_gather/):
+  // the gather is not waiting on memory latency
+  SymGroup<G> ring[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+    if (c0 + i * S < o1) load_group<G>(sym_len, sym_val, c0 + i * S + (int64_t)G * lane, nsym, ring[i]);
+  for (int64_t cb = c0; cb < o1; cb += D * S) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      const int64_t c = cb + i * S;
+      if (c >= o1) break;  // wave-uniform
+      const SymGroup<G> &cur = ring[i];
+      int pre = 0, own;  // Σ(len+1) of the lane's leading foreign symbols / of its own
+      if (c >= o0 && c + S <= o1) {  // wave-uniform: every symbol of the step is the tile's
+        own = len_prefix<G>(cur, G);
+      } else {
+        const int64_t s0 = c + (int64_t)G * lane;
+        const int64_t a = o0 - s0, e = o1 - s0;
+        const int skip = a <= 0 ? 0 : (a >= G ? G : (int)a);
+        const int nv = e <= skip ? skip : (e >= G ? G : (int)e);
+        pre = len_prefix<G>(cur, skip);
+        own = len_prefix<G>(cur, nv) - pre;
+      }
+      const int incl = wave_incl_sum_i32(own);
+      const int end = P + incl;
+      uint32_t lim = (uint32_t)(end <= 0 ? 0 : (end < span ? end : span));
+      // opaque to the optimiser: it would otherwise split the one unsigned compare
+      // below in two and sink the slot arithmetic into a branch per symbol
+      asm volatile("" : "+v"(lim));
+      int r = end - own - pre;  // r = q + 1 (q: the symbol's position)
+#pragma unroll
+      for (int k = 0; k < G; ++k) {
+        r += (int)((cur.l[k >> 2] >> (8 * (k & 3))) & 255u) + 1;
+        // slot + 1 = q + 1 + (ROW - 63) (q / 63), q / 63 = (r * 2081 - 2081) >> 17
+        int slot1 = r + __mul24((__mul24(r, 2081) - 2081) >> 17, ROW - 63);
+        asm volatile("" : "+v"(slot1));
+        slot1 = (uint32_t)(r - 1) < lim ? slot1 : trash;
+        win[slot1] = (int16_t)(cur.v[k >> 1] >> (16 * (k & 1)));
+      }
+      P += wave_last_i32(incl);
+      // refill the slot just consumed, D steps ahead
+      if (c + D * S < o1) load_group<G>(sym_len, sym_val, c + D * S + (int64_t)G * lane, nsym, ring[i]);
+    }
+  }
+  return P;
+}
+
 }  // namespace
 }  // namespace hic

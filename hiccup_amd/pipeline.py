@@ -309,16 +309,31 @@ class Decoder:
         self.rgb = device.empty((2 * (H // 2), 2 * (W // 2), 3), torch.uint8)
         self._ws = {}
 
-    def decode(self, sym_len, sym_val, counts, dc, stream=None, index=None, keep_blocks=False):
+    def decode(self, sym_len, sym_val, counts, dc, stream=None, index=None, keep_blocks=False, planes=False):
         """sym_len/sym_val/dc: {channel: device tensor}; counts: host ints per channel.
         index: an Encoder(index=True)'s tile index ({channel: device tensor}); then
         counts is the encoder's device count tensor (3,), nothing crosses to the
         host, and each plane is decoded and inverse-transformed by ONE kernel
         (hic_rle_decode_idct_u8_indexed: no tile pass, scans, DC chain or zig-zag
         blocks in HBM); keep_blocks=True writes self.blocks too (the block-level
-        indexed decode, then the IDCT)."""
+        indexed decode, then the IDCT).  With the index and whole 8x8 blocks (H, W
+        multiples of 8) the chroma planes decode first and the luminance plane goes
+        straight to RGB (hic_rle_decode_idct_rgb_indexed: self.pix["lum"] is not
+        written); planes=True keeps the Y plane and the separate colour kernel."""
         s = device.stream_ptr(stream)
         lib = _lib.load()
+        if index is not None and not keep_blocks and not planes and self.H % 8 == 0 and self.W % 8 == 0:
+            for i, k in ((1, "cr"), (2, "cb")):
+                h, w = self.shapes[k]
+                _lib.call("hic_rle_decode_idct_u8_indexed", device.ptr(sym_len[k]), device.ptr(sym_val[k]),
+                          ctypes.c_void_p(counts.data_ptr() + 8 * i), device.ptr(dc[k]), device.ptr(index[k]), h, w,
+                          TABLES[k], device.ptr(self.pix[k]), self.pix[k].stride(0),
+                          device.ptr(self.status[i:i + 1]), s)
+            _lib.call("hic_rle_decode_idct_rgb_indexed", device.ptr(sym_len["lum"]), device.ptr(sym_val["lum"]),
+                      ctypes.c_void_p(counts.data_ptr()), device.ptr(dc["lum"]), device.ptr(index["lum"]), self.H,
+                      self.W, device.ptr(self.pix["cr"]), device.ptr(self.pix["cb"]), device.ptr(self.rgb),
+                      self.rgb.stride(0), device.ptr(self.status[0:1]), s)
+            return self.rgb
         for i, k in enumerate(CHANNELS):
             h, w = self.shapes[k]
             n = self.blocks[k].shape[0]

@@ -371,6 +371,19 @@ int hic_rle_decode_idct_u8_indexed(const uint8_t *sym_len, const int16_t *sym_va
                                    const int32_t *dc_diff, const int64_t *d_index, int64_t H, int64_t W,
                                    int table_id, uint8_t *out, int64_t out_stride, int64_t *d_status,
                                    void *stream);
+/* The luminance plane's hic_rle_decode_idct_u8_indexed fused with
+ * hic_ycrcb420_to_rgb (compression.jpeg_decompression, compression.py:48-56: the
+ * Y channel's decode + inv_dct_channel, pyrUp(Cr), pyrUp(Cb), cvtColor YCrCb2RGB):
+ * each lane turns its 8x8 block of Y straight into 8x8 RGB pixels, reading the
+ * already decoded H/2 x W/2 chroma planes cr / cb (row pitch W/2, 4-byte aligned);
+ * the Y plane never reaches HBM.  H, W multiples of 8; rgb: H x W x 3, row pitch
+ * rgb_stride (>= 3W, multiple of 8, 8-byte aligned).  The bytes equal
+ * hic_rle_decode_idct_u8_indexed (table 0) followed by hic_ycrcb420_to_rgb;
+ * *d_status as hic_rle_decode_i16_indexed. */
+int hic_rle_decode_idct_rgb_indexed(const uint8_t *sym_len, const int16_t *sym_val, const int64_t *d_nsym,
+                                    const int32_t *dc_diff, const int64_t *d_index, int64_t H, int64_t W,
+                                    const uint8_t *cr, const uint8_t *cb, uint8_t *rgb, int64_t rgb_stride,
+                                    int64_t *d_status, void *stream);
 /* One tile shard's slice of the channel stream (the sharded decode of
  * codec.jpeg_decode, codec.py:397-425): d_stitch is the shard's device record from
  * hic_rle_stitch {carry zeros, closes the stream, has previous DC, previous DC}.

@@ -63,6 +63,24 @@ def test_last_error_roundtrip():
         _lib.check(rc, "x")
 
 
+def test_decode_rgb_indexed_arguments():
+    """hic_rle_decode_idct_rgb_indexed refuses what its kernel cannot take before
+    any device call: null pointers, planes that are not whole 8x8 blocks, a short or
+    unaligned RGB pitch, unaligned chroma planes."""
+    lib = _lib.load()
+    p16 = ctypes.c_void_p(1 << 20)  # never dereferenced
+    args = lambda H, W, cr=p16, stride=None: (p16, p16, p16, p16, p16, H, W, cr, p16, p16,
+                                              3 * W if stride is None else stride, p16, None)
+    assert lib.hic_rle_decode_idct_rgb_indexed(None, *args(64, 64)[1:]) == _lib.HIC_ERR_ARG
+    assert "null pointer" in _lib.last_error()
+    for H, W in ((60, 64), (64, 62), (0, 64)):
+        assert lib.hic_rle_decode_idct_rgb_indexed(*args(H, W)) == _lib.HIC_ERR_ARG, (H, W)
+    assert lib.hic_rle_decode_idct_rgb_indexed(*args(64, 64, stride=3 * 64 - 8)) == _lib.HIC_ERR_ARG
+    assert lib.hic_rle_decode_idct_rgb_indexed(*args(64, 64, stride=3 * 64 + 4)) == _lib.HIC_ERR_ARG
+    assert lib.hic_rle_decode_idct_rgb_indexed(*args(64, 64, cr=ctypes.c_void_p((1 << 20) + 2))) == _lib.HIC_ERR_ARG
+    assert "aligned" in _lib.last_error()
+
+
 def test_knob_defaults_and_ranges():
     """The launch defaults the measurements chose (hic_get_knob reports the effective
     value; no GPU call): encode_order 6 = XCD-major workgroups + odd unit rows

@@ -353,12 +353,23 @@ def test_indexed_decode(H, W, kind):
     assert d2.status.cpu().tolist() == want
     assert torch.equal(r1, r2)
     # the fused decode + IDCT (no blocks in HBM): the same planes and RGB
-    r3 = d3.decode(enc.sym_len, enc.sym_val, enc.counts, enc.dc, index=enc.index)
+    r3 = d3.decode(enc.sym_len, enc.sym_val, enc.counts, enc.dc, index=enc.index, planes=True)
     torch.cuda.synchronize()
     for k in pipeline.CHANNELS:
         assert torch.equal(d3.pix[k], d1.pix[k]), k
     assert d3.status.cpu().tolist() == want
     assert torch.equal(r1, r3)
+    # whole blocks: the luminance decode goes straight to RGB (hic_rle_decode_idct_rgb_indexed,
+    # no Y plane); ragged planes keep the planes path.  Same chroma planes, same RGB.
+    d4 = pipeline.Decoder(H, W)
+    d4.pix["lum"].fill_(0)
+    r4 = d4.decode(enc.sym_len, enc.sym_val, enc.counts, enc.dc, index=enc.index)
+    torch.cuda.synchronize()
+    for k in ("cr", "cb"):
+        assert torch.equal(d4.pix[k], d1.pix[k]), k
+    assert d4.status.cpu().tolist() == want
+    assert torch.equal(r1, r4)
+    assert bool(d4.pix["lum"].any()) == (H % 8 != 0 or W % 8 != 0)  # which path ran
 
 
 def _structured_rgb(kind, H, W, seed):

@@ -178,9 +178,10 @@ __device__ __forceinline__ void idct_block_px(const int (&q)[64], uint32_t (&px)
   // three-address v_fma_f64: LLVM's v_fmac_f64 form overwrote its accumulator,
   // so it re-materialised 128.0 (two v_mov_b32) before each of the 64 fmas
   const double k2m8 = sreg_f64(0x1p-8), k128 = vreg_f64(128.0);
-  // row r: bytes v = 0..3 in px[2r], 4..7 in px[2r+1]
-#pragma unroll
-  for (int k = 0; k < 16; ++k) px[k] = 0;
+  // row r: bytes v = 0..3 in px[2r], 4..7 in px[2r+1].  A truncated value's low
+  // byte is the wrapped pixel; bytes are packed by byte permutes, a pair of columns
+  // per v_perm and two pairs per dword (3 instructions per 4 pixels)
+  uint32_t even[8];  // row r's pixel of the even column of the pair being packed
 #pragma unroll
   for (int v = 0; v < 8; ++v) {
     double xc[8], yv[8];
@@ -190,8 +191,14 @@ __device__ __forceinline__ void idct_block_px(const int (&q)[64], uint32_t (&px)
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const double p = fma_scale_add(yv[r], k2m8, k128);  // == fl(y/256 + 128): y*2^-8 exact
-      const uint32_t b = (uint32_t)__double2int_rz(p) & 0xFFu;
-      px[2 * r + (v >> 2)] |= b << (8 * (v & 3));
+      const uint32_t b = (uint32_t)__double2int_rz(p);
+      if (!(v & 1)) {
+        even[r] = b;
+      } else {
+        const uint32_t pair = __builtin_amdgcn_perm(b, even[r], 0x0C0C0400u);  // even.b0 | b.b0 << 8
+        uint32_t &d = px[2 * r + (v >> 2)];
+        d = (v & 2) ? __builtin_amdgcn_perm(pair, d, 0x05040100u) : pair;
+      }
     }
   }
 }

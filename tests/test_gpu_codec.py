@@ -372,6 +372,33 @@ def test_indexed_decode(H, W, kind):
     assert bool(d4.pix["lum"].any()) == (H % 8 != 0 or W % 8 != 0)  # which path ran
 
 
+@pytest.mark.parametrize("mode", ["rgb", "planes", "blocks"])
+def test_indexed_decode_failed_count(mode):
+    """A failed encode's symbol count (< 1) decodes nothing of that channel and
+    reports status -1 (include/hiccup_hip.h, hic_rle_decode_i16_indexed) on every
+    indexed form -- the fused RGB kernel, the per-plane decode-IDCT, the block
+    decode -- while the other channels decode as usual."""
+    H, W = 128, 192
+    enc = pipeline.Encoder(H, W, index=True)
+    enc.encode(device.to_device(_structured_rgb("random", H, W, 11)))
+    good = pipeline.Decoder(H, W)
+    r_good = good.decode(enc.sym_len, enc.sym_val, enc.counts, enc.dc, index=enc.index).clone()
+    for ch in range(3):
+        counts = enc.counts.clone()
+        counts[ch] = 0
+        dec = pipeline.Decoder(H, W)
+        dec.decode(enc.sym_len, enc.sym_val, counts, enc.dc, index=enc.index,
+                   planes=(mode == "planes"), keep_blocks=(mode == "blocks"))
+        st = dec.status.cpu().tolist()
+        want = [enc.coef[k].shape[0] * 63 for k in pipeline.CHANNELS]
+        want[ch] = -1
+        assert st == want, (ch, st)
+        with pytest.raises(ValueError):
+            dec.check_status()
+    good.check_status()
+    assert r_good.any()
+
+
 def _structured_rgb(kind, H, W, seed):
     rng = np.random.default_rng(seed)
     if kind == "random":

@@ -291,8 +291,10 @@ __global__ __launch_bounds__(256) void k_dequant_idct(const void *__restrict__ c
 // HBM (codec.jpeg_decode's RLE / DC half, codec.py:397-421, + inv_dct_channel,
 // transform.py:169-179, for one plane).
 constexpr int kRowI16 = 68;  // LDS block row: 64 slots + pad (136 B, conflict-free 8 B reads)
+// waves per SIMD: 3 (138 VGPRs, no spills) measured 2-6 % faster than 4 (128 VGPRs,
+// ~10 spilled) once the gather went branch-free (profiles/r05/decode_wpe/)
 #ifndef HIC_DEC_WPE
-#define HIC_DEC_WPE 4
+#define HIC_DEC_WPE 3
 #endif
 // The RGB of one 8x8 luma block (pixels px as idct_block_px leaves them) at block
 // (bi, bj) of an H x W image, H and W multiples of 8: pyrUp(Cr), pyrUp(Cb) of the

@@ -33,7 +33,7 @@ class RleJob16(ctypes.Structure):
     """hic_rle_job16 (include/hiccup_hip.h)."""
     _fields_ = [("blocks", _vp), ("nblk", _i64), ("d_stitch", _vp), ("dc_diff", _vp), ("sym_len", _vp),
                 ("sym_val", _vp), ("sym_cap", _i64), ("d_count", _vp), ("workspace", _vp), ("records_per_tile", _i64),
-                ("workspace_bytes", _i64)]
+                ("workspace_bytes", _i64), ("d_index", _vp)]
 
 
 class DctPlaneJob(ctypes.Structure):

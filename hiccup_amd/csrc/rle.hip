@@ -615,6 +615,7 @@ struct RleJob16 {
   int64_t rowb;
   int64_t tpr, rpr;  // tiles and records per row
   int64_t wsb;       // workspace bytes (0: not checked; a rows job must give it)
+  int64_t *index;    // optional tile index the emit writes (hic_rle_tile_index_i16's)
 };
 struct RleJobs16 {
   RleJob16 j[kMaxJobs];
@@ -853,6 +854,14 @@ __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
     const RleJob16 &J = jobs.j[job_of(g)];
     int64_t b0, bend, r0;
     geo(J, g - J.tile0, b0, bend, r0);
+    // the tile index (hic_rle_tile_index_i16's words, from the values fetched for
+    // this tile: its first record's offsets, the DC of the block before it)
+    if (J.index && lane == 0) {
+      int64_t *ix = J.index + 3 * (g - J.tile0);
+      ix[0] = cur.off;
+      ix[1] = cur.prev;
+      ix[2] = cur.pdc;
+    }
     const int64_t b = b0 + lane;
     const bool valid = b < bend;
 #if HIC_EMIT_COAL
@@ -1684,9 +1693,10 @@ extern "C" int hic_rle_encode_i16_tiles_batch(int n, const hic_rle_job16 *jobs, 
     if (reinterpret_cast<uintptr_t>(a.blocks) & 15) return arg_error("job %d: blocks must be 16-byte aligned", k);
     if (a.records_per_tile != 0 && a.records_per_tile != 1 && a.records_per_tile != 2)
       return arg_error("job %d: records_per_tile must be 1 or 2", k);
+    if (a.d_index && a.d_stitch) return arg_error("job %d: d_index needs a job without d_stitch", k);
     J.j[k] = RleJob16{a.blocks, a.nblk, a.d_stitch, a.dc_diff, a.sym_len, a.sym_val, a.sym_cap, a.d_count,
                       static_cast<int64_t *>(a.workspace), 0, 0, 0, a.records_per_tile == 2 ? 1 : 0, 0, 0, 0,
-                      a.workspace_bytes};
+                      a.workspace_bytes, a.d_index};
   }
   return encode_batch16(J, as_stream(stream));
 }
@@ -1708,6 +1718,7 @@ extern "C" int hic_rle_encode_i16_rows_batch(int n, const hic_rle_job16 *jobs, c
       return arg_error("job %d: records_per_tile must be 1 or 2", k);
     const int64_t rb = h_row_blocks[k];
     if (rb < 1 || a.nblk % rb) return arg_error("job %d: row_blocks must divide nblk", k);
+    if (a.d_index) return arg_error("job %d: d_index is for hic_rle_encode_i16_tiles_batch", k);
     J.j[k] = RleJob16{a.blocks, a.nblk, a.d_stitch, a.dc_diff, a.sym_len, a.sym_val, a.sym_cap, a.d_count,
                       static_cast<int64_t *>(a.workspace), 0, 0, 0, a.records_per_tile == 2 ? 1 : 0, rb, 0, 0,
                       a.workspace_bytes};

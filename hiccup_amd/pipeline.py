@@ -229,24 +229,23 @@ class Encoder:
             rowb = (ctypes.c_int64 * 3)(self.W // 8, self.W // 16, self.W // 16)
             _lib.call("hic_rle_encode_i16_rows_batch", 3, self._rle_jobs(stitch), rowb, self.max_len, s)
         else:
-            _lib.call("hic_rle_encode_i16_tiles_batch", 3, self._rle_jobs(stitch), self.max_len, s)
-        if self.index is not None and stitch is None:
-            for k in CHANNELS:
-                _lib.call("hic_rle_tile_index_i16", device.ptr(self.coef[k]), self.coef[k].shape[0], self.rpt[k],
-                          device.ptr(self.ws[k]), device.ptr(self.index[k]), s)
+            # with a tile index wanted, the emit writes it too (hic_rle_job16.d_index:
+            # hic_rle_tile_index_i16's words, no launch of its own)
+            _lib.call("hic_rle_encode_i16_tiles_batch", 3, self._rle_jobs(stitch, index=True), self.max_len, s)
 
     def encode(self, rgb, stream=None, dct_events=None):
         self.transform(rgb, stream, dct_events=dct_events)
         self.entropy(stream)
 
-    def _rle_jobs(self, stitch):
+    def _rle_jobs(self, stitch, index=False):
         jobs = (_lib.RleJob16 * 3)()
         for i, k in enumerate(CHANNELS):
+            ix = self.index[k].data_ptr() if index and self.index is not None and stitch is None else None
             jobs[i] = _lib.RleJob16(self.coef[k].data_ptr(), self.coef[k].shape[0],
                                     stitch[i].data_ptr() if stitch is not None else None, self.dc[k].data_ptr(),
                                     self.sym_len[k].data_ptr(), self.sym_val[k].data_ptr(), self.cap[k],
                                     self.counts[i:i + 1].data_ptr(), self.ws[k].data_ptr(), self.rpt[k],
-                                    self.ws_bytes[k])
+                                    self.ws_bytes[k], ix)
         return jobs
 
     def hic_image(self, stream=None):

@@ -299,6 +299,10 @@ typedef struct {
                                2: one per 32 blocks (hic_encode420_u8's chroma planes) */
   int64_t workspace_bytes;  /* size of `workspace` (round 5): checked against the job's
                                records when > 0; required by hic_rle_encode_i16_rows_batch */
+  int64_t *d_index;         /* optional (round 5), hic_rle_encode_i16_tiles_batch only, no
+                               d_stitch: the emit also writes the job's tile index, exactly
+                               what hic_rle_tile_index_i16 writes ((nblk+63)/64 x 3 int64),
+                               with no launch of its own; NULL: none */
 } hic_rle_job16;
 int hic_rle_encode_i16_tiles_batch(int n, const hic_rle_job16 *jobs, int max_len, void *stream);
 /* The same over records per row segment (round 4; hic_encode420_seg_u8's records):

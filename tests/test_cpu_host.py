@@ -63,6 +63,29 @@ def test_last_error_roundtrip():
         _lib.check(rc, "x")
 
 
+def test_ctypes_structs_match_header(tmp_path):
+    """The job structs' ctypes mirrors (_lib.RleJob16, _lib.DctPlaneJob) have the
+    header's size and field offsets, as gcc lays them out."""
+    import subprocess
+    structs = {"hic_rle_job16": _lib.RleJob16, "hic_dct_plane_job": _lib.DctPlaneJob}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "hiccup_hip.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append('  printf("%s size %%zu\\n", sizeof(%s));' % (cname, cname))
+        for f, _ in py._fields_:
+            lines.append('  printf("%s %s %%zu\\n", offsetof(%s, %s));' % (cname, f, cname, f))
+    lines.append("  return 0;\n}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(l.rsplit(" ", 1) for l in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                         text=True).stdout.splitlines())
+    for cname, py in structs.items():
+        assert int(got["%s size" % cname]) == ctypes.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert int(got["%s %s" % (cname, f)]) == getattr(py, f).offset, (cname, f)
+
+
 def test_decode_rgb_indexed_arguments():
     """hic_rle_decode_idct_rgb_indexed refuses what its kernel cannot take before
     any device call: null pointers, planes that are not whole 8x8 blocks, a short or

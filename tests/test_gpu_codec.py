@@ -342,6 +342,12 @@ def test_indexed_decode(H, W, kind):
     enc = pipeline.Encoder(H, W, index=True)
     enc.encode(device.to_device(rgb))
     counts = enc.counts.cpu().tolist()
+    # the index the emit wrote (hic_rle_job16.d_index) == hic_rle_tile_index_i16's
+    for k in pipeline.CHANNELS:
+        ix = torch.full_like(enc.index[k], -5)
+        _lib.call("hic_rle_tile_index_i16", device.ptr(enc.coef[k]), enc.coef[k].shape[0], enc.rpt[k],
+                  device.ptr(enc.ws[k]), device.ptr(ix), device.stream_ptr())
+        assert torch.equal(ix, enc.index[k]), k
     d1, d2, d3 = pipeline.Decoder(H, W), pipeline.Decoder(H, W), pipeline.Decoder(H, W)
     r1 = d1.decode(enc.sym_len, enc.sym_val, counts, enc.dc)
     r2 = d2.decode(enc.sym_len, enc.sym_val, enc.counts, enc.dc, index=enc.index, keep_blocks=True)

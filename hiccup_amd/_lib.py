@@ -64,6 +64,7 @@ SIGNATURES = {
     "hic_huffman_pack_workspace_bytes": (_sz, [_i64]),
     "hic_wire_bytes": (_sz, [_i64, _int]),
     "hic_rle_decode_idct_u8_indexed": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _int, _vp, _i64, _vp, _vp]),
+    "hic_rle_decode_idct_u8_indexed_pair": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _int, _vp, _i64, _vp, _vp]),
     "hic_rle_decode_idct_rgb_indexed": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _vp, _vp]),
     "hic_rle_tile_index_i16": (_int, [_vp, _i64, _int, _vp, _vp, _vp]),
     "hic_rle_decode_i16_indexed": (_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp]),

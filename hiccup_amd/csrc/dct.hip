@@ -413,22 +413,47 @@ __device__ __forceinline__ void colour_block(const uint32_t (&px)[16], int bi, i
 // the RGB image instead of to a Y plane -- the Y plane never reaches HBM
 // (jpeg_decompression's decode of the luma channel + pyrUp + cvtColor, with the
 // chroma planes decoded before).
+// A second plane of the same shape and table (Cb beside Cr): the launch covers both
+// planes' tiles, so the two share one tail (hic_rle_decode_idct_u8_indexed_pair).
+struct DecPlane {
+  const uint8_t *sym_len;
+  const int16_t *sym_val;
+  const int64_t *d_nsym;
+  const int32_t *dc_diff;
+  const int64_t *index;
+  uint8_t *out;
+  int64_t *d_status;
+};
 template <int TABLE, bool FAST, bool RGB = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DEC_WPE))) void k_rld_idct_indexed(const uint8_t *__restrict__ sym_len,
-                                                          const int16_t *__restrict__ sym_val,
-                                                          const int64_t *__restrict__ d_nsym,
-                                                          const int32_t *__restrict__ dc_diff,
-                                                          const int64_t *__restrict__ index, int H, int W, int nbx,
-                                                          int64_t nblk, uint8_t *__restrict__ out, int64_t ostride,
-                                                          int64_t *__restrict__ d_status,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DEC_WPE))) void k_rld_idct_indexed(const uint8_t *__restrict__ sym_len_a,
+                                                          const int16_t *__restrict__ sym_val_a,
+                                                          const int64_t *__restrict__ d_nsym_a,
+                                                          const int32_t *__restrict__ dc_diff_a,
+                                                          const int64_t *__restrict__ index_a, int H, int W, int nbx,
+                                                          int64_t nblk, uint8_t *__restrict__ out_a, int64_t ostride,
+                                                          int64_t *__restrict__ d_status_a,
                                                           const uint8_t *__restrict__ cr = nullptr,
-                                                          const uint8_t *__restrict__ cb = nullptr) {
+                                                          const uint8_t *__restrict__ cb = nullptr,
+                                                          DecPlane second = DecPlane{}) {
   static_assert(!RGB || (TABLE == 0 && FAST), "the RGB form decodes whole-block luma planes");
   __shared__ uint2 s_tile[4][64 * kRowI16 / 4];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t ntiles = (nblk + 63) / 64;
-  const int64_t t = (int64_t)blockIdx.x * 4 + wv;
-  if (t >= ntiles) return;  // wave-uniform
+  int64_t t = (int64_t)blockIdx.x * 4 + wv;
+  const bool b = !RGB && t >= ntiles;  // wave-uniform: the second plane's tile t - ntiles
+  if (b) {
+    if (!second.sym_len || t >= 2 * ntiles) return;
+    t -= ntiles;
+  } else if (t >= ntiles) {
+    return;
+  }
+  const uint8_t *__restrict__ sym_len = b ? second.sym_len : sym_len_a;
+  const int16_t *__restrict__ sym_val = b ? second.sym_val : sym_val_a;
+  const int64_t *__restrict__ d_nsym = b ? second.d_nsym : d_nsym_a;
+  const int32_t *__restrict__ dc_diff = b ? second.dc_diff : dc_diff_a;
+  const int64_t *__restrict__ index = b ? second.index : index_a;
+  uint8_t *__restrict__ out = b ? second.out : out_a;
+  int64_t *__restrict__ d_status = b ? second.d_status : d_status_a;
   uint2 *tile = s_tile[wv];
   int16_t *win = reinterpret_cast<int16_t *>(tile);
   const int64_t nsym_raw = *d_nsym, nsym = nsym_raw > 0 ? nsym_raw : 0;
@@ -1004,6 +1029,42 @@ extern "C" int hic_rle_decode_idct_u8_indexed(const uint8_t *sym_len, const int1
   else HIC_RI(1, false);
 #undef HIC_RI
   return check_launch("k_rld_idct_indexed");
+}
+
+extern "C" int hic_rle_decode_idct_u8_indexed_pair(const uint8_t *const *h_sym_len, const int16_t *const *h_sym_val,
+                                                   const int64_t *const *h_d_nsym, const int32_t *const *h_dc_diff,
+                                                   const int64_t *const *h_d_index, int64_t H, int64_t W, int table_id,
+                                                   uint8_t *const *h_out, int64_t out_stride, int64_t *const *h_d_status,
+                                                   void *stream) {
+  if (!h_sym_len || !h_sym_val || !h_d_nsym || !h_dc_diff || !h_d_index || !h_out || !h_d_status)
+    return arg_error("null pointer");
+  for (int k = 0; k < 2; ++k) {
+    if (!h_sym_len[k] || !h_sym_val[k] || !h_d_nsym[k] || !h_dc_diff[k] || !h_d_index[k] || !h_out[k] ||
+        !h_d_status[k])
+      return arg_error("plane %d: null pointer", k);
+    if ((reinterpret_cast<uintptr_t>(h_sym_len[k]) | reinterpret_cast<uintptr_t>(h_sym_val[k])) % 16)
+      return arg_error("plane %d: symbol arrays must be 16-byte aligned", k);
+  }
+  if (!dims_ok(H, W) || out_stride < W) return arg_error("plane shape / stride");
+  if (table_id != HIC_TABLE_LUMINANCE && table_id != HIC_TABLE_CHROMINANCE) return arg_error("table_id");
+  const int nbx = (int)((W + 7) / 8);
+  const int64_t nblk = (int64_t)nbx * ((H + 7) / 8);
+  if (nblk * 63 >= ((int64_t)1 << 31)) return arg_error("plane too large (AC stream >= 2^31)");
+  const bool fast = H % 8 == 0 && W % 8 == 0 && out_stride % 8 == 0 && aligned(h_out[0], 8) && aligned(h_out[1], 8);
+  const int64_t ntiles = (nblk + 63) / 64;
+  const dim3 grid((unsigned)((2 * ntiles + 3) / 4)), block(256);
+  hipStream_t s = as_stream(stream);
+  const DecPlane p1{h_sym_len[1], h_sym_val[1], h_d_nsym[1], h_dc_diff[1], h_d_index[1], h_out[1], h_d_status[1]};
+#define HIC_RI2(T, F)                                                                                              \
+  hipLaunchKernelGGL((k_rld_idct_indexed<T, F>), grid, block, 0, s, h_sym_len[0], h_sym_val[0], h_d_nsym[0],     \
+                     h_dc_diff[0], h_d_index[0], (int)H, (int)W, nbx, nblk, h_out[0], out_stride, h_d_status[0], \
+                     nullptr, nullptr, p1)
+  if (table_id == 0 && fast) HIC_RI2(0, true);
+  else if (table_id == 0) HIC_RI2(0, false);
+  else if (fast) HIC_RI2(1, true);
+  else HIC_RI2(1, false);
+#undef HIC_RI2
+  return check_launch("k_rld_idct_indexed<pair>");
 }
 
 extern "C" int hic_rle_decode_idct_rgb_indexed(const uint8_t *sym_len, const int16_t *sym_val, const int64_t *d_nsym,

@@ -296,9 +296,12 @@ class Encoder:
 class Decoder:
     """Inverse chain: symbols -> zig-zag blocks -> pixels -> RGB (2h x 2w x 3)."""
 
-    def __init__(self, H, W):
+    def __init__(self, H, W, chroma_pair=True):
+        """chroma_pair: the indexed decode's Cr and Cb in one launch
+        (hic_rle_decode_idct_u8_indexed_pair); False: one launch each."""
         device.require_gpu()
         self.H, self.W = H, W
+        self.chroma_pair = chroma_pair
         self.shapes = {"lum": (H, W), "cr": (H // 2, W // 2), "cb": (H // 2, W // 2)}
         self.blocks, self.pix, self.status = {}, {}, device.zeros((3,), torch.int64)
         for k in CHANNELS:
@@ -322,12 +325,21 @@ class Decoder:
         s = device.stream_ptr(stream)
         lib = _lib.load()
         if index is not None and not keep_blocks and not planes and self.H % 8 == 0 and self.W % 8 == 0:
-            for i, k in ((1, "cr"), (2, "cb")):
-                h, w = self.shapes[k]
-                _lib.call("hic_rle_decode_idct_u8_indexed", device.ptr(sym_len[k]), device.ptr(sym_val[k]),
-                          ctypes.c_void_p(counts.data_ptr() + 8 * i), device.ptr(dc[k]), device.ptr(index[k]), h, w,
-                          TABLES[k], device.ptr(self.pix[k]), self.pix[k].stride(0),
-                          device.ptr(self.status[i:i + 1]), s)
+            # Cr and Cb in one launch (one tail), then Y straight to RGB
+            h, w = self.shapes["cr"]
+            if self.chroma_pair:
+                pair = lambda f: (ctypes.c_void_p * 2)(*(f(i, k) for i, k in ((1, "cr"), (2, "cb"))))
+                _lib.call("hic_rle_decode_idct_u8_indexed_pair", pair(lambda i, k: sym_len[k].data_ptr()),
+                          pair(lambda i, k: sym_val[k].data_ptr()), pair(lambda i, k: counts.data_ptr() + 8 * i),
+                          pair(lambda i, k: dc[k].data_ptr()), pair(lambda i, k: index[k].data_ptr()), h, w,
+                          TABLES["cr"], pair(lambda i, k: self.pix[k].data_ptr()), self.pix["cr"].stride(0),
+                          pair(lambda i, k: self.status[i:i + 1].data_ptr()), s)
+            else:
+                for i, k in ((1, "cr"), (2, "cb")):
+                    _lib.call("hic_rle_decode_idct_u8_indexed", device.ptr(sym_len[k]), device.ptr(sym_val[k]),
+                              ctypes.c_void_p(counts.data_ptr() + 8 * i), device.ptr(dc[k]), device.ptr(index[k]),
+                              h, w, TABLES[k], device.ptr(self.pix[k]), self.pix[k].stride(0),
+                              device.ptr(self.status[i:i + 1]), s)
             _lib.call("hic_rle_decode_idct_rgb_indexed", device.ptr(sym_len["lum"]), device.ptr(sym_val["lum"]),
                       ctypes.c_void_p(counts.data_ptr()), device.ptr(dc["lum"]), device.ptr(index["lum"]), self.H,
                       self.W, device.ptr(self.pix["cr"]), device.ptr(self.pix["cb"]), device.ptr(self.rgb),

@@ -375,6 +375,15 @@ int hic_rle_decode_idct_u8_indexed(const uint8_t *sym_len, const int16_t *sym_va
                                    const int32_t *dc_diff, const int64_t *d_index, int64_t H, int64_t W,
                                    int table_id, uint8_t *out, int64_t out_stride, int64_t *d_status,
                                    void *stream);
+/* Two planes of the same shape and table (Cr and Cb of one image) through
+ * hic_rle_decode_idct_u8_indexed in ONE launch, so the two share one tail.  Every
+ * h_ argument is a host array of 2 device pointers (plane 0, plane 1); the rest as
+ * hic_rle_decode_idct_u8_indexed, for both planes. */
+int hic_rle_decode_idct_u8_indexed_pair(const uint8_t *const *h_sym_len, const int16_t *const *h_sym_val,
+                                        const int64_t *const *h_d_nsym, const int32_t *const *h_dc_diff,
+                                        const int64_t *const *h_d_index, int64_t H, int64_t W, int table_id,
+                                        uint8_t *const *h_out, int64_t out_stride, int64_t *const *h_d_status,
+                                        void *stream);
 /* The luminance plane's hic_rle_decode_idct_u8_indexed fused with
  * hic_ycrcb420_to_rgb (compression.jpeg_decompression, compression.py:48-56: the
  * Y channel's decode + inv_dct_channel, pyrUp(Cr), pyrUp(Cb), cvtColor YCrCb2RGB):

@@ -104,6 +104,22 @@ def test_decode_rgb_indexed_arguments():
     assert "aligned" in _lib.last_error()
 
 
+def test_decode_pair_indexed_arguments():
+    """hic_rle_decode_idct_u8_indexed_pair checks both planes' pointers before any
+    device call."""
+    lib = _lib.load()
+    p16 = ctypes.c_void_p(1 << 20)  # never dereferenced
+    two = lambda a=p16, b=p16: (ctypes.c_void_p * 2)(a, b)
+    ok = lambda **kw: [kw.get("L", two()), two(), two(), two(), two(), 64, 64, 1, two(), 64, two(), None]
+    assert lib.hic_rle_decode_idct_u8_indexed_pair(*ok(L=two(b=None))) == _lib.HIC_ERR_ARG
+    assert "plane 1: null pointer" in _lib.last_error()
+    assert lib.hic_rle_decode_idct_u8_indexed_pair(*ok(L=two(b=ctypes.c_void_p((1 << 20) + 8)))) == _lib.HIC_ERR_ARG
+    assert "16-byte aligned" in _lib.last_error()
+    bad_table = ok()
+    bad_table[7] = 5
+    assert lib.hic_rle_decode_idct_u8_indexed_pair(*bad_table) == _lib.HIC_ERR_ARG
+
+
 def test_knob_defaults_and_ranges():
     """The launch defaults the measurements chose (hic_get_knob reports the effective
     value; no GPU call): encode_order 6 = XCD-major workgroups + odd unit rows

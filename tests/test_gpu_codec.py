@@ -376,6 +376,11 @@ def test_indexed_decode(H, W, kind):
     assert d4.status.cpu().tolist() == want
     assert torch.equal(r1, r4)
     assert bool(d4.pix["lum"].any()) == (H % 8 != 0 or W % 8 != 0)  # which path ran
+    # Cr and Cb in one launch (the default) or one launch each: the same
+    d5 = pipeline.Decoder(H, W, chroma_pair=False)
+    assert torch.equal(d5.decode(enc.sym_len, enc.sym_val, enc.counts, enc.dc, index=enc.index), r1)
+    for k in ("cr", "cb"):
+        assert torch.equal(d5.pix[k], d4.pix[k]), k
 
 
 @pytest.mark.parametrize("mode", ["rgb", "planes", "blocks"])

@@ -80,6 +80,9 @@ def parse():
                          "pairs, profiles/r03/s2/streams/), 2 with N > 1 ranks")
     ap.add_argument("--unfused", action="store_true",
                     help="A/B: colour and DCT as two kernels (the planes round-trip HBM) instead of hic_encode420_u8")
+    ap.add_argument("--no-slots", action="store_true",
+                    help="A/B: the coefficient chain (fused kernel writes int16 coefficients, scan + emit kernels) "
+                         "instead of the slot layout (the fused kernel writes the symbols, one closing scan)")
     ap.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
                     help="A/B: set a library knob (hiccup_amd._lib.KNOBS; every knob is bit-exact)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -853,7 +856,8 @@ def main():
                                                fused=False if args.unfused else None)
     else:
         H = H0
-        make = lambda j: pipeline.Encoder(H0, W0, fused=False if args.unfused else None)  # noqa: E731
+        make = lambda j: pipeline.Encoder(H0, W0, fused=False if args.unfused else None,  # noqa: E731
+                                          slots=False if (args.no_slots or args.unfused) else None)
     encs = [make(j) for j in range(n_enc)]  # rotate outputs too (~1.2 GB per 4)
     span = encs[0].span if world > 1 else (0, H)
     in_rows = span[1] - span[0]

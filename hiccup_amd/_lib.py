@@ -36,6 +36,13 @@ class RleJob16(ctypes.Structure):
                 ("workspace_bytes", _i64), ("d_index", _vp)]
 
 
+class SlotJob(ctypes.Structure):
+    """hic_slot_job (include/hiccup_hip.h): one channel of the slot-layout encode."""
+    _fields_ = [("nblk", _i64), ("records_per_tile", _i64), ("slot_len", _vp), ("slot_val", _vp), ("dc_diff", _vp),
+                ("d_index", _vp), ("workspace", _vp), ("workspace_bytes", _i64), ("d_count", _vp), ("sym_len", _vp),
+                ("sym_val", _vp), ("sym_cap", _i64)]
+
+
 class DctPlaneJob(ctypes.Structure):
     """hic_dct_plane_job (include/hiccup_hip.h)."""
     _fields_ = [("plane", _vp), ("H", _i64), ("W", _i64), ("stride", _i64), ("table_id", _int), ("out", _vp),
@@ -82,6 +89,16 @@ SIGNATURES = {
     "hic_encode420_seg_u8": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64,
                                     _i64, _int, _vp, _vp, _vp]),
     "hic_rle_encode_i16_rows_batch": (_int, [_int, _vp, _vp, _int, _vp]),
+    "hic_rle_slots_workspace_bytes": (_sz, [_i64, _int]),
+    "hic_encode420_slots_u8": (_int, [_vp, _i64, _i64, _vp, _int, _vp, _vp, _vp]),
+    "hic_rle_slots_close": (_int, [_int, _vp, _int, _vp]),
+    "hic_rle_slots_compact": (_int, [_int, _vp, _int, _vp]),
+    "hic_rle_decode_i16_slots": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _vp, _vp, _vp, _vp]),
+    "hic_rle_decode_idct_u8_slots": (_int, [_vp, _vp, _vp, _vp, _vp, _int, _i64, _i64, _int, _vp, _i64, _vp, _vp]),
+    "hic_rle_decode_idct_u8_slots_pair": (_int, [_vp, _vp, _vp, _vp, _vp, _int, _i64, _i64, _int, _vp, _i64, _vp,
+                                                 _vp]),
+    "hic_rle_decode_idct_rgb_slots": (_int, [_vp, _vp, _vp, _vp, _vp, _int, _i64, _i64, _vp, _vp, _vp, _i64, _vp,
+                                             _vp]),
     "hic_event_create": (_int, [_vp]),
     "hic_event_destroy": (_int, [_vp]),
     "hic_event_elapsed_ms": (_int, [_vp, _vp, _vp]),

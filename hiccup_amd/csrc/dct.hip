@@ -424,7 +424,9 @@ struct DecPlane {
   uint8_t *out;
   int64_t *d_status;
 };
-template <int TABLE, bool FAST, bool RGB = false>
+// SLOTS: the symbols in the slot layout (slots.h), `index` the close's int32 record
+// index, rsh = log2 records per 64-block tile.
+template <int TABLE, bool FAST, bool RGB = false, bool SLOTS = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DEC_WPE))) void k_rld_idct_indexed(const uint8_t *__restrict__ sym_len_a,
                                                           const int16_t *__restrict__ sym_val_a,
                                                           const int64_t *__restrict__ d_nsym_a,
@@ -434,7 +436,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DEC_WPE
                                                           int64_t *__restrict__ d_status_a,
                                                           const uint8_t *__restrict__ cr = nullptr,
                                                           const uint8_t *__restrict__ cb = nullptr,
-                                                          DecPlane second = DecPlane{}) {
+                                                          DecPlane second = DecPlane{}, int rsh = 0) {
   static_assert(!RGB || (TABLE == 0 && FAST), "the RGB form decodes whole-block luma planes");
   __shared__ uint2 s_tile[4][64 * kRowI16 / 4];
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -459,22 +461,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DEC_WPE
   const int64_t nsym_raw = *d_nsym, nsym = nsym_raw > 0 ? nsym_raw : 0;
   for (int i = lane; i < 64 * kRowI16 / 4; i += 64) tile[i] = make_uint2(0, 0);
   __builtin_amdgcn_wave_barrier();
-  const int64_t o0 = index[3 * t] < nsym ? index[3 * t] : nsym;
-  const int64_t o1 = t + 1 < ntiles ? (index[3 * (t + 1)] < nsym ? index[3 * (t + 1)] : nsym) : nsym;
   const int64_t tb0 = t * 64 * 63;
   const int nvb = (int)(nblk - t * 64 < 64 ? nblk - t * 64 : 64);
   const int span = nvb * 63;
   // the symbols of the tile into its LDS rows (trash: the lane's row's first pad slot)
-  const int P = gather_tile<kRowI16, HIC_DEC_G, HIC_DEC_PF>(sym_len, sym_val, o0, o1, nsym, (int)(index[3 * t + 1] + 1 - tb0),
-                                                span, win, lane * kRowI16 + 64, lane);
+  int P, pdc;
+  if constexpr (SLOTS) {
+    const int32_t *sidx = reinterpret_cast<const int32_t *>(index);
+    P = slots_gather_tile<kRowI16>(sym_len, sym_val, sidx, t, rsh, nblk, span, win, lane * kRowI16 + 64, lane);
+    pdc = sidx[4 * (t << rsh) + 2];
+  } else {
+    const int64_t o0 = index[3 * t] < nsym ? index[3 * t] : nsym;
+    const int64_t o1 = t + 1 < ntiles ? (index[3 * (t + 1)] < nsym ? index[3 * (t + 1)] : nsym) : nsym;
+    P = gather_tile<kRowI16, HIC_DEC_G, HIC_DEC_PF>(sym_len, sym_val, o0, o1, nsym, (int)(index[3 * t + 1] + 1 - tb0),
+                                                    span, win, lane * kRowI16 + 64, lane);
+    pdc = (int)index[3 * t + 2];
+  }
   const int64_t blk = t * 64 + lane;
   const int d = lane < nvb ? dc_diff[blk] : 0;
-  win[lane * kRowI16] = (int16_t)(index[3 * t + 2] + wave_incl_sum_i32(d));
+  win[lane * kRowI16] = (int16_t)(pdc + wave_incl_sum_i32(d));
   __builtin_amdgcn_wave_barrier();
   if (t == ntiles - 1 && lane == 0) {
+    // (a slot-layout stream is whole by construction: its EOB zero-fills the rest)
     const int64_t total = tb0 + (int64_t)P, n_ac = nblk * 63;
-    const bool eob = nsym > 0 && sym_len[nsym - 1] == 0 && sym_val[nsym - 1] == 0;
-    *d_status = nsym_raw < 1 ? -1 : ((eob && total <= n_ac) ? n_ac : total);
+    const bool eob = SLOTS || (nsym > 0 && sym_len[nsym - 1] == 0 && sym_val[nsym - 1] == 0);
+    *d_status = nsym_raw < 1 ? -1 : ((eob && (SLOTS || total <= n_ac)) ? n_ac : total);
   }
   if (!RGB && lane >= nvb) return;
   int qv[64];  // raster [u][v]
@@ -1086,6 +1097,102 @@ extern "C" int hic_rle_decode_idct_rgb_indexed(const uint8_t *sym_len, const int
                      as_stream(stream), sym_len, sym_val, d_nsym, dc_diff, d_index, (int)H, (int)W, nbx, nblk, rgb,
                      rgb_stride, d_status, cr, cb);
   return check_launch("k_rld_idct_indexed<rgb>");
+}
+
+// ---- the slot-layout decoders (slots.h): the *_indexed entry points above, reading
+// the slots through the close's record index
+static int slots_args(const void *slot_len, const void *slot_val, int records_per_tile, int64_t nblk) {
+  if (records_per_tile != 1 && records_per_tile != 2) return arg_error("records_per_tile must be 1 or 2");
+  if (nblk % (64 / records_per_tile)) return arg_error("the plane's blocks must form whole records");
+  if ((reinterpret_cast<uintptr_t>(slot_len) | reinterpret_cast<uintptr_t>(slot_val)) % 16)
+    return arg_error("slot arrays must be 16-byte aligned");
+  return HIC_OK;
+}
+
+extern "C" int hic_rle_decode_idct_u8_slots(const uint8_t *slot_len, const int16_t *slot_val, const int64_t *d_nsym,
+                                            const int32_t *dc_diff, const int32_t *d_index, int records_per_tile,
+                                            int64_t H, int64_t W, int table_id, uint8_t *out, int64_t out_stride,
+                                            int64_t *d_status, void *stream) {
+  if (!slot_len || !slot_val || !d_nsym || !dc_diff || !d_index || !out || !d_status) return arg_error("null pointer");
+  if (!dims_ok(H, W) || out_stride < W) return arg_error("plane shape / stride");
+  if (table_id != HIC_TABLE_LUMINANCE && table_id != HIC_TABLE_CHROMINANCE) return arg_error("table_id");
+  const int nbx = (int)((W + 7) / 8);
+  const int64_t nblk = (int64_t)nbx * ((H + 7) / 8);
+  if (nblk * 63 >= ((int64_t)1 << 31)) return arg_error("plane too large (AC stream >= 2^31)");
+  if (int e = slots_args(slot_len, slot_val, records_per_tile, nblk)) return e;
+  const bool fast = H % 8 == 0 && W % 8 == 0 && out_stride % 8 == 0 && aligned(out, 8);
+  const int64_t ntiles = (nblk + 63) / 64;
+  const dim3 grid((unsigned)((ntiles + 3) / 4)), block(256);
+  hipStream_t s = as_stream(stream);
+  const int h = (int)H, w = (int)W, rsh = records_per_tile == 2 ? 1 : 0;
+  const int64_t *ix = reinterpret_cast<const int64_t *>(d_index);
+#define HIC_RS(T, F)                                                                                                \
+  hipLaunchKernelGGL((k_rld_idct_indexed<T, F, false, true>), grid, block, 0, s, slot_len, slot_val, d_nsym, dc_diff, \
+                     ix, h, w, nbx, nblk, out, out_stride, d_status, nullptr, nullptr, DecPlane{}, rsh)
+  if (table_id == 0 && fast) HIC_RS(0, true);
+  else if (table_id == 0) HIC_RS(0, false);
+  else if (fast) HIC_RS(1, true);
+  else HIC_RS(1, false);
+#undef HIC_RS
+  return check_launch("k_rld_idct_indexed<slots>");
+}
+
+extern "C" int hic_rle_decode_idct_u8_slots_pair(const uint8_t *const *h_slot_len, const int16_t *const *h_slot_val,
+                                                 const int64_t *const *h_d_nsym, const int32_t *const *h_dc_diff,
+                                                 const int32_t *const *h_d_index, int records_per_tile, int64_t H,
+                                                 int64_t W, int table_id, uint8_t *const *h_out, int64_t out_stride,
+                                                 int64_t *const *h_d_status, void *stream) {
+  if (!h_slot_len || !h_slot_val || !h_d_nsym || !h_dc_diff || !h_d_index || !h_out || !h_d_status)
+    return arg_error("null pointer");
+  if (!dims_ok(H, W) || out_stride < W) return arg_error("plane shape / stride");
+  if (table_id != HIC_TABLE_LUMINANCE && table_id != HIC_TABLE_CHROMINANCE) return arg_error("table_id");
+  const int nbx = (int)((W + 7) / 8);
+  const int64_t nblk = (int64_t)nbx * ((H + 7) / 8);
+  if (nblk * 63 >= ((int64_t)1 << 31)) return arg_error("plane too large (AC stream >= 2^31)");
+  for (int k = 0; k < 2; ++k) {
+    if (!h_slot_len[k] || !h_slot_val[k] || !h_d_nsym[k] || !h_dc_diff[k] || !h_d_index[k] || !h_out[k] ||
+        !h_d_status[k])
+      return arg_error("plane %d: null pointer", k);
+    if (int e = slots_args(h_slot_len[k], h_slot_val[k], records_per_tile, nblk)) return e;
+  }
+  const bool fast = H % 8 == 0 && W % 8 == 0 && out_stride % 8 == 0 && aligned(h_out[0], 8) && aligned(h_out[1], 8);
+  const int64_t ntiles = (nblk + 63) / 64;
+  const dim3 grid((unsigned)((2 * ntiles + 3) / 4)), block(256);
+  hipStream_t s = as_stream(stream);
+  const int rsh = records_per_tile == 2 ? 1 : 0;
+  const DecPlane p1{h_slot_len[1], h_slot_val[1], h_d_nsym[1], h_dc_diff[1],
+                    reinterpret_cast<const int64_t *>(h_d_index[1]), h_out[1], h_d_status[1]};
+#define HIC_RS2(T, F)                                                                                              \
+  hipLaunchKernelGGL((k_rld_idct_indexed<T, F, false, true>), grid, block, 0, s, h_slot_len[0], h_slot_val[0],    \
+                     h_d_nsym[0], h_dc_diff[0], reinterpret_cast<const int64_t *>(h_d_index[0]), (int)H, (int)W, nbx, \
+                     nblk, h_out[0], out_stride, h_d_status[0], nullptr, nullptr, p1, rsh)
+  if (table_id == 0 && fast) HIC_RS2(0, true);
+  else if (table_id == 0) HIC_RS2(0, false);
+  else if (fast) HIC_RS2(1, true);
+  else HIC_RS2(1, false);
+#undef HIC_RS2
+  return check_launch("k_rld_idct_indexed<slots pair>");
+}
+
+extern "C" int hic_rle_decode_idct_rgb_slots(const uint8_t *slot_len, const int16_t *slot_val, const int64_t *d_nsym,
+                                             const int32_t *dc_diff, const int32_t *d_index, int records_per_tile,
+                                             int64_t H, int64_t W, const uint8_t *cr, const uint8_t *cb, uint8_t *rgb,
+                                             int64_t rgb_stride, int64_t *d_status, void *stream) {
+  if (!slot_len || !slot_val || !d_nsym || !dc_diff || !d_index || !cr || !cb || !rgb || !d_status)
+    return arg_error("null pointer");
+  if (!dims_ok(H, W) || H % 8 || W % 8) return arg_error("plane shape (H, W multiples of 8)");
+  if (rgb_stride < 3 * W || rgb_stride % 8 || !aligned(rgb, 8)) return arg_error("rgb stride / alignment (8 B)");
+  if (!aligned(cr, 4) || !aligned(cb, 4)) return arg_error("chroma planes must be 4-byte aligned");
+  const int nbx = (int)(W / 8);
+  const int64_t nblk = (int64_t)nbx * (H / 8);
+  if (nblk * 63 >= ((int64_t)1 << 31)) return arg_error("plane too large (AC stream >= 2^31)");
+  if (int e = slots_args(slot_len, slot_val, records_per_tile, nblk)) return e;
+  const int64_t ntiles = (nblk + 63) / 64;
+  hipLaunchKernelGGL((k_rld_idct_indexed<0, true, true, true>), dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0,
+                     as_stream(stream), slot_len, slot_val, d_nsym, dc_diff, reinterpret_cast<const int64_t *>(d_index),
+                     (int)H, (int)W, nbx, nblk, rgb, rgb_stride, d_status, cr, cb, DecPlane{},
+                     records_per_tile == 2 ? 1 : 0);
+  return check_launch("k_rld_idct_indexed<rgb slots>");
 }
 
 extern "C" int hic_dct2_f64(const double *in, int64_t nblk, double *out, void *stream) {

@@ -45,6 +45,7 @@
 #include "color_core.h"
 #include "dct_core.h"
 #include "rle_core.h"
+#include "slots.h"
 
 namespace hic {
 namespace {
@@ -59,6 +60,12 @@ struct Enc420 {
   int xcd;              // 1: workgroups remapped XCD-major (xcd_block)
   int alt;              // 1: odd unit rows run their colour rows bottom-up
   int wlast;            // pixel columns of the last strip (16 .. 512)
+  // slot layout (k_encode420<15, true>, hic_encode420_slots_u8; slots.h): per plane
+  // the symbol slots, the DC differences and the records' last DCs; coef unused
+  uint8_t *slen[3];
+  int16_t *sval[3];
+  int32_t *dc[3];
+  int32_t *rdc[3];
 };
 
 constexpr int kZZ = HIC_LAYOUT_ZIGZAG_I16;
@@ -96,12 +103,6 @@ __device__ __attribute__((noinline)) void enc_fix26_block(uint2 w0, uint2 w1, ui
 // exact in every case (fast AAN path; the rare tie sets fall back in place).
 template <int TABLE>
 __device__ __forceinline__ void enc_dct(uint2 (&w)[8], int16_t *st) {
-#if defined(HIC_DEV) && defined(HIC_ENC_DEV) && (HIC_ENC_DEV & 1)
-  // dev timing (results invalid): no DCT, the pixels go to the stage
-#pragma unroll
-  for (int r = 0; r < 8; ++r) reinterpret_cast<uint2 *>(st)[r] = w[r];
-  return;
-#endif
   bool t26 = false;
   const bool f = dct_block_aan<TABLE, kZZ>(w, st, &t26);
   if (__builtin_amdgcn_ballot_w64(f)) {
@@ -113,6 +114,9 @@ __device__ __forceinline__ void enc_dct(uint2 (&w)[8], int16_t *st) {
 
 #ifndef HIC_ENC_WPB
 #define HIC_ENC_WPB 4  // waves per workgroup
+#endif
+#ifndef HIC_ENC_LA3
+#define HIC_ENC_LA3 3  // colour rows' load lookahead
 #endif
 
 // 16 B chunk k of stage row b
@@ -424,10 +428,16 @@ struct EncColour {
 // again in round 5, with proven windows and a cooperative float64 redo: 70.5-74.9
 // vs 55.6-57.7 us, commit ae5c500), cached stores, the one-pass (look-back +
 // emission) variant and vertically stacked units.
-template <int TMF>
+//
+// SLOTS (TMF 15, whole images with W % 512 == 0; hic_encode420_slots_u8): each pass
+// emits its record's AC symbols and DC differences into the slot layout (slots.h)
+// instead of storing the int16 coefficients: no coefficient ever reaches HBM.
+template <int TMF, bool SLOTS = false>
 __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_eu(3))) void k_encode420(Enc420 E) {
+  static_assert(!SLOTS || TMF == kSlotM, "the slot layout packs 4-bit lengths (max_len 15)");
   __shared__ __attribute__((aligned(16))) uint2 s_stage[HIC_ENC_WPB * 64 * kStageU2];
   __shared__ uint32_t s_chroma_all[HIC_ENC_WPB][2 * 8 * 64];
+  __shared__ uint32_t s_dummy[SLOTS ? HIC_ENC_WPB * 64 : 1];  // slot_pass's per-lane dummy dwords
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint2 *st2 = s_stage + wv * 64 * kStageU2;
   uint32_t *s_chroma = s_chroma_all[wv];
@@ -453,6 +463,16 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
     enc_dct<0>(w, st);
     const int64_t b0 = (int64_t)(2 * u0 + br) * nbx + 64 * s;
     __builtin_amdgcn_wave_barrier();
+    if constexpr (SLOTS) {
+      uint32_t zw[32];
+      enc_stage_row(st2, fresh_lane(), zw);
+      const int64_t r = b0 >> 6;  // W % 512 == 0: block row segments are whole tiles
+      const SlotRec A{E.slen[0] + r * kSlotY, E.sval[0] + r * kSlotY, E.dc[0] + b0, E.rec[0] + r * 3, E.rdc[0] + r,
+                      b0 * 63};
+      slot_pass<false, true>(zw, st2, s_dummy + wv * 64 + lane, lane, A, A);
+      __builtin_amdgcn_sched_barrier(0);
+      return;
+    }
     int16_t *o = E.coef[0] + b0 * 64;
     enc_store(st2, fresh_lane(), o, o + 32 * 64, nb < 32 ? nb : 32, nb > 32 ? nb - 32 : 0);
     if (TMF >= 0 && E.rec[0]) {
@@ -478,6 +498,18 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
     enc_dct<1>(w, st);
     const int64_t b0 = (int64_t)u0 * nbxc + 32 * s;
     __builtin_amdgcn_wave_barrier();
+    if constexpr (SLOTS) {
+      uint32_t zw[32];
+      enc_stage_row(st2, fresh_lane(), zw);
+      const int64_t r = b0 >> 5;  // one record per 32-block half tile
+      const SlotRec A{E.slen[1] + r * kSlotC, E.sval[1] + r * kSlotC, E.dc[1] + b0, E.rec[1] + r * 3, E.rdc[1] + r,
+                      b0 * 63};
+      const SlotRec B{E.slen[2] + r * kSlotC, E.sval[2] + r * kSlotC, E.dc[2] + b0, E.rec[2] + r * 3, E.rdc[2] + r,
+                      b0 * 63};
+      slot_pass<true, false>(zw, st2, s_dummy + wv * 64 + lane, lane, A, B);
+      __builtin_amdgcn_sched_barrier(0);
+      return;
+    }
     enc_store(st2, fresh_lane(), E.coef[1] + b0 * 64, E.coef[2] + b0 * 64, nb >> 1, nb >> 1);
     if (TMF >= 0 && E.rec[1]) {
       uint32_t zw[32];
@@ -488,22 +520,11 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
-#if defined(HIC_DEV) && defined(HIC_ENC_DEV) && (HIC_ENC_DEV & 2)
-  // dev timing (results invalid): no colour stage, synthetic pixels
-#pragma unroll
-  for (int r = 0; r < 16; ++r) yq[r] = make_uint2(0x9E3779B1u * (lane + r + g), 0x85EBCA6Bu * (lane ^ r ^ g));
-#pragma unroll
-  for (int i = 0; i < 16; ++i) s_chroma[i * 64 + lane] = 0x01000193u * (lane + i + g);
-#else
-#ifndef HIC_ENC_LA3
-#define HIC_ENC_LA3 3  // load lookahead (rows)
-#endif
   EncColour<19, HIC_ENC_LA3, true> C;
   const bool rev = E.alt && (u0 & 1);  // wave-uniform
   C.init(E, y0, s, lane, nb, rev);
   C.rows(yq, s_chroma, rev);
   __builtin_amdgcn_sched_barrier(0);
-#endif
   y_blocks(0);
   y_blocks(1);
   c_blocks();
@@ -660,6 +681,62 @@ extern "C" int hic_encode420_seg_u8(const uint8_t *rgb_rows, int64_t in_row0, in
                                     int64_t ws_bytes_c, int max_len, void *stream, void *ev_start, void *ev_stop) {
   return encode420(rgb_rows, in_row0, in_rows, H, W, out_row0, out_rows, coef_y, coef_cr, coef_cb, ws_y, ws_cr, ws_cb,
                    max_len, stream, ev_start, ev_stop, true, ws_bytes_y, ws_bytes_c);
+}
+
+extern "C" int hic_encode420_slots_u8(const uint8_t *rgb, int64_t H, int64_t W, const hic_slot_job *jobs,
+                                      int max_len, void *stream, void *ev_start, void *ev_stop) {
+  if (!rgb || !jobs) return arg_error("null pointer");
+  if (max_len != kSlotM) return arg_error("the slot layout needs max_len 15");
+  if (H < 16 || W < 512 || H % 16 || W % 512 || H >= (1 << 20) || W >= (1 << 20))
+    return arg_error("hic_encode420_slots_u8 needs W %% 512 == 0 and H %% 16 == 0");
+  if (H * W * 3 > INT32_MAX) return arg_error("image exceeds 2 GiB (32-bit buffer offsets)");
+  if (reinterpret_cast<uintptr_t>(rgb) % 8) return arg_error("rgb must be 8-byte aligned");
+  const int64_t nblk[3] = {(H / 8) * (W / 8), (H / 16) * (W / 16), (H / 16) * (W / 16)};
+  const int rpt[3] = {1, 2, 2};
+  // validate every job before anything is launched
+  for (int k = 0; k < 3; ++k) {
+    const hic_slot_job &J = jobs[k];
+    if (!J.slot_len || !J.slot_val || !J.dc_diff || !J.workspace) return arg_error("job %d: null pointer", k);
+    if (J.nblk != nblk[k] || J.records_per_tile != rpt[k])
+      return arg_error("job %d: nblk %lld / records_per_tile %lld, expected %lld / %d", k, (long long)J.nblk,
+                       (long long)J.records_per_tile, (long long)nblk[k], rpt[k]);
+    if ((reinterpret_cast<uintptr_t>(J.slot_len) | reinterpret_cast<uintptr_t>(J.slot_val)) % 16)
+      return arg_error("job %d: slot arrays must be 16-byte aligned", k);
+    const int64_t need = (int64_t)hic_rle_slots_workspace_bytes(nblk[k], rpt[k]);
+    if (J.workspace_bytes < need)
+      return arg_error("job %d: workspace of %lld bytes, %lld needed", k, (long long)J.workspace_bytes,
+                       (long long)need);
+  }
+  Enc420 E{};
+  E.rgb = rgb;
+  E.in_row0 = 0;
+  E.in_rows = (int)H;
+  E.H = (int)H;
+  E.W = (int)W;
+  E.out_row0 = 0;
+  E.out_rows = (int)H;
+  for (int k = 0; k < 3; ++k) {
+    E.rec[k] = static_cast<int64_t *>(jobs[k].workspace);
+    E.slen[k] = jobs[k].slot_len;
+    E.sval[k] = jobs[k].slot_val;
+    E.dc[k] = jobs[k].dc_diff;
+    E.rdc[k] = reinterpret_cast<int32_t *>(E.rec[k] + slot_rdc_word(slot_nrec(nblk[k], rpt[k])));
+  }
+  E.M = kSlotM;
+  E.nstrips = (int)(W / 512);
+  E.wlast = 512;
+  E.nunits = E.nstrips * (int)(H / 16);
+  const int order = knob(HIC_KNOB_ENCODE_ORDER);
+  E.xcd = (order >> 1) & 1;
+  E.alt = (order >> 2) & 1;
+  const dim3 grid((unsigned)((E.nunits + HIC_ENC_WPB - 1) / HIC_ENC_WPB)), block(64 * HIC_ENC_WPB);
+  const hipStream_t s = as_stream(stream);
+  const hipEvent_t e0 = static_cast<hipEvent_t>(ev_start), e1 = static_cast<hipEvent_t>(ev_stop);
+  if (e0 || e1)
+    hipExtLaunchKernelGGL((k_encode420<kSlotM, true>), grid, block, 0, s, e0, e1, 0, E);
+  else
+    hipLaunchKernelGGL((k_encode420<kSlotM, true>), grid, block, 0, s, E);
+  return check_launch("k_encode420<slots>");
 }
 
 extern "C" int hic_probe_encode420(const uint8_t *rgb, int64_t H, int64_t W, int16_t *coef_y, int16_t *coef_cr,

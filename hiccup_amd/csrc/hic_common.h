@@ -74,5 +74,12 @@ uint32_t next_epoch();
 // Cross-file launchers (rle.hip): the hot-path RLE tile pass on int16 zig-zag
 // blocks of 64, for callers whose transform did not fuse it.
 int rle_tile16_launch(const int16_t *blocks, int64_t nblk, int max_len, int64_t *tiles, hipStream_t s);
+// Slot layout (slots.h, rle.hip): the int64 word of a slot job's workspace where
+// its records' last DCs (int32 per record) start, after the scan's records,
+// offsets and hand-off granules; and the job's record count.
+int64_t slot_rdc_word(int64_t nrec);
+inline int64_t slot_nrec(int64_t nblk, int64_t records_per_tile) {
+  return (nblk * records_per_tile + 63) / 64;
+}
 
 }  // namespace hic

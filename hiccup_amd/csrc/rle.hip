@@ -616,6 +616,12 @@ struct RleJob16 {
   int64_t tpr, rpr;  // tiles and records per row
   int64_t wsb;       // workspace bytes (0: not checked; a rows job must give it)
   int64_t *index;    // optional tile index the emit writes (hic_rle_tile_index_i16's)
+  // slot layout (slots.h; the close k_rle_scan16b<true> and the compaction)
+  uint8_t *slot_len;
+  int16_t *slot_val;
+  int32_t *sidx;     // 4 int32 per record {n, P, pdc, nfill}
+  int32_t *rdc;      // the records' last DCs (in the workspace)
+  int64_t bpr;       // blocks per record (64 or 32); capacity 63 * bpr
 };
 struct RleJobs16 {
   RleJob16 j[kMaxJobs];
@@ -657,6 +663,9 @@ inline int64_t rle_ws_words(int64_t nrec) {
   const int64_t n = nrec > 0 ? nrec : 1;
   return 5 * n + 3 * ((n + kScan16T - 1) / kScan16T) + 8;
 }
+// SLOTS (the slot layout's close, slots.h): each record's first symbol length, its
+// first block's DC difference, and its index entry, from the same exclusive scan.
+template <bool SLOTS>
 __global__ __launch_bounds__(kScan16T) void k_rle_scan16b(RleJobs16 jobs, uint32_t epoch) {
   __shared__ Agg s_wave[kScan16T / 64 + 1];
   __shared__ Agg s_pre;
@@ -744,6 +753,25 @@ __global__ __launch_bounds__(kScan16T) void k_rle_scan16b(RleJobs16 jobs, uint32
   if (t < nt) {
     offs[t * 2 + 0] = excl.last >= 0 ? excl.cnt + syms_for_run(excl.first - p0 - 1, M) : 0;
     offs[t * 2 + 1] = excl.last >= 0 ? excl.last : p0;
+  }
+  if (SLOTS && t < nt) {
+    // the record's first nonzero continues the zero run since the previous record's
+    // last nonzero: its fillers and its first symbol's length (written as 0 by the
+    // fused kernel); P: the record-relative position the run's remainder starts after
+    const int64_t prv = excl.last >= 0 ? excl.last : p0, capr = 63 * J.bpr;
+    int n = 0, P = 0, nf = 0;
+    if (rec.first >= 0) {
+      const int64_t run = rec.first - prv - 1, f = div_run(run, M);
+      const int len0 = (int)(run - f * M);
+      nf = (int)f;
+      n = (int)rec.cnt + 1;
+      P = (int)(rec.first - t * capr) - len0;
+      J.slot_len[t * capr] = (uint8_t)len0;
+    }
+    // codec.differential_coding across the record boundary
+    const int pdc = t > 0 ? J.rdc[t - 1] : 0;
+    if (t > 0) J.dc_diff[t * J.bpr] -= pdc;
+    *reinterpret_cast<int4 *>(J.sidx + 4 * t) = make_int4(n, P, pdc, nf);
   }
   if (p == np - 1 && threadIdx.x == 0) {  // the channel's last partition closes the stream
     const Agg all = agg_combine(s_pre, s_wave[kScan16T / 64], M);
@@ -900,6 +928,48 @@ __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
     if (gn >= jobs.total_tiles) break;
     g = gn;
     cur = nxt;
+  }
+}
+
+// The slot layout's closing step has no emit to fold a timed-out scan hand-off
+// into the count (k_rle_emit16b's prologue): one small launch after the close does.
+__global__ void k_rle_scan_fold(RleJobs16 jobs) {
+  if (threadIdx.x < jobs.n) {
+    const RleJob16 &J = jobs.j[threadIdx.x];
+    const int64_t np = (J.nrec + kScan16T - 1) / kScan16T;
+    int64_t f;
+    if (get_granule(reinterpret_cast<const uint64_t *>(J.ws + 5 * J.nrec) + 3 * np, (jobs.epoch << 2) | 1u, f))
+      *J.d_count = HIC_COUNT_SCAN_TIMEOUT;
+  }
+}
+
+// The contiguous stream of slot-layout channels (hic_rle_slots_compact): one wave per
+// record writes its nfill fillers and copies its slot's n symbols to the record's
+// stream offset (the scan's offs).  Records of all jobs in one grid (tile0: a job's
+// first global record).
+__global__ __launch_bounds__(256) void k_rle_slots_compact(RleJobs16 jobs) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t g = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); g < jobs.total_tiles;
+       g += nw) {
+    int k = 0;
+    while (k + 1 < jobs.n && g >= jobs.j[k + 1].tile0) ++k;
+    const RleJob16 &J = jobs.j[k];
+    const int64_t r = g - J.tile0, capr = 63 * J.bpr;
+    const int64_t off = J.ws[3 * J.nrec + 2 * r];
+    const int4 ix = *reinterpret_cast<const int4 *>(J.sidx + 4 * r);
+    const int n = ix.x, nf = ix.w;
+    for (int64_t i = lane; i < nf; i += 64)
+      if (off + i < J.cap) {
+        J.sym_len[off + i] = (uint8_t)(jobs.M - 1);
+        J.sym_val[off + i] = 0;
+      }
+    const int64_t o = off + nf;
+    for (int i = lane; i < n; i += 64)
+      if (o + i < J.cap) {
+        J.sym_len[o + i] = J.slot_len[r * capr + i];
+        J.sym_val[o + i] = J.slot_val[r * capr + i];
+      }
   }
 }
 
@@ -1383,7 +1453,8 @@ int launch_tile16(const int16_t *blocks, int64_t nblk, int M, int64_t *tiles, hi
 
 // K2 + K3 of the hot path on tile records already in the workspaces (from
 // k_rle_tile16 or the fused DCT epilogue), for up to kMaxJobs channels at once.
-int encode_batch16(RleJobs16 &jobs, hipStream_t s) {
+// job geometry (tiles, records, first global tile) and the workspace check
+int prepare_batch16(RleJobs16 &jobs) {
   int64_t t0 = 0;
   for (int k = 0; k < jobs.n; ++k) {
     // stream positions and counts travel as int32 through the scan's hand-off
@@ -1407,12 +1478,24 @@ int encode_batch16(RleJobs16 &jobs, hipStream_t s) {
       return arg_error("job %d: workspace of %lld bytes, %lld needed", k, (long long)jobs.j[k].wsb, (long long)need);
   }
   jobs.total_tiles = t0;
+  return HIC_OK;
+}
+
+// the batch's scan (SLOTS: the slot layout's close); returns its launch status
+template <bool SLOTS>
+int scan_batch16(RleJobs16 &jobs, hipStream_t s) {
   const uint32_t ep = next_epoch();
   int64_t nparts = 0;
   for (int k = 0; k < jobs.n; ++k) nparts += (jobs.j[k].nrec + kScan16T - 1) / kScan16T;
   jobs.epoch = ep;
-  hipLaunchKernelGGL(k_rle_scan16b, dim3((unsigned)nparts), dim3(kScan16T), 0, s, jobs, ep);
-  if (int e = check_launch("k_rle_scan16b")) return e;
+  hipLaunchKernelGGL(k_rle_scan16b<SLOTS>, dim3((unsigned)nparts), dim3(kScan16T), 0, s, jobs, ep);
+  return check_launch("k_rle_scan16b");
+}
+
+int encode_batch16(RleJobs16 &jobs, hipStream_t s) {
+  if (int e = prepare_batch16(jobs)) return e;
+  const int64_t t0 = jobs.total_tiles;
+  if (int e = scan_batch16<false>(jobs, s)) return e;
   // persistent: 3 workgroups (12 waves) per CU fit the 51 KB LDS stage and the registers
 #ifndef HIC_EMIT_WPC
 #define HIC_EMIT_WPC 12
@@ -1545,13 +1628,15 @@ __global__ __launch_bounds__(256) void k_rle_index16(const int64_t *__restrict__
   index[3 * t + 2] = t > 0 ? (int64_t)blocks[(t * 64 - 1) * 64] : 0;
 }
 
-template <bool NT>
+// SLOTS: the symbols are in the slot layout (slots.h) and `index` is the close's
+// int32 record index (rsh: log2 records per 64-block tile).
+template <bool NT, bool SLOTS = false>
 __global__ __launch_bounds__(256) void k_rld_indexed16(const uint8_t *__restrict__ sym_len,
                                                        const int16_t *__restrict__ sym_val,
                                                        const int64_t *__restrict__ d_nsym,
                                                        const int32_t *__restrict__ dc_diff, int64_t nblk,
                                                        const int64_t *__restrict__ index, int16_t *__restrict__ blocks,
-                                                       int64_t *__restrict__ d_status) {
+                                                       int64_t *__restrict__ d_status, int rsh = 0) {
   __shared__ uint4 s_tile[4][64 * 8 + 8];  // 64 blocks + 64 trash slots
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t ntiles = (nblk + 63) / 64;
@@ -1565,20 +1650,29 @@ __global__ __launch_bounds__(256) void k_rld_indexed16(const uint8_t *__restrict
 #pragma unroll
   for (int k = 0; k < 8; ++k) tile[64 * k + lane] = make_uint4(0, 0, 0, 0);
   __builtin_amdgcn_wave_barrier();
-  const int64_t o0 = index[3 * t] < nsym ? index[3 * t] : nsym;
-  const int64_t o1 = t + 1 < ntiles ? (index[3 * (t + 1)] < nsym ? index[3 * (t + 1)] : nsym) : nsym;
   const int64_t tb0 = t * 64 * 63;                    // the tile's first AC position
   const int nvb = (int)(nblk - t * 64 < 64 ? nblk - t * 64 : 64);
   const int span = nvb * 63;                           // its AC positions
-  // P: the position after the previous tile's last symbol, relative to the tile (a
-  // carried run can start far before it; every AC position of the stream fits int32).
-  // Trash slots (never read): the 64 after the tile.
-  const int P = gather_tile<64, HIC_DEC_G, HIC_DEC_PF>(sym_len, sym_val, o0, o1, nsym, (int)(index[3 * t + 1] + 1 - tb0), span,
-                                           win, 64 * 64 + lane, lane);
+  int P = 0, pdc;
+  if constexpr (SLOTS) {
+    // the tile's records, each from its own slot (trash slots: the 64 after the tile)
+    const int32_t *sidx = reinterpret_cast<const int32_t *>(index);
+    P = slots_gather_tile<64>(sym_len, sym_val, sidx, t, rsh, nblk, span, win, 64 * 64 + lane, lane);
+    pdc = sidx[4 * (t << rsh) + 2];
+  } else {
+    const int64_t o0 = index[3 * t] < nsym ? index[3 * t] : nsym;
+    const int64_t o1 = t + 1 < ntiles ? (index[3 * (t + 1)] < nsym ? index[3 * (t + 1)] : nsym) : nsym;
+    // P: the position after the previous tile's last symbol, relative to the tile (a
+    // carried run can start far before it; every AC position of the stream fits int32).
+    // Trash slots (never read): the 64 after the tile.
+    P = gather_tile<64, HIC_DEC_G, HIC_DEC_PF>(sym_len, sym_val, o0, o1, nsym, (int)(index[3 * t + 1] + 1 - tb0), span,
+                                               win, 64 * 64 + lane, lane);
+    pdc = (int)index[3 * t + 2];
+  }
   // DC: the previous block's value plus this tile's differences
   const int64_t b = t * 64 + lane;
   const int d = lane < nvb ? dc_diff[b] : 0;
-  win[lane * 64] = (int16_t)(index[3 * t + 2] + wave_incl_sum_i32(d));
+  win[lane * 64] = (int16_t)(pdc + wave_incl_sum_i32(d));
   __builtin_amdgcn_wave_barrier();
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
@@ -1594,10 +1688,11 @@ __global__ __launch_bounds__(256) void k_rld_indexed16(const uint8_t *__restrict
     }
   }
   if (t == ntiles - 1 && lane == 0) {
-    // codec.decode_run_length's length: an EOB zero-fills to the end
+    // codec.decode_run_length's length: an EOB zero-fills to the end (a slot-layout
+    // stream is whole by construction)
     const int64_t total = tb0 + (int64_t)P, n_ac = nblk * 63;
-    const bool eob = nsym > 0 && sym_len[nsym - 1] == 0 && sym_val[nsym - 1] == 0;
-    *d_status = nsym_raw < 1 ? -1 : ((eob && total <= n_ac) ? n_ac : total);
+    const bool eob = SLOTS || (nsym > 0 && sym_len[nsym - 1] == 0 && sym_val[nsym - 1] == 0);
+    *d_status = nsym_raw < 1 ? -1 : ((eob && (SLOTS || total <= n_ac)) ? n_ac : total);
   }
 }
 
@@ -1755,6 +1850,96 @@ extern "C" int hic_rle_decode_i16_indexed(const uint8_t *sym_len, const int16_t 
     hipLaunchKernelGGL(k_rld_indexed16<false>, grid, block, 0, as_stream(stream), sym_len, sym_val, d_nsym, dc_diff,
                        nblk, d_index, blocks, d_status);
   return check_launch("k_rld_indexed16");
+}
+
+// ---- slot layout (slots.h) ----
+namespace hic {
+int64_t slot_rdc_word(int64_t nrec) { return rle_ws_words(nrec); }
+}  // namespace hic
+
+extern "C" size_t hic_rle_slots_workspace_bytes(int64_t nblk, int records_per_tile) {
+  const int64_t nrec = slot_nrec(nblk > 0 ? nblk : 1, records_per_tile == 2 ? 2 : 1);
+  return (size_t)(rle_ws_words(nrec) + (nrec + 1) / 2 + 2) * sizeof(int64_t);
+}
+
+// hic_slot_job[n] -> the scan / compaction jobs (validated, nothing launched on error)
+static int slot_jobs(int n, const hic_slot_job *jobs, int max_len, bool compact, RleJobs16 &J) {
+  if (n < 1 || n > kMaxJobs || !jobs) return arg_error("1 <= n <= %d jobs", kMaxJobs);
+  if (max_len != 15) return arg_error("the slot layout needs max_len 15");
+  J = RleJobs16{};
+  J.n = n;
+  J.M = max_len;
+  for (int k = 0; k < n; ++k) {
+    const hic_slot_job &a = jobs[k];
+    if (!a.slot_len || !a.slot_val || !a.dc_diff || !a.d_index || !a.workspace || !a.d_count || !a.sym_len ||
+        !a.sym_val)
+      return arg_error("job %d: null pointer", k);
+    if (a.nblk <= 0 || a.nblk > (int64_t)INT32_MAX / 63) return arg_error("job %d: nblk", k);
+    if (a.records_per_tile != 1 && a.records_per_tile != 2) return arg_error("job %d: records_per_tile must be 1 or 2", k);
+    const int64_t bpr = 64 / a.records_per_tile;
+    if (a.nblk % bpr) return arg_error("job %d: nblk must be a multiple of %lld (whole records)", k, (long long)bpr);
+    const int64_t need = (int64_t)hic_rle_slots_workspace_bytes(a.nblk, (int)a.records_per_tile);
+    if (a.workspace_bytes < need)
+      return arg_error("job %d: workspace of %lld bytes, %lld needed", k, (long long)a.workspace_bytes, (long long)need);
+    RleJob16 &j = J.j[k];
+    j = RleJob16{};
+    j.nblk = a.nblk;
+    j.dc_diff = a.dc_diff;
+    j.sym_len = a.sym_len;
+    j.sym_val = a.sym_val;
+    j.cap = a.sym_cap;
+    j.d_count = a.d_count;
+    j.ws = static_cast<int64_t *>(a.workspace);
+    j.rshift = a.records_per_tile == 2 ? 1 : 0;
+    j.slot_len = a.slot_len;
+    j.slot_val = a.slot_val;
+    j.sidx = a.d_index;
+    j.bpr = bpr;
+    j.nrec = a.nblk / bpr;
+    j.rdc = reinterpret_cast<int32_t *>(j.ws + rle_ws_words(j.nrec));
+  }
+  int64_t r0 = 0;  // tile0 / total_tiles count records here (the compaction's waves)
+  for (int k = 0; k < n; ++k) {
+    J.j[k].tile0 = r0;
+    r0 += J.j[k].nrec;
+  }
+  J.total_tiles = r0;
+  (void)compact;
+  return HIC_OK;
+}
+
+extern "C" int hic_rle_slots_close(int n, const hic_slot_job *jobs, int max_len, void *stream) {
+  RleJobs16 J;
+  if (int e = slot_jobs(n, jobs, max_len, false, J)) return e;
+  hipStream_t s = as_stream(stream);
+  if (int e = scan_batch16<true>(J, s)) return e;
+  hipLaunchKernelGGL(k_rle_scan_fold, dim3(1), dim3(64), 0, s, J);
+  return check_launch("k_rle_scan_fold");
+}
+
+extern "C" int hic_rle_slots_compact(int n, const hic_slot_job *jobs, int max_len, void *stream) {
+  RleJobs16 J;
+  if (int e = slot_jobs(n, jobs, max_len, true, J)) return e;
+  const int64_t waves = J.total_tiles < 16 * (int64_t)cu_count() ? J.total_tiles : 16 * (int64_t)cu_count();
+  hipLaunchKernelGGL(k_rle_slots_compact, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, as_stream(stream), J);
+  return check_launch("k_rle_slots_compact");
+}
+
+extern "C" int hic_rle_decode_i16_slots(const uint8_t *slot_len, const int16_t *slot_val, const int64_t *d_nsym,
+                                        const int32_t *dc_diff, int64_t nblk, int records_per_tile,
+                                        const int32_t *d_index, int16_t *blocks, int64_t *d_status, void *stream) {
+  if (!slot_len || !slot_val || !d_nsym || !dc_diff || !d_index || !blocks || !d_status) return arg_error("null pointer");
+  if (nblk <= 0 || nblk * 63 >= ((int64_t)1 << 31)) return arg_error("nblk");
+  if (records_per_tile != 1 && records_per_tile != 2) return arg_error("records_per_tile must be 1 or 2");
+  if (nblk % (64 / records_per_tile)) return arg_error("nblk must hold whole records");
+  if ((reinterpret_cast<uintptr_t>(slot_len) | reinterpret_cast<uintptr_t>(slot_val) |
+       reinterpret_cast<uintptr_t>(blocks)) % 16)
+    return arg_error("slot arrays and blocks must be 16-byte aligned");
+  const int64_t ntiles = (nblk + 63) / 64;
+  hipLaunchKernelGGL((k_rld_indexed16<false, true>), dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0,
+                     as_stream(stream), slot_len, slot_val, d_nsym, dc_diff, nblk,
+                     reinterpret_cast<const int64_t *>(d_index), blocks, d_status, records_per_tile == 2 ? 1 : 0);
+  return check_launch("k_rld_indexed16<slots>");
 }
 
 extern "C" int hic_rle_shard_summary_records(const int16_t *blocks, int64_t nblk, int records_per_tile,

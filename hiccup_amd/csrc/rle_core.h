@@ -481,5 +481,32 @@ __device__ __forceinline__ int gather_tile(const uint8_t *__restrict__ sym_len, 
   return P;
 }
 
+// The slot-layout form (slots.h): a 64-block tile holds 1 << rsh records, record r's
+// n symbols at [r * cap, r * cap + n) of the slot arrays (cap = 63 x 64 >> rsh), its
+// first symbol's zeros starting after record-relative position P (sidx: the close's
+// {n, P, pdc, nfill} per record).  Returns the last record's end position (as
+// gather_tile; 0 for a tile without symbols).
+template <int ROW>
+__device__ __forceinline__ int slots_gather_tile(const uint8_t *__restrict__ slot_len,
+                                                 const int16_t *__restrict__ slot_val, const int32_t *__restrict__ sidx,
+                                                 int64_t t, int rsh, int64_t nblk, int span, int16_t *win, int trash,
+                                                 int lane) {
+  const int bpr = 64 >> rsh, capr = 63 * bpr;
+  const int64_t nrec = (nblk + bpr - 1) / bpr;
+  int P = 0;
+  for (int k = 0; k < (1 << rsh); ++k) {
+    const int64_t r = (t << rsh) + k;
+    if (r >= nrec) break;  // wave-uniform
+    const int n = __builtin_amdgcn_readfirstlane(sidx[4 * r]);
+    if (n > 0) {
+      const int Pr = __builtin_amdgcn_readfirstlane(sidx[4 * r + 1]);
+      const int64_t o0 = r * capr;
+      P = gather_tile<ROW, HIC_DEC_G, HIC_DEC_PF>(slot_len, slot_val, o0, o0 + n, o0 + capr, Pr + k * capr, span, win,
+                                                 trash, lane);
+    }
+  }
+  return P;
+}
+
 }  // namespace
 }  // namespace hic

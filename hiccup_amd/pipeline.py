@@ -16,6 +16,13 @@ H x W x 3 uint8 image that already lives in HBM:
   3. hic_rle_encode_i16_tiles_batch  DC DPCM + channel-wide AC RLE of all three
                               channels (one scan + one emit launch) -> (uint8 len, int16 val)
 
+Slot layout (round 6, the default for a whole image with W % 512 == 0, H % 16 ==
+0 and max_len 15): hic_encode420_slots_u8 writes every RLE record's symbols and DC
+differences itself (slots.h), and hic_rle_slots_close (one scan launch) closes
+the records' carried runs and writes the record index: two launches per image, no
+int16 coefficients in HBM.  compact() / materialize() give the contiguous stream
+and the zig-zag blocks when a caller asks (result(), hic_image()).
+
 All launches are asynchronous on one stream; buffers are allocated once.
 ``Decoder.decode`` runs the inverse chain (codec.jpeg_decode's RLE/DC/izigzag
 half + compression.jpeg_decompression).  The optional ``stitch`` tensors make
@@ -82,11 +89,29 @@ def encoder_layout(H, W, rows=None, fused=None, index=False):
     return f, {"lum": 1, "cr": 2 if half else 1, "cb": 2 if half else 1}
 
 
+def slots_eligible(H, W, max_len=15, rows=None, out=None, fused=None, landing_rpt=None):
+    """Whether an Encoder of this shape can take the slot layout (hic_encode420_slots_u8:
+    a whole image, W % 512 == 0, H % 16 == 0, max_len 15, < 2 GiB of RGB)."""
+    return (rows in (None, (0, H)) and out is None and landing_rpt is None and fused is not False and max_len == 15
+            and W % 512 == 0 and H % 16 == 0 and H >= 16 and H * W * 3 <= 2**31 - 1)
+
+
+class SlotIndex:
+    """The slot-layout stream of an Encoder for Decoder.decode(index=...): per channel
+    the slot arrays, the close's record index and the records per 64-block tile."""
+
+    def __init__(self, enc):
+        self.slot_len, self.slot_val, self.sidx, self.rpt = enc.slot_len, enc.slot_val, enc.sidx, enc.rpt
+
+    def __getitem__(self, k):
+        return self.sidx[k]
+
+
 class Encoder:
     """rows=(r0, r1) makes this encoder one row-shard of an H x W image (r0 even;
     shards of one image split at multiples of 16 rows so chroma blocks align)."""
 
-    def __init__(self, H, W, max_len=15, rows=None, out=None, fused=None, index=False, landing_rpt=None):
+    def __init__(self, H, W, max_len=15, rows=None, out=None, fused=None, index=False, landing_rpt=None, slots=None):
         """out: optional {channel: (coef (n, 64) int16, dc (n,) int32)} device views the
         encoder writes into (a gathering rank points them at its slice of the whole
         image's buffers, so its own shard needs no copy).
@@ -98,7 +123,9 @@ class Encoder:
         shard or an encoder with a tile index when W % 512 == 0; False = the chain.
         landing_rpt: a landing zone only (the gathering rank of a stream gather): no
         transform, no plane buffers, and the RLE record layout of the shards that
-        fill it (their encoder_layout rpt), whatever this shape alone would pick."""
+        fill it (their encoder_layout rpt), whatever this shape alone would pick.
+        slots: the slot layout (module docstring); None = whenever slots_eligible,
+        False = the coefficient + emit chain."""
         if H < 2 or W < 2:
             raise ValueError("image must be at least 2 x 2")
         device.require_gpu()
@@ -109,14 +136,21 @@ class Encoder:
         self.rows = (r0, r1)
         self.want_index = bool(index)
         self.landing = landing_rpt is not None
+        ok = slots_eligible(H, W, max_len, rows, out, fused, landing_rpt)
+        if slots and not ok:
+            raise ValueError("the slot layout needs a whole image with W % 512 == 0, H % 16 == 0 and max_len 15")
+        self.slots = ok if slots is None else bool(slots)
         if self.landing:
             self.fused, self.rpt = False, dict(landing_rpt)
+        elif self.slots:
+            self.fused, self.rpt = True, {"lum": 1, "cr": 2, "cb": 2}
         else:
             self.fused, self.rpt = encoder_layout(H, W, rows, fused, index)
         # a whole image's ragged last strip (W % 512 != 0): the fused kernel writes one
         # RLE record per strip segment (hic_encode420_seg_u8) and the scan / emit walk
         # row segments (hic_rle_encode_i16_rows_batch): no tile pass
-        self.seg = not self.landing and self.fused and rows is None and W % 512 != 0 and not self.want_index
+        self.seg = (not self.landing and not self.slots and self.fused and rows is None and W % 512 != 0
+                    and not self.want_index)
         c0, c1 = r0 // 2, min(H // 2, r1 // 2)
         self.shapes = {"lum": (r1 - r0, W), "cr": (c1 - c0, W // 2), "cb": (c1 - c0, W // 2)}
         ys, cs = self.shapes["lum"], self.shapes["cr"]
@@ -153,6 +187,20 @@ class Encoder:
             self.ws_bytes[k] = (lib.hic_rle_rows_workspace_bytes(n, rowb, self.rpt[k]) if self.seg
                                 else lib.hic_rle_workspace_bytes(n, 64))
             self.ws[k] = device.workspace(self.ws_bytes[k])
+        if self.slots:
+            # the slot layout: slots of 63 symbols per block, the close's record index
+            # (4 int32 per record), the records + their last DCs in the workspace
+            self.slot_len, self.slot_val, self.sidx = {}, {}, {}
+            for k in CHANNELS:
+                n = self.coef[k].shape[0]
+                self.slot_len[k] = device.empty((n * 63,), torch.uint8)
+                self.slot_val[k] = device.empty((n * 63,), torch.int16)
+                self.sidx[k] = device.empty((4 * (n * self.rpt[k] // 64),), torch.int32)
+                self.ws_bytes[k] = lib.hic_rle_slots_workspace_bytes(n, self.rpt[k])
+                self.ws[k] = device.workspace(self.ws_bytes[k])
+            self._mat_status = device.zeros((3,), torch.int64)
+            self.index = SlotIndex(self)
+            return
         # index=True: the encoder-side tile index a device decoder reads
         # (Decoder.decode(..., index=enc.index)): 3 int64 per 64-block tile
         self.index = ({k: device.empty((3 * -(-self.coef[k].shape[0] // 64),), torch.int64) for k in CHANNELS}
@@ -177,6 +225,14 @@ class Encoder:
             in_row0 = 0 if self.rows == (0, self.H) else self.input_span()[0]
         r0, r1 = self.rows
         ev = (dct_events.start, dct_events.stop) if dct_events is not None else (None, None)
+        if self.slots:
+            # colour + pyrDown + DCT/quantize/zig-zag + the records' symbols and DC
+            # differences, in ONE launch (slots.h): no coefficients reach HBM
+            if in_row0 != 0 or rgb.shape[0] != self.H:
+                raise ValueError("a slot-layout encoder takes the whole image")
+            _lib.call("hic_encode420_slots_u8", device.ptr(rgb), self.H, self.W, self._slot_jobs(), self.max_len, s,
+                      *ev)
+            return
         if self.fused:
             # colour + pyrDown + DCT/quantize/zig-zag of the three planes + RLE tile
             # records in ONE launch (dct_events time it).  The kernel addresses its
@@ -208,8 +264,39 @@ class Encoder:
                                        self.ws[k].data_ptr())
         _lib.call("hic_dct_quant_rle_u8_batch", 3, jobs, self.max_len, s, *ev)
 
+    def _slot_jobs(self):
+        jobs = (_lib.SlotJob * 3)()
+        for i, k in enumerate(CHANNELS):
+            jobs[i] = _lib.SlotJob(self.coef[k].shape[0], self.rpt[k], self.slot_len[k].data_ptr(),
+                                   self.slot_val[k].data_ptr(), self.dc[k].data_ptr(), self.sidx[k].data_ptr(),
+                                   self.ws[k].data_ptr(), self.ws_bytes[k], self.counts[i:i + 1].data_ptr(),
+                                   self.sym_len[k].data_ptr(), self.sym_val[k].data_ptr(), self.cap[k])
+        return jobs
+
+    def compact(self, stream=None):
+        """Slot layout: the contiguous symbol stream into sym_len / sym_val (what the
+        emit writes; hic_rle_slots_compact).  A no-op for the coefficient chain."""
+        if self.slots:
+            _lib.call("hic_rle_slots_compact", 3, self._slot_jobs(), self.max_len, device.stream_ptr(stream))
+
+    def materialize(self, stream=None):
+        """Slot layout: the contiguous stream and the zig-zag blocks (self.coef,
+        decoded from the slots: hic_rle_decode_i16_slots), as the coefficient chain
+        leaves them.  A no-op for the coefficient chain."""
+        if not self.slots:
+            return
+        self.compact(stream)
+        s = device.stream_ptr(stream)
+        for i, k in enumerate(CHANNELS):
+            _lib.call("hic_rle_decode_i16_slots", device.ptr(self.slot_len[k]), device.ptr(self.slot_val[k]),
+                      ctypes.c_void_p(self.counts.data_ptr() + 8 * i), device.ptr(self.dc[k]), self.coef[k].shape[0],
+                      self.rpt[k], device.ptr(self.sidx[k]), device.ptr(self.coef[k]),
+                      device.ptr(self._mat_status[i:i + 1]), s)
+
     def shard_summaries(self, stream=None):
         """Per-channel {trailing zeros, has nonzero, first DC, last DC} (sharded encode)."""
+        if self.slots:
+            raise ValueError("shard summaries are for row shards (a slot-layout encoder is a whole image)")
         if self.seg:
             raise ValueError("shard summaries read 64-block tile records (a row shard's); this whole-image "
                              "encoder keeps one per strip segment")
@@ -225,6 +312,11 @@ class Encoder:
         emit launch for all three).  stitch: None or a (3, 4) int64 device tensor of
         per-channel {carry_zeros, emit_eob, has_prev_dc, prev_dc}."""
         s = device.stream_ptr(stream)
+        if self.slots:
+            if stitch is not None:
+                raise ValueError("a slot-layout encoder is a whole image (no stitch)")
+            _lib.call("hic_rle_slots_close", 3, self._slot_jobs(), self.max_len, s)
+            return
         if self.seg:
             rowb = (ctypes.c_int64 * 3)(self.W // 8, self.W // 16, self.W // 16)
             _lib.call("hic_rle_encode_i16_rows_batch", 3, self._rle_jobs(stitch), rowb, self.max_len, s)
@@ -257,6 +349,7 @@ class Encoder:
         from . import huffman
         if self.rows != (0, self.H):
             raise ValueError("hic_image needs the whole image (an unsharded encoder)")
+        self.compact(stream)
         with device.on_stream(stream):  # the counts and histograms are read after the stream's kernels
             return self._hic_image(stream)
 
@@ -281,7 +374,9 @@ class Encoder:
         return hic.HicImage.jpeg_image(tables + data + [hic.TupP(h, w), hic.TupP(hc, wc)])
 
     def result(self):
-        """Host copies: {channel: (zigzag blocks, dc_diff, sym_len, sym_val)} (syncs)."""
+        """Host copies: {channel: (zigzag blocks, dc_diff, sym_len, sym_val)} (syncs;
+        a slot-layout encoder materializes its stream and blocks first)."""
+        self.materialize()
         device.sync()
         counts = self.counts.cpu().numpy()
         out = {}
@@ -324,6 +419,8 @@ class Decoder:
         written); planes=True keeps the Y plane and the separate colour kernel."""
         s = device.stream_ptr(stream)
         lib = _lib.load()
+        if isinstance(index, SlotIndex):
+            return self._decode_slots(index, counts, dc, s, keep_blocks, planes)
         if index is not None and not keep_blocks and not planes and self.H % 8 == 0 and self.W % 8 == 0:
             # Cr and Cb in one launch (one tail), then Y straight to RGB
             h, w = self.shapes["cr"]
@@ -368,6 +465,46 @@ class Decoder:
                           device.ptr(self._ws[k]), s)
             _lib.call("hic_dequant_idct_u8", device.ptr(self.blocks[k]), _lib.LAYOUT_ZIGZAG_I16, h, w, TABLES[k],
                       device.ptr(self.pix[k]), self.pix[k].stride(0), s)
+        h, w = self.shapes["cr"]
+        _lib.call("hic_ycrcb420_to_rgb", device.ptr(self.pix["lum"]), self.pix["lum"].stride(0),
+                  device.ptr(self.pix["cr"]), device.ptr(self.pix["cb"]), h, w, device.ptr(self.rgb), s)
+        return self.rgb
+
+    def _decode_slots(self, ix, counts, dc, s, keep_blocks, planes):
+        """decode() from a slot-layout encoder's stream (SlotIndex): the *_slots forms of
+        the indexed decoders."""
+        cnt = lambda i: ctypes.c_void_p(counts.data_ptr() + 8 * i)  # noqa: E731
+        if not keep_blocks and not planes and self.H % 8 == 0 and self.W % 8 == 0:
+            h, w = self.shapes["cr"]
+            if self.chroma_pair:
+                pair = lambda f: (ctypes.c_void_p * 2)(*(f(i, k) for i, k in ((1, "cr"), (2, "cb"))))  # noqa: E731
+                _lib.call("hic_rle_decode_idct_u8_slots_pair", pair(lambda i, k: ix.slot_len[k].data_ptr()),
+                          pair(lambda i, k: ix.slot_val[k].data_ptr()), pair(lambda i, k: counts.data_ptr() + 8 * i),
+                          pair(lambda i, k: dc[k].data_ptr()), pair(lambda i, k: ix.sidx[k].data_ptr()), ix.rpt["cr"],
+                          h, w, TABLES["cr"], pair(lambda i, k: self.pix[k].data_ptr()), self.pix["cr"].stride(0),
+                          pair(lambda i, k: self.status[i:i + 1].data_ptr()), s)
+            else:
+                for i, k in ((1, "cr"), (2, "cb")):
+                    _lib.call("hic_rle_decode_idct_u8_slots", device.ptr(ix.slot_len[k]), device.ptr(ix.slot_val[k]),
+                              cnt(i), device.ptr(dc[k]), device.ptr(ix.sidx[k]), ix.rpt[k], h, w, TABLES[k],
+                              device.ptr(self.pix[k]), self.pix[k].stride(0), device.ptr(self.status[i:i + 1]), s)
+            _lib.call("hic_rle_decode_idct_rgb_slots", device.ptr(ix.slot_len["lum"]), device.ptr(ix.slot_val["lum"]),
+                      cnt(0), device.ptr(dc["lum"]), device.ptr(ix.sidx["lum"]), ix.rpt["lum"], self.H, self.W,
+                      device.ptr(self.pix["cr"]), device.ptr(self.pix["cb"]), device.ptr(self.rgb),
+                      self.rgb.stride(0), device.ptr(self.status[0:1]), s)
+            return self.rgb
+        for i, k in enumerate(CHANNELS):
+            h, w = self.shapes[k]
+            if keep_blocks:
+                _lib.call("hic_rle_decode_i16_slots", device.ptr(ix.slot_len[k]), device.ptr(ix.slot_val[k]), cnt(i),
+                          device.ptr(dc[k]), self.blocks[k].shape[0], ix.rpt[k], device.ptr(ix.sidx[k]),
+                          device.ptr(self.blocks[k]), device.ptr(self.status[i:i + 1]), s)
+                _lib.call("hic_dequant_idct_u8", device.ptr(self.blocks[k]), _lib.LAYOUT_ZIGZAG_I16, h, w, TABLES[k],
+                          device.ptr(self.pix[k]), self.pix[k].stride(0), s)
+            else:
+                _lib.call("hic_rle_decode_idct_u8_slots", device.ptr(ix.slot_len[k]), device.ptr(ix.slot_val[k]),
+                          cnt(i), device.ptr(dc[k]), device.ptr(ix.sidx[k]), ix.rpt[k], h, w, TABLES[k],
+                          device.ptr(self.pix[k]), self.pix[k].stride(0), device.ptr(self.status[i:i + 1]), s)
         h, w = self.shapes["cr"]
         _lib.call("hic_ycrcb420_to_rgb", device.ptr(self.pix["lum"]), self.pix["lum"].stride(0),
                   device.ptr(self.pix["cr"]), device.ptr(self.pix["cb"]), h, w, device.ptr(self.rgb), s)

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define HIC_ABI_VERSION 3
+#define HIC_ABI_VERSION 4
 
 #define HIC_OK 0
 #define HIC_ERR_ARG (-1)      /* bad shape / pointer / enum: the reference asserts or raises */
@@ -178,6 +178,72 @@ int hic_encode420_seg_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_ro
                          int64_t out_row0, int64_t out_rows, int16_t *coef_y, int16_t *coef_cr, int16_t *coef_cb,
                          void *ws_y, void *ws_cr, void *ws_cb, int64_t ws_bytes_y, int64_t ws_bytes_c, int max_len,
                          void *stream, void *ev_start, void *ev_stop);
+/* ---- slot-layout encode (round 6): hic_encode420_u8 + hic_rle_encode_i16_tiles_batch
+ *      (compression.jpeg_compression's transform + codec.jpeg_encode's DC DPCM and AC
+ *      RLE, compression.py:16-39, codec.py:47-99,286-301) with the symbols written by
+ *      the fused kernel itself: the int16 coefficients never reach HBM and no emit
+ *      kernel re-reads them.
+ *  Slot layout of a channel: its blocks form records of 64 (Y, records_per_tile 1)
+ *  or 32 (Cr / Cb, records_per_tile 2) consecutive blocks; record r owns symbols
+ *  [r * cap, r * cap + n_r) of slot_len / slot_val (cap = 63 x its blocks, so the
+ *  slot arrays hold nblk * 63 entries).  The channel's symbol stream -- exactly
+ *  what hic_rle_encode_i16 writes -- is, over the records in order, nfill_r fillers
+ *  (max_len - 1, 0) followed by the slot's n_r symbols, then the EOB (0, 0) when
+ *  the stream ends in a zero.  max_len must be 15 (4-bit lengths in the kernel's
+ *  stage).  Whole images only, W % 512 == 0, H % 16 == 0.
+ *  hic_encode420_slots_u8: jobs[0..2] = Y, Cr, Cb (nblk (H/8)(W/8) and
+ *    (H/16)(W/16), records_per_tile 1 and 2): the slots, dc_diff (each record's first
+ *    block still holding its raw DC) and the records in `workspace`.  Events as in
+ *    hic_encode420_u8 (nullable).
+ *  hic_rle_slots_close: the records' scan: writes each record's first symbol length,
+ *    subtracts the previous record's last DC from its first block's dc_diff, fills
+ *    d_index (4 int32 per record: n_r, P_r = the record-relative AC position after
+ *    which its first symbol's zeros start (<= 0: the run is carried in), pdc_r = the
+ *    DC of the block before the record, nfill_r), *d_count (the stream's symbols,
+ *    fillers and EOB included; HIC_COUNT_SCAN_TIMEOUT if a hand-off timed out) and
+ *    the EOB into sym_len / sym_val.
+ *  hic_rle_slots_compact: the contiguous stream into sym_len / sym_val (sym_cap >=
+ *    the count; after hic_rle_slots_close).
+ *  Decoders: hic_rle_decode_i16_slots / hic_rle_decode_idct_u8_slots[_pair] /
+ *    hic_rle_decode_idct_rgb_slots are their *_indexed counterparts reading the slots
+ *    through d_index (records_per_tile as the job's; *d_status = nblk * 63, or -1
+ *    when *d_nsym < 1). */
+typedef struct {
+  int64_t nblk;             /* blocks of the channel */
+  int64_t records_per_tile; /* 1: a record per 64 blocks; 2: per 32 blocks */
+  uint8_t *slot_len;        /* nblk * 63 bytes, 16-byte aligned */
+  int16_t *slot_val;        /* nblk * 63 int16, 16-byte aligned */
+  int32_t *dc_diff;         /* nblk */
+  int32_t *d_index;         /* 4 int32 per record (hic_rle_slots_close) */
+  void *workspace;          /* hic_rle_slots_workspace_bytes(nblk, records_per_tile) bytes,
+                               zero-filled before its first use */
+  int64_t workspace_bytes;
+  int64_t *d_count;         /* device int64: the stream's symbol count */
+  uint8_t *sym_len;         /* the contiguous stream: its EOB (close) and the rest (compact) */
+  int16_t *sym_val;
+  int64_t sym_cap;
+} hic_slot_job;
+size_t hic_rle_slots_workspace_bytes(int64_t nblk, int records_per_tile);
+int hic_encode420_slots_u8(const uint8_t *rgb, int64_t H, int64_t W, const hic_slot_job *jobs, int max_len,
+                           void *stream, void *ev_start, void *ev_stop);
+int hic_rle_slots_close(int n, const hic_slot_job *jobs, int max_len, void *stream);
+int hic_rle_slots_compact(int n, const hic_slot_job *jobs, int max_len, void *stream);
+int hic_rle_decode_i16_slots(const uint8_t *slot_len, const int16_t *slot_val, const int64_t *d_nsym,
+                             const int32_t *dc_diff, int64_t nblk, int records_per_tile, const int32_t *d_index,
+                             int16_t *blocks, int64_t *d_status, void *stream);
+int hic_rle_decode_idct_u8_slots(const uint8_t *slot_len, const int16_t *slot_val, const int64_t *d_nsym,
+                                 const int32_t *dc_diff, const int32_t *d_index, int records_per_tile, int64_t H,
+                                 int64_t W, int table_id, uint8_t *out, int64_t out_stride, int64_t *d_status,
+                                 void *stream);
+int hic_rle_decode_idct_u8_slots_pair(const uint8_t *const *h_slot_len, const int16_t *const *h_slot_val,
+                                      const int64_t *const *h_d_nsym, const int32_t *const *h_dc_diff,
+                                      const int32_t *const *h_d_index, int records_per_tile, int64_t H, int64_t W,
+                                      int table_id, uint8_t *const *h_out, int64_t out_stride,
+                                      int64_t *const *h_d_status, void *stream);
+int hic_rle_decode_idct_rgb_slots(const uint8_t *slot_len, const int16_t *slot_val, const int64_t *d_nsym,
+                                  const int32_t *dc_diff, const int32_t *d_index, int records_per_tile, int64_t H,
+                                  int64_t W, const uint8_t *cr, const uint8_t *cb, uint8_t *rgb, int64_t rgb_stride,
+                                  int64_t *d_status, void *stream);
 /* Timing events (hipEvent_t handles) for the *_timed entry points. */
 int hic_event_create(void **h_event);
 int hic_event_destroy(void *event);

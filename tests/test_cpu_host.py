@@ -34,7 +34,7 @@ def test_ctypes_signatures_match_header():
     for name, args in decl.items():
         nargs = 0 if args.strip() == "void" else len([a for a in args.split(",") if a.strip()])
         assert nargs == len(_lib.SIGNATURES[name][1]), name
-    assert _lib.load().hic_abi_version() == 3
+    assert _lib.load().hic_abi_version() == 4
     # argument kinds: every pointer parameter is bound as a pointer, every scalar
     # with the header's width and signedness
     kinds = {"int64_t": ctypes.c_int64, "int": ctypes.c_int, "int32_t": ctypes.c_int32, "size_t": ctypes.c_size_t,
@@ -67,7 +67,7 @@ def test_ctypes_structs_match_header(tmp_path):
     """The job structs' ctypes mirrors (_lib.RleJob16, _lib.DctPlaneJob) have the
     header's size and field offsets, as gcc lays them out."""
     import subprocess
-    structs = {"hic_rle_job16": _lib.RleJob16, "hic_dct_plane_job": _lib.DctPlaneJob}
+    structs = {"hic_rle_job16": _lib.RleJob16, "hic_dct_plane_job": _lib.DctPlaneJob, "hic_slot_job": _lib.SlotJob}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "hiccup_hip.h"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append('  printf("%s size %%zu\\n", sizeof(%s));' % (cname, cname))

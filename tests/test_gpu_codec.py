@@ -327,23 +327,33 @@ def test_pipeline_encoder(H, W):
     np.testing.assert_array_equal(rgb2, exp_rgb)
 
 
+@pytest.mark.parametrize("slots", [None, False])
 @pytest.mark.parametrize("kind", ["random", "levels", "blocks", "flat"])
 @pytest.mark.parametrize("H,W", [(64, 96), (512, 1024), (272, 1536), (1088, 1920), (4320, 7680), (16, 16),
-                                 (250, 330), (37, 53)])
-def test_indexed_decode(H, W, kind):
+                                 (250, 330), (37, 53), (24, 40), (40, 24), (8, 8), (16, 512), (48, 1536)])
+def test_indexed_decode(H, W, kind, slots):
     """Encoder(index=True) + Decoder.decode(index=...): one wave per 64-block
     tile from the encoder-side index, counts read on the device -- the blocks and
     RGB equal the plain decode's, the status equals nblk * 63, on fused (half-tile
     chroma records) and two-kernel-chain encoders, with empty tiles and long
-    carried runs (flat)."""
+    carried runs (flat).  slots None: the default, which for W % 512 == 0 is the
+    slot layout (the decoders read the slots through the close's record index);
+    False: the coefficient chain's tile index.  (24, 40) / (40, 24): chroma planes of
+    half blocks beside whole luma blocks; (8, 8): one block."""
     if kind == "blocks" and (H % 8 or W % 8):
         pytest.skip("the blocks image needs whole 8x8 blocks")
+    if slots is False and not pipeline.slots_eligible(H, W):
+        pytest.skip("the default already is the coefficient chain")
     rgb = _structured_rgb(kind, H, W, H * 7 + W)
-    enc = pipeline.Encoder(H, W, index=True)
+    enc = pipeline.Encoder(H, W, index=True, slots=slots)
+    assert enc.slots == (slots is None and pipeline.slots_eligible(H, W))
     enc.encode(device.to_device(rgb))
+    enc.materialize()  # slot layout: the contiguous stream and the blocks, for the plain decode
     counts = enc.counts.cpu().tolist()
     # the index the emit wrote (hic_rle_job16.d_index) == hic_rle_tile_index_i16's
     for k in pipeline.CHANNELS:
+        if enc.slots:
+            break
         ix = torch.full_like(enc.index[k], -5)
         _lib.call("hic_rle_tile_index_i16", device.ptr(enc.coef[k]), enc.coef[k].shape[0], enc.rpt[k],
                   device.ptr(enc.ws[k]), device.ptr(ix), device.stream_ptr())
@@ -384,13 +394,16 @@ def test_indexed_decode(H, W, kind):
 
 
 @pytest.mark.parametrize("mode", ["rgb", "planes", "blocks"])
-def test_indexed_decode_failed_count(mode):
+@pytest.mark.parametrize("W", [192, 512])
+def test_indexed_decode_failed_count(mode, W):
     """A failed encode's symbol count (< 1) decodes nothing of that channel and
     reports status -1 (include/hiccup_hip.h, hic_rle_decode_i16_indexed) on every
     indexed form -- the fused RGB kernel, the per-plane decode-IDCT, the block
-    decode -- while the other channels decode as usual."""
-    H, W = 128, 192
+    decode -- while the other channels decode as usual (W 512: the slot layout's
+    decoders)."""
+    H = 128
     enc = pipeline.Encoder(H, W, index=True)
+    assert enc.slots == (W == 512)
     enc.encode(device.to_device(_structured_rgb("random", H, W, 11)))
     good = pipeline.Decoder(H, W)
     r_good = good.decode(enc.sym_len, enc.sym_val, enc.counts, enc.dc, index=enc.index).clone()
@@ -439,15 +452,23 @@ def test_fused_encoder_matches_two_kernel_chain(kind, H, W):
     records are 32-block half tiles)."""
     rgb = _structured_rgb(kind, H, W, H + W)
     x = device.to_device(rgb)
-    got, exp = pipeline.Encoder(H, W, fused=True), pipeline.Encoder(H, W, fused=False)
-    got.encode(x)
+    exp = pipeline.Encoder(H, W, fused=False)
     exp.encode(x)
-    a, b = got.result(), exp.result()
-    for k in pipeline.CHANNELS:
-        for j, what in enumerate(("coef", "dc", "sym_len", "sym_val")):
-            np.testing.assert_array_equal(a[k][j], b[k][j], err_msg="%s %s" % (k, what))
+    b = exp.result()
+    # the fused kernel writing coefficients + records, and (W % 512 == 0) the slot layout
+    encs = [pipeline.Encoder(H, W, fused=True, slots=False)]
+    if pipeline.slots_eligible(H, W):
+        encs.append(pipeline.Encoder(H, W, fused=True))
+        assert encs[-1].slots
+    for got in encs:
+        got.encode(x)
+        a = got.result()
+        for k in pipeline.CHANNELS:
+            for j, what in enumerate(("coef", "dc", "sym_len", "sym_val")):
+                np.testing.assert_array_equal(a[k][j], b[k][j], err_msg="%s %s slots %s" % (k, what, got.slots))
     # the shard summaries read the half-tile records (a whole ragged image keeps one
     # record per strip segment instead: no shard summaries)
+    got = encs[0]
     if not got.seg:
         np.testing.assert_array_equal(got.shard_summaries().cpu().numpy(), exp.shard_summaries().cpu().numpy())
 
@@ -653,11 +674,12 @@ def test_shards_stitch_16k():
     test_shards_stitch_to_single_stream(16384, 16384, 8, None)
 
 
-def test_two_stream_overlap_matches_single_stream():
+@pytest.mark.parametrize("H,W", [(1088, 1920), (1088, 2048)])
+def test_two_stream_overlap_matches_single_stream(H, W):
     """bench.py's default: consecutive images alternate over two HIP streams with 4
     rotating encoders.  Every encoder's output after the overlapped run equals a
-    one-stream encode of the same image (no buffer shared across streams)."""
-    H, W = 1088, 1920
+    one-stream encode of the same image (no buffer shared across streams; W 2048:
+    the slot layout)."""
     rng = np.random.default_rng(11)
     imgs = [device.to_device(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)) for _ in range(3)]
     encs = [pipeline.Encoder(H, W) for _ in range(4)]

@@ -5,10 +5,15 @@ N = 1 (default; BASELINE configs[2], the 8K encode the metric is quoted on): a
 7680 x 4320 RGB uint8 image, already resident in HBM, through the full encode
 front end = compression.jpeg_compression + the zig-zag / DC / RLE half of
 codec.jpeg_encode:
-  RGB -> YCrCb + 4:2:0 pyrDown  (1 fused kernel)
-  8x8 DCT + quantize + zig-zag   (3 planes, one launch, bit-exact vs float64)
-  DC DPCM + channel-wide AC RLE  (3 planes, one scan + one emit launch)
-One "step" encodes one such image.
+  RGB -> YCrCb + 4:2:0 pyrDown, 8x8 DCT + quantize + zig-zag (3 planes,
+  bit-exact vs float64), DC DPCM + AC RLE symbols of every 64-block (Y) / 32-block
+  (Cr, Cb) record: ONE kernel (hic_encode420_slots_u8, the slot layout: no int16
+  coefficients in HBM); the zero runs carried across records, each record's first
+  symbol and the record index: ONE scan launch (hic_rle_slots_close).
+One "step" encodes one such image; its stream is complete on the device (the
+contiguous form is one more launch, hic_rle_slots_compact, for callers that want it).
+--no-slots: the round-5 chain (the fused kernel writes coefficients + records, then
+a scan and an emit kernel).
 
 --gpus N > 1 (BASELINE configs[3]): one process per GPU over RCCL.  `python
 bench.py --gpus N` starts the N ranks itself (torch.multiprocessing, before any
@@ -393,7 +398,13 @@ def extra_8k_luma_batched(nplanes=16, steps=16, warmup=8, floor_us_per_plane=Non
     return out
 
 
-def measure_floors(steps=20):
+def slot_symbols(enc):
+    """Symbols a slot-layout encode wrote into its slots (the n_r of every record:
+    the stream's symbols less the virtual fillers and the EOB)."""
+    return int(sum(int(enc.sidx[k].view(-1, 4)[:, 0].sum().item()) for k in enc.sidx))
+
+
+def measure_floors(steps=20, slots=False):
     """In-run memory floors (hic_probe_copy / hic_probe_plane, memory-only probes in
     the product library), each timed by the launches' own HIP events over >= 1.2 GB
     of rotating buffers:
@@ -461,6 +472,28 @@ def measure_floors(steps=20):
     # 8K RGB image: k_encode420's in-run memory floor
     h, w = H8K, W8K
     px = h * w
+    if slots:
+        # the slot layout's pattern (hic_probe_encode420_slots): each rotating image
+        # encoded once for real, then its records' symbol counts replayed
+        from hiccup_amd import pipeline
+        rot = max(2, int(np.ceil(ROT_BYTES / (7 * px))))
+        g = torch.Generator(device="cuda")
+        g.manual_seed(10)
+        imgs = [torch.randint(0, 256, (h, w, 3), dtype=torch.uint8, device="cuda", generator=g) for _ in range(rot)]
+        encs = [pipeline.Encoder(h, w) for _ in range(rot)]
+        for e, x in zip(encs, imgs):
+            e.encode(x)
+        torch.cuda.synchronize()
+        nbytes = 3 * px + 3 * slot_symbols(encs[0]) + 4 * sum(e.shape[0] for e in encs[0].coef.values())
+        jobs = [e._slot_jobs() for e in encs]
+        us = timed(lambda i, e0, e1: _lib.call("hic_probe_encode420_slots", device.ptr(imgs[i % rot]), h, w,
+                                               jobs[i % rot], device.stream_ptr(), e0, e1))
+        out["encode420_pattern"] = {"image_hw": [h, w], "kernel": "hic_probe_encode420_slots", "bytes_per_launch": nbytes,
+                                    "median_launch_us": round(us, 2), "gbs": round(nbytes / (us * 1e-6) / 1e9, 1),
+                                    "frac_of_8tbs": round(nbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+        del imgs, encs, jobs
+        torch.cuda.empty_cache()
+        return out
     rot = max(2, int(np.ceil(ROT_BYTES / (6 * px))))
     g = torch.Generator(device="cuda")
     g.manual_seed(10)
@@ -498,6 +531,7 @@ def extra_16k_roundtrip(steps=4):
         enc.encode(xs[i % 2])
         if indexed:  # encoder-side tile index, counts stay on the device: no host sync
             return dec.decode(enc.sym_len, enc.sym_val, enc.counts, enc.dc, index=enc.index)
+        enc.compact()  # slot layout: the contiguous stream a bare-stream decoder reads
         counts = enc.counts.cpu().tolist()
         return dec.decode(enc.sym_len, enc.sym_val, counts, enc.dc)
 
@@ -544,11 +578,16 @@ def extra_16k_roundtrip(steps=4):
     same = bool(torch.equal(ref, out_a))
     del xs, enc, dec, enc2, dec2, pairs, ref, out_a
     torch.cuda.empty_cache()
-    return {"workload": "16384x16384 RGB encode + decode round trip, 1 GPU (BASELINE configs[4] at N=1); decode "
-                        "from the encoder-side tile index, RLE decode + IDCT fused per plane "
-                        "(hic_rle_decode_idct_u8_indexed), no host sync between the halves",
+    return {"workload": "16384x16384 RGB encode + decode round trip, 1 GPU (BASELINE configs[4] at N=1); %s"
+                        % ("slot-layout encode (hic_encode420_slots_u8 + hic_rle_slots_close), decode from the "
+                           "slots through the record index (Cr + Cb decode + IDCT in one launch, Y decode + IDCT + "
+                           "pyrUp + colour in one), no host sync between the halves" if enc.slots else
+                           "decode from the encoder-side tile index, RLE decode + IDCT fused per plane "
+                           "(hic_rle_decode_idct_u8_indexed), no host sync between the halves"),
             "ms_per_roundtrip": round(dt * 1e3, 3), "mpix_s": round(n * n / dt / 1e6, 1),
             "ms_per_roundtrip_unindexed_decode": round(res[False] * 1e3, 3),
+            "unindexed_decode_is": "the contiguous stream (hic_rle_slots_compact in the trip), counts through the host, "
+                                   "the bare-stream decode chain",
             "ms_per_roundtrip_2streams": round(dt2 * 1e3, 3), "two_stream_output_equal": same,
             "psnr_db_vs_input": round(10 * np.log10(255.0 ** 2 / mse), 3), "timed_roundtrips": steps}
 
@@ -617,6 +656,7 @@ def _extra_8k_jpeg_decode(steps, codec, device, hicimage, pipeline):
     enc.encode(x)
     blob = pickle.dumps(enc.hic_image().byte_stream())  # the .hic file's bytes (HicImage.write_file)
     symbols = int(sum(enc.counts.cpu().tolist()) * 2 + sum(enc.dc[k].numel() for k in pipeline.CHANNELS))
+    enc.materialize()  # slot layout: the blocks, for the DC check below
     want = device.to_host(enc.coef["lum"][:, 0])
     del x
     t_parse, t_dec = [], []
@@ -755,12 +795,14 @@ def extra_16k_roundtrip_sharded(rank, world, backend, steps=4):
             "psnr_db_vs_input": round(10 * np.log10(255.0 ** 2 / mse), 3), "timed_roundtrips": steps}
 
 
-def load_pmc_traffic(fused):
+def load_pmc_traffic(fused, slots=False):
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC
-    summary (profiles/pmc_encode.json for the fused encoder, profiles/pmc_dct.json
-    for the two-kernel chain's DCT: FETCH_SIZE / WRITE_SIZE calibrated on kernels of
-    known traffic with the same access pattern, MI355X_MICROARCH.md HBM section)."""
-    p = os.path.join(HERE, "profiles", "pmc_encode.json" if fused else "pmc_dct.json")
+    summary (profiles/pmc_encode_slots.json for the slot-layout kernel,
+    pmc_encode.json for the fused encoder writing coefficients, pmc_dct.json for the
+    two-kernel chain's DCT: FETCH_SIZE / WRITE_SIZE calibrated on kernels of known
+    traffic with the same access pattern, MI355X_MICROARCH.md HBM section)."""
+    p = os.path.join(HERE, "profiles", "pmc_encode_slots.json" if slots else
+                     "pmc_encode.json" if fused else "pmc_dct.json")
     if not os.path.exists(p):
         return None
     with open(p) as f:
@@ -1087,8 +1129,14 @@ def main():
                      % (len(streams), " and grouped gathers" if gather else ""))
     # algorithmic bytes of the timed launch: the two-kernel chain's DCT reads 1 B and
     # writes 2 B per plane pixel; the fused kernel reads the RGB (3 B per image
-    # pixel) and writes the same coefficients
-    roof_bytes = dct_px * 2 + (px_per_step_rank * 3 if fused else dct_px)
+    # pixel) and writes the same coefficients -- or, in the slot layout, the symbols
+    # it emits (1 B length + 2 B value each) and the DC differences (4 B per block)
+    slots = world == 1 and enc0.slots
+    nsym_slots = slot_symbols(enc0) if slots else None
+    if slots:
+        roof_bytes = px_per_step_rank * 3 + 3 * nsym_slots + 4 * (dct_px // 64)
+    else:
+        roof_bytes = dct_px * 2 + (px_per_step_rank * 3 if fused else dct_px)
     achieved = roof_bytes / (dct_us * 1e-6) / 1e9
 
     # context for the gathered strong-scaling line: the same steps with the stream
@@ -1137,7 +1185,7 @@ def main():
         med_ms = float(np.median(region_ms))
         value = total_px / (med_ms * args.steps * 1e-3) / 1e6
         value_first = total_px / elapsed / 1e6
-        pmc = load_pmc_traffic(fused)
+        pmc = load_pmc_traffic(fused, slots)
         cfg_idx = 2 if world == 1 else 3
         wl = ("%dx%d RGB -> YCrCb 4:2:0 full encode: colour+pyrDown, 8x8 DCT+quantize+zig-zag (3 planes), "
               "DC DPCM + AC RLE (3 planes)" % (W0, H0))
@@ -1198,7 +1246,11 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": ("k_encode420<15> (RGB -> YCrCb + 4:2:0 pyrDown + AAN DCT + quantize + zig-zag + RLE "
+                "kernel": ("k_encode420<15,slots> (RGB -> YCrCb + 4:2:0 pyrDown + AAN DCT + quantize + zig-zag + the "
+                           "AC symbols and DC differences of every RLE record, slot layout, in one launch; algorithmic "
+                           "bytes = 3 B RGB read per pixel + 3 B per symbol written (%d symbols, the last image's) + "
+                           "4 B per block's DC difference)" % nsym_slots if slots else
+                           "k_encode420<15> (RGB -> YCrCb + 4:2:0 pyrDown + AAN DCT + quantize + zig-zag + RLE "
                            "tile records of the rank's image/shard in one launch; algorithmic bytes = 3 B RGB read + "
                            "2 B int16 written per Y / Cr / Cb coefficient)" if fused else
                            plane_kernel(15) + " (Y + Cr + Cb of the rank's image/shard in one launch: "
@@ -1218,7 +1270,7 @@ def main():
             },
         }
         if world == 1:
-            floors = measure_floors()
+            floors = measure_floors(slots=slots)
             out["memory_floors"] = floors
             out["roofline"]["device_copy_gbs"] = floors["device_copy_gbs"]
             out["roofline"]["frac_of_device_copy"] = round(achieved / floors["device_copy_gbs"], 4)
@@ -1227,7 +1279,9 @@ def main():
                 fl = floors["encode420_pattern"]["median_launch_us"]
                 out["roofline"]["memory_floor_us"] = fl
                 out["roofline"]["frac_of_memory_floor"] = round(fl / dct_us, 4)
-                out["roofline"]["memory_floor_source"] = "memory_floors.encode420_pattern (hic_probe_encode420, this run)"
+                out["roofline"]["memory_floor_source"] = ("memory_floors.encode420_pattern (%s, this run)" %
+                                                          ("hic_probe_encode420_slots" if slots else
+                                                           "hic_probe_encode420"))
             # the headline normalised by this box's own streaming copy rate (box-to-box
             # HBM / clock spread divides out): Mpix/s per GB/s of measured device copy
             out["value_per_copy_gbs"] = round(value / floors["device_copy_gbs"], 5)

@@ -92,6 +92,7 @@ SIGNATURES = {
     "hic_rle_slots_workspace_bytes": (_sz, [_i64, _int]),
     "hic_encode420_slots_u8": (_int, [_vp, _i64, _i64, _vp, _int, _vp, _vp, _vp]),
     "hic_rle_slots_close": (_int, [_int, _vp, _int, _vp]),
+    "hic_probe_encode420_slots": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp]),
     "hic_rle_slots_compact": (_int, [_int, _vp, _int, _vp]),
     "hic_rle_decode_i16_slots": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _vp, _vp, _vp, _vp]),
     "hic_rle_decode_idct_u8_slots": (_int, [_vp, _vp, _vp, _vp, _vp, _int, _i64, _i64, _int, _vp, _i64, _vp, _vp]),

@@ -643,16 +643,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DCT_WPE
     int kj = g0 < jobs.total_sets ? job_of(g0) : 0;
     DctJob J = jobs.j[kj];
     int next0 = kj + 1 < jobs.n ? jobs.j[kj + 1].set0 : jobs.total_sets;
-    // software pipeline (path 1): the next set's pixels load while this one computes.
-    // HIC_DCT_PF 0 (default): compiled out, path 1 runs as path 2 -- 149 instead of
-    // 160 VGPRs, and 8K luma 25.6-26.2 vs 27.6-27.7 us, 4K luma 12.2 vs 13.6 us on
-    // one box (profiles/r03/s2/dct_pf/); the other waves of the SIMD hide the loads
-#ifndef HIC_DCT_PF
-#define HIC_DCT_PF 0
-#endif
-    if (!HIC_DCT_PF && path == 1) path = 2;
-    uint2 wn[8];
-    if (HIC_DCT_PF && path == 1) load(J, g0 - J.set0, wn);
+    // (a software-pipelined load of the next set's pixels was measured slower and
+    // removed: 160 vs 149 VGPRs, 8K luma 27.6-27.7 vs 25.6-26.2 us, profiles/r03/s2/dct_pf/;
+    // the other waves of the SIMD hide the loads)
     for (int g = g0; g < jobs.total_sets; g += nwaves, ++i) {
       if (g >= next0) {
         kj = job_of(g);
@@ -661,17 +654,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DCT_WPE
       }
       const int set = g - J.set0;
       uint2 w[8];
-      if (HIC_DCT_PF && path == 1) {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) w[r] = wn[r];
-        const int gn = g + nwaves;
-        if (gn < jobs.total_sets) {
-          const int kn = gn >= next0 ? job_of(gn) : kj;
-          load(jobs.j[kn], gn - jobs.j[kn].set0, wn);
-        }
-      } else {
-        load(J, set, w);
-      }
+      load(J, set, w);
       bool t26 = false;
       const bool f = dct_block_aan<TABLE, LAYOUT>(w, st, &t26, nullptr, J.table);
       if (__builtin_amdgcn_ballot_w64(f) != 0) redo |= 1ull << i;

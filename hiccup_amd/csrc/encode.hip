@@ -66,6 +66,7 @@ struct Enc420 {
   int16_t *sval[3];
   int32_t *dc[3];
   int32_t *rdc[3];
+  const int32_t *nsym[3];  // hic_probe_encode420_slots: the record index (n_r) it replays
 };
 
 constexpr int kZZ = HIC_LAYOUT_ZIGZAG_I16;
@@ -533,7 +534,22 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
 // Memory-only probe of k_encode420's byte pattern (bench.py's in-run floor for the
 // fused kernel): the same grid, unit order and 19 row loads per unit, the LDS stage
 // and the three passes' 1 KiB nontemporal stores plus their records, no colour
-// conversion, pyrDown, DCT or RLE summary.
+// conversion, pyrDown, DCT or RLE summary.  SLOTS: the slot layout's outputs instead
+// -- each record's n_r symbols (read from the index of an earlier real encode into
+// the same buffers) copied out of the stage in the kernel's 16 + 32 B nontemporal
+// stores, the DC differences, the record and its last DC.
+__device__ __forceinline__ void probe_slot_out(const uint2 *st2, int lane, int n, uint8_t *len, int16_t *val) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const uint4 *src = reinterpret_cast<const uint4 *>(st2);
+  for (int c = lane; 16 * c < n; c += 64) {
+    const uint4 p = src[(2 * c) & 511], q = src[(2 * c + 1) & 511];
+    __builtin_nontemporal_store(u32x4{p.x ^ q.y, p.y ^ q.x, p.z ^ q.w, p.w ^ q.z}, reinterpret_cast<u32x4 *>(len) + c);
+    __builtin_nontemporal_store(u32x4{p.x, p.y, p.z, p.w}, reinterpret_cast<u32x4 *>(val) + 2 * c);
+    __builtin_nontemporal_store(u32x4{q.x, q.y, q.z, q.w}, reinterpret_cast<u32x4 *>(val) + 2 * c + 1);
+  }
+}
+
+template <bool SLOTS = false>
 __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_eu(3))) void k_probe_encode420(
     Enc420 E) {
   __shared__ __attribute__((aligned(16))) uint2 s_stage[HIC_ENC_WPB * 64 * kStageU2];
@@ -556,6 +572,21 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
 #pragma unroll
     for (int k = 0; k < 16; ++k) row[k] = make_uint2(yq[k].x ^ p, yq[k].y);
     __builtin_amdgcn_wave_barrier();
+    if constexpr (SLOTS) {
+      const int64_t b0 = p < 2 ? (int64_t)(2 * u0 + p) * nbx + 64 * s : (int64_t)u0 * nbxc + 32 * s;
+      const int64_t r = p < 2 ? b0 >> 6 : b0 >> 5;
+      const int np = p < 2 ? 1 : 2;
+      for (int h = 0; h < np; ++h) {
+        const int k = p < 2 ? 0 : 1 + h, cap = p < 2 ? kSlotY : kSlotC;
+        const int n = __builtin_amdgcn_readfirstlane(E.nsym[k][4 * r]);
+        probe_slot_out(st2, lane, n, E.slen[k] + r * cap, E.sval[k] + r * cap);
+        if (lane < (p < 2 ? 64 : 32)) E.dc[k][b0 + lane] = (int)yq[lane & 15].x;
+        if (lane < 3) E.rec[k][r * 3 + lane] = yq[p].y;
+        if (lane == 0) E.rdc[k][r] = (int)yq[p].x;
+      }
+      __builtin_amdgcn_wave_barrier();
+      continue;
+    }
     int16_t *lo, *hi;
     int64_t *rec;
     if (p < 2) {
@@ -773,8 +804,55 @@ extern "C" int hic_probe_encode420(const uint8_t *rgb, int64_t H, int64_t W, int
   const hipStream_t s = as_stream(stream);
   const hipEvent_t e0 = static_cast<hipEvent_t>(ev_start), e1 = static_cast<hipEvent_t>(ev_stop);
   if (e0 || e1)
-    hipExtLaunchKernelGGL(k_probe_encode420, grid, block, 0, s, e0, e1, 0, E);
+    hipExtLaunchKernelGGL(k_probe_encode420<false>, grid, block, 0, s, e0, e1, 0, E);
   else
-    hipLaunchKernelGGL(k_probe_encode420, grid, block, 0, s, E);
+    hipLaunchKernelGGL(k_probe_encode420<false>, grid, block, 0, s, E);
   return check_launch("k_probe_encode420");
+}
+
+extern "C" int hic_probe_encode420_slots(const uint8_t *rgb, int64_t H, int64_t W, const hic_slot_job *jobs,
+                                         void *stream, void *ev_start, void *ev_stop) {
+  if (!rgb || !jobs) return arg_error("null pointer");
+  if (H < 16 || W < 512 || H % 16 || W % 512 || H >= (1 << 20) || W >= (1 << 20))
+    return arg_error("hic_probe_encode420_slots needs W %% 512 == 0 and H %% 16 == 0");
+  if (H * W * 3 > INT32_MAX) return arg_error("image exceeds 2 GiB");
+  if (reinterpret_cast<uintptr_t>(rgb) % 8) return arg_error("alignment");
+  const int64_t nblk[3] = {(H / 8) * (W / 8), (H / 16) * (W / 16), (H / 16) * (W / 16)};
+  const int rpt[3] = {1, 2, 2};
+  Enc420 E{};
+  for (int k = 0; k < 3; ++k) {
+    const hic_slot_job &J = jobs[k];
+    if (!J.slot_len || !J.slot_val || !J.dc_diff || !J.workspace || !J.d_index) return arg_error("job %d: null", k);
+    if (J.nblk != nblk[k] || J.records_per_tile != rpt[k]) return arg_error("job %d: shape", k);
+    if ((reinterpret_cast<uintptr_t>(J.slot_len) | reinterpret_cast<uintptr_t>(J.slot_val)) % 16)
+      return arg_error("job %d: alignment", k);
+    if (J.workspace_bytes < (int64_t)hic_rle_slots_workspace_bytes(nblk[k], rpt[k])) return arg_error("workspace");
+    E.rec[k] = static_cast<int64_t *>(J.workspace);
+    E.slen[k] = J.slot_len;
+    E.sval[k] = J.slot_val;
+    E.dc[k] = J.dc_diff;
+    E.rdc[k] = reinterpret_cast<int32_t *>(E.rec[k] + slot_rdc_word(slot_nrec(nblk[k], rpt[k])));
+    E.nsym[k] = J.d_index;
+  }
+  E.rgb = rgb;
+  E.in_row0 = 0;
+  E.in_rows = (int)H;
+  E.H = (int)H;
+  E.W = (int)W;
+  E.out_row0 = 0;
+  E.out_rows = (int)H;
+  E.nstrips = (int)(W / 512);
+  E.wlast = 512;
+  E.nunits = E.nstrips * (int)(H / 16);
+  const int order = knob(HIC_KNOB_ENCODE_ORDER);
+  E.xcd = (order >> 1) & 1;
+  E.alt = (order >> 2) & 1;
+  const dim3 grid((unsigned)((E.nunits + HIC_ENC_WPB - 1) / HIC_ENC_WPB)), block(64 * HIC_ENC_WPB);
+  const hipStream_t s = as_stream(stream);
+  const hipEvent_t e0 = static_cast<hipEvent_t>(ev_start), e1 = static_cast<hipEvent_t>(ev_stop);
+  if (e0 || e1)
+    hipExtLaunchKernelGGL(k_probe_encode420<true>, grid, block, 0, s, e0, e1, 0, E);
+  else
+    hipLaunchKernelGGL(k_probe_encode420<true>, grid, block, 0, s, E);
+  return check_launch("k_probe_encode420<slots>");
 }

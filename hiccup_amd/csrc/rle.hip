@@ -159,26 +159,6 @@ __global__ __launch_bounds__(kTB) void k_rle_tile(const T *__restrict__ blocks, 
 constexpr int kScanT = 1024;
 constexpr int kScanK = 8;  // tiles per thread per pass
 
-// Phase timestamps for the dev harness (tools/micro/scan_stamps.hip); compiled out
-// of the library.
-#ifdef HIC_STAMPS
-__device__ unsigned long long g_stamps[64];
-#define HIC_STAMP(i) \
-  if (threadIdx.x == 0 && blockIdx.x == 0) g_stamps[i] = __builtin_amdgcn_s_memtime()
-__device__ unsigned long long g_phase[16];
-__device__ unsigned long long g_tphase[1 << 16][8];  // per tile, per phase (no contention)
-#define HIC_PHASE_BEGIN unsigned long long hic_t0 = __builtin_amdgcn_s_memtime()
-#define HIC_PHASE(i)                                                          \
-  do {                                                                        \
-    const unsigned long long hic_t1 = __builtin_amdgcn_s_memtime();          \
-    if ((threadIdx.x & 63) == 0) g_tphase[(b / 64) & 0xFFFF][i] = hic_t1 - hic_t0; \
-    hic_t0 = hic_t1;                                                          \
-  } while (0)
-#else
-#define HIC_STAMP(i)
-#define HIC_PHASE_BEGIN
-#define HIC_PHASE(i)
-#endif
 
 struct Agg {
   int64_t first, last, cnt;
@@ -204,7 +184,6 @@ __device__ __forceinline__ void scan_tiles(const int64_t *__restrict__ tiles, in
   const bool emit_eob = stitch ? stitch[1] != 0 : true;
   const int64_t p0 = -1 - carry;  // virtual last nonzero before the stream
   Agg run{-1, -1, 0};             // aggregate of all tiles of earlier passes
-  HIC_STAMP(0);
   for (int64_t c0 = 0; c0 < ntiles; c0 += (int64_t)kScanT * kScanK) {
     const int64_t t0 = c0 + (int64_t)threadIdx.x * kScanK;
     Agg rec[kScanK];
@@ -216,7 +195,6 @@ __device__ __forceinline__ void scan_tiles(const int64_t *__restrict__ tiles, in
     Agg mine = rec[0];
 #pragma unroll
     for (int k = 1; k < kScanK; ++k) mine = agg_combine(mine, rec[k], M);
-    HIC_STAMP(1);
     // workgroup-wide inclusive scan of the per-thread aggregates
     Agg incl = mine;
 #pragma unroll
@@ -224,10 +202,8 @@ __device__ __forceinline__ void scan_tiles(const int64_t *__restrict__ tiles, in
       const Agg o = agg_shfl_up(incl, d);
       if (lane >= d) incl = agg_combine(o, incl, M);
     }
-    HIC_STAMP(2);
     if (lane == 63) s_wave[wave] = incl;
     __syncthreads();
-    HIC_STAMP(3);
     // wave 0 scans the 16 wave totals (exclusive) in place; lane 15 also forms the
     // aggregate of everything so far
     if (wave == 0) {
@@ -250,7 +226,6 @@ __device__ __forceinline__ void scan_tiles(const int64_t *__restrict__ tiles, in
     excl = agg_combine(s_wave[wave], excl, M);
     const Agg all = s_wave[kScanT / 64];
     __syncthreads();
-    HIC_STAMP(4);
     // state entering this thread's first tile
     int64_t prev = excl.last >= 0 ? excl.last : p0;
     int64_t off = excl.last >= 0 ? excl.cnt + syms_for_run(excl.first - p0 - 1, M) : 0;
@@ -267,7 +242,6 @@ __device__ __forceinline__ void scan_tiles(const int64_t *__restrict__ tiles, in
       }
     }
     run = all;
-    HIC_STAMP(5);
   }
   if (threadIdx.x == 0) {
     const int64_t last = run.last >= 0 ? run.last : p0;
@@ -447,11 +421,9 @@ __device__ __forceinline__ void emit_tile16(const uint32_t (&w)[32], const int16
                                             uint8_t *s_len, int16_t *s_val, uint8_t *__restrict__ sym_len,
                                             int16_t *__restrict__ sym_val, int64_t cap) {
   const int lane = threadIdx.x & 63;
-  HIC_PHASE_BEGIN;
   int first = -1, last = -1, nsym = 0;
   uint64_t ac = 0;
   if (valid) summarize16<MF>(w, M, first, last, nsym, &ac);
-  HIC_PHASE(1);
   const int64_t base = b * 63;
   // in-tile positions (lane * 63 + j) and counts fit int32: DPP scans
   const int incl = wave_incl_max_i32(last >= 0 ? lane * 63 + last : -1);
@@ -463,7 +435,6 @@ __device__ __forceinline__ void emit_tile16(const uint32_t (&w)[32], const int16
   const int incl_cnt = wave_incl_sum_i32(cnt);
   const int total = wave_last_i32(incl_cnt);
   const int64_t o_thr = o_tile + incl_cnt - cnt;
-  HIC_PHASE(2);
   const bool staged = total <= kWSyms;  // uniform across the wave
   // stage offsets congruent to the output position mod 16 bytes (16-byte copy-out)
   const int lo = (int)(o_tile & 15), vo = (int)(o_tile & 7);
@@ -567,14 +538,11 @@ __device__ __forceinline__ void emit_tile16(const uint32_t (&w)[32], const int16
     }
   }
   __builtin_amdgcn_wave_barrier();
-  HIC_PHASE(3);
   // (no vmcnt drain here: the copy-out reads only this wave's LDS stage, so the
   // next tile's prefetch stays in flight across it)
-  HIC_PHASE(4);
   if (staged) {
     copy_out_wave16<uint8_t, NT>(s_len, lo, sym_len, o_tile, (int)total, cap);
     copy_out_wave16<int16_t, NT>(s_val, vo, sym_val, o_tile, (int)total, cap);
-    HIC_PHASE(5);
   } else {
     // long carried runs: the whole wave writes each lane's fillers
     uint64_t m = __ballot(nf0 > 0);

@@ -244,6 +244,14 @@ int hic_rle_decode_idct_rgb_slots(const uint8_t *slot_len, const int16_t *slot_v
                                   const int32_t *dc_diff, const int32_t *d_index, int records_per_tile, int64_t H,
                                   int64_t W, const uint8_t *cr, const uint8_t *cb, uint8_t *rgb, int64_t rgb_stride,
                                   int64_t *d_status, void *stream);
+/* hic_probe_encode420_slots: the slot-layout kernel's byte pattern, memory only (a
+ * probe as hic_probe_encode420, bench.py's in-run floor): the same grid, unit order
+ * and row loads, and per record the n_r symbols its jobs' d_index holds from an
+ * earlier hic_encode420_slots_u8 + hic_rle_slots_close into the same buffers (16 +
+ * 32 B nontemporal stores per 16 symbols), the DC differences, the record and its
+ * last DC, with garbage values. */
+int hic_probe_encode420_slots(const uint8_t *rgb, int64_t H, int64_t W, const hic_slot_job *jobs, void *stream,
+                              void *ev_start, void *ev_stop);
 /* Timing events (hipEvent_t handles) for the *_timed entry points. */
 int hic_event_create(void **h_event);
 int hic_event_destroy(void *event);

@@ -1046,6 +1046,7 @@ def main():
         torch.cuda.synchronize()
         ref = pipeline.Encoder(H, W0)
         ref.encode(full)
+        ref.materialize()  # slot layout: the contiguous stream and the blocks compared below
         torch.cuda.synchronize()
         got = encs[rank].whole
         same = True

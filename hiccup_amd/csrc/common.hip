@@ -83,8 +83,12 @@ extern "C" int hic_set_knob(int k, int value) {
     return hic::arg_error("dct path %d (0 exact, 1 / 2 float64 AAN)", value);
   if (k == HIC_KNOB_COLOR_SEG && value != -1 && value != 8 && value != 16) return hic::arg_error("colour segment");
   // retired knobs (measured slower, removed in rounds 4-5: 9-12 encode waves / nontemporal
-  // stores / integer-MFMA transforms, 14-15 the packed-float32 transforms)
-  if ((k >= 9 && k <= 12) || k == 14 || k == 15) return hic::arg_error("knob %d is retired", k);
+  // stores / integer-MFMA transforms, 14-15 the packed-float32 transforms): -1 (the
+  // default) is accepted as a no-op, so a caller resetting every knob still can
+  if ((k >= 9 && k <= 12) || k == 14 || k == 15) {
+    if (value == -1) return HIC_OK;
+    return hic::arg_error("knob %d is retired", k);
+  }
   if (k == HIC_KNOB_ENCODE_ORDER && value != -1 && (value < 0 || value > 7 || (value & 1)))
     return hic::arg_error("encode_order 0, 2, 4 or 6");
   if (value < -1) return hic::arg_error("knob value %d", value);

@@ -923,12 +923,17 @@ extern "C" int hic_dct_quant_rle_u8_batch(int n, const hic_dct_plane_job *jobs, 
   // rle_workspace: every job's or none (NULL: the records-free pass, DCT + quantize +
   // zig-zag only)
   const bool recs = jobs[0].rle_workspace != nullptr;
+  // every job is checked before anything is launched (an error on job k > 0
+  // used to return after the ragged planes before it were queued)
   for (int k = 0; k < n; ++k) {
     const hic_dct_plane_job &a = jobs[k];
     if (!a.plane || !a.out) return arg_error("plane %d: null pointer", k);
     if ((a.rle_workspace != nullptr) != recs) return arg_error("plane %d: rle_workspace for every plane or none", k);
     if (!dims_ok(a.H, a.W) || a.stride < a.W) return arg_error("plane %d: shape / stride", k);
     if (a.table_id != HIC_TABLE_LUMINANCE && a.table_id != HIC_TABLE_CHROMINANCE) return arg_error("plane %d: table_id", k);
+  }
+  for (int k = 0; k < n; ++k) {
+    const hic_dct_plane_job &a = jobs[k];
     const int h = (int)a.H, w = (int)a.W;
     int64_t *tiles = static_cast<int64_t *>(a.rle_workspace);
     if (fwd_fast(h, w, a.stride, a.plane, a.out)) {

@@ -165,14 +165,22 @@ __device__ __forceinline__ void slot_pass(const uint32_t (&zw)[32], uint2 *st2, 
     uint32_t la = lds_addr(sb + o + nf0);
     const bool d = dense && first >= 0;
     int pl = first - 1 - rem;
+    // AC j is zig-zag slot j + 1: the low half of zw[(j + 1) / 2] for odd j, the
+    // high half for even j.  The packed word is formed without extracting the value:
+    // low half, (w << 4) | len (the store keeps 16 bits); high half, (w >> 12) with
+    // its low nibble replaced by len.
 #pragma unroll
     for (int j = 0; j < 63; ++j) {
-      const int v = zz_ac(zw, j);
-      const bool nz = v != 0 && d;
+      const uint32_t w = zw[(j + 1) >> 1];
+      const bool lo = ((j + 1) & 1) == 0;
+      const bool nzv = lo ? (uint16_t)w != 0 : w > 0xFFFFu;
+      const uint32_t len = (uint32_t)(j - pl - 1);
+      const uint32_t pk = lo ? ((w << 4) | len) : (((w >> 12) & 0xFFF0u) | len);
+      const bool nz = nzv && d;
       const uint32_t a = nz ? la : ldum;
-      *(lds_u16 *)(uintptr_t)a = (uint16_t)(((uint32_t)v << 4) | (uint32_t)(j - pl - 1));
+      *(lds_u16 *)(uintptr_t)a = (uint16_t)pk;
       la += nz ? 2u : 0u;
-      pl = v != 0 ? j : pl;
+      pl = nzv ? j : pl;
     }
   }
   if (__builtin_amdgcn_ballot_w64(!dense && first >= 0)) {

@@ -92,7 +92,7 @@ def encoder_layout(H, W, rows=None, fused=None, index=False):
 def slots_eligible(H, W, max_len=15, rows=None, out=None, fused=None, landing_rpt=None):
     """Whether an Encoder of this shape can take the slot layout (hic_encode420_slots_u8:
     a whole image, W % 512 == 0, H % 16 == 0, max_len 15, < 2 GiB of RGB)."""
-    return (rows in (None, (0, H)) and out is None and landing_rpt is None and fused is not False and max_len == 15
+    return (rows is None and out is None and landing_rpt is None and fused is not False and max_len == 15
             and W % 512 == 0 and H % 16 == 0 and H >= 16 and H * W * 3 <= 2**31 - 1)
 
 

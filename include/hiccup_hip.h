@@ -76,9 +76,10 @@ int hic_device_count(int *h_n);
 #define HIC_KNOB_RLD_GENERIC 7      /* 1: the generic (any block size) RLE decode */
 #define HIC_KNOB_DEV 8              /* dev builds only (-DHIC_DEV): timing bits that skip work; refused otherwise */
 /* knobs 9-12 were retired in rounds 4-5 (encode waves / nontemporal stores / integer-MFMA
- * transforms: measured slower, removed); hic_set_knob refuses them */
+ * transforms: measured slower, removed); hic_set_knob refuses any value but -1 for them
+ * (-1, the default, is a no-op: resetting every knob 0 .. HIC_KNOB_COUNT - 1 works) */
 #define HIC_KNOB_ENCODE_ORDER 13     /* hic_encode420_u8 unit order: 0 row-major; + 2: workgroups remapped XCD-major (neighbouring units on one XCD's L2); + 4: odd unit rows run their colour rows bottom-up (the halo rows two unit rows share fetched at the same time); default 6; odd values refused */
-/* 14, 15: retired in round 5 with the packed-float32 transforms (refused) */
+/* 14, 15: retired in round 5 with the packed-float32 transforms (refused, -1 a no-op) */
 #define HIC_KNOB_COUNT 16
 int hic_set_knob(int knob, int value);
 int hic_get_knob(int knob, int *h_value);

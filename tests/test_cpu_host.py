@@ -136,8 +136,11 @@ def test_knob_defaults_and_ranges():
         assert _lib.get_knob("dct_path") == 0
     for bad in (3, 4, 5, -2):  # 3 / 4: the packed and two-lane kernels, removed in round 5
         assert _lib.load().hic_set_knob(0, bad) == _lib.HIC_ERR_ARG
-    for retired in (9, 10, 11, 12, 14, 15):  # retired knobs are refused outright
+    for retired in (9, 10, 11, 12, 14, 15):  # retired knobs: any value but the default is refused
         assert _lib.load().hic_set_knob(retired, 0) == _lib.HIC_ERR_ARG
+    # resetting every knob to its default works (-1 on a retired knob is a no-op)
+    for k in range(16):
+        assert _lib.load().hic_set_knob(k, -1) == _lib.HIC_OK, k
 
 
 def _names(d, prefix):

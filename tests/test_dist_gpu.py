@@ -62,6 +62,7 @@ def _rank(rank, world, port, H, W, flat_rows, out_path):
     sd.check_status()
     whole = pipeline.Encoder(H, W)
     whole.encode(device.to_device(rgb))
+    whole.compact()  # a slot-layout encoder: the contiguous stream the plain decode reads
     wd = pipeline.Decoder(H, W)
     exp = device.to_host(wd.decode(whole.sym_len, whole.sym_val, whole.counts.cpu().tolist(), whole.dc))
     r0, r1 = sd.out_rows

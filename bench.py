@@ -526,6 +526,7 @@ def extra_16k_roundtrip(steps=4):
     g.manual_seed(5)
     xs = [torch.randint(0, 256, (n, n, 3), dtype=torch.uint8, device="cuda", generator=g) for _ in range(2)]
     enc, dec = pipeline.Encoder(n, n, index=True), pipeline.Decoder(n, n)
+    slots = enc.slots
 
     def trip(i, indexed):
         enc.encode(xs[i % 2])
@@ -581,7 +582,7 @@ def extra_16k_roundtrip(steps=4):
     return {"workload": "16384x16384 RGB encode + decode round trip, 1 GPU (BASELINE configs[4] at N=1); %s"
                         % ("slot-layout encode (hic_encode420_slots_u8 + hic_rle_slots_close), decode from the "
                            "slots through the record index (Cr + Cb decode + IDCT in one launch, Y decode + IDCT + "
-                           "pyrUp + colour in one), no host sync between the halves" if enc.slots else
+                           "pyrUp + colour in one), no host sync between the halves" if slots else
                            "decode from the encoder-side tile index, RLE decode + IDCT fused per plane "
                            "(hic_rle_decode_idct_u8_indexed), no host sync between the halves"),
             "ms_per_roundtrip": round(dt * 1e3, 3), "mpix_s": round(n * n / dt / 1e6, 1),

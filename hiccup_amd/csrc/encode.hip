@@ -438,7 +438,6 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
   static_assert(!SLOTS || TMF == kSlotM, "the slot layout packs 4-bit lengths (max_len 15)");
   __shared__ __attribute__((aligned(16))) uint2 s_stage[HIC_ENC_WPB * 64 * kStageU2];
   __shared__ uint32_t s_chroma_all[HIC_ENC_WPB][2 * 8 * 64];
-  __shared__ uint32_t s_dummy[SLOTS ? HIC_ENC_WPB * 64 : 1];  // slot_pass's per-lane dummy dwords
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint2 *st2 = s_stage + wv * 64 * kStageU2;
   uint32_t *s_chroma = s_chroma_all[wv];
@@ -470,7 +469,7 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
       const int64_t r = b0 >> 6;  // W % 512 == 0: block row segments are whole tiles
       const SlotRec A{E.slen[0] + r * kSlotY, E.sval[0] + r * kSlotY, E.dc[0] + b0, E.rec[0] + r * 3, E.rdc[0] + r,
                       b0 * 63};
-      slot_pass<false, true>(zw, st2, s_dummy + wv * 64 + lane, lane, A, A);
+      slot_pass<false, true>(zw, st2, lane, A, A);
       __builtin_amdgcn_sched_barrier(0);
       return;
     }
@@ -507,7 +506,7 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
                       b0 * 63};
       const SlotRec B{E.slen[2] + r * kSlotC, E.sval[2] + r * kSlotC, E.dc[2] + b0, E.rec[2] + r * 3, E.rdc[2] + r,
                       b0 * 63};
-      slot_pass<true, false>(zw, st2, s_dummy + wv * 64 + lane, lane, A, B);
+      slot_pass<true, false>(zw, st2, lane, A, B);
       __builtin_amdgcn_sched_barrier(0);
       return;
     }
@@ -539,13 +538,17 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
 // the same buffers) copied out of the stage in the kernel's 16 + 32 B nontemporal
 // stores, the DC differences, the record and its last DC.
 __device__ __forceinline__ void probe_slot_out(const uint2 *st2, int lane, int n, uint8_t *len, int16_t *val) {
+  // slot_pass's copy-out: 16 lengths (from 32 B of the stage) and 8 values (16 B) per
+  // lane per store, each store instruction 1 KiB contiguous
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const uint4 *src = reinterpret_cast<const uint4 *>(st2);
   for (int c = lane; 16 * c < n; c += 64) {
     const uint4 p = src[(2 * c) & 511], q = src[(2 * c + 1) & 511];
     __builtin_nontemporal_store(u32x4{p.x ^ q.y, p.y ^ q.x, p.z ^ q.w, p.w ^ q.z}, reinterpret_cast<u32x4 *>(len) + c);
-    __builtin_nontemporal_store(u32x4{p.x, p.y, p.z, p.w}, reinterpret_cast<u32x4 *>(val) + 2 * c);
-    __builtin_nontemporal_store(u32x4{q.x, q.y, q.z, q.w}, reinterpret_cast<u32x4 *>(val) + 2 * c + 1);
+  }
+  for (int c = lane; 8 * c < n; c += 64) {
+    const uint4 p = src[c & 511];
+    __builtin_nontemporal_store(u32x4{p.x, p.y, p.z, p.w}, reinterpret_cast<u32x4 *>(val) + c);
   }
 }
 

@@ -91,13 +91,13 @@ __device__ __forceinline__ void slot_symbols_general(const uint32_t (&zw)[32], i
 }
 
 // One pass's emission (see the file comment).  zw: this lane's block; st2: the
-// wave's stage (every block already read out of it); dummy: this lane's private
-// LDS dword.  SEG: lanes 0-31 hold record A's 32 blocks and 32-63 record B's
-// (the chroma pass, Cr and Cb); else one 64-block record A.  CHECK_WIDE: the
-// luminance table (zig-zag slot 3 can need 13 bits).  Every lane must call it.
+// wave's stage, still holding every block (this lane's in row `lane`).  SEG: lanes
+// 0-31 hold record A's 32 blocks and 32-63 record B's (the chroma pass, Cr and
+// Cb); else one 64-block record A.  CHECK_WIDE: the luminance table (zig-zag slot 3
+// can need 13 bits).  Every lane must call it.
 template <bool SEG, bool CHECK_WIDE, bool NT = true>
-__device__ __forceinline__ void slot_pass(const uint32_t (&zw)[32], uint2 *st2, uint32_t *dummy, int lane,
-                                          const SlotRec &A, const SlotRec &B) {
+__device__ __forceinline__ void slot_pass(const uint32_t (&zw)[32], uint2 *st2, int lane, const SlotRec &A,
+                                          const SlotRec &B) {
   const int sl = SEG ? (lane & 31) : lane;
   const bool hi = SEG && lane >= 32;
   const SlotRec &R = hi ? B : A;
@@ -106,6 +106,8 @@ __device__ __forceinline__ void slot_pass(const uint32_t (&zw)[32], uint2 *st2, 
   int first, last, nsym;
   summarize_ac<kSlotM>(ac, kSlotM, first, last, nsym);
   const bool dense = nsym == __builtin_popcountll(ac) - 1;  // no run >= 15 inside the block
+  // the first nonzero's value, from the stage before it is overwritten
+  const int vfirst = first >= 0 ? reinterpret_cast<const int16_t *>(st2 + lane * kStageU2)[1 + first] : 0;
   // DC differences inside the record; its first block keeps its raw DC (the close
   // subtracts the previous record's last DC)
   const int dc = (int)(int16_t)(zw[0] & 0xFFFFu);
@@ -155,15 +157,15 @@ __device__ __forceinline__ void slot_pass(const uint32_t (&zw)[32], uint2 *st2, 
   }
   // ---- 3. packed symbols into the stage, in place
   uint16_t *sb = reinterpret_cast<uint16_t *>(st2) + (hi ? 32 * kStageRowU16 : 0);
-  if (first >= 0) {
-    for (int k = 0; k < nf0; ++k) sb[o + k] = (uint16_t)(kSlotM - 1);
-  }
   {
-    // dense blocks, branch-free: a zero (or a lane of a general block) writes the
-    // lane's dummy dword and does not advance
-    const uint32_t ldum = lds_addr(dummy);
+    // Branch-free over the block's 63 AC: EVERY coefficient writes the lane's next
+    // free slot, which only a nonzero advances -- a zero's word is overwritten by the
+    // next nonzero's.  After a lane's last nonzero (or in an all-zero block) its
+    // writes land on the first slot of the next lane with symbols, and are undone
+    // below, after the loop, where every lane writes its carried fillers and its
+    // first symbol again.  A block with a run >= 15 inside (not dense) writes within
+    // its own symbols here, and the general loop after writes them all.
     uint32_t la = lds_addr(sb + o + nf0);
-    const bool d = dense && first >= 0;
     int pl = first - 1 - rem;
     // AC j is zig-zag slot j + 1: the low half of zw[(j + 1) / 2] for odd j, the
     // high half for even j.  The packed word is formed without extracting the value:
@@ -173,15 +175,18 @@ __device__ __forceinline__ void slot_pass(const uint32_t (&zw)[32], uint2 *st2, 
     for (int j = 0; j < 63; ++j) {
       const uint32_t w = zw[(j + 1) >> 1];
       const bool lo = ((j + 1) & 1) == 0;
-      const bool nzv = lo ? (uint16_t)w != 0 : w > 0xFFFFu;
+      const bool nz = lo ? (uint16_t)w != 0 : w > 0xFFFFu;
       const uint32_t len = (uint32_t)(j - pl - 1);
       const uint32_t pk = lo ? ((w << 4) | len) : (((w >> 12) & 0xFFF0u) | len);
-      const bool nz = nzv && d;
-      const uint32_t a = nz ? la : ldum;
-      *(lds_u16 *)(uintptr_t)a = (uint16_t)pk;
+      *(lds_u16 *)(uintptr_t)la = (uint16_t)pk;
       la += nz ? 2u : 0u;
-      pl = nzv ? j : pl;
+      pl = nz ? j : pl;
     }
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (first >= 0) {
+    for (int k = 0; k < nf0; ++k) sb[o + k] = (uint16_t)(kSlotM - 1);
+    sb[o + nf0] = (uint16_t)(((uint32_t)vfirst << 4) | (uint32_t)rem);
   }
   if (__builtin_amdgcn_ballot_w64(!dense && first >= 0)) {
     if (!dense && first >= 0)
@@ -190,7 +195,8 @@ __device__ __forceinline__ void slot_pass(const uint32_t (&zw)[32], uint2 *st2, 
       });
   }
   __builtin_amdgcn_wave_barrier();
-  // ---- 4. copy out: 16 packed words (32 B) -> 16 lengths (16 B) + 16 values (32 B)
+  // ---- 4. copy out, every store instruction 1 KiB contiguous: lengths 16 symbols
+  // per lane (32 B of packed words -> 16 B), values 8 per lane (16 B -> 16 B)
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
   for (int h = 0; h < (SEG ? 2 : 1); ++h) {
@@ -199,28 +205,30 @@ __device__ __forceinline__ void slot_pass(const uint32_t (&zw)[32], uint2 *st2, 
     const uint4 *src = reinterpret_cast<const uint4 *>(reinterpret_cast<uint16_t *>(st2) + h * 32 * kStageRowU16);
     for (int c = lane; 16 * c < n; c += 64) {
       const uint4 p = src[2 * c], q = src[2 * c + 1];
-      const uint32_t w[8] = {p.x, p.y, p.z, p.w, q.x, q.y, q.z, q.w};
-      uint32_t vv[8], ll[4];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {  // value = the word >> 4 (arithmetic), both halves
-        const i16x2_t x = __builtin_bit_cast(i16x2_t, w[k]);
-        vv[k] = __builtin_bit_cast(uint32_t, x >> (i16x2_t){4, 4});
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k)  // lengths: the low bytes of four words, low nibbles
-        ll[k] = __builtin_amdgcn_perm(w[2 * k + 1], w[2 * k], 0x06040200u) & 0x0F0F0F0Fu;
+      // lengths: the low nibbles of the words' low bytes
+      const u32x4 L = {__builtin_amdgcn_perm(p.y, p.x, 0x06040200u) & 0x0F0F0F0Fu,
+                       __builtin_amdgcn_perm(p.w, p.z, 0x06040200u) & 0x0F0F0F0Fu,
+                       __builtin_amdgcn_perm(q.y, q.x, 0x06040200u) & 0x0F0F0F0Fu,
+                       __builtin_amdgcn_perm(q.w, q.z, 0x06040200u) & 0x0F0F0F0Fu};
       u32x4 *ol = reinterpret_cast<u32x4 *>(S.len) + c;
-      u32x4 *ov = reinterpret_cast<u32x4 *>(S.val) + 2 * c;
-      const u32x4 L = {ll[0], ll[1], ll[2], ll[3]}, V0 = {vv[0], vv[1], vv[2], vv[3]}, V1 = {vv[4], vv[5], vv[6], vv[7]};
-      if (NT) {
+      if (NT)
         __builtin_nontemporal_store(L, ol);
-        __builtin_nontemporal_store(V0, ov);
-        __builtin_nontemporal_store(V1, ov + 1);
-      } else {
+      else
         *ol = L;
-        ov[0] = V0;
-        ov[1] = V1;
-      }
+    }
+    for (int c = lane; 8 * c < n; c += 64) {
+      const uint4 p = src[c];
+      const uint32_t w[4] = {p.x, p.y, p.z, p.w};
+      uint32_t vv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)  // value = the word >> 4 (arithmetic), both halves
+        vv[k] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(i16x2_t, w[k]) >> (i16x2_t){4, 4});
+      const u32x4 V = {vv[0], vv[1], vv[2], vv[3]};
+      u32x4 *ov = reinterpret_cast<u32x4 *>(S.val) + c;
+      if (NT)
+        __builtin_nontemporal_store(V, ov);
+      else
+        *ov = V;
     }
   }
   __builtin_amdgcn_wave_barrier();

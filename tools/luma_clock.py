@@ -25,13 +25,13 @@ def main():
             continue
         ns = int(t["End_Timestamp"]) - int(t["Start_Timestamp"])
         c = ctr[did]
-        rows.append((did, ns, c.get("GRBM_GUI_ACTIVE", 0) / ns * 1e3, c.get("SQ_BUSY_CYCLES", 0) / ns * 1e3))
+        rows.append((did, ns, c.get("GRBM_GUI_ACTIVE", 0) / 8 / ns * 1e3, c.get("SQ_BUSY_CYCLES", 0) / ns * 1e3))
     med = statistics.median(r[2] for r in rows)
-    print("dispatch  us  us/plane  GRBM_GUI_ACTIVE/us (MHz)  SQ_BUSY_CYCLES/us  us/plane at the median clock")
+    print("dispatch  us  us/plane  clock MHz (GRBM_GUI_ACTIVE/8/us)  SQ_BUSY_CYCLES/us  us/plane at the median clock")
     for did, ns, f, sq in rows:
         print("%6d %8.2f %7.3f %10.1f %12.1f %9.3f" % (did, ns / 1e3, ns / 1e3 / planes, f, sq,
                                                       ns / 1e3 / planes * f / med))
-    print("median clock (GRBM_GUI_ACTIVE per us): %.1f MHz over %d dispatches" % (med, len(rows)))
+    print("median clock (GRBM_GUI_ACTIVE / 8 per us): %.1f MHz over %d dispatches" % (med, len(rows)))
 
 
 if __name__ == "__main__":

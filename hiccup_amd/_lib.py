@@ -200,7 +200,7 @@ def call(name, *args):
 # A/B knobs (include/hiccup_hip.h HIC_KNOB_*): every selectable path is bit-exact
 KNOBS = {"dct_path": 0, "dct_waves_per_cu": 1, "color_tiled": 2, "color_seg": 3, "color_nt": 4, "rle_nt": 5,
          "rld_nt": 6, "rld_generic": 7, "dev": 8, "encode_order": 13}
-DCT_PATH_F64, DCT_PATH_GLDS, DCT_PATH_EXACT = 1, 2, 0  # 2: the LDS-DMA prefetch form (A/B, aligned planes)
+DCT_PATH_F64, DCT_PATH_EXACT = 1, 0  # (2 = 1 since round 6: its LDS-DMA prefetch form was removed)
 
 
 def set_knob(name, value):

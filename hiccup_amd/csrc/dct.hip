@@ -541,15 +541,13 @@ struct DctJobs {
 #ifndef HIC_DCT_WPE
 #define HIC_DCT_WPE 3  // register budget: waves per SIMD (3: <= 168 VGPRs)
 #endif
-// GLDS (knob dct_path 2, A/B; planes whose 64-block sets lie in one block row, 16-byte
-// aligned rows): each wave's next set of pixels (8 rows x 512 B) is fetched into a
-// 4 KiB LDS buffer by LDS-DMA (global_load_lds_dwordx4, no VGPRs) while the current
-// set computes from registers (VERDICT r5 item 2's last lever on this pass).
-template <int TABLE, int LAYOUT, int TMF, bool GLDS = false>
+// (An LDS-DMA prefetch of the next set's pixels, round 6's dct_path 2, was bit-exact
+// and within noise of these register loads: profiles/r06/glds_ab, commit "LDS-DMA
+// prefetch form of the plane DCT"; removed.)
+template <int TABLE, int LAYOUT, int TMF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DCT_WPE))) void k_dct_planes(DctJobs jobs,
                                                                                                        int path) {
   __shared__ uint2 s_stage[4 * 64 * kStageU2];
-  __shared__ __attribute__((aligned(16))) uint4 s_pix[GLDS ? 4 * 256 : 1];
   // wv is wave-uniform: keep it (and the set / job indices derived from it) in
   // SGPRs, so the job fields are scalar loads, not vector loads on vmcnt
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -651,19 +649,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DCT_WPE
     // (a software-pipelined load of the next set's pixels into registers was measured
     // slower and removed: 160 vs 149 VGPRs, 8K luma 27.6-27.7 vs 25.6-26.2 us,
     // profiles/r03/s2/dct_pf/; the other waves of the SIMD hide the loads)
-    uint4 *pix = s_pix + (GLDS ? wv * 256 : 0);
-    // GLDS: set `set` of J into the wave's LDS buffer, rows 2k and 2k + 1 per instruction
-    auto glds = [&](const DctJob &Jn, int set) {
-      const int blk0 = set * 64, bi = blk0 / Jn.nbx, bj0 = blk0 - bi * Jn.nbx;
-      const uint8_t *base = Jn.plane + (int64_t)bi * 8 * Jn.stride + bj0 * 8 + (lane & 31) * 16;
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(base + (2 * k + (lane >> 5)) * Jn.stride),
-                                         reinterpret_cast<__attribute__((address_space(3))) void *>(
-                                             reinterpret_cast<uintptr_t>(pix + 64 * k)),
-                                         16, 0, 0);
-    };
-    if (GLDS && g0 < jobs.total_sets) glds(J, g0 - J.set0);
     for (int g = g0; g < jobs.total_sets; g += nwaves, ++i) {
       if (g >= next0) {
         kj = job_of(g);
@@ -672,29 +657,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DCT_WPE
       }
       const int set = g - J.set0;
       uint2 w[8];
-      if constexpr (GLDS) {
-        // this set's DMA: the only vector-memory operations issued after it are the
-        // previous set's 8 output stores (none before the first set)
-        __builtin_amdgcn_sched_barrier(0);
-        if (i == 0)
-          __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-        else
-          __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8)
-        __builtin_amdgcn_sched_barrier(0);
-        const uint2 *px = reinterpret_cast<const uint2 *>(pix);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) w[r] = px[r * 64 + lane];
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the buffer is read before it is refilled
-        __builtin_amdgcn_sched_barrier(0);
-        const int gn = g + nwaves;
-        if (gn < jobs.total_sets) {
-          const int kn = gn >= next0 ? job_of(gn) : kj;
-          glds(jobs.j[kn], gn - jobs.j[kn].set0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      } else {
-        load(J, set, w);
-      }
+      load(J, set, w);
       bool t26 = false;
       const bool f = dct_block_aan<TABLE, LAYOUT>(w, st, &t26, nullptr, J.table);
       if (__builtin_amdgcn_ballot_w64(f) != 0) redo |= 1ull << i;
@@ -863,19 +826,6 @@ int launch_planes(DctJobs &jobs, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   const int waves = (cap == 0 || total < cap) ? total : cap;
   const dim3 grid((waves + 3) / 4), block(256);
   const int path = dct_path();
-  // dct_path 2 (A/B): the LDS-DMA prefetch form, where every set is 64 blocks of one
-  // block row with 16-byte aligned rows and the pass writes no tile records (its
-  // counted vmcnt assumes the 8 output stores per set)
-  bool glds = path == 2 && LAYOUT == HIC_LAYOUT_ZIGZAG_I16 && TMF < 0;
-  for (int k = 0; k < jobs.n && glds; ++k)
-    glds = jobs.j[k].nbx % 64 == 0 && jobs.j[k].stride % 16 == 0 && reinterpret_cast<uintptr_t>(jobs.j[k].plane) % 16 == 0;
-  if (glds) {
-    if (e0 || e1)
-      hipExtLaunchKernelGGL((k_dct_planes<TABLE, LAYOUT, TMF, true>), grid, block, 0, s, e0, e1, 0, jobs, path);
-    else
-      hipLaunchKernelGGL((k_dct_planes<TABLE, LAYOUT, TMF, true>), grid, block, 0, s, jobs, path);
-    return check_launch("k_dct_planes<glds>");
-  }
   if (e0 || e1)
     hipExtLaunchKernelGGL((k_dct_planes<TABLE, LAYOUT, TMF>), grid, block, 0, s, e0, e1, 0, jobs, path);
   else

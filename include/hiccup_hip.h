@@ -66,7 +66,7 @@ int hic_device_count(int *h_n);
  * Every selectable path is bit-exact: a knob never changes results, only which
  * kernel variant computes them.  The library reads no environment variables.
  * Values are process-wide; -1 restores the default. */
-#define HIC_KNOB_DCT_PATH 0         /* forward DCT of aligned planes: 1 float64 AAN (the default), 2 the same with the next set's pixels prefetched by LDS-DMA (round 6 A/B; records-free batches of planes whose rows hold whole 64-block sets), 0 exact replica; 3 / 4 (packed float32, two lanes per block: removed in round 5) are refused */
+#define HIC_KNOB_DCT_PATH 0         /* forward DCT of aligned planes: 1 / 2 float64 AAN (the default; 2's LDS-DMA prefetch form, measured within noise in round 6, was removed), 0 exact replica; 3 / 4 (packed float32, two lanes per block: removed in round 5) are refused */
 #define HIC_KNOB_DCT_WAVES_PER_CU 1 /* forward DCT persistent grid (waves per CU; 0 = one wave per set) */
 #define HIC_KNOB_COLOR_TILED 2      /* 1: LDS-tiled colour kernels instead of the wave-walk ones */
 #define HIC_KNOB_COLOR_SEG 3        /* wave-walk colour: chroma rows per segment (8 default, 16) */

@@ -98,7 +98,7 @@ def test_layouts_roundtrip(layout, shape):
         np.testing.assert_array_equal(device.to_host(rec), orcc.inv_dct_channel(exp, tab))
 
 
-@pytest.mark.parametrize("path", [-1, _lib.DCT_PATH_EXACT, _lib.DCT_PATH_GLDS])
+@pytest.mark.parametrize("path", [-1, _lib.DCT_PATH_EXACT])
 @pytest.mark.parametrize("H,W", [(4096, 4096), (4320, 7680)])
 def test_full_size_bit_exact(H, W, path):
     """BASELINE configs 2/3 plane sizes, bit-exact against the C oracle (multi-threaded),
@@ -130,7 +130,7 @@ def test_tie_blocks_many():
         np.testing.assert_array_equal(transform.dct_channel(plane, QT[tab]), orcc.dct_channel(plane, tab, threads=8))
 
 
-@pytest.mark.parametrize("path", [_lib.DCT_PATH_F64, _lib.DCT_PATH_EXACT, _lib.DCT_PATH_GLDS])
+@pytest.mark.parametrize("path", [_lib.DCT_PATH_F64, _lib.DCT_PATH_EXACT])
 @pytest.mark.parametrize("kind", ["levels4", "nearflat", "stripes", "checker", "blur"])
 def test_fast_path_structured_ties(kind, path):
     with _lib.knobs(dct_path=path):
@@ -260,7 +260,7 @@ def test_plane_batch_sixteen_planes(kind):
     _plane_batch(shapes, kind, -1, -1)
 
 
-@pytest.mark.parametrize("path", [_lib.DCT_PATH_F64, _lib.DCT_PATH_EXACT, _lib.DCT_PATH_GLDS])
+@pytest.mark.parametrize("path", [_lib.DCT_PATH_F64, _lib.DCT_PATH_EXACT])
 @pytest.mark.parametrize("waves_per_cu", [-1, 1])
 @pytest.mark.parametrize("kind", ["random", "levels4", "nearflat", "blur"])
 def test_plane_batch_records_free(kind, waves_per_cu, path):
@@ -274,7 +274,7 @@ def test_plane_batch_records_free(kind, waves_per_cu, path):
     # one table for every plane: the launch takes the kernel compiled for that table
     luma = [(8 * (40 + i), 8 * (64 + 5 * i), 0) for i in range(4)]
     chroma = [(8 * (33 + 2 * i), 8 * (70 + 3 * i), 1) for i in range(3)]
-    # every plane's rows hold whole 64-block sets: dct_path 2 takes its LDS-DMA form
+    # every plane's rows hold whole 64-block sets
     aligned = [(4320, 7680, 0), (4320, 7680, 0), (8 * 21, 1536, 1)] + \
         [(8 * (3 + i), 1024, i % 2) for i in range(5)]
     for sh in (shapes, small, luma, chroma, aligned):

@@ -195,7 +195,13 @@ def jpeg_encode(compressed):
     """codec.py:275-334: CompressedImage -> HicImage (9 tables, 9 bit strings, 2 shapes).
     Everything but the nine trees runs on the GPU: split + zig-zag, DC DPCM, AC RLE
     (encode_channel_device), the key histograms in first-appearance order and the
-    bit packing of the coded streams (huffman.DeviceStreams, csrc/huffman.hip)."""
+    bit packing of the coded streams (huffman.DeviceStreams, csrc/huffman.hip).  The
+    trees' node objects pause Python's cyclic collector as in jpeg_decode."""
+    with _gc_paused():
+        return _jpeg_encode(compressed)
+
+
+def _jpeg_encode(compressed):
     utils.debug_msg("Starting JPEG encoding")
     bs = settings.JPEG_BLOCK_SIZE
     chans = ("lum", "cr", "cb")

@@ -3,6 +3,7 @@ the compute is entirely in libhiccup_hip.so.  No CPU fallback: without a HIP
 device every entry point raises ``HipUnavailable``."""
 import contextlib
 import ctypes
+import sys
 import threading
 
 import numpy as np
@@ -41,10 +42,10 @@ def ptr(t):
 
 
 def to_device(a):
-    """A host array as a new device tensor.  Large arrays (>= 4 MiB) go through the
-    pinned staging buffer in chunks of at most _PIN_MAX bytes (threaded host copy,
-    then one DMA each): a pageable copy runs at ~4 GB/s on the MI355X boxes
-    (tools/prof_d2h.py)."""
+    """A host array as a new device tensor.  Large arrays (>= 4 MiB) go through two
+    pinned staging buffers in chunks of _CHUNK bytes: the threaded host copy of one
+    chunk overlaps the DMA of the one before it (a pageable copy runs at ~4 GB/s on
+    the MI355X boxes)."""
     require_gpu()
     a = np.ascontiguousarray(a)
     if a.nbytes < _PIN_MIN or a.dtype.hasobject:
@@ -52,10 +53,22 @@ def to_device(a):
     out = torch.empty(tuple(a.shape), dtype=torch.from_numpy(a[:0].reshape(-1)).dtype, device="cuda")
     ob, ab = out.reshape(-1).view(torch.uint8), a.reshape(-1).view(np.uint8)
     with _staging_lock:
-        for o, n in _chunks(a.nbytes):
-            st = _stage(n)
+        s = _copy_stream()
+        s.wait_stream(torch.cuda.current_stream())  # `out` was allocated on the current stream
+        done = [None, None]
+        for i, (o, n) in enumerate(_chunks(a.nbytes)):
+            st = _stage(i % 2, n)
+            if done[i % 2] is not None:
+                done[i % 2].synchronize()  # the buffer's previous DMA has read it
             _par_copy(st.numpy(), ab[o:o + n])
-            ob[o:o + n].copy_(st)  # synchronous: the buffer is reused by the next chunk
+            with torch.cuda.stream(s):
+                ob[o:o + n].copy_(st, non_blocking=True)
+                done[i % 2] = torch.cuda.Event()
+                done[i % 2].record(s)
+        torch.cuda.current_stream().wait_stream(s)
+        for e in done:
+            if e is not None:
+                e.synchronize()  # the staging buffers are free for the next caller
     return out
 
 
@@ -79,39 +92,59 @@ def sync(stream=None):
     _lib.call("hic_stream_sync", stream_ptr(stream))
 
 
+def _d2h_chunks(src_u8, nbytes, host_copy):
+    """DMA src_u8 (a flat uint8 device view) into the two pinned buffers chunk by
+    chunk on the copy stream, and hand each landed chunk to host_copy(offset, n,
+    pinned uint8 numpy view) while the next chunk's DMA runs (call with
+    _staging_lock held)."""
+    s = _copy_stream()
+    s.wait_stream(torch.cuda.current_stream())
+    chunks = _chunks(nbytes)
+    ev = [None, None]
+
+    def issue(i):
+        o, n = chunks[i]
+        with torch.cuda.stream(s):
+            _stage(i % 2, n).copy_(src_u8[o:o + n], non_blocking=True)
+            ev[i % 2] = torch.cuda.Event()
+            ev[i % 2].record(s)
+
+    issue(0)
+    for i, (o, n) in enumerate(chunks):
+        if i + 1 < len(chunks):
+            issue(i + 1)  # its buffer's previous chunk (i - 1) was copied out below
+        ev[i % 2].synchronize()
+        host_copy(o, n, _stage(i % 2, n).numpy())
+
+
 def to_host(t):
-    """A device tensor as a new numpy array (through the pinned buffer when large)."""
+    """A device tensor as a new numpy array (through the pinned buffers when large:
+    each chunk's host copy overlaps the next chunk's DMA)."""
     sync()
     nbytes = t.numel() * t.element_size()
     if nbytes < _PIN_MIN or not t.is_cuda:
         return t.cpu().numpy()
     t = t.contiguous()
-    out = np.empty(tuple(t.shape), torch.empty(0, dtype=t.dtype).numpy().dtype)
+    out = host_empty(tuple(t.shape), torch.empty(0, dtype=t.dtype).numpy().dtype)
     tb, ob = t.reshape(-1).view(torch.uint8), out.reshape(-1).view(np.uint8)
     with _staging_lock:
-        for o, n in _chunks(nbytes):
-            st = _stage(n)
-            st.copy_(tb[o:o + n])
-            _par_copy(ob[o:o + n], st.numpy())
+        _d2h_chunks(tb, nbytes, lambda o, n, st: _par_copy(ob[o:o + n], st))
     return out
 
 
 def to_host_f64(t):
     """A device int32 tensor as a new float64 numpy array (the reference's planes are
-    float64): DMA into the pinned buffer, then the cast split over host threads.
-    A pageable copy runs at ~4 GB/s here and the single-threaded cast after it
-    doubled the time (8K luma: 48 vs 17 ms, tools/prof_d2h.py)."""
+    float64): DMA into the pinned buffers, the cast split over host threads and
+    overlapped with the next chunk's DMA.  A pageable copy runs at ~4 GB/s here and
+    the single-threaded cast after it doubled the time (8K luma: 48 vs 17 ms)."""
     assert t.dtype == torch.int32 and t.is_cuda
     sync()
     t = t.contiguous()
     n = t.numel()
-    out = np.empty(n, np.float64)
-    ti = t.reshape(-1)
+    out = host_empty((n,), np.float64)
     with _staging_lock:
-        for o, nb in _chunks(4 * n):
-            st = _stage(nb)
-            st.view(torch.int32).copy_(ti[o // 4:(o + nb) // 4])
-            _par_copy(out[o // 4:(o + nb) // 4], st.numpy().view(np.int32))
+        _d2h_chunks(t.reshape(-1).view(torch.uint8), 4 * n,
+                    lambda o, nb, st: _par_copy(out[o // 4:(o + nb) // 4], st.view(np.int32)))
     return out.reshape(tuple(t.shape))
 
 
@@ -139,40 +172,89 @@ def to_device_i32(a, nonint_msg, range_msg):
     return t.to(torch.int32)
 
 
-# one pinned host staging buffer (grown on demand up to _PIN_MAX bytes, reused;
-# callers on several threads take turns under _staging_lock; larger copies go in
-# _PIN_MAX chunks, so the buffer never holds more than that) and a small thread
-# pool for the host side of the copies
+# two pinned host staging buffers of _CHUNK bytes (reused; callers on several
+# threads take turns under _staging_lock), a copy stream for their DMAs, and a small
+# thread pool for the host side of the copies
 _PIN_MIN = 4 << 20
-_PIN_MAX = 256 << 20
-_staging = None
+_CHUNK = 32 << 20
+_staging = [None, None]
 _staging_lock = threading.Lock()
+_cstream = None
 _pool = None
 
 
-def _chunks(nbytes):
-    """(offset, length) pieces of a copy of nbytes, each <= _PIN_MAX (a multiple of 8)."""
-    return [(o, min(_PIN_MAX, nbytes - o)) for o in range(0, nbytes, _PIN_MAX)]
+def _chunks(nbytes, chunk=None):
+    """(offset, length) pieces of a copy of nbytes, each <= _CHUNK (a multiple of 8)."""
+    c = _CHUNK if chunk is None else chunk
+    return [(o, min(c, nbytes - o)) for o in range(0, nbytes, c)]
 
 
-def _stage(nbytes):
-    """The first nbytes (<= _PIN_MAX) of the pinned uint8 buffer (call with
-    _staging_lock held)."""
-    global _staging
-    assert nbytes <= _PIN_MAX
-    if _staging is None or _staging.numel() < nbytes:
-        _staging = None
-        _staging = torch.empty(min(_PIN_MAX, max(2 * int(nbytes), _PIN_MIN)), dtype=torch.uint8, pin_memory=True)
-    return _staging[:nbytes]
+def _stage(k, nbytes):
+    """The first nbytes (<= _CHUNK) of pinned buffer k (call with _staging_lock held)."""
+    assert nbytes <= _CHUNK
+    if _staging[k] is None:
+        _staging[k] = torch.empty(_CHUNK, dtype=torch.uint8, pin_memory=True)
+    return _staging[k][:nbytes]
+
+
+# Host result arrays.  A fresh numpy array of a few hundred MB costs its page faults
+# on first touch (~11 ms per 133 MB single-threaded on the GPU box, ~22 ms when eight
+# copy threads fault it together; the DMA itself is 2.3 ms): the large results of
+# to_host / to_host_f64 are views of pooled, already-faulted buffers instead.  A
+# pooled buffer is handed out again only when nothing but the pool references it (a
+# caller's result, or any view of it, keeps it out of the pool).
+_HOST_POOL_MAX = 4 << 30  # bytes the pool may hold
+_host_pool = []
+_host_pool_lock = threading.Lock()
+
+
+def host_empty(shape, dtype):
+    """np.empty(shape, dtype) from the pool of faulted buffers when large."""
+    dt = np.dtype(dtype)
+    nbytes = int(np.prod(shape, dtype=np.int64)) * dt.itemsize
+    if nbytes < _PIN_MIN:
+        return np.empty(shape, dt)
+    with _host_pool_lock:
+        best = None
+        for b in _host_pool:
+            # referenced only by the list, the loop variable and getrefcount's argument
+            if b.nbytes >= nbytes and sys.getrefcount(b) <= 3 and (best is None or b.nbytes < best.nbytes):
+                best = b
+        if best is None:
+            best = np.empty(nbytes, np.uint8)
+            _fault_in(best)
+            if sum(b.nbytes for b in _host_pool) + nbytes <= _HOST_POOL_MAX:
+                _host_pool.append(best)
+        return best[:nbytes].view(dt).reshape(shape)
+
+
+def _fault_in(buf):
+    """Touch every page of a new host buffer on the worker threads, 2 MiB apart."""
+    step = 2 << 20
+    n = buf.size
+    bounds = [(o, min(n, o + step)) for o in range(0, n, step)]
+    _ensure_pool()
+    list(_pool.map(lambda ab: buf[ab[0]:ab[1]].fill(0), bounds))
+
+
+def _ensure_pool():
+    global _pool
+    if _pool is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _pool = ThreadPoolExecutor(8)
+
+
+def _copy_stream():
+    global _cstream
+    if _cstream is None:
+        _cstream = torch.cuda.Stream()
+    return _cstream
 
 
 def _par_copy(dst, src):
     """dst[...] = src (same shape; a cast if the dtypes differ) in 8 row ranges on
     host threads (numpy releases the GIL while it copies)."""
-    global _pool
-    if _pool is None:
-        from concurrent.futures import ThreadPoolExecutor
-        _pool = ThreadPoolExecutor(8)
+    _ensure_pool()
     d, s_ = dst.reshape(-1), src.reshape(-1)
     n = d.size
     k = 8 if n >= (1 << 20) else 1

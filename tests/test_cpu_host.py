@@ -531,12 +531,13 @@ def test_jpeg_decode_gc_pause_is_shared():
 
 
 def test_pinned_staging_chunks():
-    """the pinned staging buffer is capped; larger copies go in
-    _PIN_MAX pieces that tile the copy exactly (int32 / float64 aligned)."""
+    """the pinned staging buffers are capped (two of _CHUNK bytes,
+    round 6); larger copies go in _CHUNK pieces that tile the copy exactly (int32 /
+    float64 aligned)."""
     from hiccup_amd import device
     assert device._staging_lock is not None
-    for n in [device._PIN_MIN, device._PIN_MAX - 8, device._PIN_MAX, device._PIN_MAX + 4, 5 * device._PIN_MAX + 12]:
+    for n in [device._PIN_MIN, device._CHUNK - 8, device._CHUNK, device._CHUNK + 4, 5 * device._CHUNK + 12]:
         ch = device._chunks(n)
         assert ch[0][0] == 0 and sum(c for _, c in ch) == n
         assert all(o1 == o0 + c0 for (o0, c0), (o1, _) in zip(ch, ch[1:]))
-        assert all(c <= device._PIN_MAX and o % 8 == 0 for o, c in ch)
+        assert all(c <= device._CHUNK and o % 8 == 0 for o, c in ch)

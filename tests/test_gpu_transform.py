@@ -408,16 +408,17 @@ def test_pinned_host_copies(dtype):
 
 @pytest.mark.parametrize("dtype", [np.uint8, np.int32, np.float64, np.bool_])
 def test_pinned_host_copies_chunked(dtype, monkeypatch):
-    """Copies larger than the staging cap go in _PIN_MAX pieces (the cap lowered to
+    """Copies larger than a staging buffer go in _CHUNK pieces through the two pinned
+    buffers, each chunk's host copy beside the next chunk's DMA (the chunk lowered to
     4 MiB + 8 here so that a ~13 MB copy takes four, the last one short)."""
-    monkeypatch.setattr(device, "_PIN_MAX", (4 << 20) + 8)
-    monkeypatch.setattr(device, "_staging", None)
+    monkeypatch.setattr(device, "_CHUNK", (4 << 20) + 8)
+    monkeypatch.setattr(device, "_staging", [None, None])
     rng = np.random.default_rng(12)
     a = (rng.integers(0, 2, (1601, 2051)) if dtype == np.bool_ else rng.integers(-100, 100, (1601, 2051))).astype(dtype)
-    if a.nbytes < 3 * device._PIN_MAX:
-        a = np.concatenate([a] * (1 + 3 * device._PIN_MAX // a.nbytes))
+    if a.nbytes < 3 * device._CHUNK:
+        a = np.concatenate([a] * (1 + 3 * device._CHUNK // a.nbytes))
     t = device.to_device(a)
     np.testing.assert_array_equal(device.to_host(t), a)
-    assert device._staging.numel() <= device._PIN_MAX
+    assert all(b is None or b.numel() <= device._CHUNK for b in device._staging)
     if dtype == np.int32:
         np.testing.assert_array_equal(device.to_host_f64(t), a.astype(np.float64))

@@ -459,17 +459,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DEC_WPE
   uint2 *tile = s_tile[wv];
   int16_t *win = reinterpret_cast<int16_t *>(tile);
   const int64_t nsym_raw = *d_nsym, nsym = nsym_raw > 0 ? nsym_raw : 0;
+  const int nvb = (int)(nblk - t * 64 < 64 ? nblk - t * 64 : 64);
+  const int64_t blk = t * 64 + lane;
+  // loads that depend on nothing else go out before the zero-fill: this lane's DC
+  // difference and (slot layout) the tile's record index
+  const int d = lane < nvb ? dc_diff[blk] : 0;
+  SlotTileIx six;
+  if constexpr (SLOTS) six = slot_tile_ix(reinterpret_cast<const int32_t *>(index), t, rsh, nblk);
   for (int i = lane; i < 64 * kRowI16 / 4; i += 64) tile[i] = make_uint2(0, 0);
   __builtin_amdgcn_wave_barrier();
   const int64_t tb0 = t * 64 * 63;
-  const int nvb = (int)(nblk - t * 64 < 64 ? nblk - t * 64 : 64);
   const int span = nvb * 63;
   // the symbols of the tile into its LDS rows (trash: the lane's row's first pad slot)
   int P, pdc;
   if constexpr (SLOTS) {
-    const int32_t *sidx = reinterpret_cast<const int32_t *>(index);
-    P = slots_gather_tile<kRowI16>(sym_len, sym_val, sidx, t, rsh, nblk, span, win, lane * kRowI16 + 64, lane);
-    pdc = sidx[4 * (t << rsh) + 2];
+    P = slots_gather_tile<kRowI16>(sym_len, sym_val, six, t, rsh, span, win, lane * kRowI16 + 64, lane);
+    pdc = six.r[0].z;
   } else {
     const int64_t o0 = index[3 * t] < nsym ? index[3 * t] : nsym;
     const int64_t o1 = t + 1 < ntiles ? (index[3 * (t + 1)] < nsym ? index[3 * (t + 1)] : nsym) : nsym;
@@ -477,8 +482,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DEC_WPE
                                                     span, win, lane * kRowI16 + 64, lane);
     pdc = (int)index[3 * t + 2];
   }
-  const int64_t blk = t * 64 + lane;
-  const int d = lane < nvb ? dc_diff[blk] : 0;
   win[lane * kRowI16] = (int16_t)(pdc + wave_incl_sum_i32(d));
   __builtin_amdgcn_wave_barrier();
   if (t == ntiles - 1 && lane == 0) {

@@ -1624,9 +1624,9 @@ __global__ __launch_bounds__(256) void k_rld_indexed16(const uint8_t *__restrict
   int P = 0, pdc;
   if constexpr (SLOTS) {
     // the tile's records, each from its own slot (trash slots: the 64 after the tile)
-    const int32_t *sidx = reinterpret_cast<const int32_t *>(index);
-    P = slots_gather_tile<64>(sym_len, sym_val, sidx, t, rsh, nblk, span, win, 64 * 64 + lane, lane);
-    pdc = sidx[4 * (t << rsh) + 2];
+    const SlotTileIx six = slot_tile_ix(reinterpret_cast<const int32_t *>(index), t, rsh, nblk);
+    P = slots_gather_tile<64>(sym_len, sym_val, six, t, rsh, span, win, 64 * 64 + lane, lane);
+    pdc = six.r[0].z;
   } else {
     const int64_t o0 = index[3 * t] < nsym ? index[3 * t] : nsym;
     const int64_t o1 = t + 1 < ntiles ? (index[3 * (t + 1)] < nsym ? index[3 * (t + 1)] : nsym) : nsym;

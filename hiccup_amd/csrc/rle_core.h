@@ -483,25 +483,37 @@ __device__ __forceinline__ int gather_tile(const uint8_t *__restrict__ sym_len, 
 
 // The slot-layout form (slots.h): a 64-block tile holds 1 << rsh records, record r's
 // n symbols at [r * cap, r * cap + n) of the slot arrays (cap = 63 x 64 >> rsh), its
-// first symbol's zeros starting after record-relative position P (sidx: the close's
-// {n, P, pdc, nfill} per record).  Returns the last record's end position (as
-// gather_tile; 0 for a tile without symbols).
+// first symbol's zeros starting after record-relative position P.  SlotTileIx holds
+// the tile's records' {n, P, pdc, nfill} (the close's index), read by scalar loads
+// at the top of the decoder so that their latency overlaps its LDS zero-fill.
+struct SlotTileIx {
+  int4 r[2];
+};
+__device__ __forceinline__ SlotTileIx slot_tile_ix(const int32_t *sidx, int64_t t, int rsh, int64_t nblk) {
+  typedef const __attribute__((address_space(4))) int32_t cint;  // uniform address: s_load
+  const int64_t nrec = (nblk + (64 >> rsh) - 1) >> (6 - rsh), r0 = t << rsh;  // records of the plane
+  SlotTileIx x;
+  cint *a = (cint *)(uintptr_t)(sidx + 4 * r0);
+  x.r[0] = make_int4(a[0], a[1], a[2], a[3]);
+  x.r[1] = make_int4(0, 0, 0, 0);
+  if (rsh && r0 + 1 < nrec) x.r[1] = make_int4(a[4], a[5], a[6], a[7]);
+  return x;
+}
+// Returns the last record's end position (as gather_tile; 0 for a tile without symbols).
 template <int ROW>
 __device__ __forceinline__ int slots_gather_tile(const uint8_t *__restrict__ slot_len,
-                                                 const int16_t *__restrict__ slot_val, const int32_t *__restrict__ sidx,
-                                                 int64_t t, int rsh, int64_t nblk, int span, int16_t *win, int trash,
-                                                 int lane) {
-  const int bpr = 64 >> rsh, capr = 63 * bpr;
-  const int64_t nrec = (nblk + bpr - 1) / bpr;
+                                                 const int16_t *__restrict__ slot_val, const SlotTileIx &ix,
+                                                 int64_t t, int rsh, int span, int16_t *win, int trash, int lane) {
+  const int capr = 63 * (64 >> rsh);
   int P = 0;
-  for (int k = 0; k < (1 << rsh); ++k) {
-    const int64_t r = (t << rsh) + k;
-    if (r >= nrec) break;  // wave-uniform
-    const int n = __builtin_amdgcn_readfirstlane(sidx[4 * r]);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    if (k > 0 && !rsh) break;
+    const int n = __builtin_amdgcn_readfirstlane(ix.r[k].x);
     if (n > 0) {
-      const int Pr = __builtin_amdgcn_readfirstlane(sidx[4 * r + 1]);
-      const int64_t o0 = r * capr;
-      P = gather_tile<ROW, HIC_DEC_G, HIC_DEC_PF>(slot_len, slot_val, o0, o0 + n, o0 + capr, Pr + k * capr, span, win,
+      const int64_t o0 = ((t << rsh) + k) * capr;
+      P = gather_tile<ROW, HIC_DEC_G, HIC_DEC_PF>(slot_len, slot_val, o0, o0 + n, o0 + capr,
+                                                 __builtin_amdgcn_readfirstlane(ix.r[k].y) + k * capr, span, win,
                                                  trash, lane);
     }
   }

@@ -77,6 +77,17 @@ dec)
   python3 tools/trace_launches.py $out/dec_trace/run_kernel_trace.csv k_ > $out/dec_launches.txt
   head -c 3000 $out/dec_launches.txt
   ;;
+decsq)
+  # SQ counters of the round trip's kernels (two passes), RT_N = 8192 keeps them short
+  i=0
+  for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY" \
+             "SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_WAVES SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD"; do
+    i=$((i+1))
+    RT_N=${RT_N:-8192} prof timeout -s KILL 120 rocprofv3 --pmc $set -d $out/decsq_p$i -o run --output-format csv -- \
+      python3 tools/prof_roundtrip.py > $out/decsq_p$i.log 2>&1 || { tail -5 $out/decsq_p$i.log; exit 1; }
+  done
+  python3 tools/counters_table.py $out > $out/decsq.txt 2>&1; cat $out/decsq.txt
+  ;;
 *)
   echo "unknown step $step"; exit 2 ;;
 esac

@@ -81,6 +81,8 @@ SIGNATURES = {
     "hic_rle_records_rebase": (_int, [_vp, _i64, _i64, _vp, _vp]),
     "hic_huffman_decode_workspace_bytes": (_sz, [_i64, ctypes.c_int32, ctypes.c_int32]),
     "hic_huffman_decode": (_int, [_vp, _i64, _vp, ctypes.c_int32, _vp, ctypes.c_int32, _vp, _i64, _vp, _vp, _vp]),
+    "hic_huffman_build": (_int, [_vp, _i64, _vp, _vp, _vp]),
+    "hic_huffman_from_codes": (_int, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),
     "hic_huffman_pack": (_int, [_vp, _int, _i64, ctypes.c_int32, ctypes.c_int32, _vp, _vp, _vp, _i64, _vp, _vp,
                                 _vp]),
     "hic_encode420_u8": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _int, _vp,

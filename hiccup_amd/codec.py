@@ -270,7 +270,7 @@ def _jpeg_decode(hic_image):
     assert hic_image.hic_type == model.Compression.JPEG
     p = hic_image.payloads
     chans = ("lum", "cr", "cb")
-    trees = [huffman_decode(p[i]) for i in range(9)]
+    trees = [_decoding_tree(p[i]) for i in range(9)]
     streams = [_huffman_stream_device(p[9 + i], trees[i]) for i in range(9)]
     shapes = {"lum": p[18].numbers, "cr": p[19].numbers, "cb": p[19].numbers}
     bs = settings.JPEG_BLOCK_SIZE
@@ -287,13 +287,21 @@ def _jpeg_decode(hic_image):
     return model.CompressedImage.from_dict(out)
 
 
+def _decoding_tree(data):
+    """huffman_decode's tree, built natively when the table is a complete prefix code
+    of int32 values (huffman.FlatCodes: every table an encoder writes), else the
+    reference's own construction."""
+    flat = huffman.FlatCodes.from_table([p.numbers for p in data.payloads])
+    return flat if flat is not None else huffman_decode(data)
+
+
 def _huffman_stream_device(payload, tree):
     """huffman_data_decode on the GPU: (int32 device tensor, count).  Streams whose
     tree holds a leaf that is not an int32 (a table with unused codes decodes them
     to None) go through the values on the host, where the reference's arithmetic on
     them fails the same way."""
     packed, nbits = payload.packed_bits()
-    if tree.root.is_leaf:  # no edges: the reference's walk fails on the first bit
+    if isinstance(tree, huffman.HuffmanTree) and tree.root.is_leaf:  # no edges: the reference's walk fails on the first bit
         tree.decode_data("1" if nbits else "")
         return device.to_device(np.zeros(1, np.int32)), 0
     buf = np.zeros(-(-max(int(nbits), 1) // 32) * 4, np.uint8)

@@ -13,8 +13,11 @@ of the reference's per-symbol parent walk (huffman.py:131-142).
 
 Device half (codec.jpeg_encode's hot loops, csrc/huffman.hip): the key histogram
 in first-appearance order (``device_counts``) and the bit packing of a coded
-stream (``HuffmanTree.encode_device``); only the tree (a heap over the distinct
-keys) is built here.
+stream (``encode_device``).  The trees of codec.jpeg_encode / jpeg_decode are built
+in native host code (csrc/hufftree.hip): ``CodeBook`` (the codes of the heapq tree)
+and ``FlatCodes`` (the decoding tree of a coding table, in the GPU decoder's
+layout).  ``HuffmanTree`` is the reference's node-object tree, kept as the
+reference-shaped API and for tables the native builder refuses.
 """
 import ctypes
 import heapq
@@ -25,7 +28,38 @@ import torch
 from . import _lib, device, utils
 
 
-class HuffmanTree:
+class _Packer:
+    """encode_data of a device key stream through a tree's code table (the GPU
+    packer): shared by HuffmanTree and the natively built CodeBook."""
+
+    def encode_device(self, keys_dev, n, key_min, nbins, counts, stream=None):
+        """encode_data of a device key stream (uint8 / int16 / int32 tensor of n keys
+        in [key_min, key_min + nbins), with counts the per-bin histogram), packed on
+        the GPU: returns (packed uint8 numpy array, number of bits), MSB-first --
+        the bits io.padded_bs_2_bytes stores after its pad-length byte."""
+        if n == 0:
+            return np.zeros(0, np.uint8), 0
+        with device.on_stream(stream):
+            return self._encode_device(keys_dev, n, key_min, nbins, counts, stream)
+
+    def _encode_device(self, keys_dev, n, key_min, nbins, counts, stream):
+        bits, lens = self.code_table(key_min, nbins)
+        total = int(np.sum(np.asarray(counts, dtype=np.int64) * lens.astype(np.int64)))
+        nbytes = max(4, -(-total // 32) * 4)
+        out = device.empty((nbytes,), torch.uint8)
+        nbits = device.empty((1,), torch.int64)
+        ws = device.workspace(_lib.load().hic_huffman_pack_workspace_bytes(n))
+        cb, cl = device.to_device(bits.view(np.int64)), device.to_device(lens)
+        _lib.call("hic_huffman_pack", device.ptr(keys_dev), keys_dev.element_size(), n, key_min, nbins, device.ptr(cb),
+                  device.ptr(cl), device.ptr(out), nbytes, device.ptr(nbits), device.ptr(ws),
+                  device.stream_ptr(stream))
+        nb = int(nbits.cpu()[0])
+        if nb != total:
+            raise RuntimeError("packed %d bits, the histogram says %d" % (nb, total))
+        return out[:-(-nb // 8)].cpu().numpy(), nb
+
+
+class HuffmanTree(_Packer):
     class Node:
         GROUND = None
         ROOT = None
@@ -240,32 +274,6 @@ class HuffmanTree:
             lens[int(k) - key_min] = len(code)
         return bits, lens
 
-    def encode_device(self, keys_dev, n, key_min, nbins, counts, stream=None):
-        """encode_data of a device key stream (uint8 / int16 / int32 tensor of n keys
-        in [key_min, key_min + nbins), with counts the per-bin histogram), packed on
-        the GPU: returns (packed uint8 numpy array, number of bits), MSB-first --
-        the bits io.padded_bs_2_bytes stores after its pad-length byte."""
-        if n == 0:
-            return np.zeros(0, np.uint8), 0
-        with device.on_stream(stream):
-            return self._encode_device(keys_dev, n, key_min, nbins, counts, stream)
-
-    def _encode_device(self, keys_dev, n, key_min, nbins, counts, stream):
-        bits, lens = self.code_table(key_min, nbins)
-        total = int(np.sum(np.asarray(counts, dtype=np.int64) * lens.astype(np.int64)))
-        nbytes = max(4, -(-total // 32) * 4)
-        out = device.empty((nbytes,), torch.uint8)
-        nbits = device.empty((1,), torch.int64)
-        ws = device.workspace(_lib.load().hic_huffman_pack_workspace_bytes(n))
-        cb, cl = device.to_device(bits.view(np.int64)), device.to_device(lens)
-        _lib.call("hic_huffman_pack", device.ptr(keys_dev), keys_dev.element_size(), n, key_min, nbins, device.ptr(cb),
-                  device.ptr(cl), device.ptr(out), nbytes, device.ptr(nbits), device.ptr(ws),
-                  device.stream_ptr(stream))
-        nb = int(nbits.cpu()[0])
-        if nb != total:
-            raise RuntimeError("packed %d bits, the histogram says %d" % (nb, total))
-        return out[:-(-nb // 8)].cpu().numpy(), nb
-
     def flat(self):
         """The tree as hic_huffman_decode takes it: (child int32[2 * nodes], leaf nodes
         in index order).  child[2n] / child[2n + 1] = node n's left ('1') / right ('0')
@@ -310,31 +318,16 @@ class HuffmanTree:
     def decode_device(self, bits_dev, nbits, out=None, stream=None):
         """decode_data of a packed MSB-first stream on the device (hic_huffman_decode):
         bits_dev a 4-byte-aligned uint8 tensor, nbits the stream length.  Returns
-        (int32 device tensor of the decoded values, count); leaves whose value is not
-        an int32 (None, from a table with unused codes) decode to their leaf index
-        and ``self.flat()[1]`` maps them back (see decode_packed)."""
+        (int32 device tensor of the decoded values, count, ints); leaves whose value is
+        not an int32 (None, from a table with unused codes) decode to their leaf index
+        (ints False) and ``self.flat()[1]`` maps them back (see decode_packed)."""
         child, leaves = self.flat()
         vals = [l.value for l in leaves]
         ints = all(isinstance(v, (int, np.integer)) and -2 ** 31 <= int(v) < 2 ** 31 for v in vals)
         h_vals = np.asarray([int(v) for v in vals], dtype=np.int32) if ints else None
-        lib = _lib.load()
-        with device.on_stream(stream):
-            if out is None:
-                # every decoded symbol consumes at least the shallowest leaf's depth in
-                # bits: the output needs nbits / that many slots, not one per bit
-                out = device.empty((max(int(nbits) // self.min_code_length(), 1),), torch.int32)
-            ws = device.workspace(lib.hic_huffman_decode_workspace_bytes(int(nbits), len(child) // 2, len(leaves)))
-            count = ctypes.c_int64(0)
-            st = lib.hic_huffman_decode(device.ptr(bits_dev) if nbits else None, int(nbits),
-                                        child.ctypes.data_as(ctypes.c_void_p), len(child) // 2,
-                                        h_vals.ctypes.data_as(ctypes.c_void_p) if ints else None, len(leaves),
-                                        device.ptr(out), out.numel(), ctypes.byref(count), device.ptr(ws),
-                                        device.stream_ptr(stream))
-            if st == _lib.HIC_ERR_ARG and "missing child" in _lib.last_error():
-                # the reference's reduce steps into None: huffman.py:155-161
-                raise AttributeError("'NoneType' object has no attribute 'is_leaf'")
-            _lib.check(st, "hic_huffman_decode")
-        return out, int(count.value), ints
+        out, n = _decode_flat(child, len(child) // 2, h_vals, len(leaves), self.min_code_length, bits_dev, nbits,
+                              out, stream)
+        return out, n, ints
 
     def decode_packed(self, packed, nbits, stream=None):
         """decode_data of a packed MSB-first stream (numpy uint8) through the GPU
@@ -365,6 +358,130 @@ class HuffmanTree:
                 out.append(node.value)
                 node = self.root
         return out
+
+
+def _decode_flat(child, nnodes, h_vals, nleaves, minlen, bits_dev, nbits, out=None, stream=None):
+    """hic_huffman_decode over a flat tree (HuffmanTree.flat's layout): (int32
+    device tensor of the decoded values -- leaf indices when h_vals is None --,
+    count).  minlen: the shortest code, or a callable giving it (only needed to size
+    a missing `out`)."""
+    lib = _lib.load()
+    with device.on_stream(stream):
+        if out is None:
+            # every decoded symbol consumes at least the shallowest leaf's depth in
+            # bits: the output needs nbits / that many slots, not one per bit
+            ml = minlen() if callable(minlen) else minlen
+            out = device.empty((max(int(nbits) // ml, 1),), torch.int32)
+        ws = device.workspace(lib.hic_huffman_decode_workspace_bytes(int(nbits), nnodes, nleaves))
+        count = ctypes.c_int64(0)
+        st = lib.hic_huffman_decode(device.ptr(bits_dev) if nbits else None, int(nbits),
+                                    child.ctypes.data_as(ctypes.c_void_p), nnodes,
+                                    h_vals.ctypes.data_as(ctypes.c_void_p) if h_vals is not None else None, nleaves,
+                                    device.ptr(out), out.numel(), ctypes.byref(count), device.ptr(ws),
+                                    device.stream_ptr(stream))
+        if st == _lib.HIC_ERR_ARG and "missing child" in _lib.last_error():
+            # the reference's reduce steps into None: huffman.py:155-161
+            raise AttributeError("'NoneType' object has no attribute 'is_leaf'")
+        _lib.check(st, "hic_huffman_decode")
+    return out, int(count.value)
+
+
+class CodeBook(_Packer):
+    """The codes of the reference's tree over keys in first-appearance order with
+    their counts, built in native code (hic_huffman_build: HuffmanTree._construct's
+    heapq order, huffman.py:60-79) -- all codec.jpeg_encode needs of a tree: the
+    table payload (encode_table) and the code table the GPU packer reads.
+    HuffmanTree.construct_from_counts builds the same codes from node objects
+    (~12 ms of Python heap work per 8K image; tests/test_cpu_host.py pins the two
+    against each other)."""
+
+    def __init__(self, keys, counts):
+        self.leaf_keys = [int(k) for k in keys]
+        n = len(self.leaf_keys)
+        if n == 0:
+            raise ValueError("a Huffman tree needs at least one key")
+        c = np.ascontiguousarray(counts, dtype=np.int64)
+        if c.shape != (n,):
+            raise ValueError("one count per key")
+        self.lens = np.empty(n, np.uint8)
+        self.bits = np.empty(n, np.uint64)
+        text = ctypes.create_string_buffer(65 * n)
+        _lib.call("hic_huffman_build", c.ctypes.data_as(ctypes.c_void_p), n,
+                  self.lens.ctypes.data_as(ctypes.c_void_p), self.bits.ctypes.data_as(ctypes.c_void_p), text)
+        self._strs = text.value.decode("ascii").split()
+
+    def code_strings(self):
+        """Every leaf's code string, in leaf order."""
+        return self._strs
+
+    def encode_table(self):
+        """[(key, code string)] in leaf order -- HuffmanTree.encode_table's."""
+        return list(zip(self.leaf_keys, self.code_strings()))
+
+    def codes(self):
+        return dict(self.encode_table())
+
+    def code_table(self, key_min, nbins):
+        """(code bits uint64, code lengths uint8) for keys key_min .. key_min + nbins - 1
+        (0 / 0 for keys not in the tree), the table hic_huffman_pack reads."""
+        bits = np.zeros(nbins, dtype=np.uint64)
+        lens = np.zeros(nbins, dtype=np.uint8)
+        idx = np.asarray(self.leaf_keys, dtype=np.int64) - int(key_min)
+        bits[idx] = self.bits
+        lens[idx] = self.lens
+        return bits, lens
+
+
+class FlatCodes:
+    """construct_from_coding's decoding tree (huffman.py:30-58) for a table that is a
+    complete prefix code with int32 values -- every table an encoder writes --, built
+    natively straight into hic_huffman_decode's layout (hic_huffman_from_codes).
+    ``from_table`` returns None for any other table; the caller then builds the
+    reference's own tree (HuffmanTree.construct_from_coding), whose None leaves and
+    unreachable codes behave as the reference's do."""
+
+    def __init__(self, child, nnodes, values, minlen):
+        self.child, self.nnodes, self.values, self.minlen = child, nnodes, values, minlen
+
+    @classmethod
+    def from_table(cls, segments):
+        n = len(segments)
+        if n < 2:
+            return None
+        try:
+            codes = [c for _, c in segments]
+            raw = "".join(codes).encode("ascii")
+            lens = np.fromiter(map(len, codes), dtype=np.int64, count=n)
+        except (TypeError, ValueError, UnicodeEncodeError):
+            return None
+        off = np.zeros(n + 1, np.int64)
+        np.cumsum(lens, out=off[1:])
+        child = np.empty(2 * n, np.int32)
+        seg = np.empty(n, np.int32)
+        nodes, minlen = ctypes.c_int64(0), ctypes.c_int32(0)
+        st = _lib.load().hic_huffman_from_codes(raw, off.ctypes.data_as(ctypes.c_void_p), n,
+                                                child.ctypes.data_as(ctypes.c_void_p),
+                                                seg.ctypes.data_as(ctypes.c_void_p), ctypes.byref(nodes),
+                                                ctypes.byref(minlen))
+        if st != _lib.HIC_OK:
+            return None
+        nn = int(nodes.value)
+        vals = [segments[i][0] for i in seg[:nn + 1].tolist()]  # a full binary tree: nodes + 1 leaves
+        if set(map(type, vals)) <= {int}:  # the common case, checked without a Python loop
+            v64 = np.asarray(vals, dtype=object).astype(np.int64) if vals else np.zeros(0, np.int64)
+        elif all(isinstance(v, (int, np.integer)) for v in vals):
+            v64 = np.asarray([int(v) for v in vals], dtype=object).astype(np.int64)
+        else:
+            return None
+        if v64.size and (v64.min() < -2 ** 31 or v64.max() >= 2 ** 31):
+            return None
+        return cls(child[:2 * nn], nn, v64.astype(np.int32), int(minlen.value))
+
+    def decode_device(self, bits_dev, nbits, out=None, stream=None):
+        """HuffmanTree.decode_device's (values, count, True)."""
+        out, n = _decode_flat(self.child, self.nnodes, self.values, self.values.size, self.minlen, bits_dev, nbits,
+                              out, stream)
+        return out, n, True
 
 
 def first_appearance_counts(keys):
@@ -412,7 +529,7 @@ class DeviceStream:
         present = np.flatnonzero(self.counts)
         order = present[np.argsort(first[present], kind="stable")]
         self.keys_in_order = [int(self.lo + b) for b in order]
-        self.tree = HuffmanTree.construct_from_counts(self.keys_in_order, self.counts[order].astype(np.int64))
+        self.tree = CodeBook(self.keys_in_order, self.counts[order].astype(np.int64))
 
     def packed(self):
         return self.tree.encode_device(self.keys, self.n, self.lo, self.nbins, self.counts, self.stream)
@@ -477,8 +594,7 @@ class DeviceStreams:
             present = np.flatnonzero(c)
             order = present[np.argsort(f[present], kind="stable")]
             self.counts.append(c)
-            self.trees.append(HuffmanTree.construct_from_counts([int(self.lo[i] + b) for b in order],
-                                                                c[order].astype(np.int64)))
+            self.trees.append(CodeBook((order + self.lo[i]).tolist(), c[order].astype(np.int64)))
         self._lib = lib
 
     def packed(self):
@@ -507,7 +623,7 @@ class DeviceStreams:
                       ctypes.c_void_p(out.data_ptr() + int(boff[i])), nbytes[i],
                       ctypes.c_void_p(nbits.data_ptr() + 8 * i), device.ptr(ws), s)
         nb = nbits.cpu().numpy()
-        host = out.cpu().numpy()
+        host = device.to_host(out)  # ~40 MB at 8K: the pinned chunked copy
         res = []
         for i in range(m):
             if int(nb[i]) != totals[i]:

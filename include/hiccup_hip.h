@@ -531,6 +531,26 @@ int hic_huffman_decode(const uint8_t *d_bits, int64_t nbits, const int32_t *h_ch
                        const int32_t *h_values, int32_t nleaves, int32_t *d_out, int64_t out_cap,
                        int64_t *h_count, void *workspace, void *stream);
 
+/* ---- Huffman trees, host side (native, no device work; hufftree.hip).
+ *  hic_huffman_build: HuffmanTree._construct (huffman.py:60-79) over n >= 1 leaves
+ *    whose frequencies h_counts[] are in first-appearance order (utils.group_by):
+ *    heapq's heap compared on frequency only, the first node popped the left child,
+ *    left = '1'.  Leaf i's code: h_len[i] bits, right-aligned in h_code[i] (MSB =
+ *    the edge at the root).  One leaf: code "1".  HIC_ERR_ARG if a code would pass
+ *    64 bits (needs > 2^44 symbols).  h_text (may be null; >= 65 n bytes): the
+ *    codes as text, each followed by one space.
+ *  hic_huffman_from_codes: construct_from_coding (huffman.py:30-58) + the
+ *    breadth-first layout hic_huffman_decode takes, for a table of n >= 2 codes
+ *    that is a complete prefix code: code i is h_chars[h_off[i] .. h_off[i + 1])
+ *    ('0' / '1'; a repeated code keeps its last entry, as the reference's dict
+ *    does).  h_child (>= 2n int32) receives the tree, *h_nodes its internal node
+ *    count, h_leaf_seg (>= n int32) the table entry of each leaf in the tree's leaf
+ *    order, *h_minlen the shortest code.  Any other table: HIC_ERR_ARG ("irregular
+ *    table ..."), nothing written; the caller then builds the reference's own tree. */
+int hic_huffman_build(const int64_t *h_counts, int64_t n, uint8_t *h_len, uint64_t *h_code, char *h_text);
+int hic_huffman_from_codes(const char *h_chars, const int64_t *h_off, int64_t n, int32_t *h_child,
+                           int32_t *h_leaf_seg, int64_t *h_nodes, int32_t *h_minlen);
+
 /* ---- the gather's wire format (no reference counterpart: the bytes that carry a
  *      shard's quantized zig-zag blocks -- codec.jpeg_encode's input after
  *      dct_channel, codec.py:286-301 -- to the gathering rank, losslessly).  Zig-zag

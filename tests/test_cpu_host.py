@@ -432,6 +432,81 @@ def test_huffman_flat_tree_matches_walk(golden_codec):
         t.decode_data("10")
 
 
+def test_native_codebook_golden(golden_codec):
+    """CodeBook (hic_huffman_build, the native heapq tree codec.jpeg_encode uses)
+    reproduces the reference's tables on its own DC / RLE streams, and FlatCodes
+    (hic_huffman_from_codes, jpeg_decode's tree) decodes its bit strings."""
+    g = golden_codec
+    for name in _names(g, "bs_"):
+        for ch in ("lum", "cr", "cb"):
+            for kind, key in (("dc", "dc"), ("av", "acv"), ("al", "acl")):
+                keys = g["%s_%s_%s" % (key, ch, name)]
+                table = list(zip(g["%shv_%s_%s" % (kind, ch, name)].tolist(),
+                                 g["%shc_%s_%s" % (kind, ch, name)].tolist()))
+                cb = huffman.CodeBook(*huffman.first_appearance_counts(keys))
+                assert cb.encode_table() == table, (name, ch, kind)
+                bits = str(g["%sb_%s_%s" % (kind, ch, name)])
+                flat = huffman.FlatCodes.from_table(table)
+                if len(table) < 2:  # a one-code table has an unused '0' side: the reference's tree
+                    assert flat is None
+                    continue
+                assert _walk_flat(flat.child.tolist(), [huffman.HuffmanTree.Node.leaf(int(v), 0)
+                                                        for v in flat.values], bits) == keys.tolist()
+                assert flat.minlen == min(len(c) for _, c in table)
+
+
+@pytest.mark.parametrize("kind", ["uniform", "geometric", "equal_counts", "many_leaves"])
+def test_native_trees_match_heapq(kind):
+    """The native trees == the node-object trees (heapq, huffman.py:60-79), ties
+    included: equal counts in every arrangement, and more than 2500 leaves (CPython's
+    heapify switches to its cache-friendly order there; the heap it builds is the
+    same).  FlatCodes == construct_from_coding + flat() on the resulting tables."""
+    rng = np.random.default_rng({"uniform": 1, "geometric": 2, "equal_counts": 3, "many_leaves": 4}[kind])
+    for _ in range(25 if kind != "many_leaves" else 4):
+        n = int(rng.integers(1, 4000))
+        if kind == "uniform":
+            keys = rng.integers(-int(rng.integers(1, 60)), 60, n)
+        elif kind == "geometric":
+            keys = rng.geometric(0.3, n) * rng.choice([-1, 1], n)
+        elif kind == "equal_counts":
+            keys = np.repeat(rng.integers(-500, 500, max(1, n // 7)), int(rng.integers(1, 8)))
+        else:
+            keys = rng.permutation(np.repeat(np.arange(-1500, 1700), 1 + np.arange(3200) % 3))
+        uniq, counts = huffman.first_appearance_counts(keys)
+        ref = huffman.HuffmanTree.construct_from_counts(uniq, counts)
+        cb = huffman.CodeBook(uniq, counts)
+        table = ref.encode_table()
+        assert cb.encode_table() == table
+        lo, nb = min(uniq), max(uniq) - min(uniq) + 1
+        for a, b in zip(ref.code_table(lo, nb), cb.code_table(lo, nb)):
+            np.testing.assert_array_equal(a, b)
+        flat = huffman.FlatCodes.from_table(table)
+        if len(uniq) == 1:
+            assert flat is None
+            continue
+        dec = huffman.HuffmanTree.construct_from_coding(table)
+        child, leaves = dec.flat()
+        np.testing.assert_array_equal(flat.child, child)
+        assert flat.nnodes == child.size // 2
+        assert flat.values.tolist() == [l.value for l in leaves]
+        assert flat.minlen == dec.min_code_length()
+
+
+def test_native_flat_codes_refuses_irregular_tables():
+    """Tables that are not a complete prefix code of int32 values stay with the
+    reference's own construction (FlatCodes.from_table -> None); a repeated code
+    keeps its last value, as the reference's dict does."""
+    for table in ([(5, "1")], [(5, "1"), (6, "01")], [(5, "1"), (6, "0"), (7, "10")], [(5, "1"), (6, "0x")],
+                  [(5, ""), (6, "0")], [(None, "1"), (6, "0")], [(2 ** 31, "1"), (6, "0")], [(1.0, "1"), (6, "0")]):
+        assert huffman.FlatCodes.from_table(table) is None, table
+    f = huffman.FlatCodes.from_table([(5, "1"), (6, "0"), (9, "1")])
+    assert f.values.tolist() == [9, 6] and f.child.tolist() == [-2, -3]
+    f = huffman.FlatCodes.from_table([(np.int64(-3), "11"), (4, "10"), (True, "0")])
+    assert f.values.tolist() == [1, -3, 4] and f.minlen == 1
+    with pytest.raises(ValueError):
+        huffman.CodeBook([], [])
+
+
 def test_rle_workspace_covers_scan_partitions():
     """hic_rle_workspace_bytes (rle.hip) holds, for any channel size and record
     density (one record per 64-block tile, or per 32-block half tile as the fused

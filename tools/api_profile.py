@@ -48,22 +48,23 @@ ci2 = codec.jpeg_decode(hic)
 calls.append(("jpeg_decompression", lambda: compression.jpeg_decompression(ci2)))
 px = H * W
 bits = sum(len(p.packed_bits()[0]) for p in hic.payloads[9:18])
-moved = {"jpeg_compression": (3 * px, 6 * px // 4 * 4 // 4 * 4),
-         "jpeg_encode": (px * 6 // 4 * 4 // 4 * 4, bits), "jpeg_decode": (bits, px * 12),
-         "jpeg_decompression": (px * 12, 3 * px)}
 moved = {"jpeg_compression": (3 * px, 4 * px * 3 // 2), "jpeg_encode": (4 * px * 3 // 2, bits),
          "jpeg_decode": (bits, 8 * px * 3 // 2), "jpeg_decompression": (8 * px * 3 // 2, 3 * px)}
 for name, f in calls:
     f()
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    f()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t
+    walls = []
+    for _ in range(5):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        f()
+        torch.cuda.synchronize()
+        walls.append(time.perf_counter() - t)
+    wall = float(np.median(walls))
     up, down = moved[name]
     floor = up / r["h2d"] / 1e6 + down / r["d2h"] / 1e6
-    print("== %s: %.1f ms wall; PCIe floor %.1f ms (%.0f MB up, %.0f MB down)" % (name, wall * 1e3, floor, up / 1e6,
-                                                                                 down / 1e6))
+    print("== %s: %.1f ms wall (median of 5; %s); PCIe floor %.1f ms (%.0f MB up, %.0f MB down), ratio %.2f"
+          % (name, wall * 1e3, " ".join("%.1f" % (w * 1e3) for w in walls), floor, up / 1e6, down / 1e6,
+             wall * 1e3 / floor))
     pr = cProfile.Profile()
     pr.enable()
     f()

@@ -690,6 +690,24 @@ def _extra_8k_jpeg_decode(steps, codec, device, hicimage, pipeline):
             "timed_decodes": steps}
 
 
+def pinned_rates(nbytes=256 << 20, reps=4):
+    """Pinned host <-> device copy rates of this box (GB/s), torch copies of one
+    256 MiB buffer."""
+    h = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    out = {}
+    for name, f in (("h2d_gbs", lambda: d.copy_(h, non_blocking=True)),
+                    ("d2h_gbs", lambda: h.copy_(d, non_blocking=True))):
+        f()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(reps):
+            f()
+        torch.cuda.synchronize()
+        out[name] = round(reps * nbytes / (time.perf_counter() - t) / 1e9, 1)
+    return out
+
+
 def extra_8k_reference_api(steps=3):
     """The drop-in surface at 8K from host arrays, as a user of the reference calls
     it: compression.jpeg_compression (RGB -> quantized planes), codec.jpeg_encode
@@ -714,10 +732,28 @@ def extra_8k_reference_api(steps=3):
         ci2, t_dec = med(lambda: codec.jpeg_decode(hic))
         rec, t_decomp = med(lambda: compression.jpeg_decompression(ci2))
         same = all(np.array_equal(a, b) for a, b in zip(ci.as_dict.values(), ci2.as_dict.values()))
+        # each call's PCIe floor: the bytes it must move at this box's pinned rates
+        rates = pinned_rates()
+        px = H8K * W8K
+        bits = sum(int(p.packed_bits()[0].size) for p in hic.payloads[9:18])
+        moved = {"jpeg_compression": (3 * px, 4 * px * 3 // 2), "jpeg_encode": (4 * px * 3 // 2, bits),
+                 "jpeg_decode": (bits, 8 * px * 3 // 2), "jpeg_decompression": (8 * px * 3 // 2, 3 * px)}
+        walls = {"jpeg_compression": t_comp, "jpeg_encode": t_enc, "jpeg_decode": t_dec,
+                 "jpeg_decompression": t_decomp}
+        floors = {}
+        for k, (up, down) in moved.items():
+            f = up / rates["h2d_gbs"] / 1e6 + down / rates["d2h_gbs"] / 1e6
+            floors[k] = {"bytes_up": up, "bytes_down": down, "floor_ms": round(f, 2),
+                         "ratio": round(walls[k] / f, 2)}
         return {"workload": "8K RGB through the reference API from host arrays (jpeg_compression, jpeg_encode, "
                             "jpeg_decode, jpeg_decompression), host copies included",
                 "ms_jpeg_compression": t_comp, "ms_jpeg_encode": t_enc, "ms_jpeg_decode": t_dec,
-                "ms_jpeg_decompression": t_decomp, "planes_equal_after_entropy_round_trip": same,
+                "ms_jpeg_decompression": t_decomp, "pcie": dict(rates, **floors),
+                "pcie_note": "floor = the call's host<->device bytes (uint8 RGB, int32 planes for jpeg_compression's "
+                             "result / jpeg_encode's input, the coded bits, float64 planes for jpeg_decode's result / "
+                             "jpeg_decompression's input) at the pinned H2D / D2H rates measured here; ratio = "
+                             "wall / floor",
+                "planes_equal_after_entropy_round_trip": same,
                 "rgb_out_shape": list(rec.shape), "timed_calls": steps}
     finally:
         settings.DEBUG = debug

@@ -43,6 +43,13 @@ class SlotJob(ctypes.Structure):
                 ("sym_val", _vp), ("sym_cap", _i64)]
 
 
+class HuffDecodeJob(ctypes.Structure):
+    """hic_huffman_decode_job (include/hiccup_hip.h): one stream of hic_huffman_decode_batch."""
+    _fields_ = [("d_bits", _vp), ("nbits", _i64), ("h_child", _vp), ("nnodes", ctypes.c_int32), ("h_values", _vp),
+                ("nleaves", ctypes.c_int32), ("d_out", _vp), ("out_cap", _i64), ("workspace", _vp),
+                ("count", _i64), ("status", ctypes.c_int32)]
+
+
 class DctPlaneJob(ctypes.Structure):
     """hic_dct_plane_job (include/hiccup_hip.h)."""
     _fields_ = [("plane", _vp), ("H", _i64), ("W", _i64), ("stride", _i64), ("table_id", _int), ("out", _vp),
@@ -82,6 +89,7 @@ SIGNATURES = {
     "hic_huffman_decode_workspace_bytes": (_sz, [_i64, ctypes.c_int32, ctypes.c_int32]),
     "hic_huffman_decode": (_int, [_vp, _i64, _vp, ctypes.c_int32, _vp, ctypes.c_int32, _vp, _i64, _vp, _vp, _vp]),
     "hic_huffman_build": (_int, [_vp, _i64, _vp, _vp, _vp]),
+    "hic_huffman_decode_batch": (_int, [_int, _vp, _vp]),
     "hic_huffman_from_codes": (_int, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),
     "hic_huffman_pack": (_int, [_vp, _int, _i64, ctypes.c_int32, ctypes.c_int32, _vp, _vp, _vp, _i64, _vp, _vp,
                                 _vp]),

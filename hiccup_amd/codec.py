@@ -205,7 +205,7 @@ def _jpeg_encode(compressed):
     utils.debug_msg("Starting JPEG encoding")
     bs = settings.JPEG_BLOCK_SIZE
     chans = ("lum", "cr", "cb")
-    keys, dc_type = {}, {}
+    enc, dc_type = {}, {}
     for k, v in compressed.as_dict.items():
         # the reference's DC keys are elements of the plane (utils.differences over
         # block[0][0]): numpy scalars of its dtype
@@ -213,8 +213,11 @@ def _jpeg_encode(compressed):
         p = _i32_device(v, "coefficient plane")
         if p.ndim != 2:
             raise ValueError("expected a 2-D coefficient plane")
-        dc, Ls, Vs, cnt = encode_channel_device(p, p.shape[0], p.shape[1], bs)
-        count = int(device.to_host(cnt)[0])
+        # no host read here: the next plane's upload overlaps this plane's RLE
+        enc[k] = encode_channel_device(p, p.shape[0], p.shape[1], bs)
+    counts = torch.cat([enc[k][3] for k in enc]).cpu().tolist()
+    keys = {}
+    for (k, (dc, Ls, Vs, _)), count in zip(enc.items(), counts):
         # trees per channel: DC differences, AC values, AC lengths (codec.py:304-313)
         keys[k] = ((dc, dc.numel()), (Vs, count), (Ls, count))
     # the nine streams in payload order (codec.py:310-330); each tree codes the
@@ -271,7 +274,7 @@ def _jpeg_decode(hic_image):
     p = hic_image.payloads
     chans = ("lum", "cr", "cb")
     trees = [_decoding_tree(p[i]) for i in range(9)]
-    streams = [_huffman_stream_device(p[9 + i], trees[i]) for i in range(9)]
+    streams = _huffman_streams_device([p[9 + i] for i in range(9)], trees)
     shapes = {"lum": p[18].numbers, "cr": p[19].numbers, "cb": p[19].numbers}
     bs = settings.JPEG_BLOCK_SIZE
     sub_length = bs * bs - 1
@@ -295,24 +298,65 @@ def _decoding_tree(data):
     return flat if flat is not None else huffman_decode(data)
 
 
-def _huffman_stream_device(payload, tree):
-    """huffman_data_decode on the GPU: (int32 device tensor, count).  Streams whose
-    tree holds a leaf that is not an int32 (a table with unused codes decodes them
-    to None) go through the values on the host, where the reference's arithmetic on
-    them fails the same way."""
-    packed, nbits = payload.packed_bits()
-    if isinstance(tree, huffman.HuffmanTree) and tree.root.is_leaf:  # no edges: the reference's walk fails on the first bit
-        tree.decode_data("1" if nbits else "")
-        return device.to_device(np.zeros(1, np.int32)), 0
-    buf = np.zeros(-(-max(int(nbits), 1) // 32) * 4, np.uint8)
-    body = np.asarray(packed, dtype=np.uint8)[:-(-int(nbits) // 8)]
-    buf[:body.size] = body
-    d, n, ints = tree.decode_device(device.to_device(buf), nbits)
-    if not ints:
-        leaves = tree.flat()[1]
-        vals = _i32([leaves[i].value for i in device.to_host(d[:n]).tolist()], "decoded values")
-        return device.to_device(vals if n else np.zeros(1, np.int32)), n
-    return d, n
+def _huffman_streams_device(payloads, trees):
+    """_huffman_stream_device of every (payload, tree) -- codec.jpeg_decode's nine
+    huffman_data_decode calls (codec.py:372-388) -- in ONE hic_huffman_decode_batch:
+    the bits go up in one copy, the streams share each phase's host wait.  Errors as
+    the reference's sequential decode raises them: the first failing stream in
+    payload order."""
+    n = len(payloads)
+    lib = _lib.load()
+    res, errs, jobs_at = [None] * n, [None] * n, []
+    bufs, offs, tot = [], [], 0
+    for i, (pl, tree) in enumerate(zip(payloads, trees)):
+        packed, nbits = pl.packed_bits()
+        nbits = int(nbits)
+        if isinstance(tree, huffman.HuffmanTree) and tree.root.is_leaf:
+            try:  # no edges: the reference's walk fails on the first bit
+                tree.decode_data("1" if nbits else "")
+                res[i] = (device.to_device(np.zeros(1, np.int32)), 0, True)
+            except Exception as e:  # noqa: BLE001 -- raised below, in payload order
+                errs[i] = e
+            continue
+        words = -(-max(nbits, 1) // 32) * 4
+        body = np.asarray(packed, dtype=np.uint8)[:-(-nbits // 8)]
+        bufs.append((body, words))
+        offs.append(tot)
+        tot += words
+        jobs_at.append((i, nbits, tree.decode_args()))
+    if jobs_at:
+        dbits = device.to_device_parts([body for body, _ in bufs], offs, tot)
+        jobs = (_lib.HuffDecodeJob * len(jobs_at))()
+        keep = []
+        for k, ((i, nbits, (child, nnodes, h_vals, nleaves, minlen)), o) in enumerate(zip(jobs_at, offs)):
+            ml = minlen() if callable(minlen) else minlen
+            out = device.empty((max(nbits // ml, 1),), torch.int32)
+            ws = device.workspace(lib.hic_huffman_decode_workspace_bytes(nbits, nnodes, nleaves))
+            keep.append((out, ws, child, h_vals))
+            jobs[k] = _lib.HuffDecodeJob(dbits.data_ptr() + o, nbits, child.ctypes.data, nnodes,
+                                         h_vals.ctypes.data if h_vals is not None else None, nleaves, out.data_ptr(),
+                                         out.numel(), ws.data_ptr(), 0, 0)
+        st = lib.hic_huffman_decode_batch(len(jobs_at), jobs, device.stream_ptr())
+        if st != _lib.HIC_OK and all(j.status == _lib.HIC_OK for j in jobs):
+            _lib.check(st, "hic_huffman_decode_batch")  # refused before anything ran
+        for k, (i, _, (_, _, h_vals, _, _)) in enumerate(jobs_at):
+            j = jobs[k]
+            if j.status == _lib.HIC_ERR_ARG:
+                # the reference's reduce steps into None: huffman.py:155-161
+                errs[i] = AttributeError("'NoneType' object has no attribute 'is_leaf'")
+            elif j.status != _lib.HIC_OK:
+                errs[i] = MemoryError("hic_huffman_decode_batch: stream %d decoded %d symbols" % (i, j.count))
+            else:
+                res[i] = (keep[k][0], int(j.count), h_vals is not None)
+    for i in range(n):
+        if errs[i] is not None:
+            raise errs[i]
+        d, cnt, ints = res[i]
+        if not ints:  # a table with non-int32 leaves: the leaf indices map back on the host
+            leaves = trees[i].flat()[1]
+            vals = _i32([leaves[x].value for x in device.to_host(d[:cnt]).tolist()], "decoded values")
+            res[i] = (device.to_device(vals if cnt else np.zeros(1, np.int32)), cnt, True)
+    return [(d, cnt) for d, cnt, _ in res]
 
 
 def _decode_channel(dc, lens, vals, n, shape, bs):

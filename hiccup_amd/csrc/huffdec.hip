@@ -6,7 +6,7 @@
 // a leaf's value and restarts at the root; trailing bits that do not finish a code
 // are dropped, and a step into a missing child (a one-leaf encoding tree's empty
 // right side) raises.  The stream has no markers, so it is cut into fixed
-// subsequences of g.sub bits (kSub = 1024; with equal-length codes of L bits the
+// subsequences of g.sub bits (kSub = 256; with equal-length codes of L bits the
 // multiple of L at or above it, so every subsequence starts on a codeword), one
 // per thread, decoded speculatively from their nominal first bit; Huffman codes
 // resynchronise within a few codewords, so after the exit bit of subsequence i is
@@ -29,7 +29,11 @@ namespace hic {
 namespace {
 
 constexpr int kLutBits = 12, kLut = 1 << kLutBits;
-constexpr int kSub = 1024;      // bits per subsequence (one thread each), at least
+// bits per subsequence (one thread each), at least.  256: the nine streams of an 8K
+// jpeg_decode decode in 5.0-5.4 ms with the host upload, against 6.6 at 512 and 8.9
+// at 1024 (more threads, shorter serial chains; 128 and 64 measured the same or
+// slower: profiles/r06/huffdec/)
+constexpr int kSub = 256;
 constexpr int kDT = 256;        // threads per workgroup
 constexpr int kMaxRounds = 24;  // resynchronisation rounds before the serial chain
 constexpr int kRoundsPerSync = 4;  // rounds launched between two host reads of their flags
@@ -44,7 +48,14 @@ struct BitReader {
   int64_t nwords, wi;
   uint64_t acc;
   int nacc;
-  __device__ uint32_t load(int64_t i) const { return i < nwords ? __builtin_bswap32(w[i]) : 0u; }
+  // the workgroup's words [lw0, lw0 + lwn), byte-swapped, in LDS (lwn = 0: none):
+  // a thread's refills are then LDS reads, not a chain of dependent global loads
+  const uint32_t *lw = nullptr;
+  int64_t lw0 = 0, lwn = 0;
+  __device__ uint32_t load(int64_t i) const {
+    if ((uint64_t)(i - lw0) < (uint64_t)lwn) return lw[i - lw0];
+    return i < nwords ? __builtin_bswap32(w[i]) : 0u;
+  }
   __device__ void refill() {
     if (nacc <= 32) {
       acc |= (uint64_t)load(wi++) << (32 - nacc);
@@ -111,12 +122,20 @@ struct DecGeo {
 
 // Symbols starting in [start, end): count and the first codeword start >= end
 // (kEnd at the stream end or after a missing child: nothing follows).
+struct LdsWords {  // a workgroup's staged words (n = 0: read global memory)
+  const uint32_t *w;
+  int64_t w0, n;
+};
+
 __device__ void count_sub(const DecGeo &g, const uint32_t *lut, int64_t start, int64_t end, int64_t &exit,
-                          int32_t &count) {
+                          int32_t &count, LdsWords lw = LdsWords{nullptr, 0, 0}) {
   count = 0;
   exit = start;
   if (start >= end) return;
   BitReader br;
+  br.lw = lw.w;
+  br.lw0 = lw.w0;
+  br.lwn = lw.n;
   br.init(g.words, g.nwords, start);
   int64_t p = start;
   int sym;
@@ -135,16 +154,35 @@ __device__ void stage_lut(const uint32_t *__restrict__ lut, uint32_t *s_lut) {
   __syncthreads();
 }
 
+// The words this workgroup's subsequences read -- bits [b kDT sub, (b + 1) kDT sub)
+// and a margin for the codes that run past the last one -- staged in LDS by
+// coalesced loads (a subsequence is at most kSub + 23 bits: kSub, or a multiple of
+// an equal code length L <= 24 at or above it); measured: 5.0-5.2 vs 5.5 ms for the
+// nine 8K streams reading global memory directly (profiles/r06/huffdec/)
+constexpr int kWinMargin = 64;  // words past the workgroup's bits (codes up to 2048 bits)
+constexpr int kWinWords = kDT * (kSub + 23) / 32 + 2 + kWinMargin;
+__device__ LdsWords stage_words(const DecGeo &g, uint32_t *s_w) {
+  const int64_t b0 = (int64_t)blockIdx.x * kDT * g.sub;
+  const int64_t w0 = b0 >> 5;
+  int64_t n = ((b0 + (int64_t)kDT * g.sub + 31) >> 5) + kWinMargin - w0;
+  if (n > kWinWords) n = kWinWords;
+  for (int64_t k = threadIdx.x; k < n; k += kDT) s_w[k] = w0 + k < g.nwords ? __builtin_bswap32(g.words[w0 + k]) : 0u;
+  __syncthreads();
+  return LdsWords{s_w, w0, n};
+}
+
 // round 0: every subsequence from its nominal first bit
 __global__ __launch_bounds__(kDT) void k_hd_count(DecGeo g, int64_t *__restrict__ start, int64_t *__restrict__ exit,
                                                   int32_t *__restrict__ cnt) {
   __shared__ uint32_t s_lut[kLut];
+  __shared__ uint32_t s_win[kWinWords];
   stage_lut(g.lut, s_lut);
+  const LdsWords lw = stage_words(g, s_win);
   const int64_t i = (int64_t)blockIdx.x * kDT + threadIdx.x;
   if (i >= g.nsub) return;
   int64_t e;
   int32_t c;
-  count_sub(g, s_lut, i * g.sub, (i + 1) * g.sub, e, c);
+  count_sub(g, s_lut, i * g.sub, (i + 1) * g.sub, e, c, lw);
   start[i] = i * g.sub;
   exit[i] = e;
   cnt[i] = c;
@@ -155,17 +193,22 @@ __global__ __launch_bounds__(kDT) void k_hd_sync(DecGeo g, int64_t *__restrict__
                                                  const int64_t *__restrict__ exit_in, int64_t *__restrict__ exit_out,
                                                  int32_t *__restrict__ cnt, int32_t *__restrict__ changed) {
   __shared__ uint32_t s_lut[kLut];
-  stage_lut(g.lut, s_lut);
+  __shared__ uint32_t s_win[kWinWords];
   const int64_t i = (int64_t)blockIdx.x * kDT + threadIdx.x;
-  if (i >= g.nsub) return;
-  const int64_t s = i == 0 ? 0 : exit_in[i - 1];
-  if (s == start[i]) {
-    exit_out[i] = exit_in[i];
-    return;
+  int64_t s = 0;
+  bool redo = false;
+  if (i < g.nsub) {
+    s = i == 0 ? 0 : exit_in[i - 1];
+    redo = s != start[i];
+    if (!redo) exit_out[i] = exit_in[i];
   }
+  if (!__syncthreads_or(redo)) return;  // workgroup-uniform: nothing to re-decode here
+  stage_lut(g.lut, s_lut);
+  const LdsWords lw = stage_words(g, s_win);
+  if (!redo) return;
   int64_t e;
   int32_t c;
-  count_sub(g, s_lut, s, (i + 1) * g.sub, e, c);
+  count_sub(g, s_lut, s, (i + 1) * g.sub, e, c, lw);
   start[i] = s;
   exit_out[i] = e;
   cnt[i] = c;
@@ -241,8 +284,10 @@ __global__ __launch_bounds__(kDT) void k_hd_emit(DecGeo g, const int64_t *__rest
                                                  const int32_t *__restrict__ values, int32_t *__restrict__ out,
                                                  int64_t out_cap, unsigned long long *__restrict__ err) {
   __shared__ uint32_t s_lut[kLut];
+  __shared__ uint32_t s_win[kWinWords];
   __shared__ int64_t s_w[kDT / 64];
   stage_lut(g.lut, s_lut);
+  const LdsWords lw = stage_words(g, s_win);
   const int64_t i = (int64_t)blockIdx.x * kDT + threadIdx.x;
   int64_t tot;
   const int64_t o = boff[blockIdx.x] + blk_excl(i < g.nsub ? cnt[i] : 0, s_w, tot);
@@ -250,6 +295,9 @@ __global__ __launch_bounds__(kDT) void k_hd_emit(DecGeo g, const int64_t *__rest
   const int64_t s = start[i], end = (i + 1) * g.sub;
   if (s >= end) return;
   BitReader br;
+  br.lw = lw.w;
+  br.lw0 = lw.w0;
+  br.lwn = lw.n;
   br.init(g.words, g.nwords, s);
   int64_t p = s, k = o;
   int sym;
@@ -307,13 +355,26 @@ extern "C" size_t hic_huffman_decode_workspace_bytes(int64_t nbits, int32_t nnod
                   3 * round_up(nsub * 8, r) + round_up(nsub * 4, r) + round_up((nblk + 1) * 8, r) + 3 * r);
 }
 
-extern "C" int hic_huffman_decode(const uint8_t *d_bits, int64_t nbits, const int32_t *h_child, int32_t nnodes,
-                                  const int32_t *h_values, int32_t nleaves, int32_t *d_out, int64_t out_cap,
-                                  int64_t *h_count, void *workspace, void *stream) {
-  if (!h_child || !h_count || !workspace || (nbits > 0 && (!d_bits || !d_out)))
-    return arg_error("null pointer");
-  if (nbits < 0 || out_cap < 0) return arg_error("nbits / out_cap");
-  if (reinterpret_cast<uintptr_t>(d_bits) % 4) return arg_error("d_bits must be 4-byte aligned");
+namespace {
+// one stream's host-side state through the batch's phases
+struct DecState {
+  std::vector<uint32_t> lut;
+  DecGeo g;
+  DecWs w;
+  dim3 grid;
+  int64_t *ein, *eout;
+  bool synced;
+  int32_t changed[kRoundsPerSync];
+  int64_t host[2];  // {symbols, first error bit} read back
+};
+
+// validation, the lookup table and the subsequence length of one job (no device work)
+int decode_prepare(const hic_huffman_decode_job &j, DecState &st) {
+  const int32_t nnodes = j.nnodes, nleaves = j.nleaves;
+  const int32_t *h_child = j.h_child;
+  if (!h_child || !j.workspace || (j.nbits > 0 && (!j.d_bits || !j.d_out))) return arg_error("null pointer");
+  if (j.nbits < 0 || j.out_cap < 0) return arg_error("nbits / out_cap");
+  if (reinterpret_cast<uintptr_t>(j.d_bits) % 4) return arg_error("d_bits must be 4-byte aligned");
   if (nnodes < 1 || nnodes >= (1 << 24) || nleaves < 1 || nleaves >= (1 << 24))
     return arg_error("tree size (1 <= nodes, leaves < 2^24)");
   // a tree: indices in range, every node but the root the child of exactly one node
@@ -326,7 +387,7 @@ extern "C" int hic_huffman_decode(const uint8_t *d_bits, int64_t nbits, const in
       return arg_error("child[%lld] = %d is not a tree edge", (long long)k, c);
   }
   // the kLutBits-bit lookup table from the root
-  std::vector<uint32_t> lut(kLut);
+  st.lut.assign(kLut, 0);
   for (int v = 0; v < kLut; ++v) {
     int node = 0;
     uint32_t e = ((uint32_t)(kLutBits - 1)) | (kNode << 4);
@@ -343,12 +404,11 @@ extern "C" int hic_huffman_decode(const uint8_t *d_bits, int64_t nbits, const in
       node = c;
       e = ((uint32_t)(kLutBits - 1)) | (kNode << 4) | ((uint32_t)node << 8);
     }
-    lut[v] = e;
+    st.lut[v] = e;
   }
-  const hipStream_t s = as_stream(stream);
   // equal-length codes (every leaf at one depth L, e.g. a near-uniform table): a
   // subsequence of a multiple of L bits starts on a codeword, so round 0 is already
-  // synchronised (with 1024 bits and L not dividing it the rounds may never converge)
+  // synchronised (with kSub bits and L not dividing it the rounds may never converge)
   int64_t sub = kSub;
   {
     std::vector<int32_t> depth((size_t)nnodes, -1);
@@ -371,69 +431,127 @@ extern "C" int hic_huffman_decode(const uint8_t *d_bits, int64_t nbits, const in
     }
     if (equal && leaf_depth > 0) sub = (int64_t)leaf_depth * ceil_div(kSub, leaf_depth);
   }
-  const int64_t nsub = ceil_div(nbits, sub) > 0 ? ceil_div(nbits, sub) : 1;
-  DecWs w = carve(workspace, nsub, nnodes, nleaves);
-  *h_count = 0;
-  if (nbits == 0) return HIC_OK;
-  if (int e = hip_status(hipMemcpyAsync(w.lut, lut.data(), kLut * 4, hipMemcpyHostToDevice, s), "hipMemcpyAsync"))
-    return e;
-  if (int e = hip_status(hipMemcpyAsync(w.child, h_child, (size_t)2 * nnodes * 4, hipMemcpyHostToDevice, s),
-                         "hipMemcpyAsync"))
-    return e;
-  if (h_values)
-    if (int e = hip_status(hipMemcpyAsync(w.values, h_values, (size_t)nleaves * 4, hipMemcpyHostToDevice, s),
+  const int64_t nsub = ceil_div(j.nbits, sub) > 0 ? ceil_div(j.nbits, sub) : 1;
+  st.w = carve(j.workspace, nsub, nnodes, nleaves);
+  st.g = DecGeo{reinterpret_cast<const uint32_t *>(j.d_bits), ceil_div(j.nbits, 32), j.nbits, nsub, sub, st.w.lut,
+                st.w.child};
+  st.grid = dim3((unsigned)ceil_div(nsub, kDT));
+  st.ein = st.w.exit_a;
+  st.eout = st.w.exit_b;
+  st.synced = nsub == 1;
+  return HIC_OK;
+}
+}  // namespace
+
+// The streams of a batch go through each phase together on one HIP stream, so the
+// host waits once per phase for all of them (3 waits when every stream
+// resynchronises within kRoundsPerSync rounds) instead of once per phase per stream.
+extern "C" int hic_huffman_decode_batch(int n, hic_huffman_decode_job *jobs, void *stream) {
+  if (n < 0 || (n > 0 && !jobs)) return arg_error("jobs");
+  std::vector<DecState> st((size_t)n);
+  for (int i = 0; i < n; ++i) {  // every job checked before anything is queued
+    jobs[i].count = 0;
+    jobs[i].status = HIC_OK;
+    if (int e = decode_prepare(jobs[i], st[i])) return e;
+  }
+  const hipStream_t s = as_stream(stream);
+  bool any = false;
+  for (int i = 0; i < n; ++i) {
+    const hic_huffman_decode_job &j = jobs[i];
+    if (j.nbits == 0) continue;
+    any = true;
+    DecWs &w = st[i].w;
+    if (int e = hip_status(hipMemcpyAsync(w.lut, st[i].lut.data(), kLut * 4, hipMemcpyHostToDevice, s),
                            "hipMemcpyAsync"))
       return e;
+    if (int e = hip_status(hipMemcpyAsync(w.child, j.h_child, (size_t)2 * j.nnodes * 4, hipMemcpyHostToDevice, s),
+                           "hipMemcpyAsync"))
+      return e;
+    if (j.h_values)
+      if (int e = hip_status(hipMemcpyAsync(w.values, j.h_values, (size_t)j.nleaves * 4, hipMemcpyHostToDevice, s),
+                             "hipMemcpyAsync"))
+        return e;
+  }
+  if (!any) return HIC_OK;
   // the host tables are locals / the caller's: wait for the uploads before anything can return
   if (int e = hip_status(hipStreamSynchronize(s), "hipStreamSynchronize")) return e;
-  if (int e = hip_status(hipMemsetAsync(w.err, 0xFF, 8, s), "hipMemsetAsync")) return e;
-  DecGeo g{reinterpret_cast<const uint32_t *>(d_bits), ceil_div(nbits, 32), nbits, nsub, sub, w.lut, w.child};
-  const dim3 grid((unsigned)ceil_div(nsub, kDT)), block(kDT);
-  hipLaunchKernelGGL(k_hd_count, grid, block, 0, s, g, w.start, w.exit_a, w.cnt);
-  if (int e = check_launch("k_hd_count")) return e;
-  int64_t *ein = w.exit_a, *eout = w.exit_b;
-  bool synced = nsub == 1;
-  // rounds in batches of kRoundsPerSync, one host read of their change flags per
-  // batch: a round without a change means every later one has none either
-  for (int round = 0; !synced && round < kMaxRounds; round += kRoundsPerSync) {
-    if (int e = hip_status(hipMemsetAsync(w.changed, 0, 4 * kRoundsPerSync, s), "hipMemsetAsync")) return e;
-    for (int k = 0; k < kRoundsPerSync; ++k) {
-      hipLaunchKernelGGL(k_hd_sync, grid, block, 0, s, g, w.start, ein, eout, w.cnt, w.changed + k);
-      if (int e = check_launch("k_hd_sync")) return e;
-      int64_t *t = ein;
-      ein = eout;
-      eout = t;
+  for (int i = 0; i < n; ++i) {
+    if (jobs[i].nbits == 0) continue;
+    DecState &x = st[i];
+    if (int e = hip_status(hipMemsetAsync(x.w.err, 0xFF, 8, s), "hipMemsetAsync")) return e;
+    hipLaunchKernelGGL(k_hd_count, x.grid, dim3(kDT), 0, s, x.g, x.w.start, x.ein, x.w.cnt);
+    if (int e = check_launch("k_hd_count")) return e;
+  }
+  // rounds in batches of kRoundsPerSync, one host read of every stream's change flags
+  // per batch: a round without a change means every later one has none either
+  for (int round = 0; round < kMaxRounds; round += kRoundsPerSync) {
+    bool pending = false;
+    for (int i = 0; i < n; ++i) {
+      DecState &x = st[i];
+      if (jobs[i].nbits == 0 || x.synced) continue;
+      pending = true;
+      if (int e = hip_status(hipMemsetAsync(x.w.changed, 0, 4 * kRoundsPerSync, s), "hipMemsetAsync")) return e;
+      for (int k = 0; k < kRoundsPerSync; ++k) {
+        hipLaunchKernelGGL(k_hd_sync, x.grid, dim3(kDT), 0, s, x.g, x.w.start, x.ein, x.eout, x.w.cnt,
+                           x.w.changed + k);
+        if (int e = check_launch("k_hd_sync")) return e;
+        std::swap(x.ein, x.eout);
+      }
+      if (int e = hip_status(hipMemcpyAsync(x.changed, x.w.changed, 4 * kRoundsPerSync, hipMemcpyDeviceToHost, s),
+                             "hipMemcpyAsync"))
+        return e;
     }
-    int32_t changed[kRoundsPerSync] = {};
-    if (int e = hip_status(hipMemcpyAsync(changed, w.changed, 4 * kRoundsPerSync, hipMemcpyDeviceToHost, s),
-                           "hipMemcpyAsync"))
-      return e;
+    if (!pending) break;
     if (int e = hip_status(hipStreamSynchronize(s), "hipStreamSynchronize")) return e;
-    for (int k = 0; k < kRoundsPerSync; ++k) synced = synced || changed[k] == 0;
+    for (int i = 0; i < n; ++i) {
+      DecState &x = st[i];
+      if (jobs[i].nbits == 0 || x.synced) continue;
+      for (int k = 0; k < kRoundsPerSync; ++k) x.synced = x.synced || x.changed[k] == 0;
+    }
   }
-  if (!synced) {
-    hipLaunchKernelGGL(k_hd_chain, dim3(1), dim3(1), 0, s, g, w.start, ein, w.cnt);
-    if (int e = check_launch("k_hd_chain")) return e;
+  for (int i = 0; i < n; ++i) {
+    const hic_huffman_decode_job &j = jobs[i];
+    if (j.nbits == 0) continue;
+    DecState &x = st[i];
+    if (!x.synced) {
+      hipLaunchKernelGGL(k_hd_chain, dim3(1), dim3(1), 0, s, x.g, x.w.start, x.ein, x.w.cnt);
+      if (int e = check_launch("k_hd_chain")) return e;
+    }
+    hipLaunchKernelGGL(k_hd_bsum, x.grid, dim3(kDT), 0, s, x.w.cnt, x.g.nsub, x.w.bsum);
+    hipLaunchKernelGGL(k_hd_scan, dim3(1), dim3(kDT), 0, s, x.w.bsum, (int64_t)x.grid.x, x.w.total);
+    hipLaunchKernelGGL(k_hd_emit, x.grid, dim3(kDT), 0, s, x.g, x.w.start, x.w.cnt, x.w.bsum,
+                       j.h_values ? x.w.values : nullptr, j.d_out, j.out_cap, x.w.err);
+    if (int e = check_launch("k_hd_emit")) return e;
+    if (int e = hip_status(hipMemcpyAsync(x.host, x.w.total, 16, hipMemcpyDeviceToHost, s), "hipMemcpyAsync"))
+      return e;
   }
-  hipLaunchKernelGGL(k_hd_bsum, grid, block, 0, s, w.cnt, nsub, w.bsum);
-  hipLaunchKernelGGL(k_hd_scan, dim3(1), block, 0, s, w.bsum, (int64_t)grid.x, w.total);
-  hipLaunchKernelGGL(k_hd_emit, grid, block, 0, s, g, w.start, w.cnt, w.bsum, h_values ? w.values : nullptr, d_out,
-                     out_cap, w.err);
-  if (int e = check_launch("k_hd_emit")) return e;
-  int64_t host[2];
-  if (int e = hip_status(hipMemcpyAsync(host, w.total, 16, hipMemcpyDeviceToHost, s), "hipMemcpyAsync")) return e;
   if (int e = hip_status(hipStreamSynchronize(s), "hipStreamSynchronize")) return e;
-  const unsigned long long err = (unsigned long long)host[1];
-  if (err != ~0ULL) {
-    // the symbols before the failing one are in d_out; *h_count says how many
-    *h_count = host[0];
-    set_error("Huffman walk stepped into a missing child at bit %llu", err);
-    return HIC_ERR_ARG;
+  int first = HIC_OK;
+  for (int i = 0; i < n; ++i) {
+    hic_huffman_decode_job &j = jobs[i];
+    if (j.nbits == 0) continue;
+    const DecState &x = st[i];
+    const unsigned long long err = (unsigned long long)x.host[1];
+    j.count = x.host[0];  // on a missing child: the symbols before the failing one are in d_out
+    if (err != ~0ULL) {
+      j.status = HIC_ERR_ARG;
+      if (first == HIC_OK) set_error("Huffman walk stepped into a missing child at bit %llu", err);
+    } else if (x.host[0] > j.out_cap) {
+      j.status = HIC_ERR_CAPACITY;
+      if (first == HIC_OK) set_error("decoded %lld symbols, out_cap %lld", (long long)x.host[0], (long long)j.out_cap);
+    }
+    if (first == HIC_OK) first = j.status;
   }
-  *h_count = host[0];
-  if (host[0] > out_cap) {
-    set_error("decoded %lld symbols, out_cap %lld", (long long)host[0], (long long)out_cap);
-    return HIC_ERR_CAPACITY;
-  }
-  return HIC_OK;
+  return first;
+}
+
+extern "C" int hic_huffman_decode(const uint8_t *d_bits, int64_t nbits, const int32_t *h_child, int32_t nnodes,
+                                  const int32_t *h_values, int32_t nleaves, int32_t *d_out, int64_t out_cap,
+                                  int64_t *h_count, void *workspace, void *stream) {
+  if (!h_count) return arg_error("null pointer");
+  hic_huffman_decode_job j{d_bits, nbits, h_child, nnodes, h_values, nleaves, d_out, out_cap, workspace, 0, 0};
+  *h_count = 0;
+  const int rc = hic_huffman_decode_batch(1, &j, stream);
+  *h_count = j.count;
+  return rc;
 }

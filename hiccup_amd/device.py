@@ -72,6 +72,45 @@ def to_device(a):
     return out
 
 
+def to_device_parts(parts, offsets, nbytes):
+    """One new uint8 device tensor of nbytes holding host uint8 array parts[i] at
+    byte offsets[i] (ascending, non-overlapping) and zeros elsewhere: the parts go
+    straight into the pinned staging buffers (one host copy; to_device of a
+    concatenation would copy twice)."""
+    require_gpu()
+    out = torch.empty((max(int(nbytes), 1),), dtype=torch.uint8, device="cuda")
+    spans = [(int(o), np.ascontiguousarray(a).reshape(-1).view(np.uint8)) for o, a in zip(offsets, parts)]
+    with _staging_lock:
+        s = _copy_stream()
+        s.wait_stream(torch.cuda.current_stream())
+        done = [None, None]
+        for i, (c0, n) in enumerate(_chunks(int(nbytes))):
+            st = _stage(i % 2, n)
+            if done[i % 2] is not None:
+                done[i % 2].synchronize()
+            sn = st.numpy()
+            pos = c0  # bytes of this chunk before `pos` are written
+            for o, a in spans:
+                a0, a1 = max(o, c0), min(o + a.size, c0 + n)
+                if a1 <= c0 or a0 >= c0 + n:
+                    continue
+                if a0 > pos:
+                    sn[pos - c0:a0 - c0] = 0
+                _par_copy(sn[a0 - c0:a1 - c0], a[a0 - o:a1 - o])
+                pos = a1
+            if pos < c0 + n:
+                sn[pos - c0:] = 0
+            with torch.cuda.stream(s):
+                out[c0:c0 + n].copy_(st, non_blocking=True)
+                done[i % 2] = torch.cuda.Event()
+                done[i % 2].record(s)
+        torch.cuda.current_stream().wait_stream(s)
+        for e in done:
+            if e is not None:
+                e.synchronize()
+    return out
+
+
 def empty(shape, dtype):
     require_gpu()
     return torch.empty(shape, dtype=dtype, device="cuda")

@@ -321,13 +321,19 @@ class HuffmanTree(_Packer):
         (int32 device tensor of the decoded values, count, ints); leaves whose value is
         not an int32 (None, from a table with unused codes) decode to their leaf index
         (ints False) and ``self.flat()[1]`` maps them back (see decode_packed)."""
+        child, nnodes, h_vals, nleaves, minlen = self.decode_args()
+        out, n = _decode_flat(child, nnodes, h_vals, nleaves, minlen, bits_dev, nbits, out, stream)
+        return out, n, h_vals is not None
+
+    def decode_args(self):
+        """(child, nodes, int32 leaf values or None, leaves, minlen -- a callable) as
+        hic_huffman_decode takes the tree; values None when a leaf is not an int32
+        (the kernel then writes leaf indices)."""
         child, leaves = self.flat()
         vals = [l.value for l in leaves]
         ints = all(isinstance(v, (int, np.integer)) and -2 ** 31 <= int(v) < 2 ** 31 for v in vals)
         h_vals = np.asarray([int(v) for v in vals], dtype=np.int32) if ints else None
-        out, n = _decode_flat(child, len(child) // 2, h_vals, len(leaves), self.min_code_length, bits_dev, nbits,
-                              out, stream)
-        return out, n, ints
+        return child, len(child) // 2, h_vals, len(leaves), self.min_code_length
 
     def decode_packed(self, packed, nbits, stream=None):
         """decode_data of a packed MSB-first stream (numpy uint8) through the GPU
@@ -476,6 +482,9 @@ class FlatCodes:
         if v64.size and (v64.min() < -2 ** 31 or v64.max() >= 2 ** 31):
             return None
         return cls(child[:2 * nn], nn, v64.astype(np.int32), int(minlen.value))
+
+    def decode_args(self):
+        return self.child, self.nnodes, self.values, self.values.size, self.minlen
 
     def decode_device(self, bits_dev, nbits, out=None, stream=None):
         """HuffmanTree.decode_device's (values, count, True)."""

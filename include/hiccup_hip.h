@@ -530,6 +530,27 @@ size_t hic_huffman_decode_workspace_bytes(int64_t nbits, int32_t nnodes, int32_t
 int hic_huffman_decode(const uint8_t *d_bits, int64_t nbits, const int32_t *h_child, int32_t nnodes,
                        const int32_t *h_values, int32_t nleaves, int32_t *d_out, int64_t out_cap,
                        int64_t *h_count, void *workspace, void *stream);
+/* hic_huffman_decode_batch: n hic_huffman_decode calls (codec.jpeg_decode's nine
+ *    streams) on one stream with their host round trips shared: every job is
+ *    checked before anything is queued (HIC_ERR_ARG, nothing run), then the streams
+ *    go through each phase together.  Per job: count = symbols decoded, status =
+ *    HIC_OK / HIC_ERR_ARG (missing child) / HIC_ERR_CAPACITY as hic_huffman_decode
+ *    returns them; the call returns the first job's non-OK status (its message in
+ *    hic_last_error) or HIC_OK.  Each job needs its own workspace. */
+typedef struct {
+  const uint8_t *d_bits;
+  int64_t nbits;
+  const int32_t *h_child;
+  int32_t nnodes;
+  const int32_t *h_values;
+  int32_t nleaves;
+  int32_t *d_out;
+  int64_t out_cap;
+  void *workspace;
+  int64_t count;  /* out */
+  int32_t status; /* out */
+} hic_huffman_decode_job;
+int hic_huffman_decode_batch(int n, hic_huffman_decode_job *jobs, void *stream);
 
 /* ---- Huffman trees, host side (native, no device work; hufftree.hip).
  *  hic_huffman_build: HuffmanTree._construct (huffman.py:60-79) over n >= 1 leaves

@@ -797,6 +797,49 @@ def test_huffman_decode_device_edges():
         assert tree.decode_packed(*hicimage.BitStringP(bits).packed_bits()) == tree.decode_data(bits)
 
 
+def test_huffman_decode_batch_streams():
+    """codec.jpeg_decode's batched decode (hic_huffman_decode_batch through
+    codec._huffman_streams_device) == one decode_data walk per stream: native flat
+    trees and node-object trees side by side, a table with a None leaf, an empty
+    stream, a one-leaf tree; a missing child in one stream raises AttributeError
+    only after every earlier stream decoded, and the first failure in payload order
+    wins over a later one."""
+    from hiccup_amd import codec, huffman
+    rng = np.random.default_rng(11)
+    payloads, trees, want = [], [], []
+    for kind in ("values", "lengths", "none_leaf", "empty", "single", "skewed"):
+        if kind == "none_leaf":
+            t = huffman.HuffmanTree.construct_from_coding([(5, "1"), (6, "01")])  # "00" decodes to None
+            bits = "1011" * 300 + "1"
+            payloads.append(hicimage.BitStringP(bits))
+            trees.append(t)
+            want.append(t.decode_data(bits))
+            continue
+        keys = {"values": np.round(rng.laplace(0, 40, 50_001)), "lengths": rng.integers(0, 15, 70_000),
+                "empty": np.array([4, 4, 9]), "single": np.full(33, 7),
+                "skewed": (rng.geometric(0.35, 30_000) - 1) * 3 - 40}[kind].astype(np.int64)
+        table = huffman.CodeBook(*huffman.first_appearance_counts(keys)).encode_table()
+        codes = dict(table)
+        bits = "" if kind == "empty" else "".join(codes[int(k)] for k in keys)
+        t = huffman.FlatCodes.from_table(table) or huffman.HuffmanTree.construct_from_coding(table)
+        payloads.append(hicimage.BitStringP(bits))
+        trees.append(t)
+        want.append([] if kind == "empty" else keys.tolist())
+    assert isinstance(trees[0], huffman.FlatCodes) and isinstance(trees[4], huffman.HuffmanTree)
+    got = codec._huffman_streams_device(payloads, trees)
+    for (d, n), w in zip(got, want):
+        assert n == len(w) and d[:n].cpu().tolist() == [x for x in w], n
+    # a one-leaf encoding tree walks into its missing '0' child
+    bad = huffman.HuffmanTree.construct_from_data([3, 3, 3])
+    bad_bits = hicimage.BitStringP("1" * 5000 + "0" + "1" * 50)
+    with pytest.raises(AttributeError):
+        codec._huffman_streams_device(payloads[:2] + [bad_bits] + payloads[2:], trees[:2] + [bad] + trees[2:])
+    # first failure in payload order: an out-of-int32 leaf value (ValueError) before the walk error
+    big = huffman.HuffmanTree.construct_from_coding([(2 ** 40, "1"), (1, "0")])
+    with pytest.raises(ValueError):
+        codec._huffman_streams_device([hicimage.BitStringP("10"), bad_bits], [big, bad])
+
+
 def test_huffman_decode_device_full_size():
     """An 8K-sized AC value stream (22 M symbols, Laplace keys): GPU pack then GPU
     decode returns the keys (compared on the device)."""

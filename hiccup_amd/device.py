@@ -3,6 +3,7 @@ the compute is entirely in libhiccup_hip.so.  No CPU fallback: without a HIP
 device every entry point raises ``HipUnavailable``."""
 import contextlib
 import ctypes
+import os
 import sys
 import threading
 
@@ -215,6 +216,7 @@ def to_device_i32(a, nonint_msg, range_msg):
 # threads take turns under _staging_lock), a copy stream for their DMAs, and a small
 # thread pool for the host side of the copies
 _PIN_MIN = 4 << 20
+_HOST_THREADS = int(os.environ.get("HICCUP_HOST_THREADS", "8"))  # host copy threads
 _CHUNK = 32 << 20
 _staging = [None, None]
 _staging_lock = threading.Lock()
@@ -280,7 +282,7 @@ def _ensure_pool():
     global _pool
     if _pool is None:
         from concurrent.futures import ThreadPoolExecutor
-        _pool = ThreadPoolExecutor(8)
+        _pool = ThreadPoolExecutor(_HOST_THREADS)
 
 
 def _copy_stream():
@@ -296,7 +298,7 @@ def _par_copy(dst, src):
     _ensure_pool()
     d, s_ = dst.reshape(-1), src.reshape(-1)
     n = d.size
-    k = 8 if n >= (1 << 20) else 1
+    k = _HOST_THREADS if n >= (1 << 20) else 1
     bounds = [(i * n // k, (i + 1) * n // k) for i in range(k)]
     list(_pool.map(lambda ab: np.copyto(d[ab[0]:ab[1]], s_[ab[0]:ab[1]], casting="unsafe"), bounds))
 

@@ -797,6 +797,22 @@ def test_huffman_decode_device_edges():
         assert tree.decode_packed(*hicimage.BitStringP(bits).packed_bits()) == tree.decode_data(bits)
 
 
+@pytest.mark.parametrize("dtype", [np.uint8, np.int16, np.int32])
+def test_key_range_all_widths(dtype):
+    """hic_key_range (the histograms' bin range) == numpy min / max for every key
+    width, at lengths around the vectorised int32 form's 4-key loads and at an
+    address that is not 16-byte aligned (the one-key form)."""
+    from hiccup_amd import huffman
+    rng = np.random.default_rng(5)
+    info = np.iinfo(dtype)
+    for n in (1, 3, 4, 5, 1023, 4096 + 3, 1_000_001):
+        keys = rng.integers(max(info.min, -40000), min(info.max, 40000) + 1, n).astype(dtype)
+        d = device.to_device(keys)
+        assert huffman.device_key_range(d, n) == (int(keys.min()), int(keys.max())), (n, dtype)
+        if n > 2:
+            assert huffman.device_key_range(d[1:], n - 1) == (int(keys[1:].min()), int(keys[1:].max()))
+
+
 def test_huffman_decode_batch_streams():
     """codec.jpeg_decode's batched decode (hic_huffman_decode_batch through
     codec._huffman_streams_device) == one decode_data walk per stream: native flat

@@ -53,6 +53,10 @@ def to_device(a):
         return torch.from_numpy(a).to("cuda")
     out = torch.empty(tuple(a.shape), dtype=torch.from_numpy(a[:0].reshape(-1)).dtype, device="cuda")
     ob, ab = out.reshape(-1).view(torch.uint8), a.reshape(-1).view(np.uint8)
+    if _is_pinned(ab):  # already page-locked: one DMA, no staging copy
+        ob.copy_(torch.from_numpy(ab), non_blocking=True)
+        torch.cuda.current_stream().synchronize()  # the caller may reuse `a` on return
+        return out
     with _staging_lock:
         s = _copy_stream()
         s.wait_stream(torch.cuda.current_stream())  # `out` was allocated on the current stream
@@ -167,6 +171,9 @@ def to_host(t):
     t = t.contiguous()
     out = host_empty(tuple(t.shape), torch.empty(0, dtype=t.dtype).numpy().dtype)
     tb, ob = t.reshape(-1).view(torch.uint8), out.reshape(-1).view(np.uint8)
+    if _is_pinned(ob):  # a pinned pool buffer: the DMA writes the result in place
+        torch.from_numpy(ob).copy_(tb)
+        return out
     with _staging_lock:
         _d2h_chunks(tb, nbytes, lambda o, n, st: _par_copy(ob[o:o + n], st))
     return out
@@ -182,6 +189,12 @@ def to_host_f64(t):
     t = t.contiguous()
     n = t.numel()
     out = host_empty((n,), np.float64)
+    if n and _is_pinned(out):
+        # a pinned pool buffer: widen on the device and DMA the float64 values in
+        # place (CPU writes into pinned memory run at ~0.73x of pageable here, so
+        # the host-side cast below would cost more than the doubled bytes)
+        torch.from_numpy(out).copy_(t.reshape(-1).to(torch.float64))
+        return out.reshape(tuple(t.shape))
     with _staging_lock:
         _d2h_chunks(t.reshape(-1).view(torch.uint8), 4 * n,
                     lambda o, nb, st: _par_copy(out[o // 4:(o + nb) // 4], st.view(np.int32)))
@@ -241,11 +254,15 @@ def _stage(k, nbytes):
 # Host result arrays.  A fresh numpy array of a few hundred MB costs its page faults
 # on first touch (~11 ms per 133 MB single-threaded on the GPU box, ~22 ms when eight
 # copy threads fault it together; the DMA itself is 2.3 ms): the large results of
-# to_host / to_host_f64 are views of pooled, already-faulted buffers instead.  A
-# pooled buffer is handed out again only when nothing but the pool references it (a
-# caller's result, or any view of it, keeps it out of the pool).
+# to_host / to_host_f64 are views of pooled buffers instead, and the pool's buffers
+# are pinned, so a result the DMA writes needs no staging copy, and a result handed
+# back (jpeg_compression's planes into jpeg_encode, jpeg_decode's into
+# jpeg_decompression) goes up without one either.  A pooled buffer is handed out
+# again only when nothing but the pool references it (a caller's result, or any view
+# of it, keeps it out of the pool).
 _HOST_POOL_MAX = 4 << 30  # bytes the pool may hold
 _host_pool = []
+_pinned_spans = []  # [start, end) addresses of the pool's pinned buffers
 _host_pool_lock = threading.Lock()
 
 
@@ -262,11 +279,23 @@ def host_empty(shape, dtype):
             if b.nbytes >= nbytes and sys.getrefcount(b) <= 3 and (best is None or b.nbytes < best.nbytes):
                 best = b
         if best is None:
-            best = np.empty(nbytes, np.uint8)
-            _fault_in(best)
             if sum(b.nbytes for b in _host_pool) + nbytes <= _HOST_POOL_MAX:
+                # pinned (page-locked, so also faulted in): DMA reaches it directly
+                best = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True).numpy()
                 _host_pool.append(best)
+                _pinned_spans.append((best.ctypes.data, best.ctypes.data + nbytes))
+            else:
+                best = np.empty(nbytes, np.uint8)
+                _fault_in(best)
         return best[:nbytes].view(dt).reshape(shape)
+
+
+def _is_pinned(a):
+    """Whether host array a lies inside a pinned pool buffer (a result of to_host /
+    to_host_f64 or a view of one): the DMA can then read / write it in place."""
+    lo = a.ctypes.data
+    hi = lo + a.nbytes
+    return any(s <= lo and hi <= e for s, e in _pinned_spans)
 
 
 def _fault_in(buf):

@@ -43,6 +43,13 @@ class SlotJob(ctypes.Structure):
                 ("sym_val", _vp), ("sym_cap", _i64)]
 
 
+class Encode420Job(ctypes.Structure):
+    """hic_encode420_job (include/hiccup_hip.h): one encode of hic_encode420_batch_u8."""
+    _fields_ = [("rgb_rows", _vp), ("in_row0", _i64), ("in_rows", _i64), ("H", _i64), ("W", _i64),
+                ("out_row0", _i64), ("out_rows", _i64), ("coef_y", _vp), ("coef_cr", _vp), ("coef_cb", _vp),
+                ("ws_y", _vp), ("ws_cr", _vp), ("ws_cb", _vp)]
+
+
 class HuffDecodeJob(ctypes.Structure):
     """hic_huffman_decode_job (include/hiccup_hip.h): one stream of hic_huffman_decode_batch."""
     _fields_ = [("d_bits", _vp), ("nbits", _i64), ("h_child", _vp), ("nnodes", ctypes.c_int32), ("h_values", _vp),
@@ -89,6 +96,9 @@ SIGNATURES = {
     "hic_huffman_decode_workspace_bytes": (_sz, [_i64, ctypes.c_int32, ctypes.c_int32]),
     "hic_huffman_decode": (_int, [_vp, _i64, _vp, ctypes.c_int32, _vp, ctypes.c_int32, _vp, _i64, _vp, _vp, _vp]),
     "hic_huffman_build": (_int, [_vp, _i64, _vp, _vp, _vp]),
+    "hic_zigzag8_blocks_i16": (_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
+    "hic_event_record": (_int, [_vp, _vp]),
+    "hic_encode420_batch_u8": (_int, [_int, _vp, _int, _vp, _vp, _vp]),
     "hic_huffman_decode_batch": (_int, [_int, _vp, _vp]),
     "hic_huffman_from_codes": (_int, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),
     "hic_huffman_pack": (_int, [_vp, _int, _i64, ctypes.c_int32, ctypes.c_int32, _vp, _vp, _vp, _i64, _vp, _vp,

@@ -159,6 +159,29 @@ def encode_channel_device(raster_dev, H, W, bs, stream=None):
     return dc, Ls, Vs, cnt
 
 
+def encode_channel_device8(raster_dev, H, W, stream=None):
+    """encode_channel_device for 8x8 blocks through int16: the zig-zag writes int16
+    blocks (hic_zigzag8_blocks_i16) and the hot path's 16-bit RLE codes them
+    (hic_rle_encode_i16: uint8 lengths, int16 values).  Returns (dc_diff, lengths,
+    values, count, wide): wide (device int32[1]) is 1 when a coefficient did not fit
+    int16, and the plane must then go through encode_channel_device instead."""
+    nbx, nby = -(-W // 8), -(-H // 8)
+    nblk = nbx * nby
+    s = device.stream_ptr(stream)
+    blocks = device.empty((nblk, 64), torch.int16)
+    wide = device.empty((1,), torch.int32)
+    _lib.call("hic_zigzag8_blocks_i16", device.ptr(raster_dev), H, W, device.ptr(blocks), device.ptr(wide), s)
+    cap = nblk * 63 + 1
+    dc = device.empty((nblk,), torch.int32)
+    Ls = device.empty((cap,), torch.uint8)
+    Vs = device.empty((cap,), torch.int16)
+    cnt = device.empty((1,), torch.int64)
+    ws = device.workspace(_lib.load().hic_rle_workspace_bytes(nblk, 64))
+    _lib.call("hic_rle_encode_i16", device.ptr(blocks), nblk, 64, MAX_LEN, ctypes.c_void_p(0), device.ptr(dc),
+              device.ptr(Ls), device.ptr(Vs), cap, device.ptr(cnt), device.ptr(ws), s)
+    return dc, Ls, Vs, cnt, wide
+
+
 def encode_channel(plane, bs=None):
     """(dc_diffs, ac_lengths, ac_values) numpy arrays for one coefficient plane."""
     bs = settings.JPEG_BLOCK_SIZE if bs is None else bs
@@ -205,7 +228,7 @@ def _jpeg_encode(compressed):
     utils.debug_msg("Starting JPEG encoding")
     bs = settings.JPEG_BLOCK_SIZE
     chans = ("lum", "cr", "cb")
-    enc, dc_type = {}, {}
+    enc, dc_type, planes = {}, {}, {}
     for k, v in compressed.as_dict.items():
         # the reference's DC keys are elements of the plane (utils.differences over
         # block[0][0]): numpy scalars of its dtype
@@ -213,11 +236,26 @@ def _jpeg_encode(compressed):
         p = _i32_device(v, "coefficient plane")
         if p.ndim != 2:
             raise ValueError("expected a 2-D coefficient plane")
-        # no host read here: the next plane's upload overlaps this plane's RLE
-        enc[k] = encode_channel_device(p, p.shape[0], p.shape[1], bs)
-    counts = torch.cat([enc[k][3] for k in enc]).cpu().tolist()
+        planes[k] = p
+        # no host read here: the next plane's upload overlaps this plane's RLE.  8x8
+        # blocks go through int16 (the hot path's RLE); a plane with a coefficient
+        # outside int16 is redone below through int32
+        enc[k] = (encode_channel_device8(p, p.shape[0], p.shape[1]) if bs == 8 else
+                  encode_channel_device(p, p.shape[0], p.shape[1], bs) + (None,))
+    flags = torch.cat([torch.cat([e[3], e[4].to(torch.int64)]) if e[4] is not None else
+                       torch.cat([e[3], torch.zeros(1, dtype=torch.int64, device=e[3].device)])
+                       for e in enc.values()]).cpu().tolist()
+    counts = []
+    for i, k in enumerate(list(enc)):
+        cnt, wide = flags[2 * i], flags[2 * i + 1]
+        if wide:
+            p = planes[k]
+            enc[k] = encode_channel_device(p, p.shape[0], p.shape[1], bs) + (None,)
+            cnt = int(enc[k][3].cpu()[0])
+        counts.append(cnt)
+    del planes
     keys = {}
-    for (k, (dc, Ls, Vs, _)), count in zip(enc.items(), counts):
+    for (k, (dc, Ls, Vs, _, _)), count in zip(enc.items(), counts):
         # trees per channel: DC differences, AC values, AC lengths (codec.py:304-313)
         keys[k] = ((dc, dc.numel()), (Vs, count), (Ls, count))
     # the nine streams in payload order (codec.py:310-330); each tree codes the

@@ -70,6 +70,11 @@ extern "C" int hic_event_destroy(void *event) {
   return hic::hip_status(hipEventDestroy((hipEvent_t)event), "hipEventDestroy");
 }
 
+extern "C" int hic_event_record(void *event, void *stream) {
+  if (!event) return hic::arg_error("null event");
+  return hic::hip_status(hipEventRecord((hipEvent_t)event, hic::as_stream(stream)), "hipEventRecord");
+}
+
 extern "C" int hic_event_elapsed_ms(void *start, void *stop, float *h_ms) {
   if (!start || !stop || !h_ms) return hic::arg_error("null pointer");
   int rc = hic::hip_status(hipEventSynchronize((hipEvent_t)stop), "hipEventSynchronize");

@@ -433,19 +433,11 @@ struct EncColour {
 // SLOTS (TMF 15, whole images with W % 512 == 0; hic_encode420_slots_u8): each pass
 // emits its record's AC symbols and DC differences into the slot layout (slots.h)
 // instead of storing the int16 coefficients: no coefficient ever reaches HBM.
-template <int TMF, bool SLOTS = false>
-__global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_eu(3))) void k_encode420(Enc420 E) {
+// One unit (wave g of the launch's E): the kernels below map their waves to units.
+template <int TMF, bool SLOTS>
+__device__ __forceinline__ void encode_unit(const Enc420 &E, int g, int lane, uint2 *st2, uint32_t *s_chroma) {
   static_assert(!SLOTS || TMF == kSlotM, "the slot layout packs 4-bit lengths (max_len 15)");
-  __shared__ __attribute__((aligned(16))) uint2 s_stage[HIC_ENC_WPB * 64 * kStageU2];
-  __shared__ uint32_t s_chroma_all[HIC_ENC_WPB][2 * 8 * 64];
-  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint2 *st2 = s_stage + wv * 64 * kStageU2;
-  uint32_t *s_chroma = s_chroma_all[wv];
-  const int bx = __builtin_amdgcn_readfirstlane(E.xcd ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x);
   int16_t *st = reinterpret_cast<int16_t *>(st2 + lane * kStageU2);
-  // wave g: strip s of unit row u0
-  const int g = __builtin_amdgcn_readfirstlane(bx * HIC_ENC_WPB + wv);
-  if (g >= E.nunits) return;  // wave-uniform
   const int u0 = __builtin_amdgcn_readfirstlane(g / E.nstrips);
   const int s = __builtin_amdgcn_readfirstlane(g - u0 * E.nstrips);
   const int y0 = E.out_row0 + 16 * u0;
@@ -528,6 +520,43 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
   y_blocks(0);
   y_blocks(1);
   c_blocks();
+}
+
+template <int TMF, bool SLOTS = false>
+__global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_eu(3))) void k_encode420(Enc420 E) {
+  __shared__ __attribute__((aligned(16))) uint2 s_stage[HIC_ENC_WPB * 64 * kStageU2];
+  __shared__ uint32_t s_chroma_all[HIC_ENC_WPB][2 * 8 * 64];
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int bx = __builtin_amdgcn_readfirstlane(E.xcd ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x);
+  // wave g: strip s of unit row u0
+  const int g = __builtin_amdgcn_readfirstlane(bx * HIC_ENC_WPB + wv);
+  if (g >= E.nunits) return;  // wave-uniform
+  encode_unit<TMF, SLOTS>(E, g, lane, s_stage + wv * 64 * kStageU2, s_chroma_all[wv]);
+}
+
+// Several encodes in ONE launch (hic_encode420_batch_u8: the row shards of a
+// multi-GPU group, one per image): job j owns waves [unit0[j], unit0[j + 1]).  A
+// shard is 1/N of an image -- 506 waves at N = 8, a sixth of the chip's 3072 wave
+// slots -- so N launches in a row ran ~2.4x the time of one whole-image launch.
+constexpr int kEncBatchMax = 8;
+struct Enc420Batch {
+  Enc420 e[kEncBatchMax];
+  int unit0[kEncBatchMax + 1];
+  int n, xcd;
+};
+
+template <int TMF>
+__global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_eu(3))) void k_encode420_batch(
+    Enc420Batch B) {
+  __shared__ __attribute__((aligned(16))) uint2 s_stage[HIC_ENC_WPB * 64 * kStageU2];
+  __shared__ uint32_t s_chroma_all[HIC_ENC_WPB][2 * 8 * 64];
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int bx = __builtin_amdgcn_readfirstlane(B.xcd ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x);
+  const int g = __builtin_amdgcn_readfirstlane(bx * HIC_ENC_WPB + wv);
+  if (g >= B.unit0[B.n]) return;  // wave-uniform
+  int j = 0;
+  while (j + 1 < B.n && g >= B.unit0[j + 1]) ++j;  // wave-uniform
+  encode_unit<TMF, false>(B.e[j], g - B.unit0[j], lane, s_stage + wv * 64 * kStageU2, s_chroma_all[wv]);
 }
 
 // Memory-only probe of k_encode420's byte pattern (bench.py's in-run floor for the
@@ -618,10 +647,11 @@ __global__ __launch_bounds__(64 * HIC_ENC_WPB) __attribute__((amdgpu_waves_per_e
 
 using namespace hic;
 
-static int encode420(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, int64_t H, int64_t W,
-                     int64_t out_row0, int64_t out_rows, int16_t *coef_y, int16_t *coef_cr, int16_t *coef_cb,
-                     void *ws_y, void *ws_cr, void *ws_cb, int max_len, void *stream, void *ev_start, void *ev_stop,
-                     bool seg, int64_t wsb_y = 0, int64_t wsb_c = 0) {
+// checks one encode's arguments and fills its kernel argument (no launch)
+static int prep420(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, int64_t H, int64_t W, int64_t out_row0,
+                   int64_t out_rows, int16_t *coef_y, int16_t *coef_cr, int16_t *coef_cb, void *ws_y, void *ws_cr,
+                   void *ws_cb, int max_len, bool seg, int64_t wsb_y, int64_t wsb_c, Enc420 &E, bool &recs,
+                   bool &aligned) {
   if (!rgb_rows || !coef_y || !coef_cr || !coef_cb) return arg_error("null pointer");
   if (H < 16 || W < 16 || H >= (1 << 20) || W >= (1 << 20)) return arg_error("image shape");
   if (W % 16 || H % 16) return arg_error("hic_encode420_u8 needs W %% 16 == 0 and H %% 16 == 0");
@@ -636,7 +666,7 @@ static int encode420(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, 
   if ((reinterpret_cast<uintptr_t>(coef_y) | reinterpret_cast<uintptr_t>(coef_cr) |
        reinterpret_cast<uintptr_t>(coef_cb)) % 16)
     return arg_error("coefficient buffers must be 16-byte aligned");
-  const bool recs = ws_y && ws_cr && ws_cb;
+  recs = ws_y && ws_cr && ws_cb;
   if ((ws_y || ws_cr || ws_cb) && !recs) return arg_error("workspaces: all three or none");
   if (recs && (max_len < 0 || max_len > 256)) return arg_error("max_len");
   if (seg && recs) {
@@ -649,7 +679,7 @@ static int encode420(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, 
       return arg_error("hic_encode420_seg_u8: workspaces of %lld / %lld bytes, %lld / %lld needed", (long long)wsb_y,
                        (long long)wsb_c, (long long)need_y, (long long)need_c);
   }
-  Enc420 E{};
+  E = Enc420{};
   E.rgb = rgb_rows;
   E.in_row0 = (int)in_row0;
   E.in_rows = (int)in_rows;
@@ -662,7 +692,7 @@ static int encode420(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, 
   E.coef[2] = coef_cb;
   // ragged last strip: the records come from a tile pass after the launch, or (seg)
   // one per strip segment from the kernel itself
-  const bool aligned = W % 512 == 0 || seg;
+  aligned = W % 512 == 0 || seg;
   E.rec[0] = aligned ? static_cast<int64_t *>(ws_y) : nullptr;
   E.rec[1] = aligned ? static_cast<int64_t *>(ws_cr) : nullptr;
   E.rec[2] = aligned ? static_cast<int64_t *>(ws_cb) : nullptr;
@@ -678,6 +708,18 @@ static int encode420(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, 
   const int order = knob(HIC_KNOB_ENCODE_ORDER);
   E.xcd = (order >> 1) & 1;
   E.alt = (order >> 2) & 1;
+  return HIC_OK;
+}
+
+static int encode420(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, int64_t H, int64_t W,
+                     int64_t out_row0, int64_t out_rows, int16_t *coef_y, int16_t *coef_cr, int16_t *coef_cb,
+                     void *ws_y, void *ws_cr, void *ws_cb, int max_len, void *stream, void *ev_start, void *ev_stop,
+                     bool seg, int64_t wsb_y = 0, int64_t wsb_c = 0) {
+  Enc420 E;
+  bool recs = false, aligned = false;
+  if (int e = prep420(rgb_rows, in_row0, in_rows, H, W, out_row0, out_rows, coef_y, coef_cr, coef_cb, ws_y, ws_cr,
+                      ws_cb, max_len, seg, wsb_y, wsb_c, E, recs, aligned))
+    return e;
   const dim3 grid((unsigned)((E.nunits + HIC_ENC_WPB - 1) / HIC_ENC_WPB)), block(64 * HIC_ENC_WPB);
   hipStream_t s = as_stream(stream);
   hipEvent_t e0 = static_cast<hipEvent_t>(ev_start), e1 = static_cast<hipEvent_t>(ev_stop);
@@ -707,6 +749,40 @@ extern "C" int hic_encode420_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_
                                 void *ev_start, void *ev_stop) {
   return encode420(rgb_rows, in_row0, in_rows, H, W, out_row0, out_rows, coef_y, coef_cr, coef_cb, ws_y, ws_cr, ws_cb,
                    max_len, stream, ev_start, ev_stop, false);
+}
+
+extern "C" int hic_encode420_batch_u8(int n, const hic_encode420_job *jobs, int max_len, void *stream,
+                                     void *ev_start, void *ev_stop) {
+  if (n < 1 || n > kEncBatchMax || !jobs) return arg_error("1 <= n <= %d jobs", kEncBatchMax);
+  if (max_len != 15 && max_len != 0) return arg_error("max_len 15 or 0");
+  Enc420Batch B{};
+  B.n = n;
+  B.unit0[0] = 0;
+  for (int j = 0; j < n; ++j) {  // every job checked before the launch
+    const hic_encode420_job &J = jobs[j];
+    bool recs = false, aligned = false;
+    if (int e = prep420(J.rgb_rows, J.in_row0, J.in_rows, J.H, J.W, J.out_row0, J.out_rows, J.coef_y, J.coef_cr,
+                        J.coef_cb, J.ws_y, J.ws_cr, J.ws_cb, max_len, false, 0, 0, B.e[j], recs, aligned))
+      return e;
+    if (recs && !aligned) return arg_error("job %d: W %% 512 != 0 (the records need a tile pass: encode it alone)", j);
+    if ((int64_t)B.unit0[j] + B.e[j].nunits > INT32_MAX / 64) return arg_error("too many units");
+    B.unit0[j + 1] = B.unit0[j] + B.e[j].nunits;
+  }
+  B.xcd = B.e[0].xcd;
+  const dim3 grid((unsigned)((B.unit0[n] + HIC_ENC_WPB - 1) / HIC_ENC_WPB)), block(64 * HIC_ENC_WPB);
+  hipStream_t s = as_stream(stream);
+  hipEvent_t e0 = static_cast<hipEvent_t>(ev_start), e1 = static_cast<hipEvent_t>(ev_stop);
+  auto launch = [&](auto kern) {
+    if (e0 || e1)
+      hipExtLaunchKernelGGL(kern, grid, block, 0, s, e0, e1, 0, B);
+    else
+      hipLaunchKernelGGL(kern, grid, block, 0, s, B);
+  };
+  if (max_len == 15)
+    launch(k_encode420_batch<15>);
+  else
+    launch(k_encode420_batch<0>);
+  return check_launch("k_encode420_batch");
 }
 
 extern "C" int hic_encode420_seg_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_rows, int64_t H, int64_t W,

@@ -1372,6 +1372,22 @@ __global__ void k_zigzag_i32(const int32_t *__restrict__ raster, int H, int W, i
   out[i] = (yy < H && xx < W) ? raster[(int64_t)yy * W + xx] : 0;
 }
 
+// 8x8 form into int16 blocks (jpeg_encode's fast path): *wide = 1 when a value is
+// outside int16 (the caller then takes the int32 path for the plane)
+__global__ __launch_bounds__(256) void k_zigzag8_i16(const int32_t *__restrict__ raster, int H, int W, int nbx,
+                                                     int64_t total, int16_t *__restrict__ out, int *__restrict__ wide) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int64_t b = i >> 6;
+  const int bi = (int)(b / nbx), bj = (int)(b - (int64_t)bi * nbx);
+  int u, v;
+  zz_pos((int)(i & 63), 8, u, v);
+  const int yy = bi * 8 + u, xx = bj * 8 + v;
+  const int x = (yy < H && xx < W) ? raster[(int64_t)yy * W + xx] : 0;
+  if (x < -32768 || x > 32767) atomicOr(wide, 1);
+  out[i] = (int16_t)x;
+}
+
 __global__ void k_izigzag_i32(const int32_t *__restrict__ blocks, int H, int W, int N, int nbx, int64_t total,
                               int32_t *__restrict__ raster) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2017,6 +2033,19 @@ extern "C" int hic_zigzag_blocks_i32(const int32_t *raster, int64_t H, int64_t W
   hipLaunchKernelGGL(k_zigzag_i32, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream), raster,
                      (int)H, (int)W, N, nbx, total, out);
   return check_launch("k_zigzag_i32");
+}
+
+extern "C" int hic_zigzag8_blocks_i16(const int32_t *raster, int64_t H, int64_t W, int16_t *out, int32_t *d_wide,
+                                      void *stream) {
+  if (!raster || !out || !d_wide) return arg_error("null pointer");
+  if (H <= 0 || W <= 0 || H >= (1LL << 31) || W >= (1LL << 31)) return arg_error("shape");
+  const int nbx = (int)((W + 7) / 8), nby = (int)((H + 7) / 8);
+  const int64_t total = (int64_t)nbx * nby * 64;
+  hipStream_t s = as_stream(stream);
+  if (int e = hip_status(hipMemsetAsync(d_wide, 0, 4, s), "hipMemsetAsync")) return e;
+  hipLaunchKernelGGL(k_zigzag8_i16, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, raster, (int)H, (int)W,
+                     nbx, total, out, d_wide);
+  return check_launch("k_zigzag8_i16");
 }
 
 extern "C" int hic_izigzag_blocks_i32(const int32_t *blocks, int64_t H, int64_t W, int N, int32_t *raster,

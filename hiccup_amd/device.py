@@ -51,12 +51,25 @@ def to_device(a):
     a = np.ascontiguousarray(a)
     if a.nbytes < _PIN_MIN or a.dtype.hasobject:
         return torch.from_numpy(a).to("cuda")
-    out = torch.empty(tuple(a.shape), dtype=torch.from_numpy(a[:0].reshape(-1)).dtype, device="cuda")
-    ob, ab = out.reshape(-1).view(torch.uint8), a.reshape(-1).view(np.uint8)
-    if _is_pinned(ab):  # already page-locked: one DMA, no staging copy
-        ob.copy_(torch.from_numpy(ab), non_blocking=True)
-        torch.cuda.current_stream().synchronize()  # the caller may reuse `a` on return
+    dt = torch.from_numpy(a[:0].reshape(-1)).dtype
+    ab = a.reshape(-1).view(np.uint8)
+    if _is_pinned(ab):
+        # already page-locked: one DMA, no staging copy, on the copy stream (its
+        # buffer allocated there), so it runs beside the kernels already queued on
+        # the current stream (jpeg_encode: the next plane's upload beside this one's
+        # RLE); the current stream waits for it, the host too (`a` is free on return)
+        s, cur = _copy_stream(), torch.cuda.current_stream()
+        with torch.cuda.stream(s):
+            out = torch.empty(tuple(a.shape), dtype=dt, device="cuda")
+            out.reshape(-1).view(torch.uint8).copy_(torch.from_numpy(ab), non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(s)
+        cur.wait_event(done)
+        out.record_stream(cur)
+        done.synchronize()
         return out
+    out = torch.empty(tuple(a.shape), dtype=dt, device="cuda")
+    ob = out.reshape(-1).view(torch.uint8)
     with _staging_lock:
         s = _copy_stream()
         s.wait_stream(torch.cuda.current_stream())  # `out` was allocated on the current stream

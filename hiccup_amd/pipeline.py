@@ -235,12 +235,8 @@ class Encoder:
             return
         if self.fused:
             # colour + pyrDown + DCT/quantize/zig-zag of the three planes + RLE tile
-            # records in ONE launch (dct_events time it).  The kernel addresses its
-            # input rows with 32-bit offsets: hand it the span it reads (< 2 GiB by
-            # can_fuse) when the caller passes more rows
-            a, b = self.input_span()
-            if rgb.shape[0] * self.W * 3 > 2**31 - 1 and in_row0 <= a and in_row0 + rgb.shape[0] >= b:
-                rgb, in_row0 = rgb[a - in_row0:b - in_row0], a
+            # records in ONE launch (dct_events time it)
+            rgb, in_row0 = self._fused_input(rgb, in_row0)
             coefs = [device.ptr(self.coef[k]) for k in CHANNELS]
             wss = [device.ptr(self.ws[k]) for k in CHANNELS]
             if self.seg:
@@ -263,6 +259,18 @@ class Encoder:
             jobs[i] = _lib.DctPlaneJob(p.data_ptr(), h, w, p.stride(0), TABLES[k], self.coef[k].data_ptr(),
                                        self.ws[k].data_ptr())
         _lib.call("hic_dct_quant_rle_u8_batch", 3, jobs, self.max_len, s, *ev)
+
+    def _fused_input(self, rgb, in_row0):
+        """The fused kernel addresses its input rows with 32-bit offsets: hand it the
+        span it reads (< 2 GiB by can_fuse) when the caller passes more rows."""
+        a, b = self.input_span()
+        if rgb.shape[0] * self.W * 3 > 2**31 - 1 and in_row0 <= a and in_row0 + rgb.shape[0] >= b:
+            rgb, in_row0 = rgb[a - in_row0:b - in_row0], a
+        return rgb, in_row0
+
+    def batchable(self):
+        """Whether transform_batch can take this encoder into a batched launch."""
+        return (self.fused and not self.slots and not self.seg and not self.landing and self.W % 512 == 0)
 
     def _slot_jobs(self):
         jobs = (_lib.SlotJob * 3)()
@@ -386,6 +394,40 @@ class Encoder:
             out[k] = (self.coef[k].cpu().numpy(), self.dc[k].cpu().numpy(), self.sym_len[k][:c].cpu().numpy(),
                       self.sym_val[k][:c].cpu().numpy())
         return out
+
+
+def transform_batch(encoders, inputs, stream=None, in_row0s=None, dct_events=None):
+    """Encoder.transform of several encoders -- the row shards of a multi-GPU group,
+    one per image -- in ONE launch (hic_encode420_batch_u8) when every one is a fused
+    coefficient encoder whose records its kernel writes (Encoder.batchable) and at
+    most 8 share one max_len; else one transform each.  A shard is 1/N of an image,
+    too few waves to fill the chip alone: at N = 8 eight launches in a row took 2.4x
+    one whole-image launch.  dct_events (per encoder, None or device.KernelEvents):
+    each pair spans the batched launch."""
+    n = len(encoders)
+    in_row0s = in_row0s if in_row0s is not None else [None] * n
+    dct_events = dct_events if dct_events is not None else [None] * n
+    if not (2 <= n <= 8 and all(e.batchable() for e in encoders)
+            and len(set(e.max_len for e in encoders)) == 1):
+        for e, x, r, ev in zip(encoders, inputs, in_row0s, dct_events):
+            e.transform(x, stream, in_row0=r, dct_events=ev)
+        return
+    jobs = (_lib.Encode420Job * n)()
+    for i, (e, x, r) in enumerate(zip(encoders, inputs, in_row0s)):
+        if r is None:
+            r = 0 if e.rows == (0, e.H) else e.input_span()[0]
+        x, r = e._fused_input(x, r)
+        r0, r1 = e.rows
+        jobs[i] = _lib.Encode420Job(x.data_ptr(), r, x.shape[0], e.H, e.W, r0, r1 - r0,
+                                    *(e.coef[k].data_ptr() for k in CHANNELS), *(e.ws[k].data_ptr() for k in CHANNELS))
+    s = device.stream_ptr(stream)
+    evs = [ev for ev in dct_events if ev is not None]
+    for ev in evs[1:]:
+        _lib.call("hic_event_record", ev.start, s)
+    first = (evs[0].start, evs[0].stop) if evs else (None, None)
+    _lib.call("hic_encode420_batch_u8", n, jobs, encoders[0].max_len, s, *first)
+    for ev in evs[1:]:
+        _lib.call("hic_event_record", ev.stop, s)
 
 
 class Decoder:

@@ -379,14 +379,13 @@ def encode_group(encoders, rgb_rows_list, stream=None, dct_events=None):
 def _encode_group(encoders, rgb_rows_list, stream, dct_events):
     e0 = encoders[0]
     n, world = len(encoders), e0.world
+    # the group's shard transforms in one launch (pipeline.transform_batch)
+    pipeline.transform_batch([se.enc for se in encoders], rgb_rows_list, stream,
+                             in_row0s=[se.span[0] for se in encoders], dct_events=dct_events)
     if all(se.gather_kind == "stream" for se in encoders):
-        # the entropy stage runs on the gathering rank (gather_streams_group)
-        for i, (se, x) in enumerate(zip(encoders, rgb_rows_list)):
-            se.enc.transform(x, stream, in_row0=se.span[0], dct_events=dct_events[i] if dct_events else None)
-        return
+        return  # the entropy stage runs on the gathering rank (gather_streams_group)
     summs = []
-    for i, (se, x) in enumerate(zip(encoders, rgb_rows_list)):
-        se.enc.transform(x, stream, in_row0=se.span[0], dct_events=dct_events[i] if dct_events else None)
+    for se in encoders:
         summs.append(se.enc.shard_summaries(stream))
     allsumm = torch.empty((world, n, 3, 4), dtype=torch.int64, device=summs[0].device)
     _all_gather(allsumm.view(world * n * 3, 4), torch.stack(summs).view(n * 3, 4), group=e0.group)

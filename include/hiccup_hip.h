@@ -179,6 +179,19 @@ int hic_encode420_seg_u8(const uint8_t *rgb_rows, int64_t in_row0, int64_t in_ro
                          int64_t out_row0, int64_t out_rows, int16_t *coef_y, int16_t *coef_cr, int16_t *coef_cb,
                          void *ws_y, void *ws_cr, void *ws_cb, int64_t ws_bytes_y, int64_t ws_bytes_c, int max_len,
                          void *stream, void *ev_start, void *ev_stop);
+/* hic_encode420_batch_u8: n <= 8 hic_encode420_u8 calls in ONE launch (the row
+ * shards of a multi-GPU group, one per image: a shard alone fills a sixth of the chip
+ * at N = 8).  Each job as hic_encode420_u8's arguments; with workspaces, W % 512 == 0
+ * (the records come from the kernel).  Every job is checked before the launch; the
+ * events (nullable) time the whole launch. */
+typedef struct {
+  const uint8_t *rgb_rows;
+  int64_t in_row0, in_rows, H, W, out_row0, out_rows;
+  int16_t *coef_y, *coef_cr, *coef_cb;
+  void *ws_y, *ws_cr, *ws_cb;
+} hic_encode420_job;
+int hic_encode420_batch_u8(int n, const hic_encode420_job *jobs, int max_len, void *stream, void *ev_start,
+                           void *ev_stop);
 /* ---- slot-layout encode (round 6): hic_encode420_u8 + hic_rle_encode_i16_tiles_batch
  *      (compression.jpeg_compression's transform + codec.jpeg_encode's DC DPCM and AC
  *      RLE, compression.py:16-39, codec.py:47-99,286-301) with the symbols written by
@@ -256,6 +269,8 @@ int hic_probe_encode420_slots(const uint8_t *rgb, int64_t H, int64_t W, const hi
 /* Timing events (hipEvent_t handles) for the *_timed entry points. */
 int hic_event_create(void **h_event);
 int hic_event_destroy(void *event);
+/* Records an event on a stream (hipEventRecord). */
+int hic_event_record(void *event, void *stream);
 /* Milliseconds between two completed events (synchronises on `stop`). */
 int hic_event_elapsed_ms(void *start, void *stop, float *h_ms);
 
@@ -323,6 +338,11 @@ int hic_ycrcb420_to_rgb_rows(const uint8_t *y, int64_t y_stride, const uint8_t *
  *      (izigzag + merge_blocks + crop, codec.py:415-425). */
 int hic_zigzag_blocks_i32(const int32_t *raster, int64_t H, int64_t W, int N, int32_t *out,
                           void *stream);
+/* hic_zigzag_blocks_i32 for N = 8 into int16 blocks (codec.jpeg_encode's fast path,
+ * then hic_rle_encode_i16): *d_wide (device int32) = 1 if any value of the raster is
+ * outside int16 -- those blocks are then not exact and the caller re-runs the plane
+ * through the int32 calls -- else 0. */
+int hic_zigzag8_blocks_i16(const int32_t *raster, int64_t H, int64_t W, int16_t *out, int32_t *d_wide, void *stream);
 int hic_izigzag_blocks_i32(const int32_t *blocks, int64_t H, int64_t W, int N, int32_t *raster,
                            void *stream);
 

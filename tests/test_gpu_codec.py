@@ -797,6 +797,81 @@ def test_huffman_decode_device_edges():
         assert tree.decode_packed(*hicimage.BitStringP(bits).packed_bits()) == tree.decode_data(bits)
 
 
+@pytest.mark.parametrize("N", [2, 3, 8])
+def test_transform_batch_equals_shard_launches(N):
+    """pipeline.transform_batch (hic_encode420_batch_u8: a multi-GPU group's row
+    shards, one per image, in one launch) writes the same coefficients and RLE tile
+    records as one hic_encode420_u8 launch per shard; its timing events all span the
+    launch; a group it cannot batch (W % 512 != 0) runs shard by shard."""
+    H, W = 1088, 1024
+    imgs = [device.to_device(np.random.default_rng(N + i).integers(0, 256, (H, W, 3), dtype=np.uint8))
+            for i in range(N)]
+    rows = sharding.plan(H, N)
+    # shard j of image j (a group: image j's shard for this rank is its j-th)
+    def make():
+        return [pipeline.Encoder(H, W, rows=rows[j]) for j in range(N)]
+    one, bat = make(), make()
+    spans = [e.input_span() for e in one]
+    ins = [imgs[j][spans[j][0]:spans[j][1]] for j in range(N)]
+    assert all(e.batchable() for e in one)
+    for e, x, sp in zip(one, ins, spans):
+        e.transform(x, in_row0=sp[0])
+    evs = [device.KernelEvents() if j % 2 == 0 else None for j in range(N)]
+    pipeline.transform_batch(bat, ins, in_row0s=[sp[0] for sp in spans], dct_events=evs)
+    torch.cuda.synchronize()
+    for a, b in zip(one, bat):
+        for k in pipeline.CHANNELS:
+            assert torch.equal(a.coef[k], b.coef[k]), k
+            assert torch.equal(a.ws[k], b.ws[k]), k
+    assert all(ev.elapsed_ms() > 0 for ev in evs if ev is not None)
+    # W % 512 != 0: not batchable, one launch per shard, same result
+    W2 = 768
+    img2 = device.to_device(np.random.default_rng(7).integers(0, 256, (H, W2, 3), dtype=np.uint8))
+    e1 = [pipeline.Encoder(H, W2, rows=rows[j]) for j in range(N)]
+    e2 = [pipeline.Encoder(H, W2, rows=rows[j]) for j in range(N)]
+    assert not any(e.batchable() for e in e1)
+    sp2 = [e.input_span() for e in e1]
+    for e, sp in zip(e1, sp2):
+        e.transform(img2[sp[0]:sp[1]], in_row0=sp[0])
+    pipeline.transform_batch(e2, [img2[sp[0]:sp[1]] for sp in sp2], in_row0s=[sp[0] for sp in sp2])
+    for a, b in zip(e1, e2):
+        for k in pipeline.CHANNELS:
+            assert torch.equal(a.coef[k], b.coef[k]), k
+
+
+@pytest.mark.parametrize("kind", ["random", "wide", "ragged"])
+def test_jpeg_encode_int16_path_equals_int32(kind, monkeypatch):
+    """jpeg_encode's 8x8 fast path (int16 zig-zag blocks + the 16-bit RLE) writes the
+    same container as the int32 path (forced by reporting every plane wide), and a
+    plane holding a coefficient outside int16 falls back to the int32 path by
+    itself (the fast path's blocks of it are not exact)."""
+    rng = np.random.default_rng({"random": 1, "wide": 2, "ragged": 3}[kind])
+    H, W = (123, 205) if kind == "ragged" else (256, 384)
+    planes = [rng.integers(-300, 301, (H, W)).astype(np.int32),
+              rng.integers(-60, 61, ((H + 1) // 2, (W + 1) // 2)).astype(np.int32),
+              rng.integers(-60, 61, ((H + 1) // 2, (W + 1) // 2)).astype(np.int32)]
+    planes[0][::8, ::8] = rng.integers(-2000, 2001, planes[0][::8, ::8].shape)  # DC-like values
+    if kind == "wide":
+        planes[1][5, 9] = 40000
+        planes[0][17, 3] = -33000
+    ci = model.CompressedImage(*planes)
+    settings.JPEG_BLOCK_SIZE = 8
+    fast = codec.jpeg_encode(ci).byte_stream()
+    real = codec.encode_channel_device8
+
+    def forced_wide(*a, **k):
+        dc, L, V, cnt, wide = real(*a, **k)
+        return dc, L, V, cnt, torch.ones_like(wide)
+
+    monkeypatch.setattr(codec, "encode_channel_device8", forced_wide)
+    assert codec.jpeg_encode(ci).byte_stream() == fast
+    monkeypatch.undo()
+    if kind != "ragged":  # (partial blocks: the reference's decode asserts, codec.py:418)
+        back = codec.jpeg_decode(hicimage.HicImage.from_bytes(fast))
+        for a, b in zip(planes, back.as_dict.values()):
+            np.testing.assert_array_equal(a, np.asarray(b))
+
+
 @pytest.mark.parametrize("dtype", [np.uint8, np.int16, np.int32])
 def test_key_range_all_widths(dtype):
     """hic_key_range (the histograms' bin range) == numpy min / max for every key

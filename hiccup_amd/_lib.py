@@ -43,6 +43,12 @@ class SlotJob(ctypes.Structure):
                 ("sym_val", _vp), ("sym_cap", _i64)]
 
 
+class WireJob(ctypes.Structure):
+    """hic_wire_job (include/hiccup_hip.h): one segment of a batched wire pack / unpack."""
+    _fields_ = [("blocks", _vp), ("wire", _vp), ("nblk", _i64), ("table_id", ctypes.c_int32), ("d_flag", _vp),
+                ("rec_src", _vp), ("nrec", _i64), ("pos_shift", _i64), ("rec_dst", _vp), ("d_count", _vp)]
+
+
 class Encode420Job(ctypes.Structure):
     """hic_encode420_job (include/hiccup_hip.h): one encode of hic_encode420_batch_u8."""
     _fields_ = [("rgb_rows", _vp), ("in_row0", _i64), ("in_rows", _i64), ("H", _i64), ("W", _i64),
@@ -98,6 +104,9 @@ SIGNATURES = {
     "hic_huffman_build": (_int, [_vp, _i64, _vp, _vp, _vp]),
     "hic_zigzag8_blocks_i16": (_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
     "hic_event_record": (_int, [_vp, _vp]),
+    "hic_wire_pack_batch": (_int, [_int, _vp, _vp]),
+    "hic_wire_unpack_batch": (_int, [_int, _vp, _vp]),
+    "hic_wire_flags_apply": (_int, [_int, _vp, _vp]),
     "hic_encode420_batch_u8": (_int, [_int, _vp, _int, _vp, _vp, _vp]),
     "hic_huffman_decode_batch": (_int, [_int, _vp, _vp]),
     "hic_huffman_from_codes": (_int, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),

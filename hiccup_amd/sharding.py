@@ -221,23 +221,25 @@ class ShardEncoder:
     def pack(self, stream=None):
         """gather_kind "stream", a rank other than gather_to: this rank's blocks into
         the wire format and its tile records, rebased, behind them (on `stream`)."""
-        s = device.stream_ptr(stream)
+        wire_batch("hic_wire_pack_batch", self.pack_jobs(), stream)
+
+    def pack_jobs(self):
+        """hic_wire_job per channel of pack(): the blocks into the wire segment, the
+        flag in its trailer (cleared by the pack), the records rebased behind the
+        blocks."""
         lib = _lib.load()
+        jobs = []
         for k in CHANNELS:
             b0, b1 = self.ranges[k][self.rank]
             n = b1 - b0
             w = self.wire_send[k]
             wb = lib.hic_wire_bytes(n, TABLE_OF[k])
-            # the flag travels in the segment's trailer (cleared on the pack's stream)
-            flag = w[-TRAILER_BYTES:]
-            with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream()):
-                flag.zero_()
-            _lib.call("hic_wire_pack_i16", device.ptr(self.enc.coef[k]), n, TABLE_OF[k], device.ptr(w),
-                      device.ptr(flag), s)
-            if self.records:
-                nrec = -(-n * self.enc.rpt[k] // 64)
-                _lib.call("hic_rle_records_rebase", device.ptr(self.enc.ws[k]), nrec, b0 * 63,
-                          ctypes.c_void_p(w.data_ptr() + wb), s)
+            nrec = -(-n * self.enc.rpt[k] // 64) if self.records else 0
+            jobs.append(_lib.WireJob(self.enc.coef[k].data_ptr(), w.data_ptr(), n, TABLE_OF[k],
+                                     w.data_ptr() + w.numel() - TRAILER_BYTES,
+                                     self.enc.ws[k].data_ptr() if nrec else None, nrec, b0 * 63,
+                                     w.data_ptr() + wb if nrec else None, None))
+        return jobs
 
     def stream_item(self):
         """(mine, full, ranges, dst) of this image's wire gather for
@@ -259,47 +261,40 @@ class ShardEncoder:
         whole = self.whole
         if whole.rpt != self.enc.rpt:
             raise RuntimeError("landing zone record layout %r != the shards' %r" % (whole.rpt, self.enc.rpt))
-        for k in CHANNELS:
+        # every other rank's segments unpacked, every rank's records placed: one batch
+        # (hic_wire_unpack_batch: 3 launches for all channels and peers)
+        jobs, flags = [], []
+        for c, k in enumerate(CHANNELS):
             rpt = self.enc.rpt[k]  # the layout wire_ranges sized the segments with
             for r in range(self.world):
                 b0, b1 = self.ranges[k][r]
                 n = b1 - b0
-                nrec = -(-n * rpt // 64)
-                dst_rec = ctypes.c_void_p(whole.ws[k].data_ptr() + (b0 * rpt // 64) * REC_BYTES)
+                nrec = -(-n * rpt // 64) if self.records else 0
+                dst_rec = whole.ws[k].data_ptr() + (b0 * rpt // 64) * REC_BYTES
                 if r == self.rank:
-                    if self.records:
-                        _lib.call("hic_rle_records_rebase", device.ptr(self.enc.ws[k]), nrec, b0 * 63, dst_rec, s)
+                    if nrec:
+                        jobs.append(_lib.WireJob(None, None, 0, TABLE_OF[k], None, self.enc.ws[k].data_ptr(), nrec,
+                                                 b0 * 63, dst_rec, None))
                     continue
-                o0, _ = self.wranges[k][r]
-                seg = ctypes.c_void_p(self.wire_full[k].data_ptr() + o0)
-                _lib.call("hic_wire_unpack_i16", seg, n, TABLE_OF[k], device.ptr(whole.coef[k][b0:b1]), s)
-                if self.records:
-                    src = ctypes.c_void_p(self.wire_full[k].data_ptr() + o0 + lib.hic_wire_bytes(n, TABLE_OF[k]))
-                    _lib.call("hic_rle_records_rebase", src, nrec, 0, dst_rec, s)
-            if not self.records:
+                o0, o1 = self.wranges[k][r]
+                seg = self.wire_full[k].data_ptr() + o0
+                jobs.append(_lib.WireJob(whole.coef[k][b0:b1].data_ptr(), seg, n, TABLE_OF[k], None,
+                                         seg + lib.hic_wire_bytes(n, TABLE_OF[k]) if nrec else None, nrec, 0,
+                                         dst_rec if nrec else None, None))
+                # the sender's out-of-width flag (its segment's trailer) -> this channel's count
+                flags.append(_lib.WireJob(None, None, 0, TABLE_OF[k], self.wire_full[k].data_ptr() + o1 - TRAILER_BYTES,
+                                          None, 0, 0, None, whole.counts.data_ptr() + 8 * c))
+        if jobs:
+            wire_batch("hic_wire_unpack_batch", jobs, stream)
+        if not self.records:
+            for k in CHANNELS:
                 _lib.call("hic_rle_tile_records_i16", device.ptr(whole.coef[k]), whole.coef[k].shape[0],
                           whole.max_len, device.ptr(whole.ws[k]), s)
         whole.entropy(stream)
-        # the senders' out-of-width flags (segment trailers) -> the stream's count
-        # (HIC_COUNT_WIRE_OVERFLOW): device ops on `stream`, no host sync
-        with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream()):
-            for c, k in enumerate(CHANNELS):
-                idx = self._trailer_index(k)
-                if idx is None:
-                    continue
-                bad = self.wire_full[k].view(torch.int32)[idx].ne(0).any()
-                whole.counts[c:c + 1] = torch.where(bad, torch.full_like(whole.counts[c:c + 1],
-                                                                         pipeline.COUNT_WIRE_OVERFLOW),
-                                                    whole.counts[c:c + 1])
-
-    def _trailer_index(self, k):
-        """int32 indices (device) of the other ranks' trailer flags in wire_full[k]."""
-        if not hasattr(self, "_trailers"):
-            self._trailers = {}
-        if k not in self._trailers:
-            offs = [(self.wranges[k][r][1] - TRAILER_BYTES) // 4 for r in range(self.world) if r != self.rank]
-            self._trailers[k] = torch.tensor(offs, dtype=torch.int64, device="cuda") if offs else None
-        return self._trailers[k]
+        # the senders' flags override the counts after the scan (HIC_COUNT_WIRE_OVERFLOW):
+        # one launch on `stream`, no host sync
+        if flags:
+            wire_batch("hic_wire_flags_apply", flags, stream)
 
     @property
     def pixels(self):
@@ -422,9 +417,10 @@ def gather_streams_group(encoders, group=None, rccl=None, stream=None):
     elsewhere."""
     st = stream if stream is not None else torch.cuda.current_stream()
     with torch.cuda.stream(st):
-        for e in encoders:
-            if e.rank != e.gather_to:
-                e.pack(st)
+        # every image this rank sends, all channels: one batch
+        jobs = [j for e in encoders if e.rank != e.gather_to for j in e.pack_jobs()]
+        if jobs:
+            wire_batch("hic_wire_pack_batch", jobs, st)
         items = [e.stream_item() for e in encoders]
         e0 = encoders[0]
         if rccl is not None:
@@ -435,6 +431,15 @@ def gather_streams_group(encoders, group=None, rccl=None, stream=None):
             if e.rank == e.gather_to:
                 e.finish(st)
     return [e.whole for e in encoders]
+
+
+def wire_batch(fn, jobs, stream=None):
+    """One of the batched wire calls over a job list (32 jobs per call)."""
+    s = device.stream_ptr(stream)
+    for i in range(0, len(jobs), 32):
+        part = jobs[i:i + 32]
+        arr = (_lib.WireJob * len(part))(*part)
+        _lib.call(fn, len(part), arr, s)
 
 
 def gather_blocks(mine, full, ranges, rank, world, dst, group=None):

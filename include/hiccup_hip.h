@@ -613,6 +613,30 @@ int hic_huffman_from_codes(const char *h_chars, const int64_t *h_off, int64_t n,
 size_t hic_wire_bytes(int64_t nblk, int table_id);
 int hic_wire_pack_i16(const int16_t *blocks, int64_t nblk, int table_id, uint8_t *wire, int *d_flag, void *stream);
 int hic_wire_unpack_i16(const uint8_t *wire, int64_t nblk, int table_id, int16_t *blocks, void *stream);
+/* The batched forms (a multi-GPU group's segments: 3 channels x up to 7 peers in 3
+ * launches).  Each job: its blocks and wire segment (nblk 0: records only), its
+ * table, the out-of-width flag (pack: cleared, then raised), its RLE records
+ * (rec_src / nrec, nullable) copied to rec_dst rebased by pos_shift (as
+ * hic_rle_records_rebase), and d_count (hic_wire_flags_apply).  n <= 32; every job
+ * checked before the first launch.
+ *  hic_wire_pack_batch: hic_wire_pack_i16 + hic_rle_records_rebase of every job.
+ *  hic_wire_unpack_batch: hic_wire_unpack_i16 + hic_rle_records_rebase of every job.
+ *  hic_wire_flags_apply: *d_count = HIC_COUNT_WIRE_OVERFLOW for each job whose
+ *    *d_flag (a received sender flag) is set -- after the stream's scan. */
+typedef struct {
+  int16_t *blocks;
+  uint8_t *wire;
+  int64_t nblk;
+  int32_t table_id;
+  int32_t *d_flag;
+  const int64_t *rec_src;
+  int64_t nrec, pos_shift;
+  int64_t *rec_dst;
+  int64_t *d_count;
+} hic_wire_job;
+int hic_wire_pack_batch(int n, const hic_wire_job *jobs, void *stream);
+int hic_wire_unpack_batch(int n, const hic_wire_job *jobs, void *stream);
+int hic_wire_flags_apply(int n, const hic_wire_job *jobs, void *stream);
 int hic_rle_records_rebase(const int64_t *d_src, int64_t nrec, int64_t pos_shift, int64_t *d_dst, void *stream);
 
 /* ---- Multi-GPU gather over RCCL (SURVEY.md section 8(b) hic_gather_*; the

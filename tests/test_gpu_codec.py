@@ -980,6 +980,69 @@ def test_huffman_decode_device_equal_length_codes(nkeys):
     assert dt < 0.5, "%.3f s for %d bits" % (dt, nbits)
 
 
+def test_wire_batches():
+    """hic_wire_pack_batch / _unpack_batch (a multi-GPU group's segments in 3
+    launches) == one hic_wire_pack_i16 / _unpack_i16 + hic_rle_records_rebase per
+    segment, over mixed tables and sizes, a records-only job and a segment with a
+    value outside its width (its flag alone raised); hic_wire_flags_apply turns a
+    raised flag into HIC_COUNT_WIRE_OVERFLOW and leaves the other counts."""
+    import wire_host
+    rng = np.random.default_rng(3)
+    spec = [(0, 1), (1, 65), (0, 777), (1, 64), (0, 4100), (1, 3)]
+    jobs, want, outs, flags, backs = [], [], [], [], []
+    for i, (table, nblk) in enumerate(spec):
+        blocks = wire_host.random_blocks(rng, nblk, table)
+        if i == 2:
+            blocks[nblk // 3, 5] = 1 << (wire_host.WIDTHS[table][5] - 1)  # one past its width
+        b = device.to_device(blocks)
+        nb = _lib.load().hic_wire_bytes(nblk, table)
+        nrec = -(-nblk // 64)
+        rec = device.to_device(rng.integers(-1, 10 ** 6, (nrec, 3)).astype(np.int64))
+        wire = device.empty((nb + 24 * nrec,), torch.uint8)
+        flag = device.full((1,), 7, torch.int32) if hasattr(device, "full") else torch.full((1,), 7, dtype=torch.int32,
+                                                                                          device="cuda")
+        jobs.append(_lib.WireJob(b.data_ptr(), wire.data_ptr(), nblk, table, flag.data_ptr(), rec.data_ptr(), nrec,
+                                 1000 * i, wire.data_ptr() + nb, None))
+        want.append((blocks, table, rec, nb, nrec, 1000 * i))
+        outs.append((b, wire, rec))
+        flags.append(flag)
+    # a records-only job
+    rec_only = device.to_device(rng.integers(-1, 10 ** 6, (10, 3)).astype(np.int64))
+    rec_dst = device.empty((10, 3), torch.int64)
+    jobs.append(_lib.WireJob(None, None, 0, 0, None, rec_only.data_ptr(), 10, 5, rec_dst.data_ptr(), None))
+    sharding.wire_batch("hic_wire_pack_batch", jobs)
+    torch.cuda.synchronize()
+    def rebased(r, shift):
+        r = r.copy()
+        r[:, :2] = np.where(r[:, :2] >= 0, r[:, :2] + shift, r[:, :2])
+        return r
+    for i, ((blocks, table, rec, nb, nrec, shift), (_, wire, _), flag) in enumerate(zip(want, outs, flags)):
+        w = device.to_host(wire)
+        if i != 2:  # (the host restatement refuses the out-of-width value)
+            np.testing.assert_array_equal(w[:nb], wire_host.pack(blocks, table), err_msg=str(i))
+        np.testing.assert_array_equal(w[nb:].view(np.int64).reshape(nrec, 3), rebased(device.to_host(rec), shift))
+        assert int(flag.item()) == (1 if i == 2 else 0), i
+    np.testing.assert_array_equal(device.to_host(rec_dst), rebased(device.to_host(rec_only), 5))
+    # unpack: the segments back into blocks, their records rebased again
+    ujobs, backs = [], []
+    for (blocks, table, rec, nb, nrec, shift), (_, wire, _) in zip(want, outs):
+        back = device.empty((blocks.shape[0], 64), torch.int16)
+        rdst = device.empty((nrec, 3), torch.int64)
+        ujobs.append(_lib.WireJob(back.data_ptr(), wire.data_ptr(), blocks.shape[0], table, None,
+                                  wire.data_ptr() + nb, nrec, 1, rdst.data_ptr(), None))
+        backs.append((back, rdst))
+    sharding.wire_batch("hic_wire_unpack_batch", ujobs)
+    for i, ((blocks, table, rec, nb, nrec, shift), (back, rdst)) in enumerate(zip(want, backs)):
+        if i != 2:
+            np.testing.assert_array_equal(device.to_host(back), blocks, err_msg=str(i))
+        np.testing.assert_array_equal(device.to_host(rdst), rebased(rebased(device.to_host(rec), shift), 1))
+    counts = torch.tensor([11, 22, 33], dtype=torch.int64, device="cuda")
+    fj = [_lib.WireJob(None, None, 0, 0, flags[i].data_ptr(), None, 0, 0, None, counts.data_ptr() + 8 * c)
+          for c, i in ((0, 0), (1, 2), (2, 1))]
+    sharding.wire_batch("hic_wire_flags_apply", fj)
+    assert counts.cpu().tolist() == [11, pipeline.COUNT_WIRE_OVERFLOW, 33]
+
+
 @pytest.mark.parametrize("table", [0, 1])
 @pytest.mark.parametrize("nblk", [1, 63, 64, 65, 777, 129600])
 def test_wire_pack_unpack(nblk, table):

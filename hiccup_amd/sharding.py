@@ -26,6 +26,7 @@ gathering rank's own encoder writes into its slice of those buffers in place.
 streams; it needs the counts on the host.
 """
 import ctypes
+import weakref
 
 import numpy as np
 import torch
@@ -226,7 +227,12 @@ class ShardEncoder:
     def pack_jobs(self):
         """hic_wire_job per channel of pack(): the blocks into the wire segment, the
         flag in its trailer (cleared by the pack), the records rebased behind the
-        blocks."""
+        blocks.  The buffers are this encoder's for its lifetime: built once."""
+        if getattr(self, "_pack_jobs", None) is None:
+            self._pack_jobs = self._make_pack_jobs()
+        return self._pack_jobs
+
+    def _make_pack_jobs(self):
         lib = _lib.load()
         jobs = []
         for k in CHANNELS:
@@ -257,12 +263,30 @@ class ShardEncoder:
         on record boundaries, recomputed by a tile pass), then the whole image's
         scan + emit (one stream, no stitch).  On `stream`."""
         s = device.stream_ptr(stream)
-        lib = _lib.load()
         whole = self.whole
         if whole.rpt != self.enc.rpt:
             raise RuntimeError("landing zone record layout %r != the shards' %r" % (whole.rpt, self.enc.rpt))
-        # every other rank's segments unpacked, every rank's records placed: one batch
-        # (hic_wire_unpack_batch: 3 launches for all channels and peers)
+        if getattr(self, "_finish_jobs", None) is None:  # fixed buffers: built once
+            self._finish_jobs = self._make_finish_jobs()
+        jobs, flags = self._finish_jobs
+        if jobs:
+            _lib.call("hic_wire_unpack_batch", len(jobs), jobs, s)
+        if not self.records:
+            for k in CHANNELS:
+                _lib.call("hic_rle_tile_records_i16", device.ptr(whole.coef[k]), whole.coef[k].shape[0],
+                          whole.max_len, device.ptr(whole.ws[k]), s)
+        whole.entropy(stream)
+        # the senders' flags override the counts after the scan (HIC_COUNT_WIRE_OVERFLOW):
+        # one launch on `stream`, no host sync
+        if flags:
+            _lib.call("hic_wire_flags_apply", len(flags), flags, s)
+
+    def _make_finish_jobs(self):
+        """finish()'s batches as ctypes arrays: every other rank's segments unpacked
+        and every rank's records placed (hic_wire_unpack_batch: 3 launches for all
+        channels and peers), and the senders' flags -> counts."""
+        lib = _lib.load()
+        whole = self.whole
         jobs, flags = [], []
         for c, k in enumerate(CHANNELS):
             rpt = self.enc.rpt[k]  # the layout wire_ranges sized the segments with
@@ -284,17 +308,10 @@ class ShardEncoder:
                 # the sender's out-of-width flag (its segment's trailer) -> this channel's count
                 flags.append(_lib.WireJob(None, None, 0, TABLE_OF[k], self.wire_full[k].data_ptr() + o1 - TRAILER_BYTES,
                                           None, 0, 0, None, whole.counts.data_ptr() + 8 * c))
-        if jobs:
-            wire_batch("hic_wire_unpack_batch", jobs, stream)
-        if not self.records:
-            for k in CHANNELS:
-                _lib.call("hic_rle_tile_records_i16", device.ptr(whole.coef[k]), whole.coef[k].shape[0],
-                          whole.max_len, device.ptr(whole.ws[k]), s)
-        whole.entropy(stream)
-        # the senders' flags override the counts after the scan (HIC_COUNT_WIRE_OVERFLOW):
-        # one launch on `stream`, no host sync
-        if flags:
-            wire_batch("hic_wire_flags_apply", flags, stream)
+        if len(jobs) > 32 or len(flags) > 32:
+            raise ValueError("world %d: more than 32 wire segments per image" % self.world)
+        return ((_lib.WireJob * len(jobs))(*jobs) if jobs else None,
+                (_lib.WireJob * len(flags))(*flags) if flags else None)
 
     @property
     def pixels(self):
@@ -417,10 +434,19 @@ def gather_streams_group(encoders, group=None, rccl=None, stream=None):
     elsewhere."""
     st = stream if stream is not None else torch.cuda.current_stream()
     with torch.cuda.stream(st):
-        # every image this rank sends, all channels: one batch
-        jobs = [j for e in encoders if e.rank != e.gather_to for j in e.pack_jobs()]
-        if jobs:
-            wire_batch("hic_wire_pack_batch", jobs, st)
+        # every image this rank sends, all channels: one batch (the job array of a
+        # group of encoders is built once: their buffers are fixed)
+        cache = _pack_arrays.setdefault(encoders[0], {})
+        key = tuple(id(e) for e in encoders)
+        hit = cache.get(key)
+        if hit is not None and all(r() is e for r, e in zip(hit[0], encoders)):
+            arr = hit[1]
+        else:  # (an id can come back on a new encoder: the weak references tell)
+            jobs = [j for e in encoders if e.rank != e.gather_to for j in e.pack_jobs()]
+            arr = [(_lib.WireJob * len(jobs[i:i + 32]))(*jobs[i:i + 32]) for i in range(0, len(jobs), 32)]
+            cache[key] = ([weakref.ref(e) for e in encoders], arr)
+        for a in arr:
+            _lib.call("hic_wire_pack_batch", len(a), a, device.stream_ptr(st))
         items = [e.stream_item() for e in encoders]
         e0 = encoders[0]
         if rccl is not None:
@@ -431,6 +457,10 @@ def gather_streams_group(encoders, group=None, rccl=None, stream=None):
             if e.rank == e.gather_to:
                 e.finish(st)
     return [e.whole for e in encoders]
+
+
+# gather_streams_group: first encoder -> {(encoder ids): (weak refs, the group's pack job arrays)}
+_pack_arrays = weakref.WeakKeyDictionary()
 
 
 def wire_batch(fn, jobs, stream=None):

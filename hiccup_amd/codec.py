@@ -67,10 +67,10 @@ def _i32(a, what):
     return a.astype(np.int32)
 
 
-def _i32_device(a, what):
+def _i32_device(a, what, wait=True):
     """_i32's checks and result as an int32 device tensor (large float planes are
     checked and cast on the GPU: device.to_device_i32)."""
-    return device.to_device_i32(a, "%s must be integer-valued" % what, "%s out of int32 range" % what)
+    return device.to_device_i32(a, "%s must be integer-valued" % what, "%s out of int32 range" % what, wait=wait)
 
 
 def differential_coding(blocks):
@@ -233,7 +233,9 @@ def _jpeg_encode(compressed):
         # the reference's DC keys are elements of the plane (utils.differences over
         # block[0][0]): numpy scalars of its dtype
         dc_type[k] = np.asarray(v).dtype.type
-        p = _i32_device(v, "coefficient plane")
+        # wait=False: `compressed` holds the planes unchanged until the count read
+        # below synchronises, so the uploads queue back to back
+        p = _i32_device(v, "coefficient plane", wait=False)
         if p.ndim != 2:
             raise ValueError("expected a 2-D coefficient plane")
         planes[k] = p

@@ -35,23 +35,41 @@ __device__ __forceinline__ int key_at(const void *keys, int kb, int64_t i) {
   return static_cast<const int32_t *>(keys)[i];
 }
 
-// min / max of the keys; int32 keys at a 16-byte aligned address are read 4 per
-// load (the 8K jpeg_encode's nine streams: ~100 us per large stream read one key per
-// load)
+// min / max of the keys; keys at a 16-byte aligned address are read 16 bytes per
+// load (the 8K jpeg_encode's nine streams: ~105 us per large stream read one key per
+// load, 1- and 2-byte keys included)
 template <int KB, bool VEC>
 __global__ __launch_bounds__(kHT) void k_key_range(const void *__restrict__ keys, int64_t n, int *__restrict__ mm) {
   int lo = 2147483647, hi = -2147483647 - 1;
   const int64_t t0 = (int64_t)blockIdx.x * kHT + threadIdx.x, stride = (int64_t)gridDim.x * kHT;
   int64_t tail = 0;
   if constexpr (VEC) {
-    const int4 *v = static_cast<const int4 *>(keys);
-    const int64_t nv = n >> 2;
+    constexpr int kPer = 16 / KB;  // keys per 16-byte load
+    const uint4 *v = static_cast<const uint4 *>(keys);
+    const int64_t nv = n / kPer;
     for (int64_t i = t0; i < nv; i += stride) {
-      const int4 q = v[i];
-      lo = min(lo, min(min(q.x, q.y), min(q.z, q.w)));
-      hi = max(hi, max(max(q.x, q.y), max(q.z, q.w)));
+      const uint4 q = v[i];
+      const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if constexpr (KB == 4) {
+          lo = min(lo, (int)w[c]);
+          hi = max(hi, (int)w[c]);
+        } else if constexpr (KB == 2) {
+          const int a = (int)(int16_t)(w[c] & 0xFFFFu), b = (int)(int16_t)(w[c] >> 16);
+          lo = min(lo, min(a, b));
+          hi = max(hi, max(a, b));
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int a = (int)((w[c] >> (8 * k)) & 0xFFu);
+            lo = min(lo, a);
+            hi = max(hi, a);
+          }
+        }
+      }
     }
-    tail = nv << 2;
+    tail = nv * kPer;
   }
   for (int64_t i = tail + t0; i < n; i += stride) {
     const int k = key_at(keys, KB, i);
@@ -88,7 +106,9 @@ __global__ __launch_bounds__(kHT) void k_key_hist(const void *__restrict__ keys,
     if ((unsigned)b >= (unsigned)nbins) continue;  // outside the caller's range: not counted
     if (LDS) {
       atomicAdd(&s_cnt[b], 1u);
-      atomicMin(&s_first[b], (uint32_t)i);
+      // a bin's first index is found early and a thread's i only grows: read before
+      // the atomic (it may miss a smaller value in flight; the atomic then keeps the min)
+      if ((uint32_t)i < s_first[b]) atomicMin(&s_first[b], (uint32_t)i);
     } else {
       atomicAdd(&counts[b], 1u);
       atomicMin(&first[b], (uint32_t)i);
@@ -234,11 +254,16 @@ extern "C" int hic_key_range(const void *keys, int key_bytes, int64_t n, int32_t
   const int32_t init[2] = {2147483647, -2147483647 - 1};
   if (int e = hip_status(hipMemcpyAsync(d_minmax, init, sizeof init, hipMemcpyHostToDevice, s), "hipMemcpyAsync"))
     return e;
-  const bool vec = key_bytes == 4 && reinterpret_cast<uintptr_t>(keys) % 16 == 0;
-  const int64_t want = (n + (vec ? 4 : 1) * kHT - 1) / ((vec ? 4 : 1) * kHT);
+  const bool vec = reinterpret_cast<uintptr_t>(keys) % 16 == 0;
+  const int per = vec ? 16 / key_bytes : 1;
+  const int64_t want = (n + (int64_t)per * kHT - 1) / ((int64_t)per * kHT);
   const int grid = (int)(want < 4 * cu_count() ? want : 4 * cu_count());
-  if (vec)
+  if (vec && key_bytes == 4)
     hipLaunchKernelGGL((k_key_range<4, true>), dim3(grid), dim3(kHT), 0, s, keys, n, d_minmax);
+  else if (vec && key_bytes == 2)
+    hipLaunchKernelGGL((k_key_range<2, true>), dim3(grid), dim3(kHT), 0, s, keys, n, d_minmax);
+  else if (vec)
+    hipLaunchKernelGGL((k_key_range<1, true>), dim3(grid), dim3(kHT), 0, s, keys, n, d_minmax);
   else if (key_bytes == 4)
     hipLaunchKernelGGL((k_key_range<4, false>), dim3(grid), dim3(kHT), 0, s, keys, n, d_minmax);
   else if (key_bytes == 2)

@@ -42,11 +42,13 @@ def ptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
-def to_device(a):
+def to_device(a, wait=True):
     """A host array as a new device tensor.  Large arrays (>= 4 MiB) go through two
     pinned staging buffers in chunks of _CHUNK bytes: the threaded host copy of one
     chunk overlaps the DMA of the one before it (a pageable copy runs at ~4 GB/s on
-    the MI355X boxes)."""
+    the MI355X boxes).  wait=False (an array in a pinned pool buffer only): return
+    with its DMA still queued -- the caller keeps `a` unchanged until it next
+    synchronises the current stream."""
     require_gpu()
     a = np.ascontiguousarray(a)
     if a.nbytes < _PIN_MIN or a.dtype.hasobject:
@@ -66,7 +68,8 @@ def to_device(a):
             done.record(s)
         cur.wait_event(done)
         out.record_stream(cur)
-        done.synchronize()
+        if wait:
+            done.synchronize()
         return out
     out = torch.empty(tuple(a.shape), dtype=dt, device="cuda")
     ob = out.reshape(-1).view(torch.uint8)
@@ -214,7 +217,7 @@ def to_host_f64(t):
     return out.reshape(tuple(t.shape))
 
 
-def to_device_i32(a, nonint_msg, range_msg):
+def to_device_i32(a, nonint_msg, range_msg, wait=True):
     """A host array of integer values as a new int32 device tensor, refusing
     non-integer (ValueError(nonint_msg)) or out-of-int32 (ValueError(range_msg))
     values as the host checks did.  Large float arrays (the reference's float64
@@ -222,7 +225,7 @@ def to_device_i32(a, nonint_msg, range_msg):
     and two casts of an 8K float64 plane took ~0.2 s on the host."""
     a = np.asarray(a)
     if a.dtype == np.int32:  # already in range
-        return to_device(a)
+        return to_device(a, wait=wait)
     if a.dtype.kind != "f" or a.nbytes < _PIN_MIN:
         if a.size and a.dtype.kind not in "iub" and not np.all(np.mod(a, 1) == 0):
             raise ValueError(nonint_msg)

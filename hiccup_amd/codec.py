@@ -264,8 +264,9 @@ def _jpeg_encode(compressed):
     # stream it was built from
     order = [(k, j) for j in range(3) for k in chans]
     ds = huffman.DeviceStreams([keys[k][j] for k, j in order])
+    collect = ds.packed_start()  # the GPU packs while the host builds the table payloads
     tables = [huffman_encode(ds.trees[i], dc_type[k] if j == 0 else int) for i, (k, j) in enumerate(order)]
-    data = [hic.BitStringP.from_packed(*pk) for pk in ds.packed()]
+    data = [hic.BitStringP.from_packed(*pk) for pk in collect()]
     shape = compressed.shape
     payloads = tables + data + [hic.TupP(shape[0][0], shape[0][1]), hic.TupP(shape[1][0], shape[1][1])]
     return hic.HicImage.jpeg_image(payloads)

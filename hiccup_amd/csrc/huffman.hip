@@ -82,17 +82,33 @@ __global__ __launch_bounds__(kHT) void k_key_range(const void *__restrict__ keys
     lo = a < lo ? a : lo;
     hi = b > hi ? b : hi;
   }
+  // one atomic pair per workgroup: thousands on one address serialise in the L2
+  // (~100 us per large stream with one pair per wave)
+  __shared__ int s_lo[kHT / 64], s_hi[kHT / 64];
   if ((threadIdx.x & 63) == 0) {
+    s_lo[threadIdx.x >> 6] = lo;
+    s_hi[threadIdx.x >> 6] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int w = 1; w < kHT / 64; ++w) {
+      lo = s_lo[w] < lo ? s_lo[w] : lo;
+      hi = s_hi[w] > hi ? s_hi[w] : hi;
+    }
     atomicMin(mm, lo);
     atomicMax(mm + 1, hi);
   }
 }
 
 // counts / first: nbins entries, zero / 0xFFFFFFFF initialised by the launcher
+// LDS: privatised bins; with `part` each workgroup stores its bins (count, first) to
+// part[blockIdx.x] and k_hist_reduce sums them -- per-workgroup global atomics on
+// every bin (512 workgroups x thousands of bins) took ~55 us per large stream
 template <bool LDS>
 __global__ __launch_bounds__(kHT) void k_key_hist(const void *__restrict__ keys, int kb, int64_t n, int key_min,
                                                   int nbins, uint32_t *__restrict__ counts,
-                                                  uint32_t *__restrict__ first) {
+                                                  uint32_t *__restrict__ first, uint32_t *__restrict__ part = nullptr) {
   __shared__ uint32_t s_cnt[LDS ? kHistLds : 1], s_first[LDS ? kHistLds : 1];
   if (LDS) {
     for (int b = threadIdx.x; b < nbins; b += kHT) {
@@ -116,6 +132,14 @@ __global__ __launch_bounds__(kHT) void k_key_hist(const void *__restrict__ keys,
   }
   if (LDS) {
     __syncthreads();
+    if (part) {
+      uint32_t *pc = part + (int64_t)blockIdx.x * 2 * nbins;
+      for (int b = threadIdx.x; b < nbins; b += kHT) {
+        pc[b] = s_cnt[b];
+        pc[nbins + b] = s_first[b];
+      }
+      return;
+    }
     for (int b = threadIdx.x; b < nbins; b += kHT) {
       if (s_cnt[b]) {
         atomicAdd(&counts[b], s_cnt[b]);
@@ -123,6 +147,21 @@ __global__ __launch_bounds__(kHT) void k_key_hist(const void *__restrict__ keys,
       }
     }
   }
+}
+
+// counts[b] / first[b] = the sum / min of the nwg workgroups' partial bins
+__global__ __launch_bounds__(kHT) void k_hist_reduce(const uint32_t *__restrict__ part, int nwg, int nbins,
+                                                     uint32_t *__restrict__ counts, uint32_t *__restrict__ first) {
+  const int b = blockIdx.x * kHT + threadIdx.x;
+  if (b >= nbins) return;
+  uint32_t c = 0, f = 0xFFFFFFFFu;
+  for (int w = 0; w < nwg; ++w) {
+    const uint32_t *pc = part + (int64_t)w * 2 * nbins;
+    c += pc[b];
+    f = pc[nbins + b] < f ? pc[nbins + b] : f;
+  }
+  counts[b] = c;
+  first[b] = f;
 }
 
 // block-wide exclusive sum (256 threads = 4 waves)
@@ -257,7 +296,7 @@ extern "C" int hic_key_range(const void *keys, int key_bytes, int64_t n, int32_t
   const bool vec = reinterpret_cast<uintptr_t>(keys) % 16 == 0;
   const int per = vec ? 16 / key_bytes : 1;
   const int64_t want = (n + (int64_t)per * kHT - 1) / ((int64_t)per * kHT);
-  const int grid = (int)(want < 4 * cu_count() ? want : 4 * cu_count());
+  const int grid = (int)(want < cu_count() ? want : cu_count());
   if (vec && key_bytes == 4)
     hipLaunchKernelGGL((k_key_range<4, true>), dim3(grid), dim3(kHT), 0, s, keys, n, d_minmax);
   else if (vec && key_bytes == 2)
@@ -284,6 +323,18 @@ extern "C" int hic_key_histogram(const void *keys, int key_bytes, int64_t n, int
   if (int e = hip_status(hipMemsetAsync(d_first, 0xFF, (size_t)nbins * 4, s), "hipMemsetAsync")) return e;
   const int64_t want = (n + kHT * 8 - 1) / (kHT * 8);
   const int grid = (int)(want < 2 * cu_count() ? want : 2 * cu_count());
+  if (nbins <= kHistLds && grid > 1) {
+    // two phases: per-workgroup bins to a stream-ordered scratch, then one reduction
+    void *part = nullptr;
+    if (int e = hip_status(hipMallocAsync(&part, (size_t)grid * 2 * nbins * 4, s), "hipMallocAsync")) return e;
+    hipLaunchKernelGGL(k_key_hist<true>, dim3(grid), dim3(kHT), 0, s, keys, key_bytes, n, key_min, nbins, d_counts,
+                       d_first, static_cast<uint32_t *>(part));
+    if (int e = check_launch("k_key_hist")) return e;
+    hipLaunchKernelGGL(k_hist_reduce, dim3((unsigned)((nbins + kHT - 1) / kHT)), dim3(kHT), 0, s,
+                       static_cast<const uint32_t *>(part), grid, nbins, d_counts, d_first);
+    if (int e = check_launch("k_hist_reduce")) return e;
+    return hip_status(hipFreeAsync(part, s), "hipFreeAsync");
+  }
   if (nbins <= kHistLds)
     hipLaunchKernelGGL(k_key_hist<true>, dim3(grid), dim3(kHT), 0, s, keys, key_bytes, n, key_min, nbins, d_counts,
                        d_first);

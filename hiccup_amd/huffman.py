@@ -558,6 +558,27 @@ def device_counts(keys_dev, n=None, stream=None):
     return [int(lo + b) for b in order], counts[order].astype(np.int64)
 
 
+_FAN = 3
+_fan_streams = []
+
+
+def _fan_out(calls, stream=None):
+    """calls[i](stream pointer) on side stream i % _FAN, joined back into `stream`
+    (None: the current one): the nine key streams' histograms and packings are small
+    launches that fill the chip better side by side than in a row.  The buffers they
+    use were allocated on `stream`, which waits for every side stream before anything
+    can free them."""
+    cur = stream if stream is not None else torch.cuda.current_stream()
+    while len(_fan_streams) < _FAN:
+        _fan_streams.append(torch.cuda.Stream())
+    for st in _fan_streams:
+        st.wait_stream(cur)
+    for i, fn in enumerate(calls):
+        fn(device.stream_ptr(_fan_streams[i % _FAN]))
+    for st in _fan_streams:
+        cur.wait_stream(st)
+
+
 class DeviceStreams:
     """Several device key streams at once (the nine of codec.jpeg_encode): the same
     trees and packed bits as one DeviceStream each, with the host round trips
@@ -590,10 +611,10 @@ class DeviceStreams:
         off = np.concatenate([[0], np.cumsum(self.nbins)]).astype(np.int64)
         counts = device.empty((int(off[-1]),), torch.int32)
         first = device.empty((int(off[-1]),), torch.int32)
-        for i, (k, n) in enumerate(zip(self.keys, self.n)):
-            _lib.call("hic_key_histogram", device.ptr(k), k.element_size(), n, self.lo[i], self.nbins[i],
-                      ctypes.c_void_p(counts.data_ptr() + 4 * int(off[i])),
-                      ctypes.c_void_p(first.data_ptr() + 4 * int(off[i])), s)
+        _fan_out([lambda sp, i=i, k=k, n=n: _lib.call(
+            "hic_key_histogram", device.ptr(k), k.element_size(), n, self.lo[i], self.nbins[i],
+            ctypes.c_void_p(counts.data_ptr() + 4 * int(off[i])), ctypes.c_void_p(first.data_ptr() + 4 * int(off[i])),
+            sp) for i, (k, n) in enumerate(zip(self.keys, self.n))], stream)
         c_all = counts.cpu().numpy().view(np.uint32)
         f_all = first.cpu().numpy().view(np.uint32)
         self.counts, self.trees = [], []
@@ -608,6 +629,12 @@ class DeviceStreams:
 
     def packed(self):
         """[(packed uint8 numpy array, number of bits)] per stream (hic_huffman_pack)."""
+        return self.packed_start()()
+
+    def packed_start(self):
+        """packed() in two halves: the packing and its copy back are queued now and
+        the returned function waits for them, so host work in between (jpeg_encode's
+        table payloads) overlaps the GPU."""
         with device.on_stream(self.stream):
             return self._packed()
 
@@ -624,18 +651,33 @@ class DeviceStreams:
         cl = device.to_device(np.concatenate([l for _, l in tabs]))
         out = device.empty((int(boff[-1]),), torch.uint8)
         nbits = device.empty((m,), torch.int64)
-        ws = device.workspace(self._lib.hic_huffman_pack_workspace_bytes(max(self.n)))
-        for i, (k, n) in enumerate(zip(self.keys, self.n)):
-            # one workspace serves the launches in turn: they run in order on the stream
-            _lib.call("hic_huffman_pack", device.ptr(k), k.element_size(), n, self.lo[i], self.nbins[i],
-                      ctypes.c_void_p(cb.data_ptr() + 8 * int(toff[i])), ctypes.c_void_p(cl.data_ptr() + int(toff[i])),
-                      ctypes.c_void_p(out.data_ptr() + int(boff[i])), nbytes[i],
-                      ctypes.c_void_p(nbits.data_ptr() + 8 * i), device.ptr(ws), s)
-        nb = nbits.cpu().numpy()
-        host = device.to_host(out)  # ~40 MB at 8K: the pinned chunked copy
-        res = []
-        for i in range(m):
-            if int(nb[i]) != totals[i]:
-                raise RuntimeError("stream %d: packed %d bits, the histogram says %d" % (i, int(nb[i]), totals[i]))
-            res.append((host[boff[i]:boff[i] + -(-int(nb[i]) // 8)], int(nb[i])))
-        return res
+        # one workspace per side stream: the launches of one stream run in order
+        wss = [device.workspace(self._lib.hic_huffman_pack_workspace_bytes(max(self.n))) for _ in range(_FAN)]
+        _fan_out([lambda sp, i=i, k=k, n=n: _lib.call(
+            "hic_huffman_pack", device.ptr(k), k.element_size(), n, self.lo[i], self.nbins[i],
+            ctypes.c_void_p(cb.data_ptr() + 8 * int(toff[i])), ctypes.c_void_p(cl.data_ptr() + int(toff[i])),
+            ctypes.c_void_p(out.data_ptr() + int(boff[i])), nbytes[i], ctypes.c_void_p(nbits.data_ptr() + 8 * i),
+            device.ptr(wss[i % _FAN]), sp) for i, (k, n) in enumerate(zip(self.keys, self.n))], self.stream)
+        # the bits (~40 MB at 8K) and the bit counts copied back without waiting:
+        # into a pinned pool buffer, on the stream after the packing
+        cur = self.stream if self.stream is not None else torch.cuda.current_stream()
+        host = device.host_empty((out.numel(),), np.uint8)
+        nb_host = torch.empty((m,), dtype=torch.int64, pin_memory=True)
+        with torch.cuda.stream(cur):
+            nb_host.copy_(nbits, non_blocking=True)
+            if device._is_pinned(host):
+                torch.from_numpy(host).copy_(out, non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(cur)
+
+        def collect():
+            done.synchronize()
+            h = host if device._is_pinned(host) else device.to_host(out)
+            nb = nb_host.numpy()
+            res = []
+            for i in range(m):
+                if int(nb[i]) != totals[i]:
+                    raise RuntimeError("stream %d: packed %d bits, the histogram says %d" % (i, int(nb[i]), totals[i]))
+                res.append((h[boff[i]:boff[i] + -(-int(nb[i]) // 8)], int(nb[i])))
+            return res
+        return collect

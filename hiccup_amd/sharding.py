@@ -444,15 +444,26 @@ def gather_streams_group(encoders, group=None, rccl=None, stream=None):
         else:  # (an id can come back on a new encoder: the weak references tell)
             jobs = [j for e in encoders if e.rank != e.gather_to for j in e.pack_jobs()]
             arr = [(_lib.WireJob * len(jobs[i:i + 32]))(*jobs[i:i + 32]) for i in range(0, len(jobs), 32)]
+            hit = None
             cache[key] = ([weakref.ref(e) for e in encoders], arr)
         for a in arr:
             _lib.call("hic_wire_pack_batch", len(a), a, device.stream_ptr(st))
-        items = [e.stream_item() for e in encoders]
         e0 = encoders[0]
+        grp = group if group is not None else e0.group
         if rccl is not None:
-            rccl.gather_group(items, st)
+            rccl.gather_group([e.stream_item() for e in encoders], st)
+        elif dist.get_backend(grp) != "gloo":
+            # the group's P2P operations over fixed buffers: built once (their
+            # Python construction, ~42 per 8-rank group, would otherwise bound the
+            # per-group host time), posted as one batch each time
+            ops = hit[2] if (hit is not None and len(hit) > 2) else None
+            if ops is None:
+                ops = _p2p_ops([e.stream_item() for e in encoders], e0.rank, e0.world, grp)
+                cache[key] = (cache[key][0], arr, ops)
+            for req in dist.batch_isend_irecv(ops) if ops else ():
+                req.wait()
         else:
-            gather_blocks_group(items, e0.rank, e0.world, group if group is not None else e0.group)
+            gather_blocks_group([e.stream_item() for e in encoders], e0.rank, e0.world, grp)
         for e in encoders:
             if e.rank == e.gather_to:
                 e.finish(st)
@@ -482,6 +493,26 @@ def gather_blocks(mine, full, ranges, rank, world, dst, group=None):
     is expected to be written in place already.  gloo with device tensors (the
     one-GPU rehearsal) stages through the host."""
     gather_blocks_group([(mine, full, ranges, dst)], rank, world, group)
+
+
+def _p2p_ops(items, rank, world, group):
+    """gather_blocks_group's P2P operations (device tensors, an RCCL group: received
+    in place) as a reusable list."""
+    ops = []
+    for mine, full, ranges, dst in items:
+        if rank == dst:
+            for r in range(world):
+                if r == dst:
+                    continue
+                for k in CHANNELS:
+                    b0, b1 = ranges[k][r]
+                    for t in full[k]:
+                        ops.append(dist.P2POp(dist.irecv, _wire(t[b0:b1]), r, group=group))
+        else:
+            for k in CHANNELS:
+                for t in mine[k]:
+                    ops.append(dist.P2POp(dist.isend, _wire(t.contiguous()), dst, group=group))
+    return ops
 
 
 def gather_blocks_group(items, rank, world, group=None):

@@ -327,10 +327,14 @@ def test_pipeline_encoder(H, W):
     np.testing.assert_array_equal(rgb2, exp_rgb)
 
 
-@pytest.mark.parametrize("slots", [None, False])
+_IDX_SHAPES = [(64, 96), (512, 1024), (272, 1536), (1088, 1920), (4320, 7680), (16, 16), (250, 330), (37, 53),
+               (24, 40), (40, 24), (8, 8), (16, 512), (48, 1536)]
+
+
+# slots False only where the default is the slot layout (elsewhere it is the same case)
 @pytest.mark.parametrize("kind", ["random", "levels", "blocks", "flat"])
-@pytest.mark.parametrize("H,W", [(64, 96), (512, 1024), (272, 1536), (1088, 1920), (4320, 7680), (16, 16),
-                                 (250, 330), (37, 53), (24, 40), (40, 24), (8, 8), (16, 512), (48, 1536)])
+@pytest.mark.parametrize("H,W,slots", [(h, w, None) for h, w in _IDX_SHAPES] +
+                         [(h, w, False) for h, w in _IDX_SHAPES if pipeline.slots_eligible(h, w)])
 def test_indexed_decode(H, W, kind, slots):
     """Encoder(index=True) + Decoder.decode(index=...): one wave per 64-block
     tile from the encoder-side index, counts read on the device -- the blocks and
@@ -342,8 +346,6 @@ def test_indexed_decode(H, W, kind, slots):
     half blocks beside whole luma blocks; (8, 8): one block."""
     if kind == "blocks" and (H % 8 or W % 8):
         pytest.skip("the blocks image needs whole 8x8 blocks")
-    if slots is False and not pipeline.slots_eligible(H, W):
-        pytest.skip("the default already is the coefficient chain")
     rgb = _structured_rgb(kind, H, W, H * 7 + W)
     enc = pipeline.Encoder(H, W, index=True, slots=slots)
     assert enc.slots == (slots is None and pipeline.slots_eligible(H, W))

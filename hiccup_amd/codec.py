@@ -319,7 +319,10 @@ def _jpeg_decode(hic_image):
     shapes = {"lum": p[18].numbers, "cr": p[19].numbers, "cb": p[19].numbers}
     bs = settings.JPEG_BLOCK_SIZE
     sub_length = bs * bs - 1
-    out = {}
+    # the three channels' RLE decodes and izigzags are queued before any status is
+    # read (codec.py:418's checks then run in channel order), and the three planes
+    # come back in one wait: chroma's kernels run beside luma's copy
+    pending = []
     for c, k in enumerate(chans):
         dc, vals, lens = streams[c], streams[3 + c], streams[6 + c]
         n = min(vals[1], lens[1])  # zip() in codec.py:399-400
@@ -327,8 +330,11 @@ def _jpeg_decode(hic_image):
             raise TypeError("reduce() of empty iterable with no initial value")
         if sub_length == 0:
             raise ZeroDivisionError("integer division or modulo by zero")
-        out[k] = _decode_channel(dc, lens, vals, n, shapes[k], bs)
-    return model.CompressedImage.from_dict(out)
+        pending.append(_decode_channel_start(dc, lens, vals, n, shapes[k], bs))
+    for raster, check in pending:
+        check()
+    planes = device.to_host_f64_many([raster for raster, _ in pending])
+    return model.CompressedImage.from_dict(dict(zip(chans, planes)))
 
 
 def _decoding_tree(data):
@@ -400,9 +406,10 @@ def _huffman_streams_device(payloads, trees):
     return [(d, cnt) for d, cnt, _ in res]
 
 
-def _decode_channel(dc, lens, vals, n, shape, bs):
+def _decode_channel_start(dc, lens, vals, n, shape, bs):
     """The RLE decode + DC integration + izigzag of one channel from its decoded
-    streams (device int32 tensors with counts), with codec.py:418's assertions."""
+    streams (device int32 tensors with counts), queued: (the int32 raster on the
+    device, a function that runs codec.py:418's assertions on the decode's status)."""
     (Dd, nblk), (Ld, _), (Vd, _) = dc, lens, vals
     L, sub = bs * bs, bs * bs - 1
     H, W = int(shape[0]), int(shape[1])
@@ -421,13 +428,15 @@ def _decode_channel(dc, lens, vals, n, shape, bs):
     ws = device.workspace(_lib.load().hic_rld_workspace_bytes(n, nblk))
     _lib.call("hic_rle_decode_i32", device.ptr(Ld), device.ptr(Vd), n, device.ptr(Dd), nblk, L,
               device.ptr(blocks), device.ptr(status), device.ptr(ws), device.stream_ptr())
-    if H * W == nblk * L:
-        # status = max(total, nblk * sub) after an EOB, else total (k_rld_status):
-        # codec.py:418's two assertions hold exactly when it is nblk * sub
-        assert int(status.cpu()[0]) == nblk * sub
     raster = device.zeros((H, W), torch.int32)
     _lib.call("hic_izigzag_blocks_i32", device.ptr(blocks), H, W, bs, device.ptr(raster), device.stream_ptr())
-    return device.to_host_f64(raster)
+
+    def check():
+        if H * W == nblk * L:
+            # status = max(total, nblk * sub) after an EOB, else total (k_rld_status):
+            # codec.py:418's two assertions hold exactly when it is nblk * sub
+            assert int(status.cpu()[0]) == nblk * sub
+    return raster, check
 
 
 # ------------------------------------------------------------------ out of scope

@@ -217,6 +217,18 @@ def to_host_f64(t):
     return out.reshape(tuple(t.shape))
 
 
+def to_host_f64_many(tensors):
+    """[to_host_f64(t)] with one wait: each plane widened on the device and copied
+    straight into its pinned pool buffer, all queued before the host waits."""
+    outs = [host_empty((t.numel(),), np.float64) for t in tensors]
+    if not all(t.numel() and _is_pinned(o) for t, o in zip(tensors, outs)):
+        return [to_host_f64(t) for t in tensors]
+    for t, o in zip(tensors, outs):
+        torch.from_numpy(o).copy_(t.contiguous().reshape(-1).to(torch.float64), non_blocking=True)
+    torch.cuda.current_stream().synchronize()
+    return [o.reshape(tuple(t.shape)) for t, o in zip(tensors, outs)]
+
+
 def to_device_i32(a, nonint_msg, range_msg, wait=True):
     """A host array of integer values as a new int32 device tensor, refusing
     non-integer (ValueError(nonint_msg)) or out-of-int32 (ValueError(range_msg))

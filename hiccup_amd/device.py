@@ -99,8 +99,17 @@ def to_device_parts(parts, offsets, nbytes):
     straight into the pinned staging buffers (one host copy; to_device of a
     concatenation would copy twice)."""
     require_gpu()
-    out = torch.empty((max(int(nbytes), 1),), dtype=torch.uint8, device="cuda")
     spans = [(int(o), np.ascontiguousarray(a).reshape(-1).view(np.uint8)) for o, a in zip(offsets, parts)]
+    if spans and all(a.size == 0 or _is_pinned(a) for _, a in spans):
+        # every part already page-locked (jpeg_encode's packed bits handed to
+        # jpeg_decode): zeros, then one DMA per part, no staging copy
+        out = torch.zeros((max(int(nbytes), 1),), dtype=torch.uint8, device="cuda")
+        for o, a in spans:
+            if a.size:
+                out[o:o + a.size].copy_(torch.from_numpy(a), non_blocking=True)
+        torch.cuda.current_stream().synchronize()  # the parts are free on return
+        return out
+    out = torch.empty((max(int(nbytes), 1),), dtype=torch.uint8, device="cuda")
     with _staging_lock:
         s = _copy_stream()
         s.wait_stream(torch.cuda.current_stream())

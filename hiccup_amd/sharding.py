@@ -456,10 +456,12 @@ def gather_streams_group(encoders, group=None, rccl=None, stream=None):
             # the group's P2P operations over fixed buffers: built once (their
             # Python construction, ~42 per 8-rank group, would otherwise bound the
             # per-group host time), posted as one batch each time
-            ops = hit[2] if (hit is not None and len(hit) > 2) else None
+            per_group = cache[key][2] if len(cache[key]) > 2 else {}
+            ops = per_group.get(id(grp)) if hit is not None else None
             if ops is None:
                 ops = _p2p_ops([e.stream_item() for e in encoders], e0.rank, e0.world, grp)
-                cache[key] = (cache[key][0], arr, ops)
+                per_group[id(grp)] = ops
+                cache[key] = (cache[key][0], arr, per_group)
             for req in dist.batch_isend_irecv(ops) if ops else ():
                 req.wait()
         else:
@@ -470,7 +472,8 @@ def gather_streams_group(encoders, group=None, rccl=None, stream=None):
     return [e.whole for e in encoders]
 
 
-# gather_streams_group: first encoder -> {(encoder ids): (weak refs, the group's pack job arrays)}
+# gather_streams_group: first encoder -> {(encoder ids): (weak refs, the group's pack
+# job arrays, {process group id: its P2P operations})}
 _pack_arrays = weakref.WeakKeyDictionary()
 
 

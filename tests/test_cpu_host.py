@@ -67,7 +67,9 @@ def test_ctypes_structs_match_header(tmp_path):
     """The job structs' ctypes mirrors (_lib.RleJob16, _lib.DctPlaneJob) have the
     header's size and field offsets, as gcc lays them out."""
     import subprocess
-    structs = {"hic_rle_job16": _lib.RleJob16, "hic_dct_plane_job": _lib.DctPlaneJob, "hic_slot_job": _lib.SlotJob}
+    structs = {"hic_rle_job16": _lib.RleJob16, "hic_dct_plane_job": _lib.DctPlaneJob, "hic_slot_job": _lib.SlotJob,
+               "hic_huffman_decode_job": _lib.HuffDecodeJob, "hic_encode420_job": _lib.Encode420Job,
+               "hic_wire_job": _lib.WireJob}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "hiccup_hip.h"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append('  printf("%s size %%zu\\n", sizeof(%s));' % (cname, cname))
@@ -84,6 +86,39 @@ def test_ctypes_structs_match_header(tmp_path):
         assert int(got["%s size" % cname]) == ctypes.sizeof(py), cname
         for f, _ in py._fields_:
             assert int(got["%s %s" % (cname, f)]) == getattr(py, f).offset, (cname, f)
+
+
+def test_round6_batch_entry_points_refuse_bad_jobs():
+    """The round-6 batch entry points check every job before any device call:
+    refused here without a GPU (HIC_ERR_ARG, nothing launched)."""
+    lib = _lib.load()
+    p = 1 << 20  # never dereferenced (16-byte aligned)
+    # shard transforms: job count, a shape that is not 16-row aligned, a null buffer
+    job = _lib.Encode420Job(p, 0, 64, 64, 1024, 0, 64, p, p, p, p, p, p)
+    assert lib.hic_encode420_batch_u8(0, (_lib.Encode420Job * 1)(job), 15, None, None, None) == _lib.HIC_ERR_ARG
+    assert lib.hic_encode420_batch_u8(9, (_lib.Encode420Job * 9)(*[job] * 9), 15, None, None, None) == _lib.HIC_ERR_ARG
+    bad = _lib.Encode420Job(p, 0, 64, 64, 1024, 0, 24, p, p, p, p, p, p)
+    assert lib.hic_encode420_batch_u8(2, (_lib.Encode420Job * 2)(job, bad), 15, None, None, None) == _lib.HIC_ERR_ARG
+    ragged = _lib.Encode420Job(p, 0, 64, 64, 768, 0, 64, p, p, p, p, p, p)  # records need a tile pass
+    assert lib.hic_encode420_batch_u8(1, (_lib.Encode420Job * 1)(ragged), 15, None, None, None) == _lib.HIC_ERR_ARG
+    assert "512" in _lib.last_error()
+    # wire batches: a bad table, a null wire buffer, records without a destination, too many jobs
+    w = _lib.WireJob(p, p, 64, 0, p, None, 0, 0, None, None)
+    for badw in (_lib.WireJob(p, p, 64, 2, p, None, 0, 0, None, None), _lib.WireJob(p, None, 64, 0, p, None, 0, 0, None, None),
+                 _lib.WireJob(p, p, 64, 0, p, p, 1, 0, None, None)):
+        assert lib.hic_wire_pack_batch(2, (_lib.WireJob * 2)(w, badw), None) == _lib.HIC_ERR_ARG
+        assert lib.hic_wire_unpack_batch(2, (_lib.WireJob * 2)(w, badw), None) == _lib.HIC_ERR_ARG
+    assert lib.hic_wire_pack_batch(33, (_lib.WireJob * 33)(*[w] * 33), None) == _lib.HIC_ERR_ARG
+    assert lib.hic_wire_pack_batch(1, (_lib.WireJob * 1)(_lib.WireJob(p, p, 64, 0, None, None, 0, 0, None, None)),
+                                   None) == _lib.HIC_ERR_ARG  # a pack needs its flag
+    # Huffman decode batch: a job whose tree is not a tree
+    child = np.array([1, -2, -3, -4], np.int32)  # node 1 exists, node 0's '1' child -> 1, node 1 children leaves
+    bad_child = np.array([0, -2], np.int32)       # the root as its own child
+    ok_job = _lib.HuffDecodeJob(p, 64, child.ctypes.data, 2, None, 3, p, 64, p, 0, 0)
+    bad_job = _lib.HuffDecodeJob(p, 64, bad_child.ctypes.data, 1, None, 1, p, 64, p, 0, 0)
+    assert lib.hic_huffman_decode_batch(2, (_lib.HuffDecodeJob * 2)(ok_job, bad_job), None) == _lib.HIC_ERR_ARG
+    assert "tree edge" in _lib.last_error()
+    assert lib.hic_zigzag8_blocks_i16(None, 8, 8, p, p, None) == _lib.HIC_ERR_ARG
 
 
 def test_decode_rgb_indexed_arguments():

@@ -254,8 +254,10 @@ def extra_rgb_encode(H=4096, W=4096, steps=40, n_streams=2, fused=None):
             "timed_images": steps, "streams": n_streams}
 
 
-def extra_4k_rgb_encode(steps=40, n_streams=2):
-    """north_star's 4K point on one GPU: 4096 x 4096 random RGB, the headline's chain."""
+def extra_4k_rgb_encode(steps=40, n_streams=4):
+    """north_star's 4K point on one GPU: 4096 x 4096 random RGB, the headline's chain
+    on the headline's 4 streams (a 4K launch is 2048 waves, two thirds of the chip's
+    wave slots: images overlap to fill it)."""
     out = {"workload": "4096x4096 RGB -> YCrCb 4:2:0 full encode (the headline's chain at north_star's 4K point), "
                        "1 GPU, %d streams" % n_streams}
     out.update(extra_rgb_encode(4096, 4096, steps, n_streams))

@@ -514,8 +514,14 @@ __device__ __forceinline__ void encode_unit(const Enc420 &E, int g, int lane, ui
   };
   EncColour<19, HIC_ENC_LA3, true> C;
   const bool rev = E.alt && (u0 & 1);  // wave-uniform
+  // the colour stage (its row loads) at issue priority 1 over the SIMD's waves in
+  // their DCT / emission passes: kernel 72.6-73.4 vs 73.6-74.3 us, step 0.0728-0.0740
+  // vs 0.0742-0.0760 ms in 5 alternating rounds (priority 2 / 3 within that range;
+  // profiles/r06/enc_prio/)
+  __builtin_amdgcn_s_setprio(1);
   C.init(E, y0, s, lane, nb, rev);
   C.rows(yq, s_chroma, rev);
+  __builtin_amdgcn_s_setprio(0);
   __builtin_amdgcn_sched_barrier(0);
   y_blocks(0);
   y_blocks(1);

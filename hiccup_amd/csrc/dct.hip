@@ -464,6 +464,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DEC_WPE
   // loads that depend on nothing else go out before the zero-fill: this lane's DC
   // difference and (slot layout) the tile's record index
   const int d = lane < nvb ? dc_diff[blk] : 0;
+  // the gather (index, symbol loads, LDS scatter) at issue priority 1 over the
+  // SIMD's waves in their IDCT / colour: 16K decode 0.713-0.766 vs 0.749-0.807 ms,
+  // faster in 7 of 8 alternating rounds (profiles/r06/dec_prio/)
+  __builtin_amdgcn_s_setprio(1);
   SlotTileIx six;
   if constexpr (SLOTS) six = slot_tile_ix(reinterpret_cast<const int32_t *>(index), t, rsh, nblk);
   for (int i = lane; i < 64 * kRowI16 / 4; i += 64) tile[i] = make_uint2(0, 0);
@@ -484,6 +488,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HIC_DEC_WPE
   }
   win[lane * kRowI16] = (int16_t)(pdc + wave_incl_sum_i32(d));
   __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_s_setprio(0);
   if (t == ntiles - 1 && lane == 0) {
     // (a slot-layout stream is whole by construction: its EOB zero-fills the rest)
     const int64_t total = tb0 + (int64_t)P, n_ac = nblk * 63;

@@ -762,9 +762,6 @@ __global__ __launch_bounds__(kScan16T) void k_rle_scan16b(RleJobs16 jobs, uint32
   if (s_fail && threadIdx.x == 0) put_granule(gran + 3 * np, 1, tag);
 }
 
-#ifndef HIC_EMIT_COAL
-#define HIC_EMIT_COAL 1
-#endif
 template <int MF, bool NT>
 __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
   // per wave: kWSyms symbols + 16-byte alignment slack + the dummy slot
@@ -815,7 +812,6 @@ __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
     int64_t b0, bend, r0;
     geo(J, t, b0, bend, r0);
     const int64_t b = b0 + lane;
-#if HIC_EMIT_COAL
     // coalesced: 16-B chunk c = 64 k + lane of the tile (block c / 8, part c % 8)
     // into w[4k .. 4k + 3]; transposed to one block per lane through LDS (to_lanes)
     {
@@ -827,14 +823,6 @@ __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
         n.w[4 * k] = v.x; n.w[4 * k + 1] = v.y; n.w[4 * k + 2] = v.z; n.w[4 * k + 3] = v.w;
       }
     }
-#else
-    if (b < bend) {
-      load_block16(J.blocks, b, n.w);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 32; ++k) n.w[k] = 0;
-    }
-#endif
     // the tile's first record (a 64-block tile may carry two 32-block records)
     const int64_t *offs = J.ws + 3 * J.nrec;
     n.off = offs[r0 * 2 + 0];
@@ -860,7 +848,6 @@ __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
     }
     const int64_t b = b0 + lane;
     const bool valid = b < bend;
-#if HIC_EMIT_COAL
     {
       // transpose through the wave's symbol-value stage (free until this tile's
       // emit): chunk (block bb, part p) at 16-B slot 8 bb + (p ^ (bb & 7)) -- the
@@ -880,7 +867,6 @@ __global__ __launch_bounds__(256) void k_rle_emit16b(RleJobs16 jobs) {
       }
       __builtin_amdgcn_wave_barrier();
     }
-#endif
     // DC differences: the previous block's DC comes from the neighbouring lane
     const int dc = (int)(int16_t)(cur.w[0] & 0xFFFFu);
     int pdc = __shfl_up(dc, 1, 64);
